@@ -1,0 +1,152 @@
+/*
+ * kano_hip.h -- C ABI of libkano_hip.so, the MI355X (gfx950) engine behind the
+ * drop-in `kano` Python API (reference: qiyueyao/Kubernetes-verification,
+ * kano_py/).  Every entry point names the reference operation it replaces.
+ *
+ * Conventions
+ *   - return 0 on success, a negative errno-style code on failure; the message
+ *     is kept in the context and returned by kano_last_error().
+ *   - all pointers are HOST pointers (caller-owned) unless the name ends in
+ *     _dev, in which case they are device pointers on the context's device.
+ *   - device memory is owned by the context; one context = one build of the
+ *     reachability matrix (or one row shard of it) on one GPU.
+ *   - bit order: LSB-first inside little-endian uint64 words: bit j of a bit
+ *     row lives in word j >> 6, bit j & 63.  The Python layer converts to the
+ *     reference's bitarray (big-endian bytes) where the API exposes bitarrays.
+ *   - not re-entrant per context; work is issued on the context's stream
+ *     (kano_set_stream) and every call that returns host data synchronises it.
+ *
+ * Interned inputs (built by the Python host layer, kano/_intern.py):
+ *   pod_val[c * n + i]  value id of label column c on pod i; -1 = pod i lacks
+ *                       the key (value ids are equality classes of Python ==).
+ *   sel_off/sel_col/sel_val   CSR, per policy, of the WORKING-SELECTOR terms
+ *   alw_off/alw_col/alw_val   CSR, per policy, of the WORKING-ALLOW terms
+ *                       (ingress/egress side swap already applied,
+ *                       kano_py/kano/model.py:82-93; terms whose key no pod
+ *                       carries already dropped, model.py:142-147; a rule value
+ *                       no pod carries is -2 and matches nothing).
+ */
+#ifndef KANO_HIP_H
+#define KANO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct kano_ctx kano_ctx;
+
+/* Build paths for kano_build(). */
+#define KANO_PATH_AUTO    0   /* per-class choice by estimated cost          */
+#define KANO_PATH_BITWISE 1   /* LDS scatter / bitwise OR of allow rows      */
+#define KANO_PATH_MFMA    2   /* heavy classes by int8 MFMA contraction      */
+
+/* kano_info() slots */
+#define KANO_INFO_N        0
+#define KANO_INFO_W        1
+#define KANO_INFO_P        2
+#define KANO_INFO_U        3   /* row classes (pods with equal selector keys) */
+#define KANO_INFO_NNZ_SEL  4   /* sum over classes of |S(c)|                  */
+#define KANO_INFO_NNZ_ALW  5   /* sum over policies of |allow_p|              */
+#define KANO_INFO_HEAVY    6   /* classes built by the heavy (dense) path     */
+#define KANO_INFO_ROW0     7
+#define KANO_INFO_ROW1     8
+#define KANO_INFO_MAXSEL   9   /* max over classes of |S(c)|                  */
+#define KANO_INFO_NSLOTS   16
+
+/* Lifetime.  No reference counterpart: the reference keeps its state in
+ * Python objects (kano_py/kano/model.py:167-169 ReachabilityMatrix.__init__). */
+int  kano_create(int device, kano_ctx** out);
+void kano_destroy(kano_ctx* ctx);
+const char* kano_last_error(const kano_ctx* ctx);
+int  kano_set_stream(kano_ctx* ctx, void* hip_stream);   /* NULL = own stream */
+
+/* Inputs.  Replace the key-presence bitsets of build_matrix
+ * (kano_py/kano/model.py:128-133) and the per-policy selector dicts it reads
+ * through Policy.working_selector / working_allow (model.py:82-93, 142-147). */
+int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_val);
+int kano_set_policies(kano_ctx* ctx, int64_t P,
+                      const int64_t* sel_off, const int32_t* sel_col, const int32_t* sel_val,
+                      const int64_t* alw_off, const int32_t* alw_col, const int32_t* alw_val);
+/* Row shard [row_begin, row_end) of M owned by this context (multi-GPU row
+ * partition); default = all rows. */
+int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end);
+
+/* ReachabilityMatrix.build_matrix (kano_py/kano/model.py:125-165): row classes,
+ * selector evaluation (select side per class, allow side per pod), the
+ * per-policy allow lists and the matrix rows M[i] = OR_{p in S(i)} allow_p. */
+int kano_build(kano_ctx* ctx, int path);
+int kano_info(kano_ctx* ctx, int64_t* out /* KANO_INFO_NSLOTS */);
+
+/* all_reachable / all_isolated (kano_py/kano/algorithm.py:4-17): column AND
+ * and column OR of this shard's rows, W = ceil(n/64) words each. */
+int kano_col_checks(kano_ctx* ctx, uint64_t* col_and, uint64_t* col_or);
+/* Same, unpacked to one byte per column into device memory laid out as
+ * [or(n) | cross(n) | nand(n)] so that ranks can combine with a MAX all-reduce
+ * (RCCL has no bitwise reduction).  cross is filled only when a gid array was
+ * passed to kano_crosscheck_dev. */
+int kano_col_flags_dev(kano_ctx* ctx, uint8_t* flags_dev);
+
+/* user_crosscheck (kano_py/kano/algorithm.py:20-42): bit j set iff some row i
+ * of this shard has M[i,j] and gid[i] != gid[j]; gid = interned
+ * container.getValueOrDefault(label, "") (algorithm.py:23,38), all n pods. */
+int kano_crosscheck(kano_ctx* ctx, const int32_t* gid, uint64_t* cross);
+int kano_crosscheck_dev(kano_ctx* ctx, const int32_t* gid, uint8_t* flags_dev);
+
+/* Matrix access: getrow / getcol / __getitem__ / __setitem__
+ * (kano_py/kano/model.py:171-184); system_isolation reads a row
+ * (algorithm.py:45-55).  Rows are global indices inside this shard. */
+int kano_get_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* dst);
+/* Overwrite rows (assignment to ReachabilityMatrix.matrix rows / the
+ * ReachabilityMatrix(container_size, matrix) constructor, model.py:167-169). */
+int kano_put_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint64_t* src);
+int kano_get_col(kano_ctx* ctx, int64_t j, uint64_t* dst /* ceil(rows/64) */);
+int kano_get_bit(kano_ctx* ctx, int64_t i, int64_t j, int* value);
+int kano_set_bit(kano_ctx* ctx, int64_t i, int64_t j, int value);
+
+/* Policy.working_select_set / working_allow_set (model.py:119-121, 156):
+ * the n-bit sets of policy p. */
+int kano_get_policy_sets(kano_ctx* ctx, int64_t p, uint64_t* sel, uint64_t* allow);
+/* Container.select_policies (model.py:158-161): row class of every pod and the
+ * class-level ascending policy lists, CSR over classes. */
+int kano_get_classes(kano_ctx* ctx, int32_t* cls /* n */);
+int kano_get_select_csr(kano_ctx* ctx, int64_t* off /* U+1 */, int32_t* pol /* nnz_sel */);
+/* Container.allow_policies (model.py:162-163) and the allow sets as sorted pod
+ * lists, CSR over policies. */
+int kano_get_allow_csr(kano_ctx* ctx, int64_t* off /* P+1 */, int32_t* pods /* nnz_alw */);
+
+/* policy_shadow (kano_py/kano/algorithm.py:58-80): emits, for this shard's
+ * pods in ascending order, every ordered pair (j,k) of policies selecting the
+ * pod with j != k and allow_k a subset of allow_j.  kano_shadow computes and
+ * returns the pair count; kano_shadow_fetch copies 2*count int32. */
+int kano_shadow(kano_ctx* ctx, int64_t* count);
+int kano_shadow_fetch(kano_ctx* ctx, int32_t* pairs);
+
+/* policy_shadow over explicit inputs: n_lists per-container policy lists
+ * (CSR soff/slist, the values of Container.select_policies, possibly
+ * accumulated over several builds, quirk Q5) and the P allow sets as bit rows
+ * of nbits bits (Policy.working_allow_set).  The context holds no matrix
+ * afterwards; fetch the pairs with kano_shadow_fetch. */
+int kano_shadow_lists(kano_ctx* ctx, int64_t n_lists, int64_t nbits, int64_t P,
+                      const int64_t* soff, const int32_t* slist, const uint64_t* allow_rows,
+                      int64_t* count);
+
+/* policy_conflict (kano_py/kano/algorithm.py:83-100) raises AttributeError
+ * as soon as any container has two selecting policies: *raises = 1 iff some
+ * pod of this shard has |S(i)| >= 2. */
+int kano_conflict(kano_ctx* ctx, int* raises);
+
+/* Timing of the last kano_build / kano_shadow stages on the context stream
+ * (HIP events), milliseconds: [classes, select, allow, rows, shadow, total]. */
+int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
+
+/* Page-locked host buffers for fast device-to-host result copies. */
+int  kano_host_alloc(size_t bytes, void** out);
+void kano_host_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KANO_HIP_H */

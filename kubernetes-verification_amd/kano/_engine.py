@@ -1,0 +1,251 @@
+"""One device-resident build of the reachability matrix (a kano_ctx).
+
+Thin Python wrapper of the C ABI (include/kano_hip.h): uploads interned
+tables, runs the build and the checks, and hands results back as numpy
+arrays.  The drop-in API (model.py / algorithm.py) and the benchmark both
+drive the engine through this class.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_int, c_int64, c_void_p
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _native as nat
+from ._intern import Tables
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(c_void_p)
+
+
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc) viewed as a numpy array; D2H
+    copies into it run at the full PCIe rate."""
+
+    def __init__(self, nbytes: int):
+        self._lib = nat.load()
+        self._p = c_void_p()
+        self.nbytes = max(int(nbytes), 16)
+        nat.check(None, self._lib.kano_host_alloc(self.nbytes, byref(self._p)), "kano_host_alloc")
+
+    def view(self, dtype, count: int) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if count * dt.itemsize > self.nbytes:
+            raise ValueError("pinned buffer too small")
+        buf = (ctypes.c_char * (count * dt.itemsize)).from_address(self._p.value)
+        return np.frombuffer(buf, dtype=dt, count=count)
+
+    def close(self):
+        if self._p:
+            self._lib.kano_host_free(self._p)
+            self._p = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBuild:
+    """A kano_ctx holding one build (or one row shard of it) on one GPU."""
+
+    def __init__(self, tables: Optional[Tables] = None, device: int = 0,
+                 rows: Optional[Tuple[int, int]] = None, path: str = "auto",
+                 stream: Optional[int] = None, build: bool = True):
+        self.lib = nat.load()
+        self.ctx = c_void_p()
+        rc = self.lib.kano_create(int(device), byref(self.ctx))
+        if rc != 0:
+            self.ctx = c_void_p()
+            raise nat.KanoNativeError(
+                f"kano_create(device={device}) failed (rc={rc}): no usable HIP device")
+        self.device = device
+        self.path = path
+        if stream is not None:
+            self._chk(self.lib.kano_set_stream(self.ctx, c_void_p(stream)), "kano_set_stream")
+        self.tables = None
+        if tables is not None:
+            self.upload(tables)
+            if rows is not None:
+                self.set_rows(*rows)
+            if build:
+                self.build(path)
+
+    # -- plumbing -------------------------------------------------------
+    def _chk(self, rc, what):
+        nat.check(self.ctx, rc, what)
+
+    def close(self):
+        if self.ctx:
+            self.lib.kano_destroy(self.ctx)
+            self.ctx = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- inputs / build -------------------------------------------------
+    def upload(self, t: Tables) -> None:
+        self.tables = t
+        pv = np.ascontiguousarray(t.pod_val, dtype=np.int32)
+        self._chk(self.lib.kano_set_pods(self.ctx, t.n, t.ncols, _ptr(pv)), "kano_set_pods")
+        arrs = [np.ascontiguousarray(a, dtype=d) for a, d in (
+            (t.sel_off, np.int64), (t.sel_col, np.int32), (t.sel_val, np.int32),
+            (t.alw_off, np.int64), (t.alw_col, np.int32), (t.alw_val, np.int32))]
+        self._chk(self.lib.kano_set_policies(self.ctx, t.P, *[_ptr(a) for a in arrs]),
+                  "kano_set_policies")
+
+    def set_rows(self, r0: int, r1: int) -> None:
+        self._chk(self.lib.kano_set_shard(self.ctx, int(r0), int(r1)), "kano_set_shard")
+
+    def build(self, path: Optional[str] = None) -> None:
+        p = nat.PATHS[path or self.path]
+        self._chk(self.lib.kano_build(self.ctx, p), "kano_build")
+
+    def info(self) -> dict:
+        out = np.zeros(nat.INFO_SLOTS, dtype=np.int64)
+        self._chk(self.lib.kano_info(self.ctx, _ptr(out)), "kano_info")
+        return {k: int(out[v]) for k, v in nat.INFO.items()}
+
+    @property
+    def n(self) -> int:
+        return self.tables.n
+
+    @property
+    def W(self) -> int:
+        return (self.tables.n + 63) >> 6
+
+    # -- checks ---------------------------------------------------------
+    def col_checks(self) -> Tuple[np.ndarray, np.ndarray]:
+        W = self.W
+        ca = np.zeros(W, dtype=np.uint64)
+        co = np.zeros(W, dtype=np.uint64)
+        self._chk(self.lib.kano_col_checks(self.ctx, _ptr(ca), _ptr(co)), "kano_col_checks")
+        return ca, co
+
+    def crosscheck(self, gid: np.ndarray) -> np.ndarray:
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        if gid.shape[0] != self.n:
+            raise ValueError("gid must have one entry per pod")
+        out = np.zeros(self.W, dtype=np.uint64)
+        self._chk(self.lib.kano_crosscheck(self.ctx, _ptr(gid), _ptr(out)), "kano_crosscheck")
+        return out
+
+    def col_flags_dev(self, flags_dev_ptr: int) -> None:
+        self._chk(self.lib.kano_col_flags_dev(self.ctx, c_void_p(flags_dev_ptr)),
+                  "kano_col_flags_dev")
+
+    def crosscheck_dev(self, gid: np.ndarray, flags_dev_ptr: int) -> None:
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        self._chk(self.lib.kano_crosscheck_dev(self.ctx, _ptr(gid), c_void_p(flags_dev_ptr)),
+                  "kano_crosscheck_dev")
+
+    # -- matrix access --------------------------------------------------
+    def rows(self, r0: int, nrows: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros((nrows, self.W), dtype=np.uint64)
+        self._chk(self.lib.kano_get_rows(self.ctx, int(r0), int(nrows), _ptr(out)),
+                  "kano_get_rows")
+        return out
+
+    def put_rows(self, r0: int, words: np.ndarray) -> None:
+        words = np.ascontiguousarray(words, dtype=np.uint64).reshape(-1, self.W)
+        self._chk(self.lib.kano_put_rows(self.ctx, int(r0), words.shape[0], _ptr(words)),
+                  "kano_put_rows")
+
+    def col(self, j: int) -> np.ndarray:
+        info = self.info()
+        rl = info["ROW1"] - info["ROW0"]
+        out = np.zeros((rl + 63) >> 6, dtype=np.uint64)
+        self._chk(self.lib.kano_get_col(self.ctx, int(j), _ptr(out)), "kano_get_col")
+        return out
+
+    def get_bit(self, i: int, j: int) -> int:
+        v = c_int()
+        self._chk(self.lib.kano_get_bit(self.ctx, int(i), int(j), byref(v)), "kano_get_bit")
+        return int(v.value)
+
+    def set_bit(self, i: int, j: int, value) -> None:
+        self._chk(self.lib.kano_set_bit(self.ctx, int(i), int(j), 1 if value else 0),
+                  "kano_set_bit")
+
+    def policy_sets(self, p: int, sel: bool = True, allow: bool = True):
+        W = self.W
+        s = np.zeros(W, dtype=np.uint64) if sel else None
+        a = np.zeros(W, dtype=np.uint64) if allow else None
+        self._chk(self.lib.kano_get_policy_sets(self.ctx, int(p), _ptr(s), _ptr(a)),
+                  "kano_get_policy_sets")
+        return s, a
+
+    def classes(self) -> np.ndarray:
+        out = np.zeros(self.n, dtype=np.int32)
+        self._chk(self.lib.kano_get_classes(self.ctx, _ptr(out)), "kano_get_classes")
+        return out
+
+    def select_csr(self) -> Tuple[np.ndarray, np.ndarray]:
+        info = self.info()
+        off = np.zeros(info["U"] + 1, dtype=np.int64)
+        pol = np.zeros(max(info["NNZ_SEL"], 1), dtype=np.int32)
+        self._chk(self.lib.kano_get_select_csr(self.ctx, _ptr(off), _ptr(pol)),
+                  "kano_get_select_csr")
+        return off, pol[: info["NNZ_SEL"]]
+
+    def allow_csr(self) -> Tuple[np.ndarray, np.ndarray]:
+        info = self.info()
+        off = np.zeros(info["P"] + 1, dtype=np.int64)
+        pods = np.zeros(max(info["NNZ_ALW"], 1), dtype=np.int32)
+        self._chk(self.lib.kano_get_allow_csr(self.ctx, _ptr(off), _ptr(pods)),
+                  "kano_get_allow_csr")
+        return off, pods[: info["NNZ_ALW"]]
+
+    # -- policy checks --------------------------------------------------
+    def shadow_count(self) -> int:
+        cnt = c_int64()
+        self._chk(self.lib.kano_shadow(self.ctx, byref(cnt)), "kano_shadow")
+        return int(cnt.value)
+
+    def shadow_fetch(self, count: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros((count, 2), dtype=np.int32)
+        self._chk(self.lib.kano_shadow_fetch(self.ctx, _ptr(out)), "kano_shadow_fetch")
+        return out
+
+    def shadow(self) -> np.ndarray:
+        return self.shadow_fetch(self.shadow_count())
+
+    def conflict_raises(self) -> bool:
+        v = c_int()
+        self._chk(self.lib.kano_conflict(self.ctx, byref(v)), "kano_conflict")
+        return bool(v.value)
+
+    def stage_times(self) -> dict:
+        ms = np.zeros(8, dtype=np.float32)
+        self._chk(self.lib.kano_stage_times(self.ctx, _ptr(ms)), "kano_stage_times")
+        return dict(classes=float(ms[0]), select=float(ms[1]), allow=float(ms[2]),
+                    rows=float(ms[3]), shadow=float(ms[4]), build=float(ms[5]))
+
+
+def shadow_from_lists(n_lists: int, nbits: int, soff: np.ndarray, slist: np.ndarray,
+                      allow_words: np.ndarray, device: int = 0) -> np.ndarray:
+    """policy_shadow over explicit per-container policy lists and allow sets
+    (the general form of kano_py/kano/algorithm.py:58-80, used when the lists
+    are not the ones a single build produced)."""
+    lib = nat.load()
+    b = DeviceBuild(None, device=device)
+    P = allow_words.shape[0]
+    soff = np.ascontiguousarray(soff, dtype=np.int64)
+    slist = np.ascontiguousarray(slist, dtype=np.int32)
+    aw = np.ascontiguousarray(allow_words, dtype=np.uint64)
+    cnt = c_int64()
+    b._chk(lib.kano_shadow_lists(b.ctx, int(n_lists), int(nbits), int(P), _ptr(soff),
+                                 _ptr(slist), _ptr(aw), byref(cnt)), "kano_shadow_lists")
+    out = np.zeros((int(cnt.value), 2), dtype=np.int32)
+    b._chk(lib.kano_shadow_fetch(b.ctx, _ptr(out)), "kano_shadow_fetch")
+    b.close()
+    return out

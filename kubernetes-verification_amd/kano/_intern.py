@@ -1,0 +1,213 @@
+"""Host interning: kano API objects -> the integer tables of include/kano_hip.h.
+
+Semantics restated from the reference (kano_py/kano/model.py):
+
+* KEYS = every label key carried by a container passed to build_matrix
+  (the ``labelMap`` of model.py:127-133, a dict, so key equality is Python
+  hash/==).
+* A working-selector term (k, rule) whose key is not in KEYS is dropped: the
+  presence AND skips it (model.py:143,146) and the refine loop never reaches it
+  because it iterates the *container's* labels (model.py:95-111).  Quirk Q1.
+* A kept term requires the pod to carry k (presence bitset) and
+  ``matcher.match(rule, value)`` (model.py:66-68); with the default matcher
+  that is ``rule == value`` (Python ==, so 1 == 1.0 == True).  Values are
+  interned per key into equality classes with a dict; values that are not
+  equal to themselves (NaN) never match and get a private id; unhashable
+  values are matched by a linear == scan.
+* Ingress policies swap the sides (working_selector = allow,
+  model.py:82-93); that is read through the Policy properties themselves.
+* A policy with a non-default matcher gets one virtual column per term: 1 where
+  matcher.match(rule, value) holds, 0 where the pod carries the key but the
+  matcher rejects, -1 where the pod lacks the key; the term becomes (column, 1).
+
+Value id conventions: pod side -1 = key absent, -3 = never matches (NaN);
+rule side -2 = no pod value equals the rule (matches nothing).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Dict, List, Sequence
+
+import numpy as np
+
+ABSENT = -1
+NO_MATCH_RULE = -2
+NEVER_MATCH_VALUE = -3
+
+
+@dataclass
+class Tables:
+    n: int
+    ncols: int
+    pod_val: np.ndarray          # (ncols, n) int32
+    sel_off: np.ndarray          # (P+1,) int64
+    sel_col: np.ndarray
+    sel_val: np.ndarray
+    alw_off: np.ndarray
+    alw_col: np.ndarray
+    alw_val: np.ndarray
+
+    @property
+    def P(self) -> int:
+        return int(self.sel_off.shape[0] - 1)
+
+
+class _ValueIndex:
+    """Equality classes of one key's pod values under Python ==."""
+
+    __slots__ = ("ids", "unhashable", "next_id")
+
+    def __init__(self):
+        self.ids: Dict[Any, int] = {}
+        self.unhashable: List[tuple] = []
+        self.next_id = 0
+
+    def pod_id(self, v) -> int:
+        try:
+            if v != v:            # NaN-like: rule == v is False for every rule
+                return NEVER_MATCH_VALUE
+        except Exception:
+            pass
+        try:
+            got = self.ids.get(v)
+        except TypeError:
+            for val, vid in self.unhashable:
+                if val == v:
+                    return vid
+            vid = self.next_id
+            self.next_id += 1
+            self.unhashable.append((v, vid))
+            return vid
+        if got is None:
+            got = self.next_id
+            self.next_id += 1
+            self.ids[v] = got
+        return got
+
+    def rule_id(self, rule) -> int:
+        try:
+            if rule != rule:
+                return NO_MATCH_RULE
+        except Exception:
+            pass
+        try:
+            got = self.ids.get(rule)
+        except TypeError:
+            for val, vid in self.unhashable:
+                if rule == val:
+                    return vid
+            return NO_MATCH_RULE
+        return NO_MATCH_RULE if got is None else got
+
+
+def is_default_matcher(matcher) -> bool:
+    from .model import DefaultEqualityLabelRelation
+    return type(matcher).match is DefaultEqualityLabelRelation.match
+
+
+def intern(containers: Sequence, policies: Sequence) -> Tables:
+    n = len(containers)
+    labels = [c.labels for c in containers]
+    keys: Dict[Any, None] = {}
+    for lab in labels:
+        for k in lab.keys():
+            keys[k] = None
+
+    # working sides, read through the reference's own properties
+    sides = []
+    for pol in policies:
+        ws = pol.working_selector.labels
+        wa = pol.working_allow.labels
+        sides.append((ws, wa, pol.matcher))
+
+    col_of_key: Dict[Any, int] = {}
+    col_specs: List[tuple] = []          # ("key", k) or ("custom", k, rule, matcher)
+
+    def key_col(k) -> int:
+        c = col_of_key.get(k)
+        if c is None:
+            c = len(col_specs)
+            col_of_key[k] = c
+            col_specs.append(("key", k))
+        return c
+
+    raw_terms = []                       # per policy: ([(col, rule|None)], [(col, rule|None)])
+    for ws, wa, matcher in sides:
+        default = is_default_matcher(matcher)
+        per_side = []
+        for side in (ws, wa):
+            terms = []
+            for k, rule in side.items():
+                if k not in keys:
+                    continue                 # quirk Q1
+                if default:
+                    terms.append((key_col(k), rule, False))
+                else:
+                    col = len(col_specs)
+                    col_specs.append(("custom", k, rule, matcher))
+                    terms.append((col, None, True))
+            per_side.append(terms)
+        raw_terms.append(per_side)
+
+    ncols = len(col_specs)
+    pod_val = np.full((ncols, n), ABSENT, dtype=np.int32)
+    indexes: Dict[int, _ValueIndex] = {}
+    for c, spec in enumerate(col_specs):
+        row = pod_val[c]
+        if spec[0] == "key":
+            k = spec[1]
+            idx = _ValueIndex()
+            indexes[c] = idx
+            for i, lab in enumerate(labels):
+                if k in lab:
+                    row[i] = idx.pod_id(lab[k])
+        else:
+            _, k, rule, matcher = spec
+            for i, lab in enumerate(labels):
+                if k in lab:
+                    row[i] = 1 if matcher.match(rule, lab[k]) else 0
+
+    def csr(which: int):
+        off = np.zeros(len(raw_terms) + 1, dtype=np.int64)
+        cols: List[int] = []
+        vals: List[int] = []
+        for p, per_side in enumerate(raw_terms):
+            for col, rule, custom in per_side[which]:
+                cols.append(col)
+                vals.append(1 if custom else indexes[col].rule_id(rule))
+            off[p + 1] = len(cols)
+        return off, np.asarray(cols, dtype=np.int32), np.asarray(vals, dtype=np.int32)
+
+    so, sc, sv = csr(0)
+    ao, ac, av = csr(1)
+    return Tables(n, ncols, pod_val, so, sc, sv, ao, ac, av)
+
+
+def tables_from_cluster(cl) -> Tables:
+    """Direct tables of a synth.Cluster (no Python objects), restricted to the
+    columns the working terms reference."""
+    (so, sk, sv), (ao, ak, av) = cl.working_terms()
+    used = sorted(set(sk.tolist()) | set(ak.tolist()))
+    remap = {k: i for i, k in enumerate(used)}
+    pod_val = np.ascontiguousarray(cl.vals[used], dtype=np.int32) if used else \
+        np.zeros((0, cl.n), np.int32)
+    rm = np.vectorize(remap.get, otypes=[np.int32]) if used else None
+    sc = rm(sk) if sk.size else sk.astype(np.int32)
+    ac = rm(ak) if ak.size else ak.astype(np.int32)
+    return Tables(cl.n, len(used), pod_val, so, sc, sv.astype(np.int32), ao, ac,
+                  av.astype(np.int32))
+
+
+def group_ids(containers: Sequence, label) -> np.ndarray:
+    """gid[i] = dense id of container.getValueOrDefault(label, "") under the
+    dict semantics of user_hashmap (kano_py/kano/algorithm.py:20-24)."""
+    groups: Dict[Any, int] = {}
+    gid = np.empty(len(containers), dtype=np.int32)
+    for i, c in enumerate(containers):
+        v = c.getValueOrDefault(label, "")
+        g = groups.get(v)
+        if g is None:
+            g = len(groups)
+            groups[v] = g
+        gid[i] = g
+    return gid

@@ -1,0 +1,174 @@
+"""Kano verification queries, drop-in for ``kano.algorithm`` of kano_py.
+
+Every query runs on the device-resident matrix (kano/_engine.py ->
+libkano_hip.so) and returns the reference's Python types: ascending
+``List[int]`` index lists and a ``List[Tuple[int, int]]`` for policy_shadow.
+Reference: kano_py/kano/algorithm.py:4-100.
+"""
+from __future__ import annotations
+
+from typing import DefaultDict, Dict, List, Tuple
+
+import numpy as np
+
+from .model import *  # noqa: F401,F403  (the reference does the same, algorithm.py:1)
+from .model import BitArray, Container, Policy, ReachabilityMatrix
+from ._bits import bool_to_words, set_bit_indices, words_to_bool
+from ._intern import group_ids
+
+
+def _engine(matrix: ReachabilityMatrix):
+    eng = getattr(matrix, "_engine", None)
+    if eng is None:
+        raise TypeError("expected a kano ReachabilityMatrix built by this package")
+    return eng
+
+
+def all_reachable(matrix: ReachabilityMatrix) -> List[int]:
+    """Columns j with M[i, j] = 1 for every row i (algorithm.py:4-9)."""
+    eng = _engine(matrix)
+    n = matrix.container_size
+    if n == 0:
+        return []
+    col_and, _ = eng.col_checks()
+    return set_bit_indices(col_and, n).tolist()
+
+
+def all_isolated(matrix: ReachabilityMatrix) -> List[int]:
+    """Columns j with M[i, j] = 0 for every row i (algorithm.py:12-17)."""
+    eng = _engine(matrix)
+    n = matrix.container_size
+    if n == 0:
+        return []
+    _, col_or = eng.col_checks()
+    return np.flatnonzero(~words_to_bool(col_or, n)).tolist()
+
+
+def user_hashmap(containers: List[Container], label: str) -> Dict[str, BitArray]:
+    """Group bitsets keyed by container.getValueOrDefault(label, "")
+    (algorithm.py:20-24)."""
+    n = len(containers)
+    gid = group_ids(containers, label)
+    keys: Dict = {}
+    for c in containers:
+        keys.setdefault(c.getValueOrDefault(label, ""), None)
+    out: Dict = DefaultDict(lambda: BitArray(n))
+    for g, key in enumerate(keys):
+        out[key] = BitArray.from_words(bool_to_words(gid == g), n)
+    return out
+
+
+def user_crosscheck(matrix: ReachabilityMatrix, containers: List[Container],
+                    label: str) -> List[int]:
+    """Containers j reachable from a container of another user group
+    (algorithm.py:27-42): j such that M[i, j] and g(i) != g(j) for some i."""
+    eng = _engine(matrix)
+    n = matrix.container_size
+    if len(containers) != n:
+        # the reference indexes user_map bitsets (len(containers) bits) with
+        # columns of the matrix: mismatched sizes raise there as well
+        raise ValueError("bitarrays of equal length expected for bitwise operation")
+    if n == 0:
+        return []
+    gid = group_ids(containers, label)
+    cross = eng.crosscheck(gid)
+    return set_bit_indices(cross, n).tolist()
+
+
+def system_isolation(matrix: ReachabilityMatrix, idx: int) -> List[int]:
+    """Containers j not reachable from container idx (algorithm.py:45-55)."""
+    eng = _engine(matrix)
+    n = matrix.container_size
+    i = int(idx)
+    if i < 0:
+        i += n
+    if not 0 <= i < n:
+        raise IndexError("list index out of range")
+    row = eng.rows(i, 1)[0]
+    return np.flatnonzero(~words_to_bool(row, n)).tolist()
+
+
+def _pairs_to_list(pairs: np.ndarray) -> List[Tuple[int, int]]:
+    if pairs.shape[0] == 0:
+        return []
+    return list(zip(pairs[:, 0].tolist(), pairs[:, 1].tolist()))
+
+
+def _fast_path(matrix, policies, containers) -> bool:
+    """True when (policies, containers) are exactly what this matrix's build
+    saw and every container's select_policies is still that build's list."""
+    if getattr(matrix, "_lists", None) is None:
+        return False
+    if matrix._policies is not policies and list(matrix._policies) != list(policies):
+        return False
+    if len(containers) != matrix._ncontainers:
+        return False
+    if matrix._containers is not containers:
+        cs = matrix._containers
+        if any(a is not b for a, b in zip(cs, containers)):
+            return False
+    lists = matrix._lists
+    for c in containers:
+        if not isinstance(c, Container):
+            return False
+        if c._sel or len(c._pending) != 1 or c._pending[0][0] is not lists:
+            return False
+    return True
+
+
+def policy_shadow_pairs(matrix: ReachabilityMatrix, policies: List[Policy],
+                        containers: List[Container]) -> np.ndarray:
+    """policy_shadow as an (T, 2) int32 array (compact form, same order)."""
+    if _fast_path(matrix, policies, containers):
+        return _engine(matrix).shadow()
+    # general form: explicit per-container lists (accumulated builds, edited
+    # lists) and each policy's current working_allow_set
+    from ._engine import shadow_from_lists
+    lists = [list(c.select_policies) for c in containers]
+    soff = np.zeros(len(lists) + 1, dtype=np.int64)
+    np.cumsum([len(l) for l in lists], out=soff[1:])
+    flat = np.fromiter((x for l in lists for x in l), dtype=np.int64, count=int(soff[-1]))
+    P = len(policies)
+    if flat.size and (flat.min() < 0 or flat.max() >= P):
+        raise IndexError("list index out of range")
+    needed = np.unique(flat) if flat.size else np.zeros(0, np.int64)
+    nbits = None
+    for p in needed.tolist():
+        s = policies[p].working_allow_set
+        if s is None:
+            raise AttributeError("'NoneType' object has no attribute '__and__'")
+        if nbits is None:
+            nbits = len(s)
+        elif len(s) != nbits:
+            raise ValueError("bitarrays of equal length expected for bitwise operation")
+    nbits = nbits or 0
+    W = (nbits + 63) >> 6
+    aw = np.zeros((P, W), dtype=np.uint64)
+    for p in needed.tolist():
+        s = policies[p].working_allow_set
+        b = s if isinstance(s, BitArray) else BitArray(s)
+        aw[p] = b.words()[:W]
+    return shadow_from_lists(len(lists), nbits, soff, flat.astype(np.int32), aw,
+                             device=_engine(matrix).device)
+
+
+def policy_shadow(matrix: ReachabilityMatrix, policies: List[Policy],
+                  containers: List[Container]) -> List[Tuple[int, int]]:
+    """Pairs (j, k) of policies selecting a common container with allow_k a
+    subset of allow_j, one entry per container, in container order
+    (algorithm.py:58-80; duplicates kept, quirk Q4)."""
+    return _pairs_to_list(policy_shadow_pairs(matrix, policies, containers))
+
+
+def policy_conflict(matrix: ReachabilityMatrix, policies: List[Policy],
+                    containers: List[Container]) -> List[Tuple[int, int]]:
+    """Reproduces algorithm.py:83-100 as written: the loop binds ``pj`` to a
+    policy *index*, so the first container with two selecting policies raises
+    ``AttributeError`` (quirk Q3); otherwise the result is []."""
+    if _fast_path(matrix, policies, containers):
+        raises = _engine(matrix).conflict_raises()
+    else:
+        raises = any(len(c.select_policies) >= 2 for c in containers)
+    if raises:
+        raise AttributeError("'int' object has no attribute 'working_allow_set'")
+    return []

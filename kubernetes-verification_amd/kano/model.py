@@ -1,0 +1,416 @@
+"""Kano data model, drop-in for ``kano.model`` of kano_py.
+
+Same names, fields and behaviour as kano_py/kano/model.py; the difference is
+where the state lives.  ``ReachabilityMatrix.build_matrix`` interns the
+labels (kano/_intern.py) and builds the matrix on the GPU through
+libkano_hip.so (kano/_engine.py); the matrix stays in HBM and the Python
+objects are views of it:
+
+* ``m.matrix[i]`` / ``m.getrow(i)`` are *live* rows (reads and writes go to the
+  device), like the reference's list of bitarrays (model.py:167-178);
+* ``m.getcol(j)`` gathers a column on the device (model.py:180-184);
+* ``Policy.working_select_set`` / ``working_allow_set`` are filled by the
+  build with bitarray-compatible sets fetched on first use (model.py:119-121);
+* ``Container.select_policies`` / ``allow_policies`` receive the build's
+  appends lazily, in build order, so repeated builds accumulate exactly as in
+  the reference (model.py:158-163, quirk Q5).
+
+There is no CPU fallback: without the HIP library or a GPU the build raises
+``KanoNativeError``.
+"""
+from __future__ import annotations
+
+from abc import abstractmethod
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, TypeVar
+
+try:                                    # the reference imports typing_extensions
+    from typing_extensions import Protocol
+except ImportError:                     # pragma: no cover
+    from typing import Protocol
+
+import numpy as np
+
+from ._bits import BitArray, bool_to_words, words_to_bool
+from . import _native
+
+__all__ = [
+    "Container", "PolicySelect", "PolicyAllow", "PolicyDirection", "PolicyIngress",
+    "PolicyEgress", "PolicyProtocol", "LabelRelation", "DefaultEqualityLabelRelation",
+    "Policy", "ReachabilityMatrix", "BitArray", "bitarray", "KanoNativeError",
+]
+
+bitarray = BitArray
+KanoNativeError = _native.KanoNativeError
+
+
+class _BuildLists:
+    """Host-side, lazily fetched view of one build's per-container lists."""
+
+    def __init__(self, engine):
+        self._engine = engine
+        self._sel = None
+        self._alw = None
+
+    def select_list(self, i: int) -> List[int]:
+        if self._sel is None:
+            cls = self._engine.classes()
+            off, pol = self._engine.select_csr()
+            self._sel = (cls, off, pol)
+        cls, off, pol = self._sel
+        c = cls[i]
+        return pol[off[c]:off[c + 1]].tolist()
+
+    def allow_list(self, i: int) -> List[int]:
+        if self._alw is None:
+            aoff, pods = self._engine.allow_csr()
+            P = aoff.shape[0] - 1
+            pol = np.repeat(np.arange(P, dtype=np.int32), np.diff(aoff))
+            order = np.argsort(pods, kind="stable")
+            n = self._engine.n
+            cnt = np.bincount(pods, minlength=n)
+            off = np.zeros(n + 1, dtype=np.int64)
+            np.cumsum(cnt, out=off[1:])
+            self._alw = (off, pol[order])
+        off, pol = self._alw
+        return pol[off[i]:off[i + 1]].tolist()
+
+
+class Container:
+    """A container (kano_py/kano/model.py:11-25).  Dataclass-equivalent:
+    fields ``name, labels, select_policies, allow_policies``; the two lists
+    receive each build's appends lazily (see module docstring)."""
+
+    __slots__ = ("name", "labels", "_sel", "_alw", "_pending", "__weakref__")
+    __match_args__ = ("name", "labels", "select_policies", "allow_policies")
+
+    def __init__(self, name: str, labels: Dict[str, str],
+                 select_policies: Optional[List[int]] = None,
+                 allow_policies: Optional[List[int]] = None):
+        self.name = name
+        self.labels = labels
+        self._sel = [] if select_policies is None else select_policies
+        self._alw = [] if allow_policies is None else allow_policies
+        self._pending: List[tuple] = []
+
+    def _flush(self) -> None:
+        if self._pending:
+            pend, self._pending = self._pending, []
+            for lists, i in pend:
+                self._sel.extend(lists.select_list(i))
+                self._alw.extend(lists.allow_list(i))
+
+    @property
+    def select_policies(self) -> List[int]:
+        self._flush()
+        return self._sel
+
+    @select_policies.setter
+    def select_policies(self, v: List[int]) -> None:
+        self._flush()
+        self._sel = v
+
+    @property
+    def allow_policies(self) -> List[int]:
+        self._flush()
+        return self._alw
+
+    @allow_policies.setter
+    def allow_policies(self, v: List[int]) -> None:
+        self._flush()
+        self._alw = v
+
+    def getValueOrDefault(self, key: str, value: str):
+        if key in self.labels:
+            return self.labels[key]
+        return value
+
+    def getLabels(self):
+        return self.labels
+
+    def __repr__(self) -> str:
+        return (f"Container(name={self.name!r}, labels={self.labels!r}, "
+                f"select_policies={self.select_policies!r}, "
+                f"allow_policies={self.allow_policies!r})")
+
+    def __eq__(self, other):
+        if other.__class__ is not self.__class__:
+            return NotImplemented
+        return ((self.name, self.labels, self.select_policies, self.allow_policies) ==
+                (other.name, other.labels, other.select_policies, other.allow_policies))
+
+    __hash__ = None
+
+
+@dataclass
+class PolicySelect:
+    labels: Dict[str, str]
+
+
+@dataclass
+class PolicyAllow:
+    labels: Dict[str, str]
+
+
+@dataclass
+class PolicyDirection:
+    # true for ingress, false for egress (model.py:38-47)
+    direction: bool
+
+    def is_ingress(self) -> bool:
+        return self.direction
+
+    def is_egress(self) -> bool:
+        return not self.direction
+
+
+PolicyIngress = PolicyDirection(True)
+PolicyEgress = PolicyDirection(False)
+
+
+@dataclass
+class PolicyProtocol:
+    protocols: List[str]
+
+
+T = TypeVar("T")
+
+
+class LabelRelation(Protocol[T]):
+    @abstractmethod
+    def match(self, rule: T, value: T) -> bool:
+        raise NotImplementedError
+
+
+class DefaultEqualityLabelRelation(LabelRelation):
+    def match(self, rule: Any, value: Any) -> bool:
+        return rule == value
+
+
+class _LazySet(BitArray):
+    """Policy.working_select_set / working_allow_set of one build, fetched from
+    the device on first use, then an ordinary mutable bit vector."""
+
+    __slots__ = ("_src",)
+
+    def __init__(self, engine, p: int, which: str):
+        self._src = (engine, p, which)
+        self._n = engine.n
+        self._wd = None
+
+    def _words(self) -> np.ndarray:
+        if self._wd is None:
+            engine, p, which = self._src
+            s, a = engine.policy_sets(p, sel=(which == "sel"), allow=(which == "allow"))
+            self._wd = s if which == "sel" else a
+        return self._wd
+
+
+@dataclass
+class Policy:
+    name: str
+    selector: PolicySelect
+    allow: PolicyAllow
+    direction: PolicyDirection
+    protocol: PolicyProtocol
+    matcher: LabelRelation[str] = DefaultEqualityLabelRelation()
+    working_select_set: Any = None
+    working_allow_set: Any = None
+
+    @property
+    def working_selector(self):
+        # egress: (select = selector, allow = allow); ingress swaps (model.py:82-93)
+        if self.is_egress():
+            return self.selector
+        return self.allow
+
+    @property
+    def working_allow(self):
+        if self.is_egress():
+            return self.allow
+        return self.selector
+
+    # Per-container predicates kept for API parity (model.py:95-111); the build
+    # evaluates the same predicate on the GPU over interned labels.
+    def select_policy(self, container: Container) -> bool:
+        sl = self.working_selector.labels
+        for k, v in container.labels.items():
+            if k in sl.keys() and not self.matcher.match(sl[k], v):
+                return False
+        return True
+
+    def allow_policy(self, container: Container) -> bool:
+        al = self.working_allow.labels
+        for k, v in container.labels.items():
+            if k in al.keys() and not self.matcher.match(al[k], v):
+                return False
+        return True
+
+    def is_ingress(self):
+        return self.direction.is_ingress()
+
+    def is_egress(self):
+        return self.direction.is_egress()
+
+    def store_bcp(self, select_set, allow_set):
+        self.working_select_set = select_set
+        self.working_allow_set = allow_set
+
+
+class _Row(BitArray):
+    """A live row of a device-resident matrix (model.py:177-178 aliasing)."""
+
+    __slots__ = ("_m", "_i")
+
+    def __init__(self, m: "ReachabilityMatrix", i: int):
+        self._m = m
+        self._i = i
+        self._n = m.container_size
+
+    def _words(self) -> np.ndarray:
+        return self._m._engine.rows(self._i, 1)[0]
+
+    def _store(self, words: np.ndarray) -> None:
+        self._m._engine.put_rows(self._i, words.reshape(1, -1))
+
+    def __setitem__(self, key, value):
+        if isinstance(key, slice):
+            return BitArray.__setitem__(self, key, value)
+        i = self._norm(key)
+        self._m._engine.set_bit(self._i, i, value)
+
+
+class _Rows:
+    """``ReachabilityMatrix.matrix``: a list-like of live rows."""
+
+    def __init__(self, m: "ReachabilityMatrix"):
+        self._m = m
+
+    def __len__(self):
+        return self._m.container_size
+
+    def _norm(self, i: int) -> int:
+        n = self._m.container_size
+        i = int(i)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("list index out of range")
+        return i
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        return _Row(self._m, self._norm(i))
+
+    def __setitem__(self, i, row):
+        i = self._norm(i)
+        b = row if isinstance(row, BitArray) else BitArray(row)
+        if len(b) != self._m.container_size:
+            raise ValueError("row length must equal container_size")
+        self._m._engine.put_rows(i, b.words().reshape(1, -1))
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield _Row(self._m, i)
+
+
+class ReachabilityMatrix:
+    """Container-to-container reachability (kano_py/kano/model.py:124-184),
+    resident in HBM."""
+
+    @staticmethod
+    def build_matrix(containers: List[Container], policies: List[Policy]):
+        from ._engine import DeviceBuild
+        from ._intern import intern
+        tables = intern(containers, policies)
+        engine = DeviceBuild(tables)
+        for p, pol in enumerate(policies):
+            pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
+        lists = _BuildLists(engine)
+        for i, c in enumerate(containers):
+            if isinstance(c, Container):
+                c._pending.append((lists, i))
+            else:                        # foreign container type: materialise now
+                c.select_policies.extend(lists.select_list(i))
+                c.allow_policies.extend(lists.allow_list(i))
+        m = ReachabilityMatrix.__new__(ReachabilityMatrix)
+        m.container_size = len(containers)
+        m._engine = engine
+        # kept so that policy_shadow can tell whether it is handed the very
+        # lists this build produced (then it runs on the device's class lists)
+        m._containers = containers
+        m._policies = policies
+        m._ncontainers = len(containers)
+        m._lists = lists
+        return m
+
+    def __init__(self, container_size: int, matrix: Any) -> None:
+        """Wrap an explicit matrix (a sequence of container_size bit rows) as the
+        reference constructor does (model.py:167-169); it is uploaded to HBM."""
+        from ._engine import DeviceBuild
+        from ._intern import Tables
+        n = int(container_size)
+        z64 = np.zeros(1, np.int64)
+        empty = np.zeros(0, np.int32)
+        t = Tables(n, 0, np.zeros((0, n), np.int32), z64, empty, empty, z64, empty, empty)
+        self.container_size = n
+        self._engine = DeviceBuild(t)
+        self._containers = None
+        self._policies = None
+        self._ncontainers = n
+        self._lists = None
+        rows = list(matrix)
+        if len(rows) != n:
+            raise ValueError("matrix must have container_size rows")
+        if n:
+            W = (n + 63) >> 6
+            words = np.zeros((n, W), dtype=np.uint64)
+            for i, r in enumerate(rows):
+                b = r if isinstance(r, BitArray) else BitArray(r)
+                words[i] = b.words()[:W] if len(b) == n else _fit(b, n)
+            self._engine.put_rows(0, words)
+
+    @property
+    def matrix(self) -> _Rows:
+        return _Rows(self)
+
+    def __setitem__(self, key, value):
+        i, j = key
+        n = self.container_size
+        i = int(i) + n if int(i) < 0 else int(i)
+        j = int(j) + n if int(j) < 0 else int(j)
+        if not (0 <= i < n and 0 <= j < n):
+            raise IndexError("bitarray index out of range")
+        self._engine.set_bit(i, j, value)
+
+    def __getitem__(self, key):
+        i, j = key
+        n = self.container_size
+        i = int(i) + n if int(i) < 0 else int(i)
+        j = int(j) + n if int(j) < 0 else int(j)
+        if not (0 <= i < n and 0 <= j < n):
+            raise IndexError("bitarray index out of range")
+        return self._engine.get_bit(i, j)
+
+    def getrow(self, index):
+        return self.matrix[index]
+
+    def getcol(self, index):
+        n = self.container_size
+        j = int(index)
+        if not 0 <= j < n:
+            raise IndexError("bitarray index out of range")
+        return BitArray.from_words(self._engine.col(j), n)
+
+    # engine access for kano.algorithm
+    @property
+    def engine(self):
+        return self._engine
+
+
+def _fit(b: BitArray, n: int) -> np.ndarray:
+    bits = np.zeros(n, bool)
+    src = b.tobool()
+    bits[: min(n, src.shape[0])] = src[:n]
+    return bool_to_words(bits)

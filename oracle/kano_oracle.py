@@ -1,0 +1,283 @@
+"""TEST INFRASTRUCTURE ONLY -- the parity oracle.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg;
+never by the product package.  Two layers:
+
+* ``ref_py`` -- a pure-Python restatement of kano_py's build and checks that
+  works on the kano API objects (dict labels, Python ==); for small clusters
+  and the quirk cases (kano_py/kano/model.py:125-165,
+  kano_py/kano/algorithm.py:4-100).
+* ``run_c`` -- the same algorithm in C (oracle/kano_oracle.c, built into
+  oracle/liboracle.so by oracle/Makefile) on integer tables produced by
+  ``intern_json``, an interning written independently of the product's
+  (kano/_intern.py), for clusters up to ~10^4 pods.
+
+Both are pinned against tests/golden/, vectors produced by running kano_py
+itself (tests/golden/make_golden.py, run under /opt/conda/bin/python3.9 in
+the build container).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_int, c_int64, c_void_p
+from typing import Any, Dict, List, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C oracle`")
+        L = ctypes.CDLL(LIB)
+        L.oracle_build.argtypes = [c_int64, c_int64] + [c_void_p] * 3 + [c_int64] + [c_void_p] * 9
+        L.oracle_lists.argtypes = [c_int64, c_int64, c_void_p, c_void_p, c_void_p]
+        L.oracle_column_checks.argtypes = [c_int64, c_void_p, c_int64, c_int64, c_void_p, c_void_p]
+        L.oracle_crosscheck.argtypes = [c_int64, c_void_p, c_void_p, c_int64, c_int64, c_void_p]
+        L.oracle_shadow.argtypes = [c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                                    c_int64, c_int64, c_void_p, POINTER(c_int64)]
+        for f in (L.oracle_build, L.oracle_lists, L.oracle_column_checks, L.oracle_crosscheck,
+                  L.oracle_shadow):
+            f.restype = c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(c_void_p)
+
+
+# ---------------------------------------------------------------------------
+# independent interning of a JSON cluster
+# ---------------------------------------------------------------------------
+def _eq_class(table: List[Tuple[Any, int]], index: Dict, v) -> int:
+    """Equality class id of v under Python == (NaN never equal)."""
+    if v != v:
+        return -3
+    try:
+        hit = index.get(v)
+    except TypeError:
+        for w, cid in table:
+            if w == v:
+                return cid
+        cid = len(table)
+        table.append((v, cid))
+        return cid
+    if hit is None:
+        hit = len(table)
+        table.append((v, hit))
+        index[v] = hit
+    return hit
+
+
+def intern_json(obj: dict):
+    """cluster JSON -> label CSR + working term CSRs (key -1 = unknown key,
+    value -2 = rule equal to no pod value)."""
+    pods = obj["pods"]
+    keys: Dict[Any, int] = {}
+    for p in pods:
+        for k in p["labels"]:
+            keys.setdefault(k, len(keys))
+    vtable: List[Tuple[Any, int]] = []
+    vindex: Dict = {}
+    lab_off = [0]
+    lab_key: List[int] = []
+    lab_val: List[int] = []
+    for p in pods:
+        for k, v in p["labels"].items():
+            lab_key.append(keys[k])
+            lab_val.append(_eq_class(vtable, vindex, v))
+        lab_off.append(len(lab_key))
+
+    def rule_id(r):
+        if r != r:
+            return -2
+        try:
+            hit = vindex.get(r)
+            return -2 if hit is None else hit
+        except TypeError:
+            for w, cid in vtable:
+                if w == r:
+                    return cid
+            return -2
+
+    rcache: Dict = {}
+
+    def rid(r):
+        try:
+            if r in rcache:
+                return rcache[r]
+            x = rule_id(r)
+            rcache[r] = x
+            return x
+        except TypeError:
+            return rule_id(r)
+
+    def terms(side_of):
+        off, ks, vs = [0], [], []
+        for q in obj["policies"]:
+            d = side_of(q)
+            for k, r in d.items():
+                ks.append(keys.get(k, -1))
+                vs.append(rid(r))
+            off.append(len(ks))
+        return np.array(off, np.int64), np.array(ks, np.int32), np.array(vs, np.int32)
+
+    def ws(q):  # working selector (model.py:82-87)
+        return q["allow"] if q["direction"] == "ingress" else q["select"]
+
+    def wa(q):  # working allow (model.py:89-93)
+        return q["select"] if q["direction"] == "ingress" else q["allow"]
+
+    return (len(pods), len(keys), np.array(lab_off, np.int64), np.array(lab_key, np.int32),
+            np.array(lab_val, np.int32), len(obj["policies"]), terms(ws), terms(wa))
+
+
+def group_ids_json(obj: dict, label) -> np.ndarray:
+    groups: Dict = {}
+    out = []
+    for p in obj["pods"]:
+        v = p["labels"].get(label, "")
+        out.append(groups.setdefault(v, len(groups)))
+    return np.array(out, np.int32)
+
+
+def run_c(obj: dict, label="tenant", sys_idx=0, shadow_cap=10_000_000,
+          policies=None) -> dict:
+    """Full reference pipeline on a JSON cluster through the C restatement."""
+    L = lib()
+    n, K, lo, lk, lv, P, (so, sk, sv), (ao, ak, av) = intern_json(obj)
+    if policies is not None:
+        P = policies
+        so, ao = so[: P + 1], ao[: P + 1]
+    W = (n + 63) // 64
+    M = np.zeros(max(n * W, 1), np.uint64)
+    sel = np.zeros(max(P * W, 1), np.uint64)
+    alw = np.zeros(max(P * W, 1), np.uint64)
+    rc = L.oracle_build(n, K, _p(lo), _p(lk), _p(lv), P, _p(so), _p(sk), _p(sv), _p(ao), _p(ak),
+                        _p(av), _p(M), _p(sel), _p(alw))
+    assert rc == 0
+    res = dict(n=n, P=P, W=W, M=M[: n * W].reshape(n, W), sel=sel[: P * W].reshape(P, W),
+               allow=alw[: P * W].reshape(P, W))
+    for name, sets in (("select", sel), ("allow", alw)):
+        off = np.zeros(n + 1, np.int64)
+        L.oracle_lists(n, P, _p(sets), _p(off), None)
+        lst = np.zeros(max(int(off[-1]), 1), np.int32)
+        L.oracle_lists(n, P, _p(sets), _p(off), _p(lst))
+        res[name + "_off"], res[name + "_list"] = off, lst[: int(off[-1])]
+    reach = np.zeros(max(n, 1), np.uint8)
+    isol = np.zeros(max(n, 1), np.uint8)
+    L.oracle_column_checks(n, _p(M), 0, n, _p(reach), _p(isol))
+    res["all_reachable"] = np.flatnonzero(reach[:n]).tolist()
+    res["all_isolated"] = np.flatnonzero(isol[:n]).tolist()
+    gid = group_ids_json(obj, label)
+    cross = np.zeros(max(n, 1), np.uint8)
+    L.oracle_crosscheck(n, _p(M), _p(gid), 0, n, _p(cross))
+    res["user_crosscheck"] = np.flatnonzero(cross[:n]).tolist()
+    if n:
+        row = res["M"][sys_idx]
+        bits = np.unpackbits(row.view(np.uint8), bitorder="little")[:n]
+        res["system_isolation"] = np.flatnonzero(bits == 0).tolist()
+    else:
+        res["system_isolation"] = []
+    cnt = c_int64()
+    out = np.zeros(2 * max(1, min(shadow_cap, 1)), np.int32)
+    L.oracle_shadow(n, n, _p(res["select_off"]), _p(res["select_list"]), _p(alw), 0, n, 0, None,
+                    ctypes.byref(cnt))
+    total = int(cnt.value)
+    out = np.zeros(2 * max(1, min(total, shadow_cap)), np.int32)
+    L.oracle_shadow(n, n, _p(res["select_off"]), _p(res["select_list"]), _p(alw), 0, n,
+                    min(total, shadow_cap), _p(out), ctypes.byref(cnt))
+    res["shadow_count"] = total
+    res["shadow"] = out[: 2 * min(total, shadow_cap)].reshape(-1, 2)
+    res["conflict_raises"] = bool(n and np.diff(res["select_off"]).max(initial=0) >= 2)
+    return res
+
+
+# ---------------------------------------------------------------------------
+# pure-Python restatement on kano API objects (small clusters, quirk cases)
+# ---------------------------------------------------------------------------
+def ref_py(containers, policies, label="app", sys_idx=0) -> dict:
+    """kano_py semantics restated with sets of ints; returns the matrix as a
+    list of 0/1 strings and every check.  kano_py/kano/model.py:125-165 and
+    algorithm.py:4-100."""
+    n = len(containers)
+    keys = set()
+    for c in containers:
+        keys.update(c.labels.keys())                       # model.py:131-133
+    M = [[0] * n for _ in range(n)]
+    sel_sets, alw_sets = [], []
+    sel_lists = [[] for _ in range(n)]
+    alw_lists = [[] for _ in range(n)]
+
+    def pred(pol_labels, cl, matcher):                      # model.py:95-111
+        for k, v in cl.items():
+            if k in pol_labels.keys() and not matcher.match(pol_labels[k], v):
+                return False
+        return True
+
+    for p, pol in enumerate(policies):
+        ws = pol.working_selector.labels                    # model.py:82-93
+        wa = pol.working_allow.labels
+        s = [int(all(k in c.labels for k in ws if k in keys)) for c in containers]
+        a = [int(all(k in c.labels for k in wa if k in keys)) for c in containers]
+        for i, c in enumerate(containers):                  # model.py:150-154
+            if s[i] and not pred(ws, c.labels, pol.matcher):
+                s[i] = 0
+            if a[i] and not pred(wa, c.labels, pol.matcher):
+                a[i] = 0
+        sel_sets.append(s)
+        alw_sets.append(a)
+        for i in range(n):                                  # model.py:158-163
+            if s[i]:
+                M[i] = [x | y for x, y in zip(M[i], a)]
+                sel_lists[i].append(p)
+            if a[i]:
+                alw_lists[i].append(p)
+
+    def col(j):
+        return [M[i][j] for i in range(n)]
+
+    groups = {}
+    g = []
+    for c in containers:
+        v = c.getValueOrDefault(label, "")
+        g.append(groups.setdefault(v, len(groups)) if _hashable(v) else id(v))
+    res = {
+        "M": ["".join(map(str, r)) for r in M],
+        "sel": ["".join(map(str, s)) for s in sel_sets],
+        "allow": ["".join(map(str, a)) for a in alw_sets],
+        "select_policies": sel_lists,
+        "allow_policies": alw_lists,
+        "all_reachable": [j for j in range(n) if sum(col(j)) == n],
+        "all_isolated": [j for j in range(n) if sum(col(j)) == 0],
+        "user_crosscheck": [j for j in range(n)
+                            if any(col(j)[i] and g[i] != g[j] for i in range(n))],
+        "system_isolation": [j for j in range(n) if not M[sys_idx][j]] if n else [],
+    }
+    pairs = []
+    for i in range(n):                                      # algorithm.py:66-79
+        for j in sel_lists[i]:
+            for k in sel_lists[i]:
+                if j == k:
+                    continue
+                if all(alw_sets[j][x] or not alw_sets[k][x] for x in range(n)):
+                    pairs.append((j, k))
+    res["policy_shadow"] = pairs
+    res["conflict_raises"] = any(len(l) >= 2 for l in sel_lists)
+    return res
+
+
+def _hashable(v) -> bool:
+    try:
+        hash(v)
+        return True
+    except TypeError:
+        return False

@@ -1,0 +1,216 @@
+"""Golden vectors from the reference itself (kano_py), for the parity tests.
+
+Runs ONLY in the build container, under the interpreter that has the
+reference's dependencies (bitarray, PyYAML):
+
+    python3 tests/golden/make_clusters.py            # inputs (repo python)
+    /opt/conda/bin/python3.9 tests/golden/make_golden.py [--big]
+
+It imports kano_py from /root/reference/kano_py (read-only, bytecode writing
+disabled), replays every cluster of tests/golden/clusters/ (and, with --big,
+the C2 cluster written by make_clusters.py --big to /tmp) through
+ReachabilityMatrix.build_matrix and all Kano checks, and writes the results to
+tests/golden/expected/*.json.  Nothing of the reference is copied: only its
+outputs on our inputs are stored.
+
+Canonical layouts: bit rows as LSB-first little-endian uint64 words (bit j in
+word j >> 6), row-major; index lists as int32; CSR offsets as int64.  Large
+outputs are stored as sha256 of that layout.
+"""
+import contextlib
+import hashlib
+import io
+import json
+import os
+import sys
+import time
+
+sys.dont_write_bytecode = True
+REF = "/root/reference/kano_py"
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+from kano.model import *  # noqa: E402,F401,F403
+from kano import model as ref_model  # noqa: E402
+from kano.algorithm import (all_isolated, all_reachable, policy_conflict,  # noqa: E402
+                            policy_shadow, system_isolation, user_crosscheck)
+from kano.parser import ConfigParser  # noqa: E402
+import sample as ref_sample  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CLUSTERS = os.path.join(HERE, "clusters")
+EXPECTED = os.path.join(HERE, "expected")
+SMALL_N = 300          # full matrices stored up to this many pods
+
+
+def words_of(bits_list, n):
+    """bitarray rows -> (rows, W) uint64 canonical words."""
+    W = (n + 63) // 64
+    out = np.zeros((len(bits_list), W), dtype=np.uint64)
+    for r, b in enumerate(bits_list):
+        u = np.frombuffer(b.unpack(), dtype=np.uint8)[:n]
+        buf = np.zeros(W * 64, dtype=np.uint8)
+        buf[: u.shape[0]] = u
+        out[r] = np.packbits(buf, bitorder="little").view("<u8")
+    return out
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def csr(lists):
+    off = np.zeros(len(lists) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(l) for l in lists]) if lists else []
+    flat = np.array([x for l in lists for x in l], dtype=np.int32)
+    return off, flat
+
+
+def objects(obj):
+    containers = [ref_model.Container(p["name"], p["labels"]) for p in obj["pods"]]
+    policies = []
+    for q in obj["policies"]:
+        d = ref_model.PolicyIngress if q["direction"] == "ingress" else ref_model.PolicyEgress
+        policies.append(ref_model.Policy(q["name"], ref_model.PolicySelect(q["select"]),
+                                         ref_model.PolicyAllow(q["allow"]), d,
+                                         ref_model.PolicyProtocol(q.get("protocol") or [])))
+    return containers, policies
+
+
+def run_checks(m, containers, policies, label, sys_idx, full, timings):
+    n = m.container_size
+    res = {}
+    t = time.time()
+    res["all_reachable"] = all_reachable(m)
+    timings["all_reachable"] = time.time() - t
+    t = time.time()
+    res["all_isolated"] = all_isolated(m)
+    timings["all_isolated"] = time.time() - t
+    t = time.time()
+    try:
+        res["user_crosscheck"] = {"label": label, "result": user_crosscheck(m, containers, label)}
+    except Exception as e:  # noqa: BLE001
+        res["user_crosscheck"] = {"label": label, "raises": type(e).__name__}
+    timings["user_crosscheck"] = time.time() - t
+    res["system_isolation"] = {"idx": sys_idx,
+                               "result": system_isolation(m, sys_idx) if n else []}
+    t = time.time()
+    pairs = policy_shadow(m, policies, containers)
+    timings["policy_shadow"] = time.time() - t
+    arr = np.array(pairs, dtype=np.int32).reshape(-1, 2)
+    res["policy_shadow"] = {"count": len(pairs), "sha256": sha(arr),
+                            "head": [list(p) for p in pairs[:1000]]}
+    if full:
+        res["policy_shadow"]["all"] = [list(p) for p in pairs]
+    try:
+        res["policy_conflict"] = {"result": policy_conflict(m, policies, containers)}
+    except Exception as e:  # noqa: BLE001
+        res["policy_conflict"] = {"raises": type(e).__name__, "message": str(e)}
+    return res
+
+
+def matrix_record(m, containers, policies, full):
+    n = m.container_size
+    M = words_of(m.matrix, n)
+    S = words_of([p.working_select_set for p in policies], n)
+    A = words_of([p.working_allow_set for p in policies], n)
+    so, sl = csr([c.select_policies for c in containers])
+    ao, al = csr([c.allow_policies for c in containers])
+    rec = {"n": n, "P": len(policies), "M_sha256": sha(M), "sel_sha256": sha(S),
+           "allow_sha256": sha(A),
+           "select_policies_sha256": sha(np.concatenate([so.view(np.uint8), sl.view(np.uint8)])),
+           "allow_policies_sha256": sha(np.concatenate([ao.view(np.uint8), al.view(np.uint8)])),
+           "density": float(sum(r.count() for r in m.matrix)) / max(1, n * n)}
+    if full:
+        rec["M"] = [r.to01() for r in m.matrix]
+        rec["sel"] = [p.working_select_set.to01() for p in policies]
+        rec["allow"] = [p.working_allow_set.to01() for p in policies]
+        rec["select_policies"] = [list(c.select_policies) for c in containers]
+        rec["allow_policies"] = [list(c.allow_policies) for c in containers]
+    return rec
+
+
+def run_cluster(name, obj, label, sys_idx=0):
+    containers, policies = objects(obj)
+    n = len(containers)
+    full = n <= SMALL_N
+    timings = {}
+    t = time.time()
+    m = ReachabilityMatrix.build_matrix(containers, policies)
+    timings["build_matrix"] = time.time() - t
+    rec = {"name": name, "label": label}
+    if "seed" in obj:
+        rec["seed"] = obj["seed"]
+    rec.update(matrix_record(m, containers, policies, full))
+    rec.update(run_checks(m, containers, policies, label, sys_idx, full, timings))
+    rec["reference_seconds"] = timings
+    return rec
+
+
+def paper_records():
+    out = []
+    c, p = ref_sample.paper_example()
+    m = ReachabilityMatrix.build_matrix(c, p)
+    rec = {"name": "paper_example", "label": "app"}
+    rec.update(matrix_record(m, c, p, True))
+    rec.update(run_checks(m, c, p, "app", 0, True, {}))
+    rec["test_basic_asserts"] = bool(m[0, 1] & m[2, 0] & m[4, 2])
+    out.append(rec)
+    # quirk Q5: a second build on the same objects accumulates the lists
+    m2 = ReachabilityMatrix.build_matrix(c, p)
+    rec2 = {"name": "paper_example_rebuilt", "label": "app"}
+    rec2.update(matrix_record(m2, c, p, True))
+    rec2.update(run_checks(m2, c, p, "app", 0, True, {}))
+    out.append(rec2)
+    return out
+
+
+def parser_records():
+    recs = []
+    ydir = os.path.join(HERE, "yaml")
+    for fname in sorted(os.listdir(ydir)):
+        cp = ConfigParser()
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            cp.parse(os.path.join(ydir, fname))
+        recs.append({
+            "file": fname,
+            "stdout": buf.getvalue().replace(ydir, "<YAML>"),
+            "containers": [[c.name, {str(k): v for k, v in c.labels.items()}]
+                           for c in cp.containers],
+            "containers_repr": [repr(c.labels) for c in cp.containers],
+            "policies": [[q.name, None if q.selector.labels is None else repr(q.selector.labels),
+                          None if q.allow.labels is None else repr(q.allow.labels),
+                          q.direction.direction, q.protocol] for q in cp.policies],
+        })
+    # a buildable directory (broken / None-allow files excluded): parse + build
+    return recs
+
+
+def main():
+    big = "--big" in sys.argv
+    os.makedirs(EXPECTED, exist_ok=True)
+    recs = paper_records()
+    for fname in sorted(os.listdir(CLUSTERS)):
+        obj = json.load(open(os.path.join(CLUSTERS, fname)))
+        label = obj.get("label", "app")
+        t = time.time()
+        recs.append(run_cluster(fname[:-5], obj, label))
+        print(f"{fname}: {time.time() - t:.2f}s", flush=True)
+    for r in recs:
+        with open(os.path.join(EXPECTED, r["name"] + ".json"), "w") as f:
+            json.dump(r, f, indent=None, separators=(",", ":"))
+    with open(os.path.join(EXPECTED, "parser.json"), "w") as f:
+        json.dump(parser_records(), f, indent=1)
+    if big:
+        path = "/tmp/kano_golden_C2.json"
+        obj = json.load(open(path))
+        t = time.time()
+        rec = run_cluster("C2", obj, obj.get("label", "tenant"))
+        print(f"C2: {time.time() - t:.1f}s  timings={rec['reference_seconds']}", flush=True)
+        with open(os.path.join(EXPECTED, "C2.json"), "w") as f:
+            json.dump(rec, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+    main()
