@@ -1,0 +1,311 @@
+"""Benchmark: reachability build + all Kano checks on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+
+One step = one pass of the hot path over the synthetic cluster, inputs
+(interned label tables) already resident in HBM:
+  ReachabilityMatrix.build_matrix   classes, selector evaluation, allow sets,
+                                    matrix rows (kano_py/kano/model.py:125-165)
+  all_reachable, all_isolated       algorithm.py:4-17
+  user_crosscheck(label="tenant")   algorithm.py:27-42 (gid array uploaded)
+  system_isolation(idx=0)           algorithm.py:45-55
+  policy_shadow                     algorithm.py:58-80 (pairs copied to host)
+with every result on the host as index arrays.  value = n^2 / step time
+(pod-pairs/s); the n x n matrix is built once per step over
+all ranks.  For N > 1 the rows are partitioned across ranks (one process per
+GPU); the column checks combine per-rank byte flags with one RCCL MAX
+all-reduce (RCCL has no bitwise reduction); strong scaling (fixed cluster).
+
+Rank 0 prints ONE JSON line.  roofline: the dominant kernel is k_rows (the
+matrix write), algorithmic bytes = 8 * rows * W (the bit matrix it writes),
+timed with HIP events on the engine's stream.  cpu_baseline: the oracle's C
+port of the reference (oracle/kano_oracle.c, 1 core) timed on a bounded
+sample of the same cluster and extrapolated by the reference's own cost laws
+(build linear in policies, each column check linear in columns, shadow linear
+in pair tests).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "kubernetes-verification_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "pod-pairs/sec for reachability build + all-checks latency, 100k pods, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+WORKLOADS = {
+    "C2": "Synthetic 10k pods / 1k policies, Zipf labels (BASELINE configs[1])",
+    "C3": "Synthetic 100k pods / 10k policies, sparse selectors (BASELINE configs[2])",
+    "C4": "Synthetic 100k pods / 10k policies, broad namespace-wide selectors (BASELINE configs[3])",
+    "C5": "Synthetic 1M pods / 100k policies, sparse selectors (BASELINE configs[4])",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
+    ap.add_argument("--path", default="auto", choices=["auto", "bitwise", "mfma"])
+    ap.add_argument("--no-shadow", action="store_true",
+                    help="skip policy_shadow (its output is ~1e11 pairs on C4)")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU sample")
+    return ap.parse_args()
+
+
+class Step:
+    """The hot path on this rank's row shard."""
+
+    def __init__(self, eng, gid, n, rank, world, r0, r1, shadow, dist=None, torch=None):
+        self.eng, self.gid, self.n = eng, gid, n
+        self.rank, self.world, self.r0, self.r1 = rank, world, r0, r1
+        self.shadow = shadow
+        self.dist, self.torch = dist, torch
+        self.W = (n + 63) >> 6
+        if world > 1:
+            self.flags = torch.zeros(3 * n, dtype=torch.uint8, device="cuda")
+        from kano._engine import PinnedBuffer
+        self.pin = None
+        self.pin_pairs = 0
+        self.PinnedBuffer = PinnedBuffer
+        self.results = {}
+        self.k_rows_ms = []
+
+    def __call__(self):
+        eng, n = self.eng, self.n
+        eng.build()
+        res = {}
+        if self.world == 1:
+            ca, co = eng.col_checks()
+            cross = eng.crosscheck(self.gid)
+            from kano._bits import words_to_bool
+            res["all_reachable"] = np.flatnonzero(words_to_bool(ca, n))
+            res["all_isolated"] = np.flatnonzero(~words_to_bool(co, n))
+            res["user_crosscheck"] = np.flatnonzero(words_to_bool(cross, n))
+        else:
+            f = self.flags
+            eng.col_flags_dev(f.data_ptr())
+            eng.crosscheck_dev(self.gid, f.data_ptr())
+            self.torch.cuda.synchronize()
+            self.dist.all_reduce(f, op=self.dist.ReduceOp.MAX)
+            h = f.cpu().numpy()
+            res["all_isolated"] = np.flatnonzero(h[:n] == 0)
+            res["user_crosscheck"] = np.flatnonzero(h[n:2 * n])
+            res["all_reachable"] = np.flatnonzero(h[2 * n:] == 0)
+        if self.r0 <= 0 < self.r1:
+            from kano._bits import words_to_bool
+            res["system_isolation"] = np.flatnonzero(~words_to_bool(eng.rows(0, 1)[0], n))
+        if self.shadow:
+            cnt = eng.shadow_count()
+            if self.pin is None or cnt > self.pin_pairs:
+                if self.pin is not None:
+                    self.pin.close()
+                self.pin_pairs = max(cnt, 1) * 2
+                self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+            out = self.pin.view(np.int32, 2 * cnt).reshape(cnt, 2)
+            eng.shadow_fetch(cnt, out)
+            res["policy_shadow"] = out
+            res["policy_shadow_count"] = cnt
+        st = eng.stage_times()
+        self.k_rows_ms.append(st["k_rows"])
+        self.stages = st
+        self.results = res
+        return res
+
+
+def cpu_baseline(cl, tables, eng_info, shadow_pairs_total, budget):
+    """Oracle C port (1 core) on a bounded sample of the same cluster."""
+    import ctypes
+    from oracle import kano_oracle as orc
+    L = orc.lib()
+    obj = None
+    n, P = cl.n, cl.P
+    # integer tables the oracle understands: label CSR over ALL keys of the
+    # pods and working terms keyed by the same ids
+    nk = cl.vals.shape[0]
+    present = cl.vals >= 0
+    cnt = present.sum(axis=0)
+    lab_off = np.zeros(n + 1, np.int64)
+    np.cumsum(cnt, out=lab_off[1:])
+    order = np.argsort(~present.T, axis=1, kind="stable")  # keys of each pod first
+    lab_key = np.concatenate([order[i, :cnt[i]] for i in range(n)]).astype(np.int32)
+    # value ids must be unique per (key, value): offset by key
+    lab_val = (cl.vals[lab_key, np.repeat(np.arange(n), cnt)].astype(np.int64)
+               + lab_key.astype(np.int64) * 10_000_000).astype(np.int64)
+    (so, sk, sv), (ao, ak, av) = cl.working_terms()
+    sv2 = (sv.astype(np.int64) + sk.astype(np.int64) * 10_000_000)
+    av2 = (av.astype(np.int64) + ak.astype(np.int64) * 10_000_000)
+    # compress ids into int32
+    allv = np.unique(np.concatenate([lab_val, sv2, av2]))
+    lab_val = np.searchsorted(allv, lab_val).astype(np.int32)
+    sv2 = np.searchsorted(allv, sv2).astype(np.int32)
+    av2 = np.searchsorted(allv, av2).astype(np.int32)
+    W = (n + 63) // 64
+    p_s = max(1, min(P, int(P * 0.02)))
+    M = np.zeros(n * W, np.uint64)
+    alw = np.zeros(p_s * W, np.uint64)
+    sel = np.zeros(p_s * W, np.uint64)
+    t = time.perf_counter()
+    L.oracle_build(n, nk, orc._p(lab_off), orc._p(lab_key), orc._p(lab_val), p_s,
+                   orc._p(so), orc._p(sk.astype(np.int32)), orc._p(sv2), orc._p(ao),
+                   orc._p(ak.astype(np.int32)), orc._p(av2), orc._p(M), orc._p(sel), orc._p(alw))
+    t_build = (time.perf_counter() - t) * P / p_s
+    c_s = max(64, min(n, int(budget * 0.15 / 2e-4)))
+    reach = np.zeros(n, np.uint8)
+    isol = np.zeros(n, np.uint8)
+    t = time.perf_counter()
+    L.oracle_column_checks(n, orc._p(M), 0, c_s, orc._p(reach), orc._p(isol))
+    t_cols = (time.perf_counter() - t) * n / c_s * 2      # two passes in the reference
+    gid = cl.vals[0].astype(np.int32)
+    cross = np.zeros(n, np.uint8)
+    c_x = max(32, c_s // 4)
+    t = time.perf_counter()
+    L.oracle_crosscheck(n, orc._p(M), orc._p(gid), 0, c_x, orc._p(cross))
+    t_cross = (time.perf_counter() - t) * n / c_x
+    # shadow: time per pair test (allow rows of W words), times the exact pair
+    # count sum_i |S(i)|(|S(i)|-1) (from the GPU build's class lists)
+    npairs_test = 20000
+    lists_off = np.arange(0, 2 * npairs_test + 1, 2, dtype=np.int64)
+    rng = np.random.default_rng(0)
+    lst = rng.integers(0, p_s, size=2 * npairs_test).astype(np.int32)
+    c = ctypes.c_int64()
+    t = time.perf_counter()
+    L.oracle_shadow(npairs_test, n, orc._p(lists_off), orc._p(lst), orc._p(alw), 0, npairs_test,
+                    0, None, ctypes.byref(c))
+    per_test = (time.perf_counter() - t) / (2 * npairs_test)
+    t_shadow = per_test * shadow_pairs_total
+    total = t_build + t_cols + t_cross + t_shadow
+    return {
+        "value": float(n) * n / total, "unit": "pod-pairs/s", "cores": 1, "kind": "port",
+        "sample": (f"oracle C port of kano_py on the same {n}-pod cluster: build_matrix over "
+                   f"{p_s}/{P} policies (x{P / p_s:.0f}), all_reachable+all_isolated over "
+                   f"{c_s}/{n} columns, user_crosscheck over {c_x}/{n} columns, policy_shadow "
+                   f"{2 * npairs_test} subset tests x {shadow_pairs_total} tests; extrapolated "
+                   f"total {total:.1f} s"),
+        "seconds": {"build": round(t_build, 2), "col_checks": round(t_cols, 2),
+                    "crosscheck": round(t_cross, 2), "shadow": round(t_shadow, 2)},
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus N > 1 needs torch.distributed.run with N processes")
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    from kano import _native
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.synth import make_config, KEY_NAMES
+
+    cl = make_config(args.config)
+    tables = tables_from_cluster(cl)
+    n = cl.n
+    gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
+    r0, r1 = rank * n // world, (rank + 1) * n // world
+    eng = DeviceBuild(tables, device=local, rows=(r0, r1), path=args.path, build=False)
+    step = Step(eng, gid, n, rank, world, r0, r1, shadow=not args.no_shadow, dist=dist,
+                torch=torch)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    step.k_rows_ms.clear()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    info = eng.info()
+    ms_step = elapsed / args.steps * 1e3
+    value = float(n) * n / (elapsed / args.steps)
+    k_rows_ms = float(np.mean(step.k_rows_ms)) if step.k_rows_ms else float("nan")
+    rows_local = r1 - r0
+    W = (n + 63) // 64
+    alg_bytes = 8.0 * rows_local * W
+    achieved = alg_bytes / (k_rows_ms * 1e-3) / 1e9 if k_rows_ms > 0 else 0.0
+    res = step.results
+    shadow_cnt = int(res.get("policy_shadow_count", -1))
+    if dist is not None:
+        t = torch.tensor([max(shadow_cnt, 0)], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        shadow_cnt = int(t.item())
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": value, "unit": "pod-pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u64", "data": "synthetic",
+            "config": {"workload": WORKLOADS[args.config], "name": args.config, "pods": n,
+                       "policies": cl.P, "mode": cl.mode, "seed": cl.seed,
+                       "parallelism": f"rows{world}", "path": args.path,
+                       "checks": "all_reachable, all_isolated, user_crosscheck(tenant), "
+                                 "system_isolation(0)" +
+                                 ("" if args.no_shadow else ", policy_shadow")},
+            "roofline": {"bound": "hbm", "kernel": "k_rows", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "alg_bytes_per_launch": alg_bytes,
+                         "avg_launch_ms": k_rows_ms},
+            "stages_ms_last_step": {k: round(v, 4) for k, v in step.stages.items()},
+            "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
+            "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
+            "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},
+        }
+        if args.cpu_baseline and world == 1:
+            sum_s2 = 0
+            if not args.no_shadow:
+                off, _ = eng.select_csr()
+                cls = eng.classes()
+                s = np.diff(off)[cls].astype(np.int64)
+                sum_s2 = int((s * (s - 1)).sum())
+            out["cpu_baseline"] = cpu_baseline(cl, tables, info, sum_s2, args.cpu_budget)
+            out["cpu_baseline"]["cpu"] = _cpu_model()
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

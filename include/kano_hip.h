@@ -139,7 +139,8 @@ int kano_shadow_lists(kano_ctx* ctx, int64_t n_lists, int64_t nbits, int64_t P,
 int kano_conflict(kano_ctx* ctx, int* raises);
 
 /* Timing of the last kano_build / kano_shadow stages on the context stream
- * (HIP events), milliseconds: [classes, select, allow, rows, shadow, total]. */
+ * (HIP events), milliseconds: [classes, select, allow, rows stage, shadow,
+ * build total, k_rows kernel alone, 0]. */
 int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
 
 /* Page-locked host buffers for fast device-to-host result copies. */

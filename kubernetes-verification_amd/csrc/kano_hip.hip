@@ -881,6 +881,7 @@ struct kano_ctx {
   bool cols_valid = false;   // color/colnand reflect M (false after set_bit)
   bool rows_dirty = false;   // set_bit happened: classes no longer describe M
   bool lists_mode = false;   // kano_shadow_lists context: no matrix
+  bool rows_timed = false;   // ev[7]..ev[8] bracket the last k_rows launch
 
   // host copies of the policy CSRs (for the class-key remap)
   std::vector<int32_t> ckeys;
@@ -898,7 +899,7 @@ struct kano_ctx {
   i64 shadow_total = -1;
   DBuf scratch_words;
 
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[10] = {};
   float stage_ms[8] = {};
 };
 
@@ -1042,6 +1043,7 @@ int do_classes(kano_ctx* ctx) {
   KTRY(dalloc(ctx, ctx->cls, sizeof(int32_t) * n));
   KCHK(hipMemsetAsync(ctx->table.p, 0xff, sizeof(int32_t) * T, ctx->stream));
   KCHK(hipMemsetAsync(ctx->smin.p, 0x7f, sizeof(int32_t) * T, ctx->stream));
+  if (n > 0) {
   hipLaunchKernelGGL(k_class_insert, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                      P_<int32_t>(ctx->pv), n, P_<int32_t>(ctx->ckeys_d), ctx->KS,
                      P_<int32_t>(ctx->table), (uint32_t)(T - 1), P_<int32_t>(ctx->slot_of));
@@ -1052,12 +1054,14 @@ int do_classes(kano_ctx* ctx) {
   hipLaunchKernelGGL(k_class_flag, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                      P_<int32_t>(ctx->slot_of), n, P_<int32_t>(ctx->smin), P_<int32_t>(ctx->flag));
   KLAUNCH();
+  }
   KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->flag), n, P_<int32_t>(ctx->cid))));
   int32_t U32 = 0;
   KTRY(read_scalar(ctx, P_<int32_t>(ctx->cid) + n, &U32));
   const i64 U = U32;
   ctx->U = U;
   KTRY(dalloc(ctx, ctx->rep, sizeof(int32_t) * U));
+  if (n > 0)
   hipLaunchKernelGGL(k_class_assign, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                      P_<int32_t>(ctx->slot_of), n, P_<int32_t>(ctx->smin), P_<int32_t>(ctx->cid),
                      P_<int32_t>(ctx->cls), P_<int32_t>(ctx->rep));
@@ -1083,7 +1087,7 @@ int do_classes(kano_ctx* ctx) {
     KLAUNCH();
   }
   KTRY(dalloc(ctx, ctx->cval, sizeof(int32_t) * std::max<i64>(1, (i64)ctx->KS * U)));
-  if (ctx->KS > 0) {
+  if (ctx->KS > 0 && U > 0) {
     hipLaunchKernelGGL(k_class_vals, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->pv), n, P_<int32_t>(ctx->ckeys_d), ctx->KS,
                        P_<int32_t>(ctx->rep), U, P_<int32_t>(ctx->cval));
@@ -1267,9 +1271,12 @@ int do_rows(kano_ctx* ctx, int path) {
   a.cww = cww;
   a.color = P_<u64>(ctx->color);
   a.colnand = P_<u64>(ctx->colnand);
+  KCHK(hipEventRecord(ctx->ev[7], ctx->stream));
   hipLaunchKernelGGL(k_rows, dim3((unsigned)wi_ub, ncc), dim3(TPB), sizeof(u64) * cww, ctx->stream,
                      a);
   KLAUNCH();
+  KCHK(hipEventRecord(ctx->ev[8], ctx->stream));
+  ctx->rows_timed = true;
   ctx->wi_total = wi_ub;
   ctx->cols_valid = true;
   return 0;
@@ -1438,6 +1445,7 @@ int kano_build(kano_ctx* ctx, int path) {
   KCHK(hipSetDevice(ctx->device));
   ctx->built = false;
   ctx->lists_mode = false;
+  ctx->rows_timed = false;
   ctx->shadow_total = -1;
   ctx->rows_dirty = false;
   KTRY(scan_reserve(ctx, std::max<i64>({ctx->n, ctx->P, (i64)1})));
@@ -1944,6 +1952,7 @@ int kano_stage_times(kano_ctx* ctx, float* ms) {
     (void)hipEventElapsedTime(&ms[5], ctx->ev[0], ctx->ev[4]);
   }
   if (ctx->shadow_total >= 0) (void)hipEventElapsedTime(&ms[4], ctx->ev[5], ctx->ev[6]);
+  if (ctx->built && ctx->rows_timed) (void)hipEventElapsedTime(&ms[6], ctx->ev[7], ctx->ev[8]);
   return 0;
 }
 

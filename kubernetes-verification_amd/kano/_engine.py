@@ -228,7 +228,8 @@ class DeviceBuild:
         ms = np.zeros(8, dtype=np.float32)
         self._chk(self.lib.kano_stage_times(self.ctx, _ptr(ms)), "kano_stage_times")
         return dict(classes=float(ms[0]), select=float(ms[1]), allow=float(ms[2]),
-                    rows=float(ms[3]), shadow=float(ms[4]), build=float(ms[5]))
+                    rows=float(ms[3]), shadow=float(ms[4]), build=float(ms[5]),
+                    k_rows=float(ms[6]))
 
 
 def shadow_from_lists(n_lists: int, nbits: int, soff: np.ndarray, slist: np.ndarray,

@@ -1,0 +1,256 @@
+"""GPU parity: the HIP engine (through the C ABI and the drop-in API) against
+kano_py's golden vectors and the C oracle.  Bit-exact everywhere."""
+import os
+
+import numpy as np
+import pytest
+
+from _golden import (cluster, cluster_names, csr_sha, expected, lists_to_csr, sha,
+                     words_to_rows01)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    from kano import _native
+    if not _native.gpu_available():
+        pytest.fail("GPU test run without a usable HIP device / libkano_hip.so")
+
+
+def api_objects(obj):
+    from kano import model
+    from kano.synth import objects_from_json
+    return objects_from_json(obj, model)
+
+
+def api_record(m, cs, ps, label):
+    """Run every query through the drop-in API; canonical layouts."""
+    from kano import algorithm as alg
+    n = m.container_size
+    res = {"n": n, "P": len(ps)}
+    res["M"] = m.engine.rows(0, n) if n else np.zeros((0, 1), np.uint64)
+    res["sel"] = np.array([p.working_select_set.words() for p in ps]).reshape(len(ps), -1)
+    res["allow"] = np.array([p.working_allow_set.words() for p in ps]).reshape(len(ps), -1)
+    res["select_csr"] = lists_to_csr([c.select_policies for c in cs])
+    res["allow_csr"] = lists_to_csr([c.allow_policies for c in cs])
+    res["all_reachable"] = alg.all_reachable(m)
+    res["all_isolated"] = alg.all_isolated(m)
+    res["user_crosscheck"] = alg.user_crosscheck(m, cs, label)
+    res["system_isolation"] = alg.system_isolation(m, 0) if n else []
+    res["policy_shadow"] = alg.policy_shadow(m, ps, cs)
+    try:
+        res["policy_conflict"] = ("ok", alg.policy_conflict(m, ps, cs))
+    except AttributeError as e:
+        res["policy_conflict"] = ("raises", str(e))
+    return res
+
+
+def compare(res, exp):
+    n = exp["n"]
+    assert sha(res["M"]) == exp["M_sha256"]
+    if "M" in exp:
+        assert words_to_rows01(res["M"], n) == exp["M"]
+    assert sha(res["sel"]) == exp["sel_sha256"]
+    assert sha(res["allow"]) == exp["allow_sha256"]
+    assert csr_sha(*res["select_csr"]) == exp["select_policies_sha256"]
+    assert csr_sha(*res["allow_csr"]) == exp["allow_policies_sha256"]
+    assert res["all_reachable"] == exp["all_reachable"]
+    assert res["all_isolated"] == exp["all_isolated"]
+    assert res["user_crosscheck"] == exp["user_crosscheck"]["result"]
+    assert res["system_isolation"] == exp["system_isolation"]["result"]
+    pairs = res["policy_shadow"]
+    assert len(pairs) == exp["policy_shadow"]["count"]
+    assert sha(np.array(pairs, np.int32).reshape(-1, 2)) == exp["policy_shadow"]["sha256"]
+    if "raises" in exp["policy_conflict"]:
+        assert res["policy_conflict"] == ("raises", exp["policy_conflict"]["message"])
+    else:
+        assert res["policy_conflict"] == ("ok", exp["policy_conflict"]["result"])
+
+
+def test_paper_example_known_answers():
+    """kano_py/tests/test_basic.py:28-37 with paper_example."""
+    from sample import paper_example
+    from kano.model import ReachabilityMatrix
+    from kano.algorithm import (all_isolated, all_reachable, policy_conflict, policy_shadow,
+                                system_isolation, user_crosscheck)
+    cs, ps = paper_example()
+    m = ReachabilityMatrix.build_matrix(cs, ps)
+    assert m[0, 1] & m[2, 0] & m[4, 2]
+    assert all_reachable(m) == []
+    assert all_isolated(m) == [4]
+    assert user_crosscheck(m, cs, "app") == [1, 2, 3]
+    assert policy_shadow(m, ps, cs) == [(2, 3), (3, 2)]
+    assert system_isolation(m, 0) == [2, 4]
+    assert [r.to01() for r in m.matrix] == ["11010", "10010", "10010", "01000", "00100"]
+    assert [p.working_select_set.to01() for p in ps] == ["10010", "00001", "00100", "11100"]
+    assert [p.working_allow_set.to01() for p in ps] == ["01000", "00100", "10010", "10010"]
+    assert [c.select_policies for c in cs] == [[0, 3], [3], [2, 3], [0], [1]]
+    assert [c.allow_policies for c in cs] == [[2, 3], [0], [1], [2, 3], []]
+    assert m.getcol(0).to01() == "11100" and m.getrow(3).to01() == "01000"
+    with pytest.raises(AttributeError, match="'int' object has no attribute 'working_allow_set'"):
+        policy_conflict(m, ps, cs)
+    compare(api_record(m, cs, ps, "app"), expected("paper_example"))
+
+
+def test_paper_example_rebuilt_accumulates():
+    """Quirk Q5: a second build on the same objects appends again, and
+    policy_shadow then runs on the accumulated lists."""
+    from sample import paper_example
+    from kano.model import ReachabilityMatrix
+    cs, ps = paper_example()
+    ReachabilityMatrix.build_matrix(cs, ps)
+    m2 = ReachabilityMatrix.build_matrix(cs, ps)
+    compare(api_record(m2, cs, ps, "app"), expected("paper_example_rebuilt"))
+
+
+@pytest.mark.parametrize("name", cluster_names())
+def test_golden_cluster_api(name):
+    from kano.model import ReachabilityMatrix
+    obj = cluster(name)
+    cs, ps = api_objects(obj)
+    m = ReachabilityMatrix.build_matrix(cs, ps)
+    compare(api_record(m, cs, ps, obj.get("label", "app")), expected(name))
+
+
+@pytest.mark.parametrize("name", ["s_broad_300", "s_broad_1000", "s_sparse_1000",
+                                  "s_sparse_2000", "q_dirs", "q_shadow"])
+@pytest.mark.parametrize("path", ["bitwise", "mfma", "auto"])
+def test_build_paths_agree(name, path):
+    """The bitwise (LDS scatter / OR) and int8-MFMA contraction paths give
+    the same matrix and column checks."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern
+    obj = cluster(name)
+    cs, ps = api_objects(obj)
+    exp = expected(name)
+    eng = DeviceBuild(intern(cs, ps), path=path)
+    n = len(cs)
+    assert sha(eng.rows(0, n)) == exp["M_sha256"]
+    ca, co = eng.col_checks()
+    from kano._bits import set_bit_indices, words_to_bool
+    assert set_bit_indices(ca, n).tolist() == exp["all_reachable"]
+    assert np.flatnonzero(~words_to_bool(co, n)).tolist() == exp["all_isolated"]
+    if path == "mfma":
+        assert eng.info()["HEAVY"] > 0 or exp["P"] == 0
+    eng.close()
+
+
+def test_c2_engine_vs_kano_py():
+    """C2 (BASELINE configs[1]: 10k pods / 1k policies, seed 0) bit-exact
+    against kano_py's hashes, through the direct-table path of the bench."""
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano._bits import set_bit_indices, words_to_bool
+    from kano.synth import make_config, KEY_NAMES
+    exp = expected("C2")
+    cl = make_config("C2")
+    assert cl.fingerprint() == exp["seed"]["fingerprint"]
+    eng = DeviceBuild(tables_from_cluster(cl))
+    n = cl.n
+    assert sha(eng.rows(0, n)) == exp["M_sha256"]
+    ca, co = eng.col_checks()
+    assert set_bit_indices(ca, n).tolist() == exp["all_reachable"]
+    assert np.flatnonzero(~words_to_bool(co, n)).tolist() == exp["all_isolated"]
+    gid = cl.vals[KEY_NAMES.index("tenant")]
+    _, gid = np.unique(gid, return_inverse=True)
+    assert set_bit_indices(eng.crosscheck(gid), n).tolist() == exp["user_crosscheck"]["result"]
+    pairs = eng.shadow()
+    assert pairs.shape[0] == exp["policy_shadow"]["count"]
+    assert sha(pairs) == exp["policy_shadow"]["sha256"]
+    row0 = eng.rows(0, 1)[0]
+    assert np.flatnonzero(~words_to_bool(row0, n)).tolist() == exp["system_isolation"]["result"]
+    eng.close()
+
+
+def test_row_shards_combine_to_full():
+    """Row-sharded contexts (the multi-GPU partition) reproduce the full
+    matrix; their column flags combine by MAX (= OR) exactly."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern
+    from oracle import kano_oracle as orc
+    obj = cluster("s_sparse_2000")
+    cs, ps = api_objects(obj)
+    t = intern(cs, ps)
+    n = len(cs)
+    ref = orc.run_c(obj, label=obj["label"])
+    from kano._intern import group_ids
+    gid = group_ids(cs, obj["label"])
+    cuts = [0, 333, 1000, 1001, n]
+    rows, ors, nands, cross, pairs = [], [], [], [], []
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        e = DeviceBuild(t, rows=(r0, r1))
+        rows.append(e.rows(r0, r1 - r0))
+        ca, co = e.col_checks()
+        ors.append(co)
+        nands.append(~ca)
+        cross.append(e.crosscheck(gid))
+        pairs.append(e.shadow())
+        e.close()
+    assert np.array_equal(np.concatenate(rows), ref["M"])
+    from kano._bits import set_bit_indices, words_to_bool
+    co = np.bitwise_or.reduce(ors)
+    ca = ~np.bitwise_or.reduce(nands)
+    assert set_bit_indices(ca, n).tolist() == ref["all_reachable"]
+    assert np.flatnonzero(~words_to_bool(co, n)).tolist() == ref["all_isolated"]
+    assert set_bit_indices(np.bitwise_or.reduce(cross), n).tolist() == ref["user_crosscheck"]
+    assert np.array_equal(np.concatenate(pairs), ref["shadow"])
+
+
+def test_mutation_then_checks():
+    """m[i, j] = v writes the device matrix; checks then see the new matrix."""
+    from kano.model import ReachabilityMatrix
+    from kano.algorithm import all_isolated, all_reachable, user_crosscheck, system_isolation
+    from oracle import kano_oracle as orc
+    obj = cluster("s_sparse_200")
+    cs, ps = api_objects(obj)
+    m = ReachabilityMatrix.build_matrix(cs, ps)
+    n = len(cs)
+    iso = all_isolated(m)
+    assert iso, "fixture needs an isolated column"
+    j = iso[0]
+    m[5, j] = 1
+    assert m[5, j] == 1 and m.getrow(5)[j] == 1
+    assert j not in all_isolated(m)
+    row = m.matrix[7]
+    row.setall(1)
+    assert m.getrow(7).count() == n
+    M = m.engine.rows(0, n)
+    from _golden import words_to_rows01
+    # oracle checks over the mutated matrix
+    import ctypes
+    reach = np.zeros(n, np.uint8)
+    isol = np.zeros(n, np.uint8)
+    orc.lib().oracle_column_checks(n, orc._p(np.ascontiguousarray(M)), 0, n, orc._p(reach),
+                                   orc._p(isol))
+    assert all_reachable(m) == np.flatnonzero(reach).tolist()
+    assert all_isolated(m) == np.flatnonzero(isol).tolist()
+    gid = orc.group_ids_json(obj, obj["label"])
+    cross = np.zeros(n, np.uint8)
+    orc.lib().oracle_crosscheck(n, orc._p(np.ascontiguousarray(M)), orc._p(gid), 0, n,
+                                orc._p(cross))
+    assert user_crosscheck(m, cs, obj["label"]) == np.flatnonzero(cross).tolist()
+    assert system_isolation(m, 7) == []
+
+
+def test_explicit_matrix_constructor():
+    from kano.model import ReachabilityMatrix, BitArray
+    from kano.algorithm import all_reachable, all_isolated, system_isolation
+    rows = ["110", "010", "011"]
+    m = ReachabilityMatrix(3, [BitArray(r) for r in rows])
+    assert [r.to01() for r in m.matrix] == rows
+    assert all_reachable(m) == [1] and all_isolated(m) == [] and system_isolation(m, 1) == [0, 2]
+
+
+def test_degenerate_sizes():
+    from kano.model import ReachabilityMatrix, Container, Policy, PolicySelect, PolicyAllow
+    from kano.model import PolicyEgress, PolicyProtocol
+    from kano.algorithm import all_reachable, all_isolated, policy_shadow, policy_conflict
+    m = ReachabilityMatrix.build_matrix([], [])
+    assert all_reachable(m) == [] and all_isolated(m) == [] and policy_shadow(m, [], []) == []
+    cs = [Container("a", {"x": "1"}), Container("b", {})]
+    m = ReachabilityMatrix.build_matrix(cs, [])
+    assert all_isolated(m) == [0, 1] and policy_conflict(m, [], cs) == []
+    ps = [Policy("p", PolicySelect({}), PolicyAllow({}), PolicyEgress, PolicyProtocol([]))]
+    m = ReachabilityMatrix.build_matrix(cs, ps)
+    assert all_reachable(m) == [0, 1] and [r.to01() for r in m.matrix] == ["11", "11"]
