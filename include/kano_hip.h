@@ -54,6 +54,9 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_ROW0     7
 #define KANO_INFO_ROW1     8
 #define KANO_INFO_MAXSEL   9   /* max over classes of |S(c)|                  */
+#define KANO_INFO_UA      10   /* column classes (pods with equal allow keys) */
+#define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 int8 MFMA          */
+#define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the row kernel */
 #define KANO_INFO_NSLOTS   16
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in
@@ -74,9 +77,10 @@ int kano_set_policies(kano_ctx* ctx, int64_t P,
  * partition); default = all rows. */
 int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end);
 
-/* ReachabilityMatrix.build_matrix (kano_py/kano/model.py:125-165): row classes,
- * selector evaluation (select side per class, allow side per pod), the
- * per-policy allow lists and the matrix rows M[i] = OR_{p in S(i)} allow_p. */
+/* ReachabilityMatrix.build_matrix (kano_py/kano/model.py:125-165): row classes
+ * (pods with equal working-selector key values) and column classes (equal
+ * working-allow key values), selector evaluation on both, the per-policy
+ * allowed pods and the matrix rows M[i] = OR_{p in S(i)} allow_p. */
 int kano_build(kano_ctx* ctx, int path);
 int kano_info(kano_ctx* ctx, int64_t* out /* KANO_INFO_NSLOTS */);
 
@@ -113,8 +117,8 @@ int kano_get_policy_sets(kano_ctx* ctx, int64_t p, uint64_t* sel, uint64_t* allo
  * class-level ascending policy lists, CSR over classes. */
 int kano_get_classes(kano_ctx* ctx, int32_t* cls /* n */);
 int kano_get_select_csr(kano_ctx* ctx, int64_t* off /* U+1 */, int32_t* pol /* nnz_sel */);
-/* Container.allow_policies (model.py:162-163) and the allow sets as sorted pod
- * lists, CSR over policies. */
+/* Container.allow_policies (model.py:162-163) and the allow sets as pod
+ * lists (grouped by column class, not sorted), CSR over policies. */
 int kano_get_allow_csr(kano_ctx* ctx, int64_t* off /* P+1 */, int32_t* pods /* nnz_alw */);
 
 /* policy_shadow (kano_py/kano/algorithm.py:58-80): emits, for this shard's
@@ -139,8 +143,8 @@ int kano_shadow_lists(kano_ctx* ctx, int64_t n_lists, int64_t nbits, int64_t P,
 int kano_conflict(kano_ctx* ctx, int* raises);
 
 /* Timing of the last kano_build / kano_shadow stages on the context stream
- * (HIP events), milliseconds: [classes, select, allow, rows stage, shadow,
- * build total, k_rows kernel alone, 0]. */
+ * (HIP events), milliseconds: [classes, allow, select + plan, rows stage,
+ * shadow, build total, k_rows kernel alone, 0]. */
 int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
 
 /* Page-locked host buffers for fast device-to-host result copies. */

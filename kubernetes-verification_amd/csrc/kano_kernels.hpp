@@ -1,0 +1,713 @@
+// kano_kernels.hpp -- HIP kernels of the Kano engine for gfx950.
+// Host orchestration and the C ABI: kano_hip.hip.  Design: DESIGN.md.
+//
+// Reference semantics (qiyueyao/Kubernetes-verification, kano_py/kano/):
+//   selector predicate         model.py:95-111 + 142-147
+//   matrix rows                model.py:158-160   M[i] |= allow_p for p in S(i)
+//   column checks              algorithm.py:4-17
+//   user_crosscheck            algorithm.py:27-42
+//   policy_shadow              algorithm.py:58-80
+#pragma once
+#include "kano_prims.hpp"
+
+namespace kano {
+
+// ===========================================================================
+// Classes: pods hashed on the values of a key set.  Pods of one class are
+// indistinguishable to every predicate on those keys.
+// ===========================================================================
+__global__ __launch_bounds__(TPB) void k_class_insert(const int32_t* __restrict__ pv, i64 n,
+                                                      const int32_t* __restrict__ keys, int KS,
+                                                      int32_t* table, uint32_t tmask,
+                                                      int32_t* __restrict__ slot_of) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = 0x9747b28cu;
+  for (int k = 0; k < KS; ++k) h = hmix(h, (uint32_t)pv[(i64)keys[k] * n + i]);
+  uint32_t s = hfin(h) & tmask;
+  for (;;) {  // linear probing; the table has >= 2n slots, so this ends
+    int32_t cur = __hip_atomic_load(&table[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur < 0) {
+      const int32_t prev = atomicCAS(&table[s], -1, (int32_t)i);
+      if (prev < 0) { slot_of[i] = (int32_t)s; return; }
+      cur = prev;
+    }
+    bool eq = true;
+    for (int k = 0; k < KS; ++k) {
+      const int32_t* col = pv + (i64)keys[k] * n;
+      if (col[cur] != col[i]) { eq = false; break; }
+    }
+    if (eq) { slot_of[i] = (int32_t)s; return; }
+    s = (s + 1) & tmask;
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_class_min(const int32_t* __restrict__ slot_of, i64 n,
+                                                   int32_t* smin) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) atomicMin(&smin[slot_of[i]], (int32_t)i);
+}
+
+__global__ __launch_bounds__(TPB) void k_class_flag(const int32_t* __restrict__ slot_of, i64 n,
+                                                    const int32_t* __restrict__ smin,
+                                                    int32_t* __restrict__ flag) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) flag[i] = (smin[slot_of[i]] == (int32_t)i) ? 1 : 0;
+}
+
+// class ids ordered by their smallest member (deterministic)
+__global__ __launch_bounds__(TPB) void k_class_assign(const int32_t* __restrict__ slot_of, i64 n,
+                                                      const int32_t* __restrict__ smin,
+                                                      const int32_t* __restrict__ cid,
+                                                      int32_t* __restrict__ cls,
+                                                      int32_t* __restrict__ rep) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const int32_t r = smin[slot_of[i]];
+  const int32_t c = cid[r];
+  cls[i] = c;
+  if (r == (int32_t)i) rep[c] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(TPB) void k_member_count(const int32_t* __restrict__ cls, i64 m0,
+                                                      i64 m1, int32_t* mcnt) {
+  const i64 i = m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i < m1) atomicAdd(&mcnt[cls[i]], 1);
+}
+
+__global__ __launch_bounds__(TPB) void k_member_fill(const int32_t* __restrict__ cls, i64 m0,
+                                                     i64 m1, const int32_t* __restrict__ moff,
+                                                     int32_t* mcur, int32_t* __restrict__ mem) {
+  const i64 i = m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= m1) return;
+  const int32_t c = cls[i];
+  mem[moff[c] + atomicAdd(&mcur[c], 1)] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(TPB) void k_class_vals(const int32_t* __restrict__ pv, i64 n,
+                                                    const int32_t* __restrict__ keys, int KS,
+                                                    const int32_t* __restrict__ rep, i64 U,
+                                                    int32_t* __restrict__ cval) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (c >= U) return;
+  const int32_t r = rep[c];
+  for (int k = 0; k < KS; ++k) cval[(i64)k * U + c] = pv[(i64)keys[k] * n + r];
+}
+
+// ===========================================================================
+// Predicate evaluation on classes.
+//   match(p, c) = AND over terms (slot, v): cval[slot][c] == v
+// One thread per class, 64 policies per grid row.  Emits the class-major
+// word outT[pb][c] (bit q = policy 64*pb+q) and/or, through a ballot per
+// policy, the policy-major word outP[p][c/64] (bit c%64).
+// ===========================================================================
+__global__ __launch_bounds__(TPB) void k_class_eval(const int32_t* __restrict__ cval, i64 U, i64 P,
+                                                    const i64* __restrict__ off,
+                                                    const int32_t* __restrict__ slot,
+                                                    const int32_t* __restrict__ val,
+                                                    u64* __restrict__ outT,
+                                                    u64* __restrict__ outP, i64 ldP) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  const i64 pb = blockIdx.y;
+  const i64 p0 = pb * 64;
+  const int qn = (int)min((i64)64, P - p0);
+  const bool live = c < U;
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  const i64 cw = c >> 6;
+  u64 word = 0;
+  for (int q = 0; q < qn; ++q) {
+    const i64 p = p0 + q;
+    const i64 t0 = off[p], t1 = off[p + 1];
+    bool ok = live;
+    for (i64 t = t0; t < t1 && ok; ++t) ok = cval[(i64)slot[t] * U + c] == val[t];
+    word |= (u64)ok << q;
+    if (outP) {
+      const u64 b = __ballot(ok);
+      if (lane0 && cw * 64 < U) outP[p * ldP + cw] = b;
+    }
+  }
+  if (live && outT) outT[pb * U + c] = word;
+}
+
+// ===========================================================================
+// Allow side: policy -> allowed column classes -> allowed pods
+// ===========================================================================
+// block per policy: nca[p] = #allowed classes, acnt[p] = #allowed pods
+__global__ __launch_bounds__(TPB) void k_pol_count(const u64* __restrict__ AC, i64 ldC, i64 UW,
+                                                   const int32_t* __restrict__ cmoff,
+                                                   int32_t* __restrict__ nca,
+                                                   int32_t* __restrict__ acnt) {
+  __shared__ i64 sm[4];
+  const i64 p = blockIdx.x;
+  i64 nc = 0, np = 0;
+  for (i64 w = threadIdx.x; w < UW; w += TPB) {
+    u64 v = AC[p * ldC + w];
+    nc += __popcll(v);
+    if (cmoff) {
+      while (v) {
+        const i64 ca = w * 64 + __builtin_ctzll(v);
+        np += cmoff[ca + 1] - cmoff[ca];
+        v &= v - 1;
+      }
+    }
+  }
+  nc = block_sum(nc, sm);
+  np = block_sum(np, sm);
+  if (threadIdx.x == 0) {
+    nca[p] = (int32_t)nc;
+    acnt[p] = (int32_t)(cmoff ? np : nc);
+  }
+}
+
+// block per policy: ascending list of allowed classes
+__global__ __launch_bounds__(TPB) void k_pol_classes(const u64* __restrict__ AC, i64 ldC, i64 UW,
+                                                     const i64* __restrict__ alcoff,
+                                                     int32_t* __restrict__ alc) {
+  __shared__ int sm[4];
+  const i64 p = blockIdx.x;
+  i64 base = alcoff[p];
+  for (i64 w0 = 0; w0 < UW; w0 += TPB) {
+    const i64 w = w0 + threadIdx.x;
+    u64 v = (w < UW) ? AC[p * ldC + w] : 0ull;
+    int tot;
+    i64 pos = base + block_excl_scan((int)__popcll(v), sm, tot);
+    while (v) {
+      alc[pos++] = (int32_t)(w * 64 + __builtin_ctzll(v));
+      v &= v - 1;
+    }
+    base += tot;
+  }
+}
+
+// block per policy: the allowed pods (members of the allowed classes)
+__global__ __launch_bounds__(TPB) void k_pol_pods(const i64* __restrict__ alcoff,
+                                                  const int32_t* __restrict__ alc,
+                                                  const int32_t* __restrict__ cmoff,
+                                                  const int32_t* __restrict__ cmem,
+                                                  const i64* __restrict__ aloff,
+                                                  int32_t* __restrict__ alist) {
+  const i64 p = blockIdx.x;
+  i64 out = aloff[p];
+  for (i64 e = alcoff[p]; e < alcoff[p + 1]; ++e) {
+    const int32_t ca = alc[e];
+    const int32_t m0 = cmoff[ca], m1 = cmoff[ca + 1];
+    for (int32_t m = m0 + threadIdx.x; m < m1; m += TPB) alist[out + (m - m0)] = cmem[m];
+    out += m1 - m0;
+  }
+}
+
+// ===========================================================================
+// Select side: per row class, |S(c)|, rebuild cost, work items, heavy flag
+// ===========================================================================
+struct ClassPlan {
+  const u64* selT;         // [PB][U]
+  i64 U, PB;
+  const int32_t* mcnt;     // local members per class
+  const int32_t* acnt;     // pods allowed per policy
+  i64 W;                   // words per matrix row
+  int ch;                  // members per work item
+  int force;               // 0 cost-based, 1 never heavy, 2 heavy when S(c) non-empty
+  i64 heavy_factor;        // heavy when cost > heavy_factor * W (and > 1 chunk)
+  int32_t* scnt;           // out |S(c)|
+  int32_t* wicnt;          // out work items of the class
+  int32_t* hflag;          // out 1 = heavy
+  i64* sq;                 // out |S(c)|^2 for classes with local members
+  int32_t* maxs;           // out max |S(c)| over classes with local members
+};
+
+__global__ __launch_bounds__(TPB) void k_class_plan(ClassPlan a) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (c >= a.U) return;
+  int s = 0;
+  i64 cost = 0;
+  for (i64 pb = 0; pb < a.PB; ++pb) {
+    u64 w = a.selT[pb * a.U + c];
+    s += __popcll(w);
+    while (w) {
+      cost += min((i64)a.acnt[pb * 64 + __builtin_ctzll(w)], 64 * a.W);
+      w &= w - 1;
+    }
+  }
+  const int32_t m = a.mcnt[c];
+  a.scnt[c] = s;
+  const int32_t chunks = (m + a.ch - 1) / a.ch;
+  a.wicnt[c] = chunks;
+  int hv = 0;
+  if (m > 0 && s > 0) {
+    if (a.force == 2) hv = 1;
+    else if (a.force == 0) hv = cost > a.heavy_factor * a.W * (chunks > 1 ? 1 : 8);
+  }
+  a.hflag[c] = hv;
+  a.sq[c] = m > 0 ? (i64)s * s : 0;
+  if (m > 0) atomicMax(a.maxs, s);
+}
+
+__global__ __launch_bounds__(TPB) void k_sel_fill(const u64* __restrict__ selT, i64 U, i64 PB,
+                                                  const i64* __restrict__ soffc,
+                                                  int32_t* __restrict__ slist) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (c >= U) return;
+  i64 pos = soffc[c];
+  for (i64 pb = 0; pb < PB; ++pb) {
+    u64 w = selT[pb * U + c];
+    while (w) {
+      slist[pos++] = (int32_t)(pb * 64 + __builtin_ctzll(w));
+      w &= w - 1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_sq_from_off(const i64* __restrict__ off, i64 U,
+                                                     i64* __restrict__ sq) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (c < U) sq[c] = (off[c + 1] - off[c]) * (off[c + 1] - off[c]);
+}
+
+__global__ __launch_bounds__(TPB) void k_flag_list(const int32_t* __restrict__ flag,
+                                                   const int32_t* __restrict__ off, i64 U,
+                                                   int32_t* __restrict__ list) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (c < U && flag[c]) list[off[c]] = (int32_t)c;
+}
+
+// ===========================================================================
+// Heavy rows: the row of the class over COLUMN classes, Mc[h] = OR_{p in S}
+// AllowC[p], then expanded to pods (bit j = Mc[h][cla[j]]).
+// ===========================================================================
+// bitwise: one thread per Mc word
+__global__ __launch_bounds__(TPB) void k_heavy_mc_or(const int32_t* __restrict__ hlist,
+                                                     const i64* __restrict__ soffc,
+                                                     const int32_t* __restrict__ slist,
+                                                     const u64* __restrict__ AC, i64 ldC, i64 UW,
+                                                     u64* __restrict__ Mc, i64 ldMc) {
+  const int32_t c = hlist[blockIdx.x];
+  const i64 w = (i64)blockIdx.y * TPB + threadIdx.x;
+  if (w >= ldMc) return;
+  u64 acc = 0;
+  if (w < UW) {
+    const i64 s0 = soffc[c], s1 = soffc[c + 1];
+    for (i64 e = s0; e < s1; ++e) acc |= AC[(i64)slist[e] * ldC + w];
+  }
+  Mc[(i64)blockIdx.x * ldMc + w] = acc;
+}
+
+// int8 MFMA contraction (the dense path):
+//   C[h][ca] = sum_p Sel[h][p] * Allow[p][ca]   (i8 x i8 -> i32),  bit = C > 0
+// A = selT[pb][c] bits of the heavy row classes, B = ACT[pb][ca] bits of the
+// column classes (class-major), both expanded to 0/1 bytes in registers.
+// v_mfma_i32_32x32x32_i8: lane l supplies A[l&31][16*(l>>5)+0..15] and
+// B[16*(l>>5)+0..15][l&31]; accumulator reg g of lane l holds row
+// (g&3)+8*(g>>2)+4*(l>>5), column l&31 (cdna_hip_programming.md §3).  Any
+// consistent k order gives the same sum, so A and B share the byte order.
+// One wave = up to 32*HT heavy rows x 32 column classes; K = all policies.
+typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t spread4(uint32_t b4) {
+  return (b4 & 1u) | ((b4 & 2u) << 7) | ((b4 & 4u) << 14) | ((b4 & 8u) << 21);
+}
+__device__ __forceinline__ i32x4 expand16(uint32_t b16) {
+  i32x4 r;
+  r[0] = (int32_t)spread4(b16 & 15u);
+  r[1] = (int32_t)spread4((b16 >> 4) & 15u);
+  r[2] = (int32_t)spread4((b16 >> 8) & 15u);
+  r[3] = (int32_t)spread4((b16 >> 12) & 15u);
+  return r;
+}
+
+template <int HT>
+__global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ selT, i64 U,
+                                                       const int32_t* __restrict__ hlist, int H,
+                                                       const u64* __restrict__ ACT, i64 Ua,
+                                                       i64 PB, uint32_t* __restrict__ Mc32,
+                                                       i64 ldMc) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const i64 jt = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);  // 32-column tile
+  if (jt >= 2 * ldMc) return;                                        // wave-uniform
+  const i64 ca = jt * 32 + l32;
+  int32_t hc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t) {
+    const int h = t * 32 + l32;
+    hc[t] = h < H ? hlist[h] : -1;
+  }
+  i32x16 acc[HT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[t][g] = 0;
+  for (i64 pb = 0; pb < PB; ++pb) {
+    const u64 bw = ca < Ua ? ACT[pb * Ua + ca] : 0ull;
+    u64 aw[HT];
+#pragma unroll
+    for (int t = 0; t < HT; ++t) aw[t] = hc[t] >= 0 ? selT[pb * U + hc[t]] : 0ull;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int sh = ks * 32 + half * 16;
+      const i32x4 bfrag = expand16((uint32_t)(bw >> sh) & 0xffffu);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        const i32x4 afrag = expand16((uint32_t)(aw[t] >> sh) & 0xffffu);
+        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag, bfrag, acc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < HT; ++t) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const u64 bal = __ballot(acc[t][g] > 0);
+      if (lane == 0 || lane == 32) {
+        const int r = t * 32 + (g & 3) + 8 * (g >> 2) + (lane == 32 ? 4 : 0);
+        if (r < H) Mc32[(i64)r * ldMc * 2 + jt] = lane == 0 ? (uint32_t)bal : (uint32_t)(bal >> 32);
+      }
+    }
+  }
+}
+
+// expansion: M[first member of heavy class h] bit j = Mc[h][cla[j]]; one wave
+// per 64-pod word, the whole padded row is written
+__global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict__ hlist,
+                                                      const u64* __restrict__ Mc, i64 ldMc,
+                                                      const int32_t* __restrict__ cla, i64 n,
+                                                      const int32_t* __restrict__ moff,
+                                                      const int32_t* __restrict__ mem,
+                                                      u64* __restrict__ M, i64 ldM, i64 r0) {
+  const i64 h = blockIdx.y;
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  const i64 w = j >> 6;
+  if ((w << 6) >= ldM * 64) return;                 // wave-uniform
+  bool bit = false;
+  if (j < n) {
+    const int32_t ca = cla[j];
+    bit = (Mc[h * ldMc + (ca >> 6)] >> (ca & 63)) & 1ull;
+  }
+  const u64 bal = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && w < ldM) {
+    const int32_t c = hlist[h];
+    M[(i64)(mem[moff[c]] - r0) * ldM + w] = bal;
+  }
+}
+
+// ===========================================================================
+// Matrix rows (model.py:158-160).  One block = one work item (class, up to
+// ch member pods, column chunk of cww words).  Light classes rebuild their
+// row in LDS from the allowed-pod lists of S(c) (LDS 64-bit atomic OR);
+// heavy classes copy the row prebuilt at their first member.  The row is then
+// streamed to every member row (16-byte stores).  The first chunk of every
+// class folds the row into the column OR / NAND (all_isolated /
+// all_reachable) with global atomics, skipping saturated words.
+// ===========================================================================
+struct RowsArgs {
+  const int32_t* wioff;  // U+1
+  i64 U;
+  const i64* soffc;      // U+1
+  const int32_t* slist;
+  const int32_t* acnt;
+  const i64* aloff;
+  const int32_t* alist;
+  const int32_t* moff;   // U+1
+  const int32_t* mem;
+  const int32_t* hflag;  // U (nullable)
+  u64* M;
+  i64 ldM;
+  i64 r0;
+  i64 n, W;
+  int ch;
+  int cww;
+  u64* color;
+  u64* colnand;
+};
+
+__global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u64 row[];
+  const i64 b = blockIdx.x;
+  const i64 c = upper_bound_i32(a.wioff, a.U + 1, b) - 1;
+  if (c < 0 || c >= a.U) return;
+  const i64 chunk = b - a.wioff[c];
+  const i64 base = (i64)blockIdx.y * a.cww;
+  const i64 ldw = a.ldM;
+  const int nw = (int)min((i64)a.cww, ldw - base);
+  if (nw <= 0) return;
+  const int32_t m_begin = a.moff[c], m_end = a.moff[c + 1];
+  const int32_t m0 = m_begin + (int32_t)(chunk * a.ch);
+  const int32_t m1 = min(m_end, m0 + a.ch);
+  const bool heavy = a.hflag && a.hflag[c];
+
+  if (heavy) {
+    const u64* src = a.M + (i64)(a.mem[m_begin] - a.r0) * ldw + base;
+    for (int w = threadIdx.x * 2; w < nw; w += TPB * 2)
+      *(ulonglong2*)&row[w] = *(const ulonglong2*)&src[w];
+    __syncthreads();
+  } else {
+    for (int w = threadIdx.x; w < nw; w += TPB) row[w] = 0ull;
+    __syncthreads();
+    const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
+    const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
+    for (i64 e = s0; e < s1; ++e) {
+      const int32_t p = a.slist[e];
+      const int32_t* L = a.alist + a.aloff[p];
+      const i64 cnt = a.acnt[p];
+      for (i64 k = threadIdx.x; k < cnt; k += TPB) {
+        const int32_t j = L[k];
+        if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+      }
+    }
+    __syncthreads();
+  }
+  for (int32_t m = m0; m < m1; ++m) {
+    if (heavy && m == m_begin) continue;
+    u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
+    for (int w = threadIdx.x * 2; w < nw; w += TPB * 2)
+      *(ulonglong2*)&dst[w] = *(const ulonglong2*)&row[w];
+  }
+  if (chunk == 0 && a.color) {
+    for (int w = threadIdx.x; w < nw; w += TPB) {
+      const i64 gw = base + w;
+      if (gw >= a.W) break;
+      const u64 v = row[w];
+      const u64 vm = valid_mask(gw, a.n);
+      if (v & ~__hip_atomic_load(&a.color[gw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(&a.color[gw], v);
+      const u64 nv = ~v & vm;
+      if (nv && __hip_atomic_load(&a.colnand[gw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != vm)
+        atomicOr(&a.colnand[gw], nv);
+    }
+  }
+}
+
+// ===========================================================================
+// Checks
+// ===========================================================================
+__global__ __launch_bounds__(TPB) void k_col_final(const u64* __restrict__ colnand, i64 W, i64 n,
+                                                   u64* __restrict__ col_and) {
+  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (w < W) col_and[w] = ~colnand[w] & valid_mask(w, n);
+}
+
+// one byte per column
+__global__ __launch_bounds__(TPB) void k_unpack_flags(const u64* __restrict__ words, i64 n,
+                                                      uint8_t* __restrict__ out) {
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (j < n) out[j] = (uint8_t)((words[j >> 6] >> (j & 63)) & 1ull);
+}
+
+// user_crosscheck.  cross[j] = exists row i: M[i,j] and g(i) != g(j).
+// Rows of a class are equal; a class whose local members carry >= 2 groups
+// reaches every set column from another group (MULTI); single-group classes
+// are ORed per group into R[g].  Then with A1 = OR_g R[g], A2 = bits set by
+// >= 2 groups (atomicOr's previous value), own[j] = R[g(j)][j]:
+//   cross = MULTI | A2 | (A1 & ~own)
+__global__ __launch_bounds__(TPB) void k_cross_classgroup(const int32_t* __restrict__ gid,
+                                                          const int32_t* __restrict__ moff,
+                                                          const int32_t* __restrict__ mem, i64 U,
+                                                          int32_t* __restrict__ cgroup) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (c >= U) return;
+  const int32_t m0 = moff[c], m1 = moff[c + 1];
+  int32_t g = -2;  // -2: no local members, -1: several groups
+  if (m1 > m0) {
+    g = gid[mem[m0]];
+    for (int32_t m = m0 + 1; m < m1; ++m)
+      if (gid[mem[m]] != g) { g = -1; break; }
+  }
+  cgroup[c] = g;
+}
+
+__global__ __launch_bounds__(TPB) void k_cross_accum(const int32_t* __restrict__ cgroup,
+                                                     const int32_t* __restrict__ moff,
+                                                     const int32_t* __restrict__ mem,
+                                                     const u64* __restrict__ M, i64 ldM, i64 r0,
+                                                     i64 W, int32_t g0, int32_t g1,
+                                                     u64* __restrict__ R, u64* __restrict__ multi) {
+  const i64 c = blockIdx.x;
+  const int32_t g = cgroup[c];
+  if (g == -2) return;
+  const bool is_multi = g == -1;
+  if (is_multi && g0 != 0) return;  // multi rows are folded in by the first pass only
+  if (!is_multi && (g < g0 || g >= g1)) return;
+  const u64* src = M + (i64)(mem[moff[c]] - r0) * ldM;
+  u64* dst = is_multi ? multi : R + (i64)(g - g0) * ldM;
+  for (i64 w = (i64)blockIdx.y * TPB + threadIdx.x; w < W; w += (i64)gridDim.y * TPB) {
+    const u64 v = src[w];
+    if (v) atomicOr(&dst[w], v);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_cross_groups(const u64* __restrict__ R, i64 ldM, i64 W,
+                                                      u64* __restrict__ A1, u64* __restrict__ A2) {
+  const i64 g = blockIdx.x;
+  for (i64 w = (i64)blockIdx.y * TPB + threadIdx.x; w < W; w += (i64)gridDim.y * TPB) {
+    const u64 r = R[g * ldM + w];
+    if (!r) continue;
+    const u64 old = atomicOr(&A1[w], r);
+    if (old & r) atomicOr(&A2[w], old & r);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_cross_own(const int32_t* __restrict__ gid, i64 n,
+                                                   const u64* __restrict__ R, i64 ldM, int32_t g0,
+                                                   int32_t g1, u64* __restrict__ own) {
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  bool bit = false;
+  if (j < n) {
+    const int32_t g = gid[j];
+    if (g >= g0 && g < g1) bit = (R[(i64)(g - g0) * ldM + (j >> 6)] >> (j & 63)) & 1ull;
+  }
+  const u64 bal = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && bal) atomicOr(&own[j >> 6], bal);
+}
+
+__global__ __launch_bounds__(TPB) void k_cross_final(const u64* __restrict__ multi,
+                                                     const u64* __restrict__ A1,
+                                                     const u64* __restrict__ A2,
+                                                     const u64* __restrict__ own, i64 W, i64 n,
+                                                     u64* __restrict__ cross) {
+  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (w < W) cross[w] = (multi[w] | A2[w] | (A1[w] & ~own[w])) & valid_mask(w, n);
+}
+
+// getcol (model.py:180-184): bit r = M[r][j] over the local rows
+__global__ __launch_bounds__(TPB) void k_get_col(const u64* __restrict__ M, i64 ldM, i64 rows,
+                                                 i64 j, u64* __restrict__ out) {
+  const i64 r = (i64)blockIdx.x * TPB + threadIdx.x;
+  const bool bit = r < rows && ((M[r * ldM + (j >> 6)] >> (j & 63)) & 1ull);
+  const u64 bal = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && r < rows) out[r >> 6] = bal;
+}
+
+// working_select_set of policy p over all pods
+__global__ __launch_bounds__(TPB) void k_sel_row(const u64* __restrict__ selT, i64 U,
+                                                 const int32_t* __restrict__ cls, i64 n, i64 p,
+                                                 u64* __restrict__ out) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  const bool bit = i < n && ((selT[(p >> 6) * U + cls[i]] >> (p & 63)) & 1ull);
+  const u64 bal = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && i < n) out[i >> 6] = bal;
+}
+
+// working_allow_set of policy p over all pods
+__global__ __launch_bounds__(TPB) void k_allow_row(const u64* __restrict__ AC, i64 ldC, i64 p,
+                                                   const int32_t* __restrict__ cla, i64 n,
+                                                   u64* __restrict__ out) {
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  bool bit = false;
+  if (j < n) {
+    const int32_t ca = cla[j];
+    bit = (AC[p * ldC + (ca >> 6)] >> (ca & 63)) & 1ull;
+  }
+  const u64 bal = __ballot(bit);
+  if ((threadIdx.x & 63) == 0 && j < n) out[j >> 6] = bal;
+}
+
+// ===========================================================================
+// policy_shadow (algorithm.py:58-80) on row classes.  Pair (a, b) of S(c)
+// positions, a != b:  flag = allow_{S[b]} is a subset of allow_{S[a]}, tested
+// on column classes (they partition the pods and none is empty, so the pod
+// sets nest exactly when the class sets do).
+// ===========================================================================
+__device__ __forceinline__ bool subset_of(int32_t k, int32_t j, const int32_t* nca,
+                                          const i64* alcoff, const int32_t* alc, const u64* AC,
+                                          i64 ldC) {
+  const int32_t ck = nca[k];
+  if (ck == 0) return true;
+  if (ck > nca[j]) return false;
+  const int32_t* L = alc + alcoff[k];
+  const u64* aj = AC + (i64)j * ldC;
+  for (int32_t e = 0; e < ck; ++e) {
+    const int32_t x = L[e];
+    if (!((aj[x >> 6] >> (x & 63)) & 1ull)) return false;
+  }
+  return true;
+}
+
+struct ShadowArgs {
+  const i64* soffc;
+  const int32_t* slist;
+  const int32_t* mcnt;
+  const i64* pfoff;
+  const int32_t* nca;
+  const i64* alcoff;
+  const int32_t* alc;
+  const u64* AC;
+  i64 ldC;
+  uint8_t* flags;
+  i64* T;
+};
+
+__global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a) {
+  __shared__ i64 sm[4];
+  const i64 c = blockIdx.x;
+  if (a.mcnt[c] == 0) {
+    if (threadIdx.x == 0) a.T[c] = 0;
+    return;
+  }
+  const i64 s0 = a.soffc[c];
+  const i64 s = a.soffc[c + 1] - s0;
+  const i64 ss = s * s;
+  i64 cnt = 0;
+  for (i64 t = threadIdx.x; t < ss; t += TPB) {
+    const i64 x = t / s, y = t - x * s;
+    uint8_t f = 0;
+    if (x != y) {
+      const int32_t j = a.slist[s0 + x], k = a.slist[s0 + y];
+      f = (j != k) && subset_of(k, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+    }
+    a.flags[a.pfoff[c] + t] = f;
+    cnt += f;
+  }
+  cnt = block_sum(cnt, sm);
+  if (threadIdx.x == 0) a.T[c] = cnt;
+}
+
+__global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ soffc,
+                                                        const int32_t* __restrict__ slist,
+                                                        const i64* __restrict__ pfoff,
+                                                        const uint8_t* __restrict__ flags,
+                                                        const i64* __restrict__ loff,
+                                                        int2* __restrict__ L) {
+  __shared__ i64 sm[4];
+  const i64 c = blockIdx.x;
+  i64 out = loff[c];
+  if (loff[c + 1] == out) return;
+  const i64 s0 = soffc[c];
+  const i64 s = soffc[c + 1] - s0;
+  const i64 ss = s * s;
+  for (i64 t0 = 0; t0 < ss; t0 += TPB) {
+    const i64 t = t0 + threadIdx.x;
+    const i64 f = (t < ss) ? flags[pfoff[c] + t] : 0;
+    i64 tot;
+    const i64 pos = out + block_excl_scan(f, sm, tot);
+    if (f) {
+      const i64 x = t / s, y = t - x * s;
+      L[pos] = make_int2(slist[s0 + x], slist[s0 + y]);
+    }
+    out += tot;
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_shadow_podcount(const int32_t* __restrict__ cls, i64 r0,
+                                                         i64 r1, const i64* __restrict__ loff,
+                                                         i64* __restrict__ tp) {
+  const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= r1) return;
+  const int32_t c = cls[i];
+  tp[i - r0] = loff[c + 1] - loff[c];
+}
+
+// one wave per pod: out[poff[i] ...] = L_cls(i)
+__global__ __launch_bounds__(TPB) void k_shadow_emit(const int32_t* __restrict__ cls, i64 r0,
+                                                     i64 r1, const i64* __restrict__ loff,
+                                                     const int2* __restrict__ L,
+                                                     const i64* __restrict__ poff,
+                                                     int2* __restrict__ out) {
+  const i64 i = r0 + (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  if (i >= r1) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t c = cls[i];
+  const i64 l0 = loff[c], len = loff[c + 1] - l0;
+  const i64 o = poff[i - r0];
+  for (i64 k = lane; k < len; k += 64) out[o + k] = L[l0 + k];
+}
+
+}  // namespace kano

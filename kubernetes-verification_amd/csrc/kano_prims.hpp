@@ -1,0 +1,117 @@
+// kano_prims.hpp -- wave64 / block primitives and the device-wide scan used
+// by the engine (kano_hip.hip).  gfx950: 64-lane waves, 256-thread blocks.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+typedef unsigned long long u64;
+typedef long long i64;
+
+namespace kano {
+
+constexpr int TPB = 256;              // threads per block for every kernel
+constexpr int SCAN_ITEMS = 8;         // elements per thread in a scan tile
+constexpr int SCAN_TILE = TPB * SCAN_ITEMS;
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Exclusive scan over a 256-thread block; smem holds >= 4 elements.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* smem, T& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T inc = wave_incl_scan(v);
+  if (lane == 63) smem[wid] = inc;
+  __syncthreads();
+  T pre = 0;
+  for (int w = 0; w < wid; ++w) pre += smem[w];
+  total = smem[0] + smem[1] + smem[2] + smem[3];
+  __syncthreads();
+  return pre + inc - v;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* smem) {
+  T tot;
+  (void)block_excl_scan(v, smem, tot);
+  return tot;
+}
+
+// ---- device-wide exclusive scan: out[0..n] with out[n] = total -----------
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(TPB) void k_scan_sums(const Tin* __restrict__ in, i64 n,
+                                                   Tout* __restrict__ sums) {
+  __shared__ Tout sm[4];
+  const i64 base = (i64)blockIdx.x * SCAN_TILE + (i64)threadIdx.x * SCAN_ITEMS;
+  Tout s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (base + k < n) s += (Tout)in[base + k];
+  Tout tot = block_sum(s, sm);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(TPB) void k_scan_tiles(const Tin* __restrict__ in, i64 n,
+                                                    const Tout* __restrict__ tile_off,
+                                                    Tout* __restrict__ out) {
+  __shared__ Tout sm[4];
+  const i64 base = (i64)blockIdx.x * SCAN_TILE + (i64)threadIdx.x * SCAN_ITEMS;
+  Tout v[SCAN_ITEMS];
+  Tout s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    v[k] = (base + k < n) ? (Tout)in[base + k] : (Tout)0;
+    s += v[k];
+  }
+  Tout tot;
+  Tout pre = block_excl_scan(s, sm, tot) + (tile_off ? tile_off[blockIdx.x] : (Tout)0);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    if (base + k < n) out[base + k] = pre;
+    pre += v[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == TPB - 1) out[n] = pre;
+}
+
+// ---- small helpers ---------------------------------------------------------
+__device__ __forceinline__ i64 upper_bound_i32(const int32_t* a, i64 n, i64 key) {
+  i64 lo = 0, hi = n;
+  while (lo < hi) {
+    const i64 mid = (lo + hi) >> 1;
+    if ((i64)a[mid] <= key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// bits of word w that lie below n
+__device__ __forceinline__ u64 valid_mask(i64 w, i64 n) {
+  const i64 lo = w * 64;
+  if (lo + 64 <= n) return ~0ull;
+  if (lo >= n) return 0ull;
+  return (1ull << (n - lo)) - 1ull;
+}
+
+__device__ __forceinline__ uint32_t hmix(uint32_t h, uint32_t v) {
+  v *= 0xcc9e2d51u;
+  v = (v << 15) | (v >> 17);
+  v *= 0x1b873593u;
+  h ^= v;
+  h = (h << 13) | (h >> 19);
+  return h * 5u + 0xe6546b64u;
+}
+__device__ __forceinline__ uint32_t hfin(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+
+}  // namespace kano

@@ -227,7 +227,7 @@ class DeviceBuild:
     def stage_times(self) -> dict:
         ms = np.zeros(8, dtype=np.float32)
         self._chk(self.lib.kano_stage_times(self.ctx, _ptr(ms)), "kano_stage_times")
-        return dict(classes=float(ms[0]), select=float(ms[1]), allow=float(ms[2]),
+        return dict(classes=float(ms[0]), allow=float(ms[1]), select=float(ms[2]),
                     rows=float(ms[3]), shadow=float(ms[4]), build=float(ms[5]),
                     k_rows=float(ms[6]))
 
