@@ -58,6 +58,18 @@ struct ClassSet {
   DBuf keys_d, table, smin, slot_of, flag, cid, cls, rep, mcnt, mcur, moff, mem, cval;
 };
 
+// One side of the policies (working selector or working allow): terms sorted
+// by class-key slot, the distinct slot sets ("masks") and, after matching,
+// each policy's class list pcls[pstart[p] .. + plen[p]).
+struct SideMatch {
+  i64 nterms = 0;
+  int NM = 0;                     // distinct masks (hash join); 0 with dense
+  bool dense = false;             // too many masks: predicate evaluation
+  DBuf toff, tslot, tval, pmask, moff, mslot;
+  DBuf table, pslot, gcnt, goff, gcur, gmem, pstart, plen, bits, bcnt, boff;
+  i64 T = 0;
+};
+
 struct kano_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -73,20 +85,20 @@ struct kano_ctx {
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_timed = false;
   int ch = 16;
-  i64 heavy_factor = 2;
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
-  i64 UAW = 0, ldC = 0;      // words per AC row
+  SideMatch sm, am;          // selector side, allow side
+  i64 UAW = 0, ldC = 0;      // words per class-level row (column classes)
   i64 nnz_sel = 0, nnz_alc = 0, nnz_alw = 0, heavy_count = 0, wi_total = 0, nflags = 0;
   int max_sel = 0;
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
 
-  DBuf pv, soff, sslot, sval, aoff, aslot, aval;
-  DBuf selT, scnt, soffc, slist, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
+  DBuf pv;
+  DBuf scnt, cost, soffc, scur, slist, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
   DBuf ACT, AC, nca, acnt, alcoff, alc, aloff, alist;
-  DBuf M, Mc, color, colnand, col_and;
+  DBuf M, Mc, color, colnand, col_and, col_or_c, col_nand_c;
   DBuf scan_tmp;
-  DBuf gid, cgroup, R, multi, A1, A2, own, cross;
+  DBuf gid, cgroup, R, multi, A1, A2, own, cross, gmin, gmax;
   DBuf flags, T, loff, L, tp, poff, out;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
@@ -307,41 +319,115 @@ int do_classes(kano_ctx* ctx) {
   return 0;
 }
 
-// ---- allow side --------------------------------------------------------------
+// ---- policy -> class matching (hash join, dense fallback) -------------------
+// Produces sx.pstart / sx.plen: policy p matches the classes
+// sx.gmem[pstart[p] .. pstart[p] + plen[p]) (or sx.boff-based lists in the
+// dense fallback, which needs one extra host sync).
+int match_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
+  const i64 P = ctx->P, U = cs.U;
+  KTRY(dalloc(ctx, sx.pstart, sizeof(i64) * std::max<i64>(1, P)));
+  KTRY(dalloc(ctx, sx.plen, sizeof(int32_t) * std::max<i64>(1, P)));
+  if (P == 0) return 0;
+  if (U == 0) {
+    KCHK(hipMemsetAsync(sx.pstart.p, 0, sizeof(i64) * P, ctx->stream));
+    KCHK(hipMemsetAsync(sx.plen.p, 0, sizeof(int32_t) * P, ctx->stream));
+    return 0;
+  }
+  if (!sx.dense) {
+    const int NM = sx.NM;
+    i64 T = 64;
+    while (T < 2 * U) T <<= 1;
+    sx.T = T;
+    const i64 NT = std::max<i64>(1, (i64)NM * T);
+    KTRY(dalloc(ctx, sx.table, sizeof(int32_t) * NT));
+    KTRY(dalloc(ctx, sx.pslot, sizeof(int32_t) * std::max<i64>(1, (i64)NM * U)));
+    KTRY(dalloc(ctx, sx.gcnt, sizeof(int32_t) * NT));
+    KTRY(dalloc(ctx, sx.gcur, sizeof(int32_t) * NT));
+    KTRY(dalloc(ctx, sx.goff, sizeof(int32_t) * (NT + 1)));
+    KTRY(dalloc(ctx, sx.gmem, sizeof(int32_t) * ((i64)NM * U + U)));
+    if (NM > 0) {
+      KCHK(hipMemsetAsync(sx.table.p, 0xff, sizeof(int32_t) * NT, ctx->stream));
+      KCHK(hipMemsetAsync(sx.gcnt.p, 0, sizeof(int32_t) * NT, ctx->stream));
+      KCHK(hipMemsetAsync(sx.gcur.p, 0, sizeof(int32_t) * NT, ctx->stream));
+      dim3 g2(nblk(U), (unsigned)NM);
+      hipLaunchKernelGGL(k_proj_insert, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(cs.cval), U,
+                         P_<int32_t>(sx.moff), P_<int32_t>(sx.mslot), P_<int32_t>(sx.table), T,
+                         P_<int32_t>(sx.pslot));
+      KLAUNCH();
+      hipLaunchKernelGGL(k_group_count, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(sx.pslot), U, T,
+                         P_<int32_t>(sx.gcnt));
+      KLAUNCH();
+      KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(sx.gcnt), (i64)NM * T,
+                                        P_<int32_t>(sx.goff))));
+      hipLaunchKernelGGL(k_group_fill, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(sx.pslot), U, T,
+                         P_<int32_t>(sx.goff), P_<int32_t>(sx.gcur), P_<int32_t>(sx.gmem));
+      KLAUNCH();
+    }
+    hipLaunchKernelGGL(k_iota, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(sx.gmem) + (i64)NM * U, U);
+    KLAUNCH();
+    hipLaunchKernelGGL(k_pol_match, dim3(nblk(P)), dim3(TPB), 0, ctx->stream, P, P_<i64>(sx.toff),
+                       P_<int32_t>(sx.tval), P_<int32_t>(sx.pmask), P_<int32_t>(sx.moff),
+                       P_<int32_t>(sx.mslot), P_<int32_t>(cs.cval), U, P_<int32_t>(sx.table), T,
+                       P_<int32_t>(sx.goff), (i64)NM * U, P_<i64>(sx.pstart),
+                       P_<int32_t>(sx.plen));
+    KLAUNCH();
+    return 0;
+  }
+  // dense fallback: evaluate every (policy, class) predicate
+  const i64 UW = (U + 63) / 64, ld = std::max<i64>(2, (UW + 1) & ~(i64)1);
+  KTRY(dalloc(ctx, sx.bits, sizeof(u64) * P * ld));
+  KTRY(dalloc(ctx, sx.bcnt, sizeof(int32_t) * P));
+  KTRY(dalloc(ctx, sx.boff, sizeof(i64) * (P + 1)));
+  hipLaunchKernelGGL(k_class_eval, dim3(nblk(U), (unsigned)ctx->PB), dim3(TPB), 0, ctx->stream,
+                     P_<int32_t>(cs.cval), U, P, P_<i64>(sx.toff), P_<int32_t>(sx.tslot),
+                     P_<int32_t>(sx.tval), (u64*)nullptr, P_<u64>(sx.bits), ld);
+  KLAUNCH();
+  hipLaunchKernelGGL(k_popc_rows, dim3((unsigned)P), dim3(TPB), 0, ctx->stream, P_<u64>(sx.bits),
+                     ld, UW, P_<int32_t>(sx.plen));
+  KLAUNCH();
+  KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(sx.plen), P, P_<i64>(sx.boff))));
+  i64 nnz = 0;
+  KCHK(hipMemcpyAsync(&nnz, P_<i64>(sx.boff) + P, 8, hipMemcpyDeviceToHost, ctx->stream));
+  KTRY(sync(ctx));
+  KTRY(dalloc(ctx, sx.gmem, sizeof(int32_t) * std::max<i64>(1, nnz)));
+  hipLaunchKernelGGL(k_bits_to_lists, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                     P_<u64>(sx.bits), ld, UW, P_<i64>(sx.boff), P_<int32_t>(sx.gmem));
+  KLAUNCH();
+  hipLaunchKernelGGL(k_offsets_to_start, dim3(nblk(P)), dim3(TPB), 0, ctx->stream,
+                     P_<i64>(sx.boff), P, P_<i64>(sx.pstart));
+  KLAUNCH();
+  return 0;
+}
+
+// allow side: allowed classes / pods per policy
 int do_allow(kano_ctx* ctx) {
-  const i64 P = ctx->P, PB = ctx->PB, Ua = ctx->cc.U;
+  const i64 P = ctx->P, Ua = ctx->cc.U;
   ctx->UAW = (Ua + 63) / 64;
   ctx->ldC = std::max<i64>(2, (ctx->UAW + 1) & ~(i64)1);
-  KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, PB * Ua)));
-  KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
+  KTRY(match_side(ctx, ctx->am, ctx->cc));
   KTRY(dalloc(ctx, ctx->nca, sizeof(int32_t) * std::max<i64>(1, P)));
   KTRY(dalloc(ctx, ctx->acnt, sizeof(int32_t) * std::max<i64>(1, P)));
   KTRY(dalloc(ctx, ctx->alcoff, sizeof(i64) * (P + 1)));
   KTRY(dalloc(ctx, ctx->aloff, sizeof(i64) * (P + 1)));
-  if (P > 0 && Ua > 0) {
-    hipLaunchKernelGGL(k_class_eval, dim3(nblk(Ua), (unsigned)PB), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->cc.cval), Ua, P, P_<i64>(ctx->aoff),
-                       P_<int32_t>(ctx->aslot), P_<int32_t>(ctx->aval), P_<u64>(ctx->ACT),
-                       P_<u64>(ctx->AC), ctx->ldC);
+  if (P > 0) {
+    hipLaunchKernelGGL(k_pol_allow_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                       P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
+                       P_<int32_t>(ctx->am.gmem), P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca),
+                       P_<int32_t>(ctx->acnt));
     KLAUNCH();
-    hipLaunchKernelGGL(k_pol_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->AC), ctx->ldC, ctx->UAW, P_<int32_t>(ctx->cc.moff),
-                       P_<int32_t>(ctx->nca), P_<int32_t>(ctx->acnt));
-    KLAUNCH();
-  } else if (P > 0) {
-    KCHK(hipMemsetAsync(ctx->nca.p, 0, sizeof(int32_t) * P, ctx->stream));
-    KCHK(hipMemsetAsync(ctx->acnt.p, 0, sizeof(int32_t) * P, ctx->stream));
   }
   KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->nca), P, P_<i64>(ctx->alcoff))));
   KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->acnt), P, P_<i64>(ctx->aloff))));
   return 0;
 }
 
-// ---- select side and the per-class plan ------------------------------------
+// select side: |S(c)|, rebuild cost, the per-class plan
 int do_select(kano_ctx* ctx, int path) {
-  const i64 U = ctx->rc.U, P = ctx->P, PB = ctx->PB;
-  KTRY(dalloc(ctx, ctx->selT, sizeof(u64) * std::max<i64>(1, PB * U)));
+  const i64 U = ctx->rc.U, P = ctx->P;
+  KTRY(match_side(ctx, ctx->sm, ctx->rc));
   KTRY(dalloc(ctx, ctx->scnt, sizeof(int32_t) * std::max<i64>(1, U)));
+  KTRY(dalloc(ctx, ctx->cost, sizeof(u64) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, ctx->wicnt, sizeof(int32_t) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, ctx->hflag, sizeof(int32_t) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, ctx->sq, sizeof(i64) * std::max<i64>(1, U)));
@@ -351,25 +437,26 @@ int do_select(kano_ctx* ctx, int path) {
   KTRY(dalloc(ctx, ctx->hoff, sizeof(int32_t) * (U + 1)));
   KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (U + 1)));
   KCHK(hipMemsetAsync(ctx->maxs.p, 0, sizeof(int32_t), ctx->stream));
-  if (PB > 0 && U > 0) {
-    hipLaunchKernelGGL(k_class_eval, dim3(nblk(U), (unsigned)PB), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->rc.cval), U, P, P_<i64>(ctx->soff),
-                       P_<int32_t>(ctx->sslot), P_<int32_t>(ctx->sval), P_<u64>(ctx->selT),
-                       (u64*)nullptr, (i64)0);
+  if (U > 0) {
+    KCHK(hipMemsetAsync(ctx->scnt.p, 0, sizeof(int32_t) * U, ctx->stream));
+    KCHK(hipMemsetAsync(ctx->cost.p, 0, sizeof(u64) * U, ctx->stream));
+  }
+  if (P > 0 && U > 0) {
+    hipLaunchKernelGGL(k_sel_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                       P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                       P_<int32_t>(ctx->sm.gmem), P_<int32_t>(ctx->acnt), P_<int32_t>(ctx->scnt),
+                       P_<unsigned long long>(ctx->cost));
     KLAUNCH();
   }
   if (U > 0) {
     ClassPlan a;
-    a.selT = P_<u64>(ctx->selT);
     a.U = U;
-    a.PB = PB;
+    a.scnt = P_<int32_t>(ctx->scnt);
+    a.cost = P_<unsigned long long>(ctx->cost);
     a.mcnt = P_<int32_t>(ctx->rc.mcnt);
-    a.acnt = P_<int32_t>(ctx->acnt);
     a.W = ctx->W;
     a.ch = ctx->ch;
     a.force = path == KANO_PATH_MFMA ? 2 : 0;
-    a.heavy_factor = ctx->heavy_factor;
-    a.scnt = P_<int32_t>(ctx->scnt);
     a.wicnt = P_<int32_t>(ctx->wicnt);
     a.hflag = P_<int32_t>(ctx->hflag);
     a.sq = P_<i64>(ctx->sq);
@@ -407,24 +494,39 @@ int read_sizes(kano_ctx* ctx) {
   return 0;
 }
 
+// lists: S(c) ascending, allowed classes + bits + pods per policy, heavy list
 int do_fill(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, P = ctx->P;
   KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
+  KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
   KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
   KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, ctx->heavy_count)));
+  KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
+  if (P > 0) KCHK(hipMemsetAsync(ctx->AC.p, 0, sizeof(u64) * P * ctx->ldC, ctx->stream));
   if (U > 0) {
-    hipLaunchKernelGGL(k_sel_fill, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, P_<u64>(ctx->selT), U,
-                       ctx->PB, P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist));
-    KLAUNCH();
+    KCHK(hipMemsetAsync(ctx->scur.p, 0, sizeof(int32_t) * U, ctx->stream));
+    if (P > 0) {
+      hipLaunchKernelGGL(k_sel_place, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                         P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                         P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
+                         P_<int32_t>(ctx->slist));
+      KLAUNCH();
+      const size_t lds = std::max<size_t>(sizeof(int32_t) * RANK_MAX,
+                                          sizeof(u64) * (size_t)((P + 63) / 64));
+      hipLaunchKernelGGL(k_sort_lists, dim3((unsigned)U), dim3(TPB), lds, ctx->stream,
+                         P_<i64>(ctx->soffc), P, P_<int32_t>(ctx->slist));
+      KLAUNCH();
+    }
     hipLaunchKernelGGL(k_flag_list, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), U, P_<int32_t>(ctx->hlist));
     KLAUNCH();
   }
   if (P > 0 && ctx->cc.U > 0) {
-    hipLaunchKernelGGL(k_pol_classes, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->AC), ctx->ldC, ctx->UAW, P_<i64>(ctx->alcoff),
-                       P_<int32_t>(ctx->alc));
+    hipLaunchKernelGGL(k_pol_allow_fill, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                       P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
+                       P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
+                       P_<u64>(ctx->AC), ctx->ldC);
     KLAUNCH();
     hipLaunchKernelGGL(k_pol_pods, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                        P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
@@ -434,61 +536,106 @@ int do_fill(kano_ctx* ctx) {
   return 0;
 }
 
-// heavy rows: Mc over column classes, then expanded to the first member's row
-int do_heavy(kano_ctx* ctx, int path) {
-  const i64 H = ctx->heavy_count;
+// the compressed matrix Mc (row classes x column classes): light classes by
+// scatter, heavy classes by bitwise OR or the int8 MFMA contraction; then the
+// column checks at class level, expanded to pods
+int do_mc(kano_ctx* ctx, int path) {
+  const i64 U = ctx->rc.U, H = ctx->heavy_count, ldMc = ctx->ldC;
   ctx->heavy_path = 0;
-  if (H == 0 || rows_local(ctx) == 0) return 0;
-  const i64 ldMc = ctx->ldC;
-  KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * H * ldMc));
-  bool mfma = path == KANO_PATH_MFMA;
-  if (path == KANO_PATH_AUTO) {
-    // dense when the heavy rows' policy lists cover a large share of all
-    // policies: the MFMA walks every policy, the OR only S(c)
-    const double avg_s = (double)ctx->nnz_sel / std::max<i64>(1, ctx->rc.U);
-    mfma = H >= 32 && ctx->cc.U >= 64 && avg_s * 16.0 >= (double)ctx->P;
-  }
-  ctx->heavy_path = mfma ? 2 : 1;
-  if (mfma) {
-    for (i64 h0 = 0; h0 < H; h0 += HT_ROWS) {
-      const int hh = (int)std::min<i64>(HT_ROWS, H - h0);
-      const int32_t* hl = P_<int32_t>(ctx->hlist) + h0;
-      uint32_t* out = reinterpret_cast<uint32_t*>(P_<u64>(ctx->Mc) + h0 * ldMc);
-      dim3 grid(nblk(2 * ldMc, TPB / 64));
-      if (hh <= 32)
-        hipLaunchKernelGGL(k_heavy_mc_mfma<1>, grid, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->selT),
-                           ctx->rc.U, hl, hh, P_<u64>(ctx->ACT), ctx->cc.U, ctx->PB, out, ldMc);
-      else if (hh <= 64)
-        hipLaunchKernelGGL(k_heavy_mc_mfma<2>, grid, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->selT),
-                           ctx->rc.U, hl, hh, P_<u64>(ctx->ACT), ctx->cc.U, ctx->PB, out, ldMc);
-      else
-        hipLaunchKernelGGL(k_heavy_mc_mfma<4>, grid, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->selT),
-                           ctx->rc.U, hl, hh, P_<u64>(ctx->ACT), ctx->cc.U, ctx->PB, out, ldMc);
+  KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
+  KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
+  KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
+  KCHK(hipMemsetAsync(ctx->col_or_c.p, 0, sizeof(u64) * ldMc, ctx->stream));
+  KCHK(hipMemsetAsync(ctx->col_nand_c.p, 0, sizeof(u64) * ldMc, ctx->stream));
+  if (U == 0) return 0;
+  KCHK(hipMemsetAsync(ctx->Mc.p, 0, sizeof(u64) * U * ldMc, ctx->stream));
+  hipLaunchKernelGGL(k_mc_scatter, dim3((unsigned)U), dim3(TPB), 0, ctx->stream,
+                     P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
+                     P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
+                     H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr, P_<u64>(ctx->Mc),
+                     ldMc);
+  KLAUNCH();
+  if (H > 0) {
+    bool mfma = path == KANO_PATH_MFMA;
+    if (path == KANO_PATH_AUTO) {
+      // the MFMA walks every policy for every heavy row, the OR only S(c):
+      // dense when the average |S(c)| is a large share of P
+      const double avg_s = (double)ctx->nnz_sel / std::max<i64>(1, U);
+      mfma = H >= 32 && ctx->cc.U >= 64 && avg_s * 16.0 >= (double)ctx->P;
+    }
+    ctx->heavy_path = mfma ? 2 : 1;
+    if (mfma) {
+      const i64 Ua = ctx->cc.U;
+      KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, ctx->PB * Ua)));
+      KCHK(hipMemsetAsync(ctx->ACT.p, 0, sizeof(u64) * ctx->PB * Ua, ctx->stream));
+      hipLaunchKernelGGL(k_classbits, dim3((unsigned)ctx->P), dim3(TPB), 0, ctx->stream,
+                         P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
+                         P_<int32_t>(ctx->am.gmem), Ua, P_<u64>(ctx->ACT));
+      KLAUNCH();
+      // class-major selector bits of the heavy rows: selT[pb][c]
+      KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, ctx->PB * U)));
+      KCHK(hipMemsetAsync(ctx->scratch_words.p, 0, sizeof(u64) * ctx->PB * U, ctx->stream));
+      hipLaunchKernelGGL(k_classbits, dim3((unsigned)ctx->P), dim3(TPB), 0, ctx->stream,
+                         P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                         P_<int32_t>(ctx->sm.gmem), U, P_<u64>(ctx->scratch_words));
+      KLAUNCH();
+      for (i64 h0 = 0; h0 < H; h0 += HT_ROWS) {
+        const int hh = (int)std::min<i64>(HT_ROWS, H - h0);
+        const int32_t* hl = P_<int32_t>(ctx->hlist) + h0;
+        uint32_t* out = reinterpret_cast<uint32_t*>(P_<u64>(ctx->Mc));
+        dim3 grid(nblk(2 * ldMc, TPB / 64));
+        const u64* selT = P_<u64>(ctx->scratch_words);
+        if (hh <= 32)
+          hipLaunchKernelGGL(k_heavy_mc_mfma<1>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        else if (hh <= 64)
+          hipLaunchKernelGGL(k_heavy_mc_mfma<2>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        else
+          hipLaunchKernelGGL(k_heavy_mc_mfma<4>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        KLAUNCH();
+      }
+    } else {
+      hipLaunchKernelGGL(k_heavy_mc_or, dim3((unsigned)H, nblk(ldMc)), dim3(TPB), 0, ctx->stream,
+                         P_<int32_t>(ctx->hlist), P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
+                         P_<u64>(ctx->AC), ctx->ldC, ctx->UAW, P_<u64>(ctx->Mc), ldMc);
       KLAUNCH();
     }
-  } else {
-    hipLaunchKernelGGL(k_heavy_mc_or, dim3((unsigned)H, nblk(ldMc)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->hlist), P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
-                       P_<u64>(ctx->AC), ctx->ldC, ctx->UAW, P_<u64>(ctx->Mc), ldMc);
+  }
+  if (rows_local(ctx) > 0) {
+    hipLaunchKernelGGL(k_mc_cols, dim3(nblk(ctx->UAW, 64), nblk(U, 128)), dim3(TPB), 0,
+                       ctx->stream, P_<u64>(ctx->Mc), ldMc, ctx->UAW, ctx->cc.U, U,
+                       P_<int32_t>(ctx->rc.mcnt), P_<u64>(ctx->col_or_c), P_<u64>(ctx->col_nand_c));
     KLAUNCH();
   }
-  hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ctx->ldM * 64), (unsigned)H), dim3(TPB), 0,
-                     ctx->stream, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ldMc,
-                     P_<int32_t>(ctx->cc.cls), ctx->n, P_<int32_t>(ctx->rc.moff),
-                     P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ctx->ldM, ctx->r0);
-  KLAUNCH();
   return 0;
 }
 
+// heavy rows expanded from Mc into the first member's row; then the rows
 int do_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
-  KCHK(hipMemsetAsync(ctx->color.p, 0, sizeof(u64) * ldM, ctx->stream));
-  KCHK(hipMemsetAsync(ctx->colnand.p, 0, sizeof(u64) * ldM, ctx->stream));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_cols_expand, dim3(nblk(ldM * 64)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->col_or_c), P_<u64>(ctx->col_nand_c), P_<int32_t>(ctx->cc.cls),
+                       n, ldM, P_<u64>(ctx->color), P_<u64>(ctx->colnand));
+    KLAUNCH();
+  } else {
+    KCHK(hipMemsetAsync(ctx->color.p, 0, sizeof(u64) * ldM, ctx->stream));
+    KCHK(hipMemsetAsync(ctx->colnand.p, 0, sizeof(u64) * ldM, ctx->stream));
+  }
   if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
+  if (ctx->heavy_count > 0) {
+    hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), (unsigned)ctx->heavy_count), dim3(TPB),
+                       0, ctx->stream, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ctx->ldC,
+                       P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
+                       P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
+    KLAUNCH();
+  }
   const int cww = (int)std::min<i64>(ldM, MAX_CWW);
   const unsigned ncc = (unsigned)((ldM + cww - 1) / cww);
-  RowsArgs a;
+  RowsArgs a{};
   a.wioff = P_<int32_t>(ctx->wioff);
   a.U = U;
   a.soffc = P_<i64>(ctx->soffc);
@@ -506,8 +653,8 @@ int do_rows(kano_ctx* ctx) {
   a.W = W;
   a.ch = ctx->ch;
   a.cww = cww;
-  a.color = P_<u64>(ctx->color);
-  a.colnand = P_<u64>(ctx->colnand);
+  a.color = nullptr;  // column checks come from Mc
+  a.colnand = nullptr;
   KCHK(hipEventRecord(ctx->ev[7], ctx->stream));
   hipLaunchKernelGGL(k_rows, dim3((unsigned)ctx->wi_total, ncc), dim3(TPB), sizeof(u64) * cww,
                      ctx->stream, a);
@@ -586,12 +733,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
-  KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldM));
-  KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldM));
-  KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldM));
-  KTRY(dalloc(ctx, ctx->own, sizeof(u64) * ldM));
-  for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2, &ctx->own, &ctx->cross})
-    KCHK(hipMemsetAsync(b->p, 0, sizeof(u64) * ldM, ctx->stream));
+  KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
   int32_t G = 0;
   for (i64 i = 0; i < n; ++i) {
@@ -599,13 +741,52 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid) {
     G = std::max(G, gid[i] + 1);
   }
   KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-  const int32_t* moff = P_<int32_t>(ctx->rc.moff);
-  const int32_t* mem = P_<int32_t>(ctx->rc.mem);
-  i64 nclass = ctx->rc.U;
-  if (ctx->rows_dirty) {
-    KTRY(ensure_identity(ctx, &moff, &mem));
-    nclass = rows_local(ctx);
+
+  if (!ctx->rows_dirty) {
+    // class level: rows of a row class are equal, columns of a column class
+    // are equal; everything runs on Mc (U_r x U_a bits)
+    const i64 U = ctx->rc.U, ldC = ctx->ldC, UAW = ctx->UAW;
+    KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->R, sizeof(u64) * (i64)G * ldC));
+    KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
+    KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
+    KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
+    KCHK(hipMemsetAsync(ctx->gmin.p, 0x7f, sizeof(int32_t) * U, ctx->stream));
+    KCHK(hipMemsetAsync(ctx->gmax.p, 0xff, sizeof(int32_t) * U, ctx->stream));
+    KCHK(hipMemsetAsync(ctx->R.p, 0, sizeof(u64) * (i64)G * ldC, ctx->stream));
+    for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2})
+      KCHK(hipMemsetAsync(b->p, 0, sizeof(u64) * ldC, ctx->stream));
+    const i64 rl = rows_local(ctx);
+    hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->gid), P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
+                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax));
+    KLAUNCH();
+    hipLaunchKernelGGL(k_cross_mc, dim3((unsigned)U), dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc),
+                       ldC, UAW, P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
+                       P_<int32_t>(ctx->gmax), P_<u64>(ctx->R), P_<u64>(ctx->multi));
+    KLAUNCH();
+    hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
+    KLAUNCH();
+    hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->gid), P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R), ldC,
+                       P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
+                       P_<u64>(ctx->cross));
+    KLAUNCH();
+    return 0;
   }
+
+  // M edited: every row is its own class, rows read from M
+  KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldM));
+  KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldM));
+  KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldM));
+  KTRY(dalloc(ctx, ctx->own, sizeof(u64) * ldM));
+  for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2, &ctx->own})
+    KCHK(hipMemsetAsync(b->p, 0, sizeof(u64) * ldM, ctx->stream));
+  const int32_t *moff = nullptr, *mem = nullptr;
+  KTRY(ensure_identity(ctx, &moff, &mem));
+  const i64 nclass = rows_local(ctx);
   KTRY(dalloc(ctx, ctx->cgroup, sizeof(int32_t) * std::max<i64>(1, nclass)));
   hipLaunchKernelGGL(k_cross_classgroup, dim3(nblk(nclass)), dim3(TPB), 0, ctx->stream,
                      P_<int32_t>(ctx->gid), moff, mem, nclass, P_<int32_t>(ctx->cgroup));
@@ -671,17 +852,22 @@ void kano_destroy(kano_ctx* ctx) {
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
     for (DBuf* x : b) dfree(*x);
   }
-  DBuf* bufs[] = {&ctx->pv,      &ctx->soff,    &ctx->sslot,    &ctx->sval,   &ctx->aoff,
-                  &ctx->aslot,   &ctx->aval,    &ctx->selT,     &ctx->scnt,   &ctx->soffc,
-                  &ctx->slist,   &ctx->maxs,    &ctx->wicnt,    &ctx->wioff,  &ctx->hflag,
-                  &ctx->hoff,    &ctx->hlist,   &ctx->sq,       &ctx->pfoff,  &ctx->ACT,
-                  &ctx->AC,      &ctx->nca,     &ctx->acnt,     &ctx->alcoff, &ctx->alc,
-                  &ctx->aloff,   &ctx->alist,   &ctx->M,        &ctx->Mc,     &ctx->color,
-                  &ctx->colnand, &ctx->col_and, &ctx->scan_tmp, &ctx->gid,    &ctx->cgroup,
-                  &ctx->R,       &ctx->multi,   &ctx->A1,       &ctx->A2,     &ctx->own,
-                  &ctx->cross,   &ctx->flags,   &ctx->T,        &ctx->loff,   &ctx->L,
-                  &ctx->tp,      &ctx->poff,    &ctx->out,      &ctx->scratch_words,
-                  &ctx->ident};
+  for (SideMatch* sx : {&ctx->sm, &ctx->am}) {
+    DBuf* b[] = {&sx->toff,  &sx->tslot, &sx->tval, &sx->pmask,  &sx->moff, &sx->mslot,
+                 &sx->table, &sx->pslot, &sx->gcnt, &sx->goff,   &sx->gcur, &sx->gmem,
+                 &sx->pstart, &sx->plen, &sx->bits, &sx->bcnt,   &sx->boff};
+    for (DBuf* x : b) dfree(*x);
+  }
+  DBuf* bufs[] = {&ctx->pv,     &ctx->scnt,    &ctx->cost,    &ctx->soffc,     &ctx->scur,
+                  &ctx->slist,  &ctx->maxs,    &ctx->wicnt,   &ctx->wioff,     &ctx->hflag,
+                  &ctx->hoff,   &ctx->hlist,   &ctx->sq,      &ctx->pfoff,     &ctx->ACT,
+                  &ctx->AC,     &ctx->nca,     &ctx->acnt,    &ctx->alcoff,    &ctx->alc,
+                  &ctx->aloff,  &ctx->alist,   &ctx->M,       &ctx->Mc,        &ctx->color,
+                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp,
+                  &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
+                  &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
+                  &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
+                  &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -730,10 +916,15 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   return sync(ctx);
 }
 
-// The columns referenced by one side's terms become that side's class keys;
-// term columns are remapped to slots of the class value table.
-static int side_keys(kano_ctx* ctx, i64 nt, const int32_t* col, ClassSet& cs,
-                     std::vector<int32_t>& slots) {
+// One side of the policies: the columns its terms reference become the class
+// keys of that side (slots); each policy's terms are sorted by slot and
+// deduplicated (two different values for one slot match nothing); the
+// distinct slot sets become the masks of the hash join.
+static constexpr int MAX_MASKS = 64;
+
+static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t* col,
+                        const int32_t* val, ClassSet& cs, SideMatch& sx) {
+  const i64 nt = off[P];
   std::vector<int32_t> slot(ctx->ncols, -1);
   for (i64 t = 0; t < nt; ++t) {
     if (col[t] < 0 || col[t] >= ctx->ncols) return fail(ctx, -EINVAL, "term column out of range");
@@ -745,9 +936,103 @@ static int side_keys(kano_ctx* ctx, i64 nt, const int32_t* col, ClassSet& cs,
       slot[c] = (int32_t)cs.keys.size();
       cs.keys.push_back(c);
     }
-  slots.resize(std::max<i64>(1, nt));
-  for (i64 t = 0; t < nt; ++t) slots[t] = slot[col[t]];
-  return 0;
+  std::vector<i64> toff(P + 1, 0);
+  std::vector<int32_t> tslot, tval, pmask(std::max<i64>(1, P), -1), moff(1, 0), mslot;
+  std::vector<std::vector<int32_t>> masks;
+  std::vector<std::pair<int32_t, int32_t>> terms;
+  tslot.reserve(nt);
+  tval.reserve(nt);
+  for (i64 p = 0; p < P; ++p) {
+    terms.clear();
+    for (i64 t = off[p]; t < off[p + 1]; ++t) terms.emplace_back(slot[col[t]], val[t]);
+    std::sort(terms.begin(), terms.end());
+    bool contradict = false;
+    std::vector<int32_t> sl;
+    for (size_t k = 0; k < terms.size(); ++k) {
+      if (k > 0 && terms[k].first == terms[k - 1].first) {
+        if (terms[k].second != terms[k - 1].second) contradict = true;
+        continue;
+      }
+      sl.push_back(terms[k].first);
+      tslot.push_back(terms[k].first);
+      tval.push_back(terms[k].second);
+    }
+    toff[p + 1] = (i64)tslot.size();
+    if (contradict) {
+      pmask[p] = -1;
+    } else if (sl.empty()) {
+      pmask[p] = -2;
+    } else {
+      int id = -1;
+      for (size_t m = 0; m < masks.size(); ++m)
+        if (masks[m] == sl) { id = (int)m; break; }
+      if (id < 0) {
+        id = (int)masks.size();
+        masks.push_back(sl);
+      }
+      pmask[p] = id;
+    }
+  }
+  sx.nterms = (i64)tslot.size();
+  sx.dense = masks.size() > (size_t)MAX_MASKS;
+  sx.NM = sx.dense ? 0 : (int)masks.size();
+  if (sx.dense) {
+    // dense evaluation ignores masks; contradictory policies keep both terms
+    // and fail the predicate naturally
+    for (i64 p = 0; p < P; ++p)
+      if (pmask[p] == -1) {
+        tslot.push_back(0);
+        tval.push_back(-4);  // never equals a value id
+      }
+    // rebuild offsets with the sentinel term appended per contradictory policy
+    std::vector<i64> o2(P + 1, 0);
+    std::vector<int32_t> s2, v2;
+    i64 extra = (i64)toff[P];
+    for (i64 p = 0; p < P; ++p) {
+      for (i64 t = toff[p]; t < toff[p + 1]; ++t) {
+        s2.push_back(tslot[t]);
+        v2.push_back(tval[t]);
+      }
+      if (pmask[p] == -1) {
+        s2.push_back(tslot[extra]);
+        v2.push_back(tval[extra]);
+        ++extra;
+      }
+      o2[p + 1] = (i64)s2.size();
+    }
+    toff.swap(o2);
+    tslot.swap(s2);
+    tval.swap(v2);
+    sx.nterms = (i64)tslot.size();
+  } else {
+    for (auto& m : masks) {
+      mslot.insert(mslot.end(), m.begin(), m.end());
+      moff.push_back((int32_t)mslot.size());
+    }
+  }
+  KTRY(dalloc(ctx, sx.toff, sizeof(i64) * (P + 1)));
+  KTRY(dalloc(ctx, sx.tslot, sizeof(int32_t) * std::max<size_t>(1, tslot.size())));
+  KTRY(dalloc(ctx, sx.tval, sizeof(int32_t) * std::max<size_t>(1, tval.size())));
+  KTRY(dalloc(ctx, sx.pmask, sizeof(int32_t) * std::max<i64>(1, P)));
+  KTRY(dalloc(ctx, sx.moff, sizeof(int32_t) * moff.size()));
+  KTRY(dalloc(ctx, sx.mslot, sizeof(int32_t) * std::max<size_t>(1, mslot.size())));
+  KCHK(hipMemcpyAsync(sx.toff.p, toff.data(), sizeof(i64) * (P + 1), hipMemcpyHostToDevice,
+                      ctx->stream));
+  if (!tslot.empty()) {
+    KCHK(hipMemcpyAsync(sx.tslot.p, tslot.data(), sizeof(int32_t) * tslot.size(),
+                        hipMemcpyHostToDevice, ctx->stream));
+    KCHK(hipMemcpyAsync(sx.tval.p, tval.data(), sizeof(int32_t) * tval.size(),
+                        hipMemcpyHostToDevice, ctx->stream));
+  }
+  if (P > 0)
+    KCHK(hipMemcpyAsync(sx.pmask.p, pmask.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice,
+                        ctx->stream));
+  KCHK(hipMemcpyAsync(sx.moff.p, moff.data(), sizeof(int32_t) * moff.size(), hipMemcpyHostToDevice,
+                      ctx->stream));
+  if (!mslot.empty())
+    KCHK(hipMemcpyAsync(sx.mslot.p, mslot.data(), sizeof(int32_t) * mslot.size(),
+                        hipMemcpyHostToDevice, ctx->stream));
+  return sync(ctx);  // host vectors are temporaries
 }
 
 int kano_set_policies(kano_ctx* ctx, int64_t P, const int64_t* sel_off, const int32_t* sel_col,
@@ -757,37 +1042,13 @@ int kano_set_policies(kano_ctx* ctx, int64_t P, const int64_t* sel_off, const in
   if (!ctx->have_pods) return fail(ctx, -EINVAL, "kano_set_policies before kano_set_pods");
   if (P < 0 || !sel_off || !alw_off) return fail(ctx, -EINVAL, "kano_set_policies: bad arguments");
   KCHK(hipSetDevice(ctx->device));
-  const i64 ns = sel_off[P], na = alw_off[P];
-  std::vector<int32_t> sslot, aslot;
-  KTRY(side_keys(ctx, ns, sel_col, ctx->rc, sslot));
-  KTRY(side_keys(ctx, na, alw_col, ctx->cc, aslot));
   ctx->P = P;
   ctx->PB = (P + 63) / 64;
-  KTRY(dalloc(ctx, ctx->soff, sizeof(i64) * (P + 1)));
-  KTRY(dalloc(ctx, ctx->sslot, sizeof(int32_t) * std::max<i64>(1, ns)));
-  KTRY(dalloc(ctx, ctx->sval, sizeof(int32_t) * std::max<i64>(1, ns)));
-  KTRY(dalloc(ctx, ctx->aoff, sizeof(i64) * (P + 1)));
-  KTRY(dalloc(ctx, ctx->aslot, sizeof(int32_t) * std::max<i64>(1, na)));
-  KTRY(dalloc(ctx, ctx->aval, sizeof(int32_t) * std::max<i64>(1, na)));
-  KCHK(hipMemcpyAsync(ctx->soff.p, sel_off, sizeof(i64) * (P + 1), hipMemcpyHostToDevice,
-                      ctx->stream));
-  KCHK(hipMemcpyAsync(ctx->aoff.p, alw_off, sizeof(i64) * (P + 1), hipMemcpyHostToDevice,
-                      ctx->stream));
-  if (ns > 0) {
-    KCHK(hipMemcpyAsync(ctx->sslot.p, sslot.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice,
-                        ctx->stream));
-    KCHK(hipMemcpyAsync(ctx->sval.p, sel_val, sizeof(int32_t) * ns, hipMemcpyHostToDevice,
-                        ctx->stream));
-  }
-  if (na > 0) {
-    KCHK(hipMemcpyAsync(ctx->aslot.p, aslot.data(), sizeof(int32_t) * na, hipMemcpyHostToDevice,
-                        ctx->stream));
-    KCHK(hipMemcpyAsync(ctx->aval.p, alw_val, sizeof(int32_t) * na, hipMemcpyHostToDevice,
-                        ctx->stream));
-  }
+  KTRY(prepare_side(ctx, P, sel_off, sel_col, sel_val, ctx->rc, ctx->sm));
+  KTRY(prepare_side(ctx, P, alw_off, alw_col, alw_val, ctx->cc, ctx->am));
   ctx->have_pols = true;
   ctx->built = false;
-  return sync(ctx);  // the slot vectors are temporaries
+  return 0;
 }
 
 int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end) {
@@ -825,7 +1086,7 @@ int kano_build(kano_ctx* ctx, int path) {
   KTRY(read_sizes(ctx));
   KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   KTRY(do_fill(ctx));
-  KTRY(do_heavy(ctx, path));
+  KTRY(do_mc(ctx, path));
   KTRY(do_rows(ctx));
   KCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->cols_valid = true;
@@ -982,8 +1243,8 @@ int kano_get_policy_sets(kano_ctx* ctx, int64_t p, uint64_t* sel, uint64_t* allo
   KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * 2 * W));
   u64* s = P_<u64>(ctx->scratch_words);
   if (sel) {
-    hipLaunchKernelGGL(k_sel_row, dim3(nblk(n)), dim3(TPB), 0, ctx->stream, P_<u64>(ctx->selT),
-                       ctx->rc.U, P_<int32_t>(ctx->rc.cls), n, (i64)p, s);
+    hipLaunchKernelGGL(k_sel_row, dim3(nblk(n)), dim3(TPB), 0, ctx->stream, P_<i64>(ctx->soffc),
+                       P_<int32_t>(ctx->slist), P_<int32_t>(ctx->rc.cls), n, (i64)p, s);
     KLAUNCH();
     KCHK(hipMemcpyAsync(sel, s, sizeof(u64) * W, hipMemcpyDeviceToHost, ctx->stream));
   }

@@ -197,64 +197,450 @@ __global__ __launch_bounds__(TPB) void k_pol_pods(const i64* __restrict__ alcoff
 }
 
 // ===========================================================================
+// Policy -> class matching by hash join.  The terms of a policy fix the values
+// of a set of class-key slots (its "mask"); a class matches iff its
+// projection onto the mask equals the policy's values.  Classes are grouped
+// by projection, one open-addressing table per distinct mask; a policy
+// probes its mask's table once and gets its whole class list (a group).
+// O(P + U * masks) instead of the O(P * U) predicate evaluation.
+// ===========================================================================
+__device__ __forceinline__ uint32_t proj_hash(const int32_t* __restrict__ cval, i64 U, i64 c,
+                                              const int32_t* __restrict__ slots, int ns) {
+  uint32_t h = 0x2545f491u;
+  for (int k = 0; k < ns; ++k) h = hmix(h, (uint32_t)cval[(i64)slots[k] * U + c]);
+  return hfin(h);
+}
+
+// grid (classes, masks): group id of class c under mask m = its table slot
+__global__ __launch_bounds__(TPB) void k_proj_insert(const int32_t* __restrict__ cval, i64 U,
+                                                     const int32_t* __restrict__ moff,
+                                                     const int32_t* __restrict__ mslot,
+                                                     int32_t* table, i64 T,
+                                                     int32_t* __restrict__ pslot) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  const int m = blockIdx.y;
+  if (c >= U) return;
+  const int32_t* sl = mslot + moff[m];
+  const int ns = moff[m + 1] - moff[m];
+  int32_t* tab = table + (i64)m * T;
+  uint32_t s = proj_hash(cval, U, c, sl, ns) & (uint32_t)(T - 1);
+  for (;;) {
+    int32_t cur = __hip_atomic_load(&tab[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur < 0) {
+      const int32_t prev = atomicCAS(&tab[s], -1, (int32_t)c);
+      if (prev < 0) { pslot[(i64)m * U + c] = (int32_t)s; return; }
+      cur = prev;
+    }
+    bool eq = true;
+    for (int k = 0; k < ns; ++k) {
+      const int32_t* col = cval + (i64)sl[k] * U;
+      if (col[cur] != col[c]) { eq = false; break; }
+    }
+    if (eq) { pslot[(i64)m * U + c] = (int32_t)s; return; }
+    s = (s + 1) & (uint32_t)(T - 1);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_group_count(const int32_t* __restrict__ pslot, i64 U,
+                                                     i64 T, int32_t* gcnt) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  const int m = blockIdx.y;
+  if (c < U) atomicAdd(&gcnt[(i64)m * T + pslot[(i64)m * U + c]], 1);
+}
+
+__global__ __launch_bounds__(TPB) void k_group_fill(const int32_t* __restrict__ pslot, i64 U, i64 T,
+                                                    const int32_t* __restrict__ goff, int32_t* gcur,
+                                                    int32_t* __restrict__ gmem) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  const int m = blockIdx.y;
+  if (c >= U) return;
+  const i64 g = (i64)m * T + pslot[(i64)m * U + c];
+  gmem[goff[g] + atomicAdd(&gcur[g], 1)] = (int32_t)c;
+}
+
+__global__ __launch_bounds__(TPB) void k_iota(int32_t* __restrict__ out, i64 n) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) out[i] = (int32_t)i;
+}
+
+// thread per policy: its matched classes = gmem[pstart, pstart + plen)
+//   pmask -1: contradictory terms (matches nothing); -2: no terms (all
+//   classes: the iota block at all_start); terms sorted by slot = mask order
+__global__ __launch_bounds__(TPB) void k_pol_match(i64 P, const i64* __restrict__ toff,
+                                                   const int32_t* __restrict__ tval,
+                                                   const int32_t* __restrict__ pmask,
+                                                   const int32_t* __restrict__ moff,
+                                                   const int32_t* __restrict__ mslot,
+                                                   const int32_t* __restrict__ cval, i64 U,
+                                                   const int32_t* __restrict__ table, i64 T,
+                                                   const int32_t* __restrict__ goff,
+                                                   i64 all_start, i64* __restrict__ pstart,
+                                                   int32_t* __restrict__ plen) {
+  const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (p >= P) return;
+  const int m = pmask[p];
+  i64 st = 0;
+  int32_t len = 0;
+  if (m == -2) {
+    st = all_start;
+    len = (int32_t)U;
+  } else if (m >= 0) {
+    const i64 t0 = toff[p];
+    const int32_t* sl = mslot + moff[m];
+    const int ns = moff[m + 1] - moff[m];
+    bool possible = true;
+    uint32_t h = 0x2545f491u;
+    for (int k = 0; k < ns; ++k) {
+      const int32_t v = tval[t0 + k];
+      possible = possible && v >= 0;
+      h = hmix(h, (uint32_t)v);
+    }
+    if (possible && U > 0) {
+      const int32_t* tab = table + (i64)m * T;
+      uint32_t s = hfin(h) & (uint32_t)(T - 1);
+      for (;;) {
+        const int32_t cur = tab[s];
+        if (cur < 0) break;
+        bool eq = true;
+        for (int k = 0; k < ns; ++k)
+          if (cval[(i64)sl[k] * U + cur] != tval[t0 + k]) { eq = false; break; }
+        if (eq) {
+          const i64 g = (i64)m * T + s;
+          st = goff[g];
+          len = goff[g + 1] - goff[g];
+          break;
+        }
+        s = (s + 1) & (uint32_t)(T - 1);
+      }
+    }
+  }
+  pstart[p] = st;
+  plen[p] = len;
+}
+
+// dense fallback (too many distinct masks): per-policy class lists from the
+// policy-major bits of k_class_eval
+__global__ __launch_bounds__(TPB) void k_bits_to_lists(const u64* __restrict__ bits, i64 ld,
+                                                       i64 UW, const i64* __restrict__ off,
+                                                       int32_t* __restrict__ lst) {
+  __shared__ int sm[4];
+  const i64 p = blockIdx.x;
+  i64 base = off[p];
+  for (i64 w0 = 0; w0 < UW; w0 += TPB) {
+    const i64 w = w0 + threadIdx.x;
+    u64 v = (w < UW) ? bits[p * ld + w] : 0ull;
+    int tot;
+    i64 pos = base + block_excl_scan((int)__popcll(v), sm, tot);
+    while (v) {
+      lst[pos++] = (int32_t)(w * 64 + __builtin_ctzll(v));
+      v &= v - 1;
+    }
+    base += tot;
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_popc_rows(const u64* __restrict__ bits, i64 ld, i64 UW,
+                                                   int32_t* __restrict__ cnt) {
+  __shared__ int sm[4];
+  const i64 p = blockIdx.x;
+  int s = 0;
+  for (i64 w = threadIdx.x; w < UW; w += TPB) s += __popcll(bits[p * ld + w]);
+  s = block_sum(s, sm);
+  if (threadIdx.x == 0) cnt[p] = s;
+}
+
+__global__ __launch_bounds__(TPB) void k_offsets_to_start(const i64* __restrict__ off, i64 P,
+                                                          i64* __restrict__ pstart) {
+  const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (p < P) pstart[p] = off[p];
+}
+
+// ---- select side: S(c) = ascending policies whose list holds c --------------
+// block per policy: |S(c)| and the rebuild cost sum_{p in S(c)} |allow_p|
+__global__ __launch_bounds__(TPB) void k_sel_count(const i64* __restrict__ pstart,
+                                                   const int32_t* __restrict__ plen,
+                                                   const int32_t* __restrict__ pcls,
+                                                   const int32_t* __restrict__ acnt,
+                                                   int32_t* scnt, unsigned long long* cost) {
+  const i64 p = blockIdx.x;
+  const int32_t* L = pcls + pstart[p];
+  const int32_t len = plen[p];
+  const unsigned long long a = (unsigned long long)acnt[p];
+  for (int32_t k = threadIdx.x; k < len; k += TPB) {
+    const int32_t c = L[k];
+    atomicAdd(&scnt[c], 1);
+    if (a) atomicAdd(&cost[c], a);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_sel_place(const i64* __restrict__ pstart,
+                                                   const int32_t* __restrict__ plen,
+                                                   const int32_t* __restrict__ pcls,
+                                                   const i64* __restrict__ soffc, int32_t* scur,
+                                                   int32_t* __restrict__ slist) {
+  const i64 p = blockIdx.x;
+  const int32_t* L = pcls + pstart[p];
+  const int32_t len = plen[p];
+  for (int32_t k = threadIdx.x; k < len; k += TPB) {
+    const int32_t c = L[k];
+    slist[soffc[c] + atomicAdd(&scur[c], 1)] = (int32_t)p;
+  }
+}
+
+// block per class: sort S(c) ascending (the reference appends p in order,
+// model.py:161).  Entries are distinct.  s <= RANK_MAX: rank sort in LDS;
+// larger: a bitmap of all P policies in LDS, read back in order.
+constexpr int RANK_MAX = 2048;
+__global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soffc, i64 P,
+                                                    int32_t* __restrict__ slist) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds[];
+  __shared__ int sm[4];
+  const i64 c = blockIdx.x;
+  const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
+  if (s <= 1) return;
+  int32_t* L = slist + s0;
+  if (s <= RANK_MAX) {
+    int32_t* a = reinterpret_cast<int32_t*>(lds);
+    for (i64 k = threadIdx.x; k < s; k += TPB) a[k] = L[k];
+    __syncthreads();
+    for (i64 k = threadIdx.x; k < s; k += TPB) {
+      const int32_t v = a[k];
+      int r = 0;
+      for (i64 q = 0; q < s; ++q) r += a[q] < v;
+      L[r] = v;
+    }
+    return;
+  }
+  const i64 PW = (P + 63) / 64;
+  for (i64 w = threadIdx.x; w < PW; w += TPB) lds[w] = 0ull;
+  __syncthreads();
+  for (i64 k = threadIdx.x; k < s; k += TPB) {
+    const int32_t v = L[k];
+    atomicOr(&lds[v >> 6], 1ull << (v & 63));
+  }
+  __syncthreads();
+  i64 base = 0;
+  for (i64 w0 = 0; w0 < PW; w0 += TPB) {
+    const i64 w = w0 + threadIdx.x;
+    u64 v = w < PW ? lds[w] : 0ull;
+    int tot;
+    i64 pos = base + block_excl_scan((int)__popcll(v), sm, tot);
+    while (v) {
+      L[pos++] = (int32_t)(w * 64 + __builtin_ctzll(v));
+      v &= v - 1;
+    }
+    base += tot;
+  }
+}
+
+// ---- allow side: per policy the allowed column classes and pods -----------
+__global__ __launch_bounds__(TPB) void k_pol_allow_count(const i64* __restrict__ pstart,
+                                                         const int32_t* __restrict__ plen,
+                                                         const int32_t* __restrict__ pcls,
+                                                         const int32_t* __restrict__ csize,
+                                                         int32_t* __restrict__ nca,
+                                                         int32_t* __restrict__ acnt) {
+  __shared__ i64 sm[4];
+  const i64 p = blockIdx.x;
+  const int32_t* L = pcls + pstart[p];
+  const int32_t len = plen[p];
+  i64 pods = 0;
+  for (int32_t k = threadIdx.x; k < len; k += TPB) pods += csize[L[k]];
+  pods = block_sum(pods, sm);
+  if (threadIdx.x == 0) {
+    nca[p] = len;
+    acnt[p] = (int32_t)pods;
+  }
+}
+
+// block per policy: allowed class list (alc) and its bits AC[p]
+__global__ __launch_bounds__(TPB) void k_pol_allow_fill(const i64* __restrict__ pstart,
+                                                        const int32_t* __restrict__ plen,
+                                                        const int32_t* __restrict__ pcls,
+                                                        const i64* __restrict__ alcoff,
+                                                        int32_t* __restrict__ alc, u64* AC,
+                                                        i64 ldC) {
+  const i64 p = blockIdx.x;
+  const int32_t* L = pcls + pstart[p];
+  const int32_t len = plen[p];
+  int32_t* out = alc + alcoff[p];
+  for (int32_t k = threadIdx.x; k < len; k += TPB) {
+    const int32_t ca = L[k];
+    out[k] = ca;
+    atomicOr(&AC[p * ldC + (ca >> 6)], 1ull << (ca & 63));
+  }
+}
+
+// class-major policy bits for the MFMA path: out[pb][c] bit p%64 = policy p
+// matches class c (ACT over column classes, selT over row classes)
+__global__ __launch_bounds__(TPB) void k_classbits(const i64* __restrict__ pstart,
+                                                   const int32_t* __restrict__ plen,
+                                                   const int32_t* __restrict__ pcls, i64 Uc,
+                                                   u64* out) {
+  const i64 p = blockIdx.x;
+  const int32_t* L = pcls + pstart[p];
+  for (int32_t k = threadIdx.x; k < plen[p]; k += TPB)
+    atomicOr(&out[(p >> 6) * Uc + L[k]], 1ull << (p & 63));
+}
+
+// ---- compressed matrix Mc[c] over column classes (row classes x col classes)
+// light classes: scatter of the allowed-class lists of S(c)
+__global__ __launch_bounds__(TPB) void k_mc_scatter(const i64* __restrict__ soffc,
+                                                    const int32_t* __restrict__ slist,
+                                                    const i64* __restrict__ alcoff,
+                                                    const int32_t* __restrict__ alc,
+                                                    const int32_t* __restrict__ mcnt,
+                                                    const int32_t* __restrict__ hflag,
+                                                    u64* Mc, i64 ldMc) {
+  const i64 c = blockIdx.x;
+  if (mcnt[c] == 0 || (hflag && hflag[c])) return;
+  u64* row = Mc + c * ldMc;
+  for (i64 e = soffc[c]; e < soffc[c + 1]; ++e) {
+    const int32_t p = slist[e];
+    for (i64 k = alcoff[p] + threadIdx.x; k < alcoff[p + 1]; k += TPB) {
+      const int32_t ca = alc[k];
+      atomicOr(&row[ca >> 6], 1ull << (ca & 63));
+    }
+  }
+}
+
+// column OR and NAND over the classes with local members, at class level
+// block: 64 words x (4 waves x 32 classes)
+__global__ __launch_bounds__(TPB) void k_mc_cols(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
+                                                 i64 Ua, i64 U, const int32_t* __restrict__ mcnt,
+                                                 u64* col_or_c, u64* col_nand_c) {
+  __shared__ u64 red[2][4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const i64 w = (i64)blockIdx.x * 64 + lane;
+  const i64 c0 = (i64)blockIdx.y * 128 + wid * 32;
+  const u64 vm = w < UW ? valid_mask(w, Ua) : 0ull;
+  u64 o = 0, na = 0;
+  if (w < UW) {
+    for (i64 c = c0; c < min(c0 + 32, U); ++c) {
+      if (mcnt[c] == 0) continue;
+      const u64 v = Mc[c * ldMc + w];
+      o |= v;
+      na |= ~v & vm;
+    }
+  }
+  red[0][wid][lane] = o;
+  red[1][wid][lane] = na;
+  __syncthreads();
+  if (wid == 0 && w < UW) {
+    o = red[0][0][lane] | red[0][1][lane] | red[0][2][lane] | red[0][3][lane];
+    na = red[1][0][lane] | red[1][1][lane] | red[1][2][lane] | red[1][3][lane];
+    if (o) atomicOr(&col_or_c[w], o);
+    if (na) atomicOr(&col_nand_c[w], na);
+  }
+}
+
+// pod-level column words from class-level bits: bit j = X[cla[j]]
+__global__ __launch_bounds__(TPB) void k_cols_expand(const u64* __restrict__ col_or_c,
+                                                     const u64* __restrict__ col_nand_c,
+                                                     const int32_t* __restrict__ cla, i64 n,
+                                                     i64 ldM, u64* __restrict__ color,
+                                                     u64* __restrict__ colnand) {
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (((j >> 6) << 6) >= ldM * 64) return;
+  bool o = false, na = false;
+  if (j < n) {
+    const int32_t ca = cla[j];
+    o = (col_or_c[ca >> 6] >> (ca & 63)) & 1ull;
+    na = (col_nand_c[ca >> 6] >> (ca & 63)) & 1ull;
+  }
+  const u64 bo = __ballot(o), bn = __ballot(na);
+  if ((threadIdx.x & 63) == 0) {
+    color[j >> 6] = bo;
+    colnand[j >> 6] = bn;
+  }
+}
+
+// user_crosscheck at class level (kano_py/kano/algorithm.py:27-42).  Group
+// range of the local members of every row class:
+__global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restrict__ gid,
+                                                         const int32_t* __restrict__ cls, i64 r0,
+                                                         i64 r1, int32_t* gmin, int32_t* gmax) {
+  const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= r1) return;
+  const int32_t c = cls[i], g = gid[i];
+  atomicMin(&gmin[c], g);
+  atomicMax(&gmax[c], g);
+}
+
+// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise
+__global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
+                                                  const int32_t* __restrict__ mcnt,
+                                                  const int32_t* __restrict__ gmin,
+                                                  const int32_t* __restrict__ gmax, u64* R,
+                                                  u64* multi) {
+  const i64 c = blockIdx.x;
+  if (mcnt[c] == 0) return;
+  const int32_t g = gmin[c];
+  u64* dst = (g == gmax[c]) ? R + (i64)g * ldMc : multi;
+  for (i64 w = threadIdx.x; w < UW; w += TPB) {
+    const u64 v = Mc[c * ldMc + w];
+    if (v) atomicOr(&dst[w], v);
+  }
+}
+
+// cross[j] = MULTI(ca) | A2(ca) | (A1(ca) & ~R[g(j)](ca)),  ca = cla[j]
+__global__ __launch_bounds__(TPB) void k_cross_pod(const int32_t* __restrict__ gid,
+                                                   const int32_t* __restrict__ cla, i64 n,
+                                                   const u64* __restrict__ R, i64 ldMc,
+                                                   const u64* __restrict__ multi,
+                                                   const u64* __restrict__ A1,
+                                                   const u64* __restrict__ A2, i64 W,
+                                                   u64* __restrict__ cross) {
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (((j >> 6) << 6) >= W * 64) return;
+  bool bit = false;
+  if (j < n) {
+    const int32_t ca = cla[j];
+    const i64 cw = ca >> 6;
+    const u64 m = 1ull << (ca & 63);
+    const bool own = (R[(i64)gid[j] * ldMc + cw] & m) != 0;
+    bit = ((multi[cw] | A2[cw]) & m) || ((A1[cw] & m) && !own);
+  }
+  const u64 bal = __ballot(bit);
+  if ((threadIdx.x & 63) == 0) cross[j >> 6] = bal;
+}
+
+// ===========================================================================
 // Select side: per row class, |S(c)|, rebuild cost, work items, heavy flag
 // ===========================================================================
 struct ClassPlan {
-  const u64* selT;         // [PB][U]
-  i64 U, PB;
+  i64 U;
+  const int32_t* scnt;     // |S(c)|
+  const unsigned long long* cost;  // sum over S(c) of |allow_p| (rebuild scatter work)
   const int32_t* mcnt;     // local members per class
-  const int32_t* acnt;     // pods allowed per policy
   i64 W;                   // words per matrix row
   int ch;                  // members per work item
-  int force;               // 0 cost-based, 1 never heavy, 2 heavy when S(c) non-empty
-  i64 heavy_factor;        // heavy when cost > heavy_factor * W (and > 1 chunk)
-  int32_t* scnt;           // out |S(c)|
+  int force;               // 0 cost-based, 2 heavy whenever S(c) is non-empty
   int32_t* wicnt;          // out work items of the class
-  int32_t* hflag;          // out 1 = heavy
+  int32_t* hflag;          // out 1 = heavy (row built once from Mc, then copied)
   i64* sq;                 // out |S(c)|^2 for classes with local members
   int32_t* maxs;           // out max |S(c)| over classes with local members
 };
 
+// A light class rebuilds its row per member chunk by scattering its allowed
+// pods (cost atomics per chunk); a heavy one expands Mc once (about 64*W lane
+// operations) and every chunk copies it (W words).  Heavy iff cheaper.
 __global__ __launch_bounds__(TPB) void k_class_plan(ClassPlan a) {
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
   if (c >= a.U) return;
-  int s = 0;
-  i64 cost = 0;
-  for (i64 pb = 0; pb < a.PB; ++pb) {
-    u64 w = a.selT[pb * a.U + c];
-    s += __popcll(w);
-    while (w) {
-      cost += min((i64)a.acnt[pb * 64 + __builtin_ctzll(w)], 64 * a.W);
-      w &= w - 1;
-    }
-  }
+  const int32_t s = a.scnt[c];
   const int32_t m = a.mcnt[c];
-  a.scnt[c] = s;
+  const i64 cost = (i64)a.cost[c];
   const int32_t chunks = (m + a.ch - 1) / a.ch;
   a.wicnt[c] = chunks;
   int hv = 0;
   if (m > 0 && s > 0) {
     if (a.force == 2) hv = 1;
-    else if (a.force == 0) hv = cost > a.heavy_factor * a.W * (chunks > 1 ? 1 : 8);
+    else hv = cost * chunks > 64 * a.W + (i64)chunks * a.W;
   }
   a.hflag[c] = hv;
   a.sq[c] = m > 0 ? (i64)s * s : 0;
   if (m > 0) atomicMax(a.maxs, s);
-}
-
-__global__ __launch_bounds__(TPB) void k_sel_fill(const u64* __restrict__ selT, i64 U, i64 PB,
-                                                  const i64* __restrict__ soffc,
-                                                  int32_t* __restrict__ slist) {
-  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c >= U) return;
-  i64 pos = soffc[c];
-  for (i64 pb = 0; pb < PB; ++pb) {
-    u64 w = selT[pb * U + c];
-    while (w) {
-      slist[pos++] = (int32_t)(pb * 64 + __builtin_ctzll(w));
-      w &= w - 1;
-    }
-  }
 }
 
 __global__ __launch_bounds__(TPB) void k_sq_from_off(const i64* __restrict__ off, i64 U,
@@ -288,7 +674,7 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_or(const int32_t* __restrict__
     const i64 s0 = soffc[c], s1 = soffc[c + 1];
     for (i64 e = s0; e < s1; ++e) acc |= AC[(i64)slist[e] * ldC + w];
   }
-  Mc[(i64)blockIdx.x * ldMc + w] = acc;
+  Mc[(i64)c * ldMc + w] = acc;
 }
 
 // int8 MFMA contraction (the dense path):
@@ -359,7 +745,8 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
       const u64 bal = __ballot(acc[t][g] > 0);
       if (lane == 0 || lane == 32) {
         const int r = t * 32 + (g & 3) + 8 * (g >> 2) + (lane == 32 ? 4 : 0);
-        if (r < H) Mc32[(i64)r * ldMc * 2 + jt] = lane == 0 ? (uint32_t)bal : (uint32_t)(bal >> 32);
+        if (r < H)
+          Mc32[(i64)hlist[r] * ldMc * 2 + jt] = lane == 0 ? (uint32_t)bal : (uint32_t)(bal >> 32);
       }
     }
   }
@@ -373,20 +760,17 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict_
                                                       const int32_t* __restrict__ moff,
                                                       const int32_t* __restrict__ mem,
                                                       u64* __restrict__ M, i64 ldM, i64 r0) {
-  const i64 h = blockIdx.y;
+  const int32_t c = hlist[blockIdx.y];
   const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
   const i64 w = j >> 6;
   if ((w << 6) >= ldM * 64) return;                 // wave-uniform
   bool bit = false;
   if (j < n) {
     const int32_t ca = cla[j];
-    bit = (Mc[h * ldMc + (ca >> 6)] >> (ca & 63)) & 1ull;
+    bit = (Mc[(i64)c * ldMc + (ca >> 6)] >> (ca & 63)) & 1ull;
   }
   const u64 bal = __ballot(bit);
-  if ((threadIdx.x & 63) == 0 && w < ldM) {
-    const int32_t c = hlist[h];
-    M[(i64)(mem[moff[c]] - r0) * ldM + w] = bal;
-  }
+  if ((threadIdx.x & 63) == 0 && w < ldM) M[(i64)(mem[moff[c]] - r0) * ldM + w] = bal;
 }
 
 // ===========================================================================
@@ -576,12 +960,22 @@ __global__ __launch_bounds__(TPB) void k_get_col(const u64* __restrict__ M, i64 
   if ((threadIdx.x & 63) == 0 && r < rows) out[r >> 6] = bal;
 }
 
-// working_select_set of policy p over all pods
-__global__ __launch_bounds__(TPB) void k_sel_row(const u64* __restrict__ selT, i64 U,
+// working_select_set of policy p over all pods: p in S(cls(i)) (sorted lists)
+__global__ __launch_bounds__(TPB) void k_sel_row(const i64* __restrict__ soffc,
+                                                 const int32_t* __restrict__ slist,
                                                  const int32_t* __restrict__ cls, i64 n, i64 p,
                                                  u64* __restrict__ out) {
   const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool bit = i < n && ((selT[(p >> 6) * U + cls[i]] >> (p & 63)) & 1ull);
+  bool bit = false;
+  if (i < n) {
+    const int32_t c = cls[i];
+    i64 lo = soffc[c], hi = soffc[c + 1];
+    while (lo < hi) {
+      const i64 mid = (lo + hi) >> 1;
+      if (slist[mid] < p) lo = mid + 1; else hi = mid;
+    }
+    bit = lo < soffc[c + 1] && slist[lo] == p;
+  }
   const u64 bal = __ballot(bit);
   if ((threadIdx.x & 63) == 0 && i < n) out[i >> 6] = bal;
 }

@@ -206,12 +206,13 @@ def test_mutation_then_checks():
     cs, ps = api_objects(obj)
     m = ReachabilityMatrix.build_matrix(cs, ps)
     n = len(cs)
-    iso = all_isolated(m)
-    assert iso, "fixture needs an isolated column"
-    j = iso[0]
+    row5 = m.getrow(5)
+    j = row5.index(0)
+    iso_before = all_isolated(m)
     m[5, j] = 1
     assert m[5, j] == 1 and m.getrow(5)[j] == 1
     assert j not in all_isolated(m)
+    assert set(all_isolated(m)) == set(iso_before) - {j}
     row = m.matrix[7]
     row.setall(1)
     assert m.getrow(7).count() == n
