@@ -314,6 +314,15 @@ int do_classes(kano_ctx* ctx) {
   KTRY(sync(ctx));                                   // host sync 1 of the build
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
+  // the stream is idle here: size the scan scratch for the group tables too
+  i64 longest = std::max<i64>({ctx->n, ctx->P, (i64)1});
+  for (const auto* pr : {&ctx->sm, &ctx->am}) {
+    const i64 U = pr == &ctx->sm ? ctx->rc.U : ctx->cc.U;
+    i64 T = 64;
+    while (T < 2 * U) T <<= 1;
+    longest = std::max<i64>(longest, (i64)pr->NM * T);
+  }
+  KTRY(scan_reserve(ctx, longest));
   KTRY(classify_phase2(ctx, ctx->rc));
   KTRY(classify_phase2(ctx, ctx->cc));
   return 0;
