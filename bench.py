@@ -84,16 +84,31 @@ class Step:
 
     def __call__(self):
         eng, n = self.eng, self.n
-        eng.build()
+        from kano._bits import words_to_bool
         res = {}
         if self.world == 1:
-            ca, co = eng.col_checks()
-            cross = eng.crosscheck(self.gid)
-            from kano._bits import words_to_bool
-            res["all_reachable"] = np.flatnonzero(words_to_bool(ca, n))
-            res["all_isolated"] = np.flatnonzero(~words_to_bool(co, n))
-            res["user_crosscheck"] = np.flatnonzero(words_to_bool(cross, n))
+            # the fused entry point: build + every check, four host syncs
+            pairs = None
+            if self.shadow:
+                if self.pin is None:
+                    self.pin_pairs = 1 << 20
+                    self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+                pairs = self.pin.view(np.int32, 2 * self.pin_pairs)
+            r = eng.verify(self.gid, sys_row=0, shadow=self.shadow, pairs=pairs)
+            res["all_reachable"] = np.flatnonzero(words_to_bool(r["col_and"], n))
+            res["all_isolated"] = np.flatnonzero(~words_to_bool(r["col_or"], n))
+            res["user_crosscheck"] = np.flatnonzero(words_to_bool(r["cross"], n))
+            res["system_isolation"] = np.flatnonzero(~words_to_bool(r["sys"], n))
+            if self.shadow:
+                cnt = r["shadow_count"]
+                res["policy_shadow"] = r["pairs"]
+                res["policy_shadow_count"] = cnt
+                if cnt > self.pin_pairs:          # grow for the next step
+                    self.pin.close()
+                    self.pin_pairs = 2 * cnt
+                    self.pin = self.PinnedBuffer(self.pin_pairs * 8)
         else:
+            eng.build()
             f = self.flags
             eng.col_flags_dev(f.data_ptr())
             eng.crosscheck_dev(self.gid, f.data_ptr())
@@ -103,20 +118,19 @@ class Step:
             res["all_isolated"] = np.flatnonzero(h[:n] == 0)
             res["user_crosscheck"] = np.flatnonzero(h[n:2 * n])
             res["all_reachable"] = np.flatnonzero(h[2 * n:] == 0)
-        if self.r0 <= 0 < self.r1:
-            from kano._bits import words_to_bool
-            res["system_isolation"] = np.flatnonzero(~words_to_bool(eng.rows(0, 1)[0], n))
-        if self.shadow:
-            cnt = eng.shadow_count()
-            if self.pin is None or cnt > self.pin_pairs:
-                if self.pin is not None:
-                    self.pin.close()
-                self.pin_pairs = max(cnt, 1) * 2
-                self.pin = self.PinnedBuffer(self.pin_pairs * 8)
-            out = self.pin.view(np.int32, 2 * cnt).reshape(cnt, 2)
-            eng.shadow_fetch(cnt, out)
-            res["policy_shadow"] = out
-            res["policy_shadow_count"] = cnt
+            if self.r0 <= 0 < self.r1:
+                res["system_isolation"] = np.flatnonzero(~words_to_bool(eng.rows(0, 1)[0], n))
+            if self.shadow:
+                cnt = eng.shadow_count()
+                if self.pin is None or cnt > self.pin_pairs:
+                    if self.pin is not None:
+                        self.pin.close()
+                    self.pin_pairs = max(cnt, 1) * 2
+                    self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+                out = self.pin.view(np.int32, 2 * cnt).reshape(cnt, 2)
+                eng.shadow_fetch(cnt, out)
+                res["policy_shadow"] = out
+                res["policy_shadow_count"] = cnt
         st = eng.stage_times()
         self.k_rows_ms.append(st["k_rows"])
         self.stages = st

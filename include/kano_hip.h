@@ -142,6 +142,20 @@ int kano_shadow_lists(kano_ctx* ctx, int64_t n_lists, int64_t nbits, int64_t P,
  * pod of this shard has |S(i)| >= 2. */
 int kano_conflict(kano_ctx* ctx, int* raises);
 
+/* The whole verification pass in one call (the sequence kano_py's
+ * sample/example.py and tests/test_basic.py run: build_matrix, then
+ * all_reachable, all_isolated, user_crosscheck, system_isolation and
+ * policy_shadow), with four host syncs in total:
+ *   kano_build(path); col_and / col_or words (kano_col_checks); cross words
+ *   for the group ids gid (kano_crosscheck, skipped when gid is NULL);
+ *   sys_bits = row sys_row of M when it lies in this shard (system_isolation,
+ *   algorithm.py:45-55); when shadow_count is non-NULL, kano_shadow, and the
+ *   pairs copied to shadow_pairs if count <= shadow_cap (otherwise fetch them
+ *   with kano_shadow_fetch).  Any output pointer may be NULL. */
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, uint64_t* col_and,
+                uint64_t* col_or, uint64_t* cross, uint64_t* sys_bits, int32_t* shadow_pairs,
+                int64_t shadow_cap, int64_t* shadow_count);
+
 /* Timing of the last kano_build / kano_shadow stages on the context stream
  * (HIP events), milliseconds: [classes, allow, select + plan, rows stage,
  * shadow, build total, k_rows kernel alone, 0]. */

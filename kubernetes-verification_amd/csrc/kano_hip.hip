@@ -102,6 +102,8 @@ struct kano_ctx {
   DBuf flags, T, loff, L, tp, poff, out;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
+  void* hres = nullptr;      // pinned staging for kano_verify's bit rows
+  size_t hres_bytes = 0;
 
   hipEvent_t ev[10] = {};
 };
@@ -189,9 +191,8 @@ int scan_level(kano_ctx* ctx, const Tin* in, i64 n, Tout* out, char* scratch) {
     return 0;
   }
   const i64 tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  if (tiles == 1) {
-    hipLaunchKernelGGL((k_scan_tiles<Tin, Tout>), dim3(1), dim3(TPB), 0, ctx->stream, in, n,
-                       (const Tout*)nullptr, out);
+  if (n <= SCAN_SINGLE_MAX) {
+    hipLaunchKernelGGL((k_scan_single<Tin, Tout>), dim3(1), dim3(TPB), 0, ctx->stream, in, n, out);
     KLAUNCH();
     return 0;
   }
@@ -216,6 +217,34 @@ int scan_excl(kano_ctx* ctx, const Tin* in, i64 n, Tout* out) {
   return scan_level<Tin, Tout>(ctx, in, n, out, reinterpret_cast<char*>(ctx->scan_tmp.p));
 }
 
+// several device fills in one launch (k_fill_many)
+struct FillBatch {
+  FillJobs jobs{};
+  kano_ctx* ctx;
+  explicit FillBatch(kano_ctx* c) : ctx(c) { jobs.count = 0; }
+  int add(DBuf& b, size_t bytes, uint32_t value);
+  int run();
+};
+
+int FillBatch::add(DBuf& b, size_t bytes, uint32_t value) {
+  if (bytes == 0) return 0;
+  if (bytes % 4 != 0 || bytes > b.bytes) return fail(ctx, -EINVAL, "internal: bad fill job");
+  if (jobs.count == MAX_FILLS) KTRY(run());
+  jobs.j[jobs.count++] = FillJob{reinterpret_cast<uint32_t*>(b.p), (i64)(bytes / 4), value};
+  return 0;
+}
+
+int FillBatch::run() {
+  if (jobs.count == 0) return 0;
+  i64 most = 0;
+  for (int q = 0; q < jobs.count; ++q) most = std::max(most, jobs.j[q].words);
+  const unsigned grid = (unsigned)std::max<i64>(1, std::min<i64>(2048, (most + TPB - 1) / TPB));
+  hipLaunchKernelGGL(k_fill_many, dim3(grid), dim3(TPB), 0, ctx->stream, jobs);
+  KLAUNCH();
+  jobs.count = 0;
+  return 0;
+}
+
 int sync(kano_ctx* ctx) {
   KCHK(hipStreamSynchronize(ctx->stream));
   return 0;
@@ -224,11 +253,14 @@ int sync(kano_ctx* ctx) {
 i64 rows_local(const kano_ctx* ctx) { return ctx->r1 - ctx->r0; }
 
 // ---- classes ---------------------------------------------------------------
-// phase 1: hash insert, smallest member per slot, class-id scan (no sync)
-int classify_phase1(kano_ctx* ctx, ClassSet& cs) {
-  const i64 n = ctx->n;
+i64 table_size(i64 n) {
   i64 T = 64;
   while (T < 2 * n) T <<= 1;
+  return T;
+}
+
+int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
+  const i64 n = ctx->n, T = table_size(n);
   cs.KS = (int)cs.keys.size();
   KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, cs.keys.size())));
   KTRY(dalloc(ctx, cs.table, sizeof(int32_t) * T));
@@ -240,8 +272,14 @@ int classify_phase1(kano_ctx* ctx, ClassSet& cs) {
   if (cs.KS > 0)
     KCHK(hipMemcpyAsync(cs.keys_d.p, cs.keys.data(), sizeof(int32_t) * cs.KS,
                         hipMemcpyHostToDevice, ctx->stream));
-  KCHK(hipMemsetAsync(cs.table.p, 0xff, sizeof(int32_t) * T, ctx->stream));
-  KCHK(hipMemsetAsync(cs.smin.p, 0x7f, sizeof(int32_t) * T, ctx->stream));
+  KTRY(fb.add(cs.table, sizeof(int32_t) * T, 0xffffffffu));
+  KTRY(fb.add(cs.smin, sizeof(int32_t) * T, 0x7fffffffu));
+  return 0;
+}
+
+// phase 1: hash insert, smallest member per slot, class-id scan (no sync)
+int classify_phase1(kano_ctx* ctx, ClassSet& cs) {
+  const i64 n = ctx->n, T = table_size(n);
   if (n > 0) {
     hipLaunchKernelGGL(k_class_insert, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->pv), n, P_<int32_t>(cs.keys_d), cs.KS,
@@ -258,24 +296,27 @@ int classify_phase1(kano_ctx* ctx, ClassSet& cs) {
   return 0;
 }
 
-// phase 2 (U known): ids, member lists of pods [m0, m1), representative values
-int classify_phase2(kano_ctx* ctx, ClassSet& cs) {
-  const i64 n = ctx->n, U = cs.U;
+int classify_alloc2(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
+  const i64 U = cs.U;
   KTRY(dalloc(ctx, cs.rep, sizeof(int32_t) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, cs.mcnt, sizeof(int32_t) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, cs.mcur, sizeof(int32_t) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, cs.moff, sizeof(int32_t) * (U + 1)));
   KTRY(dalloc(ctx, cs.mem, sizeof(int32_t) * std::max<i64>(1, cs.m1 - cs.m0)));
   KTRY(dalloc(ctx, cs.cval, sizeof(int32_t) * std::max<i64>(1, (i64)cs.KS * U)));
+  KTRY(fb.add(cs.mcnt, sizeof(int32_t) * U, 0u));
+  KTRY(fb.add(cs.mcur, sizeof(int32_t) * U, 0u));
+  return 0;
+}
+
+// phase 2 (U known): ids, member lists of pods [m0, m1), representative values
+int classify_phase2(kano_ctx* ctx, ClassSet& cs) {
+  const i64 n = ctx->n, U = cs.U;
   if (n > 0) {
     hipLaunchKernelGGL(k_class_assign, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(cs.slot_of), n, P_<int32_t>(cs.smin), P_<int32_t>(cs.cid),
                        P_<int32_t>(cs.cls), P_<int32_t>(cs.rep));
     KLAUNCH();
-  }
-  if (U > 0) {
-    KCHK(hipMemsetAsync(cs.mcnt.p, 0, sizeof(int32_t) * U, ctx->stream));
-    KCHK(hipMemsetAsync(cs.mcur.p, 0, sizeof(int32_t) * U, ctx->stream));
   }
   const i64 rl = cs.m1 - cs.m0;
   if (rl > 0) {
@@ -299,65 +340,44 @@ int classify_phase2(kano_ctx* ctx, ClassSet& cs) {
   return 0;
 }
 
-int do_classes(kano_ctx* ctx) {
-  ctx->rc.m0 = ctx->r0;
-  ctx->rc.m1 = ctx->r1;
-  ctx->cc.m0 = 0;
-  ctx->cc.m1 = ctx->n;
-  KTRY(classify_phase1(ctx, ctx->rc));
-  KTRY(classify_phase1(ctx, ctx->cc));
-  int32_t u[2] = {0, 0};
-  KCHK(hipMemcpyAsync(&u[0], P_<int32_t>(ctx->rc.cid) + ctx->n, sizeof(int32_t),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&u[1], P_<int32_t>(ctx->cc.cid) + ctx->n, sizeof(int32_t),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  KTRY(sync(ctx));                                   // host sync 1 of the build
-  ctx->rc.U = u[0];
-  ctx->cc.U = u[1];
-  // the stream is idle here: size the scan scratch for the group tables too
-  i64 longest = std::max<i64>({ctx->n, ctx->P, (i64)1});
-  for (const auto* pr : {&ctx->sm, &ctx->am}) {
-    const i64 U = pr == &ctx->sm ? ctx->rc.U : ctx->cc.U;
-    i64 T = 64;
-    while (T < 2 * U) T <<= 1;
-    longest = std::max<i64>(longest, (i64)pr->NM * T);
-  }
-  KTRY(scan_reserve(ctx, longest));
-  KTRY(classify_phase2(ctx, ctx->rc));
-  KTRY(classify_phase2(ctx, ctx->cc));
-  return 0;
-}
-
 // ---- policy -> class matching (hash join, dense fallback) -------------------
-// Produces sx.pstart / sx.plen: policy p matches the classes
-// sx.gmem[pstart[p] .. pstart[p] + plen[p]) (or sx.boff-based lists in the
-// dense fallback, which needs one extra host sync).
-int match_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
+// sx.pstart / sx.plen: policy p matches the classes
+// sx.gmem[pstart[p] .. pstart[p] + plen[p]).
+int match_alloc(kano_ctx* ctx, SideMatch& sx, ClassSet& cs, FillBatch& fb) {
   const i64 P = ctx->P, U = cs.U;
   KTRY(dalloc(ctx, sx.pstart, sizeof(i64) * std::max<i64>(1, P)));
   KTRY(dalloc(ctx, sx.plen, sizeof(int32_t) * std::max<i64>(1, P)));
   if (P == 0) return 0;
   if (U == 0) {
-    KCHK(hipMemsetAsync(sx.pstart.p, 0, sizeof(i64) * P, ctx->stream));
-    KCHK(hipMemsetAsync(sx.plen.p, 0, sizeof(int32_t) * P, ctx->stream));
+    KTRY(fb.add(sx.pstart, sizeof(i64) * P, 0u));
+    KTRY(fb.add(sx.plen, sizeof(int32_t) * P, 0u));
     return 0;
   }
+  if (sx.dense) return 0;
+  const int NM = sx.NM;
+  sx.T = table_size(U);
+  const i64 NT = std::max<i64>(1, (i64)NM * sx.T);
+  KTRY(dalloc(ctx, sx.table, sizeof(int32_t) * NT));
+  KTRY(dalloc(ctx, sx.pslot, sizeof(int32_t) * std::max<i64>(1, (i64)NM * U)));
+  KTRY(dalloc(ctx, sx.gcnt, sizeof(int32_t) * NT));
+  KTRY(dalloc(ctx, sx.gcur, sizeof(int32_t) * NT));
+  KTRY(dalloc(ctx, sx.goff, sizeof(int32_t) * (NT + 1)));
+  KTRY(dalloc(ctx, sx.gmem, sizeof(int32_t) * ((i64)NM * U + U)));
+  if (NM > 0) {
+    KTRY(fb.add(sx.table, sizeof(int32_t) * NT, 0xffffffffu));
+    KTRY(fb.add(sx.gcnt, sizeof(int32_t) * NT, 0u));
+    KTRY(fb.add(sx.gcur, sizeof(int32_t) * NT, 0u));
+  }
+  return 0;
+}
+
+int match_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
+  const i64 P = ctx->P, U = cs.U;
+  if (P == 0 || U == 0) return 0;
   if (!sx.dense) {
     const int NM = sx.NM;
-    i64 T = 64;
-    while (T < 2 * U) T <<= 1;
-    sx.T = T;
-    const i64 NT = std::max<i64>(1, (i64)NM * T);
-    KTRY(dalloc(ctx, sx.table, sizeof(int32_t) * NT));
-    KTRY(dalloc(ctx, sx.pslot, sizeof(int32_t) * std::max<i64>(1, (i64)NM * U)));
-    KTRY(dalloc(ctx, sx.gcnt, sizeof(int32_t) * NT));
-    KTRY(dalloc(ctx, sx.gcur, sizeof(int32_t) * NT));
-    KTRY(dalloc(ctx, sx.goff, sizeof(int32_t) * (NT + 1)));
-    KTRY(dalloc(ctx, sx.gmem, sizeof(int32_t) * ((i64)NM * U + U)));
+    const i64 T = sx.T;
     if (NM > 0) {
-      KCHK(hipMemsetAsync(sx.table.p, 0xff, sizeof(int32_t) * NT, ctx->stream));
-      KCHK(hipMemsetAsync(sx.gcnt.p, 0, sizeof(int32_t) * NT, ctx->stream));
-      KCHK(hipMemsetAsync(sx.gcur.p, 0, sizeof(int32_t) * NT, ctx->stream));
       dim3 g2(nblk(U), (unsigned)NM);
       hipLaunchKernelGGL(k_proj_insert, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(cs.cval), U,
                          P_<int32_t>(sx.moff), P_<int32_t>(sx.mslot), P_<int32_t>(sx.table), T,
@@ -383,10 +403,9 @@ int match_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
     KLAUNCH();
     return 0;
   }
-  // dense fallback: evaluate every (policy, class) predicate
+  // dense fallback: evaluate every (policy, class) predicate (one extra sync)
   const i64 UW = (U + 63) / 64, ld = std::max<i64>(2, (UW + 1) & ~(i64)1);
   KTRY(dalloc(ctx, sx.bits, sizeof(u64) * P * ld));
-  KTRY(dalloc(ctx, sx.bcnt, sizeof(int32_t) * P));
   KTRY(dalloc(ctx, sx.boff, sizeof(i64) * (P + 1)));
   hipLaunchKernelGGL(k_class_eval, dim3(nblk(U), (unsigned)ctx->PB), dim3(TPB), 0, ctx->stream,
                      P_<int32_t>(cs.cval), U, P, P_<i64>(sx.toff), P_<int32_t>(sx.tslot),
@@ -409,16 +428,68 @@ int match_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
   return 0;
 }
 
-// allow side: allowed classes / pods per policy
-int do_allow(kano_ctx* ctx) {
-  const i64 P = ctx->P, Ua = ctx->cc.U;
+// classes of both sides, both matchings, allow counts, select counts and the
+// per-class plan; two host syncs (class counts, list sizes)
+int do_front(kano_ctx* ctx, int path) {
+  ctx->rc.m0 = ctx->r0;
+  ctx->rc.m1 = ctx->r1;
+  ctx->cc.m0 = 0;
+  ctx->cc.m1 = ctx->n;
+  {
+    FillBatch fb(ctx);
+    KTRY(classify_alloc1(ctx, ctx->rc, fb));
+    KTRY(classify_alloc1(ctx, ctx->cc, fb));
+    KTRY(fb.run());
+  }
+  KTRY(classify_phase1(ctx, ctx->rc));
+  KTRY(classify_phase1(ctx, ctx->cc));
+  int32_t u[2] = {0, 0};
+  KCHK(hipMemcpyAsync(&u[0], P_<int32_t>(ctx->rc.cid) + ctx->n, sizeof(int32_t),
+                      hipMemcpyDeviceToHost, ctx->stream));
+  KCHK(hipMemcpyAsync(&u[1], P_<int32_t>(ctx->cc.cid) + ctx->n, sizeof(int32_t),
+                      hipMemcpyDeviceToHost, ctx->stream));
+  KTRY(sync(ctx));                                   // host sync 1 of the build
+  ctx->rc.U = u[0];
+  ctx->cc.U = u[1];
+  KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  // the stream is idle here: size the scan scratch for the group tables too
+  i64 longest = std::max<i64>({ctx->n, ctx->P, (i64)1});
+  longest = std::max<i64>(longest, (i64)ctx->sm.NM * table_size(ctx->rc.U));
+  longest = std::max<i64>(longest, (i64)ctx->am.NM * table_size(ctx->cc.U));
+  KTRY(scan_reserve(ctx, longest));
+
+  const i64 P = ctx->P, Ur = ctx->rc.U, Ua = ctx->cc.U;
   ctx->UAW = (Ua + 63) / 64;
   ctx->ldC = std::max<i64>(2, (ctx->UAW + 1) & ~(i64)1);
+  {
+    FillBatch fb(ctx);
+    KTRY(classify_alloc2(ctx, ctx->rc, fb));
+    KTRY(classify_alloc2(ctx, ctx->cc, fb));
+    KTRY(match_alloc(ctx, ctx->am, ctx->cc, fb));
+    KTRY(match_alloc(ctx, ctx->sm, ctx->rc, fb));
+    KTRY(dalloc(ctx, ctx->nca, sizeof(int32_t) * std::max<i64>(1, P)));
+    KTRY(dalloc(ctx, ctx->acnt, sizeof(int32_t) * std::max<i64>(1, P)));
+    KTRY(dalloc(ctx, ctx->alcoff, sizeof(i64) * (P + 1)));
+    KTRY(dalloc(ctx, ctx->aloff, sizeof(i64) * (P + 1)));
+    KTRY(dalloc(ctx, ctx->scnt, sizeof(int32_t) * std::max<i64>(1, Ur)));
+    KTRY(dalloc(ctx, ctx->cost, sizeof(u64) * std::max<i64>(1, Ur)));
+    KTRY(dalloc(ctx, ctx->wicnt, sizeof(int32_t) * std::max<i64>(1, Ur)));
+    KTRY(dalloc(ctx, ctx->hflag, sizeof(int32_t) * std::max<i64>(1, Ur)));
+    KTRY(dalloc(ctx, ctx->sq, sizeof(i64) * std::max<i64>(1, Ur)));
+    KTRY(dalloc(ctx, ctx->maxs, sizeof(int32_t) * 4));
+    KTRY(dalloc(ctx, ctx->soffc, sizeof(i64) * (Ur + 1)));
+    KTRY(dalloc(ctx, ctx->wioff, sizeof(int32_t) * (Ur + 1)));
+    KTRY(dalloc(ctx, ctx->hoff, sizeof(int32_t) * (Ur + 1)));
+    KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (Ur + 1)));
+    KTRY(fb.add(ctx->maxs, 16, 0u));
+    KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
+    KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
+    KTRY(fb.run());
+  }
+  KTRY(classify_phase2(ctx, ctx->rc));
+  KTRY(classify_phase2(ctx, ctx->cc));
+  // allow side: allowed classes / pods per policy
   KTRY(match_side(ctx, ctx->am, ctx->cc));
-  KTRY(dalloc(ctx, ctx->nca, sizeof(int32_t) * std::max<i64>(1, P)));
-  KTRY(dalloc(ctx, ctx->acnt, sizeof(int32_t) * std::max<i64>(1, P)));
-  KTRY(dalloc(ctx, ctx->alcoff, sizeof(i64) * (P + 1)));
-  KTRY(dalloc(ctx, ctx->aloff, sizeof(i64) * (P + 1)));
   if (P > 0) {
     hipLaunchKernelGGL(k_pol_allow_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
@@ -428,38 +499,19 @@ int do_allow(kano_ctx* ctx) {
   }
   KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->nca), P, P_<i64>(ctx->alcoff))));
   KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->acnt), P, P_<i64>(ctx->aloff))));
-  return 0;
-}
-
-// select side: |S(c)|, rebuild cost, the per-class plan
-int do_select(kano_ctx* ctx, int path) {
-  const i64 U = ctx->rc.U, P = ctx->P;
+  KCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  // select side: |S(c)|, rebuild cost, the per-class plan
   KTRY(match_side(ctx, ctx->sm, ctx->rc));
-  KTRY(dalloc(ctx, ctx->scnt, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->cost, sizeof(u64) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->wicnt, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->hflag, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->sq, sizeof(i64) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->maxs, sizeof(int32_t)));
-  KTRY(dalloc(ctx, ctx->soffc, sizeof(i64) * (U + 1)));
-  KTRY(dalloc(ctx, ctx->wioff, sizeof(int32_t) * (U + 1)));
-  KTRY(dalloc(ctx, ctx->hoff, sizeof(int32_t) * (U + 1)));
-  KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (U + 1)));
-  KCHK(hipMemsetAsync(ctx->maxs.p, 0, sizeof(int32_t), ctx->stream));
-  if (U > 0) {
-    KCHK(hipMemsetAsync(ctx->scnt.p, 0, sizeof(int32_t) * U, ctx->stream));
-    KCHK(hipMemsetAsync(ctx->cost.p, 0, sizeof(u64) * U, ctx->stream));
-  }
-  if (P > 0 && U > 0) {
+  if (P > 0 && Ur > 0) {
     hipLaunchKernelGGL(k_sel_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                        P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                        P_<int32_t>(ctx->sm.gmem), P_<int32_t>(ctx->acnt), P_<int32_t>(ctx->scnt),
                        P_<unsigned long long>(ctx->cost));
     KLAUNCH();
   }
-  if (U > 0) {
+  if (Ur > 0) {
     ClassPlan a;
-    a.U = U;
+    a.U = Ur;
     a.scnt = P_<int32_t>(ctx->scnt);
     a.cost = P_<unsigned long long>(ctx->cost);
     a.mcnt = P_<int32_t>(ctx->rc.mcnt);
@@ -470,13 +522,13 @@ int do_select(kano_ctx* ctx, int path) {
     a.hflag = P_<int32_t>(ctx->hflag);
     a.sq = P_<i64>(ctx->sq);
     a.maxs = P_<int32_t>(ctx->maxs);
-    hipLaunchKernelGGL(k_class_plan, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, a);
+    hipLaunchKernelGGL(k_class_plan, dim3(nblk(Ur)), dim3(TPB), 0, ctx->stream, a);
     KLAUNCH();
   }
-  KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->scnt), U, P_<i64>(ctx->soffc))));
-  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->wicnt), U, P_<int32_t>(ctx->wioff))));
-  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->hflag), U, P_<int32_t>(ctx->hoff))));
-  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->sq), U, P_<i64>(ctx->pfoff))));
+  KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->scnt), Ur, P_<i64>(ctx->soffc))));
+  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->wicnt), Ur, P_<int32_t>(ctx->wioff))));
+  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->hflag), Ur, P_<int32_t>(ctx->hoff))));
+  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff))));
   return 0;
 }
 
@@ -503,29 +555,64 @@ int read_sizes(kano_ctx* ctx) {
   return 0;
 }
 
-// lists: S(c) ascending, allowed classes + bits + pods per policy, heavy list
-int do_fill(kano_ctx* ctx) {
-  const i64 U = ctx->rc.U, P = ctx->P;
-  KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
-  KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
-  KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
-  KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, ctx->heavy_count)));
-  KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
-  if (P > 0) KCHK(hipMemsetAsync(ctx->AC.p, 0, sizeof(u64) * P * ctx->ldC, ctx->stream));
+// lists (S(c) ascending, allowed classes + bits + pods per policy, heavy
+// list) and the compressed matrix Mc (row classes x column classes): light
+// classes by scatter, heavy classes by bitwise OR or the int8 MFMA
+// contraction; column checks at class level
+int do_back(kano_ctx* ctx, int path) {
+  const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
+  ctx->heavy_path = 0;
+  bool mfma = false;
+  if (H > 0) {
+    mfma = path == KANO_PATH_MFMA;
+    if (path == KANO_PATH_AUTO) {
+      // the MFMA walks every policy for every heavy row, the OR only S(c):
+      // dense when the average |S(c)| is a large share of P
+      const double avg_s = (double)ctx->nnz_sel / std::max<i64>(1, U);
+      mfma = H >= 32 && ctx->cc.U >= 64 && avg_s * 16.0 >= (double)P;
+    }
+    ctx->heavy_path = mfma ? 2 : 1;
+  }
+  {
+    FillBatch fb(ctx);
+    KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
+    KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
+    KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
+    KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, H)));
+    KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
+    KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
+    KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
+    KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
+    KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
+    KTRY(fb.add(ctx->scur, sizeof(int32_t) * U, 0u));
+    KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
+    KTRY(fb.add(ctx->col_or_c, sizeof(u64) * ldMc, 0u));
+    KTRY(fb.add(ctx->col_nand_c, sizeof(u64) * ldMc, 0u));
+    if (mfma) {
+      KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, ctx->PB * ctx->cc.U)));
+      KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, ctx->PB * U)));
+      KTRY(fb.add(ctx->ACT, sizeof(u64) * ctx->PB * ctx->cc.U, 0u));
+      KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
+    }
+    KTRY(fb.run());
+  }
   if (U > 0) {
-    KCHK(hipMemsetAsync(ctx->scur.p, 0, sizeof(int32_t) * U, ctx->stream));
     if (P > 0) {
       hipLaunchKernelGGL(k_sel_place, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                          P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                          P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
                          P_<int32_t>(ctx->slist));
       KLAUNCH();
-      const size_t lds = std::max<size_t>(sizeof(int32_t) * RANK_MAX,
-                                          sizeof(u64) * (size_t)((P + 63) / 64));
-      hipLaunchKernelGGL(k_sort_lists, dim3((unsigned)U), dim3(TPB), lds, ctx->stream,
-                         P_<i64>(ctx->soffc), P, P_<int32_t>(ctx->slist));
+      hipLaunchKernelGGL(k_sort_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                         P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist));
       KLAUNCH();
+      if (ctx->max_sel > SORT_WAVE_MAX) {
+        const size_t lds = sizeof(u64) * (size_t)((P + 63) / 64);
+        hipLaunchKernelGGL(k_sort_lists_big, dim3((unsigned)U), dim3(TPB), lds, ctx->stream,
+                           P_<i64>(ctx->soffc), P, P_<int32_t>(ctx->slist));
+        KLAUNCH();
+      }
     }
     hipLaunchKernelGGL(k_flag_list, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), U, P_<int32_t>(ctx->hlist));
@@ -542,58 +629,31 @@ int do_fill(kano_ctx* ctx) {
                        P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
     KLAUNCH();
   }
-  return 0;
-}
-
-// the compressed matrix Mc (row classes x column classes): light classes by
-// scatter, heavy classes by bitwise OR or the int8 MFMA contraction; then the
-// column checks at class level, expanded to pods
-int do_mc(kano_ctx* ctx, int path) {
-  const i64 U = ctx->rc.U, H = ctx->heavy_count, ldMc = ctx->ldC;
-  ctx->heavy_path = 0;
-  KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
-  KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
-  KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
-  KCHK(hipMemsetAsync(ctx->col_or_c.p, 0, sizeof(u64) * ldMc, ctx->stream));
-  KCHK(hipMemsetAsync(ctx->col_nand_c.p, 0, sizeof(u64) * ldMc, ctx->stream));
   if (U == 0) return 0;
-  KCHK(hipMemsetAsync(ctx->Mc.p, 0, sizeof(u64) * U * ldMc, ctx->stream));
-  hipLaunchKernelGGL(k_mc_scatter, dim3((unsigned)U), dim3(TPB), 0, ctx->stream,
-                     P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
+  hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                     P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
                      P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
                      H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr, P_<u64>(ctx->Mc),
                      ldMc);
   KLAUNCH();
   if (H > 0) {
-    bool mfma = path == KANO_PATH_MFMA;
-    if (path == KANO_PATH_AUTO) {
-      // the MFMA walks every policy for every heavy row, the OR only S(c):
-      // dense when the average |S(c)| is a large share of P
-      const double avg_s = (double)ctx->nnz_sel / std::max<i64>(1, U);
-      mfma = H >= 32 && ctx->cc.U >= 64 && avg_s * 16.0 >= (double)ctx->P;
-    }
-    ctx->heavy_path = mfma ? 2 : 1;
     if (mfma) {
       const i64 Ua = ctx->cc.U;
-      KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, ctx->PB * Ua)));
-      KCHK(hipMemsetAsync(ctx->ACT.p, 0, sizeof(u64) * ctx->PB * Ua, ctx->stream));
-      hipLaunchKernelGGL(k_classbits, dim3((unsigned)ctx->P), dim3(TPB), 0, ctx->stream,
+      hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                          P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                          P_<int32_t>(ctx->am.gmem), Ua, P_<u64>(ctx->ACT));
       KLAUNCH();
-      // class-major selector bits of the heavy rows: selT[pb][c]
-      KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, ctx->PB * U)));
-      KCHK(hipMemsetAsync(ctx->scratch_words.p, 0, sizeof(u64) * ctx->PB * U, ctx->stream));
-      hipLaunchKernelGGL(k_classbits, dim3((unsigned)ctx->P), dim3(TPB), 0, ctx->stream,
+      // class-major selector bits: selT[pb][c]
+      hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                          P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                          P_<int32_t>(ctx->sm.gmem), U, P_<u64>(ctx->scratch_words));
       KLAUNCH();
+      const u64* selT = P_<u64>(ctx->scratch_words);
+      uint32_t* out = reinterpret_cast<uint32_t*>(P_<u64>(ctx->Mc));
       for (i64 h0 = 0; h0 < H; h0 += HT_ROWS) {
         const int hh = (int)std::min<i64>(HT_ROWS, H - h0);
         const int32_t* hl = P_<int32_t>(ctx->hlist) + h0;
-        uint32_t* out = reinterpret_cast<uint32_t*>(P_<u64>(ctx->Mc));
         dim3 grid(nblk(2 * ldMc, TPB / 64));
-        const u64* selT = P_<u64>(ctx->scratch_words);
         if (hh <= 32)
           hipLaunchKernelGGL(k_heavy_mc_mfma<1>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
                              P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
@@ -742,7 +802,8 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
-  KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
+  if (n == 0 || rows_local(ctx) == 0 || W == 0 || ctx->rows_dirty)
+    KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
   int32_t G = 0;
   for (i64 i = 0; i < n; ++i) {
@@ -761,18 +822,20 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid) {
     KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
-    KCHK(hipMemsetAsync(ctx->gmin.p, 0x7f, sizeof(int32_t) * U, ctx->stream));
-    KCHK(hipMemsetAsync(ctx->gmax.p, 0xff, sizeof(int32_t) * U, ctx->stream));
-    KCHK(hipMemsetAsync(ctx->R.p, 0, sizeof(u64) * (i64)G * ldC, ctx->stream));
-    for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2})
-      KCHK(hipMemsetAsync(b->p, 0, sizeof(u64) * ldC, ctx->stream));
+    FillBatch fb(ctx);
+    KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
+    KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
+    KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
+    KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
+    for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
+    KTRY(fb.run());
     const i64 rl = rows_local(ctx);
     hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->gid), P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
                        P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax));
     KLAUNCH();
-    hipLaunchKernelGGL(k_cross_mc, dim3((unsigned)U), dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc),
-                       ldC, UAW, P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
+    hipLaunchKernelGGL(k_cross_mc, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
                        P_<int32_t>(ctx->gmax), P_<u64>(ctx->R), P_<u64>(ctx->multi));
     KLAUNCH();
     hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
@@ -856,6 +919,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->hres) (void)hipHostFree(ctx->hres);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
@@ -1087,15 +1151,10 @@ int kano_build(kano_ctx* ctx, int path) {
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  KTRY(do_classes(ctx));
-  KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-  KTRY(do_allow(ctx));
-  KCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  KTRY(do_select(ctx, path));
+  KTRY(do_front(ctx, path));
   KTRY(read_sizes(ctx));
   KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  KTRY(do_fill(ctx));
-  KTRY(do_mc(ctx, path));
+  KTRY(do_back(ctx, path));
   KTRY(do_rows(ctx));
   KCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->cols_valid = true;
@@ -1307,6 +1366,7 @@ int kano_shadow(kano_ctx* ctx, int64_t* count) {
   KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (rl + 1)));
   if (U > 0) {
     ShadowArgs a;
+    a.U = U;
     a.soffc = P_<i64>(ctx->soffc);
     a.slist = P_<int32_t>(ctx->slist);
     a.mcnt = P_<int32_t>(ctx->rc.mcnt);
@@ -1318,7 +1378,7 @@ int kano_shadow(kano_ctx* ctx, int64_t* count) {
     a.ldC = ctx->ldC;
     a.flags = P_<uint8_t>(ctx->flags);
     a.T = P_<i64>(ctx->T);
-    hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)U), dim3(TPB), 0, ctx->stream, a);
+    hipLaunchKernelGGL(k_shadow_test, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream, a);
     KLAUNCH();
   }
   KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->T), U, P_<i64>(ctx->loff))));
@@ -1337,8 +1397,8 @@ int kano_shadow(kano_ctx* ctx, int64_t* count) {
   KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nl)));
   KTRY(dalloc(ctx, ctx->out, sizeof(int2) * std::max<i64>(1, total)));
   if (U > 0 && nl > 0) {
-    hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)U), dim3(TPB), 0, ctx->stream,
-                       P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->pfoff),
+    hipLaunchKernelGGL(k_shadow_compact, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                       P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist), P_<i64>(ctx->pfoff),
                        P_<uint8_t>(ctx->flags), P_<i64>(ctx->loff), P_<int2>(ctx->L));
     KLAUNCH();
   }
@@ -1452,6 +1512,58 @@ int kano_conflict(kano_ctx* ctx, int* raises) {
   KTRY(ensure_built(ctx));
   if (!raises) return fail(ctx, -EINVAL, "kano_conflict: NULL");
   *raises = ctx->max_sel >= 2 ? 1 : 0;
+  return 0;
+}
+
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, uint64_t* col_and,
+                uint64_t* col_or, uint64_t* cross, uint64_t* sys_bits, int32_t* shadow_pairs,
+                int64_t shadow_cap, int64_t* shadow_count) {
+  KTRY(kano_build(ctx, path));
+  const i64 n = ctx->n, W = ctx->W;
+  const bool want_sys = sys_bits && sys_row >= ctx->r0 && sys_row < ctx->r1;
+  KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
+  if (W > 0) {
+    hipLaunchKernelGGL(k_col_final, dim3(nblk(W)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->colnand), W, n, P_<u64>(ctx->col_and));
+    KLAUNCH();
+  }
+  if (gid) KTRY(crosscheck_impl(ctx, gid));
+  int64_t total = 0;
+  if (shadow_count) {
+    KTRY(kano_shadow(ctx, &total));  // one sync (list sizes)
+    *shadow_count = total;
+  }
+  // every bit row through one pinned staging buffer, one final sync
+  const size_t rb = sizeof(u64) * (size_t)W, need = std::max<size_t>(16, 4 * rb);
+  if (ctx->hres_bytes < need) {
+    if (ctx->hres) KCHK(hipHostFree(ctx->hres));
+    ctx->hres = nullptr;
+    ctx->hres_bytes = 0;
+    KCHK(hipHostMalloc(&ctx->hres, need, hipHostMallocDefault));
+    ctx->hres_bytes = need;
+  }
+  char* h = static_cast<char*>(ctx->hres);
+  if (W > 0) {
+    if (col_and)
+      KCHK(hipMemcpyAsync(h, ctx->col_and.p, rb, hipMemcpyDeviceToHost, ctx->stream));
+    if (col_or)
+      KCHK(hipMemcpyAsync(h + rb, ctx->color.p, rb, hipMemcpyDeviceToHost, ctx->stream));
+    if (cross && gid)
+      KCHK(hipMemcpyAsync(h + 2 * rb, ctx->cross.p, rb, hipMemcpyDeviceToHost, ctx->stream));
+    if (want_sys)
+      KCHK(hipMemcpyAsync(h + 3 * rb, P_<u64>(ctx->M) + (sys_row - ctx->r0) * ctx->ldM, rb,
+                          hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (shadow_count && shadow_pairs && total > 0 && total <= shadow_cap)
+    KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
+                        ctx->stream));
+  KTRY(sync(ctx));
+  if (W > 0) {
+    if (col_and) memcpy(col_and, h, rb);
+    if (col_or) memcpy(col_or, h + rb, rb);
+    if (cross && gid) memcpy(cross, h + 2 * rb, rb);
+    if (want_sys) memcpy(sys_bits, h + 3 * rb, rb);
+  }
   return 0;
 }
 

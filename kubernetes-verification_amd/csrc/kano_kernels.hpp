@@ -387,30 +387,48 @@ __global__ __launch_bounds__(TPB) void k_sel_place(const i64* __restrict__ pstar
   }
 }
 
-// block per class: sort S(c) ascending (the reference appends p in order,
-// model.py:161).  Entries are distinct.  s <= RANK_MAX: rank sort in LDS;
-// larger: a bitmap of all P policies in LDS, read back in order.
-constexpr int RANK_MAX = 2048;
-__global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soffc, i64 P,
+// sort S(c) ascending (the reference appends p in policy order,
+// model.py:161); entries are distinct.  One wave per class: s <= 64 by a rank
+// sort in registers, s <= SORT_WAVE_MAX by a rank sort in the wave's LDS
+// slice; larger lists are left to k_sort_lists_big.
+constexpr int SORT_WAVE_MAX = 1024;
+__global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soffc, i64 U,
                                                     int32_t* __restrict__ slist) {
+  __shared__ int32_t buf[TPB / 64][SORT_WAVE_MAX];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + wid;
+  if (c >= U) return;
+  const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
+  if (s <= 1 || s > SORT_WAVE_MAX) return;
+  int32_t* L = slist + s0;
+  if (s <= 64) {
+    const int32_t v = lane < s ? L[lane] : 0x7fffffff;
+    int r = 0;
+    for (int k = 0; k < s; ++k) r += __shfl(v, k, 64) < v;
+    if (lane < s) L[r] = v;
+    return;
+  }
+  int32_t* a = buf[wid];
+  for (i64 k = lane; k < s; k += 64) a[k] = L[k];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  for (i64 k = lane; k < s; k += 64) {
+    const int32_t v = a[k];
+    int r = 0;
+    for (i64 q = 0; q < s; ++q) r += a[q] < v;
+    L[r] = v;
+  }
+}
+
+// block per class with s > SORT_WAVE_MAX: bitmap of all P policies in LDS
+__global__ __launch_bounds__(TPB) void k_sort_lists_big(const i64* __restrict__ soffc, i64 P,
+                                                        int32_t* __restrict__ slist) {
   extern __shared__ __attribute__((aligned(16))) u64 lds[];
   __shared__ int sm[4];
   const i64 c = blockIdx.x;
   const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
-  if (s <= 1) return;
+  if (s <= SORT_WAVE_MAX) return;
   int32_t* L = slist + s0;
-  if (s <= RANK_MAX) {
-    int32_t* a = reinterpret_cast<int32_t*>(lds);
-    for (i64 k = threadIdx.x; k < s; k += TPB) a[k] = L[k];
-    __syncthreads();
-    for (i64 k = threadIdx.x; k < s; k += TPB) {
-      const int32_t v = a[k];
-      int r = 0;
-      for (i64 q = 0; q < s; ++q) r += a[q] < v;
-      L[r] = v;
-    }
-    return;
-  }
   const i64 PW = (P + 63) / 64;
   for (i64 w = threadIdx.x; w < PW; w += TPB) lds[w] = 0ull;
   __syncthreads();
@@ -485,19 +503,20 @@ __global__ __launch_bounds__(TPB) void k_classbits(const i64* __restrict__ pstar
 
 // ---- compressed matrix Mc[c] over column classes (row classes x col classes)
 // light classes: scatter of the allowed-class lists of S(c)
-__global__ __launch_bounds__(TPB) void k_mc_scatter(const i64* __restrict__ soffc,
+__global__ __launch_bounds__(TPB) void k_mc_scatter(const i64* __restrict__ soffc, i64 U,
                                                     const int32_t* __restrict__ slist,
                                                     const i64* __restrict__ alcoff,
                                                     const int32_t* __restrict__ alc,
                                                     const int32_t* __restrict__ mcnt,
                                                     const int32_t* __restrict__ hflag,
                                                     u64* Mc, i64 ldMc) {
-  const i64 c = blockIdx.x;
-  if (mcnt[c] == 0 || (hflag && hflag[c])) return;
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= U || mcnt[c] == 0 || (hflag && hflag[c])) return;
   u64* row = Mc + c * ldMc;
   for (i64 e = soffc[c]; e < soffc[c + 1]; ++e) {
     const int32_t p = slist[e];
-    for (i64 k = alcoff[p] + threadIdx.x; k < alcoff[p + 1]; k += TPB) {
+    for (i64 k = alcoff[p] + lane; k < alcoff[p + 1]; k += 64) {
       const int32_t ca = alc[k];
       atomicOr(&row[ca >> 6], 1ull << (ca & 63));
     }
@@ -567,17 +586,18 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
   atomicMax(&gmax[c], g);
 }
 
-// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise
+// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per class)
 __global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
-                                                  const int32_t* __restrict__ mcnt,
+                                                  i64 U, const int32_t* __restrict__ mcnt,
                                                   const int32_t* __restrict__ gmin,
                                                   const int32_t* __restrict__ gmax, u64* R,
                                                   u64* multi) {
-  const i64 c = blockIdx.x;
-  if (mcnt[c] == 0) return;
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= U || mcnt[c] == 0) return;
   const int32_t g = gmin[c];
   u64* dst = (g == gmax[c]) ? R + (i64)g * ldMc : multi;
-  for (i64 w = threadIdx.x; w < UW; w += TPB) {
+  for (i64 w = lane; w < UW; w += 64) {
     const u64 v = Mc[c * ldMc + w];
     if (v) atomicOr(&dst[w], v);
   }
@@ -1016,6 +1036,7 @@ __device__ __forceinline__ bool subset_of(int32_t k, int32_t j, const int32_t* n
 }
 
 struct ShadowArgs {
+  i64 U;
   const i64* soffc;
   const int32_t* slist;
   const int32_t* mcnt;
@@ -1029,18 +1050,20 @@ struct ShadowArgs {
   i64* T;
 };
 
+// one wave per row class
 __global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a) {
-  __shared__ i64 sm[4];
-  const i64 c = blockIdx.x;
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= a.U) return;
   if (a.mcnt[c] == 0) {
-    if (threadIdx.x == 0) a.T[c] = 0;
+    if (lane == 0) a.T[c] = 0;
     return;
   }
   const i64 s0 = a.soffc[c];
   const i64 s = a.soffc[c + 1] - s0;
   const i64 ss = s * s;
   i64 cnt = 0;
-  for (i64 t = threadIdx.x; t < ss; t += TPB) {
+  for (i64 t = lane; t < ss; t += 64) {
     const i64 x = t / s, y = t - x * s;
     uint8_t f = 0;
     if (x != y) {
@@ -1050,28 +1073,30 @@ __global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a) {
     a.flags[a.pfoff[c] + t] = f;
     cnt += f;
   }
-  cnt = block_sum(cnt, sm);
-  if (threadIdx.x == 0) a.T[c] = cnt;
+  cnt = wave_sum(cnt);
+  if (lane == 0) a.T[c] = cnt;
 }
 
-__global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ soffc,
+// one wave per row class: the flagged pairs in (x, y) order
+__global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ soffc, i64 U,
                                                         const int32_t* __restrict__ slist,
                                                         const i64* __restrict__ pfoff,
                                                         const uint8_t* __restrict__ flags,
                                                         const i64* __restrict__ loff,
                                                         int2* __restrict__ L) {
-  __shared__ i64 sm[4];
-  const i64 c = blockIdx.x;
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= U) return;
   i64 out = loff[c];
   if (loff[c + 1] == out) return;
   const i64 s0 = soffc[c];
   const i64 s = soffc[c + 1] - s0;
   const i64 ss = s * s;
-  for (i64 t0 = 0; t0 < ss; t0 += TPB) {
-    const i64 t = t0 + threadIdx.x;
+  for (i64 t0 = 0; t0 < ss; t0 += 64) {
+    const i64 t = t0 + lane;
     const i64 f = (t < ss) ? flags[pfoff[c] + t] : 0;
     i64 tot;
-    const i64 pos = out + block_excl_scan(f, sm, tot);
+    const i64 pos = out + wave_excl_scan(f, tot);
     if (f) {
       const i64 x = t / s, y = t - x * s;
       L[pos] = make_int2(slist[s0 + x], slist[s0 + y]);

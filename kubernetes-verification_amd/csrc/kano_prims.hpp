@@ -40,6 +40,21 @@ __device__ __forceinline__ T block_excl_scan(T v, T* smem, T& total) {
 }
 
 template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// exclusive scan over the 64 lanes of a wave; total = sum of all lanes
+template <typename T>
+__device__ __forceinline__ T wave_excl_scan(T v, T& total) {
+  const T inc = wave_incl_scan(v);
+  total = __shfl(inc, 63, 64);
+  return inc - v;
+}
+
+template <typename T>
 __device__ __forceinline__ T block_sum(T v, T* smem) {
   T tot;
   (void)block_excl_scan(v, smem, tot);
@@ -81,6 +96,55 @@ __global__ __launch_bounds__(TPB) void k_scan_tiles(const Tin* __restrict__ in, 
     pre += v[k];
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == TPB - 1) out[n] = pre;
+}
+
+// single-block scan for n <= SCAN_SINGLE_MAX: tiles in sequence with a carry
+constexpr i64 SCAN_SINGLE_MAX = 131072;
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(TPB) void k_scan_single(const Tin* __restrict__ in, i64 n,
+                                                     Tout* __restrict__ out) {
+  __shared__ Tout sm[4];
+  Tout carry = 0;
+  for (i64 t0 = 0; t0 < n; t0 += SCAN_TILE) {
+    const i64 base = t0 + (i64)threadIdx.x * SCAN_ITEMS;
+    Tout v[SCAN_ITEMS];
+    Tout s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      v[k] = (base + k < n) ? (Tout)in[base + k] : (Tout)0;
+      s += v[k];
+    }
+    Tout tot;
+    Tout pre = block_excl_scan(s, sm, tot) + carry;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      if (base + k < n) out[base + k] = pre;
+      pre += v[k];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+}
+
+// several fills in one launch: (ptr, count of 32-bit words, value)
+struct FillJob {
+  uint32_t* ptr;
+  i64 words;
+  uint32_t value;
+};
+constexpr int MAX_FILLS = 24;
+struct FillJobs {
+  FillJob j[MAX_FILLS];
+  int count;
+};
+__global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
+  const i64 stride = (i64)gridDim.x * TPB;
+  for (int q = 0; q < jobs.count; ++q) {
+    uint32_t* p = jobs.j[q].ptr;
+    const uint32_t v = jobs.j[q].value;
+    const i64 nw = jobs.j[q].words;
+    for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < nw; i += stride) p[i] = v;
+  }
 }
 
 // ---- small helpers ---------------------------------------------------------

@@ -219,6 +219,38 @@ class DeviceBuild:
     def shadow(self) -> np.ndarray:
         return self.shadow_fetch(self.shadow_count())
 
+    def verify(self, gid: Optional[np.ndarray] = None, sys_row: int = 0, shadow: bool = True,
+               pairs: Optional[np.ndarray] = None, path: Optional[str] = None) -> dict:
+        """kano_verify: build + every check in one call (four host syncs).
+
+        Returns the bit rows (``col_and``, ``col_or``, ``cross``, ``sys``) as
+        uint64 words and, with ``shadow``, ``shadow_count`` plus ``pairs``
+        (an (count, 2) int32 view of the given buffer when it is large enough,
+        else a fresh array fetched afterwards)."""
+        W = self.W
+        words = np.zeros((4, max(W, 1)), dtype=np.uint64)
+        if gid is not None:
+            gid = np.ascontiguousarray(gid, dtype=np.int32)
+            if gid.shape[0] != self.n:
+                raise ValueError("gid must have one entry per pod")
+        cnt = c_int64(0)
+        cap = 0 if pairs is None else pairs.size // 2
+        pth = nat.PATHS[path or self.path]
+        self._chk(self.lib.kano_verify(
+            self.ctx, pth, _ptr(gid), int(sys_row), _ptr(words[0]), _ptr(words[1]),
+            _ptr(words[2]), _ptr(words[3]), _ptr(pairs), int(cap),
+            byref(cnt) if shadow else None), "kano_verify")
+        out = {"col_and": words[0, :W], "col_or": words[1, :W],
+               "cross": words[2, :W] if gid is not None else None, "sys": words[3, :W]}
+        if shadow:
+            k = int(cnt.value)
+            out["shadow_count"] = k
+            if pairs is not None and k <= cap:
+                out["pairs"] = pairs.reshape(-1)[:2 * k].reshape(k, 2)
+            else:
+                out["pairs"] = self.shadow_fetch(k)
+        return out
+
     def conflict_raises(self) -> bool:
         v = c_int()
         self._chk(self.lib.kano_conflict(self.ctx, byref(v)), "kano_conflict")

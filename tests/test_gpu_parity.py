@@ -163,6 +163,61 @@ def test_c2_engine_vs_kano_py():
     eng.close()
 
 
+@pytest.mark.parametrize("cap", [0, 1 << 22])
+def test_verify_fused_c2(cap):
+    """kano_verify (build + every check in one call, the bench's step) gives
+    the same answers as kano_py on C2; cap=0 exercises the late fetch."""
+    from kano._engine import DeviceBuild, PinnedBuffer
+    from kano._intern import tables_from_cluster
+    from kano._bits import set_bit_indices, words_to_bool
+    from kano.synth import make_config, KEY_NAMES
+    exp = expected("C2")
+    cl = make_config("C2")
+    n = cl.n
+    _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
+    eng = DeviceBuild(tables_from_cluster(cl), build=False)
+    pin = PinnedBuffer(max(cap, 1) * 8)
+    for _ in range(2):   # a rebuild in the same context must not change anything
+        r = eng.verify(gid, sys_row=0, shadow=True,
+                       pairs=pin.view(np.int32, 2 * cap) if cap else None)
+        assert sha(eng.rows(0, n)) == exp["M_sha256"]
+        assert set_bit_indices(r["col_and"], n).tolist() == exp["all_reachable"]
+        assert np.flatnonzero(~words_to_bool(r["col_or"], n)).tolist() == exp["all_isolated"]
+        assert set_bit_indices(r["cross"], n).tolist() == exp["user_crosscheck"]["result"]
+        assert (np.flatnonzero(~words_to_bool(r["sys"], n)).tolist()
+                == exp["system_isolation"]["result"])
+        assert r["shadow_count"] == exp["policy_shadow"]["count"]
+        assert sha(np.ascontiguousarray(r["pairs"])) == exp["policy_shadow"]["sha256"]
+    eng.close()
+    pin.close()
+
+
+def test_verify_fused_shards():
+    """kano_verify on row shards: per-shard pairs concatenate to the full
+    list, the system row comes only from its owner."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids
+    from oracle import kano_oracle as orc
+    obj = cluster("s_sparse_2000")
+    cs, ps = api_objects(obj)
+    t = intern(cs, ps)
+    n = len(cs)
+    ref = orc.run_c(obj, label=obj["label"])
+    gid = group_ids(cs, obj["label"])
+    pairs, cross = [], []
+    for r0, r1 in [(0, 700), (700, n)]:
+        e = DeviceBuild(t, rows=(r0, r1), build=False)
+        r = e.verify(gid, sys_row=5, shadow=True)
+        pairs.append(r["pairs"])
+        cross.append(r["cross"])
+        sys_row = e.rows(5, 1)[0] if r0 <= 5 < r1 else np.zeros_like(r["sys"])
+        assert np.array_equal(r["sys"], sys_row)
+        e.close()
+    assert np.array_equal(np.concatenate(pairs), ref["shadow"])
+    from kano._bits import set_bit_indices
+    assert set_bit_indices(np.bitwise_or.reduce(cross), n).tolist() == ref["user_crosscheck"]
+
+
 def test_row_shards_combine_to_full():
     """Row-sharded contexts (the multi-GPU partition) reproduce the full
     matrix; their column flags combine by MAX (= OR) exactly."""
