@@ -77,6 +77,7 @@ class Step:
             self.flags = torch.zeros(3 * n, dtype=torch.uint8, device="cuda")
         from kano._engine import PinnedBuffer
         self.pin = None
+        self.pin_idx = None
         self.pin_pairs = 0
         self.PinnedBuffer = PinnedBuffer
         self.results = {}
@@ -87,18 +88,20 @@ class Step:
         from kano._bits import words_to_bool
         res = {}
         if self.world == 1:
-            # the fused entry point: build + every check, four host syncs
+            # the fused entry point: build + every check, three host syncs;
+            # results arrive as the reference's index lists
             pairs = None
             if self.shadow:
                 if self.pin is None:
                     self.pin_pairs = 1 << 20
                     self.pin = self.PinnedBuffer(self.pin_pairs * 8)
                 pairs = self.pin.view(np.int32, 2 * self.pin_pairs)
-            r = eng.verify(self.gid, sys_row=0, shadow=self.shadow, pairs=pairs)
-            res["all_reachable"] = np.flatnonzero(words_to_bool(r["col_and"], n))
-            res["all_isolated"] = np.flatnonzero(~words_to_bool(r["col_or"], n))
-            res["user_crosscheck"] = np.flatnonzero(words_to_bool(r["cross"], n))
-            res["system_isolation"] = np.flatnonzero(~words_to_bool(r["sys"], n))
+            if self.pin_idx is None:
+                self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
+            r = eng.verify(self.gid, sys_row=0, shadow=self.shadow, pairs=pairs,
+                           idx=self.pin_idx.view(np.int32, 4 * max(n, 1)))
+            for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
+                res[k] = r[k]
             if self.shadow:
                 cnt = r["shadow_count"]
                 res["policy_shadow"] = r["pairs"]

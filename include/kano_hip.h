@@ -145,16 +145,20 @@ int kano_conflict(kano_ctx* ctx, int* raises);
 /* The whole verification pass in one call (the sequence kano_py's
  * sample/example.py and tests/test_basic.py run: build_matrix, then
  * all_reachable, all_isolated, user_crosscheck, system_isolation and
- * policy_shadow), with four host syncs in total:
- *   kano_build(path); col_and / col_or words (kano_col_checks); cross words
- *   for the group ids gid (kano_crosscheck, skipped when gid is NULL);
- *   sys_bits = row sys_row of M when it lies in this shard (system_isolation,
- *   algorithm.py:45-55); when shadow_count is non-NULL, kano_shadow, and the
- *   pairs copied to shadow_pairs if count <= shadow_cap (otherwise fetch them
- *   with kano_shadow_fetch).  Any output pointer may be NULL. */
-int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, uint64_t* col_and,
-                uint64_t* col_or, uint64_t* cross, uint64_t* sys_bits, int32_t* shadow_pairs,
-                int64_t shadow_cap, int64_t* shadow_count);
+ * policy_shadow) with three host syncs in total.  Results are the
+ * reference's return values: ascending pod-index lists, concatenated in idx
+ * (capacity 4*n) with counts[4] =
+ *   [all_reachable (algorithm.py:4-9), all_isolated (:12-17),
+ *    user_crosscheck for the group ids gid (:20-42; 0 when gid is NULL),
+ *    system_isolation(sys_row) (:45-55; -1 when sys_row is not in this shard)].
+ * On a row shard the column lists cover only this shard's rows (combine
+ * with kano_col_flags_dev / kano_crosscheck_dev across shards instead).
+ * When shadow_count is non-NULL, policy_shadow runs too (kano_shadow) and
+ * the pairs are copied to shadow_pairs if count <= shadow_cap (otherwise
+ * fetch them with kano_shadow_fetch). */
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, int32_t* idx,
+                int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                int64_t* shadow_count);
 
 /* Timing of the last kano_build / kano_shadow stages on the context stream
  * (HIP events), milliseconds: [classes, allow, select + plan, rows stage,

@@ -94,16 +94,18 @@ struct kano_ctx {
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
 
   DBuf pv;
-  DBuf scnt, cost, soffc, scur, slist, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
+  DBuf scnt, cost, soffc, scur, slist, ecls, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
   DBuf ACT, AC, nca, acnt, alcoff, alc, aloff, alist;
   DBuf M, Mc, color, colnand, col_and, col_or_c, col_nand_c;
   DBuf scan_tmp;
+  i64 scan_cap = 0;          // tiles per status region of scan_tmp
+  int scan_parity = 0;
   DBuf gid, cgroup, R, multi, A1, A2, own, cross, gmin, gmax;
-  DBuf flags, T, loff, L, tp, poff, out;
+  DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
-  void* hres = nullptr;      // pinned staging for kano_verify's bit rows
-  size_t hres_bytes = 0;
+  DBuf gdev, icnt, ioff;     // gathered scalars, index-list block counts / offsets
+  u64* ghost = nullptr;      // pinned landing buffer for gathered scalars
 
   hipEvent_t ev[10] = {};
 };
@@ -171,50 +173,43 @@ T* P_(DBuf& b) {
 
 inline unsigned nblk(i64 n, i64 per = TPB) { return (unsigned)((n + per - 1) / per); }
 
-// ---- device-wide scan with reserved scratch ------------------------------
-size_t scan_scratch_bytes(i64 n) {
-  size_t b = 0;
-  while (n > SCAN_TILE) {
-    const i64 t = (n + SCAN_TILE - 1) / SCAN_TILE;
-    b += ((sizeof(i64) * (2 * t + 1) + 255) / 256) * 256;
-    n = t;
-  }
-  return b + 256;
+// ---- device-wide scan: one k_scan_lb launch on reserved status regions ----
+inline i64 scan_tiles(i64 n) { return std::max<i64>(1, (n + SCAN_TILE - 1) / SCAN_TILE); }
+
+int scan_reserve(kano_ctx* ctx, i64 n) {
+  const i64 tiles = scan_tiles(n);
+  if (tiles <= ctx->scan_cap) return 0;
+  const size_t bytes = sizeof(u64) * 2 * (size_t)(1 + tiles);
+  KTRY(dalloc(ctx, ctx->scan_tmp, bytes));
+  KCHK(hipMemsetAsync(ctx->scan_tmp.p, 0, bytes, ctx->stream));
+  ctx->scan_cap = tiles;
+  ctx->scan_parity = 0;
+  return 0;
 }
 
-int scan_reserve(kano_ctx* ctx, i64 n) { return dalloc(ctx, ctx->scan_tmp, scan_scratch_bytes(n)); }
-
 template <typename Tin, typename Tout>
-int scan_level(kano_ctx* ctx, const Tin* in, i64 n, Tout* out, char* scratch) {
+int scan_level(kano_ctx* ctx, const Tin* in, i64 n, Tout* out) {
   if (n == 0) {
     KCHK(hipMemsetAsync(out, 0, sizeof(Tout), ctx->stream));
     return 0;
   }
-  const i64 tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  if (n <= SCAN_SINGLE_MAX) {
-    hipLaunchKernelGGL((k_scan_single<Tin, Tout>), dim3(1), dim3(TPB), 0, ctx->stream, in, n, out);
-    KLAUNCH();
-    return 0;
-  }
-  Tout* sums = reinterpret_cast<Tout*>(scratch);
-  Tout* offs = sums + tiles;
-  char* next = scratch + ((sizeof(i64) * (2 * tiles + 1) + 255) / 256) * 256;
-  hipLaunchKernelGGL((k_scan_sums<Tin, Tout>), dim3((unsigned)tiles), dim3(TPB), 0, ctx->stream,
-                     in, n, sums);
+  const i64 tiles = scan_tiles(n), region = 1 + ctx->scan_cap;
+  u64* st = P_<u64>(ctx->scan_tmp);
+  u64* cur = st + (ctx->scan_parity ? region : 0);
+  u64* nxt = st + (ctx->scan_parity ? 0 : region);
+  hipLaunchKernelGGL((k_scan_lb<Tin, Tout>), dim3((unsigned)tiles), dim3(TPB), 0, ctx->stream, in,
+                     n, out, cur, nxt, region);
   KLAUNCH();
-  KTRY((scan_level<Tout, Tout>(ctx, sums, tiles, offs, next)));
-  hipLaunchKernelGGL((k_scan_tiles<Tin, Tout>), dim3((unsigned)tiles), dim3(TPB), 0, ctx->stream,
-                     in, n, (const Tout*)offs, out);
-  KLAUNCH();
+  ctx->scan_parity ^= 1;
   return 0;
 }
 
 // exclusive scan, out has n+1 slots (out[n] = total)
 template <typename Tin, typename Tout>
 int scan_excl(kano_ctx* ctx, const Tin* in, i64 n, Tout* out) {
-  if (ctx->scan_tmp.bytes < scan_scratch_bytes(n))
+  if (scan_tiles(n) > ctx->scan_cap)
     return fail(ctx, -EINVAL, "internal: scan scratch not reserved for " + std::to_string(n));
-  return scan_level<Tin, Tout>(ctx, in, n, out, reinterpret_cast<char*>(ctx->scan_tmp.p));
+  return scan_level<Tin, Tout>(ctx, in, n, out);
 }
 
 // several device fills in one launch (k_fill_many)
@@ -249,6 +244,29 @@ int sync(kano_ctx* ctx) {
   KCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
+
+// device scalars read back with one kernel, one copy and one sync
+struct Gather {
+  GatherJobs g{};
+  kano_ctx* ctx;
+  explicit Gather(kano_ctx* c) : ctx(c) { g.count = 0; }
+  void add(const void* p, bool wide) {
+    g.src[g.count] = p;
+    g.wide[g.count] = wide ? 1 : 0;
+    ++g.count;
+  }
+  int run(i64* out) {
+    if (g.count == 0) return sync(ctx);
+    KTRY(dalloc(ctx, ctx->gdev, sizeof(u64) * MAX_GATHER));
+    hipLaunchKernelGGL(k_gather, dim3(1), dim3(64), 0, ctx->stream, g, P_<u64>(ctx->gdev));
+    KLAUNCH();
+    KCHK(hipMemcpyAsync(ctx->ghost, ctx->gdev.p, sizeof(u64) * g.count, hipMemcpyDeviceToHost,
+                        ctx->stream));
+    KTRY(sync(ctx));
+    for (int k = 0; k < g.count; ++k) out[k] = (i64)ctx->ghost[k];
+    return 0;
+  }
+};
 
 i64 rows_local(const kano_ctx* ctx) { return ctx->r1 - ctx->r0; }
 
@@ -443,12 +461,13 @@ int do_front(kano_ctx* ctx, int path) {
   }
   KTRY(classify_phase1(ctx, ctx->rc));
   KTRY(classify_phase1(ctx, ctx->cc));
-  int32_t u[2] = {0, 0};
-  KCHK(hipMemcpyAsync(&u[0], P_<int32_t>(ctx->rc.cid) + ctx->n, sizeof(int32_t),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&u[1], P_<int32_t>(ctx->cc.cid) + ctx->n, sizeof(int32_t),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  KTRY(sync(ctx));                                   // host sync 1 of the build
+  i64 u[2] = {0, 0};
+  {
+    Gather ga(ctx);
+    ga.add(P_<int32_t>(ctx->rc.cid) + ctx->n, false);
+    ga.add(P_<int32_t>(ctx->cc.cid) + ctx->n, false);
+    KTRY(ga.run(u));                                 // host sync 1 of the build
+  }
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -535,23 +554,23 @@ int do_front(kano_ctx* ctx, int path) {
 // host sync 2 of the build: every list size at once
 int read_sizes(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, P = ctx->P;
-  i64 h8[4] = {0, 0, 0, 0};
-  int32_t h4[3] = {0, 0, 0};
-  KCHK(hipMemcpyAsync(&h8[0], P_<i64>(ctx->soffc) + U, 8, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&h8[1], P_<i64>(ctx->alcoff) + P, 8, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&h8[2], P_<i64>(ctx->aloff) + P, 8, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&h8[3], P_<i64>(ctx->pfoff) + U, 8, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&h4[0], P_<int32_t>(ctx->wioff) + U, 4, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&h4[1], P_<int32_t>(ctx->hoff) + U, 4, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&h4[2], P_<int32_t>(ctx->maxs), 4, hipMemcpyDeviceToHost, ctx->stream));
-  KTRY(sync(ctx));
-  ctx->nnz_sel = h8[0];
-  ctx->nnz_alc = h8[1];
-  ctx->nnz_alw = h8[2];
-  ctx->nflags = h8[3];
-  ctx->wi_total = h4[0];
-  ctx->heavy_count = h4[1];
-  ctx->max_sel = h4[2];
+  Gather ga(ctx);
+  ga.add(P_<i64>(ctx->soffc) + U, true);
+  ga.add(P_<i64>(ctx->alcoff) + P, true);
+  ga.add(P_<i64>(ctx->aloff) + P, true);
+  ga.add(P_<i64>(ctx->pfoff) + U, true);
+  ga.add(P_<int32_t>(ctx->wioff) + U, false);
+  ga.add(P_<int32_t>(ctx->hoff) + U, false);
+  ga.add(P_<int32_t>(ctx->maxs), false);
+  i64 v[7];
+  KTRY(ga.run(v));
+  ctx->nnz_sel = v[0];
+  ctx->nnz_alc = v[1];
+  ctx->nnz_alw = v[2];
+  ctx->nflags = v[3];
+  ctx->wi_total = v[4];
+  ctx->heavy_count = v[5];
+  ctx->max_sel = (int)v[6];
   return 0;
 }
 
@@ -576,6 +595,7 @@ int do_back(kano_ctx* ctx, int path) {
   {
     FillBatch fb(ctx);
     KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
+    KTRY(dalloc(ctx, ctx->ecls, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
     KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
     KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
@@ -602,7 +622,7 @@ int do_back(kano_ctx* ctx, int path) {
       hipLaunchKernelGGL(k_sel_place, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                          P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                          P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
-                         P_<int32_t>(ctx->slist));
+                         P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls));
       KLAUNCH();
       hipLaunchKernelGGL(k_sort_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
                          P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist));
@@ -630,8 +650,9 @@ int do_back(kano_ctx* ctx, int path) {
     KLAUNCH();
   }
   if (U == 0) return 0;
-  hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                     P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
+  if (ctx->nnz_sel > 0)
+  hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                     ctx->nnz_sel, P_<int32_t>(ctx->ecls), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
                      P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
                      H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr, P_<u64>(ctx->Mc),
                      ldMc);
@@ -911,6 +932,11 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->ghost), sizeof(u64) * MAX_GATHER,
+                    hipHostMallocDefault) != hipSuccess) {
+    kano_destroy(ctx);
+    return -ENOMEM;
+  }
   *out = ctx;
   return 0;
 }
@@ -919,7 +945,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->hres) (void)hipHostFree(ctx->hres);
+  if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
@@ -940,7 +966,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
                   &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
-                  &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident};
+                  &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
+                  &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1355,16 +1382,30 @@ int kano_get_allow_csr(kano_ctx* ctx, int64_t* off, int32_t* pods) {
   return sync(ctx);
 }
 
-int kano_shadow(kano_ctx* ctx, int64_t* count) {
-  KTRY(ensure_built(ctx));
-  const i64 U = ctx->rc.U, rl = rows_local(ctx);
+}  // extern "C"
+
+namespace {
+// policy_shadow up to its one sync: flags, per-class counts, per-pod offsets;
+// the caller gathers toff[nt] (list length) and poff[rl] (pairs) with its own
+// scalars
+int shadow_front(kano_ctx* ctx, Gather& ga) {
+  const i64 U = ctx->rc.U, rl = rows_local(ctx), nf = ctx->nflags;
+  const i64 nt = (nf + SH_TILE - 1) / SH_TILE;
   KCHK(hipEventRecord(ctx->ev[5], ctx->stream));
-  KTRY(dalloc(ctx, ctx->flags, std::max<i64>(1, ctx->nflags)));
+  KTRY(scan_reserve(ctx, std::max<i64>({U, rl, nt, (i64)1})));
+  KTRY(dalloc(ctx, ctx->flags, nf + 16));
   KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (U + 1)));
   KTRY(dalloc(ctx, ctx->tp, sizeof(i64) * std::max<i64>(1, rl)));
   KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (rl + 1)));
-  if (U > 0) {
+  KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, nt)));
+  KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (nt + 1)));
+  {
+    FillBatch fb(ctx);
+    KTRY(fb.add(ctx->T, sizeof(i64) * U, 0u));
+    KTRY(fb.run());
+  }
+  if (nt > 0) {
     ShadowArgs a;
     a.U = U;
     a.soffc = P_<i64>(ctx->soffc);
@@ -1378,9 +1419,11 @@ int kano_shadow(kano_ctx* ctx, int64_t* count) {
     a.ldC = ctx->ldC;
     a.flags = P_<uint8_t>(ctx->flags);
     a.T = P_<i64>(ctx->T);
-    hipLaunchKernelGGL(k_shadow_test, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream, a);
+    hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)nt), dim3(TPB), 0, ctx->stream, a, nf,
+                       P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
+  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->tcnt), nt, P_<i64>(ctx->toff))));
   KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->T), U, P_<i64>(ctx->loff))));
   if (rl > 0) {
     hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
@@ -1389,17 +1432,20 @@ int kano_shadow(kano_ctx* ctx, int64_t* count) {
     KLAUNCH();
   }
   KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->tp), rl, P_<i64>(ctx->poff))));
-  i64 tot[2] = {0, 0};
-  KCHK(hipMemcpyAsync(&tot[0], P_<i64>(ctx->loff) + U, 8, hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipMemcpyAsync(&tot[1], P_<i64>(ctx->poff) + rl, 8, hipMemcpyDeviceToHost, ctx->stream));
-  KTRY(sync(ctx));
-  const i64 nl = tot[0], total = tot[1];
+  ga.add(P_<i64>(ctx->toff) + nt, true);
+  ga.add(P_<i64>(ctx->poff) + rl, true);
+  return 0;
+}
+
+int shadow_back(kano_ctx* ctx, i64 nl, i64 total) {
+  const i64 U = ctx->rc.U, rl = rows_local(ctx), nf = ctx->nflags;
+  const i64 nt = (nf + SH_TILE - 1) / SH_TILE;
   KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nl)));
   KTRY(dalloc(ctx, ctx->out, sizeof(int2) * std::max<i64>(1, total)));
-  if (U > 0 && nl > 0) {
-    hipLaunchKernelGGL(k_shadow_compact, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
+  if (nt > 0 && nl > 0) {
+    hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)nt), dim3(TPB), 0, ctx->stream,
                        P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist), P_<i64>(ctx->pfoff),
-                       P_<uint8_t>(ctx->flags), P_<i64>(ctx->loff), P_<int2>(ctx->L));
+                       P_<uint8_t>(ctx->flags), nf, P_<i64>(ctx->toff), P_<int2>(ctx->L));
     KLAUNCH();
   }
   if (rl > 0 && total > 0) {
@@ -1410,7 +1456,21 @@ int kano_shadow(kano_ctx* ctx, int64_t* count) {
   }
   KCHK(hipEventRecord(ctx->ev[6], ctx->stream));
   ctx->shadow_total = total;
-  if (count) *count = total;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kano_shadow(kano_ctx* ctx, int64_t* count) {
+  KTRY(ensure_built(ctx));
+  Gather ga(ctx);
+  KTRY(shadow_front(ctx, ga));
+  i64 tot[2] = {0, 0};
+  KTRY(ga.run(tot));
+  KTRY(shadow_back(ctx, tot[0], tot[1]));
+  if (count) *count = tot[1];
   return 0;
 }
 
@@ -1515,12 +1575,16 @@ int kano_conflict(kano_ctx* ctx, int* raises) {
   return 0;
 }
 
-int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, uint64_t* col_and,
-                uint64_t* col_or, uint64_t* cross, uint64_t* sys_bits, int32_t* shadow_pairs,
-                int64_t shadow_cap, int64_t* shadow_count) {
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, int32_t* idx,
+                int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                int64_t* shadow_count) {
+  if (!ctx) return -EINVAL;
+  if (!counts || (!idx && ctx->n > 0))
+    return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
   KTRY(kano_build(ctx, path));
   const i64 n = ctx->n, W = ctx->W;
-  const bool want_sys = sys_bits && sys_row >= ctx->r0 && sys_row < ctx->r1;
+  const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
+  // column checks, crosscheck (device words)
   KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
   if (W > 0) {
     hipLaunchKernelGGL(k_col_final, dim3(nblk(W)), dim3(TPB), 0, ctx->stream,
@@ -1528,43 +1592,52 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, ui
     KLAUNCH();
   }
   if (gid) KTRY(crosscheck_impl(ctx, gid));
-  int64_t total = 0;
+  // the four result rows as index lists
+  IdxRows ir{};
+  ir.W = W;
+  ir.n = n;
+  ir.nb = std::max<i64>(1, nblk(W));
+  ir.row[0] = P_<u64>(ctx->col_and);
+  ir.row[1] = P_<u64>(ctx->color);
+  ir.inv[1] = 1;
+  ir.row[2] = gid && rows_local(ctx) > 0 ? P_<u64>(ctx->cross) : nullptr;
+  ir.row[3] = have_sys ? P_<u64>(ctx->M) + (sys_row - ctx->r0) * ctx->ldM : nullptr;
+  ir.inv[3] = 1;
+  const i64 nb4 = 4 * ir.nb;
+  KTRY(scan_reserve(ctx, nb4));
+  KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * nb4));
+  KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * (nb4 + 1)));
+  KTRY(dalloc(ctx, ctx->scratch_words, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));
+  hipLaunchKernelGGL(k_idx_count, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
+                     P_<i64>(ctx->icnt));
+  KLAUNCH();
+  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->icnt), nb4, P_<i64>(ctx->ioff))));
+  int32_t* idx_dev = reinterpret_cast<int32_t*>(ctx->scratch_words.p);
+  hipLaunchKernelGGL(k_idx_write, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
+                     P_<i64>(ctx->ioff), idx_dev);
+  KLAUNCH();
+  // one sync for the list sizes (and policy_shadow's sizes)
+  Gather ga(ctx);
+  for (int r = 0; r <= 4; ++r) ga.add(P_<i64>(ctx->ioff) + r * ir.nb, true);
+  if (shadow_count) KTRY(shadow_front(ctx, ga));
+  i64 v[7] = {0, 0, 0, 0, 0, 0, 0};
+  KTRY(ga.run(v));
+  for (int r = 0; r < 4; ++r) counts[r] = v[r + 1] - v[r];
+  if (!have_sys) counts[3] = -1;
+  const i64 nidx = v[4];
+  i64 total = 0;
   if (shadow_count) {
-    KTRY(kano_shadow(ctx, &total));  // one sync (list sizes)
+    total = v[6];
+    KTRY(shadow_back(ctx, v[5], total));
+    ctx->shadow_total = total;
     *shadow_count = total;
   }
-  // every bit row through one pinned staging buffer, one final sync
-  const size_t rb = sizeof(u64) * (size_t)W, need = std::max<size_t>(16, 4 * rb);
-  if (ctx->hres_bytes < need) {
-    if (ctx->hres) KCHK(hipHostFree(ctx->hres));
-    ctx->hres = nullptr;
-    ctx->hres_bytes = 0;
-    KCHK(hipHostMalloc(&ctx->hres, need, hipHostMallocDefault));
-    ctx->hres_bytes = need;
-  }
-  char* h = static_cast<char*>(ctx->hres);
-  if (W > 0) {
-    if (col_and)
-      KCHK(hipMemcpyAsync(h, ctx->col_and.p, rb, hipMemcpyDeviceToHost, ctx->stream));
-    if (col_or)
-      KCHK(hipMemcpyAsync(h + rb, ctx->color.p, rb, hipMemcpyDeviceToHost, ctx->stream));
-    if (cross && gid)
-      KCHK(hipMemcpyAsync(h + 2 * rb, ctx->cross.p, rb, hipMemcpyDeviceToHost, ctx->stream));
-    if (want_sys)
-      KCHK(hipMemcpyAsync(h + 3 * rb, P_<u64>(ctx->M) + (sys_row - ctx->r0) * ctx->ldM, rb,
-                          hipMemcpyDeviceToHost, ctx->stream));
-  }
+  if (nidx > 0)
+    KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, ctx->stream));
   if (shadow_count && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         ctx->stream));
-  KTRY(sync(ctx));
-  if (W > 0) {
-    if (col_and) memcpy(col_and, h, rb);
-    if (col_or) memcpy(col_or, h + rb, rb);
-    if (cross && gid) memcpy(cross, h + 2 * rb, rb);
-    if (want_sys) memcpy(sys_bits, h + 3 * rb, rb);
-  }
-  return 0;
+  return sync(ctx);
 }
 
 int kano_host_alloc(size_t bytes, void** out) {

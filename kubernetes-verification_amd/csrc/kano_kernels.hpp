@@ -377,13 +377,16 @@ __global__ __launch_bounds__(TPB) void k_sel_place(const i64* __restrict__ pstar
                                                    const int32_t* __restrict__ plen,
                                                    const int32_t* __restrict__ pcls,
                                                    const i64* __restrict__ soffc, int32_t* scur,
-                                                   int32_t* __restrict__ slist) {
+                                                   int32_t* __restrict__ slist,
+                                                   int32_t* __restrict__ ecls) {
   const i64 p = blockIdx.x;
   const int32_t* L = pcls + pstart[p];
   const int32_t len = plen[p];
   for (int32_t k = threadIdx.x; k < len; k += TPB) {
     const int32_t c = L[k];
-    slist[soffc[c] + atomicAdd(&scur[c], 1)] = (int32_t)p;
+    const i64 e = soffc[c] + atomicAdd(&scur[c], 1);
+    slist[e] = (int32_t)p;
+    ecls[e] = c;
   }
 }
 
@@ -502,24 +505,25 @@ __global__ __launch_bounds__(TPB) void k_classbits(const i64* __restrict__ pstar
 }
 
 // ---- compressed matrix Mc[c] over column classes (row classes x col classes)
-// light classes: scatter of the allowed-class lists of S(c)
-__global__ __launch_bounds__(TPB) void k_mc_scatter(const i64* __restrict__ soffc, i64 U,
+// light classes: one wave per select entry (c, p) scatters p's allowed-class
+// list into row c (balanced over entries, not classes)
+__global__ __launch_bounds__(TPB) void k_mc_scatter(i64 nnz, const int32_t* __restrict__ ecls,
                                                     const int32_t* __restrict__ slist,
                                                     const i64* __restrict__ alcoff,
                                                     const int32_t* __restrict__ alc,
                                                     const int32_t* __restrict__ mcnt,
                                                     const int32_t* __restrict__ hflag,
                                                     u64* Mc, i64 ldMc) {
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const i64 e = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (c >= U || mcnt[c] == 0 || (hflag && hflag[c])) return;
-  u64* row = Mc + c * ldMc;
-  for (i64 e = soffc[c]; e < soffc[c + 1]; ++e) {
-    const int32_t p = slist[e];
-    for (i64 k = alcoff[p] + lane; k < alcoff[p + 1]; k += 64) {
-      const int32_t ca = alc[k];
-      atomicOr(&row[ca >> 6], 1ull << (ca & 63));
-    }
+  if (e >= nnz) return;
+  const int32_t c = ecls[e];
+  if (mcnt[c] == 0 || (hflag && hflag[c])) return;
+  u64* row = Mc + (i64)c * ldMc;
+  const int32_t p = slist[e];
+  for (i64 k = alcoff[p] + lane; k < alcoff[p + 1]; k += 64) {
+    const int32_t ca = alc[k];
+    atomicOr(&row[ca >> 6], 1ull << (ca & 63));
   }
 }
 
@@ -1050,58 +1054,114 @@ struct ShadowArgs {
   i64* T;
 };
 
-// one wave per row class
-__global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a) {
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= a.U) return;
-  if (a.mcnt[c] == 0) {
-    if (lane == 0) a.T[c] = 0;
-    return;
+// The candidate pairs of every row class c are (x, y) in [0, s_c)^2, laid out
+// flat at pfoff[c] (class-major, x-major).  Both kernels take SH_TILE
+// consecutive pairs per block, so the work is balanced whatever the |S(c)|
+// distribution.
+constexpr int SH_ITEMS = 8;
+constexpr i64 SH_TILE = (i64)TPB * SH_ITEMS;
+
+// last class c with pfoff[c] <= t (t < pfoff[U])
+__device__ __forceinline__ i64 class_of_pair(const i64* __restrict__ pfoff, i64 U, i64 t) {
+  i64 lo = 0, hi = U - 1;
+  while (lo < hi) {
+    const i64 mid = (lo + hi + 1) >> 1;
+    if (pfoff[mid] <= t) lo = mid; else hi = mid - 1;
   }
-  const i64 s0 = a.soffc[c];
-  const i64 s = a.soffc[c + 1] - s0;
-  const i64 ss = s * s;
-  i64 cnt = 0;
-  for (i64 t = lane; t < ss; t += 64) {
-    const i64 x = t / s, y = t - x * s;
-    uint8_t f = 0;
-    if (x != y) {
-      const int32_t j = a.slist[s0 + x], k = a.slist[s0 + y];
-      f = (j != k) && subset_of(k, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
-    }
-    a.flags[a.pfoff[c] + t] = f;
-    cnt += f;
-  }
-  cnt = wave_sum(cnt);
-  if (lane == 0) a.T[c] = cnt;
+  return lo;
 }
 
-// one wave per row class: the flagged pairs in (x, y) order
+// flags[t] = pair t is a shadow (x != y, j != k, allow_k subset of allow_j);
+// T[c] += flagged pairs of c (T zeroed); tile_cnt[b] = flagged pairs of tile b
+__global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a, i64 nflags,
+                                                    i64* __restrict__ tile_cnt) {
+  __shared__ i64 sm[4];
+  const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
+  i64 c = -1;
+  int run = 0, mine = 0;
+  if (base < nflags) {
+    c = class_of_pair(a.pfoff, a.U, base);
+    i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, p0 = a.pfoff[c], p1 = a.pfoff[c + 1];
+    bool live = a.mcnt[c] > 0;
+    u64 packed = 0;
+#pragma unroll
+    for (int k = 0; k < SH_ITEMS; ++k) {
+      const i64 t = base + k;
+      if (t >= nflags) break;
+      while (t >= p1) {
+        if (run) atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), (unsigned long long)run);
+        run = 0;
+        ++c;
+        s0 = a.soffc[c];
+        s = a.soffc[c + 1] - s0;
+        p0 = p1;
+        p1 = a.pfoff[c + 1];
+        live = a.mcnt[c] > 0;
+      }
+      const i64 q = t - p0, x = q / s, y = q - x * s;
+      int f = 0;
+      if (live && x != y) {
+        const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
+        f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+      }
+      packed |= (u64)f << (8 * k);
+      run += f;
+      mine += f;
+    }
+    if (base + SH_ITEMS <= nflags) {
+      *reinterpret_cast<u64*>(a.flags + base) = packed;
+    } else {
+      for (int k = 0; base + k < nflags; ++k) a.flags[base + k] = (uint8_t)(packed >> (8 * k));
+    }
+  }
+  // the last run: one atomic per wave when the whole wave ended in one class
+  const i64 c0 = __shfl(c, 0, 64);
+  const bool same = __all(c == c0 || c < 0);
+  if (same) {
+    const int r = wave_sum(run);
+    if ((threadIdx.x & 63) == 0 && r && c0 >= 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c0]), (unsigned long long)r);
+  } else if (run) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), (unsigned long long)run);
+  }
+  const i64 tot = block_sum((i64)mine, sm);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+// the flagged pairs in flat order: L[tile_off[b] + rank] = (j, k)
 __global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ soffc, i64 U,
                                                         const int32_t* __restrict__ slist,
                                                         const i64* __restrict__ pfoff,
                                                         const uint8_t* __restrict__ flags,
-                                                        const i64* __restrict__ loff,
+                                                        i64 nflags,
+                                                        const i64* __restrict__ tile_off,
                                                         int2* __restrict__ L) {
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= U) return;
-  i64 out = loff[c];
-  if (loff[c + 1] == out) return;
-  const i64 s0 = soffc[c];
-  const i64 s = soffc[c + 1] - s0;
-  const i64 ss = s * s;
-  for (i64 t0 = 0; t0 < ss; t0 += 64) {
-    const i64 t = t0 + lane;
-    const i64 f = (t < ss) ? flags[pfoff[c] + t] : 0;
-    i64 tot;
-    const i64 pos = out + wave_excl_scan(f, tot);
-    if (f) {
-      const i64 x = t / s, y = t - x * s;
-      L[pos] = make_int2(slist[s0 + x], slist[s0 + y]);
+  __shared__ i64 sm[4];
+  const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
+  u64 packed = 0;
+  if (base + SH_ITEMS <= nflags) {
+    packed = *reinterpret_cast<const u64*>(flags + base);
+  } else {
+    for (int k = 0; base + k < nflags; ++k) packed |= (u64)flags[base + k] << (8 * k);
+  }
+  const i64 cnt = __popcll(packed);   // flags are 0 / 1 bytes
+  i64 tot;
+  i64 pos = block_excl_scan(cnt, sm, tot) + tile_off[blockIdx.x];
+  if (cnt == 0) return;
+  i64 c = class_of_pair(pfoff, U, base);
+  i64 s0 = soffc[c], s = soffc[c + 1] - s0, p0 = pfoff[c], p1 = pfoff[c + 1];
+  for (int k = 0; k < SH_ITEMS; ++k) {
+    if (!((packed >> (8 * k)) & 1ull)) continue;
+    const i64 t = base + k;
+    while (t >= p1) {
+      ++c;
+      s0 = soffc[c];
+      s = soffc[c + 1] - s0;
+      p0 = p1;
+      p1 = pfoff[c + 1];
     }
-    out += tot;
+    const i64 q = t - p0, x = q / s, y = q - x * s;
+    L[pos++] = make_int2(slist[s0 + x], slist[s0 + y]);
   }
 }
 
@@ -1127,6 +1187,48 @@ __global__ __launch_bounds__(TPB) void k_shadow_emit(const int32_t* __restrict__
   const i64 l0 = loff[c], len = loff[c + 1] - l0;
   const i64 o = poff[i - r0];
   for (i64 k = lane; k < len; k += 64) out[o + k] = L[l0 + k];
+}
+
+// ===========================================================================
+// Bit rows -> ascending index lists (the reference's check results are lists
+// of pod indices, algorithm.py:4-55).  Up to 4 rows; a row may be inverted
+// (all_isolated, system_isolation report the zero bits).  Output rows are
+// concatenated; block b of row r writes at boff[r * nb + b].
+// ===========================================================================
+struct IdxRows {
+  const u64* row[4];
+  int32_t inv[4];
+  i64 W, n, nb;
+};
+
+__device__ __forceinline__ u64 idx_word(const IdxRows& a, int r, i64 w) {
+  if (!a.row[r] || w >= a.W) return 0ull;
+  const u64 v = a.row[r][w];
+  return (a.inv[r] ? ~v : v) & valid_mask(w, a.n);
+}
+
+__global__ __launch_bounds__(TPB) void k_idx_count(IdxRows a, i64* __restrict__ bcnt) {
+  __shared__ i64 sm[4];
+  const int r = blockIdx.y;
+  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
+  const i64 c = __popcll(idx_word(a, r, w));
+  const i64 tot = block_sum(c, sm);
+  if (threadIdx.x == 0) bcnt[r * a.nb + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(TPB) void k_idx_write(IdxRows a, const i64* __restrict__ boff,
+                                                   int32_t* __restrict__ idx) {
+  __shared__ i64 sm[4];
+  const int r = blockIdx.y;
+  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
+  u64 v = idx_word(a, r, w);
+  i64 tot;
+  i64 pos = block_excl_scan((i64)__popcll(v), sm, tot) + boff[r * a.nb + blockIdx.x];
+  while (v) {
+    const int b = __ffsll((long long)v) - 1;
+    idx[pos++] = (int32_t)(w * 64 + b);
+    v &= v - 1;
+  }
 }
 
 }  // namespace kano

@@ -98,32 +98,68 @@ __global__ __launch_bounds__(TPB) void k_scan_tiles(const Tin* __restrict__ in, 
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == TPB - 1) out[n] = pre;
 }
 
-// single-block scan for n <= SCAN_SINGLE_MAX: tiles in sequence with a carry
-constexpr i64 SCAN_SINGLE_MAX = 131072;
+// ---- single-pass scan (decoupled look-back) --------------------------------
+// status[0] is the tile ticket, status[1 + t] the published state of tile t:
+// (flag << 62) | value, flag 1 = tile aggregate, 2 = inclusive prefix.  The
+// caller alternates two status regions: each scan zeroes the other one for
+// the next scan (stream order makes that safe), so no separate memset.
+constexpr u64 LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ u64 lb_load(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(u64* p, u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename Tin, typename Tout>
-__global__ __launch_bounds__(TPB) void k_scan_single(const Tin* __restrict__ in, i64 n,
-                                                     Tout* __restrict__ out) {
+__global__ __launch_bounds__(TPB) void k_scan_lb(const Tin* __restrict__ in, i64 n,
+                                                 Tout* __restrict__ out, u64* status,
+                                                 u64* __restrict__ clear, i64 nclear) {
   __shared__ Tout sm[4];
-  Tout carry = 0;
-  for (i64 t0 = 0; t0 < n; t0 += SCAN_TILE) {
-    const i64 base = t0 + (i64)threadIdx.x * SCAN_ITEMS;
-    Tout v[SCAN_ITEMS];
-    Tout s = 0;
+  __shared__ i64 s_tile;
+  __shared__ Tout s_prefix;
+  for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < nclear; i += (i64)gridDim.x * TPB)
+    clear[i] = 0;
+  if (threadIdx.x == 0)
+    s_tile = (i64)__hip_atomic_fetch_add(status, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const i64 tile = s_tile;
+  const i64 base = tile * SCAN_TILE + (i64)threadIdx.x * SCAN_ITEMS;
+  Tout v[SCAN_ITEMS];
+  Tout s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-      v[k] = (base + k < n) ? (Tout)in[base + k] : (Tout)0;
-      s += v[k];
-    }
-    Tout tot;
-    Tout pre = block_excl_scan(s, sm, tot) + carry;
-#pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-      if (base + k < n) out[base + k] = pre;
-      pre += v[k];
-    }
-    carry += tot;
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    v[k] = (base + k < n) ? (Tout)in[base + k] : (Tout)0;
+    s += v[k];
   }
-  if (threadIdx.x == 0) out[n] = carry;
+  Tout tot;
+  Tout pre = block_excl_scan(s, sm, tot);
+  if (threadIdx.x == 0) {
+    u64* st = status + 1;
+    Tout excl = 0;
+    if (tile == 0) {
+      lb_store(&st[0], LB_INC | ((u64)tot & LB_VAL));
+    } else {
+      lb_store(&st[tile], LB_AGG | ((u64)tot & LB_VAL));
+      for (i64 q = tile - 1;; --q) {
+        u64 w;
+        do { w = lb_load(&st[q]); } while (w == 0);
+        excl += (Tout)(w & LB_VAL);
+        if ((w & ~LB_VAL) == LB_INC) break;
+      }
+      lb_store(&st[tile], LB_INC | ((u64)(excl + tot) & LB_VAL));
+    }
+    s_prefix = excl;
+  }
+  __syncthreads();
+  pre += s_prefix;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    if (base + k < n) out[base + k] = pre;
+    pre += v[k];
+  }
+  if (tile == (i64)gridDim.x - 1 && threadIdx.x == TPB - 1) out[n] = pre;
 }
 
 // several fills in one launch: (ptr, count of 32-bit words, value)
@@ -145,6 +181,20 @@ __global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
     const i64 nw = jobs.j[q].words;
     for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < nw; i += stride) p[i] = v;
   }
+}
+
+// several device scalars gathered into one buffer (one D2H copy per sync)
+constexpr int MAX_GATHER = 16;
+struct GatherJobs {
+  const void* src[MAX_GATHER];
+  int32_t wide[MAX_GATHER];   // 1: 64-bit source, 0: non-negative 32-bit source
+  int count;
+};
+__global__ void k_gather(GatherJobs g, u64* __restrict__ dst) {
+  const int k = threadIdx.x;
+  if (k < g.count)
+    dst[k] = g.wide[k] ? *static_cast<const u64*>(g.src[k])
+                       : (u64)(uint32_t)*static_cast<const int32_t*>(g.src[k]);
 }
 
 // ---- small helpers ---------------------------------------------------------

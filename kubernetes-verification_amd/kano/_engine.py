@@ -220,28 +220,40 @@ class DeviceBuild:
         return self.shadow_fetch(self.shadow_count())
 
     def verify(self, gid: Optional[np.ndarray] = None, sys_row: int = 0, shadow: bool = True,
-               pairs: Optional[np.ndarray] = None, path: Optional[str] = None) -> dict:
-        """kano_verify: build + every check in one call (four host syncs).
+               pairs: Optional[np.ndarray] = None, idx: Optional[np.ndarray] = None,
+               path: Optional[str] = None) -> dict:
+        """kano_verify: build + every check in one call (three host syncs).
 
-        Returns the bit rows (``col_and``, ``col_or``, ``cross``, ``sys``) as
-        uint64 words and, with ``shadow``, ``shadow_count`` plus ``pairs``
-        (an (count, 2) int32 view of the given buffer when it is large enough,
-        else a fresh array fetched afterwards)."""
-        W = self.W
-        words = np.zeros((4, max(W, 1)), dtype=np.uint64)
+        Returns the reference's result lists as int32 index arrays
+        (``all_reachable``, ``all_isolated``, ``user_crosscheck`` (None without
+        gid), ``system_isolation`` (None when sys_row is not in this shard))
+        and, with ``shadow``, ``shadow_count`` plus ``pairs`` (a (count, 2)
+        view of the given buffer when it is large enough, else fetched
+        afterwards).  ``idx`` (>= 4*n int32, e.g. pinned) receives the lists."""
+        n = self.n
+        if idx is None:
+            idx = np.empty(max(4 * n, 1), dtype=np.int32)
+        elif idx.size < 4 * n:
+            raise ValueError("idx buffer needs 4*n entries")
         if gid is not None:
             gid = np.ascontiguousarray(gid, dtype=np.int32)
-            if gid.shape[0] != self.n:
+            if gid.shape[0] != n:
                 raise ValueError("gid must have one entry per pod")
+        counts = np.zeros(4, dtype=np.int64)
         cnt = c_int64(0)
         cap = 0 if pairs is None else pairs.size // 2
         pth = nat.PATHS[path or self.path]
         self._chk(self.lib.kano_verify(
-            self.ctx, pth, _ptr(gid), int(sys_row), _ptr(words[0]), _ptr(words[1]),
-            _ptr(words[2]), _ptr(words[3]), _ptr(pairs), int(cap),
-            byref(cnt) if shadow else None), "kano_verify")
-        out = {"col_and": words[0, :W], "col_or": words[1, :W],
-               "cross": words[2, :W] if gid is not None else None, "sys": words[3, :W]}
+            self.ctx, pth, _ptr(gid), int(sys_row), _ptr(idx), _ptr(counts), _ptr(pairs),
+            int(cap), byref(cnt) if shadow else None), "kano_verify")
+        out, o = {}, 0
+        for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
+                                  "system_isolation")):
+            k = int(counts[r])
+            out[name] = idx[o:o + k] if k >= 0 else None
+            o += max(k, 0)
+        if gid is None:
+            out["user_crosscheck"] = None
         if shadow:
             k = int(cnt.value)
             out["shadow_count"] = k

@@ -166,10 +166,9 @@ def test_c2_engine_vs_kano_py():
 @pytest.mark.parametrize("cap", [0, 1 << 22])
 def test_verify_fused_c2(cap):
     """kano_verify (build + every check in one call, the bench's step) gives
-    the same answers as kano_py on C2; cap=0 exercises the late fetch."""
+    kano_py's result lists on C2; cap=0 exercises the late pair fetch."""
     from kano._engine import DeviceBuild, PinnedBuffer
     from kano._intern import tables_from_cluster
-    from kano._bits import set_bit_indices, words_to_bool
     from kano.synth import make_config, KEY_NAMES
     exp = expected("C2")
     cl = make_config("C2")
@@ -181,20 +180,41 @@ def test_verify_fused_c2(cap):
         r = eng.verify(gid, sys_row=0, shadow=True,
                        pairs=pin.view(np.int32, 2 * cap) if cap else None)
         assert sha(eng.rows(0, n)) == exp["M_sha256"]
-        assert set_bit_indices(r["col_and"], n).tolist() == exp["all_reachable"]
-        assert np.flatnonzero(~words_to_bool(r["col_or"], n)).tolist() == exp["all_isolated"]
-        assert set_bit_indices(r["cross"], n).tolist() == exp["user_crosscheck"]["result"]
-        assert (np.flatnonzero(~words_to_bool(r["sys"], n)).tolist()
-                == exp["system_isolation"]["result"])
+        assert r["all_reachable"].tolist() == exp["all_reachable"]
+        assert r["all_isolated"].tolist() == exp["all_isolated"]
+        assert r["user_crosscheck"].tolist() == exp["user_crosscheck"]["result"]
+        assert r["system_isolation"].tolist() == exp["system_isolation"]["result"]
         assert r["shadow_count"] == exp["policy_shadow"]["count"]
         assert sha(np.ascontiguousarray(r["pairs"])) == exp["policy_shadow"]["sha256"]
     eng.close()
     pin.close()
 
 
+@pytest.mark.parametrize("name", ["paper_example", "q_dirs", "s_broad_300"])
+def test_verify_fused_golden(name):
+    """kano_verify without a group label and without policy_shadow."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern
+    if name == "paper_example":
+        from sample import paper_example
+        cs, ps = paper_example()
+    else:
+        cs, ps = api_objects(cluster(name))
+    exp = expected(name)
+    eng = DeviceBuild(intern(cs, ps), build=False)
+    r = eng.verify(None, sys_row=0, shadow=False)
+    assert r["all_reachable"].tolist() == exp["all_reachable"]
+    assert r["all_isolated"].tolist() == exp["all_isolated"]
+    assert r["user_crosscheck"] is None and "pairs" not in r
+    if len(cs):
+        assert r["system_isolation"].tolist() == exp["system_isolation"]["result"]
+    eng.close()
+
+
 def test_verify_fused_shards():
     """kano_verify on row shards: per-shard pairs concatenate to the full
-    list, the system row comes only from its owner."""
+    list, per-shard crosscheck lists union to the full one, the system row
+    comes only from its owner."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids
     from oracle import kano_oracle as orc
@@ -204,18 +224,22 @@ def test_verify_fused_shards():
     n = len(cs)
     ref = orc.run_c(obj, label=obj["label"])
     gid = group_ids(cs, obj["label"])
-    pairs, cross = [], []
+    pairs, cross = [], set()
     for r0, r1 in [(0, 700), (700, n)]:
         e = DeviceBuild(t, rows=(r0, r1), build=False)
         r = e.verify(gid, sys_row=5, shadow=True)
         pairs.append(r["pairs"])
-        cross.append(r["cross"])
-        sys_row = e.rows(5, 1)[0] if r0 <= 5 < r1 else np.zeros_like(r["sys"])
-        assert np.array_equal(r["sys"], sys_row)
+        cross |= set(r["user_crosscheck"].tolist())
+        if r0 <= 5 < r1:
+            from kano._bits import words_to_bool
+            row = e.rows(5, 1)[0]
+            assert r["system_isolation"].tolist() == np.flatnonzero(
+                ~words_to_bool(row, n)).tolist()
+        else:
+            assert r["system_isolation"] is None
         e.close()
     assert np.array_equal(np.concatenate(pairs), ref["shadow"])
-    from kano._bits import set_bit_indices
-    assert set_bit_indices(np.bitwise_or.reduce(cross), n).tolist() == ref["user_crosscheck"]
+    assert sorted(cross) == ref["user_crosscheck"]
 
 
 def test_row_shards_combine_to_full():
