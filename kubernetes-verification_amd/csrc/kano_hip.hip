@@ -104,10 +104,15 @@ struct kano_ctx {
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
-  DBuf gdev, icnt, ioff;     // gathered scalars, index-list block counts / offsets
+  DBuf gdev, icnt, ioff, sysrow;     // gathered scalars, index-list block counts / offsets
   u64* ghost = nullptr;      // pinned landing buffer for gathered scalars
 
   hipEvent_t ev[10] = {};
+  // the matrix write (k_rows) runs on its own stream beside the checks, which
+  // only need class-level data; ev_rows marks its end
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_rows = nullptr;
+  bool rows_pending = false;
 };
 
 namespace {
@@ -716,9 +721,12 @@ int do_rows(kano_ctx* ctx) {
     KCHK(hipMemsetAsync(ctx->colnand.p, 0, sizeof(u64) * ldM, ctx->stream));
   }
   if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
+  KCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
+  KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+  ctx->rows_pending = true;
   if (ctx->heavy_count > 0) {
     hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), (unsigned)ctx->heavy_count), dim3(TPB),
-                       0, ctx->stream, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ctx->ldC,
+                       0, ctx->stream2, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ctx->ldC,
                        P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
@@ -745,11 +753,12 @@ int do_rows(kano_ctx* ctx) {
   a.cww = cww;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
-  KCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+  KCHK(hipEventRecord(ctx->ev[7], ctx->stream2));
   hipLaunchKernelGGL(k_rows, dim3((unsigned)ctx->wi_total, ncc), dim3(TPB), sizeof(u64) * cww,
-                     ctx->stream, a);
+                     ctx->stream2, a);
   KLAUNCH();
-  KCHK(hipEventRecord(ctx->ev[8], ctx->stream));
+  KCHK(hipEventRecord(ctx->ev[8], ctx->stream2));
+  KCHK(hipEventRecord(ctx->ev_rows, ctx->stream2));
   ctx->rows_timed = true;
   return 0;
 }
@@ -761,10 +770,18 @@ int ensure_built(kano_ctx* ctx) {
   return 0;
 }
 
+// order the main stream after the matrix write
+int join_rows(kano_ctx* ctx) {
+  if (!ctx->rows_pending) return 0;
+  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows, 0));
+  ctx->rows_pending = false;
+  return 0;
+}
+
 int ensure_matrix(kano_ctx* ctx) {
   KTRY(ensure_built(ctx));
   if (ctx->lists_mode) return fail(ctx, -EINVAL, "context holds policy lists, not a matrix");
-  return 0;
+  return join_rows(ctx);
 }
 
 // identity "classes" over the local rows (after an edit of M): row r is its
@@ -932,6 +949,12 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess) {
+    kano_destroy(ctx);
+    return -EIO;
+  }
   if (hipHostMalloc(reinterpret_cast<void**>(&ctx->ghost), sizeof(u64) * MAX_GATHER,
                     hipHostMallocDefault) != hipSuccess) {
     kano_destroy(ctx);
@@ -945,6 +968,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
@@ -967,11 +991,15 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
-                  &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff};
+                  &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff,
+                  &ctx->sysrow};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
   delete ctx;
 }
 
@@ -980,6 +1008,8 @@ const char* kano_last_error(const kano_ctx* ctx) { return ctx ? ctx->err.c_str()
 int kano_set_stream(kano_ctx* ctx, void* s) {
   if (!ctx) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
+  KCHK(hipStreamSynchronize(ctx->stream2));
+  ctx->rows_pending = false;
   if (ctx->own_stream && ctx->stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -1166,6 +1196,7 @@ int kano_build(kano_ctx* ctx, int path) {
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
   KCHK(hipSetDevice(ctx->device));
+  KTRY(join_rows(ctx));  // the previous matrix write still reads the class lists
   ctx->built = false;
   ctx->lists_mode = false;
   ctx->rows_timed = false;
@@ -1601,7 +1632,14 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, in
   ir.row[1] = P_<u64>(ctx->color);
   ir.inv[1] = 1;
   ir.row[2] = gid && rows_local(ctx) > 0 ? P_<u64>(ctx->cross) : nullptr;
-  ir.row[3] = have_sys ? P_<u64>(ctx->M) + (sys_row - ctx->r0) * ctx->ldM : nullptr;
+  if (have_sys && W > 0) {
+    KTRY(dalloc(ctx, ctx->sysrow, sizeof(u64) * ctx->ldM));
+    hipLaunchKernelGGL(k_row_from_mc, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->Mc), ctx->ldC, P_<int32_t>(ctx->rc.cls), (i64)sys_row,
+                       P_<int32_t>(ctx->cc.cls), n, W, P_<u64>(ctx->sysrow));
+    KLAUNCH();
+  }
+  ir.row[3] = have_sys ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   const i64 nb4 = 4 * ir.nb;
   KTRY(scan_reserve(ctx, nb4));
@@ -1637,6 +1675,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, in
   if (shadow_count && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         ctx->stream));
+  KTRY(join_rows(ctx));  // the matrix is part of the result
   return sync(ctx);
 }
 
@@ -1654,6 +1693,7 @@ void kano_host_free(void* p) {
 int kano_stage_times(kano_ctx* ctx, float* ms) {
   if (!ctx || !ms) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
+  KTRY(join_rows(ctx));
   KTRY(sync(ctx));
   for (int k = 0; k < 8; ++k) ms[k] = 0.f;
   if (ctx->built && !ctx->lists_mode) {

@@ -578,6 +578,24 @@ __global__ __launch_bounds__(TPB) void k_cols_expand(const u64* __restrict__ col
   }
 }
 
+// row `row` of M straight from Mc: bit j = Mc[cls(row)] bit cla[j]
+// (system_isolation without waiting for the matrix write)
+__global__ __launch_bounds__(TPB) void k_row_from_mc(const u64* __restrict__ Mc, i64 ldMc,
+                                                     const int32_t* __restrict__ clr, i64 row,
+                                                     const int32_t* __restrict__ cla, i64 n,
+                                                     i64 W, u64* __restrict__ out) {
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (((j >> 6) << 6) >= W * 64) return;
+  const u64* mr = Mc + (i64)clr[row] * ldMc;
+  bool b = false;
+  if (j < n) {
+    const int32_t ca = cla[j];
+    b = (mr[ca >> 6] >> (ca & 63)) & 1ull;
+  }
+  const u64 bal = __ballot(b);
+  if ((threadIdx.x & 63) == 0) out[j >> 6] = bal;
+}
+
 // user_crosscheck at class level (kano_py/kano/algorithm.py:27-42).  Group
 // range of the local members of every row class:
 __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restrict__ gid,
