@@ -709,8 +709,7 @@ int do_back(kano_ctx* ctx, int path) {
 
 // heavy rows expanded from Mc into the first member's row; then the rows
 int do_rows(kano_ctx* ctx) {
-  const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
-  const i64 rl = rows_local(ctx);
+  const i64 ldM = ctx->ldM, n = ctx->n;
   if (n > 0) {
     hipLaunchKernelGGL(k_cols_expand, dim3(nblk(ldM * 64)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->col_or_c), P_<u64>(ctx->col_nand_c), P_<int32_t>(ctx->cc.cls),
@@ -720,6 +719,13 @@ int do_rows(kano_ctx* ctx) {
     KCHK(hipMemsetAsync(ctx->color.p, 0, sizeof(u64) * ldM, ctx->stream));
     KCHK(hipMemsetAsync(ctx->colnand.p, 0, sizeof(u64) * ldM, ctx->stream));
   }
+  return 0;
+}
+
+// the matrix write (heavy rows from Mc, then k_rows) on stream2
+int launch_rows(kano_ctx* ctx) {
+  const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
+  const i64 rl = rows_local(ctx);
   if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
   KCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
   KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
@@ -1191,7 +1197,10 @@ int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end) {
   return 0;
 }
 
-int kano_build(kano_ctx* ctx, int path) {
+}  // extern "C"
+
+namespace {
+int build_impl(kano_ctx* ctx, int path, bool rows_now) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
@@ -1214,11 +1223,18 @@ int kano_build(kano_ctx* ctx, int path) {
   KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   KTRY(do_back(ctx, path));
   KTRY(do_rows(ctx));
+  if (rows_now) KTRY(launch_rows(ctx));
   KCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->cols_valid = true;
   ctx->built = true;
   return 0;
 }
+
+}  // namespace
+
+extern "C" {
+
+int kano_build(kano_ctx* ctx, int path) { return build_impl(ctx, path, true); }
 
 int kano_info(kano_ctx* ctx, int64_t* out) {
   if (!ctx || !out) return -EINVAL;
@@ -1612,7 +1628,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, in
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
-  KTRY(kano_build(ctx, path));
+  KTRY(build_impl(ctx, path, false));
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   // column checks, crosscheck (device words)
@@ -1623,6 +1639,9 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, in
     KLAUNCH();
   }
   if (gid) KTRY(crosscheck_impl(ctx, gid));
+  // the matrix write now runs beside the latency-bound rest (index lists,
+  // policy_shadow); the bandwidth-heavy class-level crosscheck went first
+  KTRY(launch_rows(ctx));
   // the four result rows as index lists
   IdxRows ir{};
   ir.W = W;
