@@ -94,7 +94,7 @@ struct kano_ctx {
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
 
   DBuf pv;
-  DBuf scnt, cost, soffc, scur, slist, ecls, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
+  DBuf scnt, cost, soffc, scur, slist, ecls, wicls, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
   DBuf ACT, AC, nca, acnt, alcoff, alc, aloff, alist;
   DBuf M, Mc, color, colnand, col_and, col_or_c, col_nand_c;
   DBuf scan_tmp;
@@ -605,6 +605,7 @@ int do_back(kano_ctx* ctx, int path) {
     KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
     KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
     KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, H)));
+    KTRY(dalloc(ctx, ctx->wicls, sizeof(int32_t) * std::max<i64>(1, ctx->wi_total)));
     KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
     KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
     KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
@@ -640,7 +641,8 @@ int do_back(kano_ctx* ctx, int path) {
       }
     }
     hipLaunchKernelGGL(k_flag_list, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), U, P_<int32_t>(ctx->hlist));
+                       P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), U, P_<int32_t>(ctx->hlist),
+                       P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls));
     KLAUNCH();
   }
   if (P > 0 && ctx->cc.U > 0) {
@@ -741,6 +743,7 @@ int launch_rows(kano_ctx* ctx) {
   const unsigned ncc = (unsigned)((ldM + cww - 1) / cww);
   RowsArgs a{};
   a.wioff = P_<int32_t>(ctx->wioff);
+  a.wicls = P_<int32_t>(ctx->wicls);
   a.U = U;
   a.soffc = P_<i64>(ctx->soffc);
   a.slist = P_<int32_t>(ctx->slist);
@@ -821,6 +824,7 @@ int recompute_cols(kano_ctx* ctx) {
   const int cww = (int)std::min<i64>(ldM, MAX_CWW);
   RowsArgs a{};
   a.wioff = moff;  // one work item per row
+  a.wicls = moff;  // identity
   a.U = rl;
   a.moff = moff;
   a.mem = mem;
@@ -998,7 +1002,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow};
+                  &ctx->sysrow, &ctx->wicls};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);

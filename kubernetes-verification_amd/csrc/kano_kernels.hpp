@@ -691,11 +691,17 @@ __global__ __launch_bounds__(TPB) void k_sq_from_off(const i64* __restrict__ off
   if (c < U) sq[c] = (off[c + 1] - off[c]) * (off[c + 1] - off[c]);
 }
 
+// heavy list, and the owner class of every k_rows work item (so k_rows does
+// not binary-search wioff)
 __global__ __launch_bounds__(TPB) void k_flag_list(const int32_t* __restrict__ flag,
                                                    const int32_t* __restrict__ off, i64 U,
-                                                   int32_t* __restrict__ list) {
+                                                   int32_t* __restrict__ list,
+                                                   const int32_t* __restrict__ wioff,
+                                                   int32_t* __restrict__ wicls) {
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c < U && flag[c]) list[off[c]] = (int32_t)c;
+  if (c >= U) return;
+  if (flag[c]) list[off[c]] = (int32_t)c;
+  for (int32_t w = wioff[c]; w < wioff[c + 1]; ++w) wicls[w] = (int32_t)c;
 }
 
 // ===========================================================================
@@ -826,6 +832,7 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict_
 // ===========================================================================
 struct RowsArgs {
   const int32_t* wioff;  // U+1
+  const int32_t* wicls;  // work item -> class (nullable: binary search in wioff)
   i64 U;
   const i64* soffc;      // U+1
   const int32_t* slist;
@@ -848,7 +855,7 @@ struct RowsArgs {
 __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
   const i64 b = blockIdx.x;
-  const i64 c = upper_bound_i32(a.wioff, a.U + 1, b) - 1;
+  const i64 c = a.wicls ? (i64)a.wicls[b] : upper_bound_i32(a.wioff, a.U + 1, b) - 1;
   if (c < 0 || c >= a.U) return;
   const i64 chunk = b - a.wioff[c];
   const i64 base = (i64)blockIdx.y * a.cww;
@@ -1079,9 +1086,9 @@ struct ShadowArgs {
 constexpr int SH_ITEMS = 8;
 constexpr i64 SH_TILE = (i64)TPB * SH_ITEMS;
 
-// last class c with pfoff[c] <= t (t < pfoff[U])
-__device__ __forceinline__ i64 class_of_pair(const i64* __restrict__ pfoff, i64 U, i64 t) {
-  i64 lo = 0, hi = U - 1;
+// last class c in [lo, hi] with pfoff[c] <= t
+__device__ __forceinline__ i64 class_of_pair(const i64* __restrict__ pfoff, i64 lo, i64 hi,
+                                             i64 t) {
   while (lo < hi) {
     const i64 mid = (lo + hi + 1) >> 1;
     if (pfoff[mid] <= t) lo = mid; else hi = mid - 1;
@@ -1089,16 +1096,29 @@ __device__ __forceinline__ i64 class_of_pair(const i64* __restrict__ pfoff, i64 
   return lo;
 }
 
+// the class range of this block's tile: two searches over all classes, by
+// two waves, then every thread searches only inside the range
+__device__ __forceinline__ void tile_class_range(const i64* __restrict__ pfoff, i64 U,
+                                                 i64 nflags, i64* s_rng) {
+  const i64 b0 = (i64)blockIdx.x * SH_TILE;
+  const i64 b1 = min(b0 + SH_TILE, nflags) - 1;
+  if (threadIdx.x == 0) s_rng[0] = class_of_pair(pfoff, 0, U - 1, b0);
+  if (threadIdx.x == 64) s_rng[1] = class_of_pair(pfoff, 0, U - 1, b1);
+  __syncthreads();
+}
+
 // flags[t] = pair t is a shadow (x != y, j != k, allow_k subset of allow_j);
 // T[c] += flagged pairs of c (T zeroed); tile_cnt[b] = flagged pairs of tile b
 __global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a, i64 nflags,
                                                     i64* __restrict__ tile_cnt) {
   __shared__ i64 sm[4];
+  __shared__ i64 rng[2];
+  tile_class_range(a.pfoff, a.U, nflags, rng);
   const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
   i64 c = -1;
   int run = 0, mine = 0;
   if (base < nflags) {
-    c = class_of_pair(a.pfoff, a.U, base);
+    c = class_of_pair(a.pfoff, rng[0], rng[1], base);
     i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, p0 = a.pfoff[c], p1 = a.pfoff[c + 1];
     bool live = a.mcnt[c] > 0;
     u64 packed = 0;
@@ -1155,6 +1175,8 @@ __global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ 
                                                         const i64* __restrict__ tile_off,
                                                         int2* __restrict__ L) {
   __shared__ i64 sm[4];
+  __shared__ i64 rng[2];
+  tile_class_range(pfoff, U, nflags, rng);
   const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
   u64 packed = 0;
   if (base + SH_ITEMS <= nflags) {
@@ -1166,7 +1188,7 @@ __global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ 
   i64 tot;
   i64 pos = block_excl_scan(cnt, sm, tot) + tile_off[blockIdx.x];
   if (cnt == 0) return;
-  i64 c = class_of_pair(pfoff, U, base);
+  i64 c = class_of_pair(pfoff, rng[0], rng[1], base);
   i64 s0 = soffc[c], s = soffc[c + 1] - s0, p0 = pfoff[c], p1 = pfoff[c + 1];
   for (int k = 0; k < SH_ITEMS; ++k) {
     if (!((packed >> (8 * k)) & 1ull)) continue;
