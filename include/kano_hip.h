@@ -149,15 +149,17 @@ int kano_conflict(kano_ctx* ctx, int* raises);
  * reference's return values: ascending pod-index lists, concatenated in idx
  * (capacity 4*n) with counts[4] =
  *   [all_reachable (algorithm.py:4-9), all_isolated (:12-17),
- *    user_crosscheck for the group ids gid (:20-42; 0 when gid is NULL),
+ *    user_crosscheck for the group ids gid (:20-42; 0 when gid is NULL;
+ *    ngroups > 0 declares every gid < ngroups, checked on the device, so the
+ *    host does not scan gid; ngroups <= 0 scans it),
  *    system_isolation(sys_row) (:45-55; -1 when sys_row is not in this shard)].
  * On a row shard the column lists cover only this shard's rows (combine
  * with kano_col_flags_dev / kano_crosscheck_dev across shards instead).
  * When shadow_count is non-NULL, policy_shadow runs too (kano_shadow) and
  * the pairs are copied to shadow_pairs if count <= shadow_cap (otherwise
  * fetch them with kano_shadow_fetch). */
-int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, int32_t* idx,
-                int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count);
 
 /* Timing of the last kano_build / kano_shadow stages on the context stream

@@ -104,7 +104,7 @@ struct kano_ctx {
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
-  DBuf gdev, icnt, ioff, sysrow;     // gathered scalars, index-list block counts / offsets
+  DBuf gdev, icnt, ioff, sysrow, err_dev;     // gathered scalars, index-list block counts / offsets
   u64* ghost = nullptr;      // pinned landing buffer for gathered scalars
 
   hipEvent_t ev[10] = {};
@@ -846,17 +846,23 @@ int recompute_cols(kano_ctx* ctx) {
   return 0;
 }
 
-int crosscheck_impl(kano_ctx* ctx, const int32_t* gid) {
+// ngroups > 0: the caller declares every gid in [0, ngroups) (no host scan;
+// the kernels flag a violation in ctx->err_dev); ngroups <= 0: scanned here
+int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
+  KTRY(dalloc(ctx, ctx->err_dev, 16));
   if (n == 0 || rows_local(ctx) == 0 || W == 0 || ctx->rows_dirty)
     KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
-  int32_t G = 0;
-  for (i64 i = 0; i < n; ++i) {
-    if (gid[i] < 0) return fail(ctx, -EINVAL, "kano_crosscheck: negative group id");
-    G = std::max(G, gid[i] + 1);
+  int32_t G = ngroups;
+  if (G <= 0) {
+    G = 0;
+    for (i64 i = 0; i < n; ++i) {
+      if (gid[i] < 0) return fail(ctx, -EINVAL, "kano_crosscheck: negative group id");
+      G = std::max(G, gid[i] + 1);
+    }
   }
   KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
 
@@ -864,35 +870,28 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid) {
     // class level: rows of a row class are equal, columns of a column class
     // are equal; everything runs on Mc (U_r x U_a bits)
     const i64 U = ctx->rc.U, ldC = ctx->ldC, UAW = ctx->UAW;
-    KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
-    KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->R, sizeof(u64) * (i64)G * ldC));
     KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
     FillBatch fb(ctx);
+    KTRY(fb.add(ctx->err_dev, 16, 0u));
     KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
-    KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
-    KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
     KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
     for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
     KTRY(fb.run());
-    const i64 rl = rows_local(ctx);
-    hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->gid), P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
-                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax));
-    KLAUNCH();
     hipLaunchKernelGGL(k_cross_mc, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
-                       P_<int32_t>(ctx->gmax), P_<u64>(ctx->R), P_<u64>(ctx->multi));
+                       P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.moff),
+                       P_<int32_t>(ctx->rc.mem), P_<int32_t>(ctx->gid), G, P_<u64>(ctx->R),
+                       P_<u64>(ctx->multi), P_<int32_t>(ctx->err_dev));
     KLAUNCH();
     hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
     KLAUNCH();
     hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->gid), P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R), ldC,
-                       P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
-                       P_<u64>(ctx->cross));
+                       P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
+                       ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
+                       P_<u64>(ctx->cross), P_<int32_t>(ctx->err_dev));
     KLAUNCH();
     return 0;
   }
@@ -1002,7 +1001,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow, &ctx->wicls};
+                  &ctx->sysrow, &ctx->wicls,   &ctx->err_dev};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1626,8 +1625,8 @@ int kano_conflict(kano_ctx* ctx, int* raises) {
   return 0;
 }
 
-int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, int32_t* idx,
-                int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count) {
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
@@ -1642,7 +1641,8 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, in
                        P_<u64>(ctx->colnand), W, n, P_<u64>(ctx->col_and));
     KLAUNCH();
   }
-  if (gid) KTRY(crosscheck_impl(ctx, gid));
+  const bool cross_on = gid && n > 0 && rows_local(ctx) > 0 && W > 0;
+  if (gid) KTRY(crosscheck_impl(ctx, gid, ngroups));
   // the matrix write now runs beside the latency-bound rest (index lists,
   // policy_shadow); the bandwidth-heavy class-level crosscheck went first
   KTRY(launch_rows(ctx));
@@ -1680,16 +1680,20 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int64_t sys_row, in
   // one sync for the list sizes (and policy_shadow's sizes)
   Gather ga(ctx);
   for (int r = 0; r <= 4; ++r) ga.add(P_<i64>(ctx->ioff) + r * ir.nb, true);
+  const int ishadow = 5, ierr = shadow_count ? 7 : 5;
   if (shadow_count) KTRY(shadow_front(ctx, ga));
-  i64 v[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (cross_on) ga.add(P_<int32_t>(ctx->err_dev), false);
+  i64 v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   KTRY(ga.run(v));
+  if (cross_on && v[ierr])
+    return fail(ctx, -EINVAL, "kano_verify: a group id lies outside [0, ngroups)");
   for (int r = 0; r < 4; ++r) counts[r] = v[r + 1] - v[r];
   if (!have_sys) counts[3] = -1;
   const i64 nidx = v[4];
   i64 total = 0;
   if (shadow_count) {
-    total = v[6];
-    KTRY(shadow_back(ctx, v[5], total));
+    total = v[ishadow + 1];
+    KTRY(shadow_back(ctx, v[ishadow], total));
     ctx->shadow_total = total;
     *shadow_count = total;
   }

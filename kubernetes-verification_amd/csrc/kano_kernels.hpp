@@ -608,39 +608,62 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
   atomicMax(&gmax[c], g);
 }
 
-// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per class)
+// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise; one wave
+// per class, the group range of the class's local members found by the wave.
+// An atomic is issued only for bits the (possibly stale) target word lacks:
+// big groups saturate R[g] early, and bits are only ever set.
 __global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
-                                                  i64 U, const int32_t* __restrict__ mcnt,
-                                                  const int32_t* __restrict__ gmin,
-                                                  const int32_t* __restrict__ gmax, u64* R,
-                                                  u64* multi) {
+                                                  i64 U, const int32_t* __restrict__ moff,
+                                                  const int32_t* __restrict__ mem,
+                                                  const int32_t* __restrict__ gid, int32_t G,
+                                                  u64* R, u64* multi, int32_t* err) {
   const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (c >= U || mcnt[c] == 0) return;
-  const int32_t g = gmin[c];
-  u64* dst = (g == gmax[c]) ? R + (i64)g * ldMc : multi;
+  if (c >= U) return;
+  const int32_t m0 = moff[c], m1 = moff[c + 1];
+  if (m1 == m0) return;
+  int32_t gmin = INT32_MAX, gmax = -1;
+  for (int32_t m = m0 + lane; m < m1; m += 64) {
+    const int32_t g = gid[mem[m]];
+    gmin = min(gmin, g);
+    gmax = max(gmax, g);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    gmin = min(gmin, __shfl_xor(gmin, d, 64));
+    gmax = max(gmax, __shfl_xor(gmax, d, 64));
+  }
+  if (gmin < 0 || gmax >= G) {   // caller-declared group count violated
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
+  u64* dst = (gmin == gmax) ? R + (i64)gmin * ldMc : multi;
+  const u64* src = Mc + c * ldMc;
   for (i64 w = lane; w < UW; w += 64) {
-    const u64 v = Mc[c * ldMc + w];
-    if (v) atomicOr(&dst[w], v);
+    const u64 v = src[w];
+    if (v & ~__hip_atomic_load(&dst[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicOr(&dst[w], v);
   }
 }
 
 // cross[j] = MULTI(ca) | A2(ca) | (A1(ca) & ~R[g(j)](ca)),  ca = cla[j]
-__global__ __launch_bounds__(TPB) void k_cross_pod(const int32_t* __restrict__ gid,
+__global__ __launch_bounds__(TPB) void k_cross_pod(const int32_t* __restrict__ gid, int32_t G,
                                                    const int32_t* __restrict__ cla, i64 n,
                                                    const u64* __restrict__ R, i64 ldMc,
                                                    const u64* __restrict__ multi,
                                                    const u64* __restrict__ A1,
                                                    const u64* __restrict__ A2, i64 W,
-                                                   u64* __restrict__ cross) {
+                                                   u64* __restrict__ cross, int32_t* err) {
   const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
   if (((j >> 6) << 6) >= W * 64) return;
   bool bit = false;
   if (j < n) {
-    const int32_t ca = cla[j];
+    const int32_t ca = cla[j], g = gid[j];
     const i64 cw = ca >> 6;
     const u64 m = 1ull << (ca & 63);
-    const bool own = (R[(i64)gid[j] * ldMc + cw] & m) != 0;
+    bool own = false;
+    if (g < 0 || g >= G) atomicOr(err, 1);
+    else own = (R[(i64)g * ldMc + cw] & m) != 0;
     bit = ((multi[cw] | A2[cw]) & m) || ((A1[cw] & m) && !own);
   }
   const u64 bal = __ballot(bit);

@@ -221,7 +221,7 @@ class DeviceBuild:
 
     def verify(self, gid: Optional[np.ndarray] = None, sys_row: int = 0, shadow: bool = True,
                pairs: Optional[np.ndarray] = None, idx: Optional[np.ndarray] = None,
-               path: Optional[str] = None) -> dict:
+               ngroups: int = 0, path: Optional[str] = None) -> dict:
         """kano_verify: build + every check in one call (three host syncs).
 
         Returns the reference's result lists as int32 index arrays
@@ -229,14 +229,17 @@ class DeviceBuild:
         gid), ``system_isolation`` (None when sys_row is not in this shard))
         and, with ``shadow``, ``shadow_count`` plus ``pairs`` (a (count, 2)
         view of the given buffer when it is large enough, else fetched
-        afterwards).  ``idx`` (>= 4*n int32, e.g. pinned) receives the lists."""
+        afterwards).  ``idx`` (>= 4*n int32, e.g. pinned) receives the lists.
+        ``ngroups`` > 0 declares ``gid < ngroups`` (checked on the device)."""
         n = self.n
         if idx is None:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
         elif idx.size < 4 * n:
             raise ValueError("idx buffer needs 4*n entries")
         if gid is not None:
-            gid = np.ascontiguousarray(gid, dtype=np.int32)
+            if not (isinstance(gid, np.ndarray) and gid.dtype == np.int32
+                    and gid.flags.c_contiguous):
+                gid = np.ascontiguousarray(gid, dtype=np.int32)
             if gid.shape[0] != n:
                 raise ValueError("gid must have one entry per pod")
         counts = np.zeros(4, dtype=np.int64)
@@ -244,7 +247,8 @@ class DeviceBuild:
         cap = 0 if pairs is None else pairs.size // 2
         pth = nat.PATHS[path or self.path]
         self._chk(self.lib.kano_verify(
-            self.ctx, pth, _ptr(gid), int(sys_row), _ptr(idx), _ptr(counts), _ptr(pairs),
+            self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), _ptr(idx), _ptr(counts),
+            _ptr(pairs),
             int(cap), byref(cnt) if shadow else None), "kano_verify")
         out, o = {}, 0
         for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",

@@ -46,8 +46,8 @@ SIGNATURES = {
     "kano_shadow_lists": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
                                   c_void_p, POINTER(c_int64)]),
     "kano_conflict": (c_int, [c_void_p, POINTER(c_int)]),
-    "kano_verify": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
-                            c_int64, POINTER(c_int64)]),
+    "kano_verify": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_void_p, c_void_p,
+                            c_void_p, c_int64, POINTER(c_int64)]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),

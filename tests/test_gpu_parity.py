@@ -176,8 +176,8 @@ def test_verify_fused_c2(cap):
     _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
     eng = DeviceBuild(tables_from_cluster(cl), build=False)
     pin = PinnedBuffer(max(cap, 1) * 8)
-    for _ in range(2):   # a rebuild in the same context must not change anything
-        r = eng.verify(gid, sys_row=0, shadow=True,
+    for ng in (0, int(gid.max()) + 1):   # host-scanned / declared group count
+        r = eng.verify(gid, sys_row=0, shadow=True, ngroups=ng,
                        pairs=pin.view(np.int32, 2 * cap) if cap else None)
         assert sha(eng.rows(0, n)) == exp["M_sha256"]
         assert r["all_reachable"].tolist() == exp["all_reachable"]
@@ -188,6 +188,22 @@ def test_verify_fused_c2(cap):
         assert sha(np.ascontiguousarray(r["pairs"])) == exp["policy_shadow"]["sha256"]
     eng.close()
     pin.close()
+
+
+def test_verify_declared_groups_checked():
+    """A group id outside the declared [0, ngroups) is an error, not a fault."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids
+    from kano._native import KanoNativeError
+    obj = cluster("s_sparse_1000")
+    cs, ps = api_objects(obj)
+    gid = group_ids(cs, obj["label"])
+    eng = DeviceBuild(intern(cs, ps), build=False)
+    with pytest.raises(KanoNativeError, match="ngroups"):
+        eng.verify(gid, ngroups=max(1, int(gid.max())), shadow=False)
+    r = eng.verify(gid, ngroups=int(gid.max()) + 1, shadow=False)
+    assert r["user_crosscheck"].tolist() == expected("s_sparse_1000")["user_crosscheck"]["result"]
+    eng.close()
 
 
 @pytest.mark.parametrize("name", ["paper_example", "q_dirs", "s_broad_300"])
