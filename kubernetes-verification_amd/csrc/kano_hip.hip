@@ -104,7 +104,7 @@ struct kano_ctx {
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
-  DBuf gdev, icnt, ioff, sysrow, err_dev;     // gathered scalars, index-list block counts / offsets
+  DBuf gdev, icnt, ioff, sysrow, err_dev, idxd;     // gathered scalars, index-list block counts / offsets
   u64* ghost = nullptr;      // pinned landing buffer for gathered scalars
 
   hipEvent_t ev[10] = {};
@@ -870,6 +870,8 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     // class level: rows of a row class are equal, columns of a column class
     // are equal; everything runs on Mc (U_r x U_a bits)
     const i64 U = ctx->rc.U, ldC = ctx->ldC, UAW = ctx->UAW;
+    KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->R, sizeof(u64) * (i64)G * ldC));
     KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
@@ -877,13 +879,20 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     FillBatch fb(ctx);
     KTRY(fb.add(ctx->err_dev, 16, 0u));
     KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
+    KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
+    KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
     KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
     for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
     KTRY(fb.run());
+    const i64 rl = rows_local(ctx);
+    hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
+                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), P_<int32_t>(ctx->err_dev));
+    KLAUNCH();
     hipLaunchKernelGGL(k_cross_mc, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.moff),
-                       P_<int32_t>(ctx->rc.mem), P_<int32_t>(ctx->gid), G, P_<u64>(ctx->R),
-                       P_<u64>(ctx->multi), P_<int32_t>(ctx->err_dev));
+                       P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.mcnt),
+                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), P_<u64>(ctx->R),
+                       P_<u64>(ctx->multi));
     KLAUNCH();
     hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
@@ -1001,7 +1010,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow, &ctx->wicls,   &ctx->err_dev};
+                  &ctx->sysrow, &ctx->wicls,   &ctx->err_dev, &ctx->idxd};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1643,9 +1652,6 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   }
   const bool cross_on = gid && n > 0 && rows_local(ctx) > 0 && W > 0;
   if (gid) KTRY(crosscheck_impl(ctx, gid, ngroups));
-  // the matrix write now runs beside the latency-bound rest (index lists,
-  // policy_shadow); the bandwidth-heavy class-level crosscheck went first
-  KTRY(launch_rows(ctx));
   // the four result rows as index lists
   IdxRows ir{};
   ir.W = W;
@@ -1668,20 +1674,23 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   KTRY(scan_reserve(ctx, nb4));
   KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * nb4));
   KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * (nb4 + 1)));
-  KTRY(dalloc(ctx, ctx->scratch_words, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));
+  KTRY(dalloc(ctx, ctx->idxd, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));
   hipLaunchKernelGGL(k_idx_count, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
                      P_<i64>(ctx->icnt));
   KLAUNCH();
   KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->icnt), nb4, P_<i64>(ctx->ioff))));
-  int32_t* idx_dev = reinterpret_cast<int32_t*>(ctx->scratch_words.p);
+  int32_t* idx_dev = P_<int32_t>(ctx->idxd);
   hipLaunchKernelGGL(k_idx_write, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
                      P_<i64>(ctx->ioff), idx_dev);
   KLAUNCH();
-  // one sync for the list sizes (and policy_shadow's sizes)
+  // policy_shadow up to its size read; then the matrix write on stream2 runs
+  // beside the host sync and the short tail (pair emission, copies)
   Gather ga(ctx);
   for (int r = 0; r <= 4; ++r) ga.add(P_<i64>(ctx->ioff) + r * ir.nb, true);
-  const int ishadow = 5, ierr = shadow_count ? 7 : 5;
   if (shadow_count) KTRY(shadow_front(ctx, ga));
+  KTRY(launch_rows(ctx));
+  // one sync for the list sizes (and policy_shadow's sizes)
+  const int ishadow = 5, ierr = shadow_count ? 7 : 5;
   if (cross_on) ga.add(P_<int32_t>(ctx->err_dev), false);
   i64 v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   KTRY(ga.run(v));

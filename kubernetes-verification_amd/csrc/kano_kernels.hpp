@@ -599,45 +599,38 @@ __global__ __launch_bounds__(TPB) void k_row_from_mc(const u64* __restrict__ Mc,
 // user_crosscheck at class level (kano_py/kano/algorithm.py:27-42).  Group
 // range of the local members of every row class:
 __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restrict__ gid,
+                                                         int32_t G,
                                                          const int32_t* __restrict__ cls, i64 r0,
-                                                         i64 r1, int32_t* gmin, int32_t* gmax) {
+                                                         i64 r1, int32_t* gmin, int32_t* gmax,
+                                                         int32_t* err) {
   const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
   if (i >= r1) return;
   const int32_t c = cls[i], g = gid[i];
-  atomicMin(&gmin[c], g);
-  atomicMax(&gmax[c], g);
-}
-
-// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise; one wave
-// per class, the group range of the class's local members found by the wave.
-// An atomic is issued only for bits the (possibly stale) target word lacks:
-// big groups saturate R[g] early, and bits are only ever set.
-__global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
-                                                  i64 U, const int32_t* __restrict__ moff,
-                                                  const int32_t* __restrict__ mem,
-                                                  const int32_t* __restrict__ gid, int32_t G,
-                                                  u64* R, u64* multi, int32_t* err) {
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= U) return;
-  const int32_t m0 = moff[c], m1 = moff[c + 1];
-  if (m1 == m0) return;
-  int32_t gmin = INT32_MAX, gmax = -1;
-  for (int32_t m = m0 + lane; m < m1; m += 64) {
-    const int32_t g = gid[mem[m]];
-    gmin = min(gmin, g);
-    gmax = max(gmax, g);
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    gmin = min(gmin, __shfl_xor(gmin, d, 64));
-    gmax = max(gmax, __shfl_xor(gmax, d, 64));
-  }
-  if (gmin < 0 || gmax >= G) {   // caller-declared group count violated
-    if (lane == 0) atomicOr(err, 1);
+  if (g < 0 || g >= G) {   // caller-declared group count violated
+    atomicOr(err, 1);
     return;
   }
-  u64* dst = (gmin == gmax) ? R + (i64)gmin * ldMc : multi;
+  // big classes settle after a few members: skip atomics that cannot change
+  if (g < __hip_atomic_load(&gmin[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMin(&gmin[c], g);
+  if (g > __hip_atomic_load(&gmax[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(&gmax[c], g);
+}
+
+// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per
+// class).  An atomic is issued only for bits the (possibly stale) target word
+// lacks: big groups saturate R[g] early, and bits are only ever set.
+__global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
+                                                  i64 U, const int32_t* __restrict__ mcnt,
+                                                  const int32_t* __restrict__ gmin,
+                                                  const int32_t* __restrict__ gmax, u64* R,
+                                                  u64* multi) {
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= U || mcnt[c] == 0) return;
+  const int32_t g = gmin[c];
+  if (g > gmax[c]) return;   // no valid member (error flagged)
+  u64* dst = (g == gmax[c]) ? R + (i64)g * ldMc : multi;
   const u64* src = Mc + c * ldMc;
   for (i64 w = lane; w < UW; w += 64) {
     const u64 v = src[w];
