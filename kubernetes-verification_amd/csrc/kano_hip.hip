@@ -113,6 +113,7 @@ struct kano_ctx {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_rows = nullptr;
   bool rows_pending = false;
+  bool rows_overlap = false;
 };
 
 namespace {
@@ -306,10 +307,8 @@ int classify_phase1(kano_ctx* ctx, ClassSet& cs) {
   if (n > 0) {
     hipLaunchKernelGGL(k_class_insert, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->pv), n, P_<int32_t>(cs.keys_d), cs.KS,
-                       P_<int32_t>(cs.table), (uint32_t)(T - 1), P_<int32_t>(cs.slot_of));
-    KLAUNCH();
-    hipLaunchKernelGGL(k_class_min, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(cs.slot_of), n, P_<int32_t>(cs.smin));
+                       P_<int32_t>(cs.table), (uint32_t)(T - 1), P_<int32_t>(cs.slot_of),
+                       P_<int32_t>(cs.smin));
     KLAUNCH();
     hipLaunchKernelGGL(k_class_flag, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(cs.slot_of), n, P_<int32_t>(cs.smin), P_<int32_t>(cs.flag));
@@ -729,12 +728,19 @@ int launch_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
   if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
-  KCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
-  KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-  ctx->rows_pending = true;
+  // the matrix write saturates HBM and starves kernels beside it (measured:
+  // overlapping it with the checks on stream2 was slower), so it runs in
+  // order on the main stream unless rows_overlap is set
+  hipStream_t rs = ctx->stream;
+  if (ctx->rows_overlap) {
+    KCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
+    KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+    ctx->rows_pending = true;
+    rs = ctx->stream2;
+  }
   if (ctx->heavy_count > 0) {
     hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), (unsigned)ctx->heavy_count), dim3(TPB),
-                       0, ctx->stream2, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ctx->ldC,
+                       0, rs, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ctx->ldC,
                        P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
@@ -762,12 +768,12 @@ int launch_rows(kano_ctx* ctx) {
   a.cww = cww;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
-  KCHK(hipEventRecord(ctx->ev[7], ctx->stream2));
-  hipLaunchKernelGGL(k_rows, dim3((unsigned)ctx->wi_total, ncc), dim3(TPB), sizeof(u64) * cww,
-                     ctx->stream2, a);
+  KCHK(hipEventRecord(ctx->ev[7], rs));
+  hipLaunchKernelGGL(k_rows, dim3((unsigned)ctx->wi_total, ncc), dim3(TPB), sizeof(u64) * cww, rs,
+                     a);
   KLAUNCH();
-  KCHK(hipEventRecord(ctx->ev[8], ctx->stream2));
-  KCHK(hipEventRecord(ctx->ev_rows, ctx->stream2));
+  KCHK(hipEventRecord(ctx->ev[8], rs));
+  if (ctx->rows_overlap) KCHK(hipEventRecord(ctx->ev_rows, rs));
   ctx->rows_timed = true;
   return 0;
 }

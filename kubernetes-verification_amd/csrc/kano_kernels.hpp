@@ -19,17 +19,21 @@ namespace kano {
 __global__ __launch_bounds__(TPB) void k_class_insert(const int32_t* __restrict__ pv, i64 n,
                                                       const int32_t* __restrict__ keys, int KS,
                                                       int32_t* table, uint32_t tmask,
-                                                      int32_t* __restrict__ slot_of) {
+                                                      int32_t* __restrict__ slot_of,
+                                                      int32_t* smin) {
   const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
   uint32_t h = 0x9747b28cu;
   for (int k = 0; k < KS; ++k) h = hmix(h, (uint32_t)pv[(i64)keys[k] * n + i]);
   uint32_t s = hfin(h) & tmask;
-  for (;;) {  // linear probing; the table has >= 2n slots, so this ends
-    int32_t cur = __hip_atomic_load(&table[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // linear probing; the table has >= 2n slots, so this ends.  Slots only
+  // go from -1 to a pod id, so a plain (possibly stale) read is safe: a stale
+  // -1 just sends us to the CAS, which returns the real occupant.
+  for (;;) {
+    int32_t cur = table[s];
     if (cur < 0) {
       const int32_t prev = atomicCAS(&table[s], -1, (int32_t)i);
-      if (prev < 0) { slot_of[i] = (int32_t)s; return; }
+      if (prev < 0) break;
       cur = prev;
     }
     bool eq = true;
@@ -37,15 +41,12 @@ __global__ __launch_bounds__(TPB) void k_class_insert(const int32_t* __restrict_
       const int32_t* col = pv + (i64)keys[k] * n;
       if (col[cur] != col[i]) { eq = false; break; }
     }
-    if (eq) { slot_of[i] = (int32_t)s; return; }
+    if (eq) break;
     s = (s + 1) & tmask;
   }
-}
-
-__global__ __launch_bounds__(TPB) void k_class_min(const int32_t* __restrict__ slot_of, i64 n,
-                                                   int32_t* smin) {
-  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i < n) atomicMin(&smin[slot_of[i]], (int32_t)i);
+  slot_of[i] = (int32_t)s;
+  // smallest member per slot (the class representative); smin only falls
+  if ((int32_t)i < smin[s]) atomicMin(&smin[s], (int32_t)i);
 }
 
 __global__ __launch_bounds__(TPB) void k_class_flag(const int32_t* __restrict__ slot_of, i64 n,
@@ -72,16 +73,18 @@ __global__ __launch_bounds__(TPB) void k_class_assign(const int32_t* __restrict_
 __global__ __launch_bounds__(TPB) void k_member_count(const int32_t* __restrict__ cls, i64 m0,
                                                       i64 m1, int32_t* mcnt) {
   const i64 i = m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i < m1) atomicAdd(&mcnt[cls[i]], 1);
+  const bool act = i < m1;
+  (void)wave_agg_inc(mcnt, act ? cls[i] : 0, act);
 }
 
 __global__ __launch_bounds__(TPB) void k_member_fill(const int32_t* __restrict__ cls, i64 m0,
                                                      i64 m1, const int32_t* __restrict__ moff,
                                                      int32_t* mcur, int32_t* __restrict__ mem) {
   const i64 i = m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= m1) return;
-  const int32_t c = cls[i];
-  mem[moff[c] + atomicAdd(&mcur[c], 1)] = (int32_t)i;
+  const bool act = i < m1;
+  const int32_t c = act ? cls[i] : 0;
+  const int32_t r = wave_agg_inc(mcur, c, act);
+  if (act) mem[moff[c] + r] = (int32_t)i;
 }
 
 __global__ __launch_bounds__(TPB) void k_class_vals(const int32_t* __restrict__ pv, i64 n,
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(TPB) void k_proj_insert(const int32_t* __restrict__
   int32_t* tab = table + (i64)m * T;
   uint32_t s = proj_hash(cval, U, c, sl, ns) & (uint32_t)(T - 1);
   for (;;) {
-    int32_t cur = __hip_atomic_load(&tab[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int32_t cur = tab[s];   // plain read: see k_class_insert
     if (cur < 0) {
       const int32_t prev = atomicCAS(&tab[s], -1, (int32_t)c);
       if (prev < 0) { pslot[(i64)m * U + c] = (int32_t)s; return; }
@@ -245,7 +248,8 @@ __global__ __launch_bounds__(TPB) void k_group_count(const int32_t* __restrict__
                                                      i64 T, int32_t* gcnt) {
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
   const int m = blockIdx.y;
-  if (c < U) atomicAdd(&gcnt[(i64)m * T + pslot[(i64)m * U + c]], 1);
+  const bool act = c < U;
+  (void)wave_agg_inc(gcnt, act ? (i64)m * T + pslot[(i64)m * U + c] : 0, act);
 }
 
 __global__ __launch_bounds__(TPB) void k_group_fill(const int32_t* __restrict__ pslot, i64 U, i64 T,
@@ -253,9 +257,10 @@ __global__ __launch_bounds__(TPB) void k_group_fill(const int32_t* __restrict__ 
                                                     int32_t* __restrict__ gmem) {
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
   const int m = blockIdx.y;
-  if (c >= U) return;
-  const i64 g = (i64)m * T + pslot[(i64)m * U + c];
-  gmem[goff[g] + atomicAdd(&gcur[g], 1)] = (int32_t)c;
+  const bool act = c < U;
+  const i64 g = act ? (i64)m * T + pslot[(i64)m * U + c] : 0;
+  const int32_t r = wave_agg_inc(gcur, g, act);
+  if (act) gmem[goff[g] + r] = (int32_t)c;
 }
 
 __global__ __launch_bounds__(TPB) void k_iota(int32_t* __restrict__ out, i64 n) {
@@ -611,10 +616,9 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
     return;
   }
   // big classes settle after a few members: skip atomics that cannot change
-  if (g < __hip_atomic_load(&gmin[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMin(&gmin[c], g);
-  if (g > __hip_atomic_load(&gmax[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMax(&gmax[c], g);
+  // (plain reads, possibly stale: gmin only falls, gmax only rises)
+  if (g < gmin[c]) atomicMin(&gmin[c], g);
+  if (g > gmax[c]) atomicMax(&gmax[c], g);
 }
 
 // R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per
@@ -634,8 +638,7 @@ __global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i6
   const u64* src = Mc + c * ldMc;
   for (i64 w = lane; w < UW; w += 64) {
     const u64 v = src[w];
-    if (v & ~__hip_atomic_load(&dst[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      atomicOr(&dst[w], v);
+    if (v & ~dst[w]) atomicOr(&dst[w], v);   // plain read, possibly stale
   }
 }
 
@@ -916,11 +919,9 @@ __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
       if (gw >= a.W) break;
       const u64 v = row[w];
       const u64 vm = valid_mask(gw, a.n);
-      if (v & ~__hip_atomic_load(&a.color[gw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicOr(&a.color[gw], v);
+      if (v & ~a.color[gw]) atomicOr(&a.color[gw], v);
       const u64 nv = ~v & vm;
-      if (nv && __hip_atomic_load(&a.colnand[gw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != vm)
-        atomicOr(&a.colnand[gw], nv);
+      if (nv & ~a.colnand[gw]) atomicOr(&a.colnand[gw], nv);
     }
   }
 }

@@ -197,6 +197,25 @@ __global__ void k_gather(GatherJobs g, u64* __restrict__ dst) {
                        : (u64)(uint32_t)*static_cast<const int32_t*>(g.src[k]);
 }
 
+// atomicAdd(&ctr[key], 1) for every active lane, with the lanes that share
+// the first active lane's key merged into one atomic (Zipf keys: the hot key
+// is usually the one repeated inside a wave).  Returns the lane's slot (old
+// value + rank).  Every lane of the wave must call it.
+__device__ __forceinline__ int32_t wave_agg_inc(int32_t* ctr, i64 key, bool active) {
+  const u64 act = __ballot(active);
+  if (act == 0ull) return 0;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)act) - 1;
+  const i64 k0 = __shfl(key, leader, 64);
+  const bool same = active && key == k0;
+  const u64 smask = __ballot(same);
+  int32_t base = 0;
+  if (lane == leader) base = atomicAdd(&ctr[k0], (int32_t)__popcll(smask));
+  base = __shfl(base, leader, 64);
+  if (same) return base + (int32_t)__popcll(smask & ((1ull << lane) - 1ull));
+  return active ? atomicAdd(&ctr[key], 1) : 0;
+}
+
 // ---- small helpers ---------------------------------------------------------
 __device__ __forceinline__ i64 upper_bound_i32(const int32_t* a, i64 n, i64 key) {
   i64 lo = 0, hi = n;
