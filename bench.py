@@ -53,8 +53,8 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--path", default="auto", choices=["auto", "bitwise", "mfma"])
     ap.add_argument("--no-shadow", action="store_true",
@@ -259,10 +259,13 @@ def main():
     step.k_rows_ms.clear()
     barrier()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(args.steps):
         step()
+        marks.append(time.perf_counter())   # each step ends in a host sync
     barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = np.diff(np.array([t0] + marks)) * 1e3
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -299,6 +302,9 @@ def main():
                          "traffic": None, "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": k_rows_ms},
             "stages_ms_last_step": {k: round(v, 4) for k, v in step.stages.items()},
+            "step_ms": {"min": round(float(step_ms.min()), 4),
+                        "median": round(float(np.median(step_ms)), 4),
+                        "max": round(float(step_ms.max()), 4)},
             "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},

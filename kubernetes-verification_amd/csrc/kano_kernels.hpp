@@ -616,14 +616,13 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
     return;
   }
   // big classes settle after a few members: skip atomics that cannot change
-  // (plain reads, possibly stale: gmin only falls, gmax only rises)
-  if (g < gmin[c]) atomicMin(&gmin[c], g);
-  if (g > gmax[c]) atomicMax(&gmax[c], g);
+  // no-return atomics are posted; a read-before-update check measured slower
+  atomicMin(&gmin[c], g);
+  atomicMax(&gmax[c], g);
 }
 
 // R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per
-// class).  An atomic is issued only for bits the (possibly stale) target word
-// lacks: big groups saturate R[g] early, and bits are only ever set.
+// class).
 __global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
                                                   i64 U, const int32_t* __restrict__ mcnt,
                                                   const int32_t* __restrict__ gmin,
@@ -638,7 +637,7 @@ __global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i6
   const u64* src = Mc + c * ldMc;
   for (i64 w = lane; w < UW; w += 64) {
     const u64 v = src[w];
-    if (v & ~dst[w]) atomicOr(&dst[w], v);   // plain read, possibly stale
+    if (v) atomicOr(&dst[w], v);
   }
 }
 
@@ -911,7 +910,7 @@ __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
     if (heavy && m == m_begin) continue;
     u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
     for (int w = threadIdx.x * 2; w < nw; w += TPB * 2)
-      *(ulonglong2*)&dst[w] = *(const ulonglong2*)&row[w];
+      *(u64x2*)&dst[w] = *(const u64x2*)&row[w];   // (nt stores measured slower)
   }
   if (chunk == 0 && a.color) {
     for (int w = threadIdx.x; w < nw; w += TPB) {

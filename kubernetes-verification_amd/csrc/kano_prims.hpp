@@ -7,6 +7,7 @@
 
 typedef unsigned long long u64;
 typedef long long i64;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 namespace kano {
 
