@@ -179,43 +179,65 @@ T* P_(DBuf& b) {
 
 inline unsigned nblk(i64 n, i64 per = TPB) { return (unsigned)((n + per - 1) / per); }
 
-// ---- device-wide scan: one k_scan_lb launch on reserved status regions ----
-inline i64 scan_tiles(i64 n) { return std::max<i64>(1, (n + SCAN_TILE - 1) / SCAN_TILE); }
+// ---- device-wide scans: batches of k_scan_lb jobs ------------------------
+inline i64 scan_tiles(i64 n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
-int scan_reserve(kano_ctx* ctx, i64 n) {
-  const i64 tiles = scan_tiles(n);
-  if (tiles <= ctx->scan_cap) return 0;
-  const size_t bytes = sizeof(u64) * 2 * (size_t)(1 + tiles);
+// status slots per region >= slots (grows, zeroing both regions in order)
+int scan_reserve(kano_ctx* ctx, i64 slots) {
+  if (slots <= ctx->scan_cap) return 0;
+  slots = std::max<i64>(slots, 2 * ctx->scan_cap);
+  const size_t bytes = sizeof(u64) * 2 * (size_t)slots;
   KTRY(dalloc(ctx, ctx->scan_tmp, bytes));
   KCHK(hipMemsetAsync(ctx->scan_tmp.p, 0, bytes, ctx->stream));
-  ctx->scan_cap = tiles;
+  ctx->scan_cap = slots;
   ctx->scan_parity = 0;
   return 0;
 }
 
-template <typename Tin, typename Tout>
-int scan_level(kano_ctx* ctx, const Tin* in, i64 n, Tout* out) {
-  if (n == 0) {
-    KCHK(hipMemsetAsync(out, 0, sizeof(Tout), ctx->stream));
+// several exclusive scans in one launch: out[0..n] with out[n] = total
+struct ScanBatch {
+  ScanJobs jobs{};
+  kano_ctx* ctx;
+  i64 slots = 0, maxt = 1;
+  explicit ScanBatch(kano_ctx* c) : ctx(c) { jobs.count = 0; }
+  template <typename Tin, typename Tout>
+  int add(const Tin* in, i64 n, Tout* out) {
+    static_assert(sizeof(Tin) == 4 || sizeof(Tin) == 8, "int32 / int64 scans");
+    static_assert(sizeof(Tout) == 4 || sizeof(Tout) == 8, "int32 / int64 scans");
+    if (jobs.count == MAX_SCAN_JOBS) KTRY(run());
+    ScanJob& j = jobs.j[jobs.count++];
+    j.in = in;
+    j.out = out;
+    j.n = n;
+    j.st = slots;
+    j.in64 = sizeof(Tin) == 8;
+    j.out64 = sizeof(Tout) == 8;
+    slots += 1 + scan_tiles(n);
+    maxt = std::max<i64>(maxt, scan_tiles(n));
     return 0;
   }
-  const i64 tiles = scan_tiles(n), region = 1 + ctx->scan_cap;
-  u64* st = P_<u64>(ctx->scan_tmp);
-  u64* cur = st + (ctx->scan_parity ? region : 0);
-  u64* nxt = st + (ctx->scan_parity ? 0 : region);
-  hipLaunchKernelGGL((k_scan_lb<Tin, Tout>), dim3((unsigned)tiles), dim3(TPB), 0, ctx->stream, in,
-                     n, out, cur, nxt, region);
-  KLAUNCH();
-  ctx->scan_parity ^= 1;
-  return 0;
-}
+  int run() {
+    if (jobs.count == 0) return 0;
+    KTRY(scan_reserve(ctx, slots));
+    u64* st = P_<u64>(ctx->scan_tmp);
+    u64* cur = st + (ctx->scan_parity ? ctx->scan_cap : 0);
+    u64* nxt = st + (ctx->scan_parity ? 0 : ctx->scan_cap);
+    hipLaunchKernelGGL(k_scan_lb, dim3((unsigned)maxt, (unsigned)jobs.count), dim3(TPB), 0,
+                       ctx->stream, jobs, cur, nxt, ctx->scan_cap);
+    KLAUNCH();
+    ctx->scan_parity ^= 1;
+    jobs.count = 0;
+    slots = 0;
+    maxt = 1;
+    return 0;
+  }
+};
 
-// exclusive scan, out has n+1 slots (out[n] = total)
 template <typename Tin, typename Tout>
 int scan_excl(kano_ctx* ctx, const Tin* in, i64 n, Tout* out) {
-  if (scan_tiles(n) > ctx->scan_cap)
-    return fail(ctx, -EINVAL, "internal: scan scratch not reserved for " + std::to_string(n));
-  return scan_level<Tin, Tout>(ctx, in, n, out);
+  ScanBatch sb(ctx);
+  KTRY(sb.add(in, n, out));
+  return sb.run();
 }
 
 // several device fills in one launch (k_fill_many)
@@ -301,21 +323,45 @@ int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   return 0;
 }
 
-// phase 1: hash insert, smallest member per slot, class-id scan (no sync)
-int classify_phase1(kano_ctx* ctx, ClassSet& cs) {
-  const i64 n = ctx->n, T = table_size(n);
+ClsSide cls_side(kano_ctx* ctx, ClassSet& cs) {
+  ClsSide a{};
+  a.keys = P_<int32_t>(cs.keys_d);
+  a.KS = cs.KS;
+  a.tmask = (uint32_t)(table_size(ctx->n) - 1);
+  a.table = P_<int32_t>(cs.table);
+  a.slot_of = P_<int32_t>(cs.slot_of);
+  a.smin = P_<int32_t>(cs.smin);
+  a.flag = P_<int32_t>(cs.flag);
+  a.cid = P_<int32_t>(cs.cid);
+  a.cls = P_<int32_t>(cs.cls);
+  a.rep = P_<int32_t>(cs.rep);
+  a.mcnt = P_<int32_t>(cs.mcnt);
+  a.mcur = P_<int32_t>(cs.mcur);
+  a.moff = P_<int32_t>(cs.moff);
+  a.mem = P_<int32_t>(cs.mem);
+  a.cval = P_<int32_t>(cs.cval);
+  a.m0 = cs.m0;
+  a.m1 = cs.m1;
+  a.U = cs.U;
+  return a;
+}
+
+// phase 1, both sides: hash insert + smallest member per slot, first-member
+// flags, class-id scan (no sync)
+int classify_phase1(kano_ctx* ctx) {
+  const i64 n = ctx->n;
+  ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   if (n > 0) {
-    hipLaunchKernelGGL(k_class_insert, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->pv), n, P_<int32_t>(cs.keys_d), cs.KS,
-                       P_<int32_t>(cs.table), (uint32_t)(T - 1), P_<int32_t>(cs.slot_of),
-                       P_<int32_t>(cs.smin));
+    hipLaunchKernelGGL(k_cls_insert, dim3(nblk(n), 2), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->pv), n, pr);
     KLAUNCH();
-    hipLaunchKernelGGL(k_class_flag, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(cs.slot_of), n, P_<int32_t>(cs.smin), P_<int32_t>(cs.flag));
+    hipLaunchKernelGGL(k_cls_flag, dim3(nblk(n), 2), dim3(TPB), 0, ctx->stream, n, pr);
     KLAUNCH();
   }
-  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(cs.flag), n, P_<int32_t>(cs.cid))));
-  return 0;
+  ScanBatch sb(ctx);
+  KTRY(sb.add(P_<int32_t>(ctx->rc.flag), n, P_<int32_t>(ctx->rc.cid)));
+  KTRY(sb.add(P_<int32_t>(ctx->cc.flag), n, P_<int32_t>(ctx->cc.cid)));
+  return sb.run();
 }
 
 int classify_alloc2(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
@@ -331,32 +377,32 @@ int classify_alloc2(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   return 0;
 }
 
-// phase 2 (U known): ids, member lists of pods [m0, m1), representative values
-int classify_phase2(kano_ctx* ctx, ClassSet& cs) {
-  const i64 n = ctx->n, U = cs.U;
+// phase 2, both sides (U known): ids, member lists of pods [m0, m1),
+// representative values
+int classify_phase2(kano_ctx* ctx) {
+  const i64 n = ctx->n;
+  ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   if (n > 0) {
-    hipLaunchKernelGGL(k_class_assign, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(cs.slot_of), n, P_<int32_t>(cs.smin), P_<int32_t>(cs.cid),
-                       P_<int32_t>(cs.cls), P_<int32_t>(cs.rep));
+    hipLaunchKernelGGL(k_cls_assign, dim3(nblk(n), 2), dim3(TPB), 0, ctx->stream, n, pr);
     KLAUNCH();
   }
-  const i64 rl = cs.m1 - cs.m0;
+  const i64 rl = std::max(ctx->rc.m1 - ctx->rc.m0, ctx->cc.m1 - ctx->cc.m0);
   if (rl > 0) {
-    hipLaunchKernelGGL(k_member_count, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(cs.cls), cs.m0, cs.m1, P_<int32_t>(cs.mcnt));
+    hipLaunchKernelGGL(k_cls_mcount, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
-  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(cs.mcnt), U, P_<int32_t>(cs.moff))));
+  ScanBatch sb(ctx);
+  KTRY(sb.add(P_<int32_t>(ctx->rc.mcnt), ctx->rc.U, P_<int32_t>(ctx->rc.moff)));
+  KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ctx->cc.U, P_<int32_t>(ctx->cc.moff)));
+  KTRY(sb.run());
   if (rl > 0) {
-    hipLaunchKernelGGL(k_member_fill, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(cs.cls), cs.m0, cs.m1, P_<int32_t>(cs.moff),
-                       P_<int32_t>(cs.mcur), P_<int32_t>(cs.mem));
+    hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
-  if (cs.KS > 0 && U > 0) {
-    hipLaunchKernelGGL(k_class_vals, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->pv), n, P_<int32_t>(cs.keys_d), cs.KS,
-                       P_<int32_t>(cs.rep), U, P_<int32_t>(cs.cval));
+  const i64 U = std::max(ctx->rc.U, ctx->cc.U);
+  if (U > 0) {
+    hipLaunchKernelGGL(k_cls_vals, dim3(nblk(U), 2), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->pv), n, pr);
     KLAUNCH();
   }
   return 0;
@@ -393,39 +439,67 @@ int match_alloc(kano_ctx* ctx, SideMatch& sx, ClassSet& cs, FillBatch& fb) {
   return 0;
 }
 
-int match_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
-  const i64 P = ctx->P, U = cs.U;
-  if (P == 0 || U == 0) return 0;
-  if (!sx.dense) {
-    const int NM = sx.NM;
-    const i64 T = sx.T;
-    if (NM > 0) {
-      dim3 g2(nblk(U), (unsigned)NM);
-      hipLaunchKernelGGL(k_proj_insert, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(cs.cval), U,
-                         P_<int32_t>(sx.moff), P_<int32_t>(sx.mslot), P_<int32_t>(sx.table), T,
-                         P_<int32_t>(sx.pslot));
-      KLAUNCH();
-      hipLaunchKernelGGL(k_group_count, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(sx.pslot), U, T,
-                         P_<int32_t>(sx.gcnt));
-      KLAUNCH();
-      KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(sx.gcnt), (i64)NM * T,
-                                        P_<int32_t>(sx.goff))));
-      hipLaunchKernelGGL(k_group_fill, g2, dim3(TPB), 0, ctx->stream, P_<int32_t>(sx.pslot), U, T,
-                         P_<int32_t>(sx.goff), P_<int32_t>(sx.gcur), P_<int32_t>(sx.gmem));
-      KLAUNCH();
+JoinSide join_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
+  JoinSide a{};
+  a.cval = P_<int32_t>(cs.cval);
+  a.U = cs.U;
+  a.moff = P_<int32_t>(sx.moff);
+  a.mslot = P_<int32_t>(sx.mslot);
+  a.table = P_<int32_t>(sx.table);
+  a.T = sx.T;
+  a.pslot = P_<int32_t>(sx.pslot);
+  a.gcnt = P_<int32_t>(sx.gcnt);
+  a.goff = P_<int32_t>(sx.goff);
+  a.gcur = P_<int32_t>(sx.gcur);
+  a.gmem = P_<int32_t>(sx.gmem);
+  a.toff = P_<i64>(sx.toff);
+  a.tval = P_<int32_t>(sx.tval);
+  a.pmask = P_<int32_t>(sx.pmask);
+  a.pstart = P_<i64>(sx.pstart);
+  a.plen = P_<int32_t>(sx.plen);
+  a.NM = sx.NM;
+  a.live = (ctx->P > 0 && cs.U > 0 && !sx.dense) ? 1 : 0;
+  return a;
+}
+
+int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs);
+
+// hash join of both sides in the same launches: side 0 = allow side on the
+// column classes, side 1 = select side on the row classes; a dense side
+// (too many masks) takes match_dense instead
+int match_both(kano_ctx* ctx) {
+  JoinPair pr{{join_side(ctx, ctx->am, ctx->cc), join_side(ctx, ctx->sm, ctx->rc)}};
+  const JoinSide &a0 = pr.s[0], &a1 = pr.s[1];
+  const i64 maxU = std::max(a0.live ? a0.U : 0, a1.live ? a1.U : 0);
+  const unsigned rows_i = (a0.live ? a0.NM : 0) + (a1.live ? a1.NM : 0);
+  const unsigned rows_f = (a0.live ? a0.NM + 1 : 0) + (a1.live ? a1.NM + 1 : 0);
+  if (rows_i > 0) {
+    hipLaunchKernelGGL(k_join_insert, dim3(nblk(maxU), rows_i), dim3(TPB), 0, ctx->stream, pr);
+    KLAUNCH();
+    hipLaunchKernelGGL(k_join_count, dim3(nblk(maxU), rows_i), dim3(TPB), 0, ctx->stream, pr);
+    KLAUNCH();
+    ScanBatch sb(ctx);
+    for (int q = 0; q < 2; ++q) {
+      SideMatch& sx = q ? ctx->sm : ctx->am;
+      if (pr.s[q].live && sx.NM > 0)
+        KTRY(sb.add(P_<int32_t>(sx.gcnt), (i64)sx.NM * sx.T, P_<int32_t>(sx.goff)));
     }
-    hipLaunchKernelGGL(k_iota, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(sx.gmem) + (i64)NM * U, U);
-    KLAUNCH();
-    hipLaunchKernelGGL(k_pol_match, dim3(nblk(P)), dim3(TPB), 0, ctx->stream, P, P_<i64>(sx.toff),
-                       P_<int32_t>(sx.tval), P_<int32_t>(sx.pmask), P_<int32_t>(sx.moff),
-                       P_<int32_t>(sx.mslot), P_<int32_t>(cs.cval), U, P_<int32_t>(sx.table), T,
-                       P_<int32_t>(sx.goff), (i64)NM * U, P_<i64>(sx.pstart),
-                       P_<int32_t>(sx.plen));
-    KLAUNCH();
-    return 0;
+    KTRY(sb.run());
   }
-  // dense fallback: evaluate every (policy, class) predicate (one extra sync)
+  if (rows_f > 0) {
+    hipLaunchKernelGGL(k_join_fill, dim3(nblk(maxU), rows_f), dim3(TPB), 0, ctx->stream, pr);
+    KLAUNCH();
+    hipLaunchKernelGGL(k_join_match, dim3(nblk(ctx->P), 2), dim3(TPB), 0, ctx->stream, ctx->P, pr);
+    KLAUNCH();
+  }
+  if (ctx->P > 0 && ctx->cc.U > 0 && ctx->am.dense) KTRY(match_dense(ctx, ctx->am, ctx->cc));
+  if (ctx->P > 0 && ctx->rc.U > 0 && ctx->sm.dense) KTRY(match_dense(ctx, ctx->sm, ctx->rc));
+  return 0;
+}
+
+// dense fallback: evaluate every (policy, class) predicate (one extra sync)
+int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
+  const i64 P = ctx->P, U = cs.U;
   const i64 UW = (U + 63) / 64, ld = std::max<i64>(2, (UW + 1) & ~(i64)1);
   KTRY(dalloc(ctx, sx.bits, sizeof(u64) * P * ld));
   KTRY(dalloc(ctx, sx.boff, sizeof(i64) * (P + 1)));
@@ -463,8 +537,7 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(classify_alloc1(ctx, ctx->cc, fb));
     KTRY(fb.run());
   }
-  KTRY(classify_phase1(ctx, ctx->rc));
-  KTRY(classify_phase1(ctx, ctx->cc));
+  KTRY(classify_phase1(ctx));
   i64 u[2] = {0, 0};
   {
     Gather ga(ctx);
@@ -475,11 +548,6 @@ int do_front(kano_ctx* ctx, int path) {
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-  // the stream is idle here: size the scan scratch for the group tables too
-  i64 longest = std::max<i64>({ctx->n, ctx->P, (i64)1});
-  longest = std::max<i64>(longest, (i64)ctx->sm.NM * table_size(ctx->rc.U));
-  longest = std::max<i64>(longest, (i64)ctx->am.NM * table_size(ctx->cc.U));
-  KTRY(scan_reserve(ctx, longest));
 
   const i64 P = ctx->P, Ur = ctx->rc.U, Ua = ctx->cc.U;
   ctx->UAW = (Ua + 63) / 64;
@@ -509,10 +577,10 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
     KTRY(fb.run());
   }
-  KTRY(classify_phase2(ctx, ctx->rc));
-  KTRY(classify_phase2(ctx, ctx->cc));
+  KTRY(classify_phase2(ctx));
+  KTRY(match_both(ctx));
+  KCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   // allow side: allowed classes / pods per policy
-  KTRY(match_side(ctx, ctx->am, ctx->cc));
   if (P > 0) {
     hipLaunchKernelGGL(k_pol_allow_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
@@ -520,11 +588,7 @@ int do_front(kano_ctx* ctx, int path) {
                        P_<int32_t>(ctx->acnt));
     KLAUNCH();
   }
-  KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->nca), P, P_<i64>(ctx->alcoff))));
-  KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->acnt), P, P_<i64>(ctx->aloff))));
-  KCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   // select side: |S(c)|, rebuild cost, the per-class plan
-  KTRY(match_side(ctx, ctx->sm, ctx->rc));
   if (P > 0 && Ur > 0) {
     hipLaunchKernelGGL(k_sel_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                        P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
@@ -548,10 +612,14 @@ int do_front(kano_ctx* ctx, int path) {
     hipLaunchKernelGGL(k_class_plan, dim3(nblk(Ur)), dim3(TPB), 0, ctx->stream, a);
     KLAUNCH();
   }
-  KTRY((scan_excl<int32_t, i64>(ctx, P_<int32_t>(ctx->scnt), Ur, P_<i64>(ctx->soffc))));
-  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->wicnt), Ur, P_<int32_t>(ctx->wioff))));
-  KTRY((scan_excl<int32_t, int32_t>(ctx, P_<int32_t>(ctx->hflag), Ur, P_<int32_t>(ctx->hoff))));
-  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff))));
+  ScanBatch sb(ctx);
+  KTRY(sb.add(P_<int32_t>(ctx->nca), P, P_<i64>(ctx->alcoff)));
+  KTRY(sb.add(P_<int32_t>(ctx->acnt), P, P_<i64>(ctx->aloff)));
+  KTRY(sb.add(P_<int32_t>(ctx->scnt), Ur, P_<i64>(ctx->soffc)));
+  KTRY(sb.add(P_<int32_t>(ctx->wicnt), Ur, P_<int32_t>(ctx->wioff)));
+  KTRY(sb.add(P_<int32_t>(ctx->hflag), Ur, P_<int32_t>(ctx->hoff)));
+  KTRY(sb.add(P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff)));
+  KTRY(sb.run());
   return 0;
 }
 
@@ -1230,7 +1298,6 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now) {
   ctx->rows_dirty = false;
   ctx->cols_valid = false;
   ctx->shadow_total = -1;
-  KTRY(scan_reserve(ctx, std::max<i64>({ctx->n, ctx->P, (i64)1})));
   const i64 rl = rows_local(ctx);
   KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM)));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
@@ -1457,7 +1524,6 @@ int shadow_front(kano_ctx* ctx, Gather& ga) {
   const i64 U = ctx->rc.U, rl = rows_local(ctx), nf = ctx->nflags;
   const i64 nt = (nf + SH_TILE - 1) / SH_TILE;
   KCHK(hipEventRecord(ctx->ev[5], ctx->stream));
-  KTRY(scan_reserve(ctx, std::max<i64>({U, rl, nt, (i64)1})));
   KTRY(dalloc(ctx, ctx->flags, nf + 16));
   KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, U)));
   KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (U + 1)));
@@ -1488,8 +1554,12 @@ int shadow_front(kano_ctx* ctx, Gather& ga) {
                        P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
-  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->tcnt), nt, P_<i64>(ctx->toff))));
-  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->T), U, P_<i64>(ctx->loff))));
+  {
+    ScanBatch sb(ctx);
+    KTRY(sb.add(P_<i64>(ctx->tcnt), nt, P_<i64>(ctx->toff)));
+    KTRY(sb.add(P_<i64>(ctx->T), U, P_<i64>(ctx->loff)));
+    KTRY(sb.run());
+  }
   if (rl > 0) {
     hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
@@ -1576,7 +1646,6 @@ int kano_shadow_lists(kano_ctx* ctx, int64_t n_lists, int64_t nbits, int64_t P,
   ctx->cc.U = nbits;
   ctx->UAW = ctx->W;
   ctx->ldC = ctx->ldM;
-  KTRY(scan_reserve(ctx, std::max<i64>({n_lists, P, (i64)1})));
   const i64 U = n_lists;
   KTRY(dalloc(ctx, ctx->soffc, sizeof(i64) * (U + 1)));
   KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, nnz)));
@@ -1677,7 +1746,6 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   ir.row[3] = have_sys ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   const i64 nb4 = 4 * ir.nb;
-  KTRY(scan_reserve(ctx, nb4));
   KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * nb4));
   KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * (nb4 + 1)));
   KTRY(dalloc(ctx, ctx->idxd, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));

@@ -16,85 +16,103 @@ namespace kano {
 // Classes: pods hashed on the values of a key set.  Pods of one class are
 // indistinguishable to every predicate on those keys.
 // ===========================================================================
-__global__ __launch_bounds__(TPB) void k_class_insert(const int32_t* __restrict__ pv, i64 n,
-                                                      const int32_t* __restrict__ keys, int KS,
-                                                      int32_t* table, uint32_t tmask,
-                                                      int32_t* __restrict__ slot_of,
-                                                      int32_t* smin) {
+// Both sides (row classes on the working-selector keys, column classes on
+// the working-allow keys) run in the same launches: blockIdx.y = side.
+struct ClsSide {
+  const int32_t* keys;
+  int KS;
+  uint32_t tmask;
+  int32_t* table;
+  int32_t* slot_of;
+  int32_t* smin;
+  int32_t* flag;
+  const int32_t* cid;
+  int32_t* cls;
+  int32_t* rep;
+  int32_t* mcnt;
+  int32_t* mcur;
+  const int32_t* moff;
+  int32_t* mem;
+  int32_t* cval;
+  i64 m0, m1, U;
+};
+struct ClsPair {
+  ClsSide s[2];
+};
+
+__global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ pv, i64 n,
+                                                    ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
   uint32_t h = 0x9747b28cu;
-  for (int k = 0; k < KS; ++k) h = hmix(h, (uint32_t)pv[(i64)keys[k] * n + i]);
-  uint32_t s = hfin(h) & tmask;
+  for (int k = 0; k < a.KS; ++k) h = hmix(h, (uint32_t)pv[(i64)a.keys[k] * n + i]);
+  uint32_t s = hfin(h) & a.tmask;
   // linear probing; the table has >= 2n slots, so this ends.  Slots only
   // go from -1 to a pod id, so a plain (possibly stale) read is safe: a stale
   // -1 just sends us to the CAS, which returns the real occupant.
   for (;;) {
-    int32_t cur = table[s];
+    int32_t cur = a.table[s];
     if (cur < 0) {
-      const int32_t prev = atomicCAS(&table[s], -1, (int32_t)i);
+      const int32_t prev = atomicCAS(&a.table[s], -1, (int32_t)i);
       if (prev < 0) break;
       cur = prev;
     }
     bool eq = true;
-    for (int k = 0; k < KS; ++k) {
-      const int32_t* col = pv + (i64)keys[k] * n;
+    for (int k = 0; k < a.KS; ++k) {
+      const int32_t* col = pv + (i64)a.keys[k] * n;
       if (col[cur] != col[i]) { eq = false; break; }
     }
     if (eq) break;
-    s = (s + 1) & tmask;
+    s = (s + 1) & a.tmask;
   }
-  slot_of[i] = (int32_t)s;
+  a.slot_of[i] = (int32_t)s;
   // smallest member per slot (the class representative); smin only falls
-  if ((int32_t)i < smin[s]) atomicMin(&smin[s], (int32_t)i);
+  if ((int32_t)i < a.smin[s]) atomicMin(&a.smin[s], (int32_t)i);
 }
 
-__global__ __launch_bounds__(TPB) void k_class_flag(const int32_t* __restrict__ slot_of, i64 n,
-                                                    const int32_t* __restrict__ smin,
-                                                    int32_t* __restrict__ flag) {
+__global__ __launch_bounds__(TPB) void k_cls_flag(i64 n, ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i < n) flag[i] = (smin[slot_of[i]] == (int32_t)i) ? 1 : 0;
+  if (i < n) a.flag[i] = (a.smin[a.slot_of[i]] == (int32_t)i) ? 1 : 0;
 }
 
 // class ids ordered by their smallest member (deterministic)
-__global__ __launch_bounds__(TPB) void k_class_assign(const int32_t* __restrict__ slot_of, i64 n,
-                                                      const int32_t* __restrict__ smin,
-                                                      const int32_t* __restrict__ cid,
-                                                      int32_t* __restrict__ cls,
-                                                      int32_t* __restrict__ rep) {
+__global__ __launch_bounds__(TPB) void k_cls_assign(i64 n, ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
-  const int32_t r = smin[slot_of[i]];
-  const int32_t c = cid[r];
-  cls[i] = c;
-  if (r == (int32_t)i) rep[c] = (int32_t)i;
+  const int32_t r = a.smin[a.slot_of[i]];
+  const int32_t c = a.cid[r];
+  a.cls[i] = c;
+  if (r == (int32_t)i) a.rep[c] = (int32_t)i;
 }
 
-__global__ __launch_bounds__(TPB) void k_member_count(const int32_t* __restrict__ cls, i64 m0,
-                                                      i64 m1, int32_t* mcnt) {
-  const i64 i = m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool act = i < m1;
-  (void)wave_agg_inc(mcnt, act ? cls[i] : 0, act);
+// member counts of the pods [m0, m1) of each side
+__global__ __launch_bounds__(TPB) void k_cls_mcount(ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
+  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  const bool act = i < a.m1;
+  (void)wave_agg_inc(a.mcnt, act ? a.cls[i] : 0, act);
 }
 
-__global__ __launch_bounds__(TPB) void k_member_fill(const int32_t* __restrict__ cls, i64 m0,
-                                                     i64 m1, const int32_t* __restrict__ moff,
-                                                     int32_t* mcur, int32_t* __restrict__ mem) {
-  const i64 i = m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool act = i < m1;
-  const int32_t c = act ? cls[i] : 0;
-  const int32_t r = wave_agg_inc(mcur, c, act);
-  if (act) mem[moff[c] + r] = (int32_t)i;
+__global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
+  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  const bool act = i < a.m1;
+  const int32_t c = act ? a.cls[i] : 0;
+  const int32_t r = wave_agg_inc(a.mcur, c, act);
+  if (act) a.mem[a.moff[c] + r] = (int32_t)i;
 }
 
-__global__ __launch_bounds__(TPB) void k_class_vals(const int32_t* __restrict__ pv, i64 n,
-                                                    const int32_t* __restrict__ keys, int KS,
-                                                    const int32_t* __restrict__ rep, i64 U,
-                                                    int32_t* __restrict__ cval) {
+// key values of each class's representative, slot-major: cval[k * U + c]
+__global__ __launch_bounds__(TPB) void k_cls_vals(const int32_t* __restrict__ pv, i64 n,
+                                                  ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c >= U) return;
-  const int32_t r = rep[c];
-  for (int k = 0; k < KS; ++k) cval[(i64)k * U + c] = pv[(i64)keys[k] * n + r];
+  if (c >= a.U) return;
+  const int32_t r = a.rep[c];
+  for (int k = 0; k < a.KS; ++k) a.cval[(i64)k * a.U + c] = pv[(i64)a.keys[k] * n + r];
 }
 
 // ===========================================================================
@@ -214,113 +232,138 @@ __device__ __forceinline__ uint32_t proj_hash(const int32_t* __restrict__ cval, 
   return hfin(h);
 }
 
-// grid (classes, masks): group id of class c under mask m = its table slot
-__global__ __launch_bounds__(TPB) void k_proj_insert(const int32_t* __restrict__ cval, i64 U,
-                                                     const int32_t* __restrict__ moff,
-                                                     const int32_t* __restrict__ mslot,
-                                                     int32_t* table, i64 T,
-                                                     int32_t* __restrict__ pslot) {
+// Both sides in one launch: grid.y enumerates (side 0 rows, side 1 rows); a
+// side contributes NM mask rows (+1 iota row in k_join_fill) when live.
+struct JoinSide {
+  const int32_t* cval;
+  i64 U;
+  const int32_t* moff;   // mask -> slot list
+  const int32_t* mslot;
+  int32_t* table;        // NM tables of T slots
+  i64 T;
+  int32_t* pslot;        // [m * U + c] = group slot of class c under mask m
+  int32_t* gcnt;
+  const int32_t* goff;
+  int32_t* gcur;
+  int32_t* gmem;         // NM * U grouped classes, then the iota block
+  const i64* toff;       // policy terms (sorted by slot)
+  const int32_t* tval;
+  const int32_t* pmask;
+  i64* pstart;
+  int32_t* plen;
+  int NM;
+  int live;
+};
+struct JoinPair {
+  JoinSide s[2];
+};
+
+__device__ __forceinline__ int join_row(const JoinPair& pr, int y, int extra, int* m) {
+  const int r0 = pr.s[0].live ? pr.s[0].NM + extra : 0;
+  if (y < r0) { *m = y; return 0; }
+  *m = y - r0;
+  return 1;
+}
+
+// group id of class c under mask m = its table slot
+__global__ __launch_bounds__(TPB) void k_join_insert(JoinPair pr) {
+  int m;
+  const JoinSide a = join_row(pr, blockIdx.y, 0, &m) ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  const int m = blockIdx.y;
-  if (c >= U) return;
-  const int32_t* sl = mslot + moff[m];
-  const int ns = moff[m + 1] - moff[m];
-  int32_t* tab = table + (i64)m * T;
-  uint32_t s = proj_hash(cval, U, c, sl, ns) & (uint32_t)(T - 1);
+  if (c >= a.U) return;
+  const int32_t* sl = a.mslot + a.moff[m];
+  const int ns = a.moff[m + 1] - a.moff[m];
+  int32_t* tab = a.table + (i64)m * a.T;
+  const uint32_t tm = (uint32_t)(a.T - 1);
+  uint32_t s = proj_hash(a.cval, a.U, c, sl, ns) & tm;
   for (;;) {
-    int32_t cur = tab[s];   // plain read: see k_class_insert
+    int32_t cur = tab[s];   // plain read: see k_cls_insert
     if (cur < 0) {
       const int32_t prev = atomicCAS(&tab[s], -1, (int32_t)c);
-      if (prev < 0) { pslot[(i64)m * U + c] = (int32_t)s; return; }
+      if (prev < 0) break;
       cur = prev;
     }
     bool eq = true;
     for (int k = 0; k < ns; ++k) {
-      const int32_t* col = cval + (i64)sl[k] * U;
+      const int32_t* col = a.cval + (i64)sl[k] * a.U;
       if (col[cur] != col[c]) { eq = false; break; }
     }
-    if (eq) { pslot[(i64)m * U + c] = (int32_t)s; return; }
-    s = (s + 1) & (uint32_t)(T - 1);
+    if (eq) break;
+    s = (s + 1) & tm;
   }
+  a.pslot[(i64)m * a.U + c] = (int32_t)s;
 }
 
-__global__ __launch_bounds__(TPB) void k_group_count(const int32_t* __restrict__ pslot, i64 U,
-                                                     i64 T, int32_t* gcnt) {
+__global__ __launch_bounds__(TPB) void k_join_count(JoinPair pr) {
+  int m;
+  const JoinSide a = join_row(pr, blockIdx.y, 0, &m) ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  const int m = blockIdx.y;
-  const bool act = c < U;
-  (void)wave_agg_inc(gcnt, act ? (i64)m * T + pslot[(i64)m * U + c] : 0, act);
+  const bool act = c < a.U;
+  (void)wave_agg_inc(a.gcnt, act ? (i64)m * a.T + a.pslot[(i64)m * a.U + c] : 0, act);
 }
 
-__global__ __launch_bounds__(TPB) void k_group_fill(const int32_t* __restrict__ pslot, i64 U, i64 T,
-                                                    const int32_t* __restrict__ goff, int32_t* gcur,
-                                                    int32_t* __restrict__ gmem) {
+// grouped class lists; the extra row per side writes the iota block (the
+// class list of policies without terms)
+__global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr) {
+  int m;
+  const JoinSide a = join_row(pr, blockIdx.y, 1, &m) ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  const int m = blockIdx.y;
-  const bool act = c < U;
-  const i64 g = act ? (i64)m * T + pslot[(i64)m * U + c] : 0;
-  const int32_t r = wave_agg_inc(gcur, g, act);
-  if (act) gmem[goff[g] + r] = (int32_t)c;
-}
-
-__global__ __launch_bounds__(TPB) void k_iota(int32_t* __restrict__ out, i64 n) {
-  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i < n) out[i] = (int32_t)i;
+  if (m == a.NM) {
+    if (c < a.U) a.gmem[(i64)a.NM * a.U + c] = (int32_t)c;
+    return;
+  }
+  const bool act = c < a.U;
+  const i64 g = act ? (i64)m * a.T + a.pslot[(i64)m * a.U + c] : 0;
+  const int32_t r = wave_agg_inc(a.gcur, g, act);
+  if (act) a.gmem[a.goff[g] + r] = (int32_t)c;
 }
 
 // thread per policy: its matched classes = gmem[pstart, pstart + plen)
 //   pmask -1: contradictory terms (matches nothing); -2: no terms (all
-//   classes: the iota block at all_start); terms sorted by slot = mask order
-__global__ __launch_bounds__(TPB) void k_pol_match(i64 P, const i64* __restrict__ toff,
-                                                   const int32_t* __restrict__ tval,
-                                                   const int32_t* __restrict__ pmask,
-                                                   const int32_t* __restrict__ moff,
-                                                   const int32_t* __restrict__ mslot,
-                                                   const int32_t* __restrict__ cval, i64 U,
-                                                   const int32_t* __restrict__ table, i64 T,
-                                                   const int32_t* __restrict__ goff,
-                                                   i64 all_start, i64* __restrict__ pstart,
-                                                   int32_t* __restrict__ plen) {
+//   classes: the iota block); terms sorted by slot = mask order
+__global__ __launch_bounds__(TPB) void k_join_match(i64 P, JoinPair pr) {
+  const JoinSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (p >= P) return;
-  const int m = pmask[p];
+  if (!a.live || p >= P) return;
+  const int m = a.pmask[p];
   i64 st = 0;
   int32_t len = 0;
   if (m == -2) {
-    st = all_start;
-    len = (int32_t)U;
+    st = (i64)a.NM * a.U;
+    len = (int32_t)a.U;
   } else if (m >= 0) {
-    const i64 t0 = toff[p];
-    const int32_t* sl = mslot + moff[m];
-    const int ns = moff[m + 1] - moff[m];
+    const i64 t0 = a.toff[p];
+    const int32_t* sl = a.mslot + a.moff[m];
+    const int ns = a.moff[m + 1] - a.moff[m];
     bool possible = true;
     uint32_t h = 0x2545f491u;
     for (int k = 0; k < ns; ++k) {
-      const int32_t v = tval[t0 + k];
+      const int32_t v = a.tval[t0 + k];
       possible = possible && v >= 0;
       h = hmix(h, (uint32_t)v);
     }
-    if (possible && U > 0) {
-      const int32_t* tab = table + (i64)m * T;
-      uint32_t s = hfin(h) & (uint32_t)(T - 1);
+    if (possible && a.U > 0) {
+      const int32_t* tab = a.table + (i64)m * a.T;
+      const uint32_t tm = (uint32_t)(a.T - 1);
+      uint32_t s = hfin(h) & tm;
       for (;;) {
         const int32_t cur = tab[s];
         if (cur < 0) break;
         bool eq = true;
         for (int k = 0; k < ns; ++k)
-          if (cval[(i64)sl[k] * U + cur] != tval[t0 + k]) { eq = false; break; }
+          if (a.cval[(i64)sl[k] * a.U + cur] != a.tval[t0 + k]) { eq = false; break; }
         if (eq) {
-          const i64 g = (i64)m * T + s;
-          st = goff[g];
-          len = goff[g + 1] - goff[g];
+          const i64 g = (i64)m * a.T + s;
+          st = a.goff[g];
+          len = a.goff[g + 1] - a.goff[g];
           break;
         }
-        s = (s + 1) & (uint32_t)(T - 1);
+        s = (s + 1) & tm;
       }
     }
   }
-  pstart[p] = st;
-  plen[p] = len;
+  a.pstart[p] = st;
+  a.plen[p] = len;
 }
 
 // dense fallback (too many distinct masks): per-policy class lists from the

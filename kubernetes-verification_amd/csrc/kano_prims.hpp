@@ -113,54 +113,97 @@ __device__ __forceinline__ void lb_store(u64* p, u64 v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename Tin, typename Tout>
-__global__ __launch_bounds__(TPB) void k_scan_lb(const Tin* __restrict__ in, i64 n,
-                                                 Tout* __restrict__ out, u64* status,
+// Up to MAX_SCAN_JOBS independent scans in one launch (blockIdx.y = job),
+// int32 or int64 on either side, arithmetic in int64.  Job j's ticket and
+// tile states live at status[st], status[st + 1 + t].
+struct ScanJob {
+  const void* in;
+  void* out;
+  i64 n;
+  i64 st;
+  int in64, out64;
+};
+constexpr int MAX_SCAN_JOBS = 8;
+struct ScanJobs {
+  ScanJob j[MAX_SCAN_JOBS];
+  int count;
+};
+
+__global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
                                                  u64* __restrict__ clear, i64 nclear) {
-  __shared__ Tout sm[4];
+  __shared__ i64 sm[4];
   __shared__ i64 s_tile;
-  __shared__ Tout s_prefix;
-  for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < nclear; i += (i64)gridDim.x * TPB)
-    clear[i] = 0;
+  __shared__ i64 s_prefix;
+  const i64 lin = (i64)blockIdx.y * gridDim.x + blockIdx.x;
+  const i64 nthr = (i64)gridDim.x * gridDim.y * TPB;
+  for (i64 i = lin * TPB + threadIdx.x; i < nclear; i += nthr) clear[i] = 0;
+  ScanJob jb = jobs.j[0];   // select, not a dynamic index (kernarg stays in SGPRs)
+#pragma unroll
+  for (int q = 1; q < MAX_SCAN_JOBS; ++q)
+    if ((int)blockIdx.y == q) jb = jobs.j[q];
+  const i64 tiles = (jb.n + SCAN_TILE - 1) / SCAN_TILE;
+  if (jb.n == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (jb.out64) static_cast<i64*>(jb.out)[0] = 0;
+      else static_cast<int32_t*>(jb.out)[0] = 0;
+    }
+    return;
+  }
+  u64* st = status + jb.st;
   if (threadIdx.x == 0)
-    s_tile = (i64)__hip_atomic_fetch_add(status, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = (i64)__hip_atomic_fetch_add(st, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const i64 tile = s_tile;
+  if (tile >= tiles) return;
   const i64 base = tile * SCAN_TILE + (i64)threadIdx.x * SCAN_ITEMS;
-  Tout v[SCAN_ITEMS];
-  Tout s = 0;
+  i64 v[SCAN_ITEMS];
+  i64 s = 0;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
-    v[k] = (base + k < n) ? (Tout)in[base + k] : (Tout)0;
+    const i64 x = base + k;
+    v[k] = x < jb.n ? (jb.in64 ? static_cast<const i64*>(jb.in)[x]
+                               : (i64) static_cast<const int32_t*>(jb.in)[x])
+                    : 0;
     s += v[k];
   }
-  Tout tot;
-  Tout pre = block_excl_scan(s, sm, tot);
+  i64 tot;
+  i64 pre = block_excl_scan(s, sm, tot);
   if (threadIdx.x == 0) {
-    u64* st = status + 1;
-    Tout excl = 0;
+    u64* ts = st + 1;
+    i64 excl = 0;
     if (tile == 0) {
-      lb_store(&st[0], LB_INC | ((u64)tot & LB_VAL));
+      lb_store(&ts[0], LB_INC | ((u64)tot & LB_VAL));
     } else {
-      lb_store(&st[tile], LB_AGG | ((u64)tot & LB_VAL));
+      lb_store(&ts[tile], LB_AGG | ((u64)tot & LB_VAL));
       for (i64 q = tile - 1;; --q) {
         u64 w;
-        do { w = lb_load(&st[q]); } while (w == 0);
-        excl += (Tout)(w & LB_VAL);
+        do { w = lb_load(&ts[q]); } while (w == 0);
+        excl += (i64)(w & LB_VAL);
         if ((w & ~LB_VAL) == LB_INC) break;
       }
-      lb_store(&st[tile], LB_INC | ((u64)(excl + tot) & LB_VAL));
+      lb_store(&ts[tile], LB_INC | ((u64)(excl + tot) & LB_VAL));
     }
     s_prefix = excl;
   }
   __syncthreads();
   pre += s_prefix;
+  if (jb.out64) {
+    i64* o = static_cast<i64*>(jb.out);
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    if (base + k < n) out[base + k] = pre;
-    pre += v[k];
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      if (base + k < jb.n) o[base + k] = pre;
+      pre += v[k];
+    }
+    if (tile == tiles - 1 && threadIdx.x == TPB - 1) o[jb.n] = pre;
+  } else {
+    int32_t* o = static_cast<int32_t*>(jb.out);
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      if (base + k < jb.n) o[base + k] = (int32_t)pre;
+      pre += v[k];
+    }
+    if (tile == tiles - 1 && threadIdx.x == TPB - 1) o[jb.n] = (int32_t)pre;
   }
-  if (tile == (i64)gridDim.x - 1 && threadIdx.x == TPB - 1) out[n] = pre;
 }
 
 // several fills in one launch: (ptr, count of 32-bit words, value)
