@@ -285,6 +285,7 @@ def main():
         dist.all_reduce(t)
         shadow_cnt = int(t.item())
     out = None
+    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "pod-pairs/s", "n_gpus": world,
@@ -299,7 +300,8 @@ def main():
                                  ("" if args.no_shadow else ", policy_shadow")},
             "roofline": {"bound": "hbm", "kernel": "k_rows", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "alg_bytes_per_launch": alg_bytes,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": k_rows_ms},
             "stages_ms_last_step": {k: round(v, 4) for k, v in step.stages.items()},
             "step_ms": {"min": round(float(step_ms.min()), 4),
@@ -323,6 +325,20 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(config):
+    """HBM bytes per k_rows launch from the committed PMC summary of this
+    workload (scripts/pmc.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3
+    passes of this same bench command, FETCH doubled for gfx950)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"]["kano::k_rows"]
+        return float(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError, TypeError):
+        return None, None
 
 
 def _cpu_model():
