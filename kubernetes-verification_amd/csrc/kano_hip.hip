@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -84,7 +85,8 @@ struct kano_ctx {
   bool cols_valid = false;   // color/colnand describe M
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_timed = false;
-  int ch = 16;
+  int ch = 16;               // member rows per k_rows work item
+  int ld_align = 2;          // M row pitch multiple, in words
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -1041,6 +1043,24 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  // tuning overrides for experiments: KANO_TUNE="ch=32,align=16"
+  if (const char* t = getenv("KANO_TUNE")) {
+    std::string spec(t);
+    size_t pos = 0;
+    while (pos < spec.size()) {
+      size_t end = spec.find(',', pos);
+      if (end == std::string::npos) end = spec.size();
+      const std::string kv = spec.substr(pos, end - pos);
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos) {
+        const std::string k = kv.substr(0, eq);
+        const int v = atoi(kv.c_str() + eq + 1);
+        if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
+        if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
+      }
+      pos = end + 1;
+    }
+  }
   if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess) {
@@ -1124,7 +1144,8 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   KCHK(hipSetDevice(ctx->device));
   ctx->n = n;
   ctx->W = (n + 63) / 64;
-  ctx->ldM = std::max<i64>(2, (ctx->W + 1) & ~(i64)1);
+  ctx->ldM = std::max<i64>(ctx->ld_align,
+                           (ctx->W + ctx->ld_align - 1) / ctx->ld_align * ctx->ld_align);
   ctx->ncols = ncols;
   KTRY(dalloc(ctx, ctx->pv, sizeof(int32_t) * std::max<i64>(1, n * ncols)));
   if (n * ncols > 0)
