@@ -71,6 +71,13 @@ struct SideMatch {
   i64 T = 0;
 };
 
+// size slots (u64) written by the kernels that produce them (scan totals,
+// counters) and read by the host with one copy per sync
+enum {
+  SZ_UR = 0, SZ_UA, SZ_NNZ_SEL, SZ_NNZ_ALC, SZ_NNZ_ALW, SZ_NFLAGS, SZ_WI, SZ_HEAVY, SZ_MAXSEL,
+  SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 16
+};
+
 struct kano_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -106,8 +113,9 @@ struct kano_ctx {
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
-  DBuf gdev, icnt, ioff, sysrow, err_dev, idxd;     // gathered scalars, index-list block counts / offsets
-  u64* ghost = nullptr;      // pinned landing buffer for gathered scalars
+  DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
+  DBuf icnt, ioff, sysrow, idxd;
+  u64* ghost = nullptr;      // pinned landing buffer for the size slots
 
   hipEvent_t ev[10] = {};
   // the matrix write (k_rows) runs on its own stream beside the checks, which
@@ -203,13 +211,14 @@ struct ScanBatch {
   i64 slots = 0, maxt = 1;
   explicit ScanBatch(kano_ctx* c) : ctx(c) { jobs.count = 0; }
   template <typename Tin, typename Tout>
-  int add(const Tin* in, i64 n, Tout* out) {
+  int add(const Tin* in, i64 n, Tout* out, int total_slot = -1) {
     static_assert(sizeof(Tin) == 4 || sizeof(Tin) == 8, "int32 / int64 scans");
     static_assert(sizeof(Tout) == 4 || sizeof(Tout) == 8, "int32 / int64 scans");
     if (jobs.count == MAX_SCAN_JOBS) KTRY(run());
     ScanJob& j = jobs.j[jobs.count++];
     j.in = in;
     j.out = out;
+    j.total = total_slot >= 0 ? P_<u64>(ctx->sizes) + total_slot : nullptr;
     j.n = n;
     j.st = slots;
     j.in64 = sizeof(Tin) == 8;
@@ -248,6 +257,12 @@ struct FillBatch {
   kano_ctx* ctx;
   explicit FillBatch(kano_ctx* c) : ctx(c) { jobs.count = 0; }
   int add(DBuf& b, size_t bytes, uint32_t value);
+  int add_raw(void* p, size_t bytes, uint32_t value) {
+    if (bytes == 0) return 0;
+    if (jobs.count == MAX_FILLS) KTRY(run());
+    jobs.j[jobs.count++] = FillJob{static_cast<uint32_t*>(p), (i64)(bytes / 4), value};
+    return 0;
+  }
   int run();
 };
 
@@ -275,28 +290,14 @@ int sync(kano_ctx* ctx) {
   return 0;
 }
 
-// device scalars read back with one kernel, one copy and one sync
-struct Gather {
-  GatherJobs g{};
-  kano_ctx* ctx;
-  explicit Gather(kano_ctx* c) : ctx(c) { g.count = 0; }
-  void add(const void* p, bool wide) {
-    g.src[g.count] = p;
-    g.wide[g.count] = wide ? 1 : 0;
-    ++g.count;
-  }
-  int run(i64* out) {
-    if (g.count == 0) return sync(ctx);
-    KTRY(dalloc(ctx, ctx->gdev, sizeof(u64) * MAX_GATHER));
-    hipLaunchKernelGGL(k_gather, dim3(1), dim3(64), 0, ctx->stream, g, P_<u64>(ctx->gdev));
-    KLAUNCH();
-    KCHK(hipMemcpyAsync(ctx->ghost, ctx->gdev.p, sizeof(u64) * g.count, hipMemcpyDeviceToHost,
-                        ctx->stream));
-    KTRY(sync(ctx));
-    for (int k = 0; k < g.count; ++k) out[k] = (i64)ctx->ghost[k];
-    return 0;
-  }
-};
+// size slots [first, first + count) to the host: one copy, one sync
+int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
+  KCHK(hipMemcpyAsync(ctx->ghost, P_<u64>(ctx->sizes) + first, sizeof(u64) * count,
+                      hipMemcpyDeviceToHost, ctx->stream));
+  KTRY(sync(ctx));
+  for (int k = 0; k < count; ++k) out[k] = (i64)ctx->ghost[k];
+  return 0;
+}
 
 i64 rows_local(const kano_ctx* ctx) { return ctx->r1 - ctx->r0; }
 
@@ -309,17 +310,12 @@ i64 table_size(i64 n) {
 
 int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   const i64 n = ctx->n, T = table_size(n);
-  cs.KS = (int)cs.keys.size();
-  KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, cs.keys.size())));
   KTRY(dalloc(ctx, cs.table, sizeof(int32_t) * T));
   KTRY(dalloc(ctx, cs.smin, sizeof(int32_t) * T));
   KTRY(dalloc(ctx, cs.slot_of, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, cs.flag, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, cs.cid, sizeof(int32_t) * (n + 1)));
   KTRY(dalloc(ctx, cs.cls, sizeof(int32_t) * std::max<i64>(1, n)));
-  if (cs.KS > 0)
-    KCHK(hipMemcpyAsync(cs.keys_d.p, cs.keys.data(), sizeof(int32_t) * cs.KS,
-                        hipMemcpyHostToDevice, ctx->stream));
   KTRY(fb.add(cs.table, sizeof(int32_t) * T, 0xffffffffu));
   KTRY(fb.add(cs.smin, sizeof(int32_t) * T, 0x7fffffffu));
   return 0;
@@ -361,8 +357,8 @@ int classify_phase1(kano_ctx* ctx) {
     KLAUNCH();
   }
   ScanBatch sb(ctx);
-  KTRY(sb.add(P_<int32_t>(ctx->rc.flag), n, P_<int32_t>(ctx->rc.cid)));
-  KTRY(sb.add(P_<int32_t>(ctx->cc.flag), n, P_<int32_t>(ctx->cc.cid)));
+  KTRY(sb.add(P_<int32_t>(ctx->rc.flag), n, P_<int32_t>(ctx->rc.cid), SZ_UR));
+  KTRY(sb.add(P_<int32_t>(ctx->cc.flag), n, P_<int32_t>(ctx->cc.cid), SZ_UA));
   return sb.run();
 }
 
@@ -535,18 +531,15 @@ int do_front(kano_ctx* ctx, int path) {
   ctx->cc.m1 = ctx->n;
   {
     FillBatch fb(ctx);
+    KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
+    KTRY(fb.add(ctx->sizes, sizeof(u64) * SZ_SLOTS, 0u));
     KTRY(classify_alloc1(ctx, ctx->rc, fb));
     KTRY(classify_alloc1(ctx, ctx->cc, fb));
     KTRY(fb.run());
   }
   KTRY(classify_phase1(ctx));
   i64 u[2] = {0, 0};
-  {
-    Gather ga(ctx);
-    ga.add(P_<int32_t>(ctx->rc.cid) + ctx->n, false);
-    ga.add(P_<int32_t>(ctx->cc.cid) + ctx->n, false);
-    KTRY(ga.run(u));                                 // host sync 1 of the build
-  }
+  KTRY(read_slots(ctx, SZ_UR, 2, u));               // host sync 1 of the build
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -569,12 +562,10 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(dalloc(ctx, ctx->wicnt, sizeof(int32_t) * std::max<i64>(1, Ur)));
     KTRY(dalloc(ctx, ctx->hflag, sizeof(int32_t) * std::max<i64>(1, Ur)));
     KTRY(dalloc(ctx, ctx->sq, sizeof(i64) * std::max<i64>(1, Ur)));
-    KTRY(dalloc(ctx, ctx->maxs, sizeof(int32_t) * 4));
     KTRY(dalloc(ctx, ctx->soffc, sizeof(i64) * (Ur + 1)));
     KTRY(dalloc(ctx, ctx->wioff, sizeof(int32_t) * (Ur + 1)));
     KTRY(dalloc(ctx, ctx->hoff, sizeof(int32_t) * (Ur + 1)));
     KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (Ur + 1)));
-    KTRY(fb.add(ctx->maxs, 16, 0u));
     KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
     KTRY(fb.run());
@@ -610,41 +601,32 @@ int do_front(kano_ctx* ctx, int path) {
     a.wicnt = P_<int32_t>(ctx->wicnt);
     a.hflag = P_<int32_t>(ctx->hflag);
     a.sq = P_<i64>(ctx->sq);
-    a.maxs = P_<int32_t>(ctx->maxs);
+    a.maxs = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_MAXSEL);  // low half
     hipLaunchKernelGGL(k_class_plan, dim3(nblk(Ur)), dim3(TPB), 0, ctx->stream, a);
     KLAUNCH();
   }
   ScanBatch sb(ctx);
-  KTRY(sb.add(P_<int32_t>(ctx->nca), P, P_<i64>(ctx->alcoff)));
-  KTRY(sb.add(P_<int32_t>(ctx->acnt), P, P_<i64>(ctx->aloff)));
-  KTRY(sb.add(P_<int32_t>(ctx->scnt), Ur, P_<i64>(ctx->soffc)));
-  KTRY(sb.add(P_<int32_t>(ctx->wicnt), Ur, P_<int32_t>(ctx->wioff)));
-  KTRY(sb.add(P_<int32_t>(ctx->hflag), Ur, P_<int32_t>(ctx->hoff)));
-  KTRY(sb.add(P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff)));
+  KTRY(sb.add(P_<int32_t>(ctx->nca), P, P_<i64>(ctx->alcoff), SZ_NNZ_ALC));
+  KTRY(sb.add(P_<int32_t>(ctx->acnt), P, P_<i64>(ctx->aloff), SZ_NNZ_ALW));
+  KTRY(sb.add(P_<int32_t>(ctx->scnt), Ur, P_<i64>(ctx->soffc), SZ_NNZ_SEL));
+  KTRY(sb.add(P_<int32_t>(ctx->wicnt), Ur, P_<int32_t>(ctx->wioff), SZ_WI));
+  KTRY(sb.add(P_<int32_t>(ctx->hflag), Ur, P_<int32_t>(ctx->hoff), SZ_HEAVY));
+  KTRY(sb.add(P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff), SZ_NFLAGS));
   KTRY(sb.run());
   return 0;
 }
 
 // host sync 2 of the build: every list size at once
 int read_sizes(kano_ctx* ctx) {
-  const i64 U = ctx->rc.U, P = ctx->P;
-  Gather ga(ctx);
-  ga.add(P_<i64>(ctx->soffc) + U, true);
-  ga.add(P_<i64>(ctx->alcoff) + P, true);
-  ga.add(P_<i64>(ctx->aloff) + P, true);
-  ga.add(P_<i64>(ctx->pfoff) + U, true);
-  ga.add(P_<int32_t>(ctx->wioff) + U, false);
-  ga.add(P_<int32_t>(ctx->hoff) + U, false);
-  ga.add(P_<int32_t>(ctx->maxs), false);
-  i64 v[7];
-  KTRY(ga.run(v));
-  ctx->nnz_sel = v[0];
-  ctx->nnz_alc = v[1];
-  ctx->nnz_alw = v[2];
-  ctx->nflags = v[3];
-  ctx->wi_total = v[4];
-  ctx->heavy_count = v[5];
-  ctx->max_sel = (int)v[6];
+  i64 v[SZ_MAXSEL - SZ_NNZ_SEL + 1];
+  KTRY(read_slots(ctx, SZ_NNZ_SEL, SZ_MAXSEL - SZ_NNZ_SEL + 1, v));
+  ctx->nnz_sel = v[SZ_NNZ_SEL - SZ_NNZ_SEL];
+  ctx->nnz_alc = v[SZ_NNZ_ALC - SZ_NNZ_SEL];
+  ctx->nnz_alw = v[SZ_NNZ_ALW - SZ_NNZ_SEL];
+  ctx->nflags = v[SZ_NFLAGS - SZ_NNZ_SEL];
+  ctx->wi_total = v[SZ_WI - SZ_NNZ_SEL];
+  ctx->heavy_count = v[SZ_HEAVY - SZ_NNZ_SEL];
+  ctx->max_sel = (int)(v[SZ_MAXSEL - SZ_NNZ_SEL] & 0xffffffff);
   return 0;
 }
 
@@ -928,7 +910,8 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
-  KTRY(dalloc(ctx, ctx->err_dev, 16));
+  KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
+  int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
   if (n == 0 || rows_local(ctx) == 0 || W == 0 || ctx->rows_dirty)
     KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
@@ -953,7 +936,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
     FillBatch fb(ctx);
-    KTRY(fb.add(ctx->err_dev, 16, 0u));
+    KTRY(fb.add_raw(err, sizeof(u64), 0u));
     KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
     KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
     KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
@@ -963,7 +946,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     const i64 rl = rows_local(ctx);
     hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
-                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), P_<int32_t>(ctx->err_dev));
+                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
     KLAUNCH();
     hipLaunchKernelGGL(k_cross_mc, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.mcnt),
@@ -976,7 +959,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
                        ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
-                       P_<u64>(ctx->cross), P_<int32_t>(ctx->err_dev));
+                       P_<u64>(ctx->cross), err);
     KLAUNCH();
     return 0;
   }
@@ -1067,7 +1050,7 @@ int kano_create(int device, kano_ctx** out) {
     kano_destroy(ctx);
     return -EIO;
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->ghost), sizeof(u64) * MAX_GATHER,
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->ghost), sizeof(u64) * SZ_SLOTS,
                     hipHostMallocDefault) != hipSuccess) {
     kano_destroy(ctx);
     return -ENOMEM;
@@ -1103,8 +1086,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
-                  &ctx->tcnt,   &ctx->toff,    &ctx->gdev,    &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow, &ctx->wicls,   &ctx->err_dev, &ctx->idxd};
+                  &ctx->tcnt,   &ctx->toff,    &ctx->sizes,   &ctx->icnt,      &ctx->ioff,
+                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1179,6 +1162,10 @@ static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t*
       slot[c] = (int32_t)cs.keys.size();
       cs.keys.push_back(c);
     }
+  cs.KS = (int)cs.keys.size();
+  KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, cs.keys.size())));
+  if (cs.KS > 0)   // uploaded once per policy set, not per build
+    KCHK(hipMemcpy(cs.keys_d.p, cs.keys.data(), sizeof(int32_t) * cs.KS, hipMemcpyHostToDevice));
   std::vector<i64> toff(P + 1, 0);
   std::vector<int32_t> tslot, tval, pmask(std::max<i64>(1, P), -1), moff(1, 0), mslot;
   std::vector<std::vector<int32_t>> masks;
@@ -1541,9 +1528,10 @@ namespace {
 // policy_shadow up to its one sync: flags, per-class counts, per-pod offsets;
 // the caller gathers toff[nt] (list length) and poff[rl] (pairs) with its own
 // scalars
-int shadow_front(kano_ctx* ctx, Gather& ga) {
+int shadow_front(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, rl = rows_local(ctx), nf = ctx->nflags;
   const i64 nt = (nf + SH_TILE - 1) / SH_TILE;
+  KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
   KCHK(hipEventRecord(ctx->ev[5], ctx->stream));
   KTRY(dalloc(ctx, ctx->flags, nf + 16));
   KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, U)));
@@ -1577,7 +1565,7 @@ int shadow_front(kano_ctx* ctx, Gather& ga) {
   }
   {
     ScanBatch sb(ctx);
-    KTRY(sb.add(P_<i64>(ctx->tcnt), nt, P_<i64>(ctx->toff)));
+    KTRY(sb.add(P_<i64>(ctx->tcnt), nt, P_<i64>(ctx->toff), SZ_NL));
     KTRY(sb.add(P_<i64>(ctx->T), U, P_<i64>(ctx->loff)));
     KTRY(sb.run());
   }
@@ -1587,9 +1575,11 @@ int shadow_front(kano_ctx* ctx, Gather& ga) {
                        P_<i64>(ctx->tp));
     KLAUNCH();
   }
-  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->tp), rl, P_<i64>(ctx->poff))));
-  ga.add(P_<i64>(ctx->toff) + nt, true);
-  ga.add(P_<i64>(ctx->poff) + rl, true);
+  {
+    ScanBatch sb(ctx);
+    KTRY(sb.add(P_<i64>(ctx->tp), rl, P_<i64>(ctx->poff), SZ_PAIRS));
+    KTRY(sb.run());
+  }
   return 0;
 }
 
@@ -1605,7 +1595,7 @@ int shadow_back(kano_ctx* ctx, i64 nl, i64 total) {
     KLAUNCH();
   }
   if (rl > 0 && total > 0) {
-    hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl, TPB / 64)), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
                        P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out));
     KLAUNCH();
@@ -1621,10 +1611,9 @@ extern "C" {
 
 int kano_shadow(kano_ctx* ctx, int64_t* count) {
   KTRY(ensure_built(ctx));
-  Gather ga(ctx);
-  KTRY(shadow_front(ctx, ga));
+  KTRY(shadow_front(ctx));
   i64 tot[2] = {0, 0};
-  KTRY(ga.run(tot));
+  KTRY(read_slots(ctx, SZ_NL, 2, tot));
   KTRY(shadow_back(ctx, tot[0], tot[1]));
   if (count) *count = tot[1];
   return 0;
@@ -1768,36 +1757,40 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   ir.inv[3] = 1;
   const i64 nb4 = 4 * ir.nb;
   KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * nb4));
-  KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * (nb4 + 1)));
+  KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * (nb4 + 4)));
   KTRY(dalloc(ctx, ctx->idxd, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));
   hipLaunchKernelGGL(k_idx_count, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
                      P_<i64>(ctx->icnt));
   KLAUNCH();
-  KTRY((scan_excl<i64, i64>(ctx, P_<i64>(ctx->icnt), nb4, P_<i64>(ctx->ioff))));
+  {
+    ScanBatch sb(ctx);   // one job per row; row totals land in SZ_IDX0..3
+    for (int r = 0; r < 4; ++r)
+      KTRY(sb.add(P_<i64>(ctx->icnt) + r * ir.nb, ir.nb, P_<i64>(ctx->ioff) + r * (ir.nb + 1),
+                  SZ_IDX0 + r));
+    KTRY(sb.run());
+  }
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
   hipLaunchKernelGGL(k_idx_write, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
-                     P_<i64>(ctx->ioff), idx_dev);
+                     P_<i64>(ctx->ioff), ir.nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
   KLAUNCH();
-  // policy_shadow up to its size read; then the matrix write on stream2 runs
-  // beside the host sync and the short tail (pair emission, copies)
-  Gather ga(ctx);
-  for (int r = 0; r <= 4; ++r) ga.add(P_<i64>(ctx->ioff) + r * ir.nb, true);
-  if (shadow_count) KTRY(shadow_front(ctx, ga));
+  // policy_shadow up to its size read
+  if (shadow_count) KTRY(shadow_front(ctx));
   KTRY(launch_rows(ctx));
-  // one sync for the list sizes (and policy_shadow's sizes)
-  const int ishadow = 5, ierr = shadow_count ? 7 : 5;
-  if (cross_on) ga.add(P_<int32_t>(ctx->err_dev), false);
-  i64 v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  KTRY(ga.run(v));
-  if (cross_on && v[ierr])
+  // one sync for the list sizes, policy_shadow's sizes and the group check
+  i64 v[SZ_ERR - SZ_NL + 1];
+  KTRY(read_slots(ctx, SZ_NL, SZ_ERR - SZ_NL + 1, v));
+  if (cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff))
     return fail(ctx, -EINVAL, "kano_verify: a group id lies outside [0, ngroups)");
-  for (int r = 0; r < 4; ++r) counts[r] = v[r + 1] - v[r];
+  i64 nidx = 0;
+  for (int r = 0; r < 4; ++r) {
+    counts[r] = v[SZ_IDX0 - SZ_NL + r];
+    nidx += counts[r];
+  }
   if (!have_sys) counts[3] = -1;
-  const i64 nidx = v[4];
   i64 total = 0;
   if (shadow_count) {
-    total = v[ishadow + 1];
-    KTRY(shadow_back(ctx, v[ishadow], total));
+    total = v[SZ_PAIRS - SZ_NL];
+    KTRY(shadow_back(ctx, v[0], total));
     ctx->shadow_total = total;
     *shadow_count = total;
   }

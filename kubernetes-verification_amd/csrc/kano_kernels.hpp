@@ -1273,19 +1273,18 @@ __global__ __launch_bounds__(TPB) void k_shadow_podcount(const int32_t* __restri
   tp[i - r0] = loff[c + 1] - loff[c];
 }
 
-// one wave per pod: out[poff[i] ...] = L_cls(i)
+// one thread per pod: out[poff[i] ...] = L_cls(i) (most pods emit 0-3 pairs)
 __global__ __launch_bounds__(TPB) void k_shadow_emit(const int32_t* __restrict__ cls, i64 r0,
                                                      i64 r1, const i64* __restrict__ loff,
                                                      const int2* __restrict__ L,
                                                      const i64* __restrict__ poff,
                                                      int2* __restrict__ out) {
-  const i64 i = r0 + (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
   if (i >= r1) return;
-  const int lane = threadIdx.x & 63;
   const int32_t c = cls[i];
   const i64 l0 = loff[c], len = loff[c + 1] - l0;
   const i64 o = poff[i - r0];
-  for (i64 k = lane; k < len; k += 64) out[o + k] = L[l0 + k];
+  for (i64 k = 0; k < len; ++k) out[o + k] = L[l0 + k];
 }
 
 // ===========================================================================
@@ -1315,14 +1314,18 @@ __global__ __launch_bounds__(TPB) void k_idx_count(IdxRows a, i64* __restrict__ 
   if (threadIdx.x == 0) bcnt[r * a.nb + blockIdx.x] = tot;
 }
 
+// row r's lists start after the totals of rows < r (rowtot: 4 size slots)
 __global__ __launch_bounds__(TPB) void k_idx_write(IdxRows a, const i64* __restrict__ boff,
+                                                   i64 ldo, const u64* __restrict__ rowtot,
                                                    int32_t* __restrict__ idx) {
   __shared__ i64 sm[4];
   const int r = blockIdx.y;
   const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
   u64 v = idx_word(a, r, w);
+  i64 row0 = 0;
+  for (int q = 0; q < r; ++q) row0 += (i64)rowtot[q];
   i64 tot;
-  i64 pos = block_excl_scan((i64)__popcll(v), sm, tot) + boff[r * a.nb + blockIdx.x];
+  i64 pos = block_excl_scan((i64)__popcll(v), sm, tot) + row0 + boff[r * ldo + blockIdx.x];
   while (v) {
     const int b = __ffsll((long long)v) - 1;
     idx[pos++] = (int32_t)(w * 64 + b);

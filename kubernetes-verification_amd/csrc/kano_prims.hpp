@@ -119,6 +119,7 @@ __device__ __forceinline__ void lb_store(u64* p, u64 v) {
 struct ScanJob {
   const void* in;
   void* out;
+  u64* total;   // nullable: the total also lands here (a host-read size slot)
   i64 n;
   i64 st;
   int in64, out64;
@@ -146,6 +147,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       if (jb.out64) static_cast<i64*>(jb.out)[0] = 0;
       else static_cast<int32_t*>(jb.out)[0] = 0;
+      if (jb.total) *jb.total = 0;
     }
     return;
   }
@@ -194,7 +196,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       if (base + k < jb.n) o[base + k] = pre;
       pre += v[k];
     }
-    if (tile == tiles - 1 && threadIdx.x == TPB - 1) o[jb.n] = pre;
+    if (tile == tiles - 1 && threadIdx.x == TPB - 1) {
+      o[jb.n] = pre;
+      if (jb.total) *jb.total = (u64)pre;
+    }
   } else {
     int32_t* o = static_cast<int32_t*>(jb.out);
 #pragma unroll
@@ -202,7 +207,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       if (base + k < jb.n) o[base + k] = (int32_t)pre;
       pre += v[k];
     }
-    if (tile == tiles - 1 && threadIdx.x == TPB - 1) o[jb.n] = (int32_t)pre;
+    if (tile == tiles - 1 && threadIdx.x == TPB - 1) {
+      o[jb.n] = (int32_t)pre;
+      if (jb.total) *jb.total = (u64)pre;
+    }
   }
 }
 
@@ -225,20 +233,6 @@ __global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
     const i64 nw = jobs.j[q].words;
     for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < nw; i += stride) p[i] = v;
   }
-}
-
-// several device scalars gathered into one buffer (one D2H copy per sync)
-constexpr int MAX_GATHER = 16;
-struct GatherJobs {
-  const void* src[MAX_GATHER];
-  int32_t wide[MAX_GATHER];   // 1: 64-bit source, 0: non-negative 32-bit source
-  int count;
-};
-__global__ void k_gather(GatherJobs g, u64* __restrict__ dst) {
-  const int k = threadIdx.x;
-  if (k < g.count)
-    dst[k] = g.wide[k] ? *static_cast<const u64*>(g.src[k])
-                       : (u64)(uint32_t)*static_cast<const int32_t*>(g.src[k]);
 }
 
 // atomicAdd(&ctr[key], 1) for every active lane, with the lanes that share
