@@ -93,6 +93,7 @@ struct kano_ctx {
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_timed = false;
   int ch = 16;               // member rows per k_rows work item
+  int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
@@ -797,7 +798,7 @@ int launch_rows(kano_ctx* ctx) {
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
   }
-  const int cww = (int)std::min<i64>(ldM, MAX_CWW);
+  const int cww = (int)std::min<i64>(ldM, ctx->cww_max);
   const unsigned ncc = (unsigned)((ldM + cww - 1) / cww);
   RowsArgs a{};
   a.wioff = P_<int32_t>(ctx->wioff);
@@ -1039,6 +1040,7 @@ int kano_create(int device, kano_ctx** out) {
         const std::string k = kv.substr(0, eq);
         const int v = atoi(kv.c_str() + eq + 1);
         if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
+        if (k == "cww" && v >= 256 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }
       pos = end + 1;
