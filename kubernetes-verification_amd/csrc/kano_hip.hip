@@ -94,7 +94,8 @@ struct kano_ctx {
   bool rows_timed = false;
   int ch = 16;               // member rows per k_rows work item
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
-  int ld_align = 16;         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
+  int ld_align = 16;
+  int pitch_mul = 1;         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -798,8 +799,9 @@ int launch_rows(kano_ctx* ctx) {
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
   }
-  const int cww = (int)std::min<i64>(ldM, ctx->cww_max);
-  const unsigned ncc = (unsigned)((ldM + cww - 1) / cww);
+  const i64 wW = ldM / ctx->pitch_mul;
+  const int cww = (int)std::min<i64>(wW, ctx->cww_max);
+  const unsigned ncc = (unsigned)((wW + cww - 1) / cww);
   RowsArgs a{};
   a.wioff = P_<int32_t>(ctx->wioff);
   a.wicls = P_<int32_t>(ctx->wicls);
@@ -814,6 +816,7 @@ int launch_rows(kano_ctx* ctx) {
   a.hflag = ctx->heavy_count > 0 ? P_<int32_t>(ctx->hflag) : nullptr;
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
+  a.wW = ldM / ctx->pitch_mul;
   a.r0 = ctx->r0;
   a.n = n;
   a.W = W;
@@ -890,6 +893,7 @@ int recompute_cols(kano_ctx* ctx) {
   a.hflag = mem + rl;  // every row "prebuilt": copy + column fold, no writes
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
+  a.wW = ldM / ctx->pitch_mul;
   a.r0 = ctx->r0;
   a.n = ctx->n;
   a.W = W;
@@ -1041,6 +1045,7 @@ int kano_create(int device, kano_ctx** out) {
         const int v = atoi(kv.c_str() + eq + 1);
         if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
         if (k == "cww" && v >= 256 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
+        if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }
       pos = end + 1;
@@ -1130,7 +1135,8 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   ctx->n = n;
   ctx->W = (n + 63) / 64;
   ctx->ldM = std::max<i64>(ctx->ld_align,
-                           (ctx->W + ctx->ld_align - 1) / ctx->ld_align * ctx->ld_align);
+                           (ctx->W + ctx->ld_align - 1) / ctx->ld_align * ctx->ld_align) *
+             ctx->pitch_mul;
   ctx->ncols = ncols;
   KTRY(dalloc(ctx, ctx->pv, sizeof(int32_t) * std::max<i64>(1, n * ncols)));
   if (n * ncols > 0)

@@ -905,6 +905,7 @@ struct RowsArgs {
   const int32_t* hflag;  // U (nullable)
   u64* M;
   i64 ldM;
+  i64 wW;                // words written per row (<= ldM)
   i64 r0;
   i64 n, W;
   int ch;
@@ -921,7 +922,7 @@ __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
   const i64 chunk = b - a.wioff[c];
   const i64 base = (i64)blockIdx.y * a.cww;
   const i64 ldw = a.ldM;
-  const int nw = (int)min((i64)a.cww, ldw - base);
+  const int nw = (int)min((i64)a.cww, a.wW - base);
   if (nw <= 0) return;
   const int32_t m_begin = a.moff[c], m_end = a.moff[c + 1];
   const int32_t m0 = m_begin + (int32_t)(chunk * a.ch);
