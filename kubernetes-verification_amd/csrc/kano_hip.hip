@@ -95,7 +95,8 @@ struct kano_ctx {
   int ch = 16;               // member rows per k_rows work item
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;
-  int pitch_mul = 1;         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
+  int pitch_mul = 1;
+  int rows_rot = 1;          // k_rows rotated store order         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -817,6 +818,7 @@ int launch_rows(kano_ctx* ctx) {
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
   a.wW = ldM / ctx->pitch_mul;
+  a.rot = ctx->rows_rot;
   a.r0 = ctx->r0;
   a.n = n;
   a.W = W;
@@ -894,6 +896,7 @@ int recompute_cols(kano_ctx* ctx) {
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
   a.wW = ldM / ctx->pitch_mul;
+  a.rot = ctx->rows_rot;
   a.r0 = ctx->r0;
   a.n = ctx->n;
   a.W = W;
@@ -1046,6 +1049,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
         if (k == "cww" && v >= 256 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
         if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
+        if (k == "rot") ctx->rows_rot = v ? 1 : 0;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }
       pos = end + 1;

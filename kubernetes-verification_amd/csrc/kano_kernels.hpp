@@ -910,6 +910,7 @@ struct RowsArgs {
   i64 n, W;
   int ch;
   int cww;
+  int rot;               // rotate each row's store order (spreads HBM channels)
   u64* color;
   u64* colnand;
 };
@@ -950,11 +951,19 @@ __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
     }
     __syncthreads();
   }
+  // every row is stored from a different starting offset: the blocks in
+  // flight then write different column ranges instead of all rows' heads at
+  // once (measured: the aligned order camps on a subset of HBM channels)
+  const uint32_t half = (uint32_t)(nw >> 1);
   for (int32_t m = m0; m < m1; ++m) {
     if (heavy && m == m_begin) continue;
     u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
-    for (int w = threadIdx.x * 2; w < nw; w += TPB * 2)
+    const int rot = a.rot ? (int)(((uint32_t)b * 97u + (uint32_t)m * 131u) % half) * 2 : 0;
+    for (int k = threadIdx.x * 2; k < nw; k += TPB * 2) {
+      int w = k + rot;
+      if (w >= nw) w -= nw;
       *(u64x2*)&dst[w] = *(const u64x2*)&row[w];   // (nt stores measured slower)
+    }
   }
   if (chunk == 0 && a.color) {
     for (int w = threadIdx.x; w < nw; w += TPB) {
