@@ -96,7 +96,8 @@ struct kano_ctx {
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;
   int pitch_mul = 1;
-  int rows_rot = 1;          // k_rows rotated store order         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
+  int rows_rot = 0;          // k_rows rotated store order (measured: no gain)
+  int pitch_pad = 0;         // extra words per M row (experiment)         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -800,7 +801,7 @@ int launch_rows(kano_ctx* ctx) {
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
   }
-  const i64 wW = ldM / ctx->pitch_mul;
+  const i64 wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
   const int cww = (int)std::min<i64>(wW, ctx->cww_max);
   const unsigned ncc = (unsigned)((wW + cww - 1) / cww);
   RowsArgs a{};
@@ -817,7 +818,7 @@ int launch_rows(kano_ctx* ctx) {
   a.hflag = ctx->heavy_count > 0 ? P_<int32_t>(ctx->hflag) : nullptr;
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
-  a.wW = ldM / ctx->pitch_mul;
+  a.wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
   a.rot = ctx->rows_rot;
   a.r0 = ctx->r0;
   a.n = n;
@@ -895,7 +896,7 @@ int recompute_cols(kano_ctx* ctx) {
   a.hflag = mem + rl;  // every row "prebuilt": copy + column fold, no writes
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
-  a.wW = ldM / ctx->pitch_mul;
+  a.wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
   a.rot = ctx->rows_rot;
   a.r0 = ctx->r0;
   a.n = ctx->n;
@@ -1050,6 +1051,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "cww" && v >= 256 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
         if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
         if (k == "rot") ctx->rows_rot = v ? 1 : 0;
+        if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }
       pos = end + 1;
@@ -1138,8 +1140,9 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   KCHK(hipSetDevice(ctx->device));
   ctx->n = n;
   ctx->W = (n + 63) / 64;
-  ctx->ldM = std::max<i64>(ctx->ld_align,
-                           (ctx->W + ctx->ld_align - 1) / ctx->ld_align * ctx->ld_align) *
+  ctx->ldM = (std::max<i64>(ctx->ld_align,
+                            (ctx->W + ctx->ld_align - 1) / ctx->ld_align * ctx->ld_align) +
+              ctx->pitch_pad) *
              ctx->pitch_mul;
   ctx->ncols = ncols;
   KTRY(dalloc(ctx, ctx->pv, sizeof(int32_t) * std::max<i64>(1, n * ncols)));
