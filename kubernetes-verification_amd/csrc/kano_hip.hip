@@ -92,6 +92,7 @@ struct kano_ctx {
   bool cols_valid = false;   // color/colnand describe M
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_timed = false;
+  bool alist_valid = false;  // allowed-pod lists materialised (kano_get_allow_csr)
   int ch = 16;               // member rows per k_rows work item
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;
@@ -658,7 +659,6 @@ int do_back(kano_ctx* ctx, int path) {
     KTRY(dalloc(ctx, ctx->ecls, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
     KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
-    KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
     KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, H)));
     KTRY(dalloc(ctx, ctx->wicls, sizeof(int32_t) * std::max<i64>(1, ctx->wi_total)));
     KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
@@ -706,11 +706,8 @@ int do_back(kano_ctx* ctx, int path) {
                        P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
                        P_<u64>(ctx->AC), ctx->ldC);
     KLAUNCH();
-    hipLaunchKernelGGL(k_pol_pods, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
-                       P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
-                       P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
-    KLAUNCH();
   }
+  ctx->alist_valid = false;   // allowed-pod lists: built on demand (API only)
   if (U == 0) return 0;
   if (ctx->nnz_sel > 0)
   hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0, ctx->stream,
@@ -749,7 +746,7 @@ int do_back(kano_ctx* ctx, int path) {
         KLAUNCH();
       }
     } else {
-      hipLaunchKernelGGL(k_heavy_mc_or, dim3((unsigned)H, nblk(ldMc)), dim3(TPB), 0, ctx->stream,
+      hipLaunchKernelGGL(k_heavy_mc_or, dim3((unsigned)H, nblk(ldMc, 64)), dim3(TPB), 0, ctx->stream,
                          P_<int32_t>(ctx->hlist), P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
                          P_<u64>(ctx->AC), ctx->ldC, ctx->UAW, P_<u64>(ctx->Mc), ldMc);
       KLAUNCH();
@@ -810,9 +807,10 @@ int launch_rows(kano_ctx* ctx) {
   a.U = U;
   a.soffc = P_<i64>(ctx->soffc);
   a.slist = P_<int32_t>(ctx->slist);
-  a.acnt = P_<int32_t>(ctx->acnt);
-  a.aloff = P_<i64>(ctx->aloff);
-  a.alist = P_<int32_t>(ctx->alist);
+  a.alcoff = P_<i64>(ctx->alcoff);
+  a.alc = P_<int32_t>(ctx->alc);
+  a.cmoff = P_<int32_t>(ctx->cc.moff);
+  a.cmem = P_<int32_t>(ctx->cc.mem);
   a.moff = P_<int32_t>(ctx->rc.moff);
   a.mem = P_<int32_t>(ctx->rc.mem);
   a.hflag = ctx->heavy_count > 0 ? P_<int32_t>(ctx->hflag) : nullptr;
@@ -1528,6 +1526,17 @@ int kano_get_select_csr(kano_ctx* ctx, int64_t* off, int32_t* pol) {
 
 int kano_get_allow_csr(kano_ctx* ctx, int64_t* off, int32_t* pods) {
   KTRY(ensure_matrix(ctx));
+  if (!ctx->alist_valid) {
+    const i64 P = ctx->P;
+    KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
+    if (P > 0 && ctx->cc.U > 0) {
+      hipLaunchKernelGGL(k_pol_pods, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                         P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
+                         P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
+      KLAUNCH();
+    }
+    ctx->alist_valid = true;
+  }
   if (off)
     KCHK(hipMemcpyAsync(off, ctx->aloff.p, sizeof(i64) * (ctx->P + 1), hipMemcpyDeviceToHost,
                         ctx->stream));

@@ -439,36 +439,22 @@ __global__ __launch_bounds__(TPB) void k_sel_place(const i64* __restrict__ pstar
 }
 
 // sort S(c) ascending (the reference appends p in policy order,
-// model.py:161); entries are distinct.  One wave per class: s <= 64 by a rank
-// sort in registers, s <= SORT_WAVE_MAX by a rank sort in the wave's LDS
-// slice; larger lists are left to k_sort_lists_big.
-constexpr int SORT_WAVE_MAX = 1024;
+// model.py:161); entries are distinct.  One wave per class with s <= 64: a
+// rank sort in registers; larger lists are left to k_sort_lists_big (block
+// bitmap over all policies).
+constexpr int SORT_WAVE_MAX = 64;
 __global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soffc, i64 U,
                                                     int32_t* __restrict__ slist) {
-  __shared__ int32_t buf[TPB / 64][SORT_WAVE_MAX];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const i64 c = (i64)blockIdx.x * (TPB / 64) + wid;
   if (c >= U) return;
   const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
   if (s <= 1 || s > SORT_WAVE_MAX) return;
   int32_t* L = slist + s0;
-  if (s <= 64) {
-    const int32_t v = lane < s ? L[lane] : 0x7fffffff;
-    int r = 0;
-    for (int k = 0; k < s; ++k) r += __shfl(v, k, 64) < v;
-    if (lane < s) L[r] = v;
-    return;
-  }
-  int32_t* a = buf[wid];
-  for (i64 k = lane; k < s; k += 64) a[k] = L[k];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  for (i64 k = lane; k < s; k += 64) {
-    const int32_t v = a[k];
-    int r = 0;
-    for (i64 q = 0; q < s; ++q) r += a[q] < v;
-    L[r] = v;
-  }
+  const int32_t v = lane < s ? L[lane] : 0x7fffffff;
+  int r = 0;
+  for (int k = 0; k < s; ++k) r += __shfl(v, k, 64) < v;
+  if (lane < s) L[r] = v;
 }
 
 // block per class with s > SORT_WAVE_MAX: bitmap of all P policies in LDS
@@ -652,16 +638,13 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
                                                          i64 r1, int32_t* gmin, int32_t* gmax,
                                                          int32_t* err) {
   const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= r1) return;
-  const int32_t c = cls[i], g = gid[i];
-  if (g < 0 || g >= G) {   // caller-declared group count violated
+  bool act = i < r1;
+  const int32_t c = act ? cls[i] : 0, g = act ? gid[i] : 0;
+  if (act && (g < 0 || g >= G)) {   // caller-declared group count violated
     atomicOr(err, 1);
-    return;
+    act = false;
   }
-  // big classes settle after a few members: skip atomics that cannot change
-  // no-return atomics are posted; a read-before-update check measured slower
-  atomicMin(&gmin[c], g);
-  atomicMax(&gmax[c], g);
+  wave_agg_minmax(gmin, gmax, c, g, act);
 }
 
 // R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per
@@ -769,21 +752,34 @@ __global__ __launch_bounds__(TPB) void k_flag_list(const int32_t* __restrict__ f
 // Heavy rows: the row of the class over COLUMN classes, Mc[h] = OR_{p in S}
 // AllowC[p], then expanded to pods (bit j = Mc[h][cla[j]]).
 // ===========================================================================
-// bitwise: one thread per Mc word
+// bitwise: block per (heavy class, chunk of <= 64 Mc words); the threads
+// split the policies of S(c) as well as the words, then OR-reduce in LDS
 __global__ __launch_bounds__(TPB) void k_heavy_mc_or(const int32_t* __restrict__ hlist,
                                                      const i64* __restrict__ soffc,
                                                      const int32_t* __restrict__ slist,
                                                      const u64* __restrict__ AC, i64 ldC, i64 UW,
                                                      u64* __restrict__ Mc, i64 ldMc) {
+  __shared__ u64 red[TPB];
   const int32_t c = hlist[blockIdx.x];
-  const i64 w = (i64)blockIdx.y * TPB + threadIdx.x;
-  if (w >= ldMc) return;
+  const i64 w0 = (i64)blockIdx.y * 64;
+  const int wc = (int)min((i64)64, ldMc - w0);
+  int wc2 = 1;
+  while (wc2 < wc) wc2 <<= 1;
+  const int npp = TPB / wc2;
+  const int wl = threadIdx.x & (wc2 - 1), pp = threadIdx.x / wc2;
+  const i64 w = w0 + wl;
   u64 acc = 0;
-  if (w < UW) {
-    const i64 s0 = soffc[c], s1 = soffc[c + 1];
-    for (i64 e = s0; e < s1; ++e) acc |= AC[(i64)slist[e] * ldC + w];
+  if (wl < wc && w < UW) {
+    const i64 s1 = soffc[c + 1];
+    for (i64 e = soffc[c] + pp; e < s1; e += npp) acc |= AC[(i64)slist[e] * ldC + w];
   }
-  Mc[(i64)c * ldMc + w] = acc;
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = npp >> 1; st >= 1; st >>= 1) {
+    if (pp < st) red[threadIdx.x] |= red[threadIdx.x + st * wc2];
+    __syncthreads();
+  }
+  if (pp == 0 && wl < wc) Mc[(i64)c * ldMc + w] = red[threadIdx.x];
 }
 
 // int8 MFMA contraction (the dense path):
@@ -897,9 +893,10 @@ struct RowsArgs {
   i64 U;
   const i64* soffc;      // U+1
   const int32_t* slist;
-  const int32_t* acnt;
-  const i64* aloff;
-  const int32_t* alist;
+  const i64* alcoff;     // allowed column classes per policy (CSR)
+  const int32_t* alc;
+  const int32_t* cmoff;  // members of each column class
+  const int32_t* cmem;
   const int32_t* moff;   // U+1
   const int32_t* mem;
   const int32_t* hflag;  // U (nullable)
@@ -938,15 +935,24 @@ __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
   } else {
     for (int w = threadIdx.x; w < nw; w += TPB) row[w] = 0ull;
     __syncthreads();
+    // the allowed pods of S(c): for each (policy, allowed column class)
+    // entry, the class's members; entries dealt round-robin to the 4 waves,
+    // members across the lanes
     const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
     const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int t = 0;
     for (i64 e = s0; e < s1; ++e) {
       const int32_t p = a.slist[e];
-      const int32_t* L = a.alist + a.aloff[p];
-      const i64 cnt = a.acnt[p];
-      for (i64 k = threadIdx.x; k < cnt; k += TPB) {
-        const int32_t j = L[k];
-        if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+      const i64 q1 = a.alcoff[p + 1];
+      for (i64 q = a.alcoff[p]; q < q1; ++q, ++t) {
+        if ((t & 3) != wid) continue;
+        const int32_t ca = a.alc[q];
+        const int32_t k1 = a.cmoff[ca + 1];
+        for (int32_t k = a.cmoff[ca] + lane; k < k1; k += 64) {
+          const int32_t j = a.cmem[k];
+          if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+        }
       }
     }
     __syncthreads();

@@ -235,23 +235,64 @@ __global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
   }
 }
 
-// atomicAdd(&ctr[key], 1) for every active lane, with the lanes that share
-// the first active lane's key merged into one atomic (Zipf keys: the hot key
-// is usually the one repeated inside a wave).  Returns the lane's slot (old
+// atomicAdd(&ctr[key], 1) for every active lane, lanes with equal keys merged
+// into one atomic: up to AGG_ROUNDS rounds each take the first remaining
+// lane's key and every lane sharing it (Zipf keys: the hot keys repeat
+// inside a wave); the rest add one by one.  Returns the lane's slot (old
 // value + rank).  Every lane of the wave must call it.
+constexpr int AGG_ROUNDS = 4;
 __device__ __forceinline__ int32_t wave_agg_inc(int32_t* ctr, i64 key, bool active) {
-  const u64 act = __ballot(active);
-  if (act == 0ull) return 0;
   const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)act) - 1;
-  const i64 k0 = __shfl(key, leader, 64);
-  const bool same = active && key == k0;
-  const u64 smask = __ballot(same);
-  int32_t base = 0;
-  if (lane == leader) base = atomicAdd(&ctr[k0], (int32_t)__popcll(smask));
-  base = __shfl(base, leader, 64);
-  if (same) return base + (int32_t)__popcll(smask & ((1ull << lane) - 1ull));
-  return active ? atomicAdd(&ctr[key], 1) : 0;
+  const u64 below = (1ull << lane) - 1ull;
+  u64 rem = __ballot(active);
+  bool done = !active;
+  int32_t res = 0;
+  for (int round = 0; round < AGG_ROUNDS && rem; ++round) {
+    const int leader = __ffsll((long long)rem) - 1;
+    const i64 k0 = __shfl(key, leader, 64);
+    const bool same = !done && key == k0;
+    const u64 smask = __ballot(same);
+    int32_t base = 0;
+    if (lane == leader) base = atomicAdd(&ctr[k0], (int32_t)__popcll(smask));
+    base = __shfl(base, leader, 64);
+    if (same) {
+      res = base + (int32_t)__popcll(smask & below);
+      done = true;
+    }
+    rem &= ~smask;
+  }
+  if (!done) res = atomicAdd(&ctr[key], 1);
+  return res;
+}
+
+// atomicMin(&lo[key], v), atomicMax(&hi[key], v) with the same merging
+__device__ __forceinline__ void wave_agg_minmax(int32_t* lo, int32_t* hi, i64 key, int32_t v,
+                                                bool active) {
+  const int lane = threadIdx.x & 63;
+  u64 rem = __ballot(active);
+  bool done = !active;
+  for (int round = 0; round < AGG_ROUNDS && rem; ++round) {
+    const int leader = __ffsll((long long)rem) - 1;
+    const i64 k0 = __shfl(key, leader, 64);
+    const bool same = !done && key == k0;
+    const u64 smask = __ballot(same);
+    int32_t mn = same ? v : INT32_MAX, mx = same ? v : INT32_MIN;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      mn = min(mn, __shfl_xor(mn, d, 64));
+      mx = max(mx, __shfl_xor(mx, d, 64));
+    }
+    if (lane == leader) {
+      atomicMin(&lo[k0], mn);
+      atomicMax(&hi[k0], mx);
+    }
+    if (same) done = true;
+    rem &= ~smask;
+  }
+  if (!done) {
+    atomicMin(&lo[key], v);
+    atomicMax(&hi[key], v);
+  }
 }
 
 // ---- small helpers ---------------------------------------------------------
