@@ -75,7 +75,7 @@ struct SideMatch {
 // counters) and read by the host with one copy per sync
 enum {
   SZ_UR = 0, SZ_UA, SZ_NNZ_SEL, SZ_NNZ_ALC, SZ_NNZ_ALW, SZ_NFLAGS, SZ_WI, SZ_HEAVY, SZ_MAXSEL,
-  SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 16
+  SZ_LIGHT, SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 17
 };
 
 struct kano_ctx {
@@ -97,13 +97,16 @@ struct kano_ctx {
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;
   int pitch_mul = 1;
-  int rows_rot = 0;          // k_rows rotated store order (measured: no gain)
+  int rows_alist = -1;       // k_rows build from allowed-pod lists: -1 auto, 0 no, 1 yes
+  int rows_nt = 0;           // k_rows block size: 0 auto, 256 / 512 / 1024
   int pitch_pad = 0;         // extra words per M row (experiment)         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
   i64 UAW = 0, ldC = 0;      // words per class-level row (column classes)
   i64 nnz_sel = 0, nnz_alc = 0, nnz_alw = 0, heavy_count = 0, wi_total = 0, nflags = 0;
+  i64 light_cost = 0;        // allowed-pod entries the light classes' rows read
+  bool rows_use_alist = false;
   int max_sel = 0;
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
 
@@ -607,6 +610,7 @@ int do_front(kano_ctx* ctx, int path) {
     a.hflag = P_<int32_t>(ctx->hflag);
     a.sq = P_<i64>(ctx->sq);
     a.maxs = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_MAXSEL);  // low half
+    a.light = P_<unsigned long long>(ctx->sizes) + SZ_LIGHT;
     hipLaunchKernelGGL(k_class_plan, dim3(nblk(Ur)), dim3(TPB), 0, ctx->stream, a);
     KLAUNCH();
   }
@@ -623,8 +627,8 @@ int do_front(kano_ctx* ctx, int path) {
 
 // host sync 2 of the build: every list size at once
 int read_sizes(kano_ctx* ctx) {
-  i64 v[SZ_MAXSEL - SZ_NNZ_SEL + 1];
-  KTRY(read_slots(ctx, SZ_NNZ_SEL, SZ_MAXSEL - SZ_NNZ_SEL + 1, v));
+  i64 v[SZ_LIGHT - SZ_NNZ_SEL + 1];
+  KTRY(read_slots(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1, v));
   ctx->nnz_sel = v[SZ_NNZ_SEL - SZ_NNZ_SEL];
   ctx->nnz_alc = v[SZ_NNZ_ALC - SZ_NNZ_SEL];
   ctx->nnz_alw = v[SZ_NNZ_ALW - SZ_NNZ_SEL];
@@ -632,6 +636,21 @@ int read_sizes(kano_ctx* ctx) {
   ctx->wi_total = v[SZ_WI - SZ_NNZ_SEL];
   ctx->heavy_count = v[SZ_HEAVY - SZ_NNZ_SEL];
   ctx->max_sel = (int)(v[SZ_MAXSEL - SZ_NNZ_SEL] & 0xffffffff);
+  ctx->light_cost = v[SZ_LIGHT - SZ_NNZ_SEL];
+  return 0;
+}
+
+// allowed-pod lists per policy (members of its allowed column classes)
+int build_alist(kano_ctx* ctx) {
+  const i64 P = ctx->P;
+  KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
+  if (P > 0 && ctx->cc.U > 0) {
+    hipLaunchKernelGGL(k_pol_pods, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                       P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
+                       P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
+    KLAUNCH();
+  }
+  ctx->alist_valid = true;
   return 0;
 }
 
@@ -707,7 +726,14 @@ int do_back(kano_ctx* ctx, int path) {
                        P_<u64>(ctx->AC), ctx->ldC);
     KLAUNCH();
   }
-  ctx->alist_valid = false;   // allowed-pod lists: built on demand (API only)
+  // light rows read either the flat allowed-pod lists (materialised here,
+  // one pass over nnz_alw entries) or the column-class member lists; the
+  // flat lists pay off when the light rows read them several times over
+  ctx->alist_valid = false;
+  int ua = ctx->rows_alist;
+  if (ua < 0) ua = ctx->light_cost > 4 * ctx->nnz_alw ? 1 : 0;
+  ctx->rows_use_alist = ua && ctx->light_cost > 0;
+  if (ctx->rows_use_alist) KTRY(build_alist(ctx));
   if (U == 0) return 0;
   if (ctx->nnz_sel > 0)
   hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0, ctx->stream,
@@ -807,6 +833,8 @@ int launch_rows(kano_ctx* ctx) {
   a.U = U;
   a.soffc = P_<i64>(ctx->soffc);
   a.slist = P_<int32_t>(ctx->slist);
+  a.aloff = ctx->rows_use_alist ? P_<i64>(ctx->aloff) : nullptr;
+  a.alist = ctx->rows_use_alist ? P_<int32_t>(ctx->alist) : nullptr;
   a.alcoff = P_<i64>(ctx->alcoff);
   a.alc = P_<int32_t>(ctx->alc);
   a.cmoff = P_<int32_t>(ctx->cc.moff);
@@ -817,7 +845,6 @@ int launch_rows(kano_ctx* ctx) {
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
   a.wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
-  a.rot = ctx->rows_rot;
   a.r0 = ctx->r0;
   a.n = n;
   a.W = W;
@@ -825,9 +852,15 @@ int launch_rows(kano_ctx* ctx) {
   a.cww = cww;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
+  // wide chunks hold few blocks per CU (LDS): give those blocks more waves
+  int nt = ctx->rows_nt;
+  if (nt == 0) nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   KCHK(hipEventRecord(ctx->ev[7], rs));
-  hipLaunchKernelGGL(k_rows, dim3((unsigned)ctx->wi_total, ncc), dim3(TPB), sizeof(u64) * cww, rs,
-                     a);
+  const dim3 grid((unsigned)ctx->wi_total, ncc);
+  const size_t lds = sizeof(u64) * cww;
+  if (nt == 1024) hipLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, a);
+  else if (nt == 512) hipLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, a);
+  else hipLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, a);
   KLAUNCH();
   KCHK(hipEventRecord(ctx->ev[8], rs));
   if (ctx->rows_overlap) KCHK(hipEventRecord(ctx->ev_rows, rs));
@@ -895,7 +928,6 @@ int recompute_cols(kano_ctx* ctx) {
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
   a.wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
-  a.rot = ctx->rows_rot;
   a.r0 = ctx->r0;
   a.n = ctx->n;
   a.W = W;
@@ -903,8 +935,8 @@ int recompute_cols(kano_ctx* ctx) {
   a.cww = cww;
   a.color = P_<u64>(ctx->color);
   a.colnand = P_<u64>(ctx->colnand);
-  hipLaunchKernelGGL(k_rows, dim3((unsigned)rl, (unsigned)((ldM + cww - 1) / cww)), dim3(TPB),
-                     sizeof(u64) * cww, ctx->stream, a);
+  hipLaunchKernelGGL(k_rows<TPB>, dim3((unsigned)rl, (unsigned)((ldM + cww - 1) / cww)),
+                     dim3(TPB), sizeof(u64) * cww, ctx->stream, a);
   KLAUNCH();
   KTRY(sync(ctx));
   ctx->cols_valid = true;
@@ -1048,7 +1080,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
         if (k == "cww" && v >= 256 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
         if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
-        if (k == "rot") ctx->rows_rot = v ? 1 : 0;
+        if (k == "alist") ctx->rows_alist = v < 0 ? -1 : (v ? 1 : 0);
+        if (k == "nt" && (v == 0 || v == 256 || v == 512 || v == 1024)) ctx->rows_nt = v;
         if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }
@@ -1526,17 +1559,7 @@ int kano_get_select_csr(kano_ctx* ctx, int64_t* off, int32_t* pol) {
 
 int kano_get_allow_csr(kano_ctx* ctx, int64_t* off, int32_t* pods) {
   KTRY(ensure_matrix(ctx));
-  if (!ctx->alist_valid) {
-    const i64 P = ctx->P;
-    KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
-    if (P > 0 && ctx->cc.U > 0) {
-      hipLaunchKernelGGL(k_pol_pods, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
-                         P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
-                         P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
-      KLAUNCH();
-    }
-    ctx->alist_valid = true;
-  }
+  if (!ctx->alist_valid) KTRY(build_alist(ctx));
   if (off)
     KCHK(hipMemcpyAsync(off, ctx->aloff.p, sizeof(i64) * (ctx->P + 1), hipMemcpyDeviceToHost,
                         ctx->stream));

@@ -706,6 +706,7 @@ struct ClassPlan {
   int32_t* hflag;          // out 1 = heavy (row built once from Mc, then copied)
   i64* sq;                 // out |S(c)|^2 for classes with local members
   int32_t* maxs;           // out max |S(c)| over classes with local members
+  unsigned long long* light;  // out sum of cost * chunks over light classes
 };
 
 // A light class rebuilds its row per member chunk by scattering its allowed
@@ -713,20 +714,32 @@ struct ClassPlan {
 // operations) and every chunk copies it (W words).  Heavy iff cheaper.
 __global__ __launch_bounds__(TPB) void k_class_plan(ClassPlan a) {
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c >= a.U) return;
-  const int32_t s = a.scnt[c];
-  const int32_t m = a.mcnt[c];
-  const i64 cost = (i64)a.cost[c];
-  const int32_t chunks = (m + a.ch - 1) / a.ch;
-  a.wicnt[c] = chunks;
-  int hv = 0;
-  if (m > 0 && s > 0) {
-    if (a.force == 2) hv = 1;
-    else hv = cost * chunks > 64 * a.W + (i64)chunks * a.W;
+  int32_t smax = 0;
+  unsigned long long light = 0;
+  if (c < a.U) {
+    const int32_t s = a.scnt[c];
+    const int32_t m = a.mcnt[c];
+    const i64 cost = (i64)a.cost[c];
+    const int32_t chunks = (m + a.ch - 1) / a.ch;
+    a.wicnt[c] = chunks;
+    int hv = 0;
+    if (m > 0 && s > 0) {
+      if (a.force == 2) hv = 1;
+      else hv = cost * chunks > 64 * a.W + (i64)chunks * a.W;
+    }
+    a.hflag[c] = hv;
+    a.sq[c] = m > 0 ? (i64)s * s : 0;
+    if (m > 0) smax = s;
+    if (m > 0 && !hv) light = (unsigned long long)cost * (unsigned long long)chunks;
   }
-  a.hflag[c] = hv;
-  a.sq[c] = m > 0 ? (i64)s * s : 0;
-  if (m > 0) atomicMax(a.maxs, s);
+  // one atomic per wave
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) smax = max(smax, __shfl_xor(smax, d, 64));
+  light = wave_sum(light);
+  if ((threadIdx.x & 63) == 0) {
+    if (smax > 0) atomicMax(a.maxs, smax);
+    if (light) atomicAdd(a.light, light);
+  }
 }
 
 __global__ __launch_bounds__(TPB) void k_sq_from_off(const i64* __restrict__ off, i64 U,
@@ -893,6 +906,8 @@ struct RowsArgs {
   i64 U;
   const i64* soffc;      // U+1
   const int32_t* slist;
+  const i64* aloff;      // allowed-pod lists per policy (nullable: use the
+  const int32_t* alist;  //   column-class member lists below instead)
   const i64* alcoff;     // allowed column classes per policy (CSR)
   const int32_t* alc;
   const int32_t* cmoff;  // members of each column class
@@ -907,13 +922,14 @@ struct RowsArgs {
   i64 n, W;
   int ch;
   int cww;
-  int rot;               // rotate each row's store order (spreads HBM channels)
   u64* color;
   u64* colnand;
 };
 
-__global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
+  constexpr int NW = NT / 64;
   const i64 b = blockIdx.x;
   const i64 c = a.wicls ? (i64)a.wicls[b] : upper_bound_i32(a.wioff, a.U + 1, b) - 1;
   if (c < 0 || c >= a.U) return;
@@ -929,50 +945,54 @@ __global__ __launch_bounds__(TPB) void k_rows(RowsArgs a) {
 
   if (heavy) {
     const u64* src = a.M + (i64)(a.mem[m_begin] - a.r0) * ldw + base;
-    for (int w = threadIdx.x * 2; w < nw; w += TPB * 2)
-      *(ulonglong2*)&row[w] = *(const ulonglong2*)&src[w];
+    for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+      *(u64x2*)&row[w] = *(const u64x2*)&src[w];
     __syncthreads();
   } else {
-    for (int w = threadIdx.x; w < nw; w += TPB) row[w] = 0ull;
+    for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
     __syncthreads();
-    // the allowed pods of S(c): for each (policy, allowed column class)
-    // entry, the class's members; entries dealt round-robin to the 4 waves,
-    // members across the lanes
     const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
     const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int t = 0;
-    for (i64 e = s0; e < s1; ++e) {
-      const int32_t p = a.slist[e];
-      const i64 q1 = a.alcoff[p + 1];
-      for (i64 q = a.alcoff[p]; q < q1; ++q, ++t) {
-        if ((t & 3) != wid) continue;
-        const int32_t ca = a.alc[q];
-        const int32_t k1 = a.cmoff[ca + 1];
-        for (int32_t k = a.cmoff[ca] + lane; k < k1; k += 64) {
-          const int32_t j = a.cmem[k];
+    if (a.alist) {
+      // the flat allowed-pod list of each policy of S(c), across all threads
+      for (i64 e = s0; e < s1; ++e) {
+        const int32_t p = a.slist[e];
+        const int32_t* L = a.alist + a.aloff[p];
+        const i64 cnt = a.aloff[p + 1] - a.aloff[p];
+        for (i64 k = threadIdx.x; k < cnt; k += NT) {
+          const int32_t j = L[k];
           if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+        }
+      }
+    } else {
+      // (policy, allowed column class) entries dealt round-robin to the
+      // waves, the class's members across the lanes
+      const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      int t = 0;
+      for (i64 e = s0; e < s1; ++e) {
+        const int32_t p = a.slist[e];
+        const i64 q1 = a.alcoff[p + 1];
+        for (i64 q = a.alcoff[p]; q < q1; ++q, ++t) {
+          if (t % NW != wid) continue;
+          const int32_t ca = a.alc[q];
+          const int32_t k1 = a.cmoff[ca + 1];
+          for (int32_t k = a.cmoff[ca] + lane; k < k1; k += 64) {
+            const int32_t j = a.cmem[k];
+            if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+          }
         }
       }
     }
     __syncthreads();
   }
-  // every row is stored from a different starting offset: the blocks in
-  // flight then write different column ranges instead of all rows' heads at
-  // once (measured: the aligned order camps on a subset of HBM channels)
-  const uint32_t half = (uint32_t)(nw >> 1);
   for (int32_t m = m0; m < m1; ++m) {
     if (heavy && m == m_begin) continue;
     u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
-    const int rot = a.rot ? (int)(((uint32_t)b * 97u + (uint32_t)m * 131u) % half) * 2 : 0;
-    for (int k = threadIdx.x * 2; k < nw; k += TPB * 2) {
-      int w = k + rot;
-      if (w >= nw) w -= nw;
+    for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
       *(u64x2*)&dst[w] = *(const u64x2*)&row[w];   // (nt stores measured slower)
-    }
   }
   if (chunk == 0 && a.color) {
-    for (int w = threadIdx.x; w < nw; w += TPB) {
+    for (int w = threadIdx.x; w < nw; w += NT) {
       const i64 gw = base + w;
       if (gw >= a.W) break;
       const u64 v = row[w];
