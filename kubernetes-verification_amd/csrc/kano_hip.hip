@@ -727,11 +727,15 @@ int do_back(kano_ctx* ctx, int path) {
     KLAUNCH();
   }
   // light rows read either the flat allowed-pod lists (materialised here,
-  // one pass over nnz_alw entries) or the column-class member lists; the
-  // flat lists pay off when the light rows read them several times over
+  // one pass over nnz_alw entries) or the column-class member lists (n
+  // entries, cache-resident).  Measured: the flat lists win when they stay
+  // on-die (C3: 6 MB, k_rows -10%) and the rows read them several times
+  // over; past the Infinity Cache the member lists win (C5: 450 MB of
+  // lists, k_rows -10%; C4: 500 MB)
   ctx->alist_valid = false;
   int ua = ctx->rows_alist;
-  if (ua < 0) ua = ctx->light_cost > 4 * ctx->nnz_alw ? 1 : 0;
+  if (ua < 0)
+    ua = ctx->light_cost > 4 * ctx->nnz_alw && ctx->nnz_alw * 4 <= (64ll << 20) ? 1 : 0;
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx));
   if (U == 0) return 0;
