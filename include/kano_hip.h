@@ -111,10 +111,12 @@ int kano_get_bit(kano_ctx* ctx, int64_t i, int64_t j, int* value);
 int kano_set_bit(kano_ctx* ctx, int64_t i, int64_t j, int value);
 
 /* Policy.working_select_set / working_allow_set (model.py:119-121, 156):
- * the n-bit sets of policy p. */
+ * the n-bit sets of policy p (on a row shard, select bits exist for the
+ * shard's pods only; the others read 0). */
 int kano_get_policy_sets(kano_ctx* ctx, int64_t p, uint64_t* sel, uint64_t* allow);
 /* Container.select_policies (model.py:158-161): row class of every pod and the
- * class-level ascending policy lists, CSR over classes. */
+ * class-level ascending policy lists, CSR over classes (row classes cover the
+ * shard's pods; cls is -1 outside the shard). */
 int kano_get_classes(kano_ctx* ctx, int32_t* cls /* n */);
 int kano_get_select_csr(kano_ctx* ctx, int64_t* off /* U+1 */, int32_t* pol /* nnz_sel */);
 /* Container.allow_policies (model.py:162-163) and the allow sets as pod

@@ -354,19 +354,22 @@ ClsSide cls_side(kano_ctx* ctx, ClassSet& cs) {
 
 // phase 1, both sides: hash insert + smallest member per slot, first-member
 // flags, class-id scan (no sync)
+// (row classes cover only this shard's pods [r0, r1); column classes all pods)
 int classify_phase1(kano_ctx* ctx) {
   const i64 n = ctx->n;
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
-  if (n > 0) {
-    hipLaunchKernelGGL(k_cls_insert, dim3(nblk(n), 2), dim3(TPB), 0, ctx->stream,
+  const i64 nr = ctx->rc.m1 - ctx->rc.m0, na = ctx->cc.m1 - ctx->cc.m0;
+  const i64 most = std::max(nr, na);
+  if (most > 0) {
+    hipLaunchKernelGGL(k_cls_insert, dim3(nblk(most), 2), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->pv), n, pr);
     KLAUNCH();
-    hipLaunchKernelGGL(k_cls_flag, dim3(nblk(n), 2), dim3(TPB), 0, ctx->stream, n, pr);
+    hipLaunchKernelGGL(k_cls_flag, dim3(nblk(most), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
   ScanBatch sb(ctx);
-  KTRY(sb.add(P_<int32_t>(ctx->rc.flag), n, P_<int32_t>(ctx->rc.cid), SZ_UR));
-  KTRY(sb.add(P_<int32_t>(ctx->cc.flag), n, P_<int32_t>(ctx->cc.cid), SZ_UA));
+  KTRY(sb.add(P_<int32_t>(ctx->rc.flag), nr, P_<int32_t>(ctx->rc.cid), SZ_UR));
+  KTRY(sb.add(P_<int32_t>(ctx->cc.flag), na, P_<int32_t>(ctx->cc.cid), SZ_UA));
   return sb.run();
 }
 
@@ -388,11 +391,11 @@ int classify_alloc2(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
 int classify_phase2(kano_ctx* ctx) {
   const i64 n = ctx->n;
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
-  if (n > 0) {
-    hipLaunchKernelGGL(k_cls_assign, dim3(nblk(n), 2), dim3(TPB), 0, ctx->stream, n, pr);
+  const i64 rl = std::max(ctx->rc.m1 - ctx->rc.m0, ctx->cc.m1 - ctx->cc.m0);
+  if (rl > 0) {
+    hipLaunchKernelGGL(k_cls_assign, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
-  const i64 rl = std::max(ctx->rc.m1 - ctx->rc.m0, ctx->cc.m1 - ctx->cc.m0);
   if (rl > 0) {
     hipLaunchKernelGGL(k_cls_mcount, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
@@ -1529,7 +1532,8 @@ int kano_get_policy_sets(kano_ctx* ctx, int64_t p, uint64_t* sel, uint64_t* allo
   u64* s = P_<u64>(ctx->scratch_words);
   if (sel) {
     hipLaunchKernelGGL(k_sel_row, dim3(nblk(n)), dim3(TPB), 0, ctx->stream, P_<i64>(ctx->soffc),
-                       P_<int32_t>(ctx->slist), P_<int32_t>(ctx->rc.cls), n, (i64)p, s);
+                       P_<int32_t>(ctx->slist), P_<int32_t>(ctx->rc.cls), n, ctx->r0, ctx->r1,
+                       (i64)p, s);
     KLAUNCH();
     KCHK(hipMemcpyAsync(sel, s, sizeof(u64) * W, hipMemcpyDeviceToHost, ctx->stream));
   }
@@ -1544,9 +1548,13 @@ int kano_get_policy_sets(kano_ctx* ctx, int64_t p, uint64_t* sel, uint64_t* allo
 
 int kano_get_classes(kano_ctx* ctx, int32_t* cls) {
   KTRY(ensure_matrix(ctx));
-  if (cls && ctx->n > 0)
-    KCHK(hipMemcpyAsync(cls, ctx->rc.cls.p, sizeof(int32_t) * ctx->n, hipMemcpyDeviceToHost,
-                        ctx->stream));
+  if (cls && ctx->n > 0) {   // row classes exist for this shard's pods only: -1 elsewhere
+    for (i64 i = 0; i < ctx->n; ++i)
+      if (i < ctx->r0 || i >= ctx->r1) cls[i] = -1;
+    if (rows_local(ctx) > 0)
+      KCHK(hipMemcpyAsync(cls + ctx->r0, P_<int32_t>(ctx->rc.cls) + ctx->r0,
+                          sizeof(int32_t) * rows_local(ctx), hipMemcpyDeviceToHost, ctx->stream));
+  }
   return sync(ctx);
 }
 

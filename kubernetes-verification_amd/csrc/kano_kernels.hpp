@@ -43,8 +43,8 @@ struct ClsPair {
 __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ pv, i64 n,
                                                     ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= n) return;
+  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;   // pods [m0, m1) of the side
+  if (i >= a.m1) return;
   uint32_t h = 0x9747b28cu;
   for (int k = 0; k < a.KS; ++k) h = hmix(h, (uint32_t)pv[(i64)a.keys[k] * n + i]);
   uint32_t s = hfin(h) & a.tmask;
@@ -71,19 +71,20 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
   if ((int32_t)i < a.smin[s]) atomicMin(&a.smin[s], (int32_t)i);
 }
 
-__global__ __launch_bounds__(TPB) void k_cls_flag(i64 n, ClsPair pr) {
+// flag / cid are indexed by i - m0
+__global__ __launch_bounds__(TPB) void k_cls_flag(ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i < n) a.flag[i] = (a.smin[a.slot_of[i]] == (int32_t)i) ? 1 : 0;
+  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i < a.m1) a.flag[i - a.m0] = (a.smin[a.slot_of[i]] == (int32_t)i) ? 1 : 0;
 }
 
 // class ids ordered by their smallest member (deterministic)
-__global__ __launch_bounds__(TPB) void k_cls_assign(i64 n, ClsPair pr) {
+__global__ __launch_bounds__(TPB) void k_cls_assign(ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= n) return;
+  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= a.m1) return;
   const int32_t r = a.smin[a.slot_of[i]];
-  const int32_t c = a.cid[r];
+  const int32_t c = a.cid[r - a.m0];
   a.cls[i] = c;
   if (r == (int32_t)i) a.rep[c] = (int32_t)i;
 }
@@ -1107,11 +1108,12 @@ __global__ __launch_bounds__(TPB) void k_get_col(const u64* __restrict__ M, i64 
 // working_select_set of policy p over all pods: p in S(cls(i)) (sorted lists)
 __global__ __launch_bounds__(TPB) void k_sel_row(const i64* __restrict__ soffc,
                                                  const int32_t* __restrict__ slist,
-                                                 const int32_t* __restrict__ cls, i64 n, i64 p,
+                                                 const int32_t* __restrict__ cls, i64 n,
+                                                 i64 r0, i64 r1, i64 p,
                                                  u64* __restrict__ out) {
   const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
   bool bit = false;
-  if (i < n) {
+  if (i < n && i >= r0 && i < r1) {   // row classes exist for this shard's pods
     const int32_t c = cls[i];
     i64 lo = soffc[c], hi = soffc[c + 1];
     while (lo < hi) {

@@ -281,6 +281,16 @@ def test_row_shards_combine_to_full():
         nands.append(~ca)
         cross.append(e.crosscheck(gid))
         pairs.append(e.shadow())
+        # row classes are shard-local: select bits only for the shard's pods
+        from kano._bits import words_to_bool
+        cls = e.classes()
+        assert (cls[:r0] == -1).all() and (cls[r1:] == -1).all() and (cls[r0:r1] >= 0).all()
+        for p in (0, 7, len(ps) - 1):
+            sel, _ = e.policy_sets(p)
+            full = words_to_bool(ref["sel"][p], n)
+            mask = np.zeros(n, bool)
+            mask[r0:r1] = True
+            assert np.array_equal(words_to_bool(sel, n), full & mask)
         e.close()
     assert np.array_equal(np.concatenate(rows), ref["M"])
     from kano._bits import set_bit_indices, words_to_bool
