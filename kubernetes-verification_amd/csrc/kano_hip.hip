@@ -92,7 +92,8 @@ struct kano_ctx {
   bool cols_valid = false;   // color/colnand describe M
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_timed = false;
-  bool alist_valid = false;  // allowed-pod lists materialised (kano_get_allow_csr)
+  bool alist_valid = false;
+  bool cols_deferred = false;  // column checks folded into the crosscheck pass (kano_verify)  // allowed-pod lists materialised (kano_get_allow_csr)
   int ch = 16;               // member rows per k_rows work item
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;
@@ -117,7 +118,7 @@ struct kano_ctx {
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
-  DBuf gid, cgroup, R, multi, A1, A2, own, cross, gmin, gmax;
+  DBuf gid, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
@@ -643,6 +644,18 @@ int read_sizes(kano_ctx* ctx) {
   return 0;
 }
 
+// column OR / NAND at class level (all_isolated / all_reachable)
+int mc_cols(kano_ctx* ctx) {
+  const i64 U = ctx->rc.U;
+  if (rows_local(ctx) > 0 && U > 0) {
+    hipLaunchKernelGGL(k_mc_cols, dim3(nblk(ctx->UAW, 64), nblk(U, 128)), dim3(TPB), 0,
+                       ctx->stream, P_<u64>(ctx->Mc), ctx->ldC, ctx->UAW, ctx->cc.U, U,
+                       P_<int32_t>(ctx->rc.mcnt), P_<u64>(ctx->col_or_c), P_<u64>(ctx->col_nand_c));
+    KLAUNCH();
+  }
+  return 0;
+}
+
 // allowed-pod lists per policy (members of its allowed column classes)
 int build_alist(kano_ctx* ctx) {
   const i64 P = ctx->P;
@@ -785,12 +798,7 @@ int do_back(kano_ctx* ctx, int path) {
       KLAUNCH();
     }
   }
-  if (rows_local(ctx) > 0) {
-    hipLaunchKernelGGL(k_mc_cols, dim3(nblk(ctx->UAW, 64), nblk(U, 128)), dim3(TPB), 0,
-                       ctx->stream, P_<u64>(ctx->Mc), ldMc, ctx->UAW, ctx->cc.U, U,
-                       P_<int32_t>(ctx->rc.mcnt), P_<u64>(ctx->col_or_c), P_<u64>(ctx->col_nand_c));
-    KLAUNCH();
-  }
+  if (!ctx->cols_deferred) KTRY(mc_cols(ctx));
   return 0;
 }
 
@@ -978,6 +986,10 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->R, sizeof(u64) * (i64)G * ldC));
+    KTRY(dalloc(ctx, ctx->ckey, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->corder, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1)));
+    KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * ((i64)G + 2)));
     KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
@@ -988,17 +1000,43 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
     KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
     for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
+    KTRY(fb.add(ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1), 0u));   // counts + cursors
     KTRY(fb.run());
     const i64 rl = rows_local(ctx);
     hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
                        P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
     KLAUNCH();
-    hipLaunchKernelGGL(k_cross_mc, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->Mc), ldC, UAW, U, P_<int32_t>(ctx->rc.mcnt),
-                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), P_<u64>(ctx->R),
-                       P_<u64>(ctx->multi));
+    // classes in group order (counting sort), then one pass over Mc; the
+    // pass also folds the column checks when the build deferred them
+    int32_t* kcnt = P_<int32_t>(ctx->kcnt);
+    hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+                       P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
+                       G, P_<int32_t>(ctx->ckey), kcnt);
     KLAUNCH();
+    {
+      ScanBatch sb(ctx);
+      KTRY(sb.add(kcnt, (i64)G + 1, P_<int32_t>(ctx->koff)));
+      KTRY(sb.run());
+    }
+    hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+                       P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
+                       P_<int32_t>(ctx->corder));
+    KLAUNCH();
+    const bool cols = ctx->cols_deferred;
+    // the live class count is koff[G + 1]: size the grid by U (idle tails
+    // exit at once)
+    hipLaunchKernelGGL(k_mc_fold, dim3(nblk(UAW, 64), nblk(U, (TPB / 64) * FOLD_PER_WAVE)),
+                       dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), ldC, UAW, ctx->cc.U,
+                       P_<int32_t>(ctx->corder), P_<int32_t>(ctx->koff) + G + 1,
+                       P_<int32_t>(ctx->ckey), G, P_<u64>(ctx->R), P_<u64>(ctx->multi),
+                       cols ? P_<u64>(ctx->col_or_c) : nullptr,
+                       cols ? P_<u64>(ctx->col_nand_c) : nullptr);
+    KLAUNCH();
+    if (cols) {
+      ctx->cols_deferred = false;
+      KTRY(do_rows(ctx));   // expand the column checks to pods
+    }
     hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
     KLAUNCH();
@@ -1138,7 +1176,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->sizes,   &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd};
+                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd,
+                  &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1347,7 +1386,9 @@ int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end) {
 }  // extern "C"
 
 namespace {
-int build_impl(kano_ctx* ctx, int path, bool rows_now) {
+// rows_now: launch the matrix write here; defer_cols: leave the column
+// checks to the crosscheck pass over Mc (kano_verify), finish_cols() after
+int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
@@ -1367,8 +1408,9 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now) {
   KTRY(do_front(ctx, path));
   KTRY(read_sizes(ctx));
   KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  ctx->cols_deferred = defer_cols;
   KTRY(do_back(ctx, path));
-  KTRY(do_rows(ctx));
+  if (!defer_cols) KTRY(do_rows(ctx));
   if (rows_now) KTRY(launch_rows(ctx));
   KCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->cols_valid = true;
@@ -1784,18 +1826,23 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
-  KTRY(build_impl(ctx, path, false));
+  KTRY(build_impl(ctx, path, false, gid != nullptr));
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
-  // column checks, crosscheck (device words)
+  const bool cross_on = gid && n > 0 && rows_local(ctx) > 0 && W > 0;
+  if (gid) KTRY(crosscheck_impl(ctx, gid, ngroups));
+  if (ctx->cols_deferred) {   // no crosscheck pass ran (empty shard / matrix)
+    ctx->cols_deferred = false;
+    KTRY(mc_cols(ctx));
+    KTRY(do_rows(ctx));
+  }
+  // column checks (device words)
   KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
   if (W > 0) {
     hipLaunchKernelGGL(k_col_final, dim3(nblk(W)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->colnand), W, n, P_<u64>(ctx->col_and));
     KLAUNCH();
   }
-  const bool cross_on = gid && n > 0 && rows_local(ctx) > 0 && W > 0;
-  if (gid) KTRY(crosscheck_impl(ctx, gid, ngroups));
   // the four result rows as index lists
   IdxRows ir{};
   ir.W = W;

@@ -648,6 +648,77 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
   wave_agg_minmax(gmin, gmax, c, g, act);
 }
 
+// Classes keyed by their group for one pass over Mc: key = g for classes
+// whose local members are all in group g, G for classes mixing groups (MULTI),
+// -1 for classes without local members.  Counted per key (counting sort).
+__global__ __launch_bounds__(TPB) void k_cls_key(i64 U, const int32_t* __restrict__ mcnt,
+                                                 const int32_t* __restrict__ gmin,
+                                                 const int32_t* __restrict__ gmax, int32_t G,
+                                                 int32_t* __restrict__ ckey, int32_t* kcnt) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  int32_t key = -1;
+  if (c < U && mcnt[c] > 0 && gmin[c] <= gmax[c]) key = gmin[c] == gmax[c] ? gmin[c] : G;
+  if (c < U) ckey[c] = key;
+  (void)wave_agg_inc(kcnt, key < 0 ? 0 : key, key >= 0);
+}
+
+__global__ __launch_bounds__(TPB) void k_cls_key_place(i64 U, const int32_t* __restrict__ ckey,
+                                                       const int32_t* __restrict__ koff,
+                                                       int32_t* kcur, int32_t* __restrict__ order) {
+  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  const int32_t key = c < U ? ckey[c] : -1;
+  const int32_t r = wave_agg_inc(kcur, key < 0 ? 0 : key, key >= 0);
+  if (key >= 0) order[koff[key] + r] = (int32_t)c;
+}
+
+// One pass over Mc in group order: R[g] |= Mc[c] (g = key), MULTI for key G;
+// with col_or / col_nand non-null also the column OR / NAND of
+// all_reachable / all_isolated.  Block = 64 words x (4 waves x 16 sorted
+// classes); runs of equal key are OR-ed in registers, one atomic per run.
+constexpr int FOLD_PER_WAVE = 16;
+__global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
+                                                 i64 Ua, const int32_t* __restrict__ order,
+                                                 const int32_t* __restrict__ nlive_p,
+                                                 const int32_t* __restrict__ ckey,
+                                                 int32_t G, u64* R, u64* multi, u64* col_or,
+                                                 u64* col_nand) {
+  __shared__ u64 red[2][TPB / 64][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const i64 w = (i64)blockIdx.x * 64 + lane;
+  const i64 nlive = *nlive_p;
+  const i64 k0 = ((i64)blockIdx.y * (TPB / 64) + wid) * FOLD_PER_WAVE;
+  const i64 k1 = min(nlive, k0 + FOLD_PER_WAVE);
+  const bool wok = w < UW;
+  const u64 vm = wok ? valid_mask(w, Ua) : 0ull;
+  u64 o = 0, na = 0, acc = 0;
+  int32_t cur = -1;
+  for (i64 k = k0; k < k1; ++k) {
+    const int32_t c = order[k];
+    const int32_t key = ckey[c];
+    const u64 v = wok ? Mc[(i64)c * ldMc + w] : 0ull;
+    o |= v;
+    na |= ~v & vm;
+    if (key != cur) {
+      if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
+      cur = key;
+      acc = 0;
+    }
+    acc |= v;
+  }
+  if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
+  if (col_or) {
+    red[0][wid][lane] = o;
+    red[1][wid][lane] = na;
+    __syncthreads();
+    if (wid == 0 && wok) {
+      o = red[0][0][lane] | red[0][1][lane] | red[0][2][lane] | red[0][3][lane];
+      na = red[1][0][lane] | red[1][1][lane] | red[1][2][lane] | red[1][3][lane];
+      if (o) atomicOr(&col_or[w], o);
+      if (na) atomicOr(&col_nand[w], na);
+    }
+  }
+}
+
 // R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per
 // class).
 __global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
