@@ -988,8 +988,11 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     KTRY(dalloc(ctx, ctx->R, sizeof(u64) * (i64)G * ldC));
     KTRY(dalloc(ctx, ctx->ckey, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->corder, sizeof(int32_t) * std::max<i64>(1, U)));
-    KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1)));
-    KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * ((i64)G + 2)));
+    const bool key_lds = (i64)G + 1 <= KEY_LDS_MAX;
+    const i64 knb = std::max<i64>(1, nblk(U, (i64)TPB * KEY_ITEMS));
+    const i64 kslots = key_lds ? ((i64)G + 1) * knb : (i64)G + 1;
+    KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1) + sizeof(int32_t) * kslots));
+    KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * (kslots + 1)));
     KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
     KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
@@ -1010,25 +1013,39 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     // classes in group order (counting sort), then one pass over Mc; the
     // pass also folds the column checks when the build deferred them
     int32_t* kcnt = P_<int32_t>(ctx->kcnt);
-    hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
-                       P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
-                       G, P_<int32_t>(ctx->ckey), kcnt);
-    KLAUNCH();
-    {
+    const int32_t* nlive = P_<int32_t>(ctx->koff) + kslots;   // the scan total
+    if (key_lds) {
+      int32_t* hist = kcnt + 2 * ((i64)G + 1);
+      hipLaunchKernelGGL(k_key_hist, dim3((unsigned)knb), dim3(TPB), 0, ctx->stream, U,
+                         P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
+                         P_<int32_t>(ctx->gmax), G, P_<int32_t>(ctx->ckey), hist);
+      KLAUNCH();
+      ScanBatch sb(ctx);
+      KTRY(sb.add(hist, kslots, P_<int32_t>(ctx->koff)));
+      KTRY(sb.run());
+      hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)knb), dim3(TPB), 0, ctx->stream, U,
+                         P_<int32_t>(ctx->ckey), G, P_<int32_t>(ctx->koff),
+                         P_<int32_t>(ctx->corder));
+      KLAUNCH();
+    } else {
+      hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+                         P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
+                         P_<int32_t>(ctx->gmax), G, P_<int32_t>(ctx->ckey), kcnt);
+      KLAUNCH();
       ScanBatch sb(ctx);
       KTRY(sb.add(kcnt, (i64)G + 1, P_<int32_t>(ctx->koff)));
       KTRY(sb.run());
+      hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+                         P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
+                         P_<int32_t>(ctx->corder));
+      KLAUNCH();
     }
-    hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
-                       P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
-                       P_<int32_t>(ctx->corder));
-    KLAUNCH();
     const bool cols = ctx->cols_deferred;
     // the live class count is koff[G + 1]: size the grid by U (idle tails
     // exit at once)
     hipLaunchKernelGGL(k_mc_fold, dim3(nblk(UAW, 64), nblk(U, (TPB / 64) * FOLD_PER_WAVE)),
                        dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), ldC, UAW, ctx->cc.U,
-                       P_<int32_t>(ctx->corder), P_<int32_t>(ctx->koff) + G + 1,
+                       P_<int32_t>(ctx->corder), nlive,
                        P_<int32_t>(ctx->ckey), G, P_<u64>(ctx->R), P_<u64>(ctx->multi),
                        cols ? P_<u64>(ctx->col_or_c) : nullptr,
                        cols ? P_<u64>(ctx->col_nand_c) : nullptr);

@@ -671,6 +671,52 @@ __global__ __launch_bounds__(TPB) void k_cls_key_place(i64 U, const int32_t* __r
   if (key >= 0) order[koff[key] + r] = (int32_t)c;
 }
 
+// Small key spaces (G + 1 <= KEY_LDS_MAX): a stable-free counting sort with
+// per-block histograms in LDS, no global atomics.  hist is bin-major,
+// hist[k * nb + b], so its exclusive scan is every (bin, block) start.
+constexpr int KEY_LDS_MAX = 8192;
+constexpr int KEY_ITEMS = 8;   // classes per thread
+__global__ __launch_bounds__(TPB) void k_key_hist(i64 U, const int32_t* __restrict__ mcnt,
+                                                  const int32_t* __restrict__ gmin,
+                                                  const int32_t* __restrict__ gmax, int32_t G,
+                                                  int32_t* __restrict__ ckey,
+                                                  int32_t* __restrict__ hist) {
+  __shared__ int32_t h[KEY_LDS_MAX];
+  const int nk = G + 1;
+  const i64 nb = gridDim.x;
+  for (int k = threadIdx.x; k < nk; k += TPB) h[k] = 0;
+  __syncthreads();
+  const i64 c0 = (i64)blockIdx.x * TPB * KEY_ITEMS;
+  for (int q = 0; q < KEY_ITEMS; ++q) {
+    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
+    if (c >= U) break;
+    int32_t key = -1;
+    if (mcnt[c] > 0 && gmin[c] <= gmax[c]) key = gmin[c] == gmax[c] ? gmin[c] : G;
+    ckey[c] = key;
+    if (key >= 0) atomicAdd(&h[key], 1);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nk; k += TPB) hist[(i64)k * nb + blockIdx.x] = h[k];
+}
+
+__global__ __launch_bounds__(TPB) void k_key_place_lds(i64 U, const int32_t* __restrict__ ckey,
+                                                       int32_t G,
+                                                       const int32_t* __restrict__ hoff,
+                                                       int32_t* __restrict__ order) {
+  __shared__ int32_t h[KEY_LDS_MAX];
+  const int nk = G + 1;
+  const i64 nb = gridDim.x;
+  for (int k = threadIdx.x; k < nk; k += TPB) h[k] = hoff[(i64)k * nb + blockIdx.x];
+  __syncthreads();
+  const i64 c0 = (i64)blockIdx.x * TPB * KEY_ITEMS;
+  for (int q = 0; q < KEY_ITEMS; ++q) {
+    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
+    if (c >= U) break;
+    const int32_t key = ckey[c];
+    if (key >= 0) order[atomicAdd(&h[key], 1)] = (int32_t)c;
+  }
+}
+
 // One pass over Mc in group order: R[g] |= Mc[c] (g = key), MULTI for key G;
 // with col_or / col_nand non-null also the column OR / NAND of
 // all_reachable / all_isolated.  Block = 64 words x (4 waves x 16 sorted

@@ -258,6 +258,34 @@ def test_verify_fused_shards():
     assert sorted(cross) == ref["user_crosscheck"]
 
 
+@pytest.mark.parametrize("mod", [3, 10**9])
+def test_crosscheck_group_counts(mod):
+    """user_crosscheck with few groups (LDS counting sort) and with one group
+    per pod (G > 8192: the atomic fallback), against M itself."""
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano._bits import set_bit_indices, words_to_bool
+    from kano.synth import make_config
+    cl = make_config("C2")
+    n = cl.n
+    gid = (np.arange(n) % mod).astype(np.int32)
+    eng = DeviceBuild(tables_from_cluster(cl), build=False)
+    r = eng.verify(gid, ngroups=int(gid.max()) + 1, shadow=False)
+    M = np.stack([words_to_bool(w, n) for w in eng.rows(0, n)])   # n x n bools
+    # cross[j] = exists i: M[i, j] and g(i) != g(j): column count minus the
+    # count from j's own group
+    total = M.sum(axis=0)
+    if mod >= n:
+        same = M[np.arange(n), np.arange(n)].astype(np.int64)
+    else:
+        per_group = np.stack([M[gid == g].sum(axis=0) for g in range(mod)])
+        same = per_group[gid, np.arange(n)]
+    cross = total - same > 0
+    assert r["user_crosscheck"].tolist() == np.flatnonzero(cross).tolist()
+    assert set_bit_indices(eng.crosscheck(gid), n).tolist() == np.flatnonzero(cross).tolist()
+    eng.close()
+
+
 def test_row_shards_combine_to_full():
     """Row-sharded contexts (the multi-GPU partition) reproduce the full
     matrix; their column flags combine by MAX (= OR) exactly."""
