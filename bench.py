@@ -78,11 +78,10 @@ class Step:
         from kano._engine import PinnedBuffer
         self.pin = None
         self.pin_idx = None
-        # group ids in page-locked memory (async upload), group count declared
-        self.ngroups = int(gid.max()) + 1 if len(gid) else 0
-        self.pin_gid = PinnedBuffer(4 * max(n, 1))
-        self.gid_pinned = self.pin_gid.view(np.int32, n)
-        self.gid_pinned[:] = gid
+        # the tenant groups are resident input, uploaded once like the label
+        # tables (user_hashmap, algorithm.py:20-24)
+        if world == 1:
+            eng.set_groups(gid)
         self.pin_pairs = 0
         self.PinnedBuffer = PinnedBuffer
         self.results = {}
@@ -103,8 +102,8 @@ class Step:
                 pairs = self.pin.view(np.int32, 2 * self.pin_pairs)
             if self.pin_idx is None:
                 self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
-            r = eng.verify(self.gid_pinned, sys_row=0, shadow=self.shadow, pairs=pairs,
-                           idx=self.pin_idx.view(np.int32, 4 * max(n, 1)), ngroups=self.ngroups)
+            r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs,
+                           idx=self.pin_idx.view(np.int32, 4 * max(n, 1)))
             for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
                 res[k] = r[k]
             if self.shadow:

@@ -153,7 +153,8 @@ int kano_conflict(kano_ctx* ctx, int* raises);
  *   [all_reachable (algorithm.py:4-9), all_isolated (:12-17),
  *    user_crosscheck for the group ids gid (:20-42; 0 when gid is NULL;
  *    ngroups > 0 declares every gid < ngroups, checked on the device, so the
- *    host does not scan gid; ngroups <= 0 scans it),
+ *    host does not scan gid; ngroups <= 0 scans it; gid NULL with ngroups ==
+ *    KANO_STORED_GROUPS uses the groups stored by kano_set_groups),
  *    system_isolation(sys_row) (:45-55; -1 when sys_row is not in this shard)].
  * On a row shard the column lists cover only this shard's rows (combine
  * with kano_col_flags_dev / kano_crosscheck_dev across shards instead).
@@ -163,6 +164,12 @@ int kano_conflict(kano_ctx* ctx, int* raises);
 int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
                 int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count);
+
+/* user_hashmap (algorithm.py:20-24) as resident input: the group id of
+ * every pod uploaded once (like the label tables), for kano_verify with
+ * gid = NULL, ngroups = KANO_STORED_GROUPS.  ngroups <= 0: max(gid) + 1. */
+#define KANO_STORED_GROUPS (-1)
+int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups);
 
 /* Timing of the last kano_build / kano_shadow stages on the context stream
  * (HIP events), milliseconds: [classes, allow, select + plan, rows stage,

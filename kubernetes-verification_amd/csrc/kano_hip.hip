@@ -93,7 +93,10 @@ struct kano_ctx {
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_timed = false;
   bool alist_valid = false;
-  bool cols_deferred = false;  // column checks folded into the crosscheck pass (kano_verify)  // allowed-pod lists materialised (kano_get_allow_csr)
+  bool cols_deferred = false;
+  int32_t cross_G = 0;         // group count of the last class-level crosscheck
+  i64 groups_n = -1;           // kano_set_groups: pods covered (-1: none stored)
+  int32_t groups_G = 0;  // column checks folded into the crosscheck pass (kano_verify)  // allowed-pod lists materialised (kano_get_allow_csr)
   int ch = 16;               // member rows per k_rows work item
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
   int ld_align = 16;
@@ -960,7 +963,10 @@ int recompute_cols(kano_ctx* ctx) {
 
 // ngroups > 0: the caller declares every gid in [0, ngroups) (no host scan;
 // the kernels flag a violation in ctx->err_dev); ngroups <= 0: scanned here
-int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
+// tail_in_verify: leave the per-pod cross bits and the column expansion to
+// kano_verify's fused k_verify_cols
+int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
+                    bool tail_in_verify = false) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
@@ -970,14 +976,21 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
   int32_t G = ngroups;
-  if (G <= 0) {
-    G = 0;
-    for (i64 i = 0; i < n; ++i) {
-      if (gid[i] < 0) return fail(ctx, -EINVAL, "kano_crosscheck: negative group id");
-      G = std::max(G, gid[i] + 1);
+  if (!gid) {   // the groups stored by kano_set_groups (already on the device)
+    if (ctx->groups_n != n) return fail(ctx, -EINVAL, "crosscheck: no stored groups for these pods");
+    G = ctx->groups_G;
+  } else {
+    if (G <= 0) {
+      G = 0;
+      for (i64 i = 0; i < n; ++i) {
+        if (gid[i] < 0) return fail(ctx, -EINVAL, "kano_crosscheck: negative group id");
+        G = std::max(G, gid[i] + 1);
+      }
     }
+    ctx->groups_n = -1;   // the device copy no longer holds the stored groups
+    KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                        ctx->stream));
   }
-  KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
 
   if (!ctx->rows_dirty) {
     // class level: rows of a row class are equal, columns of a column class
@@ -1052,11 +1065,13 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     KLAUNCH();
     if (cols) {
       ctx->cols_deferred = false;
-      KTRY(do_rows(ctx));   // expand the column checks to pods
+      if (!tail_in_verify) KTRY(do_rows(ctx));   // expand the column checks to pods
     }
     hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
     KLAUNCH();
+    ctx->cross_G = G;
+    if (tail_in_verify) return 0;
     hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
                        ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
@@ -1843,59 +1858,85 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
-  KTRY(build_impl(ctx, path, false, gid != nullptr));
+  KTRY(build_impl(ctx, path, false, gid != nullptr || ngroups == KANO_STORED_GROUPS));
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
-  const bool cross_on = gid && n > 0 && rows_local(ctx) > 0 && W > 0;
-  if (gid) KTRY(crosscheck_impl(ctx, gid, ngroups));
+  const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
+  const bool want_cross = gid || stored;
+  const bool cross_on = want_cross && n > 0 && rows_local(ctx) > 0 && W > 0;
+  if (want_cross) KTRY(crosscheck_impl(ctx, gid, ngroups, true));
   if (ctx->cols_deferred) {   // no crosscheck pass ran (empty shard / matrix)
     ctx->cols_deferred = false;
     KTRY(mc_cols(ctx));
-    KTRY(do_rows(ctx));
   }
-  // column checks (device words)
+  // the column tail in one pass (k_verify_cols), then the four result rows
+  // as index lists: all_reachable, all_isolated, user_crosscheck,
+  // system_isolation
+  const i64 nb = std::max<i64>(1, nblk(W * 64));
   KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
-  if (W > 0) {
-    hipLaunchKernelGGL(k_col_final, dim3(nblk(W)), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->colnand), W, n, P_<u64>(ctx->col_and));
-    KLAUNCH();
-  }
-  // the four result rows as index lists
-  IdxRows ir{};
-  ir.W = W;
-  ir.n = n;
-  ir.nb = std::max<i64>(1, nblk(W));
-  ir.row[0] = P_<u64>(ctx->col_and);
-  ir.row[1] = P_<u64>(ctx->color);
-  ir.inv[1] = 1;
-  ir.row[2] = gid && rows_local(ctx) > 0 ? P_<u64>(ctx->cross) : nullptr;
-  if (have_sys && W > 0) {
-    KTRY(dalloc(ctx, ctx->sysrow, sizeof(u64) * ctx->ldM));
-    hipLaunchKernelGGL(k_row_from_mc, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->Mc), ctx->ldC, P_<int32_t>(ctx->rc.cls), (i64)sys_row,
-                       P_<int32_t>(ctx->cc.cls), n, W, P_<u64>(ctx->sysrow));
-    KLAUNCH();
-  }
-  ir.row[3] = have_sys ? P_<u64>(ctx->sysrow) : nullptr;
-  ir.inv[3] = 1;
-  const i64 nb4 = 4 * ir.nb;
-  KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * nb4));
-  KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * (nb4 + 4)));
+  KTRY(dalloc(ctx, ctx->sysrow, sizeof(u64) * std::max<i64>(1, W)));
+  KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * 4 * nb));
+  KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * 4 * (nb + 1)));
   KTRY(dalloc(ctx, ctx->idxd, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));
-  hipLaunchKernelGGL(k_idx_count, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
-                     P_<i64>(ctx->icnt));
-  KLAUNCH();
+  const bool sys_on = have_sys && W > 0;
+  if (n > 0 && W > 0) {
+    FinishArgs fa{};
+    fa.cla = P_<int32_t>(ctx->cc.cls);
+    fa.n = n;
+    fa.W = W;
+    fa.nb = nb;
+    fa.col_or_c = P_<u64>(ctx->col_or_c);
+    fa.col_nand_c = P_<u64>(ctx->col_nand_c);
+    fa.color = P_<u64>(ctx->color);
+    fa.colnand = P_<u64>(ctx->colnand);
+    fa.col_and = P_<u64>(ctx->col_and);
+    if (cross_on) {
+      fa.gid = P_<int32_t>(ctx->gid);
+      fa.G = ctx->cross_G;
+      fa.R = P_<u64>(ctx->R);
+      fa.ldC = ctx->ldC;
+      fa.multi = P_<u64>(ctx->multi);
+      fa.A1 = P_<u64>(ctx->A1);
+      fa.A2 = P_<u64>(ctx->A2);
+      fa.cross = P_<u64>(ctx->cross);
+      fa.err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
+    }
+    fa.ldC = ctx->ldC;
+    if (sys_on) {
+      fa.Mc = P_<u64>(ctx->Mc);
+      fa.clr = P_<int32_t>(ctx->rc.cls);
+      fa.sys_row = sys_row;
+      fa.sysrow = P_<u64>(ctx->sysrow);
+    }
+    fa.icnt = P_<i64>(ctx->icnt);
+    hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
+    KLAUNCH();
+  } else {
+    KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
+  }
   {
     ScanBatch sb(ctx);   // one job per row; row totals land in SZ_IDX0..3
     for (int r = 0; r < 4; ++r)
-      KTRY(sb.add(P_<i64>(ctx->icnt) + r * ir.nb, ir.nb, P_<i64>(ctx->ioff) + r * (ir.nb + 1),
+      KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
                   SZ_IDX0 + r));
     KTRY(sb.run());
   }
+  IdxRows ir{};
+  ir.W = W;
+  ir.n = n;
+  ir.nb = nb;
+  ir.row[0] = P_<u64>(ctx->col_and);
+  ir.row[1] = P_<u64>(ctx->color);
+  ir.inv[1] = 1;
+  ir.row[2] = cross_on ? P_<u64>(ctx->cross) : nullptr;
+  ir.row[3] = sys_on ? P_<u64>(ctx->sysrow) : nullptr;
+  ir.inv[3] = 1;
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
-  hipLaunchKernelGGL(k_idx_write, dim3((unsigned)ir.nb, 4), dim3(TPB), 0, ctx->stream, ir,
-                     P_<i64>(ctx->ioff), ir.nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
-  KLAUNCH();
+  if (n > 0 && W > 0) {
+    hipLaunchKernelGGL(k_idx_write, dim3((unsigned)nb, 4), dim3(TPB), 0, ctx->stream, ir,
+                       P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
+    KLAUNCH();
+  }
   // policy_shadow up to its size read
   if (shadow_count) KTRY(shadow_front(ctx));
   KTRY(launch_rows(ctx));
@@ -1924,6 +1965,29 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
                         ctx->stream));
   KTRY(join_rows(ctx));  // the matrix is part of the result
   return sync(ctx);
+}
+
+int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups) {
+  if (!ctx) return -EINVAL;
+  if (!ctx->have_pods) return fail(ctx, -EINVAL, "kano_set_groups before kano_set_pods");
+  const i64 n = ctx->n;
+  if (n > 0 && !gid) return fail(ctx, -EINVAL, "kano_set_groups: gid is NULL");
+  KCHK(hipSetDevice(ctx->device));
+  int32_t G = 0;
+  for (i64 i = 0; i < n; ++i) {
+    if (gid[i] < 0) return fail(ctx, -EINVAL, "kano_set_groups: negative group id");
+    G = std::max(G, gid[i] + 1);
+  }
+  if (ngroups > 0 && ngroups < G) return fail(ctx, -EINVAL, "kano_set_groups: id >= ngroups");
+  if (ngroups > 0) G = ngroups;
+  KTRY(join_rows(ctx));
+  KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
+  if (n > 0)
+    KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+  KTRY(sync(ctx));
+  ctx->groups_n = n;
+  ctx->groups_G = G;
+  return 0;
 }
 
 int kano_host_alloc(size_t bytes, void** out) {

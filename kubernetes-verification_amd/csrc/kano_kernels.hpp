@@ -1454,38 +1454,91 @@ struct IdxRows {
   i64 W, n, nb;
 };
 
-__device__ __forceinline__ u64 idx_word(const IdxRows& a, int r, i64 w) {
-  if (!a.row[r] || w >= a.W) return 0ull;
-  const u64 v = a.row[r][w];
-  return (a.inv[r] ? ~v : v) & valid_mask(w, a.n);
+// kano_verify's column tail in one pass, thread per pod j (ca = its column
+// class): the column checks expanded from class level (all_isolated /
+// all_reachable words), user_crosscheck's cross bit from the group rows
+// (cross = MULTI | A2 | (A1 & ~R[g(j)])), the system row from Mc, and per
+// block of TPB pods the count of each result row's listed pods.
+struct FinishArgs {
+  const int32_t* cla;
+  i64 n, W, nb;
+  const u64* col_or_c;
+  const u64* col_nand_c;
+  u64* color;
+  u64* colnand;
+  u64* col_and;
+  const int32_t* gid;    // nullable: no crosscheck
+  int32_t G;
+  const u64* R;
+  i64 ldC;
+  const u64* multi;
+  const u64* A1;
+  const u64* A2;
+  u64* cross;
+  int32_t* err;
+  const u64* Mc;         // nullable: no system row
+  const int32_t* clr;    // row class of each pod
+  i64 sys_row;
+  u64* sysrow;
+  i64* icnt;             // [r * nb + b], r: reachable, isolated, cross, sys-isolated
+};
+
+__device__ __forceinline__ bool mc_bit(const u64* row, int32_t ca) {
+  return (row[ca >> 6] >> (ca & 63)) & 1ull;
 }
 
-__global__ __launch_bounds__(TPB) void k_idx_count(IdxRows a, i64* __restrict__ bcnt) {
+__global__ __launch_bounds__(TPB) void k_verify_cols(FinishArgs a) {
   __shared__ i64 sm[4];
-  const int r = blockIdx.y;
-  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
-  const i64 c = __popcll(idx_word(a, r, w));
-  const i64 tot = block_sum(c, sm);
-  if (threadIdx.x == 0) bcnt[r * a.nb + blockIdx.x] = tot;
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;   // grid covers W * 64
+  const bool live = j < a.n;
+  const int32_t ca = live ? a.cla[j] : 0;
+  const bool orb = live && mc_bit(a.col_or_c, ca);
+  const bool nab = live && mc_bit(a.col_nand_c, ca);
+  bool crb = false;
+  if (a.gid && live) {
+    const int32_t g = a.gid[j];
+    bool own = false;
+    if (g < 0 || g >= a.G) atomicOr(a.err, 1);
+    else own = mc_bit(a.R + (i64)g * a.ldC, ca);
+    crb = mc_bit(a.multi, ca) || mc_bit(a.A2, ca) || (mc_bit(a.A1, ca) && !own);
+  }
+  const bool syb = a.Mc && live && mc_bit(a.Mc + (i64)a.clr[a.sys_row] * a.ldC, ca);
+  const u64 wo = __ballot(orb), wn = __ballot(nab), wc = __ballot(crb), ws = __ballot(syb);
+  const i64 w = j >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    a.color[w] = wo;
+    a.colnand[w] = wn;
+    a.col_and[w] = ~wn & valid_mask(w, a.n);
+    if (a.gid) a.cross[w] = wc;
+    if (a.Mc) a.sysrow[w] = ws;
+  }
+  const i64 c0 = block_sum((i64)(live && !nab), sm);
+  const i64 c1 = block_sum((i64)(live && !orb), sm);
+  const i64 c2 = block_sum((i64)crb, sm);
+  const i64 c3 = block_sum((i64)(a.Mc && live && !syb), sm);
+  if (threadIdx.x == 0) {
+    a.icnt[blockIdx.x] = c0;
+    a.icnt[a.nb + blockIdx.x] = c1;
+    a.icnt[2 * a.nb + blockIdx.x] = c2;
+    a.icnt[3 * a.nb + blockIdx.x] = c3;
+  }
 }
 
-// row r's lists start after the totals of rows < r (rowtot: 4 size slots)
+// thread per pod: row r's listed pods in ascending order; row r starts after
+// the totals of rows < r (rowtot: 4 size slots)
 __global__ __launch_bounds__(TPB) void k_idx_write(IdxRows a, const i64* __restrict__ boff,
                                                    i64 ldo, const u64* __restrict__ rowtot,
                                                    int32_t* __restrict__ idx) {
   __shared__ i64 sm[4];
   const int r = blockIdx.y;
-  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
-  u64 v = idx_word(a, r, w);
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
+  bool bit = false;
+  if (a.row[r] && j < a.n) bit = ((a.row[r][j >> 6] >> (j & 63)) & 1ull) != (a.inv[r] != 0);
   i64 row0 = 0;
   for (int q = 0; q < r; ++q) row0 += (i64)rowtot[q];
   i64 tot;
-  i64 pos = block_excl_scan((i64)__popcll(v), sm, tot) + row0 + boff[r * ldo + blockIdx.x];
-  while (v) {
-    const int b = __ffsll((long long)v) - 1;
-    idx[pos++] = (int32_t)(w * 64 + b);
-    v &= v - 1;
-  }
+  const i64 pos = block_excl_scan((i64)bit, sm, tot) + row0 + boff[r * ldo + blockIdx.x];
+  if (bit) idx[pos] = (int32_t)j;
 }
 
 }  // namespace kano

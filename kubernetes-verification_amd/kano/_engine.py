@@ -219,7 +219,15 @@ class DeviceBuild:
     def shadow(self) -> np.ndarray:
         return self.shadow_fetch(self.shadow_count())
 
-    def verify(self, gid: Optional[np.ndarray] = None, sys_row: int = 0, shadow: bool = True,
+    def set_groups(self, gid: np.ndarray, ngroups: int = 0) -> None:
+        """kano_set_groups: upload the pods' group ids once (resident input);
+        then ``verify(gid="stored")`` runs user_crosscheck on them."""
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        if gid.shape[0] != self.n:
+            raise ValueError("gid must have one entry per pod")
+        self._chk(self.lib.kano_set_groups(self.ctx, _ptr(gid), int(ngroups)), "kano_set_groups")
+
+    def verify(self, gid=None, sys_row: int = 0, shadow: bool = True,
                pairs: Optional[np.ndarray] = None, idx: Optional[np.ndarray] = None,
                ngroups: int = 0, path: Optional[str] = None) -> dict:
         """kano_verify: build + every check in one call (three host syncs).
@@ -236,7 +244,10 @@ class DeviceBuild:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
         elif idx.size < 4 * n:
             raise ValueError("idx buffer needs 4*n entries")
-        if gid is not None:
+        stored = isinstance(gid, str) and gid == "stored"
+        if stored:
+            gid, ngroups = None, nat.STORED_GROUPS
+        elif gid is not None:
             if not (isinstance(gid, np.ndarray) and gid.dtype == np.int32
                     and gid.flags.c_contiguous):
                 gid = np.ascontiguousarray(gid, dtype=np.int32)
@@ -256,7 +267,7 @@ class DeviceBuild:
             k = int(counts[r])
             out[name] = idx[o:o + k] if k >= 0 else None
             o += max(k, 0)
-        if gid is None:
+        if gid is None and not stored:
             out["user_crosscheck"] = None
         if shadow:
             k = int(cnt.value)

@@ -48,6 +48,7 @@ SIGNATURES = {
     "kano_conflict": (c_int, [c_void_p, POINTER(c_int)]),
     "kano_verify": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_void_p, c_void_p,
                             c_void_p, c_int64, POINTER(c_int64)]),
+    "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),
@@ -57,6 +58,7 @@ INFO_SLOTS = 16
 INFO = dict(N=0, W=1, P=2, U=3, NNZ_SEL=4, NNZ_ALW=5, HEAVY=6, ROW0=7, ROW1=8, MAXSEL=9,
             UA=10, HEAVY_PATH=11, WORK_ITEMS=12)
 PATHS = {"auto": 0, "bitwise": 1, "mfma": 2}
+STORED_GROUPS = -1   # KANO_STORED_GROUPS
 
 
 class KanoNativeError(RuntimeError):

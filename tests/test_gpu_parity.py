@@ -176,8 +176,10 @@ def test_verify_fused_c2(cap):
     _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
     eng = DeviceBuild(tables_from_cluster(cl), build=False)
     pin = PinnedBuffer(max(cap, 1) * 8)
-    for ng in (0, int(gid.max()) + 1):   # host-scanned / declared group count
-        r = eng.verify(gid, sys_row=0, shadow=True, ngroups=ng,
+    eng.set_groups(gid)
+    for g, ng in ((gid, 0), (gid, int(gid.max()) + 1), ("stored", 0)):
+        # host-scanned / declared group count / groups stored on the device
+        r = eng.verify(g, sys_row=0, shadow=True, ngroups=ng,
                        pairs=pin.view(np.int32, 2 * cap) if cap else None)
         assert sha(eng.rows(0, n)) == exp["M_sha256"]
         assert r["all_reachable"].tolist() == exp["all_reachable"]
