@@ -121,7 +121,7 @@ struct kano_ctx {
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
-  DBuf gid, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
+  DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   i64 shadow_total = -1;
@@ -976,9 +976,11 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
     KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
   int32_t G = ngroups;
+  const int32_t* gdev = P_<int32_t>(ctx->gid);
   if (!gid) {   // the groups stored by kano_set_groups (already on the device)
     if (ctx->groups_n != n) return fail(ctx, -EINVAL, "crosscheck: no stored groups for these pods");
     G = ctx->groups_G;
+    gdev = P_<int32_t>(ctx->gids);
   } else {
     if (G <= 0) {
       G = 0;
@@ -987,7 +989,6 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
         G = std::max(G, gid[i] + 1);
       }
     }
-    ctx->groups_n = -1;   // the device copy no longer holds the stored groups
     KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice,
                         ctx->stream));
   }
@@ -1020,7 +1021,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
     KTRY(fb.run());
     const i64 rl = rows_local(ctx);
     hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
+                       gdev, G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
                        P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
     KLAUNCH();
     // classes in group order (counting sort), then one pass over Mc; the
@@ -1073,7 +1074,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
     ctx->cross_G = G;
     if (tail_in_verify) return 0;
     hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->gid), G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
+                       gdev, G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
                        ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
                        P_<u64>(ctx->cross), err);
     KLAUNCH();
@@ -1092,7 +1093,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
   const i64 nclass = rows_local(ctx);
   KTRY(dalloc(ctx, ctx->cgroup, sizeof(int32_t) * std::max<i64>(1, nclass)));
   hipLaunchKernelGGL(k_cross_classgroup, dim3(nblk(nclass)), dim3(TPB), 0, ctx->stream,
-                     P_<int32_t>(ctx->gid), moff, mem, nclass, P_<int32_t>(ctx->cgroup));
+                     gdev, moff, mem, nclass, P_<int32_t>(ctx->cgroup));
   KLAUNCH();
   // groups in batches so that R fits ~2 GiB
   const i64 budget_rows = std::max<i64>(1, (2ll << 30) / (8 * ldM));
@@ -1110,7 +1111,7 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
                        P_<u64>(ctx->R), ldM, W, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
     KLAUNCH();
     hipLaunchKernelGGL(k_cross_own, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->gid), n, P_<u64>(ctx->R), ldM, g0, g1, P_<u64>(ctx->own));
+                       gdev, n, P_<u64>(ctx->R), ldM, g0, g1, P_<u64>(ctx->own));
     KLAUNCH();
   }
   hipLaunchKernelGGL(k_cross_final, dim3(nblk(W)), dim3(TPB), 0, ctx->stream, P_<u64>(ctx->multi),
@@ -1209,7 +1210,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->sizes,   &ctx->icnt,      &ctx->ioff,
                   &ctx->sysrow, &ctx->wicls,   &ctx->idxd,
-                  &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff};
+                  &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff,
+                  &ctx->gids};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1891,7 +1893,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
     fa.colnand = P_<u64>(ctx->colnand);
     fa.col_and = P_<u64>(ctx->col_and);
     if (cross_on) {
-      fa.gid = P_<int32_t>(ctx->gid);
+      fa.gid = stored ? P_<int32_t>(ctx->gids) : P_<int32_t>(ctx->gid);
       fa.G = ctx->cross_G;
       fa.R = P_<u64>(ctx->R);
       fa.ldC = ctx->ldC;
@@ -1981,9 +1983,10 @@ int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups) {
   if (ngroups > 0 && ngroups < G) return fail(ctx, -EINVAL, "kano_set_groups: id >= ngroups");
   if (ngroups > 0) G = ngroups;
   KTRY(join_rows(ctx));
-  KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
+  KTRY(dalloc(ctx, ctx->gids, sizeof(int32_t) * std::max<i64>(1, n)));
   if (n > 0)
-    KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+    KCHK(hipMemcpyAsync(ctx->gids.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                        ctx->stream));
   KTRY(sync(ctx));
   ctx->groups_n = n;
   ctx->groups_G = G;
