@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cerrno>
 #include <cstdint>
 #include <cstdlib>
@@ -677,7 +678,7 @@ int build_alist(kano_ctx* ctx) {
 // list) and the compressed matrix Mc (row classes x column classes): light
 // classes by scatter, heavy classes by bitwise OR or the int8 MFMA
 // contraction; column checks at class level
-int do_back(kano_ctx* ctx, int path) {
+int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra) {
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
   ctx->heavy_path = 0;
   bool mfma = false;
@@ -714,6 +715,7 @@ int do_back(kano_ctx* ctx, int path) {
       KTRY(fb.add(ctx->ACT, sizeof(u64) * ctx->PB * ctx->cc.U, 0u));
       KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
     }
+    if (extra) KTRY(extra(fb));   // the caller's fills (kano_verify: crosscheck, shadow)
     KTRY(fb.run());
   }
   if (U > 0) {
@@ -963,24 +965,35 @@ int recompute_cols(kano_ctx* ctx) {
 
 // ngroups > 0: the caller declares every gid in [0, ngroups) (no host scan;
 // the kernels flag a violation in ctx->err_dev); ngroups <= 0: scanned here
-// tail_in_verify: leave the per-pod cross bits and the column expansion to
-// kano_verify's fused k_verify_cols
-int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
-                    bool tail_in_verify = false) {
+// ---- user_crosscheck at class level, in stages ------------------------------
+// (kano_verify interleaves the stages with policy_shadow's so that their
+// fills and scans share launches)
+struct CrossPlan {
+  bool on = false;           // class-level pass needed (pods, rows, words present)
+  const int32_t* gdev = nullptr;
+  int32_t G = 0;
+  bool key_lds = false;
+  i64 knb = 0, kslots = 0;
+};
+
+// host checks, group upload, allocations; fills go to fb
+int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp,
+                  FillBatch& fb) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
   KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
-  if (n == 0 || rows_local(ctx) == 0 || W == 0 || ctx->rows_dirty)
-    KCHK(hipMemsetAsync(ctx->cross.p, 0, sizeof(u64) * ldM, ctx->stream));
+  KTRY(fb.add_raw(err, sizeof(u64), 0u));
+  KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
+  cp.on = false;
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
   int32_t G = ngroups;
-  const int32_t* gdev = P_<int32_t>(ctx->gid);
+  cp.gdev = P_<int32_t>(ctx->gid);
   if (!gid) {   // the groups stored by kano_set_groups (already on the device)
     if (ctx->groups_n != n) return fail(ctx, -EINVAL, "crosscheck: no stored groups for these pods");
     G = ctx->groups_G;
-    gdev = P_<int32_t>(ctx->gids);
+    cp.gdev = P_<int32_t>(ctx->gids);
   } else {
     if (G <= 0) {
       G = 0;
@@ -992,90 +1005,114 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0,
     KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice,
                         ctx->stream));
   }
+  cp.G = G;
+  cp.on = true;
+  if (ctx->rows_dirty) return 0;   // the M-based path allocates its own
+  const i64 U = ctx->rc.U, ldC = ctx->ldC;
+  KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
+  KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * std::max<i64>(1, U)));
+  KTRY(dalloc(ctx, ctx->R, sizeof(u64) * std::max<i64>(1, (i64)G * ldC)));
+  KTRY(dalloc(ctx, ctx->ckey, sizeof(int32_t) * std::max<i64>(1, U)));
+  KTRY(dalloc(ctx, ctx->corder, sizeof(int32_t) * std::max<i64>(1, U)));
+  cp.key_lds = (i64)G + 1 <= KEY_LDS_MAX;
+  cp.knb = std::max<i64>(1, nblk(U, (i64)TPB * KEY_ITEMS));
+  cp.kslots = cp.key_lds ? ((i64)G + 1) * cp.knb : (i64)G + 1;
+  KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1) + sizeof(int32_t) * cp.kslots));
+  KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * (cp.kslots + 1)));
+  KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
+  KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
+  KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
+  KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
+  KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
+  KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
+  for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
+  KTRY(fb.add(ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1), 0u));   // counts + cursors
+  return 0;
+}
 
+// group range per class, group keys and their histogram; the key scan job
+// goes to sb
+int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
+  if (!cp.on) return 0;
+  const i64 U = ctx->rc.U, G = cp.G, rl = rows_local(ctx);
+  int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
+  hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
+                     (int32_t)G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
+                     P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
+  KLAUNCH();
+  int32_t* kcnt = P_<int32_t>(ctx->kcnt);
+  if (cp.key_lds) {   // classes in group order: per-block LDS histograms
+    int32_t* hist = kcnt + 2 * (G + 1);
+    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, U,
+                       P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
+                       (int32_t)G, P_<int32_t>(ctx->ckey), hist);
+    KLAUNCH();
+    KTRY(sb.add(hist, cp.kslots, P_<int32_t>(ctx->koff)));
+  } else {
+    hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+                       P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
+                       (int32_t)G, P_<int32_t>(ctx->ckey), kcnt);
+    KLAUNCH();
+    KTRY(sb.add(kcnt, G + 1, P_<int32_t>(ctx->koff)));
+  }
+  return 0;
+}
+
+// classes placed in group order, one pass over Mc (R[g], MULTI, and the
+// column checks when the build deferred them), group overlaps A1 / A2
+int cross_stage_b(kano_ctx* ctx, const CrossPlan& cp) {
+  if (!cp.on) return 0;
+  const i64 U = ctx->rc.U, G = cp.G, ldC = ctx->ldC, UAW = ctx->UAW;
+  int32_t* kcnt = P_<int32_t>(ctx->kcnt);
+  if (cp.key_lds) {
+    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, U,
+                       P_<int32_t>(ctx->ckey), (int32_t)G, P_<int32_t>(ctx->koff),
+                       P_<int32_t>(ctx->corder));
+  } else {
+    hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+                       P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
+                       P_<int32_t>(ctx->corder));
+  }
+  KLAUNCH();
+  const bool cols = ctx->cols_deferred;
+  const int32_t* nlive = P_<int32_t>(ctx->koff) + cp.kslots;   // the key scan's total
+  hipLaunchKernelGGL(k_mc_fold, dim3(nblk(UAW, 64), nblk(U, (TPB / 64) * FOLD_PER_WAVE)),
+                     dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), ldC, UAW, ctx->cc.U,
+                     P_<int32_t>(ctx->corder), nlive, P_<int32_t>(ctx->ckey), (int32_t)G,
+                     P_<u64>(ctx->R), P_<u64>(ctx->multi),
+                     cols ? P_<u64>(ctx->col_or_c) : nullptr,
+                     cols ? P_<u64>(ctx->col_nand_c) : nullptr);
+  KLAUNCH();
+  ctx->cols_deferred = false;
+  hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
+                     P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
+  KLAUNCH();
+  ctx->cross_G = (int32_t)G;
+  return 0;
+}
+
+int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
+  const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
+  CrossPlan cp;
+  {
+    FillBatch fb(ctx);
+    KTRY(cross_prepare(ctx, gid, ngroups, cp, fb));
+    KTRY(fb.run());
+  }
+  if (!cp.on) return 0;
+  const int32_t G = cp.G;
+  const int32_t* gdev = cp.gdev;
+  int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
   if (!ctx->rows_dirty) {
     // class level: rows of a row class are equal, columns of a column class
     // are equal; everything runs on Mc (U_r x U_a bits)
-    const i64 U = ctx->rc.U, ldC = ctx->ldC, UAW = ctx->UAW;
-    KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
-    KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * std::max<i64>(1, U)));
-    KTRY(dalloc(ctx, ctx->R, sizeof(u64) * (i64)G * ldC));
-    KTRY(dalloc(ctx, ctx->ckey, sizeof(int32_t) * std::max<i64>(1, U)));
-    KTRY(dalloc(ctx, ctx->corder, sizeof(int32_t) * std::max<i64>(1, U)));
-    const bool key_lds = (i64)G + 1 <= KEY_LDS_MAX;
-    const i64 knb = std::max<i64>(1, nblk(U, (i64)TPB * KEY_ITEMS));
-    const i64 kslots = key_lds ? ((i64)G + 1) * knb : (i64)G + 1;
-    KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1) + sizeof(int32_t) * kslots));
-    KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * (kslots + 1)));
-    KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
-    KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
-    KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
-    FillBatch fb(ctx);
-    KTRY(fb.add_raw(err, sizeof(u64), 0u));
-    KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
-    KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
-    KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
-    KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
-    for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
-    KTRY(fb.add(ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1), 0u));   // counts + cursors
-    KTRY(fb.run());
-    const i64 rl = rows_local(ctx);
-    hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
-                       gdev, G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
-                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
-    KLAUNCH();
-    // classes in group order (counting sort), then one pass over Mc; the
-    // pass also folds the column checks when the build deferred them
-    int32_t* kcnt = P_<int32_t>(ctx->kcnt);
-    const int32_t* nlive = P_<int32_t>(ctx->koff) + kslots;   // the scan total
-    if (key_lds) {
-      int32_t* hist = kcnt + 2 * ((i64)G + 1);
-      hipLaunchKernelGGL(k_key_hist, dim3((unsigned)knb), dim3(TPB), 0, ctx->stream, U,
-                         P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
-                         P_<int32_t>(ctx->gmax), G, P_<int32_t>(ctx->ckey), hist);
-      KLAUNCH();
-      ScanBatch sb(ctx);
-      KTRY(sb.add(hist, kslots, P_<int32_t>(ctx->koff)));
-      KTRY(sb.run());
-      hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)knb), dim3(TPB), 0, ctx->stream, U,
-                         P_<int32_t>(ctx->ckey), G, P_<int32_t>(ctx->koff),
-                         P_<int32_t>(ctx->corder));
-      KLAUNCH();
-    } else {
-      hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
-                         P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin),
-                         P_<int32_t>(ctx->gmax), G, P_<int32_t>(ctx->ckey), kcnt);
-      KLAUNCH();
-      ScanBatch sb(ctx);
-      KTRY(sb.add(kcnt, (i64)G + 1, P_<int32_t>(ctx->koff)));
-      KTRY(sb.run());
-      hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
-                         P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
-                         P_<int32_t>(ctx->corder));
-      KLAUNCH();
-    }
-    const bool cols = ctx->cols_deferred;
-    // the live class count is koff[G + 1]: size the grid by U (idle tails
-    // exit at once)
-    hipLaunchKernelGGL(k_mc_fold, dim3(nblk(UAW, 64), nblk(U, (TPB / 64) * FOLD_PER_WAVE)),
-                       dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), ldC, UAW, ctx->cc.U,
-                       P_<int32_t>(ctx->corder), nlive,
-                       P_<int32_t>(ctx->ckey), G, P_<u64>(ctx->R), P_<u64>(ctx->multi),
-                       cols ? P_<u64>(ctx->col_or_c) : nullptr,
-                       cols ? P_<u64>(ctx->col_nand_c) : nullptr);
-    KLAUNCH();
-    if (cols) {
-      ctx->cols_deferred = false;
-      if (!tail_in_verify) KTRY(do_rows(ctx));   // expand the column checks to pods
-    }
-    hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
-                       P_<u64>(ctx->R), ldC, UAW, P_<u64>(ctx->A1), P_<u64>(ctx->A2));
-    KLAUNCH();
-    ctx->cross_G = G;
-    if (tail_in_verify) return 0;
+    ScanBatch sb(ctx);
+    KTRY(cross_stage_a(ctx, cp, sb));
+    KTRY(sb.run());
+    KTRY(cross_stage_b(ctx, cp));
     hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
                        gdev, G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
-                       ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
+                       ctx->ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
                        P_<u64>(ctx->cross), err);
     KLAUNCH();
     return 0;
@@ -1422,7 +1459,9 @@ int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end) {
 namespace {
 // rows_now: launch the matrix write here; defer_cols: leave the column
 // checks to the crosscheck pass over Mc (kano_verify), finish_cols() after
-int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false) {
+using ExtraFills = std::function<int(FillBatch&)>;
+int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
+               const ExtraFills& extra = ExtraFills()) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
@@ -1443,7 +1482,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false) 
   KTRY(read_sizes(ctx));
   KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   ctx->cols_deferred = defer_cols;
-  KTRY(do_back(ctx, path));
+  KTRY(do_back(ctx, path, extra));
   if (!defer_cols) KTRY(do_rows(ctx));
   if (rows_now) KTRY(launch_rows(ctx));
   KCHK(hipEventRecord(ctx->ev[4], ctx->stream));
@@ -1663,26 +1702,32 @@ namespace {
 // policy_shadow up to its one sync: flags, per-class counts, per-pod offsets;
 // the caller gathers toff[nt] (list length) and poff[rl] (pairs) with its own
 // scalars
-int shadow_front(kano_ctx* ctx) {
-  const i64 U = ctx->rc.U, rl = rows_local(ctx), nf = ctx->nflags;
-  const i64 nt = (nf + SH_TILE - 1) / SH_TILE;
+struct ShadowPlan {
+  i64 U = 0, rl = 0, nf = 0, nt = 0;
+};
+
+int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
+  sp.U = ctx->rc.U;
+  sp.rl = rows_local(ctx);
+  sp.nf = ctx->nflags;
+  sp.nt = (sp.nf + SH_TILE - 1) / SH_TILE;
   KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
+  KTRY(dalloc(ctx, ctx->flags, sp.nf + 16));
+  KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, sp.U)));
+  KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (sp.U + 1)));
+  KTRY(dalloc(ctx, ctx->tp, sizeof(i64) * std::max<i64>(1, sp.rl)));
+  KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (sp.rl + 1)));
+  KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, sp.nt)));
+  KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
+  return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
+}
+
+// subset tests; the list-offset scans go to sb
+int shadow_stage_a(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
   KCHK(hipEventRecord(ctx->ev[5], ctx->stream));
-  KTRY(dalloc(ctx, ctx->flags, nf + 16));
-  KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (U + 1)));
-  KTRY(dalloc(ctx, ctx->tp, sizeof(i64) * std::max<i64>(1, rl)));
-  KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (rl + 1)));
-  KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, nt)));
-  KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (nt + 1)));
-  {
-    FillBatch fb(ctx);
-    KTRY(fb.add(ctx->T, sizeof(i64) * U, 0u));
-    KTRY(fb.run());
-  }
-  if (nt > 0) {
+  if (sp.nt > 0) {
     ShadowArgs a;
-    a.U = U;
+    a.U = sp.U;
     a.soffc = P_<i64>(ctx->soffc);
     a.slist = P_<int32_t>(ctx->slist);
     a.mcnt = P_<int32_t>(ctx->rc.mcnt);
@@ -1694,28 +1739,42 @@ int shadow_front(kano_ctx* ctx) {
     a.ldC = ctx->ldC;
     a.flags = P_<uint8_t>(ctx->flags);
     a.T = P_<i64>(ctx->T);
-    hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)nt), dim3(TPB), 0, ctx->stream, a, nf,
+    hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, ctx->stream, a, sp.nf,
                        P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
-  {
-    ScanBatch sb(ctx);
-    KTRY(sb.add(P_<i64>(ctx->tcnt), nt, P_<i64>(ctx->toff), SZ_NL));
-    KTRY(sb.add(P_<i64>(ctx->T), U, P_<i64>(ctx->loff)));
-    KTRY(sb.run());
-  }
-  if (rl > 0) {
-    hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
+  KTRY(sb.add(P_<i64>(ctx->tcnt), sp.nt, P_<i64>(ctx->toff), SZ_NL));
+  KTRY(sb.add(P_<i64>(ctx->T), sp.U, P_<i64>(ctx->loff)));
+  return 0;
+}
+
+// pairs per pod; the per-pod offset scan goes to sb
+int shadow_stage_b(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
+  if (sp.rl > 0) {
+    hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(sp.rl)), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
                        P_<i64>(ctx->tp));
     KLAUNCH();
   }
+  return sb.add(P_<i64>(ctx->tp), sp.rl, P_<i64>(ctx->poff), SZ_PAIRS);
+}
+
+// policy_shadow up to its one sync (the caller reads SZ_NL, SZ_PAIRS)
+int shadow_front(kano_ctx* ctx) {
+  ShadowPlan sp;
+  {
+    FillBatch fb(ctx);
+    KTRY(shadow_prepare(ctx, sp, fb));
+    KTRY(fb.run());
+  }
   {
     ScanBatch sb(ctx);
-    KTRY(sb.add(P_<i64>(ctx->tp), rl, P_<i64>(ctx->poff), SZ_PAIRS));
+    KTRY(shadow_stage_a(ctx, sp, sb));
     KTRY(sb.run());
   }
-  return 0;
+  ScanBatch sb(ctx);
+  KTRY(shadow_stage_b(ctx, sp, sb));
+  return sb.run();
 }
 
 int shadow_back(kano_ctx* ctx, i64 nl, i64 total) {
@@ -1860,17 +1919,36 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
-  KTRY(build_impl(ctx, path, false, gid != nullptr || ngroups == KANO_STORED_GROUPS));
-  const i64 n = ctx->n, W = ctx->W;
-  const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
   const bool want_cross = gid || stored;
-  const bool cross_on = want_cross && n > 0 && rows_local(ctx) > 0 && W > 0;
-  if (want_cross) KTRY(crosscheck_impl(ctx, gid, ngroups, true));
+  const bool want_shadow = shadow_count != nullptr;
+  // the crosscheck and policy_shadow buffers are filled in the build's last
+  // fill launch
+  CrossPlan cp;
+  ShadowPlan sp;
+  auto extra = [&](FillBatch& fb) -> int {
+    if (want_cross) KTRY(cross_prepare(ctx, gid, ngroups, cp, fb));
+    if (want_shadow) KTRY(shadow_prepare(ctx, sp, fb));
+    return 0;
+  };
+  KTRY(build_impl(ctx, path, false, want_cross, extra));
+  const i64 n = ctx->n, W = ctx->W;
+  const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
+  const bool cross_on = want_cross && cp.on;
+  // stage A of both checks, their scans in one launch, stage B
+  {
+    ScanBatch sb(ctx);
+    if (cross_on) KTRY(cross_stage_a(ctx, cp, sb));
+    if (want_shadow) KTRY(shadow_stage_a(ctx, sp, sb));
+    KTRY(sb.run());
+  }
+  if (cross_on) KTRY(cross_stage_b(ctx, cp));
   if (ctx->cols_deferred) {   // no crosscheck pass ran (empty shard / matrix)
     ctx->cols_deferred = false;
     KTRY(mc_cols(ctx));
   }
+  ScanBatch sb2(ctx);
+  if (want_shadow) KTRY(shadow_stage_b(ctx, sp, sb2));
   // the column tail in one pass (k_verify_cols), then the four result rows
   // as index lists: all_reachable, all_isolated, user_crosscheck,
   // system_isolation
@@ -1892,18 +1970,17 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
     fa.color = P_<u64>(ctx->color);
     fa.colnand = P_<u64>(ctx->colnand);
     fa.col_and = P_<u64>(ctx->col_and);
+    fa.ldC = ctx->ldC;
     if (cross_on) {
-      fa.gid = stored ? P_<int32_t>(ctx->gids) : P_<int32_t>(ctx->gid);
-      fa.G = ctx->cross_G;
+      fa.gid = cp.gdev;
+      fa.G = cp.G;
       fa.R = P_<u64>(ctx->R);
-      fa.ldC = ctx->ldC;
       fa.multi = P_<u64>(ctx->multi);
       fa.A1 = P_<u64>(ctx->A1);
       fa.A2 = P_<u64>(ctx->A2);
       fa.cross = P_<u64>(ctx->cross);
       fa.err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
     }
-    fa.ldC = ctx->ldC;
     if (sys_on) {
       fa.Mc = P_<u64>(ctx->Mc);
       fa.clr = P_<int32_t>(ctx->rc.cls);
@@ -1916,13 +1993,10 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   } else {
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
   }
-  {
-    ScanBatch sb(ctx);   // one job per row; row totals land in SZ_IDX0..3
-    for (int r = 0; r < 4; ++r)
-      KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
-                  SZ_IDX0 + r));
-    KTRY(sb.run());
-  }
+  for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
+    KTRY(sb2.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
+                 SZ_IDX0 + r));
+  KTRY(sb2.run());
   IdxRows ir{};
   ir.W = W;
   ir.n = n;
@@ -1939,8 +2013,6 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
                        P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
     KLAUNCH();
   }
-  // policy_shadow up to its size read
-  if (shadow_count) KTRY(shadow_front(ctx));
   KTRY(launch_rows(ctx));
   // one sync for the list sizes, policy_shadow's sizes and the group check
   i64 v[SZ_ERR - SZ_NL + 1];
@@ -1954,7 +2026,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   }
   if (!have_sys) counts[3] = -1;
   i64 total = 0;
-  if (shadow_count) {
+  if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
     KTRY(shadow_back(ctx, v[0], total));
     ctx->shadow_total = total;
@@ -1962,7 +2034,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   }
   if (nidx > 0)
     KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, ctx->stream));
-  if (shadow_count && shadow_pairs && total > 0 && total <= shadow_cap)
+  if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         ctx->stream));
   KTRY(join_rows(ctx));  // the matrix is part of the result
