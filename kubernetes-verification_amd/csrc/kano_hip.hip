@@ -104,6 +104,7 @@ struct kano_ctx {
   int pitch_mul = 1;
   int rows_alist = -1;       // k_rows build from allowed-pod lists: -1 auto, 0 no, 1 yes
   int rows_nt = 0;           // k_rows block size: 0 auto, 256 / 512 / 1024
+  int rows_probe = 0;        // experiments only (KANO_TUNE probe=1|2): results are wrong
   int pitch_pad = 0;         // extra words per M row (experiment)         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
@@ -870,6 +871,7 @@ int launch_rows(kano_ctx* ctx) {
   a.W = W;
   a.ch = ctx->ch;
   a.cww = cww;
+  a.probe = ctx->rows_probe;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
@@ -1197,6 +1199,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
         if (k == "alist") ctx->rows_alist = v < 0 ? -1 : (v ? 1 : 0);
         if (k == "nt" && (v == 0 || v == 256 || v == 512 || v == 1024)) ctx->rows_nt = v;
+        if (k == "probe" && v >= 0 && v <= 2) ctx->rows_probe = v;
         if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }

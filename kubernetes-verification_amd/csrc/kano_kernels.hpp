@@ -1040,6 +1040,7 @@ struct RowsArgs {
   i64 n, W;
   int ch;
   int cww;
+  int probe;             // experiments: 1 skip the row build, 2 skip the stores
   u64* color;
   u64* colnand;
 };
@@ -1061,7 +1062,10 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   const int32_t m1 = min(m_end, m0 + a.ch);
   const bool heavy = a.hflag && a.hflag[c];
 
-  if (heavy) {
+  if (a.probe == 1) {
+    for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
+    __syncthreads();
+  } else if (heavy) {
     const u64* src = a.M + (i64)(a.mem[m_begin] - a.r0) * ldw + base;
     for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
       *(u64x2*)&row[w] = *(const u64x2*)&src[w];
@@ -1103,12 +1107,13 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
     }
     __syncthreads();
   }
-  for (int32_t m = m0; m < m1; ++m) {
+  for (int32_t m = m0; m < m1 && a.probe != 2; ++m) {
     if (heavy && m == m_begin) continue;
     u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
     for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
       *(u64x2*)&dst[w] = *(const u64x2*)&row[w];   // (nt stores measured slower)
   }
+  if (a.probe == 2 && threadIdx.x == 0 && row[0] == 0x5eed5eed5eed5eedull) a.M[0] = 1;
   if (chunk == 0 && a.color) {
     for (int w = threadIdx.x; w < nw; w += NT) {
       const i64 gw = base + w;
