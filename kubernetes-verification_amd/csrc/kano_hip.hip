@@ -104,7 +104,8 @@ struct kano_ctx {
   int pitch_mul = 1;
   int rows_alist = -1;       // k_rows build from allowed-pod lists: -1 auto, 0 no, 1 yes
   int rows_nt = 0;           // k_rows block size: 0 auto, 256 / 512 / 1024
-  int rows_probe = 0;        // experiments only (KANO_TUNE probe=1|2): results are wrong
+  int rows_probe = 0;
+  int m_over = 1;            // experiment: over-allocate M by this factor        // experiments only (KANO_TUNE probe=1|2): results are wrong
   int pitch_pad = 0;         // extra words per M row (experiment)         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
@@ -1200,6 +1201,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "alist") ctx->rows_alist = v < 0 ? -1 : (v ? 1 : 0);
         if (k == "nt" && (v == 0 || v == 256 || v == 512 || v == 1024)) ctx->rows_nt = v;
         if (k == "probe" && v >= 0 && v <= 2) ctx->rows_probe = v;
+        if (k == "mover" && v >= 1 && v <= 64) ctx->m_over = v;
         if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
       }
@@ -1477,7 +1479,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->cols_valid = false;
   ctx->shadow_total = -1;
   const i64 rl = rows_local(ctx);
-  KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM)));
+  KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KCHK(hipEventRecord(ctx->ev[0], ctx->stream));
