@@ -15,8 +15,10 @@ One step = one pass of the hot path over the synthetic cluster, inputs
 with every result on the host as index arrays.  value = n^2 / step time
 (pod-pairs/s); the n x n matrix is built once per step over
 all ranks.  For N > 1 the rows are partitioned across ranks (one process per
-GPU); the column checks combine per-rank byte flags with one RCCL MAX
-all-reduce (RCCL has no bitwise reduction); strong scaling (fixed cluster).
+GPU, kano_verify_shard); the column checks combine the ranks' [OR | cross |
+NAND] bit words (3 * W u64 each) gathered by one RCCL all-gather over xGMI and
+OR-ed on the device (kano_verify_combine; RCCL has no bitwise reduction);
+strong scaling (fixed cluster).
 
 Rank 0 prints ONE JSON line.  roofline: the dominant kernel is k_rows (the
 matrix write), algorithmic bytes = 8 * rows * W (the bit matrix it writes),
@@ -67,21 +69,23 @@ def parse():
 class Step:
     """The hot path on this rank's row shard."""
 
-    def __init__(self, eng, gid, n, rank, world, r0, r1, shadow, dist=None, torch=None):
+    def __init__(self, eng, gid, n, rank, world, r0, r1, shadow, dist=None, torch=None,
+                 stream=None):
         self.eng, self.gid, self.n = eng, gid, n
         self.rank, self.world, self.r0, self.r1 = rank, world, r0, r1
         self.shadow = shadow
-        self.dist, self.torch = dist, torch
+        self.dist, self.torch, self.stream = dist, torch, stream
         self.W = (n + 63) >> 6
         if world > 1:
-            self.flags = torch.zeros(3 * n, dtype=torch.uint8, device="cuda")
+            # [OR | cross | NAND] words of this rank's rows, and all ranks'
+            self.words = torch.zeros(3 * self.W, dtype=torch.int64, device="cuda")
+            self.gathered = torch.zeros(world * 3 * self.W, dtype=torch.int64, device="cuda")
         from kano._engine import PinnedBuffer
         self.pin = None
         self.pin_idx = None
         # the tenant groups are resident input, uploaded once like the label
         # tables (user_hashmap, algorithm.py:20-24)
-        if world == 1:
-            eng.set_groups(gid)
+        eng.set_groups(gid)
         self.pin_pairs = 0
         self.PinnedBuffer = PinnedBuffer
         self.results = {}
@@ -89,55 +93,40 @@ class Step:
 
     def __call__(self):
         eng, n = self.eng, self.n
-        from kano._bits import words_to_bool
         res = {}
+        pairs = None
+        if self.shadow:
+            if self.pin is None:
+                self.pin_pairs = 1 << 20
+                self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+            pairs = self.pin.view(np.int32, 2 * self.pin_pairs)
+        if self.pin_idx is None:
+            self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
+        idx = self.pin_idx.view(np.int32, 4 * max(n, 1))
         if self.world == 1:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
-            pairs = None
-            if self.shadow:
-                if self.pin is None:
-                    self.pin_pairs = 1 << 20
-                    self.pin = self.PinnedBuffer(self.pin_pairs * 8)
-                pairs = self.pin.view(np.int32, 2 * self.pin_pairs)
-            if self.pin_idx is None:
-                self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
-            r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs,
-                           idx=self.pin_idx.view(np.int32, 4 * max(n, 1)))
-            for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
-                res[k] = r[k]
-            if self.shadow:
-                cnt = r["shadow_count"]
-                res["policy_shadow"] = r["pairs"]
-                res["policy_shadow_count"] = cnt
-                if cnt > self.pin_pairs:          # grow for the next step
-                    self.pin.close()
-                    self.pin_pairs = 2 * cnt
-                    self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+            r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=idx)
         else:
-            eng.build()
-            f = self.flags
-            eng.col_flags_dev(f.data_ptr())
-            eng.crosscheck_dev(self.gid, f.data_ptr())
-            self.torch.cuda.synchronize()
-            self.dist.all_reduce(f, op=self.dist.ReduceOp.MAX)
-            h = f.cpu().numpy()
-            res["all_isolated"] = np.flatnonzero(h[:n] == 0)
-            res["user_crosscheck"] = np.flatnonzero(h[n:2 * n])
-            res["all_reachable"] = np.flatnonzero(h[2 * n:] == 0)
-            if self.r0 <= 0 < self.r1:
-                res["system_isolation"] = np.flatnonzero(~words_to_bool(eng.rows(0, 1)[0], n))
-            if self.shadow:
-                cnt = eng.shadow_count()
-                if self.pin is None or cnt > self.pin_pairs:
-                    if self.pin is not None:
-                        self.pin.close()
-                    self.pin_pairs = max(cnt, 1) * 2
-                    self.pin = self.PinnedBuffer(self.pin_pairs * 8)
-                out = self.pin.view(np.int32, 2 * cnt).reshape(cnt, 2)
-                eng.shadow_fetch(cnt, out)
-                res["policy_shadow"] = out
-                res["policy_shadow_count"] = cnt
+            # this rank's rows and checks up to its column words, one RCCL
+            # all-gather of 3*W words per rank over xGMI (on the engine's
+            # stream), then the OR-combine and the lists on the device
+            with self.torch.cuda.stream(self.stream):
+                eng.verify_shard(self.words.data_ptr(), gid="stored", sys_row=0,
+                                 shadow=self.shadow)
+                self.dist.all_gather_into_tensor(self.gathered, self.words)
+                r = eng.verify_combine(self.gathered.data_ptr(), self.world, pairs=pairs, idx=idx)
+        for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
+            if r[k] is not None:
+                res[k] = r[k]
+        if self.shadow:
+            cnt = r["shadow_count"]
+            res["policy_shadow"] = r["pairs"]
+            res["policy_shadow_count"] = cnt
+            if cnt > self.pin_pairs:          # grow for the next step
+                self.pin.close()
+                self.pin_pairs = 2 * cnt
+                self.pin = self.PinnedBuffer(self.pin_pairs * 8)
         st = eng.stage_times()
         self.k_rows_ms.append(st["k_rows"])
         self.stages = st
@@ -231,8 +220,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one GPU per rank; KANO_DIST_BACKEND=gloo with fewer GPUs than ranks
+        # rehearses the N > 1 code path on one device (timings meaningless)
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dist.init_process_group(os.environ.get("KANO_DIST_BACKEND", "nccl"))
     from kano import _native
     from kano._engine import DeviceBuild
     from kano._intern import tables_from_cluster
@@ -243,9 +234,12 @@ def main():
     n = cl.n
     gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
     r0, r1 = rank * n // world, (rank + 1) * n // world
-    eng = DeviceBuild(tables, device=local, rows=(r0, r1), path=args.path, build=False)
+    stream = torch.cuda.Stream() if world > 1 else None
+    eng = DeviceBuild(tables, device=torch.cuda.current_device(), rows=(r0, r1), path=args.path,
+                      build=False,
+                      stream=stream.cuda_stream if stream is not None else None)
     step = Step(eng, gid, n, rank, world, r0, r1, shadow=not args.no_shadow, dist=dist,
-                torch=torch)
+                torch=torch, stream=stream)
 
     def barrier():
         torch.cuda.synchronize()
@@ -305,7 +299,10 @@ def main():
             "stages_ms_last_step": {k: round(v, 4) for k, v in step.stages.items()},
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),
-                        "max": round(float(step_ms.max()), 4)},
+                        "p90": round(float(np.percentile(step_ms, 90)), 4),
+                        "max": round(float(step_ms.max()), 4),
+                        "worst5": [round(float(v), 3) for v in np.sort(step_ms)[-5:]],
+                        "worst5_at": [int(i) for i in np.argsort(step_ms)[-5:]]},
             "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},

@@ -165,6 +165,26 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
                 int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count);
 
+/* kano_verify for one row shard of a multi-GPU build, in two
+ * halves around the ranks' exchange step.
+ *   kano_verify_shard: the build of this shard's rows and every check up to
+ *     the column words, written to words_dev (DEVICE memory, 3*W uint64:
+ *     [column OR | cross | column NAND] over this shard's rows; cross is 0
+ *     without groups).  Asynchronous on the context stream.
+ *   (the caller gathers the nranks word sets rank-major into one device
+ *     buffer on the same stream, e.g. an RCCL all-gather over xGMI)
+ *   kano_verify_combine: OR of the gathered sets -- all_isolated[j] = no
+ *     shard reaches j (algorithm.py:12-17), all_reachable[j] = no shard
+ *     misses j (:4-9), user_crosscheck[j] = some shard crosses (:27-42) --
+ *     then the same outputs as kano_verify: the three global lists, this
+ *     shard's system_isolation row (-1 when sys_row is elsewhere), and this
+ *     shard's policy_shadow pairs (rank order = the reference's order). */
+int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
+                      int64_t sys_row, int with_shadow, uint64_t* words_dev);
+int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nranks,
+                        int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                        int64_t* shadow_count);
+
 /* user_hashmap (algorithm.py:20-24) as resident input: the group id of
  * every pod uploaded once (like the label tables), for kano_verify with
  * gid = NULL, ngroups = KANO_STORED_GROUPS.  ngroups <= 0: max(gid) + 1. */

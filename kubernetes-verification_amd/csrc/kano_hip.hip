@@ -97,16 +97,18 @@ struct kano_ctx {
   bool cols_deferred = false;
   int32_t cross_G = 0;         // group count of the last class-level crosscheck
   i64 groups_n = -1;           // kano_set_groups: pods covered (-1: none stored)
-  int32_t groups_G = 0;  // column checks folded into the crosscheck pass (kano_verify)  // allowed-pod lists materialised (kano_get_allow_csr)
+  int32_t groups_G = 0;      // group count of the stored groups
   int ch = 16;               // member rows per k_rows work item
   int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
-  int ld_align = 16;
-  int pitch_mul = 1;
+  int ld_align = 16;         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
+  int pitch_mul = 1;         // experiment: spread rows over pitch_mul x the memory
   int rows_alist = -1;       // k_rows build from allowed-pod lists: -1 auto, 0 no, 1 yes
   int rows_nt = 0;           // k_rows block size: 0 auto, 256 / 512 / 1024
-  int rows_probe = 0;
-  int m_over = 1;            // experiment: over-allocate M by this factor        // experiments only (KANO_TUNE probe=1|2): results are wrong
-  int pitch_pad = 0;         // extra words per M row (experiment)         // experiment: spread rows over pitch_mul x the memory         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
+  int rows_probe = 0;        // experiments only (KANO_TUNE probe=1|2): results are wrong
+  int m_over = 1;            // experiment: over-allocate M by this factor
+  int pitch_pad = 0;         // experiment: extra words per M row
+  int rows_early = 0;        // kano_verify: launch k_rows right after the lists (on stream2)
+  int prio = 0;              // checks stream high priority, matrix-write stream low
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -139,6 +141,11 @@ struct kano_ctx {
   hipEvent_t ev_fork = nullptr, ev_rows = nullptr;
   bool rows_pending = false;
   bool rows_overlap = false;
+  hipEvent_t ev_sizes = nullptr;   // kano_verify: the size slots reached the host buffer
+  // kano_verify halves (kano_verify_shard -> kano_verify_combine)
+  bool vs_open = false, vs_shadow = false, vs_cross_want = false, vs_cross_on = false;
+  bool vs_have_sys = false, vs_sys_on = false, vs_early = false;
+  i64 vs_nb = 0, vs_rl = 0;
 };
 
 namespace {
@@ -1204,13 +1211,31 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "mover" && v >= 1 && v <= 64) ctx->m_over = v;
         if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
+        if (k == "overlap") ctx->rows_overlap = v != 0;
+        if (k == "early") ctx->rows_early = v;
+        if (k == "prio") ctx->prio = v;
       }
       pos = end + 1;
     }
   }
-  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+  // priorities: the checks' stream high, the matrix write's low, so that the
+  // short check kernels get CUs while k_rows streams
+  int prio_lo = 0, prio_hi = 0;
+  const bool use_prio = ctx->prio && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) ==
+                                         hipSuccess && prio_lo != prio_hi;
+  if (use_prio) {
+    (void)hipStreamDestroy(ctx->stream);
+    if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      ctx->stream = nullptr;
+      kano_destroy(ctx);
+      return -EIO;
+    }
+  }
+  if ((use_prio ? hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_lo)
+                : hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking)) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess) {
     kano_destroy(ctx);
     return -EIO;
   }
@@ -1261,6 +1286,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
+  if (ctx->ev_sizes) (void)hipEventDestroy(ctx->ev_sizes);
   delete ctx;
 }
 
@@ -1918,15 +1944,18 @@ int kano_conflict(kano_ctx* ctx, int* raises) {
   return 0;
 }
 
-int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
-                int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
-                int64_t* shadow_count) {
-  if (!ctx) return -EINVAL;
-  if (!counts || (!idx && ctx->n > 0))
-    return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
+}  // extern "C"
+
+namespace {
+// kano_verify in two halves.  verify_front: the build and every check up to
+// the column words (k_verify_cols; with words_dev also this shard's
+// [OR | cross | NAND] words for the ranks' gather).  verify_back: (combine
+// the gathered words of all shards,) list the results, the matrix write,
+// policy_shadow's pairs, the copies to the host.
+int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                 bool want_shadow, u64* words_dev) {
   const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
   const bool want_cross = gid || stored;
-  const bool want_shadow = shadow_count != nullptr;
   // the crosscheck and policy_shadow buffers are filled in the build's last
   // fill launch
   CrossPlan cp;
@@ -1936,7 +1965,12 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
     if (want_shadow) KTRY(shadow_prepare(ctx, sp, fb));
     return 0;
   };
+  ctx->vs_open = false;
   KTRY(build_impl(ctx, path, false, want_cross, extra));
+  // the matrix write needs only the lists: with rows_early it starts here on
+  // stream2, beside the class-level checks
+  const bool early = ctx->rows_early && ctx->rows_overlap;
+  if (early) KTRY(launch_rows(ctx));
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   const bool cross_on = want_cross && cp.on;
@@ -1952,11 +1986,14 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
     ctx->cols_deferred = false;
     KTRY(mc_cols(ctx));
   }
-  ScanBatch sb2(ctx);
-  if (want_shadow) KTRY(shadow_stage_b(ctx, sp, sb2));
-  // the column tail in one pass (k_verify_cols), then the four result rows
-  // as index lists: all_reachable, all_isolated, user_crosscheck,
-  // system_isolation
+  // per-pod pair counts; their scan joins verify_back's batch
+  if (want_shadow && sp.rl > 0) {
+    hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(sp.rl)), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
+                       P_<i64>(ctx->tp));
+    KLAUNCH();
+  }
+  // the column tail in one pass (k_verify_cols)
   const i64 nb = std::max<i64>(1, nblk(W * 64));
   KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
   KTRY(dalloc(ctx, ctx->sysrow, sizeof(u64) * std::max<i64>(1, W)));
@@ -1993,15 +2030,49 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
       fa.sysrow = P_<u64>(ctx->sysrow);
     }
     fa.icnt = P_<i64>(ctx->icnt);
+    fa.words = words_dev;
     hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
     KLAUNCH();
   } else {
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
   }
+  ctx->vs_open = true;
+  ctx->vs_shadow = want_shadow;
+  ctx->vs_cross_want = want_cross;
+  ctx->vs_cross_on = cross_on;
+  ctx->vs_have_sys = have_sys;
+  ctx->vs_sys_on = sys_on;
+  ctx->vs_early = early;
+  ctx->vs_nb = nb;
+  ctx->vs_rl = sp.rl;
+  return 0;
+}
+
+int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx, int64_t* counts,
+                int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count) {
+  if (!ctx->vs_open) return fail(ctx, -EINVAL, "kano_verify_combine without kano_verify_shard");
+  ctx->vs_open = false;
+  const i64 n = ctx->n, W = ctx->W, nb = ctx->vs_nb;
+  const bool want_shadow = ctx->vs_shadow;
+  // a gathered combine lists the crosscheck whenever it was asked for (other
+  // shards may hold its rows)
+  const bool cross_row = gathered ? ctx->vs_cross_want : ctx->vs_cross_on;
+  ScanBatch sb(ctx);
+  if (want_shadow) KTRY(sb.add(P_<i64>(ctx->tp), ctx->vs_rl, P_<i64>(ctx->poff), SZ_PAIRS));
+  if (gathered && n > 0 && W > 0) {
+    if (cross_row) KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ctx->ldM));
+    hipLaunchKernelGGL(k_combine_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, gathered,
+                       nranks, n, W, nb, P_<u64>(ctx->color), P_<u64>(ctx->colnand),
+                       P_<u64>(ctx->col_and), cross_row ? P_<u64>(ctx->cross) : nullptr,
+                       P_<i64>(ctx->icnt));
+    KLAUNCH();
+  }
+  // the four result rows as index lists: all_reachable, all_isolated,
+  // user_crosscheck, system_isolation
   for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
-    KTRY(sb2.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
-                 SZ_IDX0 + r));
-  KTRY(sb2.run());
+    KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
+                SZ_IDX0 + r));
+  KTRY(sb.run());
   IdxRows ir{};
   ir.W = W;
   ir.n = n;
@@ -2009,8 +2080,8 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   ir.row[0] = P_<u64>(ctx->col_and);
   ir.row[1] = P_<u64>(ctx->color);
   ir.inv[1] = 1;
-  ir.row[2] = cross_on ? P_<u64>(ctx->cross) : nullptr;
-  ir.row[3] = sys_on ? P_<u64>(ctx->sysrow) : nullptr;
+  ir.row[2] = cross_row ? P_<u64>(ctx->cross) : nullptr;
+  ir.row[3] = ctx->vs_sys_on ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
   if (n > 0 && W > 0) {
@@ -2018,18 +2089,34 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
                        P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
     KLAUNCH();
   }
-  KTRY(launch_rows(ctx));
-  // one sync for the list sizes, policy_shadow's sizes and the group check
-  i64 v[SZ_ERR - SZ_NL + 1];
-  KTRY(read_slots(ctx, SZ_NL, SZ_ERR - SZ_NL + 1, v));
-  if (cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff))
+  // the list sizes, policy_shadow's sizes and the group check travel to the
+  // host while the matrix write runs: the host waits on the copy's event
+  // only, then queues policy_shadow's emission and the copies behind k_rows
+  constexpr int NS = SZ_ERR - SZ_NL + 1;
+  KCHK(hipMemcpyAsync(ctx->ghost, P_<u64>(ctx->sizes) + SZ_NL, sizeof(u64) * NS,
+                      hipMemcpyDeviceToHost, ctx->stream));
+  KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
+  if (!ctx->vs_early) KTRY(launch_rows(ctx));
+  KCHK(hipEventSynchronize(ctx->ev_sizes));
+  i64 v[NS];
+  for (int k = 0; k < NS; ++k) v[k] = (i64)ctx->ghost[k];
+  if (ctx->vs_cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff)) {
+    (void)sync(ctx);
     return fail(ctx, -EINVAL, "kano_verify: a group id lies outside [0, ngroups)");
+  }
   i64 nidx = 0;
   for (int r = 0; r < 4; ++r) {
     counts[r] = v[SZ_IDX0 - SZ_NL + r];
     nidx += counts[r];
   }
-  if (!have_sys) counts[3] = -1;
+  if (!ctx->vs_have_sys) counts[3] = -1;
+  // the lists were written before the matrix write: copy them beside it
+  // (stream2 is free unless the matrix write runs there)
+  hipStream_t cs = ctx->rows_overlap ? ctx->stream : ctx->stream2;
+  if (nidx > 0) {
+    if (cs != ctx->stream) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+    KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, cs));
+  }
   i64 total = 0;
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
@@ -2037,13 +2124,45 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
     ctx->shadow_total = total;
     *shadow_count = total;
   }
-  if (nidx > 0)
-    KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, ctx->stream));
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         ctx->stream));
   KTRY(join_rows(ctx));  // the matrix is part of the result
+  if (nidx > 0 && cs != ctx->stream) KCHK(hipStreamSynchronize(cs));
   return sync(ctx);
+}
+}  // namespace
+
+extern "C" {
+
+int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                int64_t* shadow_count) {
+  if (!ctx) return -EINVAL;
+  if (!counts || (!idx && ctx->n > 0))
+    return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
+  KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr));
+  return verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count);
+}
+
+int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
+                      int64_t sys_row, int with_shadow, uint64_t* words_dev) {
+  if (!ctx) return -EINVAL;
+  if (!words_dev) return fail(ctx, -EINVAL, "kano_verify_shard: words_dev is NULL");
+  return verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0,
+                      reinterpret_cast<u64*>(words_dev));
+}
+
+int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nranks,
+                        int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                        int64_t* shadow_count) {
+  if (!ctx) return -EINVAL;
+  if (!counts || (!idx && ctx->n > 0) || !gathered_dev || nranks < 1)
+    return fail(ctx, -EINVAL, "kano_verify_combine: bad arguments");
+  if (ctx->vs_open && ctx->vs_shadow && !shadow_count)
+    return fail(ctx, -EINVAL, "kano_verify_combine: shadow_count is NULL but the shard ran policy_shadow");
+  return verify_back(ctx, reinterpret_cast<const u64*>(gathered_dev), nranks, idx, counts,
+                     shadow_pairs, shadow_cap, shadow_count);
 }
 
 int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups) {

@@ -1486,6 +1486,7 @@ struct FinishArgs {
   i64 sys_row;
   u64* sysrow;
   i64* icnt;             // [r * nb + b], r: reachable, isolated, cross, sys-isolated
+  u64* words;            // nullable: this shard's [OR | cross | NAND] words (3 W) for the gather
 };
 
 __device__ __forceinline__ bool mc_bit(const u64* row, int32_t ca) {
@@ -1510,12 +1511,17 @@ __global__ __launch_bounds__(TPB) void k_verify_cols(FinishArgs a) {
   const bool syb = a.Mc && live && mc_bit(a.Mc + (i64)a.clr[a.sys_row] * a.ldC, ca);
   const u64 wo = __ballot(orb), wn = __ballot(nab), wc = __ballot(crb), ws = __ballot(syb);
   const i64 w = j >> 6;
-  if ((threadIdx.x & 63) == 0) {
+  if ((threadIdx.x & 63) == 0 && w < a.W) {   // the grid's tail waves hold no word
     a.color[w] = wo;
     a.colnand[w] = wn;
     a.col_and[w] = ~wn & valid_mask(w, a.n);
     if (a.gid) a.cross[w] = wc;
     if (a.Mc) a.sysrow[w] = ws;
+    if (a.words) {
+      a.words[w] = wo;
+      a.words[a.W + w] = wc;
+      a.words[2 * a.W + w] = wn;
+    }
   }
   const i64 c0 = block_sum((i64)(live && !nab), sm);
   const i64 c1 = block_sum((i64)(live && !orb), sm);
@@ -1526,6 +1532,53 @@ __global__ __launch_bounds__(TPB) void k_verify_cols(FinishArgs a) {
     a.icnt[a.nb + blockIdx.x] = c1;
     a.icnt[2 * a.nb + blockIdx.x] = c2;
     a.icnt[3 * a.nb + blockIdx.x] = c3;
+  }
+}
+
+// Row shards combined (kano_verify_combine): thread per pod j, the gathered
+// [OR | cross | NAND] words of nr shards (rank-major, 3 W words each) OR-ed
+// (all_isolated = no shard has a row reaching j, all_reachable = no shard
+// has a row missing j, user_crosscheck = some shard has a cross row), and the
+// per-block counts of result rows 0..2 (row 3, the system row, stays local).
+__global__ __launch_bounds__(TPB) void k_combine_cols(const u64* __restrict__ g, int32_t nr, i64 n,
+                                                      i64 W, i64 nb, u64* __restrict__ color,
+                                                      u64* __restrict__ colnand,
+                                                      u64* __restrict__ col_and,
+                                                      u64* __restrict__ cross,
+                                                      i64* __restrict__ icnt) {
+  __shared__ i64 sm[4];
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;   // grid covers W * 64
+  const i64 w = j >> 6;
+  u64 o = 0, c = 0, na = 0;
+  if (w < W) {
+    for (int32_t r = 0; r < nr; ++r) {
+      const u64* s = g + (i64)r * 3 * W;
+      o |= s[w];
+      c |= s[W + w];
+      na |= s[2 * W + w];
+    }
+    const u64 vm = valid_mask(w, n);
+    o &= vm;
+    c &= vm;
+    na &= vm;
+    if ((threadIdx.x & 63) == 0) {
+      color[w] = o;
+      colnand[w] = na;
+      col_and[w] = ~na & vm;
+      if (cross) cross[w] = c;
+    }
+  }
+  const bool live = j < n;
+  const int bit = (int)(j & 63);
+  const bool orb = (o >> bit) & 1ull, nab = (na >> bit) & 1ull;
+  const bool crb = cross && ((c >> bit) & 1ull);
+  const i64 c0 = block_sum((i64)(live && !nab), sm);
+  const i64 c1 = block_sum((i64)(live && !orb), sm);
+  const i64 c2 = block_sum((i64)(live && crb), sm);
+  if (threadIdx.x == 0) {
+    icnt[blockIdx.x] = c0;
+    icnt[nb + blockIdx.x] = c1;
+    icnt[2 * nb + blockIdx.x] = c2;
   }
 }
 

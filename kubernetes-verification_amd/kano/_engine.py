@@ -278,6 +278,62 @@ class DeviceBuild:
                 out["pairs"] = self.shadow_fetch(k)
         return out
 
+    def verify_shard(self, words_dev_ptr: int, gid=None, sys_row: int = 0, shadow: bool = True,
+                     ngroups: int = 0, path: Optional[str] = None) -> None:
+        """kano_verify_shard: build this row shard and run its checks up to the
+        column words, written (3*W u64, [OR | cross | NAND]) to the device
+        buffer at ``words_dev_ptr``.  Asynchronous on the engine's stream;
+        gather the ranks' words on that stream, then ``verify_combine``."""
+        self._gid_keep = None
+        if isinstance(gid, str) and gid == "stored":
+            gid, ngroups = None, nat.STORED_GROUPS
+        elif gid is not None:
+            gid = np.ascontiguousarray(gid, dtype=np.int32)
+            if gid.shape[0] != self.n:
+                raise ValueError("gid must have one entry per pod")
+            self._gid_keep = gid
+        self._shard_shadow = bool(shadow)
+        pth = nat.PATHS[path or self.path]
+        self._chk(self.lib.kano_verify_shard(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row),
+                                             1 if shadow else 0, c_void_p(words_dev_ptr)),
+                  "kano_verify_shard")
+
+    def verify_combine(self, gathered_dev_ptr: int, nranks: int, cross: bool = True,
+                       pairs: Optional[np.ndarray] = None,
+                       idx: Optional[np.ndarray] = None) -> dict:
+        """kano_verify_combine: OR the gathered word sets of ``nranks`` shards
+        and return the results like ``verify`` (column lists global, the
+        system row and the shadow pairs of this shard)."""
+        n = self.n
+        if idx is None:
+            idx = np.empty(max(4 * n, 1), dtype=np.int32)
+        elif idx.size < 4 * n:
+            raise ValueError("idx buffer needs 4*n entries")
+        counts = np.zeros(4, dtype=np.int64)
+        cnt = c_int64(0)
+        shadow = self._shard_shadow
+        cap = 0 if pairs is None else pairs.size // 2
+        self._chk(self.lib.kano_verify_combine(self.ctx, c_void_p(gathered_dev_ptr), int(nranks),
+                                               _ptr(idx), _ptr(counts), _ptr(pairs), int(cap),
+                                               byref(cnt) if shadow else None),
+                  "kano_verify_combine")
+        out, o = {}, 0
+        for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
+                                  "system_isolation")):
+            k = int(counts[r])
+            out[name] = idx[o:o + k] if k >= 0 else None
+            o += max(k, 0)
+        if not cross:
+            out["user_crosscheck"] = None
+        if shadow:
+            k = int(cnt.value)
+            out["shadow_count"] = k
+            if pairs is not None and k <= cap:
+                out["pairs"] = pairs.reshape(-1)[:2 * k].reshape(k, 2)
+            else:
+                out["pairs"] = self.shadow_fetch(k)
+        return out
+
     def conflict_raises(self) -> bool:
         v = c_int()
         self._chk(self.lib.kano_conflict(self.ctx, byref(v)), "kano_conflict")

@@ -48,6 +48,9 @@ SIGNATURES = {
     "kano_conflict": (c_int, [c_void_p, POINTER(c_int)]),
     "kano_verify": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_void_p, c_void_p,
                             c_void_p, c_int64, POINTER(c_int64)]),
+    "kano_verify_shard": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_int, c_void_p]),
+    "kano_verify_combine": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                    c_int64, POINTER(c_int64)]),
     "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),

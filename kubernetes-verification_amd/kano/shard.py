@@ -10,12 +10,15 @@ rows, so they combine over shards:
   all_reachable[j]   = NOT OR_r colNAND_r[j]        (algorithm.py:4-9)
   user_crosscheck[j] = OR_r cross_r[j]              (algorithm.py:27-42)
 
-RCCL has no bitwise reduction, so each rank unpacks its three bit vectors to
-one byte per column, [or | cross | nand] (3n bytes), and one MAX all-reduce
-over xGMI combines them (MAX of 0/1 bytes = OR).  system_isolation reads one
-row from the rank that owns it; policy_shadow's output is ordered by
-container, so each rank emits its own rows' pairs and rank order is the
-global order.
+RCCL has no bitwise reduction.  The bench's step (kano_verify_shard /
+kano_verify_combine) gathers every rank's three bit vectors as words,
+[or | cross | nand] (3 W u64 = n*3/8 bytes per rank), with one all-gather over
+xGMI and ORs them on the device; ``combine_words`` is the host statement of
+that combine.  The older byte form (``pack_flags``: one byte per column, one
+MAX all-reduce, MAX of 0/1 bytes = OR) stays for kano_col_flags_dev.
+system_isolation reads one row from the rank that owns it; policy_shadow's
+output is ordered by container, so each rank emits its own rows' pairs and
+rank order is the global order.
 """
 from __future__ import annotations
 
@@ -54,4 +57,21 @@ def decode_flags(flags: np.ndarray, n: int) -> Dict[str, np.ndarray]:
         "all_isolated": np.flatnonzero(f[:n] == 0),
         "user_crosscheck": np.flatnonzero(f[n:2 * n]),
         "all_reachable": np.flatnonzero(f[2 * n:3 * n] == 0),
+    }
+
+
+def combine_words(gathered: np.ndarray, n: int) -> Dict[str, np.ndarray]:
+    """Gathered [rank][or | cross | nand][W] u64 words -> the three check
+    results (host statement of k_combine_cols)."""
+    W = (n + 63) // 64
+    g = np.asarray(gathered, dtype=np.uint64).reshape(-1, 3, W)
+    o, c, na = (np.bitwise_or.reduce(g[:, k, :], axis=0) for k in range(3))
+
+    def bits(w):
+        return np.unpackbits(np.ascontiguousarray(w, dtype="<u8").view(np.uint8),
+                             bitorder="little")[:n].astype(bool)
+    return {
+        "all_isolated": np.flatnonzero(~bits(o)),
+        "user_crosscheck": np.flatnonzero(bits(c)),
+        "all_reachable": np.flatnonzero(~bits(na)),
     }

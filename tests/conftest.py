@@ -3,7 +3,16 @@ import sys
 
 import pytest
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# torch first: it bundles its own HIP runtime with the same soname as
+# /opt/rocm's (libamdhip64.so.7), and whichever loads first serves the whole
+# process.  The bench imports torch before libkano_hip.so; so do the tests
+# (the shard tests use torch for device buffers, as the bench does for RCCL).
+try:
+    import torch  # noqa: F401
+except ImportError:   # pragma: no cover
+    torch = None
+
+ROOT =os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "kubernetes-verification_amd")
 for p in (ROOT, PKG):
     if p not in sys.path:

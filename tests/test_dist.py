@@ -1,5 +1,6 @@
-"""World-size-2 test of the row partition and its one exchange step (a MAX
-all-reduce of byte flags, kano/shard.py) on CPU with the gloo backend.  The
+"""World-size-2/3 tests of the row partition and its one exchange step
+(kano/shard.py) on CPU with the gloo backend: the bench's all-gather of
+[or | cross | nand] words combined by OR, and the byte-flag MAX all-reduce.  The
 per-shard partials come from the oracle's matrix, so this checks that the
 decomposition itself reproduces kano_py's column checks exactly."""
 import os
@@ -33,7 +34,7 @@ def _partials(M, gid, r0, r1, n):
     return bool_to_words(col_or), bool_to_words(cross), bool_to_words(col_nand)
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, q, mode="bytes"):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-verification_amd"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -47,9 +48,18 @@ def _worker(rank, world, port, name, q):
     n = ref["n"]
     gid = orc.group_ids_json(obj, obj["label"])
     r0, r1 = shard.row_range(n, world, rank)
-    flags = torch.from_numpy(shard.pack_flags(*_partials(ref["M"], gid, r0, r1, n), n))
-    dist.all_reduce(flags, op=dist.ReduceOp.MAX)
-    got = shard.decode_flags(flags.numpy(), n)
+    parts = _partials(ref["M"], gid, r0, r1, n)
+    if mode == "bytes":
+        flags = torch.from_numpy(shard.pack_flags(*parts, n))
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX)
+        got = shard.decode_flags(flags.numpy(), n)
+    else:   # the bench's exchange: all-gather of the words, OR on the receiver
+        W = (n + 63) // 64
+        words = torch.from_numpy(np.concatenate(parts).astype(np.uint64).view(np.int64))
+        assert words.numel() == 3 * W
+        gathered = torch.zeros(world * 3 * W, dtype=torch.int64)
+        dist.all_gather_into_tensor(gathered, words)
+        got = shard.combine_words(gathered.numpy().view(np.uint64), n)
     ok = (got["all_isolated"].tolist() == ref["all_isolated"] and
           got["all_reachable"].tolist() == ref["all_reachable"] and
           got["user_crosscheck"].tolist() == ref["user_crosscheck"])
@@ -57,14 +67,15 @@ def _worker(rank, world, port, name, q):
     q.put((rank, ok))
 
 
+@pytest.mark.parametrize("mode", ["words", "bytes"])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("name", ["s_sparse_500", "q_dirs", "s_broad_300"])
-def test_row_partition_gloo(world, name):
+def test_row_partition_gloo(world, name, mode):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]

@@ -260,6 +260,58 @@ def test_verify_fused_shards():
     assert sorted(cross) == ref["user_crosscheck"]
 
 
+@pytest.mark.parametrize("name,spans", [
+    ("s_sparse_2000", [(0, 700), (700, 2000)]),
+    ("s_sparse_2000", [(0, 0), (0, 1), (1, 1300), (1300, 2000)]),   # empty shards
+    ("C2", [(k * 10000 // 8, (k + 1) * 10000 // 8) for k in range(8)]),
+    ("s_broad_1000", [(0, 333), (333, 667), (667, 1000)]),
+])
+def test_verify_shard_combine(name, spans):
+    """The multi-GPU step on one device: every shard runs kano_verify_shard
+    into its slot of one gathered word buffer (what the RCCL all-gather
+    builds), then kano_verify_combine gives the full column lists on every
+    shard, the system row on its owner, and pairs that concatenate in shard
+    order to the reference's list."""
+    import torch
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids, tables_from_cluster
+    from kano.synth import make_config, KEY_NAMES
+    if name == "C2":
+        cl = make_config("C2")
+        t = tables_from_cluster(cl)
+        gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
+    else:
+        obj = cluster(name)
+        cs, ps = api_objects(obj)
+        t = intern(cs, ps)
+        gid = group_ids(cs, obj["label"])
+    exp = expected(name)
+    n = t.n
+    W = (n + 63) // 64
+    N = len(spans)
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    gathered = torch.zeros(N * 3 * W, dtype=torch.int64, device="cuda")
+    engs = [DeviceBuild(t, rows=s, build=False) for s in spans]
+    for k, e in enumerate(engs):
+        e.verify_shard(gathered.data_ptr() + 8 * 3 * W * k, gid=gid, sys_row=0, shadow=True)
+    torch.cuda.synchronize()
+    pairs = []
+    for k, (e, (r0, r1)) in enumerate(zip(engs, spans)):
+        r = e.verify_combine(gathered.data_ptr(), N)
+        assert r["all_reachable"].tolist() == exp["all_reachable"]
+        assert r["all_isolated"].tolist() == exp["all_isolated"]
+        assert r["user_crosscheck"].tolist() == exp["user_crosscheck"]["result"]
+        if r0 <= 0 < r1:
+            assert r["system_isolation"].tolist() == exp["system_isolation"]["result"]
+        else:
+            assert r["system_isolation"] is None
+        pairs.append(np.ascontiguousarray(r["pairs"]).reshape(-1, 2))
+        e.close()
+    allp = np.ascontiguousarray(np.concatenate(pairs).astype(np.int32))
+    assert allp.shape[0] == exp["policy_shadow"]["count"]
+    assert sha(allp) == exp["policy_shadow"]["sha256"]
+
+
 @pytest.mark.parametrize("mod", [3, 10**9])
 def test_crosscheck_group_counts(mod):
     """user_crosscheck with few groups (LDS counting sort) and with one group
