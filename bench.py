@@ -63,6 +63,9 @@ def parse():
                     help="skip policy_shadow (its output is ~1e11 pairs on C4)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU sample")
+    ap.add_argument("--rank-of", type=int, default=0,
+                    help="diagnostic: time rank 0's shard step of an N-rank run on one GPU "
+                         "(the all-gather replaced by a local copy; not a bench line)")
     return ap.parse_args()
 
 
@@ -70,16 +73,19 @@ class Step:
     """The hot path on this rank's row shard."""
 
     def __init__(self, eng, gid, n, rank, world, r0, r1, shadow, dist=None, torch=None,
-                 stream=None):
+                 stream=None, emulate=0):
         self.eng, self.gid, self.n = eng, gid, n
         self.rank, self.world, self.r0, self.r1 = rank, world, r0, r1
         self.shadow = shadow
         self.dist, self.torch, self.stream = dist, torch, stream
         self.W = (n + 63) >> 6
-        if world > 1:
+        self.emulate = emulate
+        self.nranks = emulate or world
+        if self.nranks > 1:
             # [OR | cross | NAND] words of this rank's rows, and all ranks'
             self.words = torch.zeros(3 * self.W, dtype=torch.int64, device="cuda")
-            self.gathered = torch.zeros(world * 3 * self.W, dtype=torch.int64, device="cuda")
+            self.gathered = torch.zeros(self.nranks * 3 * self.W, dtype=torch.int64,
+                                        device="cuda")
         from kano._engine import PinnedBuffer
         self.pin = None
         self.pin_idx = None
@@ -103,7 +109,7 @@ class Step:
         if self.pin_idx is None:
             self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
         idx = self.pin_idx.view(np.int32, 4 * max(n, 1))
-        if self.world == 1:
+        if self.nranks == 1:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
             r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=idx)
@@ -114,8 +120,12 @@ class Step:
             with self.torch.cuda.stream(self.stream):
                 eng.verify_shard(self.words.data_ptr(), gid="stored", sys_row=0,
                                  shadow=self.shadow)
-                self.dist.all_gather_into_tensor(self.gathered, self.words)
-                r = eng.verify_combine(self.gathered.data_ptr(), self.world, pairs=pairs, idx=idx)
+                if self.emulate:
+                    self.gathered[:3 * self.W].copy_(self.words)
+                else:
+                    self.dist.all_gather_into_tensor(self.gathered, self.words)
+                r = eng.verify_combine(self.gathered.data_ptr(), self.nranks, pairs=pairs,
+                                       idx=idx)
         for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
             if r[k] is not None:
                 res[k] = r[k]
@@ -234,12 +244,14 @@ def main():
     n = cl.n
     gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
     r0, r1 = rank * n // world, (rank + 1) * n // world
-    stream = torch.cuda.Stream() if world > 1 else None
+    if args.rank_of > 1:
+        r0, r1 = 0, n // args.rank_of
+    stream = torch.cuda.Stream() if world > 1 or args.rank_of > 1 else None
     eng = DeviceBuild(tables, device=torch.cuda.current_device(), rows=(r0, r1), path=args.path,
                       build=False,
                       stream=stream.cuda_stream if stream is not None else None)
     step = Step(eng, gid, n, rank, world, r0, r1, shadow=not args.no_shadow, dist=dist,
-                torch=torch, stream=stream)
+                torch=torch, stream=stream, emulate=args.rank_of if args.rank_of > 1 else 0)
 
     def barrier():
         torch.cuda.synchronize()
@@ -287,7 +299,10 @@ def main():
             "dtype": "u64", "data": "synthetic",
             "config": {"workload": WORKLOADS[args.config], "name": args.config, "pods": n,
                        "policies": cl.P, "mode": cl.mode, "seed": cl.seed,
-                       "parallelism": f"rows{world}", "path": args.path,
+                       "parallelism": (f"rows{world}" if args.rank_of <= 1 else
+                                       f"rank 0 of {args.rank_of} emulated on one GPU, "
+                                       "no collective (diagnostic, not a bench line)"),
+                       "path": args.path,
                        "checks": "all_reachable, all_isolated, user_crosscheck(tenant), "
                                  "system_isolation(0)" +
                                  ("" if args.no_shadow else ", policy_shadow")},

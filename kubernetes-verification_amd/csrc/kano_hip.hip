@@ -109,6 +109,10 @@ struct kano_ctx {
   int pitch_pad = 0;         // experiment: extra words per M row
   int rows_early = 0;        // kano_verify: launch k_rows right after the lists (on stream2)
   int prio = 0;              // checks stream high priority, matrix-write stream low
+  int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
+  int grange_m = 1;          // crosscheck group ranges along the member lists
+  int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
+                             // (measured C3: 16.9 us vs 24-27 us for the serial walk)
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -138,6 +142,9 @@ struct kano_ctx {
   // the matrix write (k_rows) runs on its own stream beside the checks, which
   // only need class-level data; ev_rows marks its end
   hipStream_t stream2 = nullptr;
+  // kano_verify's tail (result copies, policy_shadow's emission) beside the
+  // matrix write, at high priority so that its short kernels get CUs
+  hipStream_t stream3 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_rows = nullptr;
   bool rows_pending = false;
   bool rows_overlap = false;
@@ -321,6 +328,21 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
   return 0;
 }
 
+// the same in two halves: the copy and an event now, the wait later, so
+// that the GPU runs the work queued in between while the host waits
+int slots_begin(kano_ctx* ctx, int first, int count) {
+  KCHK(hipMemcpyAsync(ctx->ghost, P_<u64>(ctx->sizes) + first, sizeof(u64) * count,
+                      hipMemcpyDeviceToHost, ctx->stream));
+  KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
+  return 0;
+}
+
+int slots_wait(kano_ctx* ctx, int count, i64* out) {
+  KCHK(hipEventSynchronize(ctx->ev_sizes));
+  for (int k = 0; k < count; ++k) out[k] = (i64)ctx->ghost[k];
+  return 0;
+}
+
 i64 rows_local(const kano_ctx* ctx) { return ctx->r1 - ctx->r0; }
 
 // ---- classes ---------------------------------------------------------------
@@ -340,6 +362,16 @@ int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   KTRY(dalloc(ctx, cs.cls, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(fb.add(cs.table, sizeof(int32_t) * T, 0xffffffffu));
   KTRY(fb.add(cs.smin, sizeof(int32_t) * T, 0x7fffffffu));
+  // per-class arrays of phase 2a, sized by the side's pods (>= its classes)
+  // so that they need not wait for the class count
+  const i64 m = std::max<i64>(1, cs.m1 - cs.m0);
+  KTRY(dalloc(ctx, cs.rep, sizeof(int32_t) * m));
+  KTRY(dalloc(ctx, cs.mcnt, sizeof(int32_t) * m));
+  KTRY(dalloc(ctx, cs.mcur, sizeof(int32_t) * m));
+  KTRY(dalloc(ctx, cs.moff, sizeof(int32_t) * (m + 1)));
+  KTRY(dalloc(ctx, cs.mem, sizeof(int32_t) * m));
+  KTRY(fb.add(cs.mcnt, sizeof(int32_t) * m, 0u));
+  KTRY(fb.add(cs.mcur, sizeof(int32_t) * m, 0u));
   return 0;
 }
 
@@ -387,45 +419,41 @@ int classify_phase1(kano_ctx* ctx) {
   return sb.run();
 }
 
-int classify_alloc2(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
-  const i64 U = cs.U;
-  KTRY(dalloc(ctx, cs.rep, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, cs.mcnt, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, cs.mcur, sizeof(int32_t) * std::max<i64>(1, U)));
-  KTRY(dalloc(ctx, cs.moff, sizeof(int32_t) * (U + 1)));
-  KTRY(dalloc(ctx, cs.mem, sizeof(int32_t) * std::max<i64>(1, cs.m1 - cs.m0)));
-  KTRY(dalloc(ctx, cs.cval, sizeof(int32_t) * std::max<i64>(1, (i64)cs.KS * U)));
-  KTRY(fb.add(cs.mcnt, sizeof(int32_t) * U, 0u));
-  KTRY(fb.add(cs.mcur, sizeof(int32_t) * U, 0u));
-  return 0;
+int classify_alloc2(kano_ctx* ctx, ClassSet& cs) {
+  return dalloc(ctx, cs.cval, sizeof(int32_t) * std::max<i64>(1, (i64)cs.KS * cs.U));
 }
 
-// phase 2, both sides (U known): ids, member lists of pods [m0, m1),
-// representative values
-int classify_phase2(kano_ctx* ctx) {
-  const i64 n = ctx->n;
+// phase 2a, both sides, without the class counts (the host reads them
+// meanwhile): ids, member counts, their offsets (scanned over the side's pod
+// count; the entries past U are zero), member lists of pods [m0, m1)
+int classify_phase2a(kano_ctx* ctx) {
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
-  const i64 rl = std::max(ctx->rc.m1 - ctx->rc.m0, ctx->cc.m1 - ctx->cc.m0);
+  const i64 mr = ctx->rc.m1 - ctx->rc.m0, ma = ctx->cc.m1 - ctx->cc.m0;
+  const i64 rl = std::max(mr, ma);
   if (rl > 0) {
     hipLaunchKernelGGL(k_cls_assign, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
-  }
-  if (rl > 0) {
     hipLaunchKernelGGL(k_cls_mcount, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
   ScanBatch sb(ctx);
-  KTRY(sb.add(P_<int32_t>(ctx->rc.mcnt), ctx->rc.U, P_<int32_t>(ctx->rc.moff)));
-  KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ctx->cc.U, P_<int32_t>(ctx->cc.moff)));
+  KTRY(sb.add(P_<int32_t>(ctx->rc.mcnt), mr, P_<int32_t>(ctx->rc.moff)));
+  KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ma, P_<int32_t>(ctx->cc.moff)));
   KTRY(sb.run());
   if (rl > 0) {
     hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
+  return 0;
+}
+
+// phase 2b (U known): representative values, slot-major cval[k * U + c]
+int classify_phase2b(kano_ctx* ctx) {
+  ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   const i64 U = std::max(ctx->rc.U, ctx->cc.U);
   if (U > 0) {
     hipLaunchKernelGGL(k_cls_vals, dim3(nblk(U), 2), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->pv), n, pr);
+                       P_<int32_t>(ctx->pv), ctx->n, pr);
     KLAUNCH();
   }
   return 0;
@@ -563,8 +591,12 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(fb.run());
   }
   KTRY(classify_phase1(ctx));
+  // host sync 1 of the build (the class counts), overlapped: the counts
+  // travel while phase 2a runs
+  KTRY(slots_begin(ctx, SZ_UR, 2));
+  KTRY(classify_phase2a(ctx));
   i64 u[2] = {0, 0};
-  KTRY(read_slots(ctx, SZ_UR, 2, u));               // host sync 1 of the build
+  KTRY(slots_wait(ctx, 2, u));
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -574,8 +606,8 @@ int do_front(kano_ctx* ctx, int path) {
   ctx->ldC = std::max<i64>(2, (ctx->UAW + 1) & ~(i64)1);
   {
     FillBatch fb(ctx);
-    KTRY(classify_alloc2(ctx, ctx->rc, fb));
-    KTRY(classify_alloc2(ctx, ctx->cc, fb));
+    KTRY(classify_alloc2(ctx, ctx->rc));
+    KTRY(classify_alloc2(ctx, ctx->cc));
     KTRY(match_alloc(ctx, ctx->am, ctx->cc, fb));
     KTRY(match_alloc(ctx, ctx->sm, ctx->rc, fb));
     KTRY(dalloc(ctx, ctx->nca, sizeof(int32_t) * std::max<i64>(1, P)));
@@ -595,7 +627,7 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
     KTRY(fb.run());
   }
-  KTRY(classify_phase2(ctx));
+  KTRY(classify_phase2b(ctx));
   KTRY(match_both(ctx));
   KCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   // allow side: allowed classes / pods per policy
@@ -645,7 +677,7 @@ int do_front(kano_ctx* ctx, int path) {
 // host sync 2 of the build: every list size at once
 int read_sizes(kano_ctx* ctx) {
   i64 v[SZ_LIGHT - SZ_NNZ_SEL + 1];
-  KTRY(read_slots(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1, v));
+  KTRY(slots_wait(ctx, SZ_LIGHT - SZ_NNZ_SEL + 1, v));
   ctx->nnz_sel = v[SZ_NNZ_SEL - SZ_NNZ_SEL];
   ctx->nnz_alc = v[SZ_NNZ_ALC - SZ_NNZ_SEL];
   ctx->nnz_alw = v[SZ_NNZ_ALW - SZ_NNZ_SEL];
@@ -683,6 +715,32 @@ int build_alist(kano_ctx* ctx) {
   return 0;
 }
 
+// the part of the back end that needs only the class counts: zeroed AC,
+// Mc, cursors and class-level column words, then the caller's fills and
+// launches (kano_verify: the crosscheck's group keys) -- queued while the
+// list sizes travel to the host
+using PreLaunch = std::function<int(FillBatch&)>;
+int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const std::function<int()>& pre_run) {
+  const i64 U = ctx->rc.U, P = ctx->P, ldMc = ctx->ldC;
+  {
+    FillBatch fb(ctx);
+    KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
+    KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
+    KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
+    KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
+    KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
+    KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
+    KTRY(fb.add(ctx->scur, sizeof(int32_t) * U, 0u));
+    KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
+    KTRY(fb.add(ctx->col_or_c, sizeof(u64) * ldMc, 0u));
+    KTRY(fb.add(ctx->col_nand_c, sizeof(u64) * ldMc, 0u));
+    if (pre_fill) KTRY(pre_fill(fb));
+    KTRY(fb.run());
+  }
+  if (pre_run) KTRY(pre_run());
+  return 0;
+}
+
 // lists (S(c) ascending, allowed classes + bits + pods per policy, heavy
 // list) and the compressed matrix Mc (row classes x column classes): light
 // classes by scatter, heavy classes by bitwise OR or the int8 MFMA
@@ -705,19 +763,9 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     FillBatch fb(ctx);
     KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
     KTRY(dalloc(ctx, ctx->ecls, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
-    KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->alc, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alc)));
     KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, H)));
     KTRY(dalloc(ctx, ctx->wicls, sizeof(int32_t) * std::max<i64>(1, ctx->wi_total)));
-    KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
-    KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
-    KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
-    KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
-    KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
-    KTRY(fb.add(ctx->scur, sizeof(int32_t) * U, 0u));
-    KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
-    KTRY(fb.add(ctx->col_or_c, sizeof(u64) * ldMc, 0u));
-    KTRY(fb.add(ctx->col_nand_c, sizeof(u64) * ldMc, 0u));
     if (mfma) {
       KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, ctx->PB * ctx->cc.U)));
       KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, ctx->PB * U)));
@@ -1046,9 +1094,14 @@ int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
   if (!cp.on) return 0;
   const i64 U = ctx->rc.U, G = cp.G, rl = rows_local(ctx);
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
-  hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
-                     (int32_t)G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
-                     P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
+  if (ctx->grange_m)
+    hipLaunchKernelGGL(k_cls_group_range_m, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
+                       (int32_t)G, P_<int32_t>(ctx->rc.cls), P_<int32_t>(ctx->rc.mem), rl,
+                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
+  else
+    hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
+                       (int32_t)G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
+                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
   KLAUNCH();
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {   // classes in group order: per-block LDS histograms
@@ -1070,9 +1123,9 @@ int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
 
 // classes placed in group order, one pass over Mc (R[g], MULTI, and the
 // column checks when the build deferred them), group overlaps A1 / A2
-int cross_stage_b(kano_ctx* ctx, const CrossPlan& cp) {
+int cross_stage_b1(kano_ctx* ctx, const CrossPlan& cp) {
   if (!cp.on) return 0;
-  const i64 U = ctx->rc.U, G = cp.G, ldC = ctx->ldC, UAW = ctx->UAW;
+  const i64 U = ctx->rc.U, G = cp.G;
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {
     hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, U,
@@ -1084,14 +1137,36 @@ int cross_stage_b(kano_ctx* ctx, const CrossPlan& cp) {
                        P_<int32_t>(ctx->corder));
   }
   KLAUNCH();
+  return 0;
+}
+
+int cross_stage_b2(kano_ctx* ctx, const CrossPlan& cp) {
+  if (!cp.on) return 0;
+  const i64 U = ctx->rc.U, G = cp.G, ldC = ctx->ldC, UAW = ctx->UAW;
   const bool cols = ctx->cols_deferred;
   const int32_t* nlive = P_<int32_t>(ctx->koff) + cp.kslots;   // the key scan's total
-  hipLaunchKernelGGL(k_mc_fold, dim3(nblk(UAW, 64), nblk(U, (TPB / 64) * FOLD_PER_WAVE)),
-                     dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), ldC, UAW, ctx->cc.U,
-                     P_<int32_t>(ctx->corder), nlive, P_<int32_t>(ctx->ckey), (int32_t)G,
-                     P_<u64>(ctx->R), P_<u64>(ctx->multi),
-                     cols ? P_<u64>(ctx->col_or_c) : nullptr,
-                     cols ? P_<u64>(ctx->col_nand_c) : nullptr);
+  {
+    const int32_t* ord = P_<int32_t>(ctx->corder);
+    const int32_t* ck = P_<int32_t>(ctx->ckey);
+    u64* co = cols ? P_<u64>(ctx->col_or_c) : nullptr;
+    u64* cn = cols ? P_<u64>(ctx->col_nand_c) : nullptr;
+    const int fm = ctx->fold_mode;   // 0 serial 16; 1 batched 16; 2 batched 32; +10 skip
+    const int pw = (fm % 10) == 2 ? 32 : 16;
+    const dim3 g(nblk(UAW, 64), nblk(U, (TPB / 64) * pw));
+#define KANO_FOLD(PW, B, S)                                                                 \
+  hipLaunchKernelGGL((k_mc_fold<PW, B, S>), g, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), \
+                     ldC, UAW, ctx->cc.U, ord, nlive, ck, (int32_t)G, P_<u64>(ctx->R),     \
+                     P_<u64>(ctx->multi), co, cn)
+    switch (fm) {
+      case 1: KANO_FOLD(16, true, false); break;
+      case 2: KANO_FOLD(32, true, false); break;
+      case 10: KANO_FOLD(16, false, true); break;
+      case 11: KANO_FOLD(16, true, true); break;
+      case 12: KANO_FOLD(32, true, true); break;
+      default: KANO_FOLD(16, false, false); break;
+    }
+#undef KANO_FOLD
+  }
   KLAUNCH();
   ctx->cols_deferred = false;
   hipLaunchKernelGGL(k_cross_groups, dim3((unsigned)G, nblk(UAW)), dim3(TPB), 0, ctx->stream,
@@ -1119,7 +1194,8 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
     ScanBatch sb(ctx);
     KTRY(cross_stage_a(ctx, cp, sb));
     KTRY(sb.run());
-    KTRY(cross_stage_b(ctx, cp));
+    KTRY(cross_stage_b1(ctx, cp));
+    KTRY(cross_stage_b2(ctx, cp));
     hipLaunchKernelGGL(k_cross_pod, dim3(nblk(W * 64)), dim3(TPB), 0, ctx->stream,
                        gdev, G, P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->R),
                        ctx->ldC, P_<u64>(ctx->multi), P_<u64>(ctx->A1), P_<u64>(ctx->A2), W,
@@ -1214,6 +1290,9 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "overlap") ctx->rows_overlap = v != 0;
         if (k == "early") ctx->rows_early = v;
         if (k == "prio") ctx->prio = v;
+        if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
+        if (k == "grm") ctx->grange_m = v;
+        if (k == "fold") ctx->fold_mode = v;
       }
       pos = end + 1;
     }
@@ -1227,6 +1306,15 @@ int kano_create(int device, kano_ctx** out) {
     (void)hipStreamDestroy(ctx->stream);
     if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
       ctx->stream = nullptr;
+      kano_destroy(ctx);
+      return -EIO;
+    }
+  }
+  {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    if (hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, hi) != hipSuccess) {
+      ctx->stream3 = nullptr;
       kano_destroy(ctx);
       return -EIO;
     }
@@ -1253,6 +1341,7 @@ void kano_destroy(kano_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
@@ -1284,6 +1373,7 @@ void kano_destroy(kano_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
   if (ctx->ev_sizes) (void)hipEventDestroy(ctx->ev_sizes);
@@ -1492,7 +1582,8 @@ namespace {
 // checks to the crosscheck pass over Mc (kano_verify), finish_cols() after
 using ExtraFills = std::function<int(FillBatch&)>;
 int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
-               const ExtraFills& extra = ExtraFills()) {
+               const ExtraFills& extra = ExtraFills(), const ExtraFills& pre_fill = ExtraFills(),
+               const std::function<int()>& pre_run = std::function<int()>()) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
@@ -1510,6 +1601,10 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   KTRY(do_front(ctx, path));
+  // host sync 2 (the list sizes), overlapped with the size-independent part
+  // of the back end
+  KTRY(slots_begin(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1));
+  KTRY(do_back_pre(ctx, pre_fill, pre_run));
   KTRY(read_sizes(ctx));
   KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   ctx->cols_deferred = defer_cols;
@@ -1750,6 +1845,7 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (sp.rl + 1)));
   KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, sp.nt)));
   KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
+  if (ctx->sh_items == 1) KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));   // accumulated
   return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
 }
 
@@ -1770,8 +1866,12 @@ int shadow_stage_a(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
     a.ldC = ctx->ldC;
     a.flags = P_<uint8_t>(ctx->flags);
     a.T = P_<i64>(ctx->T);
-    hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, ctx->stream, a, sp.nf,
-                       P_<i64>(ctx->tcnt));
+    if (ctx->sh_items == 1)
+      hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)(sp.nt * SH_ITEMS)), dim3(TPB), 0,
+                         ctx->stream, a, sp.nf, P_<i64>(ctx->tcnt));
+    else
+      hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, ctx->stream, a,
+                         sp.nf, P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
   KTRY(sb.add(P_<i64>(ctx->tcnt), sp.nt, P_<i64>(ctx->toff), SZ_NL));
@@ -1808,24 +1908,25 @@ int shadow_front(kano_ctx* ctx) {
   return sb.run();
 }
 
-int shadow_back(kano_ctx* ctx, i64 nl, i64 total) {
+int shadow_back(kano_ctx* ctx, i64 nl, i64 total, hipStream_t st = nullptr) {
+  if (!st) st = ctx->stream;
   const i64 U = ctx->rc.U, rl = rows_local(ctx), nf = ctx->nflags;
   const i64 nt = (nf + SH_TILE - 1) / SH_TILE;
   KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nl)));
   KTRY(dalloc(ctx, ctx->out, sizeof(int2) * std::max<i64>(1, total)));
   if (nt > 0 && nl > 0) {
-    hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)nt), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)nt), dim3(TPB), 0, st,
                        P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist), P_<i64>(ctx->pfoff),
                        P_<uint8_t>(ctx->flags), nf, P_<i64>(ctx->toff), P_<int2>(ctx->L));
     KLAUNCH();
   }
   if (rl > 0 && total > 0) {
-    hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
                        P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
                        P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out));
     KLAUNCH();
   }
-  KCHK(hipEventRecord(ctx->ev[6], ctx->stream));
+  KCHK(hipEventRecord(ctx->ev[6], st));
   ctx->shadow_total = total;
   return 0;
 }
@@ -1960,13 +2061,23 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // fill launch
   CrossPlan cp;
   ShadowPlan sp;
+  // the crosscheck's fills and its group-key sort need only the class
+  // counts: they run while the list sizes travel (build sync 2)
+  auto pre_fill = [&](FillBatch& fb) -> int {
+    return want_cross ? cross_prepare(ctx, gid, ngroups, cp, fb) : 0;
+  };
+  auto pre_run = [&]() -> int {
+    if (!want_cross || !cp.on) return 0;
+    ScanBatch sb(ctx);
+    KTRY(cross_stage_a(ctx, cp, sb));
+    KTRY(sb.run());
+    return cross_stage_b1(ctx, cp);
+  };
   auto extra = [&](FillBatch& fb) -> int {
-    if (want_cross) KTRY(cross_prepare(ctx, gid, ngroups, cp, fb));
-    if (want_shadow) KTRY(shadow_prepare(ctx, sp, fb));
-    return 0;
+    return want_shadow ? shadow_prepare(ctx, sp, fb) : 0;
   };
   ctx->vs_open = false;
-  KTRY(build_impl(ctx, path, false, want_cross, extra));
+  KTRY(build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run));
   // the matrix write needs only the lists: with rows_early it starts here on
   // stream2, beside the class-level checks
   const bool early = ctx->rows_early && ctx->rows_overlap;
@@ -1974,14 +2085,13 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   const bool cross_on = want_cross && cp.on;
-  // stage A of both checks, their scans in one launch, stage B
-  {
+  // policy_shadow's stage A and its scans, the crosscheck's pass over Mc
+  if (want_shadow) {
     ScanBatch sb(ctx);
-    if (cross_on) KTRY(cross_stage_a(ctx, cp, sb));
-    if (want_shadow) KTRY(shadow_stage_a(ctx, sp, sb));
+    KTRY(shadow_stage_a(ctx, sp, sb));
     KTRY(sb.run());
   }
-  if (cross_on) KTRY(cross_stage_b(ctx, cp));
+  if (cross_on) KTRY(cross_stage_b2(ctx, cp));
   if (ctx->cols_deferred) {   // no crosscheck pass ran (empty shard / matrix)
     ctx->cols_deferred = false;
     KTRY(mc_cols(ctx));
@@ -2110,25 +2220,27 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     nidx += counts[r];
   }
   if (!ctx->vs_have_sys) counts[3] = -1;
-  // the lists were written before the matrix write: copy them beside it
-  // (stream2 is free unless the matrix write runs there)
-  hipStream_t cs = ctx->rows_overlap ? ctx->stream : ctx->stream2;
-  if (nidx > 0) {
-    if (cs != ctx->stream) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+  // everything the matrix write does not touch runs beside it on stream3:
+  // the list copies, policy_shadow's compaction and emission, the pairs copy
+  hipStream_t cs = ctx->stream3;
+  KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+  if (nidx > 0)
     KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, cs));
-  }
   i64 total = 0;
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
-    KTRY(shadow_back(ctx, v[0], total));
+    KTRY(shadow_back(ctx, v[0], total, cs));
     ctx->shadow_total = total;
     *shadow_count = total;
   }
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
-                        ctx->stream));
+                        cs));
+  // later work on the main stream (a fetch of the pairs, the next build)
+  // follows the tail
+  KCHK(hipEventRecord(ctx->ev_fork, cs));
+  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
   KTRY(join_rows(ctx));  // the matrix is part of the result
-  if (nidx > 0 && cs != ctx->stream) KCHK(hipStreamSynchronize(cs));
   return sync(ctx);
 }
 }  // namespace

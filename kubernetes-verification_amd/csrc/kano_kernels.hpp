@@ -648,6 +648,26 @@ __global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restri
   wave_agg_minmax(gmin, gmax, c, g, act);
 }
 
+// The same ranges read along the class-grouped member list (mem, moff over
+// the shard's pods): a wave's lanes hold mostly one class, so one atomic pair
+// per class run instead of per-lane or per-unique-key merging.
+__global__ __launch_bounds__(TPB) void k_cls_group_range_m(const int32_t* __restrict__ gid,
+                                                           int32_t G,
+                                                           const int32_t* __restrict__ cls,
+                                                           const int32_t* __restrict__ mem,
+                                                           i64 rl, int32_t* gmin, int32_t* gmax,
+                                                           int32_t* err) {
+  const i64 k = (i64)blockIdx.x * TPB + threadIdx.x;
+  bool act = k < rl;
+  const int32_t i = act ? mem[k] : 0;
+  const int32_t c = act ? cls[i] : -1, g = act ? gid[i] : 0;
+  if (act && (g < 0 || g >= G)) {   // caller-declared group count violated
+    atomicOr(err, 1);
+    act = false;
+  }
+  wave_seg_minmax(gmin, gmax, c, g, act);
+}
+
 // Classes keyed by their group for one pass over Mc: key = g for classes
 // whose local members are all in group g, G for classes mixing groups (MULTI),
 // -1 for classes without local members.  Counted per key (counting sort).
@@ -722,6 +742,11 @@ __global__ __launch_bounds__(TPB) void k_key_place_lds(i64 U, const int32_t* __r
 // all_reachable / all_isolated.  Block = 64 words x (4 waves x 16 sorted
 // classes); runs of equal key are OR-ed in registers, one atomic per run.
 constexpr int FOLD_PER_WAVE = 16;
+// PW classes per wave; BATCH: the wave's class ids and keys in one round trip
+// (lane q holds entry k0+q) and all its Mc words in flight together, else a
+// serial walk with wave-uniform index loads; SKIP: column atomics skipped
+// when saturated (or_if_new)
+template <int PW, bool BATCH, bool SKIP>
 __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
                                                  i64 Ua, const int32_t* __restrict__ order,
                                                  const int32_t* __restrict__ nlive_p,
@@ -732,24 +757,53 @@ __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const i64 w = (i64)blockIdx.x * 64 + lane;
   const i64 nlive = *nlive_p;
-  const i64 k0 = ((i64)blockIdx.y * (TPB / 64) + wid) * FOLD_PER_WAVE;
-  const i64 k1 = min(nlive, k0 + FOLD_PER_WAVE);
+  const i64 k0 = ((i64)blockIdx.y * (TPB / 64) + wid) * PW;
+  const i64 k1 = min(nlive, k0 + PW);
   const bool wok = w < UW;
   const u64 vm = wok ? valid_mask(w, Ua) : 0ull;
   u64 o = 0, na = 0, acc = 0;
   int32_t cur = -1;
-  for (i64 k = k0; k < k1; ++k) {
-    const int32_t c = order[k];
-    const int32_t key = ckey[c];
-    const u64 v = wok ? Mc[(i64)c * ldMc + w] : 0ull;
-    o |= v;
-    na |= ~v & vm;
-    if (key != cur) {
-      if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
-      cur = key;
-      acc = 0;
+  if (BATCH) {
+    int32_t myc = 0, myk = 0;
+    if (lane < PW && k0 + lane < k1) {
+      myc = order[k0 + lane];
+      myk = ckey[myc];
     }
-    acc |= v;
+    const int cnt = (int)max((i64)0, k1 - k0);
+    u64 v[PW];
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const int32_t c = __shfl(myc, q, 64);
+      v[q] = (wok && q < cnt) ? Mc[(i64)c * ldMc + w] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const int32_t key = __shfl(myk, q, 64);
+      if (q < cnt) {
+        o |= v[q];
+        na |= ~v[q] & vm;
+        if (key != cur) {
+          if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
+          cur = key;
+          acc = 0;
+        }
+        acc |= v[q];
+      }
+    }
+  } else {
+    for (i64 k = k0; k < k1; ++k) {
+      const int32_t c = order[k];
+      const int32_t key = ckey[c];
+      const u64 v = wok ? Mc[(i64)c * ldMc + w] : 0ull;
+      o |= v;
+      na |= ~v & vm;
+      if (key != cur) {
+        if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
+        cur = key;
+        acc = 0;
+      }
+      acc |= v;
+    }
   }
   if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
   if (col_or) {
@@ -759,8 +813,13 @@ __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64
     if (wid == 0 && wok) {
       o = red[0][0][lane] | red[0][1][lane] | red[0][2][lane] | red[0][3][lane];
       na = red[1][0][lane] | red[1][1][lane] | red[1][2][lane] | red[1][3][lane];
-      if (o) atomicOr(&col_or[w], o);
-      if (na) atomicOr(&col_nand[w], na);
+      if (SKIP) {
+        if (o) or_if_new(&col_or[w], o);
+        if (na) or_if_new(&col_nand[w], na);
+      } else {
+        if (o) atomicOr(&col_or[w], o);
+        if (na) atomicOr(&col_nand[w], na);
+      }
     }
   }
 }
@@ -1383,6 +1442,48 @@ __global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a, i64 nflags,
   }
   const i64 tot = block_sum((i64)mine, sm);
   if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+// The same test with one candidate pair per thread: the tile of SH_TILE
+// pairs is spread over SH_ITEMS blocks, so the chip holds enough waves to hide
+// the subset tests' dependent loads (the 8-pairs-per-thread form above leaves
+// about two waves per SIMD on C3).  tile_cnt accumulates (zeroed first).
+__global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
+                                                     i64* __restrict__ tile_cnt) {
+  __shared__ i64 sm[4];
+  __shared__ i64 rng[2];
+  const i64 tile = blockIdx.x / SH_ITEMS, part = blockIdx.x % SH_ITEMS;
+  const i64 b0 = tile * SH_TILE + part * TPB;
+  if (b0 >= nflags) return;                      // block-uniform
+  const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
+  if (threadIdx.x == 0) rng[0] = class_of_pair(a.pfoff, 0, a.U - 1, b0);
+  if (threadIdx.x == 64) rng[1] = class_of_pair(a.pfoff, 0, a.U - 1, b1);
+  __syncthreads();
+  const i64 t = b0 + threadIdx.x;
+  int f = 0;
+  i64 c = -1;
+  if (t < nflags) {
+    c = class_of_pair(a.pfoff, rng[0], rng[1], t);
+    const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
+    const i64 x = q / s, y = q - x * s;
+    if (a.mcnt[c] > 0 && x != y) {
+      const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
+      f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+    }
+    a.flags[t] = (uint8_t)f;
+  }
+  // T[c] += f: one atomic per wave when the wave lies in one class
+  const i64 c0 = __shfl(c, 0, 64);
+  if (__all(c == c0 || c < 0)) {
+    const int r = wave_sum(f);
+    if ((threadIdx.x & 63) == 0 && r && c0 >= 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c0]), (unsigned long long)r);
+  } else if (f) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
+  }
+  const i64 tot = block_sum((i64)f, sm);
+  if (threadIdx.x == 0 && tot)
+    atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
 }
 
 // the flagged pairs in flat order: L[tile_off[b] + rank] = (j, k)

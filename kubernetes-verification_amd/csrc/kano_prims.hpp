@@ -295,6 +295,30 @@ __device__ __forceinline__ void wave_agg_minmax(int32_t* lo, int32_t* hi, i64 ke
   }
 }
 
+// atomicMin(&lo[key], v), atomicMax(&hi[key], v) for keys that come in
+// contiguous runs along the lanes (a class-grouped member list): a segmented
+// min / max over the wave, one atomic pair per run.  Every lane must call it.
+__device__ __forceinline__ void wave_seg_minmax(int32_t* lo, int32_t* hi, i64 key, int32_t v,
+                                                bool active) {
+  const int lane = threadIdx.x & 63;
+  int32_t mn = active ? v : INT32_MAX, mx = active ? v : INT32_MIN;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const i64 ko = __shfl_up(key, d, 64);
+    const int32_t a = __shfl_up(mn, d, 64), b = __shfl_up(mx, d, 64);
+    if (lane >= d && ko == key) {
+      mn = min(mn, a);
+      mx = max(mx, b);
+    }
+  }
+  const i64 kn = __shfl_down(key, 1, 64);
+  const bool last = lane == 63 || kn != key;
+  if (last && mn <= mx) {
+    atomicMin(&lo[key], mn);
+    atomicMax(&hi[key], mx);
+  }
+}
+
 // ---- small helpers ---------------------------------------------------------
 __device__ __forceinline__ i64 upper_bound_i32(const int32_t* a, i64 n, i64 key) {
   i64 lo = 0, hi = n;
@@ -303,6 +327,16 @@ __device__ __forceinline__ i64 upper_bound_i32(const int32_t* a, i64 n, i64 key)
     if ((i64)a[mid] <= key) lo = mid + 1; else hi = mid;
   }
   return lo;
+}
+
+// *p |= v with the atomic skipped when every bit of v is already set.  Bits
+// only ever get set, so a stale read can only show fewer of them (one atomic
+// too many), never more: the skip is safe without coherence.  Saturating OR
+// targets (column words hit by every block) then take one atomic per new bit
+// group instead of one per block.  (Measured on k_mc_fold's column words:
+// the read before the atomic cost more than the atomics it saved.)
+__device__ __forceinline__ void or_if_new(u64* p, u64 v) {
+  if (v & ~*p) atomicOr(p, v);
 }
 
 // bits of word w that lie below n

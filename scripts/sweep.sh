@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 extra=""
 [ "$cfg" = "C4" ] && extra="--no-shadow"
 for t in "$@"; do
-  KANO_TUNE="$t" timeout -k 10 400 python bench.py --config $cfg --steps $steps --warmup ${WARMUP:-1} --cpu-baseline 0 $extra > gpurun_out/sweep.log 2>&1
+  KANO_TUNE="$t" timeout -k 10 400 python bench.py --config $cfg --steps $steps --warmup ${WARMUP:-1} --cpu-baseline 0 $extra ${EXTRA:-} > gpurun_out/sweep.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "$cfg $t rc=$rc"; tail -5 gpurun_out/sweep.log; exit $rc; fi
   python3 -c "
