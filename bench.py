@@ -96,6 +96,7 @@ class Step:
         self.PinnedBuffer = PinnedBuffer
         self.results = {}
         self.k_rows_ms = []
+        self.host_stage_s = 0.0
 
     def __call__(self):
         eng, n = self.eng, self.n
@@ -105,10 +106,12 @@ class Step:
             if self.pin is None:
                 self.pin_pairs = 1 << 20
                 self.pin = self.PinnedBuffer(self.pin_pairs * 8)
-            pairs = self.pin.view(np.int32, 2 * self.pin_pairs)
+                self.pairs_view = self.pin.view(np.int32, 2 * self.pin_pairs)
+            pairs = self.pairs_view
         if self.pin_idx is None:
             self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
-        idx = self.pin_idx.view(np.int32, 4 * max(n, 1))
+            self.idx_view = self.pin_idx.view(np.int32, 4 * max(n, 1))
+        idx = self.idx_view
         if self.nranks == 1:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
@@ -137,7 +140,10 @@ class Step:
                 self.pin.close()
                 self.pin_pairs = 2 * cnt
                 self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+                self.pairs_view = self.pin.view(np.int32, 2 * self.pin_pairs)
+        t1 = time.perf_counter()
         st = eng.stage_times()
+        self.host_stage_s += time.perf_counter() - t1
         self.k_rows_ms.append(st["k_rows"])
         self.stages = st
         self.results = res
@@ -262,6 +268,7 @@ def main():
     for _ in range(args.warmup):
         step()
     step.k_rows_ms.clear()
+    step.host_stage_s = 0.0
     barrier()
     t0 = time.perf_counter()
     marks = []
@@ -312,6 +319,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": k_rows_ms},
             "stages_ms_last_step": {k: round(v, 4) for k, v in step.stages.items()},
+            "host_stage_times_ms_per_step": round(step.host_stage_s / args.steps * 1e3, 4),
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),
                         "p90": round(float(np.percentile(step_ms, 90)), 4),

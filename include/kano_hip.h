@@ -193,7 +193,9 @@ int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups);
 
 /* Timing of the last kano_build / kano_shadow stages on the context stream
  * (HIP events), milliseconds: [classes, allow, select + plan, rows stage,
- * shadow, build total, k_rows kernel alone, 0]. */
+ * shadow, build total, k_rows kernel alone, 0].  Slots 0-5 are recorded only
+ * when the context was created with KANO_TUNE=timing=1 (each event costs
+ * host time on the launch path); slot 6 always. */
 int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
 
 /* Page-locked host buffers for fast device-to-host result copies. */

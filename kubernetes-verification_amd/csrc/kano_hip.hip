@@ -111,6 +111,7 @@ struct kano_ctx {
   int prio = 0;              // checks stream high priority, matrix-write stream low
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
   int grange_m = 1;          // crosscheck group ranges along the member lists
+  int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
   int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
                              // (measured C3: 16.9 us vs 24-27 us for the serial walk)
 
@@ -340,6 +341,14 @@ int slots_begin(kano_ctx* ctx, int first, int count) {
 int slots_wait(kano_ctx* ctx, int count, i64* out) {
   KCHK(hipEventSynchronize(ctx->ev_sizes));
   for (int k = 0; k < count; ++k) out[k] = (i64)ctx->ghost[k];
+  return 0;
+}
+
+// stage-boundary events (kano_stage_times) only when asked for: each record
+// costs host time on the launch path.  The k_rows events (7, 8) always run:
+// the bench's roofline needs them.
+int stage_mark(kano_ctx* ctx, int k, hipStream_t st) {
+  if (ctx->stage_timing) KCHK(hipEventRecord(ctx->ev[k], st));
   return 0;
 }
 
@@ -599,7 +608,7 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(slots_wait(ctx, 2, u));
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
-  KCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  KTRY(stage_mark(ctx, 1, ctx->stream));
 
   const i64 P = ctx->P, Ur = ctx->rc.U, Ua = ctx->cc.U;
   ctx->UAW = (Ua + 63) / 64;
@@ -629,10 +638,10 @@ int do_front(kano_ctx* ctx, int path) {
   }
   KTRY(classify_phase2b(ctx));
   KTRY(match_both(ctx));
-  KCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  KTRY(stage_mark(ctx, 2, ctx->stream));
   // allow side: allowed classes / pods per policy
   if (P > 0) {
-    hipLaunchKernelGGL(k_pol_allow_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_pol_allow_count, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                        P_<int32_t>(ctx->am.gmem), P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca),
                        P_<int32_t>(ctx->acnt));
@@ -640,7 +649,7 @@ int do_front(kano_ctx* ctx, int path) {
   }
   // select side: |S(c)|, rebuild cost, the per-class plan
   if (P > 0 && Ur > 0) {
-    hipLaunchKernelGGL(k_sel_count, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_sel_count, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                        P_<int32_t>(ctx->sm.gmem), P_<int32_t>(ctx->acnt), P_<int32_t>(ctx->scnt),
                        P_<unsigned long long>(ctx->cost));
@@ -706,7 +715,7 @@ int build_alist(kano_ctx* ctx) {
   const i64 P = ctx->P;
   KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
   if (P > 0 && ctx->cc.U > 0) {
-    hipLaunchKernelGGL(k_pol_pods, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_pol_pods, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
                        P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
     KLAUNCH();
@@ -777,7 +786,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   if (U > 0) {
     if (P > 0) {
-      hipLaunchKernelGGL(k_sel_place, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+      hipLaunchKernelGGL(k_sel_place, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
                          P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                          P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
                          P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls));
@@ -798,7 +807,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     KLAUNCH();
   }
   if (P > 0 && ctx->cc.U > 0) {
-    hipLaunchKernelGGL(k_pol_allow_fill, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                        P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
                        P_<u64>(ctx->AC), ctx->ldC);
@@ -807,13 +816,14 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
   // entries, cache-resident).  Measured: the flat lists win when they stay
-  // on-die (C3: 6 MB, k_rows -10%) and the rows read them several times
-  // over; past the Infinity Cache the member lists win (C5: 450 MB of
-  // lists, k_rows -10%; C4: 500 MB)
+  // on-die (C3: 6 MB, k_rows -10% at one rank; at 1/8 of the rows, where the
+  // rows' build is exposed, k_rows 99 -> 49 us with the flattened walk) ;
+  // past the Infinity Cache the member lists win (C5: 450 MB of lists,
+  // k_rows -10%; C4: 500 MB)
   ctx->alist_valid = false;
   int ua = ctx->rows_alist;
   if (ua < 0)
-    ua = ctx->light_cost > 4 * ctx->nnz_alw && ctx->nnz_alw * 4 <= (64ll << 20) ? 1 : 0;
+    ua = ctx->nnz_alw * 4 <= (64ll << 20) ? 1 : 0;
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx));
   if (U == 0) return 0;
@@ -1293,6 +1303,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
         if (k == "grm") ctx->grange_m = v;
         if (k == "fold") ctx->fold_mode = v;
+        if (k == "timing") ctx->stage_timing = v;
       }
       pos = end + 1;
     }
@@ -1599,19 +1610,19 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
-  KCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  KTRY(stage_mark(ctx, 0, ctx->stream));
   KTRY(do_front(ctx, path));
   // host sync 2 (the list sizes), overlapped with the size-independent part
   // of the back end
   KTRY(slots_begin(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1));
   KTRY(do_back_pre(ctx, pre_fill, pre_run));
   KTRY(read_sizes(ctx));
-  KCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  KTRY(stage_mark(ctx, 3, ctx->stream));
   ctx->cols_deferred = defer_cols;
   KTRY(do_back(ctx, path, extra));
   if (!defer_cols) KTRY(do_rows(ctx));
   if (rows_now) KTRY(launch_rows(ctx));
-  KCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  KTRY(stage_mark(ctx, 4, ctx->stream));
   ctx->cols_valid = true;
   ctx->built = true;
   return 0;
@@ -1851,7 +1862,7 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
 
 // subset tests; the list-offset scans go to sb
 int shadow_stage_a(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
-  KCHK(hipEventRecord(ctx->ev[5], ctx->stream));
+  KTRY(stage_mark(ctx, 5, ctx->stream));
   if (sp.nt > 0) {
     ShadowArgs a;
     a.U = sp.U;
@@ -1926,7 +1937,7 @@ int shadow_back(kano_ctx* ctx, i64 nl, i64 total, hipStream_t st = nullptr) {
                        P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out));
     KLAUNCH();
   }
-  KCHK(hipEventRecord(ctx->ev[6], st));
+  KTRY(stage_mark(ctx, 6, st));
   ctx->shadow_total = total;
   return 0;
 }
@@ -2222,10 +2233,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   if (!ctx->vs_have_sys) counts[3] = -1;
   // everything the matrix write does not touch runs beside it on stream3:
   // the list copies, policy_shadow's compaction and emission, the pairs copy
+  // (the copies are blit kernels that crawl beside k_rows: the short
+  // shadow kernels go first so that they do not queue behind them)
   hipStream_t cs = ctx->stream3;
   KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
-  if (nidx > 0)
-    KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, cs));
   i64 total = 0;
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
@@ -2233,6 +2244,8 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     ctx->shadow_total = total;
     *shadow_count = total;
   }
+  if (nidx > 0)
+    KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, cs));
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         cs));
@@ -2319,11 +2332,14 @@ int kano_stage_times(kano_ctx* ctx, float* ms) {
   KTRY(sync(ctx));
   for (int k = 0; k < 8; ++k) ms[k] = 0.f;
   if (ctx->built && !ctx->lists_mode) {
-    for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&ms[k], ctx->ev[k], ctx->ev[k + 1]);
-    (void)hipEventElapsedTime(&ms[5], ctx->ev[0], ctx->ev[4]);
+    if (ctx->stage_timing) {
+      for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&ms[k], ctx->ev[k], ctx->ev[k + 1]);
+      (void)hipEventElapsedTime(&ms[5], ctx->ev[0], ctx->ev[4]);
+    }
     if (ctx->rows_timed) (void)hipEventElapsedTime(&ms[6], ctx->ev[7], ctx->ev[8]);
   }
-  if (ctx->shadow_total >= 0) (void)hipEventElapsedTime(&ms[4], ctx->ev[5], ctx->ev[6]);
+  if (ctx->stage_timing && ctx->shadow_total >= 0)
+    (void)hipEventElapsedTime(&ms[4], ctx->ev[5], ctx->ev[6]);
   return 0;
 }
 

@@ -67,8 +67,22 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
     s = (s + 1) & a.tmask;
   }
   a.slot_of[i] = (int32_t)s;
-  // smallest member per slot (the class representative); smin only falls
-  if ((int32_t)i < a.smin[s]) atomicMin(&a.smin[s], (int32_t)i);
+  // smallest member per slot (the class representative); smin only falls.
+  // Pods rise with the lane, so among the lanes of a wave that share a slot
+  // the lowest holds the smallest pod: only it needs the atomic (popular
+  // classes otherwise send every member's atomic to one address).
+  const int lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1ull;
+  bool first = true;
+  u64 pend = __ballot(true);   // lanes that returned early (i >= m1) are off
+  for (int round = 0; round < 4 && pend; ++round) {
+    const int leader = __ffsll((long long)pend) - 1;
+    const uint32_t sl = __shfl(s, leader, 64);
+    const u64 same = __ballot(s == sl);
+    if (s == sl && (same & below)) first = false;
+    pend &= ~same;
+  }
+  if (first && (int32_t)i < a.smin[s]) atomicMin(&a.smin[s], (int32_t)i);
 }
 
 // flag / cid are indexed by i - m0
@@ -202,19 +216,53 @@ __global__ __launch_bounds__(TPB) void k_pol_classes(const u64* __restrict__ AC,
 }
 
 // block per policy: the allowed pods (members of the allowed classes)
-__global__ __launch_bounds__(TPB) void k_pol_pods(const i64* __restrict__ alcoff,
+// Per-policy kernels below run one wave per policy (WPB policies per block):
+// most policies match a handful of classes, so a block per policy leaves
+// most of its lanes idle and quadruples the waves to schedule.
+constexpr int WPB = TPB / 64;
+__device__ __forceinline__ i64 wave_policy() {
+  return (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
+}
+
+// allowed pods of policy p: members of its allowed column classes, streamed
+// 64 classes at a time as one flat range (no per-class round trips)
+__global__ __launch_bounds__(TPB) void k_pol_pods(i64 P, const i64* __restrict__ alcoff,
                                                   const int32_t* __restrict__ alc,
                                                   const int32_t* __restrict__ cmoff,
                                                   const int32_t* __restrict__ cmem,
                                                   const i64* __restrict__ aloff,
                                                   int32_t* __restrict__ alist) {
-  const i64 p = blockIdx.x;
+  __shared__ int32_t seg_m0[WPB][64];
+  __shared__ int32_t seg_pre[WPB][65];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const i64 p = wave_policy();
+  if (p >= P) return;                      // wave-uniform
   i64 out = aloff[p];
-  for (i64 e = alcoff[p]; e < alcoff[p + 1]; ++e) {
-    const int32_t ca = alc[e];
-    const int32_t m0 = cmoff[ca], m1 = cmoff[ca + 1];
-    for (int32_t m = m0 + threadIdx.x; m < m1; m += TPB) alist[out + (m - m0)] = cmem[m];
-    out += m1 - m0;
+  const i64 e1 = alcoff[p + 1];
+  for (i64 e0 = alcoff[p]; e0 < e1; e0 += 64) {
+    const int ns = (int)min((i64)64, e1 - e0);
+    int32_t m0 = 0, len = 0;
+    if (lane < ns) {
+      const int32_t ca = alc[e0 + lane];
+      m0 = cmoff[ca];
+      len = cmoff[ca + 1] - m0;
+    }
+    int32_t tot;
+    const int32_t pre = wave_excl_scan(len, tot);
+    seg_m0[wid][lane] = m0;
+    seg_pre[wid][lane] = pre;
+    if (lane == 0) seg_pre[wid][ns] = tot;
+    __builtin_amdgcn_wave_barrier();
+    for (int32_t id = lane; id < tot; id += 64) {
+      int lo = 0, hi = ns - 1;               // last segment with prefix <= id
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (seg_pre[wid][mid] <= id) lo = mid; else hi = mid - 1;
+      }
+      alist[out + id] = cmem[seg_m0[wid][lo] + (id - seg_pre[wid][lo])];
+    }
+    out += tot;
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -406,32 +454,34 @@ __global__ __launch_bounds__(TPB) void k_offsets_to_start(const i64* __restrict_
 
 // ---- select side: S(c) = ascending policies whose list holds c --------------
 // block per policy: |S(c)| and the rebuild cost sum_{p in S(c)} |allow_p|
-__global__ __launch_bounds__(TPB) void k_sel_count(const i64* __restrict__ pstart,
+__global__ __launch_bounds__(TPB) void k_sel_count(i64 P, const i64* __restrict__ pstart,
                                                    const int32_t* __restrict__ plen,
                                                    const int32_t* __restrict__ pcls,
                                                    const int32_t* __restrict__ acnt,
                                                    int32_t* scnt, unsigned long long* cost) {
-  const i64 p = blockIdx.x;
+  const i64 p = wave_policy();
+  if (p >= P) return;
   const int32_t* L = pcls + pstart[p];
   const int32_t len = plen[p];
   const unsigned long long a = (unsigned long long)acnt[p];
-  for (int32_t k = threadIdx.x; k < len; k += TPB) {
+  for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
     const int32_t c = L[k];
     atomicAdd(&scnt[c], 1);
     if (a) atomicAdd(&cost[c], a);
   }
 }
 
-__global__ __launch_bounds__(TPB) void k_sel_place(const i64* __restrict__ pstart,
+__global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict__ pstart,
                                                    const int32_t* __restrict__ plen,
                                                    const int32_t* __restrict__ pcls,
                                                    const i64* __restrict__ soffc, int32_t* scur,
                                                    int32_t* __restrict__ slist,
                                                    int32_t* __restrict__ ecls) {
-  const i64 p = blockIdx.x;
+  const i64 p = wave_policy();
+  if (p >= P) return;
   const int32_t* L = pcls + pstart[p];
   const int32_t len = plen[p];
-  for (int32_t k = threadIdx.x; k < len; k += TPB) {
+  for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
     const int32_t c = L[k];
     const i64 e = soffc[c] + atomicAdd(&scur[c], 1);
     slist[e] = (int32_t)p;
@@ -490,37 +540,38 @@ __global__ __launch_bounds__(TPB) void k_sort_lists_big(const i64* __restrict__ 
 }
 
 // ---- allow side: per policy the allowed column classes and pods -----------
-__global__ __launch_bounds__(TPB) void k_pol_allow_count(const i64* __restrict__ pstart,
+__global__ __launch_bounds__(TPB) void k_pol_allow_count(i64 P, const i64* __restrict__ pstart,
                                                          const int32_t* __restrict__ plen,
                                                          const int32_t* __restrict__ pcls,
                                                          const int32_t* __restrict__ csize,
                                                          int32_t* __restrict__ nca,
                                                          int32_t* __restrict__ acnt) {
-  __shared__ i64 sm[4];
-  const i64 p = blockIdx.x;
+  const i64 p = wave_policy();
+  if (p >= P) return;
   const int32_t* L = pcls + pstart[p];
   const int32_t len = plen[p];
   i64 pods = 0;
-  for (int32_t k = threadIdx.x; k < len; k += TPB) pods += csize[L[k]];
-  pods = block_sum(pods, sm);
-  if (threadIdx.x == 0) {
+  for (int32_t k = threadIdx.x & 63; k < len; k += 64) pods += csize[L[k]];
+  pods = wave_sum(pods);
+  if ((threadIdx.x & 63) == 0) {
     nca[p] = len;
     acnt[p] = (int32_t)pods;
   }
 }
 
 // block per policy: allowed class list (alc) and its bits AC[p]
-__global__ __launch_bounds__(TPB) void k_pol_allow_fill(const i64* __restrict__ pstart,
+__global__ __launch_bounds__(TPB) void k_pol_allow_fill(i64 P, const i64* __restrict__ pstart,
                                                         const int32_t* __restrict__ plen,
                                                         const int32_t* __restrict__ pcls,
                                                         const i64* __restrict__ alcoff,
                                                         int32_t* __restrict__ alc, u64* AC,
                                                         i64 ldC) {
-  const i64 p = blockIdx.x;
+  const i64 p = wave_policy();
+  if (p >= P) return;
   const int32_t* L = pcls + pstart[p];
   const int32_t len = plen[p];
   int32_t* out = alc + alcoff[p];
-  for (int32_t k = threadIdx.x; k < len; k += TPB) {
+  for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
     const int32_t ca = L[k];
     out[k] = ca;
     atomicOr(&AC[p * ldC + (ca >> 6)], 1ull << (ca & 63));
@@ -909,11 +960,23 @@ __global__ __launch_bounds__(TPB) void k_class_plan(ClassPlan a) {
     if (m > 0) smax = s;
     if (m > 0 && !hv) light = (unsigned long long)cost * (unsigned long long)chunks;
   }
-  // one atomic per wave
+  // one atomic pair per block (per wave, the two slots took ~700 contended
+  // atomics on C3)
+  __shared__ unsigned long long sl[TPB / 64];
+  __shared__ int32_t sx[TPB / 64];
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) smax = max(smax, __shfl_xor(smax, d, 64));
   light = wave_sum(light);
   if ((threadIdx.x & 63) == 0) {
+    sl[threadIdx.x >> 6] = light;
+    sx[threadIdx.x >> 6] = smax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < TPB / 64; ++w) {
+      light += sl[w];
+      smax = max(smax, sx[w]);
+    }
     if (smax > 0) atomicMax(a.maxs, smax);
     if (light) atomicAdd(a.light, light);
   }
@@ -1104,6 +1167,7 @@ struct RowsArgs {
   u64* colnand;
 };
 
+constexpr int ROWS_UNROLL = 4;
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
@@ -1134,7 +1198,50 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
     __syncthreads();
     const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
     const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
-    if (a.alist) {
+    if (a.alist && s1 - s0 <= NT) {
+      // the allowed-pod lists of S(c) as one flat range: a segment table
+      // (start, prefix) in LDS, then every thread streams entries with
+      // ROWS_UNROLL loads in flight -- no per-policy round trips
+      __shared__ i64 seg_start[NT];
+      __shared__ i64 seg_pre[NT + 1];
+      __shared__ i64 sm_scan[NT / 64];
+      const int ns = (int)(s1 - s0);
+      i64 len = 0, st = 0;
+      if ((int)threadIdx.x < ns) {
+        const int32_t p = a.slist[s0 + threadIdx.x];
+        st = a.aloff[p];
+        len = a.aloff[p + 1] - st;
+      }
+      i64 total;
+      const i64 pre = block_excl_scan_nw<NT / 64>(len, sm_scan, total);
+      if ((int)threadIdx.x < ns) {
+        seg_start[threadIdx.x] = st;
+        seg_pre[threadIdx.x] = pre;
+      }
+      if (threadIdx.x == 0) seg_pre[ns] = total;
+      __syncthreads();
+      for (i64 i0 = threadIdx.x; i0 < total; i0 += (i64)NT * ROWS_UNROLL) {
+        int32_t jv[ROWS_UNROLL];
+#pragma unroll
+        for (int u = 0; u < ROWS_UNROLL; ++u) {
+          const i64 id = i0 + (i64)u * NT;
+          jv[u] = -1;
+          if (id < total) {
+            int lo = 0, hi = ns - 1;   // last segment with seg_pre <= id
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (seg_pre[mid] <= id) lo = mid; else hi = mid - 1;
+            }
+            jv[u] = a.alist[seg_start[lo] + (id - seg_pre[lo])];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < ROWS_UNROLL; ++u) {
+          const int32_t j = jv[u];
+          if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+        }
+      }
+    } else if (a.alist) {
       // the flat allowed-pod list of each policy of S(c), across all threads
       for (i64 e = s0; e < s1; ++e) {
         const int32_t p = a.slist[e];

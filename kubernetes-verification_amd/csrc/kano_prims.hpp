@@ -27,6 +27,24 @@ __device__ __forceinline__ T wave_incl_scan(T x) {
 }
 
 // Exclusive scan over a 256-thread block; smem holds >= 4 elements.
+// the same for a block of NW waves (smem: NW entries)
+template <int NW, typename T>
+__device__ __forceinline__ T block_excl_scan_nw(T v, T* smem, T& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T inc = wave_incl_scan(v);
+  if (lane == 63) smem[wid] = inc;
+  __syncthreads();
+  T pre = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wid) pre += smem[w];
+    total += smem[w];
+  }
+  __syncthreads();
+  return pre + inc - v;
+}
+
 template <typename T>
 __device__ __forceinline__ T block_excl_scan(T v, T* smem, T& total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;

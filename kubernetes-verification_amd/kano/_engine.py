@@ -18,7 +18,9 @@ from ._intern import Tables
 
 
 def _ptr(a: Optional[np.ndarray]):
-    return None if a is None else a.ctypes.data_as(c_void_p)
+    # the address as an int: the argtypes are c_void_p, and ctypes converts
+    # an int much faster than numpy's data_as builds a pointer object
+    return None if a is None else a.ctypes.data
 
 
 class PinnedBuffer:
@@ -65,6 +67,7 @@ class DeviceBuild:
                 f"kano_create(device={device}) failed (rc={rc}): no usable HIP device")
         self.device = device
         self.path = path
+        self._counts = None
         if stream is not None:
             self._chk(self.lib.kano_set_stream(self.ctx, c_void_p(stream)), "kano_set_stream")
         self.tables = None
@@ -253,14 +256,18 @@ class DeviceBuild:
                 gid = np.ascontiguousarray(gid, dtype=np.int32)
             if gid.shape[0] != n:
                 raise ValueError("gid must have one entry per pod")
-        counts = np.zeros(4, dtype=np.int64)
-        cnt = c_int64(0)
+        if self._counts is None:   # reused result slots (no per-call allocation)
+            self._counts = np.zeros(4, dtype=np.int64)
+            self._cnt = c_int64(0)
+            self._cnt_ref = byref(self._cnt)
+        counts, cnt = self._counts, self._cnt
         cap = 0 if pairs is None else pairs.size // 2
         pth = nat.PATHS[path or self.path]
-        self._chk(self.lib.kano_verify(
-            self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), _ptr(idx), _ptr(counts),
-            _ptr(pairs),
-            int(cap), byref(cnt) if shadow else None), "kano_verify")
+        rc = self.lib.kano_verify(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), _ptr(idx),
+                                  counts.ctypes.data, _ptr(pairs), int(cap),
+                                  self._cnt_ref if shadow else None)
+        if rc != 0:
+            self._chk(rc, "kano_verify")
         out, o = {}, 0
         for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
                                   "system_isolation")):
