@@ -815,15 +815,14 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   // light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
-  // entries, cache-resident).  Measured: the flat lists win when they stay
-  // on-die (C3: 6 MB, k_rows -10% at one rank; at 1/8 of the rows, where the
-  // rows' build is exposed, k_rows 99 -> 49 us with the flattened walk) ;
-  // past the Infinity Cache the member lists win (C5: 450 MB of lists,
-  // k_rows -10%; C4: 500 MB)
+  // entries, cache-resident).  With the flattened walk in k_rows the flat
+  // lists win wherever the light rows read them at all (measured: C3 at 1/8
+  // of the rows k_rows 99 -> 49 us; C5 21.8 -> 20.9 ms); where nearly every
+  // class is heavy (C4) building them is pure cost (+0.45 ms a step)
   ctx->alist_valid = false;
   int ua = ctx->rows_alist;
   if (ua < 0)
-    ua = ctx->nnz_alw * 4 <= (64ll << 20) ? 1 : 0;
+    ua = ctx->light_cost * 2 > ctx->nnz_alw && ctx->nnz_alw * 4 <= (1ll << 30) ? 1 : 0;
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx));
   if (U == 0) return 0;

@@ -1168,6 +1168,10 @@ struct RowsArgs {
 };
 
 constexpr int ROWS_UNROLL = 4;
+// segments (policies of S(c)) of the flattened walk: a fixed small table, so
+// that the static LDS does not cost the wide (NT = 1024, 64 KB row) blocks
+// their second slot per CU
+constexpr int ROWS_SEG = 256;
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
@@ -1198,16 +1202,16 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
     __syncthreads();
     const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
     const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
-    if (a.alist && s1 - s0 <= NT) {
+    if (a.alist && s1 - s0 <= ROWS_SEG) {
       // the allowed-pod lists of S(c) as one flat range: a segment table
       // (start, prefix) in LDS, then every thread streams entries with
       // ROWS_UNROLL loads in flight -- no per-policy round trips
-      __shared__ i64 seg_start[NT];
-      __shared__ i64 seg_pre[NT + 1];
+      __shared__ i64 seg_start[ROWS_SEG];
+      __shared__ i64 seg_pre[ROWS_SEG + 1];
       __shared__ i64 sm_scan[NT / 64];
       const int ns = (int)(s1 - s0);
       i64 len = 0, st = 0;
-      if ((int)threadIdx.x < ns) {
+      if ((int)threadIdx.x < ns) {   // ns <= ROWS_SEG <= NT
         const int32_t p = a.slist[s0 + threadIdx.x];
         st = a.aloff[p];
         len = a.aloff[p + 1] - st;
