@@ -791,18 +791,13 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                          P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
                          P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls));
       KLAUNCH();
-      hipLaunchKernelGGL(k_sort_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                         P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist));
-      KLAUNCH();
-      if (ctx->max_sel > SORT_WAVE_MAX) {
-        const size_t lds = sizeof(u64) * (size_t)((P + 63) / 64);
-        hipLaunchKernelGGL(k_sort_lists_big, dim3((unsigned)U), dim3(TPB), lds, ctx->stream,
-                           P_<i64>(ctx->soffc), P, P_<int32_t>(ctx->slist));
-        KLAUNCH();
-      }
     }
-    hipLaunchKernelGGL(k_flag_list, dim3(nblk(U)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), U, P_<int32_t>(ctx->hlist),
+    // S(c) sorted, heavy list and work-item map in one launch
+    const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
+                           ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
+    hipLaunchKernelGGL(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream,
+                       P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), P > 0 ? 1 : 0,
+                       P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), P_<int32_t>(ctx->hlist),
                        P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls));
     KLAUNCH();
   }
@@ -2106,13 +2101,8 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     ctx->cols_deferred = false;
     KTRY(mc_cols(ctx));
   }
-  // per-pod pair counts; their scan joins verify_back's batch
-  if (want_shadow && sp.rl > 0) {
-    hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(sp.rl)), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
-                       P_<i64>(ctx->tp));
-    KLAUNCH();
-  }
+  // (policy_shadow's per-pod pair counts come out of k_verify_cols below;
+  // their scan joins verify_back's batch)
   // the column tail in one pass (k_verify_cols)
   const i64 nb = std::max<i64>(1, nblk(W * 64));
   KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
@@ -2151,6 +2141,13 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     }
     fa.icnt = P_<i64>(ctx->icnt);
     fa.words = words_dev;
+    if (want_shadow && sp.rl > 0) {
+      fa.rcls = P_<int32_t>(ctx->rc.cls);
+      fa.loff = P_<i64>(ctx->loff);
+      fa.tp = P_<i64>(ctx->tp);
+      fa.r0 = ctx->r0;
+      fa.r1 = ctx->r1;
+    }
     hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
     KLAUNCH();
   } else {

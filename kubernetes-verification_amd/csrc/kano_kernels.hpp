@@ -508,6 +508,58 @@ __global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soff
   if (lane < s) L[r] = v;
 }
 
+// One wave per class, three jobs in one launch: the class's entry in the
+// heavy list, its k_rows work items' owner map (k_flag_list), and S(c)
+// sorted ascending (with sort != 0): a rank sort in registers for s <= 64,
+// else the wave's own LDS bitmap of all P policies (dynamic LDS: WPB x
+// ceil(P/64) words, passed only when some list is longer than 64).
+__global__ __launch_bounds__(TPB) void k_class_lists(const i64* __restrict__ soffc, i64 U, i64 P,
+                                                     int32_t* __restrict__ slist, int sort,
+                                                     const int32_t* __restrict__ hflag,
+                                                     const int32_t* __restrict__ hoff,
+                                                     int32_t* __restrict__ hlist,
+                                                     const int32_t* __restrict__ wioff,
+                                                     int32_t* __restrict__ wicls) {
+  extern __shared__ __attribute__((aligned(16))) u64 lds_bm[];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const i64 c = (i64)blockIdx.x * (TPB / 64) + wid;
+  if (c >= U) return;                       // wave-uniform; waves never meet at a barrier
+  if (lane == 0 && hflag[c]) hlist[hoff[c]] = (int32_t)c;
+  for (int32_t w = wioff[c] + lane; w < wioff[c + 1]; w += 64) wicls[w] = (int32_t)c;
+  if (!sort) return;
+  const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
+  if (s <= 1) return;
+  int32_t* L = slist + s0;
+  if (s <= SORT_WAVE_MAX) {
+    const int32_t v = lane < s ? L[lane] : 0x7fffffff;
+    int r = 0;
+    for (int k = 0; k < s; ++k) r += __shfl(v, k, 64) < v;
+    if (lane < s) L[r] = v;
+    return;
+  }
+  const i64 PW = (P + 63) / 64;
+  u64* bm = lds_bm + (i64)wid * PW;
+  for (i64 w = lane; w < PW; w += 64) bm[w] = 0ull;
+  __builtin_amdgcn_wave_barrier();
+  for (i64 k = lane; k < s; k += 64) {
+    const int32_t v = L[k];
+    atomicOr(&bm[v >> 6], 1ull << (v & 63));
+  }
+  __builtin_amdgcn_wave_barrier();
+  i64 base = 0;
+  for (i64 w0 = 0; w0 < PW; w0 += 64) {
+    const i64 w = w0 + lane;
+    u64 v = w < PW ? bm[w] : 0ull;
+    i64 tot;
+    i64 pos = base + wave_excl_scan((i64)__popcll(v), tot);
+    while (v) {
+      L[pos++] = (int32_t)(w * 64 + __builtin_ctzll(v));
+      v &= v - 1;
+    }
+    base += tot;
+  }
+}
+
 // block per class with s > SORT_WAVE_MAX: bitmap of all P policies in LDS
 __global__ __launch_bounds__(TPB) void k_sort_lists_big(const i64* __restrict__ soffc, i64 P,
                                                         int32_t* __restrict__ slist) {
@@ -1699,6 +1751,12 @@ struct FinishArgs {
   u64* sysrow;
   i64* icnt;             // [r * nb + b], r: reachable, isolated, cross, sys-isolated
   u64* words;            // nullable: this shard's [OR | cross | NAND] words (3 W) for the gather
+  // policy_shadow's per-pod pair counts (k_shadow_podcount folded in):
+  // tp[i - r0] = loff[c + 1] - loff[c] for the shard's pods (tp nullable)
+  const int32_t* rcls;
+  const i64* loff;
+  i64* tp;
+  i64 r0, r1;
 };
 
 __device__ __forceinline__ bool mc_bit(const u64* row, int32_t ca) {
@@ -1709,6 +1767,10 @@ __global__ __launch_bounds__(TPB) void k_verify_cols(FinishArgs a) {
   __shared__ i64 sm[4];
   const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;   // grid covers W * 64
   const bool live = j < a.n;
+  if (a.tp && j >= a.r0 && j < a.r1) {
+    const int32_t c = a.rcls[j];
+    a.tp[j - a.r0] = a.loff[c + 1] - a.loff[c];
+  }
   const int32_t ca = live ? a.cla[j] : 0;
   const bool orb = live && mc_bit(a.col_or_c, ca);
   const bool nab = live && mc_bit(a.col_nand_c, ca);

@@ -188,22 +188,32 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
   }
   i64 tot;
   i64 pre = block_excl_scan(s, sm, tot);
-  if (threadIdx.x == 0) {
+  // look-back by wave 0: its 64 lanes read 64 predecessor states at once and
+  // sum back to the nearest inclusive prefix, so a tile waits only for its
+  // predecessors' aggregates, never for a chain of prefixes
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
     u64* ts = st + 1;
     i64 excl = 0;
     if (tile == 0) {
-      lb_store(&ts[0], LB_INC | ((u64)tot & LB_VAL));
+      if (lane == 0) lb_store(&ts[0], LB_INC | ((u64)tot & LB_VAL));
     } else {
-      lb_store(&ts[tile], LB_AGG | ((u64)tot & LB_VAL));
-      for (i64 q = tile - 1;; --q) {
-        u64 w;
-        do { w = lb_load(&ts[q]); } while (w == 0);
-        excl += (i64)(w & LB_VAL);
-        if ((w & ~LB_VAL) == LB_INC) break;
+      if (lane == 0) lb_store(&ts[tile], LB_AGG | ((u64)tot & LB_VAL));
+      for (i64 q0 = tile - 1;; q0 -= 64) {
+        const i64 q = q0 - lane;
+        u64 w = LB_INC;                  // before tile 0: an inclusive zero
+        if (q >= 0) {
+          do { w = lb_load(&ts[q]); } while (w == 0);
+        }
+        const u64 inc = __ballot((w & ~LB_VAL) == LB_INC);
+        const int f = inc ? __ffsll((long long)inc) - 1 : 63;
+        const i64 part = wave_sum(lane <= f ? (i64)(w & LB_VAL) : (i64)0);
+        excl += part;
+        if (inc) break;
       }
-      lb_store(&ts[tile], LB_INC | ((u64)(excl + tot) & LB_VAL));
+      if (lane == 0) lb_store(&ts[tile], LB_INC | ((u64)(excl + tot) & LB_VAL));
     }
-    s_prefix = excl;
+    if (lane == 0) s_prefix = excl;
   }
   __syncthreads();
   pre += s_prefix;
