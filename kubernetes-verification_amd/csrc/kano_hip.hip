@@ -253,8 +253,21 @@ struct ScanBatch {
     j.st = slots;
     j.in64 = sizeof(Tin) == 8;
     j.out64 = sizeof(Tout) == 8;
+    j.gen = 0;
     slots += 1 + scan_tiles(n);
     maxt = std::max<i64>(maxt, scan_tiles(n));
+    return 0;
+  }
+  // class-id scan over the representative flags of pods [m0, m0 + n), the
+  // flags generated inside the scan (no flag pass)
+  int add_rep_flags(const int32_t* smin, const int32_t* slot_of, i64 m0, i64 n, int32_t* out,
+                    int total_slot) {
+    KTRY(add(static_cast<const int32_t*>(nullptr), n, out, total_slot));
+    ScanJob& j = jobs.j[jobs.count - 1];
+    j.gen = 1;
+    j.gsmin = smin;
+    j.gslot = slot_of;
+    j.gm0 = m0;
     return 0;
   }
   int run() {
@@ -419,12 +432,13 @@ int classify_phase1(kano_ctx* ctx) {
     hipLaunchKernelGGL(k_cls_insert, dim3(nblk(most), 2), dim3(TPB), 0, ctx->stream,
                        P_<int32_t>(ctx->pv), n, pr);
     KLAUNCH();
-    hipLaunchKernelGGL(k_cls_flag, dim3(nblk(most), 2), dim3(TPB), 0, ctx->stream, pr);
-    KLAUNCH();
   }
+  // class ids: a scan over the representative flags (generated in the scan)
   ScanBatch sb(ctx);
-  KTRY(sb.add(P_<int32_t>(ctx->rc.flag), nr, P_<int32_t>(ctx->rc.cid), SZ_UR));
-  KTRY(sb.add(P_<int32_t>(ctx->cc.flag), na, P_<int32_t>(ctx->cc.cid), SZ_UA));
+  KTRY(sb.add_rep_flags(P_<int32_t>(ctx->rc.smin), P_<int32_t>(ctx->rc.slot_of), ctx->rc.m0, nr,
+                        P_<int32_t>(ctx->rc.cid), SZ_UR));
+  KTRY(sb.add_rep_flags(P_<int32_t>(ctx->cc.smin), P_<int32_t>(ctx->cc.slot_of), ctx->cc.m0, na,
+                        P_<int32_t>(ctx->cc.cid), SZ_UA));
   return sb.run();
 }
 
@@ -439,10 +453,8 @@ int classify_phase2a(kano_ctx* ctx) {
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   const i64 mr = ctx->rc.m1 - ctx->rc.m0, ma = ctx->cc.m1 - ctx->cc.m0;
   const i64 rl = std::max(mr, ma);
-  if (rl > 0) {
-    hipLaunchKernelGGL(k_cls_assign, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
-    KLAUNCH();
-    hipLaunchKernelGGL(k_cls_mcount, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
+  if (rl > 0) {   // ids and member counts in one pass
+    hipLaunchKernelGGL(k_cls_assign_count, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
   }
   ScanBatch sb(ctx);
@@ -535,8 +547,6 @@ int match_both(kano_ctx* ctx) {
   const unsigned rows_f = (a0.live ? a0.NM + 1 : 0) + (a1.live ? a1.NM + 1 : 0);
   if (rows_i > 0) {
     hipLaunchKernelGGL(k_join_insert, dim3(nblk(maxU), rows_i), dim3(TPB), 0, ctx->stream, pr);
-    KLAUNCH();
-    hipLaunchKernelGGL(k_join_count, dim3(nblk(maxU), rows_i), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
     ScanBatch sb(ctx);
     for (int q = 0; q < 2; ++q) {
@@ -639,20 +649,16 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(classify_phase2b(ctx));
   KTRY(match_both(ctx));
   KTRY(stage_mark(ctx, 2, ctx->stream));
-  // allow side: allowed classes / pods per policy
+  // allowed classes / pods per policy, then |S(c)| and the rebuild cost
+  // (one wave per policy, both sides)
   if (P > 0) {
-    hipLaunchKernelGGL(k_pol_allow_count, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
+    const bool sel = Ur > 0;
+    hipLaunchKernelGGL(k_pol_counts, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                        P_<int32_t>(ctx->am.gmem), P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca),
-                       P_<int32_t>(ctx->acnt));
-    KLAUNCH();
-  }
-  // select side: |S(c)|, rebuild cost, the per-class plan
-  if (P > 0 && Ur > 0) {
-    hipLaunchKernelGGL(k_sel_count, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
-                       P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
-                       P_<int32_t>(ctx->sm.gmem), P_<int32_t>(ctx->acnt), P_<int32_t>(ctx->scnt),
-                       P_<unsigned long long>(ctx->cost));
+                       P_<int32_t>(ctx->acnt), P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                       sel ? P_<int32_t>(ctx->sm.gmem) : (const int32_t*)nullptr,
+                       P_<int32_t>(ctx->scnt), P_<unsigned long long>(ctx->cost));
     KLAUNCH();
   }
   if (Ur > 0) {

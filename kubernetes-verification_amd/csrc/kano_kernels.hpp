@@ -103,6 +103,22 @@ __global__ __launch_bounds__(TPB) void k_cls_assign(ClsPair pr) {
   if (r == (int32_t)i) a.rep[c] = (int32_t)i;
 }
 
+// k_cls_assign and k_cls_mcount in one pass: the class id of every pod of
+// [m0, m1), the representatives, the member counts
+__global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
+  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
+  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
+  const bool act = i < a.m1;
+  int32_t c = 0;
+  if (act) {
+    const int32_t r = a.smin[a.slot_of[i]];
+    c = a.cid[r - a.m0];
+    a.cls[i] = c;
+    if (r == (int32_t)i) a.rep[c] = (int32_t)i;
+  }
+  (void)wave_agg_inc(a.mcnt, c, act);
+}
+
 // member counts of the pods [m0, m1) of each side
 __global__ __launch_bounds__(TPB) void k_cls_mcount(ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
@@ -315,32 +331,38 @@ __device__ __forceinline__ int join_row(const JoinPair& pr, int y, int extra, in
 }
 
 // group id of class c under mask m = its table slot
+// group id of class c under mask m = its table slot; the group sizes are
+// counted in the same pass (k_join_count folded in)
 __global__ __launch_bounds__(TPB) void k_join_insert(JoinPair pr) {
   int m;
   const JoinSide a = join_row(pr, blockIdx.y, 0, &m) ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c >= a.U) return;
-  const int32_t* sl = a.mslot + a.moff[m];
-  const int ns = a.moff[m + 1] - a.moff[m];
-  int32_t* tab = a.table + (i64)m * a.T;
-  const uint32_t tm = (uint32_t)(a.T - 1);
-  uint32_t s = proj_hash(a.cval, a.U, c, sl, ns) & tm;
-  for (;;) {
-    int32_t cur = tab[s];   // plain read: see k_cls_insert
-    if (cur < 0) {
-      const int32_t prev = atomicCAS(&tab[s], -1, (int32_t)c);
-      if (prev < 0) break;
-      cur = prev;
+  const bool act = c < a.U;
+  uint32_t s = 0;
+  if (act) {
+    const int32_t* sl = a.mslot + a.moff[m];
+    const int ns = a.moff[m + 1] - a.moff[m];
+    int32_t* tab = a.table + (i64)m * a.T;
+    const uint32_t tm = (uint32_t)(a.T - 1);
+    s = proj_hash(a.cval, a.U, c, sl, ns) & tm;
+    for (;;) {
+      int32_t cur = tab[s];   // plain read: see k_cls_insert
+      if (cur < 0) {
+        const int32_t prev = atomicCAS(&tab[s], -1, (int32_t)c);
+        if (prev < 0) break;
+        cur = prev;
+      }
+      bool eq = true;
+      for (int k = 0; k < ns; ++k) {
+        const int32_t* col = a.cval + (i64)sl[k] * a.U;
+        if (col[cur] != col[c]) { eq = false; break; }
+      }
+      if (eq) break;
+      s = (s + 1) & tm;
     }
-    bool eq = true;
-    for (int k = 0; k < ns; ++k) {
-      const int32_t* col = a.cval + (i64)sl[k] * a.U;
-      if (col[cur] != col[c]) { eq = false; break; }
-    }
-    if (eq) break;
-    s = (s + 1) & tm;
+    a.pslot[(i64)m * a.U + c] = (int32_t)s;
   }
-  a.pslot[(i64)m * a.U + c] = (int32_t)s;
+  (void)wave_agg_inc(a.gcnt, act ? (i64)m * a.T + s : 0, act);
 }
 
 __global__ __launch_bounds__(TPB) void k_join_count(JoinPair pr) {
@@ -592,6 +614,42 @@ __global__ __launch_bounds__(TPB) void k_sort_lists_big(const i64* __restrict__ 
 }
 
 // ---- allow side: per policy the allowed column classes and pods -----------
+// k_pol_allow_count and k_sel_count in one pass: policy p's allowed classes
+// and pods (allow-side group), then its selected classes' |S(c)| and rebuild
+// cost (select-side group), the pod count passed in registers
+__global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict__ apstart,
+                                                    const int32_t* __restrict__ aplen,
+                                                    const int32_t* __restrict__ apcls,
+                                                    const int32_t* __restrict__ csize,
+                                                    int32_t* __restrict__ nca,
+                                                    int32_t* __restrict__ acnt,
+                                                    const i64* __restrict__ spstart,
+                                                    const int32_t* __restrict__ splen,
+                                                    const int32_t* __restrict__ spcls,
+                                                    int32_t* scnt, unsigned long long* cost) {
+  const i64 p = wave_policy();
+  if (p >= P) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t* L = apcls + apstart[p];
+  const int32_t len = aplen[p];
+  i64 pods = 0;
+  for (int32_t k = lane; k < len; k += 64) pods += csize[L[k]];
+  pods = wave_sum(pods);
+  if (lane == 0) {
+    nca[p] = len;
+    acnt[p] = (int32_t)pods;
+  }
+  if (!spcls) return;
+  const int32_t* S = spcls + spstart[p];
+  const int32_t slen = splen[p];
+  const unsigned long long a = (unsigned long long)(int32_t)pods;
+  for (int32_t k = lane; k < slen; k += 64) {
+    const int32_t c = S[k];
+    atomicAdd(&scnt[c], 1);
+    if (a) atomicAdd(&cost[c], a);
+  }
+}
+
 __global__ __launch_bounds__(TPB) void k_pol_allow_count(i64 P, const i64* __restrict__ pstart,
                                                          const int32_t* __restrict__ plen,
                                                          const int32_t* __restrict__ pcls,

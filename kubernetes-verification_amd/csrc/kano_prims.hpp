@@ -141,6 +141,13 @@ struct ScanJob {
   i64 n;
   i64 st;
   int in64, out64;
+  // generated input instead of `in` (gen = 1): element x is 1 iff pod
+  // m0 + x is the smallest member of its hash slot (a class representative),
+  // smin[slot_of[m0 + x]] == m0 + x
+  int gen;
+  const int32_t* gsmin;
+  const int32_t* gslot;
+  i64 gm0;
 };
 constexpr int MAX_SCAN_JOBS = 8;
 struct ScanJobs {
@@ -181,9 +188,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const i64 x = base + k;
-    v[k] = x < jb.n ? (jb.in64 ? static_cast<const i64*>(jb.in)[x]
-                               : (i64) static_cast<const int32_t*>(jb.in)[x])
-                    : 0;
+    if (x >= jb.n) v[k] = 0;
+    else if (jb.gen) v[k] = jb.gsmin[jb.gslot[jb.gm0 + x]] == (int32_t)(jb.gm0 + x) ? 1 : 0;
+    else v[k] = jb.in64 ? static_cast<const i64*>(jb.in)[x]
+                        : (i64) static_cast<const int32_t*>(jb.in)[x];
     s += v[k];
   }
   i64 tot;
