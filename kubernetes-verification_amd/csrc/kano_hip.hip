@@ -55,6 +55,7 @@ struct DBuf {
 struct ClassSet {
   std::vector<int32_t> keys;     // pod_val columns hashed
   int KS = 0;
+  int packed = 0;                // the key tuple fits one u64 (bits per key: keys_d[KS..2KS))
   i64 U = 0;
   i64 m0 = 0, m1 = 0;            // pods whose membership is listed
   DBuf keys_d, table, smin, slot_of, flag, cid, cls, rep, mcnt, mcur, moff, mem, cval;
@@ -87,6 +88,7 @@ struct kano_ctx {
 
   i64 n = 0, W = 0, ldM = 0, P = 0, PB = 0;
   int ncols = 0;
+  std::vector<int32_t> colbits;  // bits of (value id + 1) per pod_val column
   i64 r0 = 0, r1 = -1;
   bool have_pods = false, have_pols = false, built = false;
   bool lists_mode = false;   // kano_shadow_lists context: no matrix
@@ -112,6 +114,7 @@ struct kano_ctx {
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
+  int cls_packed = 1;        // packed-key classification where the tuple fits 63 bits
   int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
                              // (measured C3: 16.9 us vs 24-27 us for the serial walk)
 
@@ -376,13 +379,13 @@ i64 table_size(i64 n) {
 
 int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   const i64 n = ctx->n, T = table_size(n);
-  KTRY(dalloc(ctx, cs.table, sizeof(int32_t) * T));
+  KTRY(dalloc(ctx, cs.table, sizeof(u64) * T));   // int32 pods, or u64 packed keys
   KTRY(dalloc(ctx, cs.smin, sizeof(int32_t) * T));
   KTRY(dalloc(ctx, cs.slot_of, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, cs.flag, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, cs.cid, sizeof(int32_t) * (n + 1)));
   KTRY(dalloc(ctx, cs.cls, sizeof(int32_t) * std::max<i64>(1, n)));
-  KTRY(fb.add(cs.table, sizeof(int32_t) * T, 0xffffffffu));
+  KTRY(fb.add(cs.table, (cs.packed ? sizeof(u64) : sizeof(int32_t)) * T, 0xffffffffu));
   KTRY(fb.add(cs.smin, sizeof(int32_t) * T, 0x7fffffffu));
   // per-class arrays of phase 2a, sized by the side's pods (>= its classes)
   // so that they need not wait for the class count
@@ -401,6 +404,7 @@ ClsSide cls_side(kano_ctx* ctx, ClassSet& cs) {
   ClsSide a{};
   a.keys = P_<int32_t>(cs.keys_d);
   a.KS = cs.KS;
+  a.packed = cs.packed;
   a.tmask = (uint32_t)(table_size(ctx->n) - 1);
   a.table = P_<int32_t>(cs.table);
   a.slot_of = P_<int32_t>(cs.slot_of);
@@ -1304,6 +1308,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "grm") ctx->grange_m = v;
         if (k == "fold") ctx->fold_mode = v;
         if (k == "timing") ctx->stage_timing = v;
+        if (k == "packed") ctx->cls_packed = v;
       }
       pos = end + 1;
     }
@@ -1425,6 +1430,17 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
               ctx->pitch_pad) *
              ctx->pitch_mul;
   ctx->ncols = ncols;
+  // bit width of every column's (value id + 1): key tuples that fit 63 bits
+  // are hashed and compared as one packed word (no gathers of pod values)
+  ctx->colbits.assign(ncols, 1);
+  for (int32_t c = 0; c < ncols; ++c) {
+    int32_t mx = 0;
+    const int32_t* col = pod_val + (i64)c * n;
+    for (i64 i = 0; i < n; ++i) mx = std::max(mx, col[i] + 1);
+    int b = 1;
+    while (b < 31 && (1 << b) <= mx) ++b;
+    ctx->colbits[c] = b;
+  }
   KTRY(dalloc(ctx, ctx->pv, sizeof(int32_t) * std::max<i64>(1, n * ncols)));
   if (n * ncols > 0)
     KCHK(hipMemcpyAsync(ctx->pv.p, pod_val, sizeof(int32_t) * n * ncols, hipMemcpyHostToDevice,
@@ -1458,9 +1474,17 @@ static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t*
       cs.keys.push_back(c);
     }
   cs.KS = (int)cs.keys.size();
-  KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, cs.keys.size())));
+  // keys_d = [columns | bits]; packed when the bits sum to at most 63
+  std::vector<int32_t> kd(cs.keys);
+  int tb = 0;
+  for (int32_t c : cs.keys) {
+    kd.push_back(ctx->colbits[c]);
+    tb += ctx->colbits[c];
+  }
+  cs.packed = (cs.KS > 0 && tb <= 63 && ctx->cls_packed) ? 1 : 0;
+  KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, kd.size())));
   if (cs.KS > 0)   // uploaded once per policy set, not per build
-    KCHK(hipMemcpy(cs.keys_d.p, cs.keys.data(), sizeof(int32_t) * cs.KS, hipMemcpyHostToDevice));
+    KCHK(hipMemcpy(cs.keys_d.p, kd.data(), sizeof(int32_t) * kd.size(), hipMemcpyHostToDevice));
   std::vector<i64> toff(P + 1, 0);
   std::vector<int32_t> tslot, tval, pmask(std::max<i64>(1, P), -1), moff(1, 0), mslot;
   std::vector<std::vector<int32_t>> masks;

@@ -19,8 +19,9 @@ namespace kano {
 // Both sides (row classes on the working-selector keys, column classes on
 // the working-allow keys) run in the same launches: blockIdx.y = side.
 struct ClsSide {
-  const int32_t* keys;
+  const int32_t* keys;   // KS columns, then their bit widths (packed mode)
   int KS;
+  int packed;
   uint32_t tmask;
   int32_t* table;
   int32_t* slot_of;
@@ -45,9 +46,30 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;   // pods [m0, m1) of the side
   if (i >= a.m1) return;
+  uint32_t s;
+  if (a.packed) {
+    // the key tuple as one word, (value + 1) per key: compare words, no
+    // gathers of the occupant's pod values
+    u64 key = 0;
+    for (int k = 0; k < a.KS; ++k)
+      key = (key << a.keys[a.KS + k]) | (u64)(uint32_t)(pv[(i64)a.keys[k] * n + i] + 1);
+    s = hfin(hmix(hmix(0x9747b28cu, (uint32_t)key), (uint32_t)(key >> 32))) & a.tmask;
+    u64* tab = reinterpret_cast<u64*>(a.table);
+    for (;;) {
+      u64 cur = tab[s];   // plain read, as below
+      if (cur == ~0ull) {
+        const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[s]), ~0ull,
+                                   (unsigned long long)key);
+        if (prev == ~0ull) break;
+        cur = prev;
+      }
+      if (cur == key) break;
+      s = (s + 1) & a.tmask;
+    }
+  } else {
   uint32_t h = 0x9747b28cu;
   for (int k = 0; k < a.KS; ++k) h = hmix(h, (uint32_t)pv[(i64)a.keys[k] * n + i]);
-  uint32_t s = hfin(h) & a.tmask;
+  s = hfin(h) & a.tmask;
   // linear probing; the table has >= 2n slots, so this ends.  Slots only
   // go from -1 to a pod id, so a plain (possibly stale) read is safe: a stale
   // -1 just sends us to the CAS, which returns the real occupant.
@@ -65,6 +87,7 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
     }
     if (eq) break;
     s = (s + 1) & a.tmask;
+  }
   }
   a.slot_of[i] = (int32_t)s;
   // smallest member per slot (the class representative); smin only falls.
