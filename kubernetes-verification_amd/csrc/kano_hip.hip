@@ -114,6 +114,7 @@ struct kano_ctx {
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
+  int rows_store = 0;        // k_rows store order (experiments)
   int cls_packed = 1;        // packed-key classification where the tuple fits 63 bits
   int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
                              // (measured C3: 16.9 us vs 24-27 us for the serial walk)
@@ -827,7 +828,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   ctx->alist_valid = false;
   int ua = ctx->rows_alist;
   if (ua < 0)
-    ua = ctx->light_cost * 2 > ctx->nnz_alw && ctx->nnz_alw * 4 <= (1ll << 30) ? 1 : 0;
+    ua = ctx->light_cost * 16 > ctx->nnz_alw && ctx->nnz_alw * 4 <= (2ll << 30) ? 1 : 0;
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx));
   if (U == 0) return 0;
@@ -942,6 +943,7 @@ int launch_rows(kano_ctx* ctx) {
   a.ch = ctx->ch;
   a.cww = cww;
   a.probe = ctx->rows_probe;
+  a.store_mode = ctx->rows_store;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
@@ -1309,6 +1311,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "fold") ctx->fold_mode = v;
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
+        if (k == "store") ctx->rows_store = v;
       }
       pos = end + 1;
     }

@@ -1296,6 +1296,7 @@ struct RowsArgs {
   int ch;
   int cww;
   int probe;             // experiments: 1 skip the row build, 2 skip the stores
+  int store_mode;        // experiments: 0 row-major stores, 1 word-major, 2 nontemporal
   u64* color;
   u64* colnand;
 };
@@ -1410,11 +1411,27 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
     }
     __syncthreads();
   }
-  for (int32_t m = m0; m < m1 && a.probe != 2; ++m) {
-    if (heavy && m == m_begin) continue;
-    u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
-    for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-      *(u64x2*)&dst[w] = *(const u64x2*)&row[w];   // (nt stores measured slower)
+  if (a.store_mode == 1 && a.probe != 2) {
+    // word-major: each thread's words go to every member row before the
+    // next words (all member rows' streams open at once)
+    const int32_t mfirst = heavy && m0 == m_begin ? m0 + 1 : m0;
+    for (int w = threadIdx.x * 2; w < nw; w += NT * 2) {
+      const u64x2 v = *(const u64x2*)&row[w];
+      for (int32_t m = mfirst; m < m1; ++m)
+        *(u64x2*)&a.M[(i64)(a.mem[m] - a.r0) * ldw + base + w] = v;
+    }
+  } else {
+    for (int32_t m = m0; m < m1 && a.probe != 2; ++m) {
+      if (heavy && m == m_begin) continue;
+      u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
+      if (a.store_mode == 2) {
+        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+          __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
+      } else {
+        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+          *(u64x2*)&dst[w] = *(const u64x2*)&row[w];
+      }
+    }
   }
   if (a.probe == 2 && threadIdx.x == 0 && row[0] == 0x5eed5eed5eed5eedull) a.M[0] = 1;
   if (chunk == 0 && a.color) {
