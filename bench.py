@@ -354,9 +354,10 @@ def pmc_traffic(config):
     try:
         with open(path) as f:
             d = json.load(f)
-        k = d["kernels"]["kano::k_rows"]
+        # the kernel's name as rocprofv3 prints it ("void kano::k_rows<256>")
+        k = next(v for name, v in d["kernels"].items() if "kano::k_rows" in name)
         return float(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
-    except (OSError, KeyError, ValueError, TypeError):
+    except (OSError, KeyError, ValueError, TypeError, StopIteration):
         return None, None
 
 
