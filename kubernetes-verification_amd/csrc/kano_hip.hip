@@ -36,6 +36,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <chrono>
+#include <cstdio>
 
 #include "kano_hip.h"
 #include "kano_kernels.hpp"
@@ -115,6 +117,19 @@ struct kano_ctx {
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
   int rows_store = 0;        // k_rows store order (experiments)
+  // kano_verify: policy_shadow's subset tests on stream2 beside the Mc
+  // chain (set by verify_front around the build; called once the lists and
+  // AC exist), joined through ev_join2 before the shadow scans
+  int fork_checks = 1;
+  std::function<int()> fork_hook;
+  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
+  bool fork_pending = false;
+  // host-time breakdown of kano_verify (KANO_TUNE=hosttime=1), printed at
+  // kano_destroy: [calls, gap since the previous return, front, back, waits]
+  int host_timing = 0;
+  double ht[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // + [5..7] the three size waits apart
+  int ht_wait = 0;
+  std::chrono::steady_clock::time_point ht_last{};
   int cls_packed = 1;        // packed-key classification where the tuple fits 63 bits
   int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
                              // (measured C3: 16.9 us vs 24-27 us for the serial walk)
@@ -356,7 +371,14 @@ int slots_begin(kano_ctx* ctx, int first, int count) {
 }
 
 int slots_wait(kano_ctx* ctx, int count, i64* out) {
+  const auto t0 = std::chrono::steady_clock::now();
   KCHK(hipEventSynchronize(ctx->ev_sizes));
+  if (ctx->host_timing) {
+    const double w =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    ctx->ht[4] += w;
+    ctx->ht[5 + std::min(ctx->ht_wait++, 2)] += w;
+  }
   for (int k = 0; k < count; ++k) out[k] = (i64)ctx->ghost[k];
   return 0;
 }
@@ -819,6 +841,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                        P_<u64>(ctx->AC), ctx->ldC);
     KLAUNCH();
   }
+  if (ctx->fork_hook) KTRY(ctx->fork_hook());   // lists and AC are complete here
   // light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
   // entries, cache-resident).  With the flattened walk in k_rows the flat
@@ -1312,6 +1335,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
         if (k == "store") ctx->rows_store = v;
+        if (k == "hosttime") ctx->host_timing = v;
+        if (k == "fork") ctx->fork_checks = v;
       }
       pos = end + 1;
     }
@@ -1342,7 +1367,9 @@ int kano_create(int device, kano_ctx** out) {
                 : hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking)) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess) {
     kano_destroy(ctx);
     return -EIO;
   }
@@ -1357,6 +1384,13 @@ int kano_create(int device, kano_ctx** out) {
 
 void kano_destroy(kano_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->host_timing && ctx->ht[0] > 1)
+    fprintf(stderr,
+            "kano host us/verify: gap %.1f front %.1f back %.1f (waits %.1f = %.1f + %.1f + %.1f) "
+            "over %.0f calls\n",
+            ctx->ht[1] / (ctx->ht[0] - 1), ctx->ht[2] / ctx->ht[0], ctx->ht[3] / ctx->ht[0],
+            ctx->ht[4] / ctx->ht[0], ctx->ht[5] / ctx->ht[0], ctx->ht[6] / ctx->ht[0],
+            ctx->ht[7] / ctx->ht[0], ctx->ht[0]);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
@@ -1396,6 +1430,8 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
   if (ctx->ev_sizes) (void)hipEventDestroy(ctx->ev_sizes);
+  if (ctx->ev_fork2) (void)hipEventDestroy(ctx->ev_fork2);
+  if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
   delete ctx;
 }
 
@@ -1888,8 +1924,8 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
 }
 
 // subset tests; the list-offset scans go to sb
-int shadow_stage_a(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
-  KTRY(stage_mark(ctx, 5, ctx->stream));
+int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
+  KTRY(stage_mark(ctx, 5, st));
   if (sp.nt > 0) {
     ShadowArgs a;
     a.U = sp.U;
@@ -1905,16 +1941,25 @@ int shadow_stage_a(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
     a.flags = P_<uint8_t>(ctx->flags);
     a.T = P_<i64>(ctx->T);
     if (ctx->sh_items == 1)
-      hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)(sp.nt * SH_ITEMS)), dim3(TPB), 0,
-                         ctx->stream, a, sp.nf, P_<i64>(ctx->tcnt));
-    else
-      hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, ctx->stream, a,
+      hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)(sp.nt * SH_ITEMS)), dim3(TPB), 0, st, a,
                          sp.nf, P_<i64>(ctx->tcnt));
+    else
+      hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, st, a, sp.nf,
+                         P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
+  return 0;
+}
+
+int shadow_stage_a_scans(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
   KTRY(sb.add(P_<i64>(ctx->tcnt), sp.nt, P_<i64>(ctx->toff), SZ_NL));
   KTRY(sb.add(P_<i64>(ctx->T), sp.U, P_<i64>(ctx->loff)));
   return 0;
+}
+
+int shadow_stage_a(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
+  KTRY(shadow_test_launch(ctx, sp, ctx->stream));
+  return shadow_stage_a_scans(ctx, sp, sb);
 }
 
 // pairs per pod; the per-pod offset scan goes to sb
@@ -2115,7 +2160,22 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     return want_shadow ? shadow_prepare(ctx, sp, fb) : 0;
   };
   ctx->vs_open = false;
-  KTRY(build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run));
+  // policy_shadow's subset tests need only the lists and AC: they run on
+  // stream2 beside the Mc chain (scatter, fold) and the flat-list build
+  ctx->fork_pending = false;
+  if (want_shadow && ctx->fork_checks) {
+    ctx->fork_hook = [&]() -> int {
+      KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));
+      KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
+      KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
+      KCHK(hipEventRecord(ctx->ev_join2, ctx->stream2));
+      ctx->fork_pending = true;
+      return 0;
+    };
+  }
+  const int brc = build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run);
+  ctx->fork_hook = nullptr;
+  KTRY(brc);
   // the matrix write needs only the lists: with rows_early it starts here on
   // stream2, beside the class-level checks
   const bool early = ctx->rows_early && ctx->rows_overlap;
@@ -2123,13 +2183,20 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   const bool cross_on = want_cross && cp.on;
-  // policy_shadow's stage A and its scans, the crosscheck's pass over Mc
+  // the crosscheck's pass over Mc, then policy_shadow's scans (its tests ran
+  // beside the build on stream2, or run here)
+  if (cross_on) KTRY(cross_stage_b2(ctx, cp));
   if (want_shadow) {
     ScanBatch sb(ctx);
-    KTRY(shadow_stage_a(ctx, sp, sb));
+    if (ctx->fork_pending) {
+      KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join2, 0));
+      ctx->fork_pending = false;
+      KTRY(shadow_stage_a_scans(ctx, sp, sb));
+    } else {
+      KTRY(shadow_stage_a(ctx, sp, sb));
+    }
     KTRY(sb.run());
   }
-  if (cross_on) KTRY(cross_stage_b2(ctx, cp));
   if (ctx->cols_deferred) {   // no crosscheck pass ran (empty shard / matrix)
     ctx->cols_deferred = false;
     KTRY(mc_cols(ctx));
@@ -2295,8 +2362,22 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  ctx->ht_wait = 0;
   KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr));
-  return verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count);
+  const auto t1 = clk::now();
+  const int rc = verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count);
+  if (ctx->host_timing) {
+    const auto t2 = clk::now();
+    auto us = [](clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
+    if (ctx->ht[0] > 0) ctx->ht[1] += us(t0 - ctx->ht_last);
+    ctx->ht[0] += 1;
+    ctx->ht[2] += us(t1 - t0);
+    ctx->ht[3] += us(t2 - t1);
+    ctx->ht_last = t2;
+  }
+  return rc;
 }
 
 int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
