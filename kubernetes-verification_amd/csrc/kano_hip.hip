@@ -419,7 +419,6 @@ int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   KTRY(dalloc(ctx, cs.moff, sizeof(int32_t) * (m + 1)));
   KTRY(dalloc(ctx, cs.mem, sizeof(int32_t) * m));
   KTRY(fb.add(cs.mcnt, sizeof(int32_t) * m, 0u));
-  KTRY(fb.add(cs.mcur, sizeof(int32_t) * m, 0u));
   return 0;
 }
 
@@ -527,13 +526,12 @@ int match_alloc(kano_ctx* ctx, SideMatch& sx, ClassSet& cs, FillBatch& fb) {
   KTRY(dalloc(ctx, sx.table, sizeof(int32_t) * NT));
   KTRY(dalloc(ctx, sx.pslot, sizeof(int32_t) * std::max<i64>(1, (i64)NM * U)));
   KTRY(dalloc(ctx, sx.gcnt, sizeof(int32_t) * NT));
-  KTRY(dalloc(ctx, sx.gcur, sizeof(int32_t) * NT));
+  KTRY(dalloc(ctx, sx.gcur, sizeof(int32_t) * std::max<i64>(1, (i64)NM * U)));
   KTRY(dalloc(ctx, sx.goff, sizeof(int32_t) * (NT + 1)));
   KTRY(dalloc(ctx, sx.gmem, sizeof(int32_t) * ((i64)NM * U + U)));
   if (NM > 0) {
     KTRY(fb.add(sx.table, sizeof(int32_t) * NT, 0xffffffffu));
     KTRY(fb.add(sx.gcnt, sizeof(int32_t) * NT, 0u));
-    KTRY(fb.add(sx.gcur, sizeof(int32_t) * NT, 0u));
   }
   return 0;
 }

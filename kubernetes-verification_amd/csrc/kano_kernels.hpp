@@ -31,7 +31,7 @@ struct ClsSide {
   int32_t* cls;
   int32_t* rep;
   int32_t* mcnt;
-  int32_t* mcur;
+  int32_t* mcur;         // rank of pod i among its class's members, [i - m0]
   const int32_t* moff;
   int32_t* mem;
   int32_t* cval;
@@ -139,7 +139,10 @@ __global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
     a.cls[i] = c;
     if (r == (int32_t)i) a.rep[c] = (int32_t)i;
   }
-  (void)wave_agg_inc(a.mcnt, c, act);
+  // the counter's old value + rank in the wave is the pod's place in its
+  // class's member list: k_cls_mfill then scatters without atomics
+  const int32_t r = wave_agg_inc(a.mcnt, c, act);
+  if (act) a.mcur[i - a.m0] = r;
 }
 
 // member counts of the pods [m0, m1) of each side
@@ -150,13 +153,12 @@ __global__ __launch_bounds__(TPB) void k_cls_mcount(ClsPair pr) {
   (void)wave_agg_inc(a.mcnt, act ? a.cls[i] : 0, act);
 }
 
+// member lists: pod i at its rank (from k_cls_assign_count) in its class
 __global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool act = i < a.m1;
-  const int32_t c = act ? a.cls[i] : 0;
-  const int32_t r = wave_agg_inc(a.mcur, c, act);
-  if (act) a.mem[a.moff[c] + r] = (int32_t)i;
+  if (i >= a.m1) return;
+  a.mem[a.moff[a.cls[i]] + a.mcur[i - a.m0]] = (int32_t)i;
 }
 
 // key values of each class's representative, slot-major: cval[k * U + c]
@@ -332,7 +334,7 @@ struct JoinSide {
   int32_t* pslot;        // [m * U + c] = group slot of class c under mask m
   int32_t* gcnt;
   const int32_t* goff;
-  int32_t* gcur;
+  int32_t* gcur;         // [m * U + c] = rank of class c in its group (k_join_insert)
   int32_t* gmem;         // NM * U grouped classes, then the iota block
   const i64* toff;       // policy terms (sorted by slot)
   const int32_t* tval;
@@ -385,7 +387,8 @@ __global__ __launch_bounds__(TPB) void k_join_insert(JoinPair pr) {
     }
     a.pslot[(i64)m * a.U + c] = (int32_t)s;
   }
-  (void)wave_agg_inc(a.gcnt, act ? (i64)m * a.T + s : 0, act);
+  const int32_t r = wave_agg_inc(a.gcnt, act ? (i64)m * a.T + s : 0, act);
+  if (act) a.gcur[(i64)m * a.U + c] = r;   // place in the group (k_join_fill scatters)
 }
 
 __global__ __launch_bounds__(TPB) void k_join_count(JoinPair pr) {
@@ -406,10 +409,9 @@ __global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr) {
     if (c < a.U) a.gmem[(i64)a.NM * a.U + c] = (int32_t)c;
     return;
   }
-  const bool act = c < a.U;
-  const i64 g = act ? (i64)m * a.T + a.pslot[(i64)m * a.U + c] : 0;
-  const int32_t r = wave_agg_inc(a.gcur, g, act);
-  if (act) a.gmem[a.goff[g] + r] = (int32_t)c;
+  if (c >= a.U) return;
+  const i64 g = (i64)m * a.T + a.pslot[(i64)m * a.U + c];
+  a.gmem[a.goff[g] + a.gcur[(i64)m * a.U + c]] = (int32_t)c;
 }
 
 // thread per policy: its matched classes = gmem[pstart, pstart + plen)
