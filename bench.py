@@ -63,6 +63,9 @@ def parse():
                     help="skip policy_shadow (its output is ~1e11 pairs on C4)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU sample")
+    ap.add_argument("--shard-path", action="store_true",
+                    help="diagnostic: the N > 1 step (shard verify + RCCL all-gather + combine) "
+                         "even at one rank, e.g. under torch.distributed.run --nproc-per-node 1")
     ap.add_argument("--rank-of", type=int, default=0,
                     help="diagnostic: time rank 0's shard step of an N-rank run on one GPU "
                          "(the all-gather replaced by a local copy; not a bench line)")
@@ -81,7 +84,8 @@ class Step:
         self.W = (n + 63) >> 6
         self.emulate = emulate
         self.nranks = emulate or world
-        if self.nranks > 1:
+        self.shard_path = self.nranks > 1 or dist is not None
+        if self.shard_path:
             # [OR | cross | NAND] words of this rank's rows, and all ranks'
             self.words = torch.zeros(3 * self.W, dtype=torch.int64, device="cuda")
             self.gathered = torch.zeros(self.nranks * 3 * self.W, dtype=torch.int64,
@@ -112,7 +116,7 @@ class Step:
             self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
             self.idx_view = self.pin_idx.view(np.int32, 4 * max(n, 1))
         idx = self.idx_view
-        if self.nranks == 1:
+        if not self.shard_path:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
             r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=idx)
@@ -234,7 +238,7 @@ def main():
             sys.exit("--gpus N > 1 needs torch.distributed.run with N processes")
     import torch
     dist = None
-    if world > 1:
+    if world > 1 or (args.shard_path and "RANK" in os.environ):
         import torch.distributed as dist
         # one GPU per rank; KANO_DIST_BACKEND=gloo with fewer GPUs than ranks
         # rehearses the N > 1 code path on one device (timings meaningless)
@@ -252,7 +256,7 @@ def main():
     r0, r1 = rank * n // world, (rank + 1) * n // world
     if args.rank_of > 1:
         r0, r1 = 0, n // args.rank_of
-    stream = torch.cuda.Stream() if world > 1 or args.rank_of > 1 else None
+    stream = torch.cuda.Stream() if dist is not None or args.rank_of > 1 else None
     eng = DeviceBuild(tables, device=torch.cuda.current_device(), rows=(r0, r1), path=args.path,
                       build=False,
                       stream=stream.cuda_stream if stream is not None else None)
