@@ -1469,14 +1469,19 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   ctx->ncols = ncols;
   // bit width of every column's (value id + 1): key tuples that fit 63 bits
   // are hashed and compared as one packed word (no gathers of pod values)
+  // (pod value ids are >= -3: -1 absent, -3 never matches; packed as v + 3;
+  // a column with anything lower is marked unpackable, 64 bits)
   ctx->colbits.assign(ncols, 1);
   for (int32_t c = 0; c < ncols; ++c) {
-    int32_t mx = 0;
+    int32_t mx = 0, mn = 0;
     const int32_t* col = pod_val + (i64)c * n;
-    for (i64 i = 0; i < n; ++i) mx = std::max(mx, col[i] + 1);
+    for (i64 i = 0; i < n; ++i) {
+      mx = std::max(mx, col[i] + 3);
+      mn = std::min(mn, col[i] + 3);
+    }
     int b = 1;
     while (b < 31 && (1 << b) <= mx) ++b;
-    ctx->colbits[c] = b;
+    ctx->colbits[c] = mn < 0 ? 64 : b;
   }
   KTRY(dalloc(ctx, ctx->pv, sizeof(int32_t) * std::max<i64>(1, n * ncols)));
   if (n * ncols > 0)

@@ -48,11 +48,11 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
   if (i >= a.m1) return;
   uint32_t s;
   if (a.packed) {
-    // the key tuple as one word, (value + 1) per key: compare words, no
-    // gathers of the occupant's pod values
+    // the key tuple as one word, (value + 3) per key (ids are >= -3): compare
+    // words, no gathers of the occupant's pod values
     u64 key = 0;
     for (int k = 0; k < a.KS; ++k)
-      key = (key << a.keys[a.KS + k]) | (u64)(uint32_t)(pv[(i64)a.keys[k] * n + i] + 1);
+      key = (key << a.keys[a.KS + k]) | (u64)(uint32_t)(pv[(i64)a.keys[k] * n + i] + 3);
     s = hfin(hmix(hmix(0x9747b28cu, (uint32_t)key), (uint32_t)(key >> 32))) & a.tmask;
     u64* tab = reinterpret_cast<u64*>(a.table);
     for (;;) {

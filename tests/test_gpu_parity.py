@@ -442,3 +442,56 @@ def test_degenerate_sizes():
     ps = [Policy("p", PolicySelect({}), PolicyAllow({}), PolicyEgress, PolicyProtocol([]))]
     m = ReachabilityMatrix.build_matrix(cs, ps)
     assert all_reachable(m) == [0, 1] and [r.to01() for r in m.matrix] == ["11", "11"]
+
+
+def _mixed_cluster(seed, n=300, P=60, nkeys=6):
+    """Labels of mixed Python types (ints, floats equal to ints, bools, strings,
+    NaN) over a few keys, selectors drawn from the same values: the interning
+    folds == classes and NaN never matches (quirk Q7)."""
+    import math
+    rng = np.random.default_rng(seed)
+    vals = [0, 1, 2, 1.0, True, "1", "a", "b", math.nan, 3, 4.5]
+    keys = [f"k{i}" for i in range(nkeys)]
+    pods = []
+    for i in range(n):
+        labels = {}
+        for k in keys:
+            if rng.random() < 0.7:
+                labels[k] = vals[rng.integers(len(vals))]
+        labels["tenant"] = f"t{rng.integers(4)}"
+        pods.append({"name": f"p{i}", "labels": labels})
+    pols = []
+    for p in range(P):
+        sel = {k: vals[rng.integers(len(vals))]
+               for k in rng.choice(keys, size=rng.integers(0, 3), replace=False)}
+        alw = {k: vals[rng.integers(len(vals))]
+               for k in rng.choice(keys, size=rng.integers(0, 3), replace=False)}
+        pols.append({"name": f"q{p}", "select": sel, "allow": alw,
+                     "direction": "ingress" if rng.random() < 0.5 else "egress",
+                     "protocol": ["TCP", "80"]})
+    return {"label": "tenant", "pods": pods, "policies": pols}
+
+
+@pytest.mark.parametrize("packed", ["1", "0"])
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
+    """Class hashing on packed key words (value id + 3, ids >= -3 with NaN's
+    -3) and on gathered pod values give the oracle's matrix and checks."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids
+    from kano._bits import set_bit_indices, words_to_bool
+    from oracle import kano_oracle as orc
+    monkeypatch.setenv("KANO_TUNE", f"packed={packed}")
+    obj = _mixed_cluster(seed)
+    cs, ps = api_objects(obj)
+    ref = orc.run_c(obj, label="tenant")
+    eng = DeviceBuild(intern(cs, ps))
+    n = len(cs)
+    assert np.array_equal(eng.rows(0, n), ref["M"])
+    r = eng.verify(group_ids(cs, "tenant"), sys_row=0, shadow=True)
+    assert r["all_reachable"].tolist() == ref["all_reachable"]
+    assert r["all_isolated"].tolist() == ref["all_isolated"]
+    assert r["user_crosscheck"].tolist() == ref["user_crosscheck"]
+    assert r["system_isolation"].tolist() == ref["system_isolation"]
+    assert np.array_equal(np.ascontiguousarray(r["pairs"]).reshape(-1, 2), ref["shadow"])
+    eng.close()
