@@ -131,6 +131,7 @@ struct kano_ctx {
   int ht_wait = 0;
   std::chrono::steady_clock::time_point ht_last{};
   int cls_packed = 1;        // packed-key classification where the tuple fits 63 bits
+  int mfma_kmin = 8;         // min policy blocks (64 policies each) per MFMA wave
   int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
                              // (measured C3: 16.9 us vs 24-27 us for the serial walk)
 
@@ -874,19 +875,29 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       KLAUNCH();
       const u64* selT = P_<u64>(ctx->scratch_words);
       uint32_t* out = reinterpret_cast<uint32_t*>(P_<u64>(ctx->Mc));
+      // split K (policy blocks) so that the launch has ~2048 waves whatever
+      // the number of 32-column tiles
+      const i64 tiles = 2 * ldMc;
+      // (at least MFMA_KMIN policy blocks per wave: the epilogue, 16 ballots
+      // and OR-atomics per 32-row tile, must not dominate)
+      const i64 ksplit = std::max<i64>(
+          1, std::min<i64>((ctx->PB + ctx->mfma_kmin - 1) / ctx->mfma_kmin,
+                           2048 / std::max<i64>(1, tiles)));
+      const i64 kchunk = (ctx->PB + ksplit - 1) / ksplit;
+      const unsigned gy = (unsigned)((ctx->PB + kchunk - 1) / kchunk);
       for (i64 h0 = 0; h0 < H; h0 += HT_ROWS) {
         const int hh = (int)std::min<i64>(HT_ROWS, H - h0);
         const int32_t* hl = P_<int32_t>(ctx->hlist) + h0;
-        dim3 grid(nblk(2 * ldMc, TPB / 64));
+        dim3 grid(nblk(tiles, TPB / 64), gy);
         if (hh <= 32)
           hipLaunchKernelGGL(k_heavy_mc_mfma<1>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
-                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc, kchunk);
         else if (hh <= 64)
           hipLaunchKernelGGL(k_heavy_mc_mfma<2>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
-                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc, kchunk);
         else
           hipLaunchKernelGGL(k_heavy_mc_mfma<4>, grid, dim3(TPB), 0, ctx->stream, selT, U, hl, hh,
-                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc, kchunk);
         KLAUNCH();
       }
     } else {
@@ -1330,6 +1341,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
         if (k == "grm") ctx->grange_m = v;
         if (k == "fold") ctx->fold_mode = v;
+        if (k == "kmin" && v >= 1) ctx->mfma_kmin = v;
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
         if (k == "store") ctx->rows_store = v;

@@ -1194,12 +1194,17 @@ __device__ __forceinline__ i32x4 expand16(uint32_t b16) {
   return r;
 }
 
+// Split-K: blockIdx.y takes policy blocks [y*kchunk, (y+1)*kchunk); the
+// thresholded partial contractions are OR-ed into Mc (zeroed; OR over the
+// splits of "some p in the split" is exactly "some p"), so the K loop of a
+// wave is short and the grid fills the chip even for a handful of column
+// tiles.
 template <int HT>
 __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ selT, i64 U,
                                                        const int32_t* __restrict__ hlist, int H,
                                                        const u64* __restrict__ ACT, i64 Ua,
                                                        i64 PB, uint32_t* __restrict__ Mc32,
-                                                       i64 ldMc) {
+                                                       i64 ldMc, i64 kchunk) {
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
   const i64 jt = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);  // 32-column tile
   if (jt >= 2 * ldMc) return;                                        // wave-uniform
@@ -1215,7 +1220,8 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
   for (int t = 0; t < HT; ++t)
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[t][g] = 0;
-  for (i64 pb = 0; pb < PB; ++pb) {
+  const i64 pb0 = (i64)blockIdx.y * kchunk, pb1 = min(PB, pb0 + kchunk);
+  for (i64 pb = pb0; pb < pb1; ++pb) {
     const u64 bw = ca < Ua ? ACT[pb * Ua + ca] : 0ull;
     u64 aw[HT];
 #pragma unroll
@@ -1238,8 +1244,8 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
       const u64 bal = __ballot(acc[t][g] > 0);
       if (lane == 0 || lane == 32) {
         const int r = t * 32 + (g & 3) + 8 * (g >> 2) + (lane == 32 ? 4 : 0);
-        if (r < H)
-          Mc32[(i64)hlist[r] * ldMc * 2 + jt] = lane == 0 ? (uint32_t)bal : (uint32_t)(bal >> 32);
+        const uint32_t word = lane == 0 ? (uint32_t)bal : (uint32_t)(bal >> 32);
+        if (r < H && word) atomicOr(&Mc32[(i64)hlist[r] * ldMc * 2 + jt], word);
       }
     }
   }
