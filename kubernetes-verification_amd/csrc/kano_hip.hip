@@ -158,6 +158,10 @@ struct kano_ctx {
   DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
   DBuf icnt, ioff, sysrow, idxd;
   u64* ghost = nullptr;      // pinned landing buffer for the size slots
+  // pinned, coherent mirror of the size slots that the scans write directly
+  // (slot-indexed): the overlapped syncs wait on an event, with no copy
+  u64* gmirror = nullptr;
+  u64* gmirror_dev = nullptr;
 
   hipEvent_t ev[10] = {};
   // the matrix write (k_rows) runs on its own stream beside the checks, which
@@ -261,7 +265,18 @@ struct ScanBatch {
   ScanJobs jobs{};
   kano_ctx* ctx;
   i64 slots = 0, maxt = 1;
-  explicit ScanBatch(kano_ctx* c) : ctx(c) { jobs.count = 0; }
+  explicit ScanBatch(kano_ctx* c) : ctx(c) {
+    jobs.count = 0;
+    jobs.npub = 0;
+  }
+  // copy size slot `slot` (written by an earlier kernel) to its host mirror
+  // in this launch
+  void publish(int slot) {
+    if (!ctx->gmirror_dev || jobs.npub == MAX_PUBLISH) return;
+    jobs.pub_src[jobs.npub] = P_<u64>(ctx->sizes) + slot;
+    jobs.pub_dst[jobs.npub] = ctx->gmirror_dev + slot;
+    ++jobs.npub;
+  }
   template <typename Tin, typename Tout>
   int add(const Tin* in, i64 n, Tout* out, int total_slot = -1) {
     static_assert(sizeof(Tin) == 4 || sizeof(Tin) == 8, "int32 / int64 scans");
@@ -271,6 +286,7 @@ struct ScanBatch {
     j.in = in;
     j.out = out;
     j.total = total_slot >= 0 ? P_<u64>(ctx->sizes) + total_slot : nullptr;
+    j.total_host = total_slot >= 0 && ctx->gmirror_dev ? ctx->gmirror_dev + total_slot : nullptr;
     j.n = n;
     j.st = slots;
     j.in64 = sizeof(Tin) == 8;
@@ -303,6 +319,7 @@ struct ScanBatch {
     KLAUNCH();
     ctx->scan_parity ^= 1;
     jobs.count = 0;
+    jobs.npub = 0;
     slots = 0;
     maxt = 1;
     return 0;
@@ -383,16 +400,16 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
   return 0;
 }
 
-// the same in two halves: the copy and an event now, the wait later, so
-// that the GPU runs the work queued in between while the host waits
-int slots_begin(kano_ctx* ctx, int first, int count) {
-  KCHK(hipMemcpyAsync(ctx->ghost, P_<u64>(ctx->sizes) + first, sizeof(u64) * count,
-                      hipMemcpyDeviceToHost, ctx->stream));
+// the overlapped syncs: the slots reach their host mirror inside the scans
+// (totals) or by a scan's publish list (atomic slots); the host records an
+// event behind them now, queues more work, and later waits on the event and
+// reads the mirror -- no copy
+int mirror_begin(kano_ctx* ctx) {
   KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
   return 0;
 }
 
-int slots_wait(kano_ctx* ctx, int count, i64* out) {
+int mirror_wait(kano_ctx* ctx, int first, int count, i64* out) {
   const auto t0 = std::chrono::steady_clock::now();
   KTRY(wait_event(ctx, ctx->ev_sizes));
   if (ctx->host_timing) {
@@ -401,7 +418,7 @@ int slots_wait(kano_ctx* ctx, int count, i64* out) {
     ctx->ht[4] += w;
     ctx->ht[5 + std::min(ctx->ht_wait++, 2)] += w;
   }
-  for (int k = 0; k < count; ++k) out[k] = (i64)ctx->ghost[k];
+  for (int k = 0; k < count; ++k) out[k] = (i64)((volatile u64*)ctx->gmirror)[first + k];
   return 0;
 }
 
@@ -659,10 +676,10 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(classify_phase1(ctx));
   // host sync 1 of the build (the class counts), overlapped: the counts
   // travel while phase 2a runs
-  KTRY(slots_begin(ctx, SZ_UR, 2));
+  KTRY(mirror_begin(ctx));
   KTRY(classify_phase2a(ctx));
   i64 u[2] = {0, 0};
-  KTRY(slots_wait(ctx, 2, u));
+  KTRY(mirror_wait(ctx, SZ_UR, 2, u));
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KTRY(stage_mark(ctx, 1, ctx->stream));
@@ -732,6 +749,8 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(sb.add(P_<int32_t>(ctx->wicnt), Ur, P_<int32_t>(ctx->wioff), SZ_WI));
   KTRY(sb.add(P_<int32_t>(ctx->hflag), Ur, P_<int32_t>(ctx->hoff), SZ_HEAVY));
   KTRY(sb.add(P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff), SZ_NFLAGS));
+  sb.publish(SZ_MAXSEL);   // k_class_plan's atomics, for the host's sync 2
+  sb.publish(SZ_LIGHT);
   KTRY(sb.run());
   return 0;
 }
@@ -739,7 +758,7 @@ int do_front(kano_ctx* ctx, int path) {
 // host sync 2 of the build: every list size at once
 int read_sizes(kano_ctx* ctx) {
   i64 v[SZ_LIGHT - SZ_NNZ_SEL + 1];
-  KTRY(slots_wait(ctx, SZ_LIGHT - SZ_NNZ_SEL + 1, v));
+  KTRY(mirror_wait(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1, v));
   ctx->nnz_sel = v[SZ_NNZ_SEL - SZ_NNZ_SEL];
   ctx->nnz_alc = v[SZ_NNZ_ALC - SZ_NNZ_SEL];
   ctx->nnz_alw = v[SZ_NNZ_ALW - SZ_NNZ_SEL];
@@ -1411,6 +1430,14 @@ int kano_create(int device, kano_ctx** out) {
     kano_destroy(ctx);
     return -ENOMEM;
   }
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->gmirror), sizeof(u64) * SZ_SLOTS,
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->gmirror_dev), ctx->gmirror, 0) !=
+          hipSuccess) {
+    kano_destroy(ctx);
+    return -ENOMEM;
+  }
+  for (int k = 0; k < SZ_SLOTS; ++k) ctx->gmirror[k] = 0;
   *out = ctx;
   return 0;
 }
@@ -1429,6 +1456,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
+  if (ctx->gmirror) (void)hipHostFree(ctx->gmirror);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
@@ -1716,7 +1744,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KTRY(do_front(ctx, path));
   // host sync 2 (the list sizes), overlapped with the size-independent part
   // of the back end
-  KTRY(slots_begin(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1));
+  KTRY(mirror_begin(ctx));
   KTRY(do_back_pre(ctx, pre_fill, pre_run));
   KTRY(read_sizes(ctx));
   KTRY(stage_mark(ctx, 3, ctx->stream));
@@ -2328,6 +2356,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
     KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
                 SZ_IDX0 + r));
+  sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
   KTRY(sb.run());
   IdxRows ir{};
   ir.W = W;
@@ -2349,13 +2378,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // host while the matrix write runs: the host waits on the copy's event
   // only, then queues policy_shadow's emission and the copies behind k_rows
   constexpr int NS = SZ_ERR - SZ_NL + 1;
-  KCHK(hipMemcpyAsync(ctx->ghost, P_<u64>(ctx->sizes) + SZ_NL, sizeof(u64) * NS,
-                      hipMemcpyDeviceToHost, ctx->stream));
-  KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
+  KTRY(mirror_begin(ctx));
   if (!ctx->vs_early) KTRY(launch_rows(ctx));
-  KTRY(wait_event(ctx, ctx->ev_sizes));
   i64 v[NS];
-  for (int k = 0; k < NS; ++k) v[k] = (i64)ctx->ghost[k];
+  KTRY(mirror_wait(ctx, SZ_NL, NS, v));
   if (ctx->vs_cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff)) {
     (void)sync(ctx);
     return fail(ctx, -EINVAL, "kano_verify: a group id lies outside [0, ngroups)");

@@ -138,6 +138,7 @@ struct ScanJob {
   const void* in;
   void* out;
   u64* total;   // nullable: the total also lands here (a host-read size slot)
+  u64* total_host;   // nullable: ... and here (the slot's pinned host mirror)
   i64 n;
   i64 st;
   int in64, out64;
@@ -150,9 +151,15 @@ struct ScanJob {
   i64 gm0;
 };
 constexpr int MAX_SCAN_JOBS = 8;
+constexpr int MAX_PUBLISH = 4;
 struct ScanJobs {
   ScanJob j[MAX_SCAN_JOBS];
   int count;
+  // size slots produced by earlier kernels (atomics), copied by one thread
+  // to their host mirrors: they travel with the scan's own totals
+  int npub;
+  const u64* pub_src[MAX_PUBLISH];
+  u64* pub_dst[MAX_PUBLISH];
 };
 
 __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
@@ -163,6 +170,8 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
   const i64 lin = (i64)blockIdx.y * gridDim.x + blockIdx.x;
   const i64 nthr = (i64)gridDim.x * gridDim.y * TPB;
   for (i64 i = lin * TPB + threadIdx.x; i < nclear; i += nthr) clear[i] = 0;
+  if (lin == 0 && threadIdx.x == 0)
+    for (int q = 0; q < jobs.npub; ++q) *jobs.pub_dst[q] = *jobs.pub_src[q];
   ScanJob jb = jobs.j[0];   // select, not a dynamic index (kernarg stays in SGPRs)
 #pragma unroll
   for (int q = 1; q < MAX_SCAN_JOBS; ++q)
@@ -173,6 +182,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       if (jb.out64) static_cast<i64*>(jb.out)[0] = 0;
       else static_cast<int32_t*>(jb.out)[0] = 0;
       if (jb.total) *jb.total = 0;
+      if (jb.total_host) *jb.total_host = 0;
     }
     return;
   }
@@ -235,6 +245,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
     if (tile == tiles - 1 && threadIdx.x == TPB - 1) {
       o[jb.n] = pre;
       if (jb.total) *jb.total = (u64)pre;
+      if (jb.total_host) *jb.total_host = (u64)pre;
     }
   } else {
     int32_t* o = static_cast<int32_t*>(jb.out);
@@ -246,6 +257,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
     if (tile == tiles - 1 && threadIdx.x == TPB - 1) {
       o[jb.n] = (int32_t)pre;
       if (jb.total) *jb.total = (u64)pre;
+      if (jb.total_host) *jb.total_host = (u64)pre;
     }
   }
 }
