@@ -121,6 +121,7 @@ struct kano_ctx {
   // chain (set by verify_front around the build; called once the lists and
   // AC exist), joined through ev_join2 before the shadow scans
   int fork_checks = 1;
+  int side_tail = 1;         // kano_verify's tail on stream3 beside k_rows (else after it)
   std::function<int()> fork_hook;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   bool fork_pending = false;
@@ -1388,6 +1389,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hosttime") ctx->host_timing = v;
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
+        if (k == "tail") ctx->side_tail = v;
       }
       pos = end + 1;
     }
@@ -2396,8 +2398,8 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // the list copies, policy_shadow's compaction and emission, the pairs copy
   // (the copies are blit kernels that crawl beside k_rows: the short
   // shadow kernels go first so that they do not queue behind them)
-  hipStream_t cs = ctx->stream3;
-  KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+  hipStream_t cs = ctx->side_tail ? ctx->stream3 : ctx->stream;
+  if (cs != ctx->stream) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
   i64 total = 0;
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
@@ -2412,8 +2414,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
                         cs));
   // later work on the main stream (a fetch of the pairs, the next build)
   // follows the tail
-  KCHK(hipEventRecord(ctx->ev_fork, cs));
-  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
+  if (cs != ctx->stream) {
+    KCHK(hipEventRecord(ctx->ev_fork, cs));
+    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
+  }
   KTRY(join_rows(ctx));  // the matrix is part of the result
   return sync(ctx);
 }
