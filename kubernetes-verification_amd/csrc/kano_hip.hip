@@ -121,6 +121,10 @@ struct kano_ctx {
   // chain (set by verify_front around the build; called once the lists and
   // AC exist), joined through ev_join2 before the shadow scans
   int fork_checks = 1;
+  int shard_rows_early = 0;  // kano_verify_shard: k_rows before the exchange, on stream2
+                             // (measured slower: +18 us over RCCL at one rank, +32 us
+                             // emulated at 1/8 -- the small combine kernels queue
+                             // behind k_rows' blocks)
   int side_tail = 1;         // kano_verify's tail on stream3 beside k_rows (else after it)
   std::function<int()> fork_hook;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
@@ -968,7 +972,7 @@ int do_rows(kano_ctx* ctx) {
 }
 
 // the matrix write (heavy rows from Mc, then k_rows) on stream2
-int launch_rows(kano_ctx* ctx) {
+int launch_rows(kano_ctx* ctx, bool side = false) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
   if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
@@ -976,7 +980,7 @@ int launch_rows(kano_ctx* ctx) {
   // overlapping it with the checks on stream2 was slower), so it runs in
   // order on the main stream unless rows_overlap is set
   hipStream_t rs = ctx->stream;
-  if (ctx->rows_overlap) {
+  if (ctx->rows_overlap || side) {
     KCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
     KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     ctx->rows_pending = true;
@@ -1030,7 +1034,7 @@ int launch_rows(kano_ctx* ctx) {
   else hipLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, a);
   KLAUNCH();
   KCHK(hipEventRecord(ctx->ev[8], rs));
-  if (ctx->rows_overlap) KCHK(hipEventRecord(ctx->ev_rows, rs));
+  if (rs != ctx->stream) KCHK(hipEventRecord(ctx->ev_rows, rs));
   ctx->rows_timed = true;
   return 0;
 }
@@ -1390,6 +1394,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
         if (k == "tail") ctx->side_tail = v;
+        if (k == "shardearly") ctx->shard_rows_early = v;
       }
       pos = end + 1;
     }
@@ -2247,7 +2252,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   KTRY(brc);
   // the matrix write needs only the lists: with rows_early it starts here on
   // stream2, beside the class-level checks
-  const bool early = ctx->rows_early && ctx->rows_overlap;
+  bool early = ctx->rows_early && ctx->rows_overlap;
   if (early) KTRY(launch_rows(ctx));
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
@@ -2321,6 +2326,12 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     KLAUNCH();
   } else {
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
+  }
+  // a row shard's matrix write needs nothing from the ranks' exchange: it
+  // starts now on stream2, so the all-gather and the combine run beside it
+  if (words_dev && !early && ctx->shard_rows_early) {
+    KTRY(launch_rows(ctx, true));
+    early = true;
   }
   ctx->vs_open = true;
   ctx->vs_shadow = want_shadow;
