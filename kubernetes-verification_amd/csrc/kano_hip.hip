@@ -125,6 +125,9 @@ struct kano_ctx {
                              // (measured slower: +18 us over RCCL at one rank, +32 us
                              // emulated at 1/8 -- the small combine kernels queue
                              // behind k_rows' blocks)
+  int s3_prio = 0;           // the tail stream at high priority (measured: k_rows
+                             // 0.209-0.213 ms beside a normal-priority tail, 0.233-0.239
+                             // beside a high-priority one; step 0.556 vs 0.582 ms)
   int side_tail = 1;         // kano_verify's tail on stream3 beside k_rows (else after it)
   std::function<int()> fork_hook;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
@@ -173,7 +176,7 @@ struct kano_ctx {
   // only need class-level data; ev_rows marks its end
   hipStream_t stream2 = nullptr;
   // kano_verify's tail (result copies, policy_shadow's emission) beside the
-  // matrix write, at high priority so that its short kernels get CUs
+  // matrix write (normal priority: a high-priority tail slowed k_rows 10%)
   hipStream_t stream3 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_rows = nullptr;
   bool rows_pending = false;
@@ -1394,6 +1397,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
         if (k == "tail") ctx->side_tail = v;
+        if (k == "s3prio") ctx->s3_prio = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
       }
       pos = end + 1;
@@ -1415,7 +1419,10 @@ int kano_create(int device, kano_ctx** out) {
   {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-    if (hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, hi) != hipSuccess) {
+    const hipError_t e3 =
+        ctx->s3_prio ? hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, hi)
+                     : hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking);
+    if (e3 != hipSuccess) {
       ctx->stream3 = nullptr;
       kano_destroy(ctx);
       return -EIO;
