@@ -198,6 +198,23 @@ int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups);
  * host time on the launch path); slot 6 always. */
 int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
 
+/* Multi-hop reachability, replacing kubesv's
+ * `path` relation (kubesv/kubesv/constraint.py:233-237: path :- edge;
+ * path :- edge o edge) with kano's matrix as `edge`.  Writes into dst's matrix
+ *   hops = 2: P = M | M.M  (the kubesv rule),
+ *   hops = k >= 1: pairs joined by a path of at most k edges,
+ *   hops = 0: the transitive closure M+ (paths of any length >= 1),
+ * computed from src's build at class level (row / column classes; identity
+ * classes after an edit of src's matrix).  dst is a context of the same n
+ * holding a matrix (e.g. a build with no policies); afterwards it is an
+ * edited matrix that every query and check of this header reads.  src must
+ * hold every row (no row shard).  mode: KANO_PATH_AUTO picks per step
+ * between the semi-naive bit-packed OR (sparse delta) and the int8 MFMA
+ * contraction (dense); KANO_PATH_BITWISE / KANO_PATH_MFMA force one.
+ * info (nullable, 6 slots): [composition steps that added pairs, steps run,
+ * steps on the MFMA, row classes, column classes, identity classes]. */
+int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info);
+
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);
 void kano_host_free(void* p);

@@ -41,6 +41,7 @@
 
 #include "kano_hip.h"
 #include "kano_kernels.hpp"
+#include "kano_path.hpp"
 
 using namespace kano;
 
@@ -162,6 +163,12 @@ struct kano_ctx {
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
+  // kano_path (in the destination context): T, R / delta ping-pong buffers,
+  // the MFMA operands, the step counter
+  DBuf pT, pR[2], pD[2], pA, pB, pcnt;
+  int path_dens = 16;        // kano_path auto: MFMA step when the delta holds more than
+                             // path_dens % of the class-level bits
+  int path_tm = 2;           // k_path_mfma rows tiles per wave (1, 2 or 4)
   i64 shadow_total = -1;
   DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
   DBuf icnt, ioff, sysrow, idxd;
@@ -1399,6 +1406,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
+        if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
+        if (k == "pathtm" && (v == 1 || v == 2 || v == 4)) ctx->path_tm = v;
       }
       pos = end + 1;
     }
@@ -1495,7 +1504,9 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->tcnt,   &ctx->toff,    &ctx->sizes,   &ctx->icnt,      &ctx->ioff,
                   &ctx->sysrow, &ctx->wicls,   &ctx->idxd,
                   &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff,
-                  &ctx->gids};
+                  &ctx->gids,
+                  &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
+                  &ctx->pA,     &ctx->pB,      &ctx->pcnt};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -2538,6 +2549,221 @@ int kano_stage_times(kano_ctx* ctx, float* ms) {
   if (ctx->stage_timing && ctx->shadow_total >= 0)
     (void)hipEventElapsedTime(&ms[4], ctx->ev[5], ctx->ev[6]);
   return 0;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Multi-hop reachability (kubesv/kubesv/
+// constraint.py:233-237).  See kano_path.hpp for the class-level recurrence.
+// ===========================================================================
+namespace {
+
+struct PathGeom {
+  bool identity = false;   // an edited M: every pod is its own row / column class
+  i64 rows = 0;            // row classes (or n)
+  i64 Ua = 0;              // column classes (or n)
+  i64 KW = 0;              // words of a class-level row holding bits (ceil(Ua / 64))
+  i64 ldR = 0;             // pitch of the class-level rows
+  const u64* base = nullptr;   // R_1 = Mc (or M)
+  const u64* T = nullptr;      // one hop out of a column class (pitch ldR)
+};
+
+template <int CW>
+int path_or_launch(kano_ctx* ctx, const u64* D, u64* R, u64* Dn, const PathGeom& g) {
+  const i64 nch = (g.ldR + 64 * CW - 1) / (64 * CW);
+  hipLaunchKernelGGL(k_path_or<CW>, dim3(nblk(g.rows * nch, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                     D, R, Dn, g.ldR, g.T, g.ldR, g.rows, g.KW, nch, P_<u64>(ctx->pcnt));
+  KLAUNCH();
+  return 0;
+}
+
+template <int TM>
+int path_mfma_launch(kano_ctx* ctx, const PathMfmaArgs& a, i64 tiles) {
+  hipLaunchKernelGGL((k_path_mfma<TM, 2>), dim3(nblk(tiles, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                     a);
+  KLAUNCH();
+  return 0;
+}
+
+int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
+  const i64 n = src->n, W = src->W, ldM = src->ldM;
+  PathGeom g;
+  g.identity = src->rows_dirty;
+  if (g.identity) {
+    g.rows = n;
+    g.Ua = n;
+    g.KW = W;
+    g.ldR = ldM;
+    g.base = P_<u64>(src->M);
+    g.T = P_<u64>(src->M);   // T[b] = M[b]: column class b is pod b
+  } else {
+    g.rows = src->rc.U;
+    g.Ua = src->cc.U;
+    g.KW = (g.Ua + 63) / 64;
+    g.ldR = src->ldC;
+    g.base = P_<u64>(src->Mc);
+  }
+  const i64 Rw = g.rows * g.ldR;   // words of one class-level matrix
+  i64 steps = 0, used = 0, mfma_steps = 0;
+  if (n > 0 && W > 0 && hops != 1 && g.rows > 0 && g.Ua > 0) {
+    if (!g.identity) {
+      KTRY(dalloc(ctx, ctx->pT, sizeof(u64) * g.Ua * g.ldR));
+      const i64 nch = (g.ldR + 255) / 256;
+      hipLaunchKernelGGL(k_path_t<4>, dim3(nblk(g.Ua * nch, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                         g.base, g.ldR, P_<int32_t>(src->rc.cls), P_<int32_t>(src->cc.moff),
+                         P_<int32_t>(src->cc.mem), g.Ua, g.KW, nch, P_<u64>(ctx->pT));
+      KLAUNCH();
+      g.T = P_<u64>(ctx->pT);
+    }
+    // R[0] (the identity case writes the destination matrix in place), R[1]
+    // for the MFMA's out-of-place steps, two delta buffers
+    u64* Rb[2];
+    if (g.identity) {
+      Rb[0] = P_<u64>(ctx->M);
+    } else {
+      KTRY(dalloc(ctx, ctx->pR[0], sizeof(u64) * Rw));
+      Rb[0] = P_<u64>(ctx->pR[0]);
+    }
+    KTRY(dalloc(ctx, ctx->pD[0], sizeof(u64) * Rw));
+    KTRY(dalloc(ctx, ctx->pD[1], sizeof(u64) * Rw));
+    KTRY(dalloc(ctx, ctx->pcnt, sizeof(u64)));
+    // (the MFMA step writes the words its tiles cover: the rest stay zero)
+    KCHK(hipMemsetAsync(ctx->pD[0].p, 0, sizeof(u64) * Rw, ctx->stream));
+    KCHK(hipMemsetAsync(ctx->pD[1].p, 0, sizeof(u64) * Rw, ctx->stream));
+    Rb[1] = nullptr;
+    u64* Db[2] = {P_<u64>(ctx->pD[0]), P_<u64>(ctx->pD[1])};
+    KCHK(hipMemcpyAsync(Rb[0], g.base, sizeof(u64) * Rw, hipMemcpyDeviceToDevice, ctx->stream));
+    // the delta of step 1 is R_1 itself; its size decides the first step
+    const u64* D = g.base;
+    KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64), ctx->stream));
+    hipLaunchKernelGGL(k_popcount_words, dim3(std::min<i64>(2048, nblk(Rw))), dim3(TPB), 0,
+                       ctx->stream, g.base, Rw, P_<u64>(ctx->pcnt));
+    KLAUNCH();
+    u64 dbits = 0;
+    KCHK(hipMemcpyAsync(&dbits, ctx->pcnt.p, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    KTRY(sync(ctx));
+    int ri = 0, di = 0;
+    const i64 TMr = 32 * ctx->path_tm;
+    const i64 Rpad = (g.rows + 127) / 128 * 128, Upad = (g.Ua + 127) / 128 * 128;
+    bool have_b = false;
+    const double cells = (double)g.rows * (double)g.Ua;
+    for (i64 k = 2; (hops == 0 || k <= hops) && dbits > 0; ++k) {
+      bool mf = mode == KANO_PATH_MFMA;
+      if (mode == KANO_PATH_AUTO) mf = (double)dbits * 100.0 > ctx->path_dens * cells;
+      KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64), ctx->stream));
+      if (!mf) {
+        if (g.ldR <= 128) KTRY(path_or_launch<2>(ctx, D, Rb[ri], Db[di], g));
+        else KTRY(path_or_launch<4>(ctx, D, Rb[ri], Db[di], g));
+      } else {
+        if (!have_b) {   // T bit-transposed: B[kw][c] bit t = T[64 kw + t][c]
+          KTRY(dalloc(ctx, ctx->pB, sizeof(u64) * g.KW * Upad));
+          const i64 CWn = Upad / 64;
+          hipLaunchKernelGGL(k_bit_transpose, dim3(nblk(g.KW * CWn, TPB / 64)), dim3(TPB), 0,
+                             ctx->stream, g.T, g.ldR, g.Ua, g.KW, CWn, P_<u64>(ctx->pB), Upad);
+          KLAUNCH();
+          have_b = true;
+        }
+        KTRY(dalloc(ctx, ctx->pA, sizeof(u64) * g.KW * Rpad));
+        hipLaunchKernelGGL(k_word_transpose, dim3(nblk(g.KW, 64), (unsigned)(Rpad / 64)),
+                           dim3(TPB), 0, ctx->stream, Rb[ri], g.ldR, g.rows, g.KW,
+                           P_<u64>(ctx->pA), Rpad, g.KW);
+        KLAUNCH();
+        if (!Rb[1]) {
+          KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * Rw));
+          Rb[1] = P_<u64>(ctx->pR[1]);
+          KCHK(hipMemsetAsync(Rb[1], 0, sizeof(u64) * Rw, ctx->stream));
+        }
+        PathMfmaArgs a{};
+        a.A = P_<u64>(ctx->pA);
+        a.B = P_<u64>(ctx->pB);
+        a.ldA = Rpad;
+        a.ldB = Upad;
+        a.KW = g.KW;
+        a.base = g.base;
+        a.old = Rb[ri];
+        a.out = Rb[ri ^ 1];
+        a.delta = Db[di];
+        a.ldR = g.ldR;
+        a.rows = g.rows;
+        a.tiles_n = Upad / 64;
+        a.cnt = P_<u64>(ctx->pcnt);
+        const i64 tiles = (Rpad / TMr) * a.tiles_n;
+        if (ctx->path_tm == 1) KTRY(path_mfma_launch<1>(ctx, a, tiles));
+        else if (ctx->path_tm == 4) KTRY(path_mfma_launch<4>(ctx, a, tiles));
+        else KTRY(path_mfma_launch<2>(ctx, a, tiles));
+        ri ^= 1;
+        ++mfma_steps;
+      }
+      KCHK(hipMemcpyAsync(&dbits, ctx->pcnt.p, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+      KTRY(sync(ctx));
+      D = Db[di];
+      di ^= 1;
+      ++used;
+      if (dbits > 0) ++steps;
+    }
+    if (g.identity) {
+      if (ri != 0)
+        KCHK(hipMemcpyAsync(Rb[0], Rb[ri], sizeof(u64) * Rw, hipMemcpyDeviceToDevice,
+                            ctx->stream));
+    } else {
+      // P[i] bit j = R[rc(i)][cc(j)]
+      constexpr int RT = 8;
+      const size_t lds = sizeof(u64) * (size_t)g.ldR;
+      if (lds > 64 * 1024)
+        return fail(ctx, -ENOTSUP, "kano_path: more than 524288 column classes");
+      hipLaunchKernelGGL(k_path_expand<RT>, dim3(nblk(ldM, TPB), nblk(g.rows, RT)), dim3(TPB), lds,
+                         ctx->stream, Rb[ri], g.ldR, g.rows, P_<int32_t>(src->cc.cls), n,
+                         P_<int32_t>(src->rc.moff), P_<int32_t>(src->rc.mem), P_<u64>(ctx->M),
+                         ldM);
+      KLAUNCH();
+    }
+  } else if (n > 0 && W > 0) {
+    // one hop (or an empty class set): the matrix itself
+    KCHK(hipMemcpyAsync(ctx->M.p, src->M.p, sizeof(u64) * n * ldM, hipMemcpyDeviceToDevice,
+                        ctx->stream));
+  }
+  KTRY(sync(ctx));
+  ctx->cols_valid = false;
+  ctx->rows_dirty = true;
+  if (info) {
+    info[0] = steps;
+    info[1] = used;
+    info[2] = mfma_steps;
+    info[3] = g.rows;
+    info[4] = g.Ua;
+    info[5] = g.identity ? 1 : 0;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info) {
+  if (!src || !dst) return -EINVAL;
+  if (src == dst) return fail(dst, -EINVAL, "kano_path: the destination must be another context");
+  if (hops < 0) return fail(dst, -EINVAL, "kano_path: hops < 0");
+  if (mode < KANO_PATH_AUTO || mode > KANO_PATH_MFMA)
+    return fail(dst, -EINVAL, "kano_path: unknown mode");
+  if (src->device != dst->device) return fail(dst, -EINVAL, "kano_path: contexts on two devices");
+  kano_ctx* ctx = dst;
+  KCHK(hipSetDevice(dst->device));
+  {
+    const int rc = ensure_matrix(src);
+    if (rc) return fail(dst, rc, "kano_path: source: " + src->err);
+  }
+  if (src->r0 != 0 || src->r1 != src->n)
+    return fail(dst, -ENOTSUP, "kano_path: the source holds a row shard (needs every row)");
+  KTRY(ensure_matrix(dst));
+  if (dst->n != src->n || dst->r0 != 0 || dst->r1 != dst->n || dst->ldM != src->ldM)
+    return fail(dst, -EINVAL, "kano_path: the destination must hold a matrix of the same size");
+  {
+    const int rc = sync(src);   // the source's matrix and classes are complete
+    if (rc) return fail(dst, rc, "kano_path: source: " + src->err);
+  }
+  return path_impl(src, dst, hops, mode, info);
 }
 
 }  // extern "C"

@@ -124,6 +124,24 @@ class DeviceBuild:
     def W(self) -> int:
         return (self.tables.n + 63) >> 6
 
+    @staticmethod
+    def empty(n: int, device: int = 0) -> "DeviceBuild":
+        """A context holding an n x n matrix and no policies (the target of
+        put_rows or of path_from)."""
+        z64 = np.zeros(1, np.int64)
+        e = np.zeros(0, np.int32)
+        t = Tables(int(n), 0, np.zeros((0, int(n)), np.int32), z64, e, e, z64, e, e)
+        return DeviceBuild(t, device=device)
+
+    def path_from(self, src: "DeviceBuild", hops: int = 2, mode: str = "auto") -> dict:
+        """This context's matrix := the multi-hop reachability of src's
+        matrix (kano_path; kubesv/kubesv/constraint.py:233-237)."""
+        info = np.zeros(6, dtype=np.int64)
+        self._chk(self.lib.kano_path(src.ctx, self.ctx, int(hops), nat.PATHS[mode], _ptr(info)),
+                  "kano_path")
+        keys = ("steps", "steps_run", "mfma_steps", "row_classes", "col_classes", "identity")
+        return {k: int(v) for k, v in zip(keys, info)}
+
     # -- checks ---------------------------------------------------------
     def col_checks(self) -> Tuple[np.ndarray, np.ndarray]:
         W = self.W

@@ -172,3 +172,44 @@ def policy_conflict(matrix: ReachabilityMatrix, policies: List[Policy],
     if raises:
         raise AttributeError("'int' object has no attribute 'working_allow_set'")
     return []
+
+
+# ---------------------------------------------------------------------------
+# Multi-hop reachability.  Not part of kano_py's
+# algorithm.py: kubesv's `path` relation (kubesv/kubesv/constraint.py:233-237,
+# path(src, dst) :- edge(src, dst); path(src, dst) :- edge(src, sel),
+# edge(sel, dst)) with kano's matrix as `edge`.  The result is a
+# ReachabilityMatrix on the device, so every query above runs on it.
+
+def _path_matrix(matrix: ReachabilityMatrix, hops: int, mode: str) -> ReachabilityMatrix:
+    from ._engine import DeviceBuild
+    src = _engine(matrix)
+    n = matrix.container_size
+    out = ReachabilityMatrix.__new__(ReachabilityMatrix)
+    out.container_size = n
+    out._engine = DeviceBuild.empty(n, device=src.device)
+    out._containers = None
+    out._policies = None
+    out._ncontainers = n
+    out._lists = None
+    out.path_info = out._engine.path_from(src, hops=hops, mode=mode)
+    return out
+
+
+def two_hop(matrix: ReachabilityMatrix, mode: str = "auto") -> ReachabilityMatrix:
+    """kubesv's path relation: P = M | M.M (pairs joined by one or two
+    edges)."""
+    return _path_matrix(matrix, 2, mode)
+
+
+def k_hop(matrix: ReachabilityMatrix, hops: int, mode: str = "auto") -> ReachabilityMatrix:
+    """Pairs joined by a path of at most `hops` (>= 1) edges."""
+    if int(hops) < 1:
+        raise ValueError("hops must be >= 1")
+    return _path_matrix(matrix, int(hops), mode)
+
+
+def transitive_closure(matrix: ReachabilityMatrix, mode: str = "auto") -> ReachabilityMatrix:
+    """M+: pairs joined by a path of any length >= 1 (the fixpoint of the
+    path rule applied to itself)."""
+    return _path_matrix(matrix, 0, mode)

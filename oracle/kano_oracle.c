@@ -215,3 +215,39 @@ int oracle_shadow(int64_t n_lists, int64_t nbits, const int64_t* off, const int3
   *count = cnt;
   return 0;
 }
+
+/*
+ * Multi-hop reachability: kubesv's `path` relation,
+ *   path(src, dst) :- edge(src, dst).
+ *   path(src, dst) :- edge(src, sel), edge(sel, dst).
+ * (kubesv/kubesv/constraint.py:233-237), over kano's matrix as `edge`.
+ * hops = 2 is that rule: P = M | M.M.  hops = k >= 1 extends it to paths of
+ * at most k edges, hops = 0 to the transitive closure M+ (any length >= 1).
+ * Row i after step k: P_k[i] = M[i] | OR_{j in P_{k-1}[i]} M[j], P_1 = M,
+ * iterated until k = hops or nothing changes.  M and P are n rows of W words.
+ * Returns the number of composition steps that changed some row.
+ */
+int64_t oracle_path(int64_t n, int64_t W, const u64* M, int64_t hops, u64* P) {
+  u64* cur = (u64*)malloc(sizeof(u64) * (size_t)(n * W + 1));
+  if (!cur) return -1;
+  memcpy(P, M, sizeof(u64) * (size_t)(n * W));
+  int64_t steps = 0;
+  for (int64_t k = 2; hops == 0 || k <= hops; ++k) {
+    memcpy(cur, P, sizeof(u64) * (size_t)(n * W));
+    int changed = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      u64* out = P + i * W;
+      const u64* ri = cur + i * W;
+      for (int64_t j = 0; j < n; ++j) {
+        if (!getbit(ri, j)) continue;          /* edge / path (i, j) */
+        const u64* mj = M + j * W;             /* edge (j, dst) */
+        for (int64_t w = 0; w < W; ++w) out[w] |= mj[w];
+      }
+      for (int64_t w = 0; w < W; ++w) changed |= out[w] != ri[w];
+    }
+    if (!changed) break;
+    ++steps;
+  }
+  free(cur);
+  return steps;
+}

@@ -46,6 +46,8 @@ def lib():
         for f in (L.oracle_build, L.oracle_lists, L.oracle_column_checks, L.oracle_crosscheck,
                   L.oracle_shadow):
             f.restype = c_int
+        L.oracle_path.argtypes = [c_int64, c_int64, c_void_p, c_int64, c_void_p]
+        L.oracle_path.restype = c_int64
         _lib = L
     return _lib
 
@@ -281,3 +283,37 @@ def _hashable(v) -> bool:
         return True
     except TypeError:
         return False
+
+
+# ---------------------------------------------------------------------------
+# multi-hop reachability (kubesv/kubesv/constraint.py:233-237)
+def path_c(M: np.ndarray, n: int, hops: int = 2):
+    """kubesv's `path` over kano's matrix (oracle_path): P = M | M.M for
+    hops=2, paths of <= hops edges, or the transitive closure for hops=0.
+    M: (n, W) uint64 LSB-first rows.  Returns (P, steps)."""
+    M = np.ascontiguousarray(M, dtype=np.uint64)
+    W = M.shape[1] if M.ndim == 2 else 0
+    P = np.zeros_like(M)
+    steps = lib().oracle_path(n, W, _p(M), int(hops), _p(P))
+    if steps < 0:
+        raise MemoryError("oracle_path")
+    return P, int(steps)
+
+
+def path_py(edges: set, n: int, hops: int = 2) -> set:
+    """The Datalog rules of kubesv/kubesv/constraint.py:233-237 restated on
+    sets of (src, dst) pairs, for tiny cases: path :- edge; path :- edge o
+    edge (hops=2), extended to <= hops edges or to the closure (hops=0)."""
+    succ = {}
+    for a, b in edges:
+        succ.setdefault(a, set()).add(b)
+    path = set(edges)
+    k = 1
+    while hops == 0 or k < hops:
+        new = {(a, c) for (a, b) in path for c in succ.get(b, ())} | set(edges)
+        new |= path
+        k += 1
+        if new == path:
+            break
+        path = new
+    return path
