@@ -166,9 +166,11 @@ struct kano_ctx {
   // kano_path (in the destination context): T, R / delta ping-pong buffers,
   // the MFMA operands, the step counter
   DBuf pT, pR[2], pD[2], pA, pB, pcnt;
-  int path_dens = 16;        // kano_path auto: MFMA step when the delta holds more than
+  int path_dens = 8;         // kano_path auto: MFMA step when the delta holds more than
                              // path_dens % of the class-level bits
   int path_tm = 2;           // k_path_mfma rows tiles per wave (1, 2 or 4)
+  int path_tn = 2;           // k_path_mfma column tiles per wave (2 or 4)
+  int path_lds = 1;          // k_path_expand16: the group table in LDS when it fits (tests: 0)
   i64 shadow_total = -1;
   DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
   DBuf icnt, ioff, sysrow, idxd;
@@ -1408,6 +1410,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "shardearly") ctx->shard_rows_early = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
         if (k == "pathtm" && (v == 1 || v == 2 || v == 4)) ctx->path_tm = v;
+        if (k == "pathlds") ctx->path_lds = v;
+        if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
       }
       pos = end + 1;
     }
@@ -2578,9 +2582,9 @@ int path_or_launch(kano_ctx* ctx, const u64* D, u64* R, u64* Dn, const PathGeom&
   return 0;
 }
 
-template <int TM>
+template <int TM, int TN>
 int path_mfma_launch(kano_ctx* ctx, const PathMfmaArgs& a, i64 tiles) {
-  hipLaunchKernelGGL((k_path_mfma<TM, 2>), dim3(nblk(tiles, TPB / 64)), dim3(TPB), 0, ctx->stream,
+  hipLaunchKernelGGL((k_path_mfma<TM, TN>), dim3(nblk(tiles, TPB / 64)), dim3(TPB), 0, ctx->stream,
                      a);
   KLAUNCH();
   return 0;
@@ -2627,7 +2631,7 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
     }
     KTRY(dalloc(ctx, ctx->pD[0], sizeof(u64) * Rw));
     KTRY(dalloc(ctx, ctx->pD[1], sizeof(u64) * Rw));
-    KTRY(dalloc(ctx, ctx->pcnt, sizeof(u64)));
+    KTRY(dalloc(ctx, ctx->pcnt, sizeof(u64) * PATH_CNT_SLOTS * PATH_CNT_STRIDE));
     // (the MFMA step writes the words its tiles cover: the rest stay zero)
     KCHK(hipMemsetAsync(ctx->pD[0].p, 0, sizeof(u64) * Rw, ctx->stream));
     KCHK(hipMemsetAsync(ctx->pD[1].p, 0, sizeof(u64) * Rw, ctx->stream));
@@ -2636,31 +2640,41 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
     KCHK(hipMemcpyAsync(Rb[0], g.base, sizeof(u64) * Rw, hipMemcpyDeviceToDevice, ctx->stream));
     // the delta of step 1 is R_1 itself; its size decides the first step
     const u64* D = g.base;
-    KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64), ctx->stream));
+    KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64) * PATH_CNT_SLOTS * PATH_CNT_STRIDE, ctx->stream));
     hipLaunchKernelGGL(k_popcount_words, dim3(std::min<i64>(2048, nblk(Rw))), dim3(TPB), 0,
                        ctx->stream, g.base, Rw, P_<u64>(ctx->pcnt));
     KLAUNCH();
+    std::vector<u64> slots(PATH_CNT_SLOTS * PATH_CNT_STRIDE);
+    auto read_count = [&](u64& out) -> int {
+      KCHK(hipMemcpyAsync(slots.data(), ctx->pcnt.p, sizeof(u64) * slots.size(),
+                          hipMemcpyDeviceToHost, ctx->stream));
+      KTRY(sync(ctx));
+      out = 0;
+      for (int k = 0; k < PATH_CNT_SLOTS; ++k) out += slots[(size_t)k * PATH_CNT_STRIDE];
+      return 0;
+    };
     u64 dbits = 0;
-    KCHK(hipMemcpyAsync(&dbits, ctx->pcnt.p, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
-    KTRY(sync(ctx));
+    KTRY(read_count(dbits));
     int ri = 0, di = 0;
     const i64 TMr = 32 * ctx->path_tm;
-    const i64 Rpad = (g.rows + 127) / 128 * 128, Upad = (g.Ua + 127) / 128 * 128;
+    const i64 Rpad = (g.rows + 255) / 256 * 256, Upad = (g.Ua + 255) / 256 * 256;
     bool have_b = false;
     const double cells = (double)g.rows * (double)g.Ua;
     for (i64 k = 2; (hops == 0 || k <= hops) && dbits > 0; ++k) {
       bool mf = mode == KANO_PATH_MFMA;
       if (mode == KANO_PATH_AUTO) mf = (double)dbits * 100.0 > ctx->path_dens * cells;
-      KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64), ctx->stream));
+      KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64) * PATH_CNT_SLOTS * PATH_CNT_STRIDE, ctx->stream));
       if (!mf) {
         if (g.ldR <= 128) KTRY(path_or_launch<2>(ctx, D, Rb[ri], Db[di], g));
         else KTRY(path_or_launch<4>(ctx, D, Rb[ri], Db[di], g));
       } else {
         if (!have_b) {   // T bit-transposed: B[kw][c] bit t = T[64 kw + t][c]
           KTRY(dalloc(ctx, ctx->pB, sizeof(u64) * g.KW * Upad));
-          const i64 CWn = Upad / 64;
-          hipLaunchKernelGGL(k_bit_transpose, dim3(nblk(g.KW * CWn, TPB / 64)), dim3(TPB), 0,
-                             ctx->stream, g.T, g.ldR, g.Ua, g.KW, CWn, P_<u64>(ctx->pB), Upad);
+          // (T rows b = column classes; out row kw = 64 of them, Upad columns)
+          const i64 CG = (Upad / 64 + 15) / 16;
+          hipLaunchKernelGGL(k_bit_transpose<false>, dim3(nblk(g.KW * CG, TPB / 64)), dim3(TPB),
+                             0, ctx->stream, g.T, g.ldR, g.Ua, g.KW, CG, Upad,
+                             (void*)P_<u64>(ctx->pB), Upad, (i64)0);
           KLAUNCH();
           have_b = true;
         }
@@ -2686,17 +2700,21 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
         a.delta = Db[di];
         a.ldR = g.ldR;
         a.rows = g.rows;
-        a.tiles_n = Upad / 64;
+        const int TNc = ctx->path_tn == 4 ? 4 : 2;
+        const i64 TMc = ctx->path_tn == 4 ? 64 : TMr;
+        a.tiles_n = Upad / (32 * TNc);
         a.cnt = P_<u64>(ctx->pcnt);
-        const i64 tiles = (Rpad / TMr) * a.tiles_n;
-        if (ctx->path_tm == 1) KTRY(path_mfma_launch<1>(ctx, a, tiles));
-        else if (ctx->path_tm == 4) KTRY(path_mfma_launch<4>(ctx, a, tiles));
-        else KTRY(path_mfma_launch<2>(ctx, a, tiles));
+        // (2 x 2 waves per block, XCD-grouped block order: 8 * ceil(blocks / 8))
+        const i64 blocks = (Rpad / (2 * TMc)) * (a.tiles_n / 2);
+        const i64 tiles = (blocks + 7) / 8 * 8 * (TPB / 64);
+        if (ctx->path_tn == 4) KTRY((path_mfma_launch<2, 4>(ctx, a, tiles)));
+        else if (ctx->path_tm == 1) KTRY((path_mfma_launch<1, 2>(ctx, a, tiles)));
+        else if (ctx->path_tm == 4) KTRY((path_mfma_launch<4, 2>(ctx, a, tiles)));
+        else KTRY((path_mfma_launch<2, 2>(ctx, a, tiles)));
         ri ^= 1;
         ++mfma_steps;
       }
-      KCHK(hipMemcpyAsync(&dbits, ctx->pcnt.p, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
-      KTRY(sync(ctx));
+      KTRY(read_count(dbits));
       D = Db[di];
       di ^= 1;
       ++used;
@@ -2707,15 +2725,26 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
         KCHK(hipMemcpyAsync(Rb[0], Rb[ri], sizeof(u64) * Rw, hipMemcpyDeviceToDevice,
                             ctx->stream));
     } else {
-      // P[i] bit j = R[rc(i)][cc(j)]
-      constexpr int RT = 8;
-      const size_t lds = sizeof(u64) * (size_t)g.ldR;
-      if (lds > 64 * 1024)
-        return fail(ctx, -ENOTSUP, "kano_path: more than 524288 column classes");
-      hipLaunchKernelGGL(k_path_expand<RT>, dim3(nblk(ldM, TPB), nblk(g.rows, RT)), dim3(TPB), lds,
-                         ctx->stream, Rb[ri], g.ldR, g.rows, P_<int32_t>(src->cc.cls), n,
-                         P_<int32_t>(src->rc.moff), P_<int32_t>(src->rc.mem), P_<u64>(ctx->M),
-                         ldM);
+      // P[i] bit j = R[rc(i)][cc(j)]: R bit-transposed into 16-row groups,
+      // then one block per (group, word range)
+      const i64 ng = (g.rows + 15) / 16, RW = (g.rows + 63) / 64, CWn = (g.Ua + 63) / 64;
+      KTRY(dalloc(ctx, ctx->pA, sizeof(uint16_t) * ng * g.Ua));
+      const i64 CG = (CWn + 15) / 16;
+      hipLaunchKernelGGL(k_bit_transpose<true>, dim3(nblk(RW * CG, TPB / 64)), dim3(TPB), 0,
+                         ctx->stream, Rb[ri], g.ldR, g.rows, RW, CG, g.Ua, ctx->pA.p, g.Ua, ng);
+      KLAUNCH();
+      constexpr int SUB = 2;
+      const dim3 grid(nblk(ldM, (i64)TPB * SUB), (unsigned)ng);
+      const size_t lds = sizeof(uint16_t) * (size_t)g.Ua;
+      const uint16_t* rt16 = reinterpret_cast<const uint16_t*>(ctx->pA.p);
+      if (lds <= 64 * 1024 && ctx->path_lds)
+        hipLaunchKernelGGL((k_path_expand16<SUB, true>), grid, dim3(TPB), lds, ctx->stream, rt16,
+                           g.Ua, g.rows, P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
+                           P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM);
+      else
+        hipLaunchKernelGGL((k_path_expand16<SUB, false>), grid, dim3(TPB), 0, ctx->stream, rt16,
+                           g.Ua, g.rows, P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
+                           P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM);
       KLAUNCH();
     }
   } else if (n > 0 && W > 0) {

@@ -1182,8 +1182,10 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_or(const int32_t* __restrict__
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
+// bit i of b4 -> bit 8 i: b4 * (1 + 2^7 + 2^14 + 2^21) puts bit i at i, i+7,
+// i+14, i+21 (no carries); the mask keeps bit 8 i (one v_mul_u32_u24 + and)
 __device__ __forceinline__ uint32_t spread4(uint32_t b4) {
-  return (b4 & 1u) | ((b4 & 2u) << 7) | ((b4 & 4u) << 14) | ((b4 & 8u) << 21);
+  return __umul24(b4, 0x204081u) & 0x01010101u;
 }
 __device__ __forceinline__ i32x4 expand16(uint32_t b16) {
   i32x4 r;

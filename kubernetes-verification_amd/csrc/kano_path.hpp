@@ -22,6 +22,14 @@
 
 namespace kano {
 
+// step counters: one 128-byte line per slot, waves spread over the slots
+// (same-address atomics from every wave serialise)
+constexpr int PATH_CNT_SLOTS = 256, PATH_CNT_STRIDE = 16;
+__device__ __forceinline__ void path_count(u64* cnt, u64 v) {
+  const unsigned slot = (blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)) & (PATH_CNT_SLOTS - 1);
+  if (v) atomicAdd(cnt + slot * PATH_CNT_STRIDE, v);
+}
+
 // T[b] = OR of Mc[rc(j)] over the members j of column class b.  One wave per
 // (class, chunk of 64*CW words); consecutive members of one row class are
 // read once.
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(TPB) void k_path_or(const u64* __restrict__ D, u64*
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) pc += __shfl_xor(pc, d, 64);
-  if (lane == 0 && pc) atomicAdd(cnt, (u64)pc);
+  if (lane == 0) path_count(cnt, (u64)pc);
 }
 
 // dst[kw][r] = src[r][kw]: word transpose through a 64 x 64 LDS tile; rows
@@ -129,34 +137,58 @@ __global__ __launch_bounds__(TPB) void k_word_transpose(const u64* __restrict__ 
   }
 }
 
-// Bit transpose of T (rows b, columns c): dst[kw][c] bit t = T[64*kw + t][c].
-// One wave per 64 x 64 bit block: lane t holds row 64*kw + t, 64 ballots
-// give the transposed words, lane c keeps word c.
-__global__ __launch_bounds__(TPB) void k_bit_transpose(const u64* __restrict__ T, i64 ldT,
-                                                       i64 rowsT, i64 KW, i64 CWn,
-                                                       u64* __restrict__ dst, i64 ldd) {
+// Bit transpose of a bit matrix X (rows r < rows, pitch ldX words):
+// out word (rw, c) = bits X[64 rw + t][c], t = 0..63.  One wave per 64 rows x
+// 16 words: lane t loads its row's 16 words (one 128-byte line), 64 ballots
+// per word transpose the 64 x 64 block, lane c keeps word c.  OUT16 stores
+// each transposed word as four 16-row groups dst16[4 rw + q][c], else
+// dst[rw][c] (ldd = columns per output row).
+template <bool OUT16>
+__global__ __launch_bounds__(TPB) void k_bit_transpose(const u64* __restrict__ X, i64 ldX,
+                                                       i64 rows, i64 RW, i64 CG, i64 ncols,
+                                                       void* __restrict__ dstv, i64 ldd,
+                                                       i64 ngroups) {
   const int lane = threadIdx.x & 63;
   const i64 item = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-  if (item >= KW * CWn) return;                       // wave-uniform
-  const i64 kw = item / CWn, cw = item % CWn;
-  const i64 b = kw * 64 + lane;
-  const u64 x = (b < rowsT && cw < ldT) ? T[b * ldT + cw] : 0ull;
-  u64 mine = 0;
+  if (item >= RW * CG) return;                        // wave-uniform
+  const i64 rw = item / CG, cw0 = (item % CG) * 16;
+  const i64 r = rw * 64 + lane;
+  u64 x[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) x[k] = (r < rows && cw0 + k < ldX) ? X[r * ldX + cw0 + k] : 0ull;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (cw0 + k >= (ncols + 63) / 64) break;          // wave-uniform
+    u64 mine = 0;
 #pragma unroll 8
-  for (int c = 0; c < 64; ++c) {
-    const u64 bal = __ballot((x >> c) & 1ull);
-    if (lane == c) mine = bal;
+    for (int c = 0; c < 64; ++c) {
+      const u64 bal = __ballot((x[k] >> c) & 1ull);
+      if (lane == c) mine = bal;
+    }
+    const i64 col = (cw0 + k) * 64 + lane;
+    if (col < ldd) {
+      if (OUT16) {
+        uint16_t* dst = reinterpret_cast<uint16_t*>(dstv);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const i64 g = rw * 4 + q;
+          if (g < ngroups) dst[g * ldd + col] = (uint16_t)(mine >> (16 * q));
+        }
+      } else {
+        reinterpret_cast<u64*>(dstv)[rw * ldd + col] = mine;
+      }
+    }
   }
-  const i64 col = cw * 64 + lane;
-  if (col < ldd) dst[kw * ldd + col] = mine;
 }
 
 typedef int32_t p_i32x16 __attribute__((ext_vector_type(16)));
 typedef int32_t p_i32x4 __attribute__((ext_vector_type(4)));
 
-// 16 bits -> 16 int8 lanes of 0 / 1 (bit t -> byte t)
+// 16 bits -> 16 int8 lanes of 0 / 1 (bit t -> byte t).  4 bits -> 4 bytes
+// is one 24-bit multiply: b * (1 + 2^7 + 2^14 + 2^21) puts bit i at bits
+// i, i+7, i+14, i+21 (no carries), and the mask keeps bit i at 8 i.
 __device__ __forceinline__ uint32_t pspread4(uint32_t b4) {
-  return (b4 & 1u) | ((b4 & 2u) << 7) | ((b4 & 4u) << 14) | ((b4 & 8u) << 21);
+  return __umul24(b4, 0x204081u) & 0x01010101u;
 }
 __device__ __forceinline__ p_i32x4 pexpand16(uint32_t b16) {
   p_i32x4 r;
@@ -175,7 +207,7 @@ struct PathMfmaArgs {
   const u64* old;    // R_k (pitch ldR): for the change count
   u64* out;          // R_{k+1} (pitch ldR)
   u64* delta;        // R_{k+1} & ~R_k (pitch ldR): the next semi-naive step's input
-  i64 ldR, rows, tiles_n;
+  i64 ldR, rows, tiles_n;   // tiles_n = 32 TN-column tiles (even); ldA = a multiple of 64 TM
   u64* cnt;          // bits of R_{k+1} not in R_k
 };
 
@@ -186,8 +218,21 @@ struct PathMfmaArgs {
 template <int TM, int TN>
 __global__ __launch_bounds__(TPB) void k_path_mfma(PathMfmaArgs a) {
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
-  const i64 wave = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-  const i64 tm = wave / a.tiles_n, tn = wave % a.tiles_n;
+  // block = 2 x 2 waves; blocks of one XCD (blockIdx.x mod 8 under the
+  // round-robin dispatch) take one contiguous range of the block order, which
+  // walks GM block-rows at a time column by column, so that the blocks
+  // resident on an XCD share A and B panels in its L2
+  constexpr i64 GM = 8;
+  const i64 nbm = a.ldA / (64 * TM), nbn = a.tiles_n / 2, total = nbm * nbn;
+  const i64 per = (total + 7) / 8;
+  const i64 L = (i64)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= total) return;                             // block-uniform
+  const i64 grp = L / (GM * nbn), first = grp * GM;
+  const i64 gm = nbm - first < GM ? nbm - first : GM;
+  const i64 in = L - grp * GM * nbn;
+  const i64 bm = first + in % gm, bn = in / gm;
+  const int wv = threadIdx.x >> 6;
+  const i64 tm = bm * 2 + (wv >> 1), tn = bn * 2 + (wv & 1);
   const i64 rb = tm * 32 * TM, cb = tn * 32 * TN;
   if (rb >= a.ldA) return;                            // wave-uniform
   p_i32x16 acc[TM][TN];
@@ -251,7 +296,7 @@ __global__ __launch_bounds__(TPB) void k_path_mfma(PathMfmaArgs a) {
     }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) pc += __shfl_xor(pc, d, 64);
-  if (lane == 0 && pc) atomicAdd(a.cnt, (u64)pc);
+  if (lane == 0) path_count(a.cnt, (u64)pc);
 }
 
 // cnt += popcount of words [0, nw)
@@ -262,45 +307,69 @@ __global__ __launch_bounds__(TPB) void k_popcount_words(const u64* __restrict__ 
     pc += __popcll(w[i]);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) pc += __shfl_xor(pc, d, 64);
-  if ((threadIdx.x & 63) == 0 && pc) atomicAdd(cnt, pc);
+  if ((threadIdx.x & 63) == 0) path_count(cnt, pc);
 }
 
-// P[i] bit j = R[rc(i)][cc(j)] for the members i of row classes
-// [blockIdx.y * RT, + RT), words [blockIdx.x * 256, + 256) (64 per wave).
-// Lane l of a wave holds the column classes of pod 64 * (w + s) + l for its
-// 64 words s; per row class the row is staged in LDS, 64 ballots give the
-// wave's 64 words (lane s keeps word s) and each member row gets one
-// 512-byte store.
-template <int RT>
-__global__ __launch_bounds__(TPB) void k_path_expand(const u64* __restrict__ R, i64 ldR,
-                                                     i64 rows, const int32_t* __restrict__ ccls,
-                                                     i64 n, const int32_t* __restrict__ moff,
-                                                     const int32_t* __restrict__ mem,
-                                                     u64* __restrict__ M, i64 ldM) {
-  extern __shared__ u64 row[];
+// P[i] bit j = R[rc(i)][cc(j)].  Block = (16 row classes of group
+// blockIdx.y, words [blockIdx.x * 256 * SUB, + 256 * SUB)).  The group's bits
+// per column class (tab[c], 16 bits, from k_bit_transpose<true>) sit in LDS
+// (USE_LDS) or are read from L2.  Lane l owns word w = wb + l: it loads the
+// column classes of its 64 pods (all loads in flight at once), looks up their
+// 16-bit entries, and packs bit t of entry k into bit k of the word of class
+// t; each member row of a class then gets one 512-byte store per wave.
+template <int SUB, bool USE_LDS>
+__global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restrict__ RT16, i64 Ua,
+                                                       i64 rows, const int32_t* __restrict__ ccls,
+                                                       i64 n, const int32_t* __restrict__ moff,
+                                                       const int32_t* __restrict__ mem,
+                                                       u64* __restrict__ M, i64 ldM) {
+  extern __shared__ uint16_t tab[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const i64 wb = (i64)blockIdx.x * TPB + wv * 64;     // first word of this wave
-  int32_t cid[64];
-#pragma unroll
-  for (int s = 0; s < 64; ++s) {
-    const i64 j = (wb + s) * 64 + lane;
-    cid[s] = j < n ? ccls[j] : -1;
+  const i64 g = blockIdx.y;
+  const uint16_t* grow = RT16 + g * Ua;
+  if (USE_LDS) {
+    for (i64 c = threadIdx.x; c < Ua; c += TPB) tab[c] = grow[c];
+    __syncthreads();
   }
-  const i64 c0 = (i64)blockIdx.y * RT, c1 = c0 + RT < rows ? c0 + RT : rows;
-  for (i64 c = c0; c < c1; ++c) {
-    __syncthreads();
-    for (i64 w = threadIdx.x; w < ldR; w += TPB) row[w] = R[c * ldR + w];
-    __syncthreads();
-    u64 mine = 0;
+  const int nc = (int)(rows - 16 * g < 16 ? rows - 16 * g : 16);
+  for (int sub = 0; sub < SUB; ++sub) {
+    const i64 wb = ((i64)blockIdx.x * SUB + sub) * TPB + wv * 64;
+    if (wb >= ldM) break;                             // wave-uniform
+    const i64 w = wb + lane, j0 = w * 64;
+    uint32_t x[64];
+    if (j0 + 64 <= n) {
+      const int4* src = reinterpret_cast<const int4*>(ccls + j0);
 #pragma unroll
-    for (int s = 0; s < 64; ++s) {
-      const int32_t b = cid[s];
-      const bool bit = b >= 0 && ((row[b >> 6] >> (b & 63)) & 1ull);
-      const u64 bal = __ballot(bit);
-      if (lane == s) mine = bal;
+      for (int q = 0; q < 16; ++q) {
+        const int4 v = src[q];
+        x[4 * q] = (uint32_t)v.x;
+        x[4 * q + 1] = (uint32_t)v.y;
+        x[4 * q + 2] = (uint32_t)v.z;
+        x[4 * q + 3] = (uint32_t)v.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 64; ++k) x[k] = USE_LDS ? tab[x[k]] : grow[x[k]];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const i64 j = j0 + k;
+        x[k] = j < n ? (USE_LDS ? tab[ccls[j]] : grow[ccls[j]]) : 0u;
+      }
     }
-    if (wb + lane < ldM) {
-      for (int32_t m = moff[c]; m < moff[c + 1]; ++m) M[(i64)mem[m] * ldM + wb + lane] = mine;
+    const bool inside = w < ldM;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (t >= nc) break;                             // wave-uniform
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        lo |= ((x[k] >> t) & 1u) << k;
+        hi |= ((x[k + 32] >> t) & 1u) << k;
+      }
+      const u64 word = ((u64)hi << 32) | lo;
+      const i64 c = 16 * g + t;
+      if (inside)
+        for (int32_t m = moff[c]; m < moff[c + 1]; ++m) M[(i64)mem[m] * ldM + w] = word;
     }
   }
 }

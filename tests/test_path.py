@@ -157,3 +157,20 @@ def test_path_synthetic_seeds(seed):
             assert np.array_equal(dst.rows(0, n), ref), (hops, mode)
             dst.close()
     eng.close()
+
+
+@pytest.mark.gpu
+def test_path_expand_table_from_l2(monkeypatch):
+    """The expansion's L2-read variant (column-class tables too large for LDS,
+    forced here with KANO_TUNE=pathlds=0) writes the same matrix."""
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.synth import make_cluster
+    from oracle import kano_oracle as orc
+    cl = make_cluster(1200, 120, "sparse", seed=105)
+    eng = DeviceBuild(tables_from_cluster(cl))
+    monkeypatch.setenv("KANO_TUNE", "pathlds=0")
+    dst = DeviceBuild.empty(cl.n)
+    dst.path_from(eng, 2, "bitwise")
+    M = eng.rows(0, cl.n)
+    assert np.array_equal(dst.rows(0, cl.n), orc.path_c(M, cl.n, 2)[0])
