@@ -215,6 +215,15 @@ int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
  * steps on the MFMA, row classes, column classes, identity classes]. */
 int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info);
 
+/* The on-disk / tooling row format: rows of M as
+ * kano_py holds them, bitarray bytes in bitarray's default big-endian bit
+ * order (kano_py/kano/model.py:136-139,158-160; bitarray.tobytes(): bit j of
+ * a row is bit 7 - (j & 7) of byte j >> 3, pad bits zero), ceil(n / 8) bytes
+ * per row, rows [r0, r0 + nrows) of this shard.  kano_import_rows writes such
+ * rows back (an edit of M, like kano_put_rows; pad bits are cleared). */
+int kano_export_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint8_t* dst);
+int kano_import_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint8_t* src);
+
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);
 void kano_host_free(void* p);

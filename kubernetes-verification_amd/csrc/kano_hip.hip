@@ -2795,4 +2795,50 @@ int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info) {
   return path_impl(src, dst, hops, mode, info);
 }
 
+
+int kano_export_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint8_t* dst) {
+  KTRY(ensure_matrix(ctx));
+  if (nrows < 0 || r0 < ctx->r0 || r0 + nrows > ctx->r1 || (!dst && nrows > 0))
+    return fail(ctx, -EINVAL, "kano_export_rows: rows outside this shard");
+  const i64 nb = (ctx->n + 7) / 8;
+  if (nrows == 0 || nb == 0) return 0;
+  // staged through scratch in chunks of <= 64 MB
+  const i64 chunk = std::max<i64>(1, (64ll << 20) / nb);
+  KTRY(dalloc(ctx, ctx->scratch_words, (size_t)(std::min(chunk, (i64)nrows) * nb + 16)));
+  uint8_t* st = reinterpret_cast<uint8_t*>(ctx->scratch_words.p);
+  for (i64 c0 = 0; c0 < nrows; c0 += chunk) {
+    const i64 cr = std::min<i64>(chunk, nrows - c0);
+    const i64 q = (nb + 3) / 4;
+    hipLaunchKernelGGL(k_words_to_bytes, dim3(nblk(cr * q)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->M) + (r0 - ctx->r0 + c0) * ctx->ldM, ctx->ldM, cr, nb, st);
+    KLAUNCH();
+    KCHK(hipMemcpyAsync(dst + c0 * nb, st, (size_t)(cr * nb), hipMemcpyDeviceToHost, ctx->stream));
+    KTRY(sync(ctx));
+  }
+  return 0;
+}
+
+int kano_import_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint8_t* src) {
+  KTRY(ensure_matrix(ctx));
+  if (nrows < 0 || r0 < ctx->r0 || r0 + nrows > ctx->r1 || (!src && nrows > 0))
+    return fail(ctx, -EINVAL, "kano_import_rows: rows outside this shard");
+  const i64 nb = (ctx->n + 7) / 8;
+  if (nrows == 0 || nb == 0) return 0;
+  const i64 chunk = std::max<i64>(1, (64ll << 20) / nb);
+  KTRY(dalloc(ctx, ctx->scratch_words, (size_t)(std::min(chunk, (i64)nrows) * nb + 16)));
+  uint8_t* st = reinterpret_cast<uint8_t*>(ctx->scratch_words.p);
+  for (i64 c0 = 0; c0 < nrows; c0 += chunk) {
+    const i64 cr = std::min<i64>(chunk, nrows - c0);
+    KCHK(hipMemcpyAsync(st, src + c0 * nb, (size_t)(cr * nb), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_bytes_to_words, dim3(nblk(cr * ctx->ldM)), dim3(TPB), 0, ctx->stream, st,
+                       cr, nb, ctx->n, P_<u64>(ctx->M) + (r0 - ctx->r0 + c0) * ctx->ldM,
+                       ctx->ldM);
+    KLAUNCH();
+    KTRY(sync(ctx));
+  }
+  ctx->cols_valid = false;
+  ctx->rows_dirty = true;
+  return 0;
+}
+
 }  // extern "C"

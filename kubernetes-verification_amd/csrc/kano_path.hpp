@@ -374,4 +374,41 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
   }
 }
 
+// bitarray byte rows (kano_py's M rows, model.py:136-139,158-160, bitarray's
+// default big-endian bit order: bit j -> byte j >> 3, bit 7 - (j & 7)) from
+// LSB-first words and back.  One thread per 4 bytes of a row of nb bytes.
+__global__ __launch_bounds__(TPB) void k_words_to_bytes(const u64* __restrict__ M, i64 ldM,
+                                                        i64 nrows, i64 nb,
+                                                        uint8_t* __restrict__ out) {
+  const i64 q = (nb + 3) / 4;
+  const i64 t = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (t >= nrows * q) return;
+  const i64 r = t / q, k0 = (t % q) * 4;
+  const uint32_t w = reinterpret_cast<const uint32_t*>(M + r * ldM)[k0 >> 2];
+  // reverse the bits inside every byte: reverse the dword, then its bytes
+  const uint32_t v = __builtin_bswap32(__builtin_bitreverse32(w));
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if (k0 + b < nb) out[r * nb + k0 + b] = (uint8_t)(v >> (8 * b));
+}
+
+__global__ __launch_bounds__(TPB) void k_bytes_to_words(const uint8_t* __restrict__ in, i64 nrows,
+                                                        i64 nb, i64 nbits,
+                                                        u64* __restrict__ M, i64 ldM) {
+  const i64 t = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (t >= nrows * ldM) return;
+  const i64 r = t / ldM, w = t % ldM;
+  u64 x = 0;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const i64 k = w * 8 + b;
+    if (k < nb) x |= (u64)__builtin_bitreverse8(in[r * nb + k]) << (8 * b);
+  }
+  // pad bits past the row's length stay zero (bitarray zeroes them in
+  // tobytes(); a file may carry anything there)
+  const i64 j0 = w * 64;
+  if (j0 + 64 > nbits) x = j0 >= nbits ? 0ull : x & ((1ull << (nbits - j0)) - 1ull);
+  M[r * ldM + w] = x;
+}
+
 }  // namespace kano

@@ -142,6 +142,20 @@ class DeviceBuild:
         keys = ("steps", "steps_run", "mfma_steps", "row_classes", "col_classes", "identity")
         return {k: int(v) for k, v in zip(keys, info)}
 
+    def export_rows(self, r0: int, nrows: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Rows as bitarray bytes (big-endian bit order), (nrows, ceil(n/8))."""
+        nb = (self.tables.n + 7) >> 3
+        if out is None:
+            out = np.empty((max(nrows, 0), nb), dtype=np.uint8)
+        self._chk(self.lib.kano_export_rows(self.ctx, int(r0), int(nrows), _ptr(out)),
+                  "kano_export_rows")
+        return out
+
+    def import_rows(self, r0: int, rows: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.uint8)
+        self._chk(self.lib.kano_import_rows(self.ctx, int(r0), int(rows.shape[0]), _ptr(rows)),
+                  "kano_import_rows")
+
     # -- checks ---------------------------------------------------------
     def col_checks(self) -> Tuple[np.ndarray, np.ndarray]:
         W = self.W

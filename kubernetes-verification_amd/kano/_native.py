@@ -53,6 +53,8 @@ SIGNATURES = {
                                     c_int64, POINTER(c_int64)]),
     "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "kano_export_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
+    "kano_import_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 from abc import abstractmethod
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, TypeVar
+from typing import Any, Dict, List, Optional, Tuple, TypeVar
 
 try:                                    # the reference imports typing_extensions
     from typing_extensions import Protocol
@@ -407,6 +407,77 @@ class ReachabilityMatrix:
     @property
     def engine(self):
         return self._engine
+
+    # ---- on-disk / tooling format -------------
+    # Not in kano_py: its rows are bitarrays (model.py:136-139), and this
+    # format is their bytes.  File: b"KANOMAT1", then n, r0, r1, row_bytes as
+    # little-endian u64, then rows r0..r1-1, each bitarray(row).tobytes()
+    # (big-endian bit order, ceil(n/8) bytes, pad bits zero).  A row shard
+    # (multi-GPU, kano/shard.py) writes its own range; shard files of one
+    # matrix concatenate in row order.
+    MAGIC = b"KANOMAT1"
+
+    def row_bytes(self, r0: int = 0, nrows: Optional[int] = None) -> np.ndarray:
+        """Rows [r0, r0+nrows) as bitarray bytes, shape (nrows, ceil(n/8))."""
+        n = self.container_size
+        if nrows is None:
+            nrows = n - r0
+        return self._engine.export_rows(r0, nrows)
+
+    def save(self, path: str, rows: Optional[Tuple[int, int]] = None,
+             chunk_bytes: int = 64 << 20) -> None:
+        n = self.container_size
+        r0, r1 = rows if rows is not None else (0, n)
+        nb = (n + 7) >> 3
+        step = max(1, chunk_bytes // max(nb, 1))
+        with open(path, "wb") as f:
+            f.write(self.MAGIC)
+            f.write(np.array([n, r0, r1, nb], dtype="<u8").tobytes())
+            for a in range(r0, r1, step):
+                f.write(self._engine.export_rows(a, min(step, r1 - a)).tobytes())
+
+    @staticmethod
+    def load(paths, device: int = 0) -> "ReachabilityMatrix":
+        """A matrix from one file or from row-shard files covering [0, n)."""
+        from ._engine import DeviceBuild
+        if isinstance(paths, (str, bytes)) or hasattr(paths, "__fspath__"):
+            paths = [paths]
+        heads = []
+        for p in paths:
+            with open(p, "rb") as f:
+                if f.read(8) != ReachabilityMatrix.MAGIC:
+                    raise ValueError(f"{p}: not a kano matrix file")
+                heads.append((np.frombuffer(f.read(32), dtype="<u8").astype(np.int64), p))
+        n = int(heads[0][0][0])
+        heads.sort(key=lambda h: int(h[0][1]))
+        pos = 0
+        for h, p in heads:
+            hn, r0, r1, nb = (int(x) for x in h)
+            if hn != n or nb != (n + 7) >> 3 or r0 != pos or r1 < r0:
+                raise ValueError(f"{p}: shard [{r0}, {r1}) of n={hn} does not continue at {pos}")
+            pos = r1
+        if pos != n:
+            raise ValueError(f"shards cover [0, {pos}) of {n} rows")
+        m = ReachabilityMatrix.__new__(ReachabilityMatrix)
+        m.container_size = n
+        m._engine = DeviceBuild.empty(n, device=device)
+        m._containers = None
+        m._policies = None
+        m._ncontainers = n
+        m._lists = None
+        nb = (n + 7) >> 3
+        for h, p in heads:
+            r0, r1 = int(h[1]), int(h[2])
+            step = max(1, (64 << 20) // max(nb, 1))
+            with open(p, "rb") as f:
+                f.seek(40)
+                for a in range(r0, r1, step):
+                    k = min(step, r1 - a)
+                    buf = np.frombuffer(f.read(k * nb), dtype=np.uint8)
+                    if buf.size != k * nb:
+                        raise ValueError(f"{p}: truncated")
+                    m._engine.import_rows(a, buf.reshape(k, nb))
+        return m
 
 
 def _fit(b: BitArray, n: int) -> np.ndarray:
