@@ -2614,9 +2614,23 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
     if (!g.identity) {
       KTRY(dalloc(ctx, ctx->pT, sizeof(u64) * g.Ua * g.ldR));
       const i64 nch = (g.ldR + 255) / 256;
-      hipLaunchKernelGGL(k_path_t<4>, dim3(nblk(g.Ua * nch, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                         g.base, g.ldR, P_<int32_t>(src->rc.cls), P_<int32_t>(src->cc.moff),
-                         P_<int32_t>(src->cc.mem), g.Ua, g.KW, nch, P_<u64>(ctx->pT));
+      if (g.KW <= 4 && g.Ua <= 65536) {
+        // narrow class rows: slices of the column classes' member lists
+        KTRY(dalloc(ctx, ctx->pB, sizeof(int32_t) * (g.Ua + 1)));
+        KCHK(hipMemsetAsync(ctx->pT.p, 0, sizeof(u64) * g.Ua * g.ldR, ctx->stream));
+        hipLaunchKernelGGL(k_path_t_items, dim3(1), dim3(TPB), 0, ctx->stream,
+                           P_<int32_t>(src->cc.moff), g.Ua, P_<int32_t>(ctx->pB));
+        KLAUNCH();
+        const i64 nitems = (n + 64 * NT_SLICE - 1) / (64 * NT_SLICE) + g.Ua;   // upper bound
+        hipLaunchKernelGGL(k_path_t_narrow, dim3(nblk(nitems, TPB / 64)), dim3(TPB), 0,
+                           ctx->stream, g.base, g.ldR, P_<int32_t>(src->rc.cls),
+                           P_<int32_t>(src->cc.moff), P_<int32_t>(src->cc.mem), g.Ua, g.KW,
+                           P_<int32_t>(ctx->pB), nitems, P_<u64>(ctx->pT));
+      } else
+        hipLaunchKernelGGL(k_path_t<4>, dim3(nblk(g.Ua * nch, TPB / 64)), dim3(TPB), 0,
+                           ctx->stream, g.base, g.ldR, P_<int32_t>(src->rc.cls),
+                           P_<int32_t>(src->cc.moff), P_<int32_t>(src->cc.mem), g.Ua, g.KW, nch,
+                           P_<u64>(ctx->pT));
       KLAUNCH();
       g.T = P_<u64>(ctx->pT);
     }
@@ -2734,17 +2748,25 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
                          ctx->stream, Rb[ri], g.ldR, g.rows, RW, CG, g.Ua, ctx->pA.p, g.Ua, ng);
       KLAUNCH();
       constexpr int SUB = 2;
-      const dim3 grid(nblk(ldM, (i64)TPB * SUB), (unsigned)ng);
+      // member slices when the (group, word range) blocks alone cannot fill
+      // the chip and the classes are large (broad selectors)
+      const i64 gxy = (i64)nblk(ldM, (i64)TPB * SUB) * ng;
+      const i64 avg_members = (n + g.rows - 1) / g.rows;
+      const i64 Z = std::max<i64>(1, std::min<i64>({(2048 + gxy - 1) / gxy, avg_members / 8, 64}));
+      const dim3 grid(nblk(ldM, (i64)TPB * SUB), (unsigned)ng, (unsigned)Z);
       const size_t lds = sizeof(uint16_t) * (size_t)g.Ua;
       const uint16_t* rt16 = reinterpret_cast<const uint16_t*>(ctx->pA.p);
-      if (lds <= 64 * 1024 && ctx->path_lds)
-        hipLaunchKernelGGL((k_path_expand16<SUB, true>), grid, dim3(TPB), lds, ctx->stream, rt16,
-                           g.Ua, g.rows, P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
+      const bool use_lds = lds <= 64 * 1024 && ctx->path_lds;
+      const bool staged = avg_members >= 16;
+      auto launch = [&](auto kern, size_t shm) {
+        hipLaunchKernelGGL(kern, grid, dim3(TPB), shm, ctx->stream, rt16, g.Ua, g.rows,
+                           P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
                            P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM);
-      else
-        hipLaunchKernelGGL((k_path_expand16<SUB, false>), grid, dim3(TPB), 0, ctx->stream, rt16,
-                           g.Ua, g.rows, P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
-                           P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM);
+      };
+      if (use_lds && staged) launch(k_path_expand16<SUB, true, true>, lds);
+      else if (use_lds) launch(k_path_expand16<SUB, true, false>, lds);
+      else if (staged) launch(k_path_expand16<SUB, false, true>, 0);
+      else launch(k_path_expand16<SUB, false, false>, 0);
       KLAUNCH();
     }
   } else if (n > 0 && W > 0) {

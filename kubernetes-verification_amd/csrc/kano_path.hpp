@@ -65,6 +65,74 @@ __global__ __launch_bounds__(TPB) void k_path_t(const u64* __restrict__ Mc, i64 
   }
 }
 
+// The same for narrow class rows (KW <= 4 words) and large classes: the 64
+// lanes of a wave split the class's members, each ORs its members' Mc rows
+// into registers, and the wave reduces.  One wave per column class.
+// Work item = (class b, slice of 64 * NT_SLICE members): the wave ORs into T
+// (zeroed) with one atomic per word, so large classes spread over many waves.
+constexpr int NT_SLICE = 4;
+__global__ __launch_bounds__(TPB) void k_path_t_narrow(const u64* __restrict__ Mc, i64 ldC,
+                                                       const int32_t* __restrict__ rcls,
+                                                       const int32_t* __restrict__ moff,
+                                                       const int32_t* __restrict__ mem, i64 Ua,
+                                                       i64 KW, const int32_t* __restrict__ ioff,
+                                                       i64 nitems, u64* __restrict__ T) {
+  const int lane = threadIdx.x & 63;
+  const i64 item = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  if (item >= nitems) return;                         // wave-uniform
+  // class of this item: ioff[b] = first item of class b (binary search)
+  i64 lo = 0, hi = Ua - 1;
+  while (lo < hi) {
+    const i64 mid = (lo + hi + 1) >> 1;
+    if (ioff[mid] <= item) lo = mid; else hi = mid - 1;
+  }
+  const i64 b = lo;
+  const int32_t mb = moff[b] + (int32_t)(item - ioff[b]) * 64 * NT_SLICE;
+  const int32_t me = min(moff[b + 1], mb + 64 * NT_SLICE);
+  u64 acc[4] = {0, 0, 0, 0};
+  int32_t prev = -1;
+  for (int32_t m = mb + lane; m < me; m += 64) {
+    const int32_t r = rcls[mem[m]];
+    if (r == prev) continue;
+    prev = r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < KW) acc[k] |= Mc[(i64)r * ldC + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc[k] |= __shfl_xor(acc[k], d, 64);
+  }
+  const u64 mine = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
+  if (lane < KW && lane < 4 && mine) atomicOr(T + b * ldC + lane, mine);
+}
+
+// items per class for k_path_t_narrow: ioff[b] = sum_{b' < b} ceil(size / slice)
+// (one block, serial scan over Ua <= a few thousand classes is not needed:
+// a wave-wide scan per 64 classes)
+__global__ __launch_bounds__(TPB) void k_path_t_items(const int32_t* __restrict__ moff, i64 Ua,
+                                                      int32_t* __restrict__ ioff) {
+  __shared__ int32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (i64 b0 = 0; b0 <= Ua; b0 += TPB) {
+    const i64 b = b0 + threadIdx.x;
+    int32_t v = 0;
+    if (b < Ua) {
+      const int32_t sz = moff[b + 1] - moff[b];
+      v = sz > 0 ? (sz + 64 * NT_SLICE - 1) / (64 * NT_SLICE) : 0;
+    }
+    __shared__ int32_t tmp[TPB / 64];
+    int32_t total;
+    const int32_t ex = block_excl_scan(v, tmp, total);
+    if (b <= Ua) ioff[b] = carry + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += total;
+    __syncthreads();
+  }
+}
+
 // One semi-naive step.  Wave = (row r, chunk of 64*CW words): new bits
 // acc = OR_{b in D[r]} T[b] over the chunk, Dn[r] = acc & ~R[r], R[r] |= Dn[r];
 // cnt += popcount(Dn) (one atomic per wave).  D and Dn have pitch ldR, T ldT.
@@ -311,19 +379,27 @@ __global__ __launch_bounds__(TPB) void k_popcount_words(const u64* __restrict__ 
 }
 
 // P[i] bit j = R[rc(i)][cc(j)].  Block = (16 row classes of group
-// blockIdx.y, words [blockIdx.x * 256 * SUB, + 256 * SUB)).  The group's bits
-// per column class (tab[c], 16 bits, from k_bit_transpose<true>) sit in LDS
-// (USE_LDS) or are read from L2.  Lane l owns word w = wb + l: it loads the
-// column classes of its 64 pods (all loads in flight at once), looks up their
-// 16-bit entries, and packs bit t of entry k into bit k of the word of class
-// t; each member row of a class then gets one 512-byte store per wave.
-template <int SUB, bool USE_LDS>
+// blockIdx.y, words [blockIdx.x * 256 * SUB, + 256 * SUB), member slice z of
+// Z = gridDim.z: member k of a class goes to slice k mod Z, so that few large
+// classes (broad selectors) still fill the chip).  The group's bits per
+// column class (tab[c], 16 bits, from k_bit_transpose<true>) sit in LDS
+// (USE_LDS) or are read from L2.  Per 256-word chunk, lane l of wave v owns
+// word w = 64 v + l: it loads the column classes of its 64 pods (all loads in
+// flight), looks up their 16-bit entries and packs bit t of entry k into bit
+// k of class t's word, kept in LDS.  Then the waves stream the chunk to the
+// member rows, one 2-KB row piece per wave at a time (16-byte stores) --
+// STAGED, for large classes; otherwise each lane stores its own word to every
+// member row right away (512 bytes per wave store; measured faster with ~5
+// members per class, C3: 0.42 vs 0.50 ms; staged C4: 0.45 vs 0.72 ms).
+template <int SUB, bool USE_LDS, bool STAGED>
 __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restrict__ RT16, i64 Ua,
                                                        i64 rows, const int32_t* __restrict__ ccls,
                                                        i64 n, const int32_t* __restrict__ moff,
                                                        const int32_t* __restrict__ mem,
                                                        u64* __restrict__ M, i64 ldM) {
+  const int32_t Z = (int32_t)gridDim.z, z = (int32_t)blockIdx.z;
   extern __shared__ uint16_t tab[];
+  __shared__ u64 cw[STAGED ? 16 : 1][TPB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const i64 g = blockIdx.y;
   const uint16_t* grow = RT16 + g * Ua;
@@ -333,9 +409,9 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
   }
   const int nc = (int)(rows - 16 * g < 16 ? rows - 16 * g : 16);
   for (int sub = 0; sub < SUB; ++sub) {
-    const i64 wb = ((i64)blockIdx.x * SUB + sub) * TPB + wv * 64;
-    if (wb >= ldM) break;                             // wave-uniform
-    const i64 w = wb + lane, j0 = w * 64;
+    const i64 cb = ((i64)blockIdx.x * SUB + sub) * TPB;   // first word of the chunk
+    if (cb >= ldM) break;                                 // block-uniform
+    const i64 w = cb + wv * 64 + lane, j0 = w * 64;
     uint32_t x[64];
     if (j0 + 64 <= n) {
       const int4* src = reinterpret_cast<const int4*>(ccls + j0);
@@ -356,10 +432,8 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
         x[k] = j < n ? (USE_LDS ? tab[ccls[j]] : grow[ccls[j]]) : 0u;
       }
     }
-    const bool inside = w < ldM;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      if (t >= nc) break;                             // wave-uniform
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
@@ -367,10 +441,48 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
         hi |= ((x[k + 32] >> t) & 1u) << k;
       }
       const u64 word = ((u64)hi << 32) | lo;
-      const i64 c = 16 * g + t;
-      if (inside)
-        for (int32_t m = moff[c]; m < moff[c + 1]; ++m) M[(i64)mem[m] * ldM + w] = word;
+      if (STAGED) {
+        cw[t][wv * 64 + lane] = word;
+      } else if (t < nc && w < ldM) {
+        const i64 c = 16 * g + t;
+        const int32_t m1 = moff[c + 1];
+        int32_t m = moff[c] + z;
+        for (; m + 3 * Z < m1; m += 4 * Z) {   // four member rows' stores in flight
+          const int32_t a0 = mem[m], a1 = mem[m + Z], a2 = mem[m + 2 * Z], a3 = mem[m + 3 * Z];
+          M[(i64)a0 * ldM + w] = word;
+          M[(i64)a1 * ldM + w] = word;
+          M[(i64)a2 * ldM + w] = word;
+          M[(i64)a3 * ldM + w] = word;
+        }
+        for (; m < m1; m += Z) M[(i64)mem[m] * ldM + w] = word;
+      }
     }
+    if (!STAGED) continue;
+    __syncthreads();
+    // stream: the (class, member) pieces of this slice, round-robin over waves
+    const i64 nw = ldM - cb < TPB ? ldM - cb : TPB;       // words in this chunk
+    int q = 0;
+    for (int t = 0; t < nc; ++t) {
+      const i64 c = 16 * g + t;
+      const int32_t m1 = moff[c + 1];
+      for (int32_t m = moff[c] + z; m < m1; m += Z, ++q) {
+        if ((q & 3) != wv) continue;
+        u64* dst = M + (i64)mem[m] * ldM + cb;
+#pragma unroll
+        for (int h = 0; h < TPB / 128; ++h) {
+          const int k = 2 * (h * 64 + lane);
+          if (k + 1 < nw) {
+            u64x2 v;
+            v.x = cw[t][k];
+            v.y = cw[t][k + 1];
+            *reinterpret_cast<u64x2*>(dst + k) = v;
+          } else if (k < nw) {
+            dst[k] = cw[t][k];
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
