@@ -224,6 +224,26 @@ int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info);
 int kano_export_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint8_t* dst);
 int kano_import_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint8_t* src);
 
+/* Incremental policy updates.  The matrix after
+ * the update equals ReachabilityMatrix.build_matrix over the updated policy
+ * list (kano_py/kano/model.py:125-165); only rows the changed policies select
+ * are written.  Policy ids are stable: the build's 0..P-1, then added ones in
+ * order (first_id returns the batch's first).  kano_add_policies takes the
+ * new policies' working terms as kano_set_policies does; term columns
+ * >= the build's ncols index ncols_x extra pod columns (xval[c*n + i], the
+ * batch's new keys / custom matchers, appended to earlier batches' extras).
+ * kano_remove_policies marks ids removed and rewrites the rows they selected
+ * from the alive policies (-EINVAL after an explicit edit of M).  Afterwards
+ * the matrix reads as an edited one; kano_build / kano_verify rebuild from
+ * the uploaded tables and drop the updates.  kano_added_policy_sets returns
+ * an added policy's working_select_set / working_allow_set (model.py:119-121). */
+int kano_add_policies(kano_ctx* ctx, int64_t Pn, int32_t ncols_x, const int32_t* xval,
+                      const int64_t* sel_off, const int32_t* sel_col, const int32_t* sel_val,
+                      const int64_t* alw_off, const int32_t* alw_col, const int32_t* alw_val,
+                      int64_t* first_id);
+int kano_remove_policies(kano_ctx* ctx, int64_t count, const int64_t* ids);
+int kano_added_policy_sets(kano_ctx* ctx, int64_t id, uint64_t* sel, uint64_t* allow);
+
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);
 void kano_host_free(void* p);

@@ -42,6 +42,7 @@
 #include "kano_hip.h"
 #include "kano_kernels.hpp"
 #include "kano_path.hpp"
+#include "kano_inc.hpp"
 
 using namespace kano;
 
@@ -166,6 +167,12 @@ struct kano_ctx {
   // kano_path (in the destination context): T, R / delta ping-pong buffers,
   // the MFMA operands, the step counter
   DBuf pT, pR[2], pD[2], pA, pB, pcnt;
+  // incremental updates: added policies' pod-level sets (A x W words each),
+  // their extra label columns, alive flags over build + added ids
+  DBuf xv, asel, aalw, iterm, idead, irows;
+  i64 inc_A = 0, inc_acap = 0, inc_xcols = 0;
+  std::vector<uint8_t> dead;       // P + inc_A entries
+  bool user_edited = false;        // put_rows / set_bit / import: removal cannot rewrite rows
   int path_dens = 8;         // kano_path auto: MFMA step when the delta holds more than
                              // path_dens % of the class-level bits
   int path_tm = 2;           // k_path_mfma rows tiles per wave (1, 2 or 4)
@@ -1510,7 +1517,9 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff,
                   &ctx->gids,
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
-                  &ctx->pA,     &ctx->pB,      &ctx->pcnt};
+                  &ctx->pA,     &ctx->pB,      &ctx->pcnt,
+                  &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
+                  &ctx->irows};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1784,6 +1793,11 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KTRY(stage_mark(ctx, 4, ctx->stream));
   ctx->cols_valid = true;
   ctx->built = true;
+  // a build discards earlier incremental updates and edits
+  ctx->inc_A = 0;
+  ctx->inc_xcols = 0;
+  ctx->dead.assign((size_t)ctx->P, 0);
+  ctx->user_edited = false;
   return 0;
 }
 
@@ -1887,6 +1901,7 @@ int kano_put_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint64_t* src)
   KTRY(sync(ctx));
   ctx->cols_valid = false;
   ctx->rows_dirty = true;
+  ctx->user_edited = true;
   return 0;
 }
 
@@ -1931,6 +1946,7 @@ int kano_set_bit(kano_ctx* ctx, int64_t i, int64_t j, int value) {
   KTRY(sync(ctx));
   ctx->cols_valid = false;
   ctx->rows_dirty = true;
+  ctx->user_edited = true;
   return 0;
 }
 
@@ -2860,7 +2876,176 @@ int kano_import_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint8_t* sr
   }
   ctx->cols_valid = false;
   ctx->rows_dirty = true;
+  ctx->user_edited = true;
   return 0;
+}
+
+
+// ---------------------------------------------------------------------------
+// Incremental policy updates (kano_inc.hpp)
+
+int kano_add_policies(kano_ctx* ctx, int64_t Pn, int32_t ncols_x, const int32_t* xval,
+                      const int64_t* sel_off, const int32_t* sel_col, const int32_t* sel_val,
+                      const int64_t* alw_off, const int32_t* alw_col, const int32_t* alw_val,
+                      int64_t* first_id) {
+  KTRY(ensure_matrix(ctx));
+  if (Pn < 0 || ncols_x < 0 || (Pn > 0 && (!sel_off || !alw_off)) ||
+      (ncols_x > 0 && !xval && ctx->n > 0))
+    return fail(ctx, -EINVAL, "kano_add_policies: bad arguments");
+  const i64 n = ctx->n, W = ctx->W;
+  if (first_id) *first_id = ctx->P + ctx->inc_A;
+  if (Pn == 0) return 0;
+  const i64 ns = sel_off[Pn], na = alw_off[Pn];
+  const int32_t ncol_all = ctx->ncols + (int32_t)(ctx->inc_xcols + ncols_x);
+  for (i64 t = 0; t < ns; ++t)
+    if (sel_col[t] < 0 || sel_col[t] >= ncol_all)
+      return fail(ctx, -EINVAL, "kano_add_policies: select term column out of range");
+  for (i64 t = 0; t < na; ++t)
+    if (alw_col[t] < 0 || alw_col[t] >= ncol_all)
+      return fail(ctx, -EINVAL, "kano_add_policies: allow term column out of range");
+  // the extra columns append to the ones earlier additions brought
+  if (ncols_x > 0 && n > 0) {
+    const i64 have = ctx->inc_xcols * n, add = (i64)ncols_x * n;
+    DBuf grown;
+    KTRY(dalloc(ctx, grown, sizeof(int32_t) * (have + add)));
+    if (have > 0)
+      KCHK(hipMemcpyAsync(grown.p, ctx->xv.p, sizeof(int32_t) * have, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    KCHK(hipMemcpyAsync(P_<int32_t>(grown) + have, xval, sizeof(int32_t) * add,
+                        hipMemcpyHostToDevice, ctx->stream));
+    KTRY(sync(ctx));
+    dfree(ctx->xv);
+    ctx->xv = grown;
+  }
+  ctx->inc_xcols += ncols_x;
+  // pod-level sets of the added policies (A x W words each side)
+  const i64 A0 = ctx->inc_A, A1 = A0 + Pn;
+  if (A1 > ctx->inc_acap) {
+    const i64 cap = std::max<i64>(A1, 2 * ctx->inc_acap);
+    DBuf s2, a2;
+    KTRY(dalloc(ctx, s2, sizeof(u64) * std::max<i64>(1, cap * W)));
+    KTRY(dalloc(ctx, a2, sizeof(u64) * std::max<i64>(1, cap * W)));
+    if (A0 > 0 && W > 0) {
+      KCHK(hipMemcpyAsync(s2.p, ctx->asel.p, sizeof(u64) * A0 * W, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+      KCHK(hipMemcpyAsync(a2.p, ctx->aalw.p, sizeof(u64) * A0 * W, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    }
+    KTRY(sync(ctx));
+    dfree(ctx->asel);
+    dfree(ctx->aalw);
+    ctx->asel = s2;
+    ctx->aalw = a2;
+    ctx->inc_acap = cap;
+  }
+  // the batch's terms: [soff | aoff] (i64) then [scol | sval | acol | aval] (i32)
+  const size_t hdr = sizeof(i64) * 2 * (Pn + 1);
+  const size_t body = sizeof(int32_t) * 2 * (ns + na);
+  std::vector<uint8_t> h(hdr + body + 16);
+  std::memcpy(h.data(), sel_off, sizeof(i64) * (Pn + 1));
+  std::memcpy(h.data() + sizeof(i64) * (Pn + 1), alw_off, sizeof(i64) * (Pn + 1));
+  int32_t* hb = reinterpret_cast<int32_t*>(h.data() + hdr);
+  if (ns) std::memcpy(hb, sel_col, sizeof(int32_t) * ns);
+  if (ns) std::memcpy(hb + ns, sel_val, sizeof(int32_t) * ns);
+  if (na) std::memcpy(hb + 2 * ns, alw_col, sizeof(int32_t) * na);
+  if (na) std::memcpy(hb + 2 * ns + na, alw_val, sizeof(int32_t) * na);
+  KTRY(dalloc(ctx, ctx->iterm, h.size()));
+  KCHK(hipMemcpyAsync(ctx->iterm.p, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+  const i64* d_soff = P_<i64>(ctx->iterm);
+  const i64* d_aoff = d_soff + (Pn + 1);
+  const int32_t* d_b = reinterpret_cast<const int32_t*>(P_<uint8_t>(ctx->iterm) + hdr);
+  u64* sel = P_<u64>(ctx->asel) + A0 * W;
+  u64* alw = P_<u64>(ctx->aalw) + A0 * W;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_inc_eval, dim3(nblk(n), (unsigned)Pn, 2), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->pv), n, ctx->ncols, P_<int32_t>(ctx->xv), d_soff, d_b,
+                       d_b + ns, d_aoff, d_b + 2 * ns, d_b + 2 * ns + na, W, sel, alw);
+    KLAUNCH();
+    const i64 rl = rows_local(ctx);
+    if (rl > 0)
+      hipLaunchKernelGGL(k_inc_or, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
+                         P_<u64>(ctx->asel), P_<u64>(ctx->aalw), W, A0, Pn, ctx->r0, rl,
+                         P_<u64>(ctx->M), ctx->ldM);
+    KLAUNCH();
+  }
+  KTRY(sync(ctx));
+  ctx->inc_A = A1;
+  ctx->dead.resize((size_t)(ctx->P + A1), 0);
+  ctx->cols_valid = false;
+  ctx->rows_dirty = true;
+  return 0;
+}
+
+int kano_remove_policies(kano_ctx* ctx, int64_t count, const int64_t* ids) {
+  KTRY(ensure_matrix(ctx));
+  if (count < 0 || (count > 0 && !ids)) return fail(ctx, -EINVAL, "kano_remove_policies");
+  if (ctx->user_edited)
+    return fail(ctx, -EINVAL, "kano_remove_policies: the matrix was edited; rebuild instead");
+  const i64 Ptot = ctx->P + ctx->inc_A;
+  std::vector<uint8_t> newdead((size_t)std::max<i64>(1, Ptot), 0);
+  i64 fresh = 0;
+  for (i64 k = 0; k < count; ++k) {
+    if (ids[k] < 0 || ids[k] >= Ptot) return fail(ctx, -EINVAL, "kano_remove_policies: bad id");
+    if (ctx->dead[ids[k]]) return fail(ctx, -EINVAL, "kano_remove_policies: id already removed");
+    if (!newdead[ids[k]]) ++fresh;
+    newdead[ids[k]] = 1;
+  }
+  if (fresh == 0) return 0;
+  for (i64 p = 0; p < Ptot; ++p) ctx->dead[p] |= newdead[p];
+  const i64 n = ctx->n, W = ctx->W, rl = rows_local(ctx);
+  // [newdead | dead] flags, the row list, its count
+  KTRY(dalloc(ctx, ctx->idead, 2 * (size_t)std::max<i64>(1, Ptot) + 16));
+  KCHK(hipMemcpyAsync(ctx->idead.p, newdead.data(), (size_t)Ptot, hipMemcpyHostToDevice,
+                      ctx->stream));
+  KCHK(hipMemcpyAsync(P_<uint8_t>(ctx->idead) + Ptot, ctx->dead.data(), (size_t)Ptot,
+                      hipMemcpyHostToDevice, ctx->stream));
+  KTRY(dalloc(ctx, ctx->irows, sizeof(int32_t) * std::max<i64>(1, rl) + 64));
+  u64* cnt = reinterpret_cast<u64*>(P_<int32_t>(ctx->irows) + std::max<i64>(1, rl) + 8);
+  cnt = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(cnt) + 7) & ~(uintptr_t)7);
+  KCHK(hipMemsetAsync(cnt, 0, sizeof(u64), ctx->stream));
+  const bool classes = ctx->rc.U > 0 && rl > 0;
+  if (rl > 0) {
+    hipLaunchKernelGGL(k_inc_mark, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream,
+                       classes ? P_<int32_t>(ctx->rc.cls) : (const int32_t*)nullptr,
+                       P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<uint8_t>(ctx->idead),
+                       ctx->P, P_<u64>(ctx->asel), W, ctx->inc_A, ctx->r0, rl,
+                       P_<int32_t>(ctx->irows), cnt);
+    KLAUNCH();
+  }
+  u64 nrows = 0;
+  KCHK(hipMemcpyAsync(&nrows, cnt, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  KTRY(sync(ctx));
+  if (nrows > 0) {
+    const size_t lds = sizeof(u64) * (size_t)std::max<i64>(1, ctx->ldC);
+    if (lds > 64 * 1024) return fail(ctx, -ENOTSUP, "kano_remove_policies: too many column classes");
+    hipLaunchKernelGGL(k_inc_rewrite, dim3((unsigned)nrows), dim3(TPB), lds, ctx->stream,
+                       P_<int32_t>(ctx->irows),
+                       classes ? P_<int32_t>(ctx->rc.cls) : (const int32_t*)nullptr,
+                       P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
+                       P_<uint8_t>(ctx->idead) + Ptot, ctx->P, P_<u64>(ctx->AC), ctx->ldC,
+                       P_<int32_t>(ctx->cc.cls), n, P_<u64>(ctx->asel), P_<u64>(ctx->aalw), W,
+                       ctx->inc_A, ctx->r0, P_<u64>(ctx->M), ctx->ldM);
+    KLAUNCH();
+  }
+  KTRY(sync(ctx));
+  ctx->cols_valid = false;
+  ctx->rows_dirty = true;
+  return 0;
+}
+
+int kano_added_policy_sets(kano_ctx* ctx, int64_t id, uint64_t* sel, uint64_t* allow) {
+  KTRY(ensure_matrix(ctx));
+  const i64 q = id - ctx->P;
+  if (q < 0 || q >= ctx->inc_A) return fail(ctx, -EINVAL, "kano_added_policy_sets: bad id");
+  const i64 W = ctx->W;
+  if (W == 0) return 0;
+  if (sel)
+    KCHK(hipMemcpyAsync(sel, P_<u64>(ctx->asel) + q * W, sizeof(u64) * W, hipMemcpyDeviceToHost,
+                        ctx->stream));
+  if (allow)
+    KCHK(hipMemcpyAsync(allow, P_<u64>(ctx->aalw) + q * W, sizeof(u64) * W,
+                        hipMemcpyDeviceToHost, ctx->stream));
+  return sync(ctx);
 }
 
 }  // extern "C"

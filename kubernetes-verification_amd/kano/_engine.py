@@ -156,6 +156,34 @@ class DeviceBuild:
         self._chk(self.lib.kano_import_rows(self.ctx, int(r0), int(rows.shape[0]), _ptr(rows)),
                   "kano_import_rows")
 
+    # -- incremental updates ---------------------
+    def add_policies(self, xval: np.ndarray, sel_csr, alw_csr) -> int:
+        """Append policies (terms in this build's id space, kano._intern.
+        intern_more); returns the first new engine id."""
+        so, sc, sv = (np.ascontiguousarray(a, dtype=d) for a, d in
+                      zip(sel_csr, (np.int64, np.int32, np.int32)))
+        ao, ac, av = (np.ascontiguousarray(a, dtype=d) for a, d in
+                      zip(alw_csr, (np.int64, np.int32, np.int32)))
+        xv = np.ascontiguousarray(xval, dtype=np.int32)
+        first = c_int64(0)
+        self._chk(self.lib.kano_add_policies(
+            self.ctx, int(so.shape[0] - 1), int(xv.shape[0]), _ptr(xv), _ptr(so), _ptr(sc),
+            _ptr(sv), _ptr(ao), _ptr(ac), _ptr(av), byref(first)), "kano_add_policies")
+        return int(first.value)
+
+    def remove_policies(self, ids) -> None:
+        a = np.ascontiguousarray(np.asarray(ids, dtype=np.int64).reshape(-1))
+        self._chk(self.lib.kano_remove_policies(self.ctx, int(a.shape[0]), _ptr(a)),
+                  "kano_remove_policies")
+
+    def added_policy_sets(self, eid: int) -> Tuple[np.ndarray, np.ndarray]:
+        W = self.W
+        s = np.zeros(W, dtype=np.uint64)
+        a = np.zeros(W, dtype=np.uint64)
+        self._chk(self.lib.kano_added_policy_sets(self.ctx, int(eid), _ptr(s), _ptr(a)),
+                  "kano_added_policy_sets")
+        return s, a
+
     # -- checks ---------------------------------------------------------
     def col_checks(self) -> Tuple[np.ndarray, np.ndarray]:
         W = self.W
@@ -211,6 +239,9 @@ class DeviceBuild:
                   "kano_set_bit")
 
     def policy_sets(self, p: int, sel: bool = True, allow: bool = True):
+        if self.tables is not None and p >= self.tables.P:   # an added policy
+            s, a = self.added_policy_sets(p)
+            return (s if sel else None), (a if allow else None)
         W = self.W
         s = np.zeros(W, dtype=np.uint64) if sel else None
         a = np.zeros(W, dtype=np.uint64) if allow else None

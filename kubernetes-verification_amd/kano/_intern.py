@@ -46,6 +46,9 @@ class Tables:
     alw_off: np.ndarray
     alw_col: np.ndarray
     alw_val: np.ndarray
+    # interning state of intern(): lets intern_more() put later policies in
+    # the same id space (incremental updates)
+    state: Any = None
 
     @property
     def P(self) -> int:
@@ -180,7 +183,77 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
 
     so, sc, sv = csr(0)
     ao, ac, av = csr(1)
-    return Tables(n, ncols, pod_val, so, sc, sv, ao, ac, av)
+    st = _InternState(labels, keys, col_of_key, indexes, ncols)
+    return Tables(n, ncols, pod_val, so, sc, sv, ao, ac, av, st)
+
+
+class _InternState:
+    __slots__ = ("labels", "keys", "col_of_key", "indexes", "ncols")
+
+    def __init__(self, labels, keys, col_of_key, indexes, ncols):
+        self.labels, self.keys, self.col_of_key = labels, keys, col_of_key
+        self.indexes, self.ncols = indexes, ncols
+
+
+def intern_more(t: Tables, policies: Sequence):
+    """Working terms of further policies in the id space of intern()'s
+    tables t (same KEYS, same value ids): returns (xval, sel CSR, allow CSR)
+    where xval (ncols_x, n) holds the pod columns these policies add (keys no
+    earlier policy used, custom-matcher columns), numbered after every column
+    so far.  KEYS stay the build's (kano_py's labelMap, model.py:127-133)."""
+    st = t.state
+    if st is None:
+        raise ValueError("tables without interning state (use intern())")
+    n = t.n
+    labels = st.labels
+    new_cols: List[np.ndarray] = []
+
+    def key_col(k) -> int:
+        c = st.col_of_key.get(k)
+        if c is None:
+            c = st.ncols
+            st.ncols += 1
+            st.col_of_key[k] = c
+            idx = _ValueIndex()
+            st.indexes[c] = idx
+            row = np.full(n, ABSENT, dtype=np.int32)
+            for i, lab in enumerate(labels):
+                if k in lab:
+                    row[i] = idx.pod_id(lab[k])
+            new_cols.append(row)
+        return c
+
+    sides = [[], []]
+    for pol in policies:
+        default = is_default_matcher(pol.matcher)
+        for which, side in enumerate((pol.working_selector.labels, pol.working_allow.labels)):
+            terms = []
+            for k, rule in side.items():
+                if k not in st.keys:
+                    continue                 # quirk Q1
+                if default:
+                    c = key_col(k)
+                    terms.append((c, st.indexes[c].rule_id(rule)))
+                else:
+                    c = st.ncols
+                    st.ncols += 1
+                    row = np.full(n, ABSENT, dtype=np.int32)
+                    for i, lab in enumerate(labels):
+                        if k in lab:
+                            row[i] = 1 if pol.matcher.match(rule, lab[k]) else 0
+                    new_cols.append(row)
+                    terms.append((c, 1))
+            sides[which].append(terms)
+
+    def csr(lists):
+        off = np.zeros(len(lists) + 1, dtype=np.int64)
+        np.cumsum([len(x) for x in lists], out=off[1:])
+        cols = np.array([c for x in lists for c, _ in x], dtype=np.int32)
+        vals = np.array([v for x in lists for _, v in x], dtype=np.int32)
+        return off, cols, vals
+
+    xval = np.stack(new_cols) if new_cols else np.zeros((0, n), np.int32)
+    return xval, csr(sides[0]), csr(sides[1])
 
 
 def tables_from_cluster(cl) -> Tables:

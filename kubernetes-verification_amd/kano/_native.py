@@ -54,6 +54,10 @@ SIGNATURES = {
     "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "kano_export_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
+    "kano_add_policies": (c_int, [c_void_p, c_int64, c_int32, c_void_p] + [c_void_p] * 6 +
+                          [POINTER(c_int64)]),
+    "kano_remove_policies": (c_int, [c_void_p, c_int64, c_void_p]),
+    "kano_added_policy_sets": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "kano_import_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),

@@ -76,6 +76,25 @@ class _BuildLists:
         return pol[off[i]:off[i + 1]].tolist()
 
 
+class _Renumber:
+    """ReachabilityMatrix.remove_policies on a container's lists: drop the
+    removed policy indices, renumber the rest (what a build over the updated
+    policy list would have appended)."""
+
+    __slots__ = ("gone", "lo")
+
+    def __init__(self, gone: np.ndarray):
+        self.gone = gone
+        self.lo = int(gone[0])
+
+    def apply(self, lst: List[int]) -> None:
+        lo = self.lo
+        if any(x >= lo for x in lst):
+            arr = np.asarray(lst, dtype=np.int64)
+            keep = arr[~np.isin(arr, self.gone)]
+            lst[:] = (keep - np.searchsorted(self.gone, keep, side="right")).tolist()
+
+
 class Container:
     """A container (kano_py/kano/model.py:11-25).  Dataclass-equivalent:
     fields ``name, labels, select_policies, allow_policies``; the two lists
@@ -97,6 +116,10 @@ class Container:
         if self._pending:
             pend, self._pending = self._pending, []
             for lists, i in pend:
+                if isinstance(lists, _Renumber):   # a policy removal, applied lazily
+                    lists.apply(self._sel)
+                    lists.apply(self._alw)
+                    continue
                 self._sel.extend(lists.select_list(i))
                 self._alw.extend(lists.allow_list(i))
 
@@ -407,6 +430,69 @@ class ReachabilityMatrix:
     @property
     def engine(self):
         return self._engine
+
+    # ---- incremental policy updates ----------
+    # Not in kano_py, whose only way to change the policy set is another
+    # build_matrix call.  After add_policies / remove_policies the matrix,
+    # every container's select_policies / allow_policies and the policies'
+    # working sets are what build_matrix(containers, updated policies) gives
+    # (model.py:125-165); the device writes only the rows the changed
+    # policies select.  The build's policy list is updated in place.
+
+    def _check_inc(self):
+        if getattr(self, "_policies", None) is None:
+            raise TypeError("incremental updates need a matrix from build_matrix")
+        if getattr(self, "_eids", None) is None:
+            self._eids = list(range(len(self._policies)))
+
+    def add_policies(self, new_policies: List["Policy"]) -> None:
+        from ._intern import intern_more
+        from ._bits import set_bit_indices
+        self._check_inc()
+        new_policies = list(new_policies)
+        for pol in new_policies:          # allow=None raises here, as the build does
+            pol.working_selector.labels
+            pol.working_allow.labels
+        eng = self._engine
+        n = self.container_size
+        xval, sel, alw = intern_more(eng.tables, new_policies)
+        first = eng.add_policies(xval, sel, alw)
+        cs, ps = self._containers, self._policies
+        for k, pol in enumerate(new_policies):
+            eid = first + k
+            idx = len(ps)
+            s, a = eng.added_policy_sets(eid)
+            pol.store_bcp(BitArray.from_words(s, n), BitArray.from_words(a, n))
+            for i in set_bit_indices(s, n).tolist():
+                cs[i].select_policies.append(idx)
+            for j in set_bit_indices(a, n).tolist():
+                cs[j].allow_policies.append(idx)
+            ps.append(pol)
+            self._eids.append(eid)
+        self._lists = None
+
+    def remove_policies(self, indices) -> None:
+        self._check_inc()
+        ps, cs = self._policies, self._containers
+        idx = sorted({int(k) + len(ps) if int(k) < 0 else int(k) for k in indices})
+        if any(k < 0 or k >= len(ps) for k in idx):
+            raise IndexError("list index out of range")
+        if not idx:
+            return
+        self._engine.remove_policies([self._eids[k] for k in idx])
+        # the lists drop the removed indices and renumber the rest (lazily,
+        # in order with the build's own pending lists)
+        op = _Renumber(np.asarray(idx, dtype=np.int64))
+        for c in cs:
+            if isinstance(c, Container):
+                c._pending.append((op, -1))
+            else:
+                op.apply(c.select_policies)
+                op.apply(c.allow_policies)
+        for k in reversed(idx):
+            del ps[k]
+            del self._eids[k]
+        self._lists = None
 
     # ---- on-disk / tooling format -------------
     # Not in kano_py: its rows are bitarrays (model.py:136-139), and this
