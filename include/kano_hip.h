@@ -215,6 +215,20 @@ int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
  * steps on the MFMA, row classes, column classes, identity classes]. */
 int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info);
 
+/* kano_path on one row shard of a multi-GPU build, in two
+ * halves around one exchange: T, the one-hop table over column classes, is
+ * an OR over all rows, everything else is per row.
+ *   kano_path_shard_words: words of T (0 for an edited shard: unsupported).
+ *   kano_path_shard: this shard's part of T into t_dev (DEVICE memory).
+ *   (the caller gathers the ranks' parts rank-major into one device buffer,
+ *   e.g. an RCCL all-gather over xGMI)
+ *   kano_path_combine: OR of the parts, then this shard's rows of the path
+ *   matrix into dst (a matrix context over the same rows). */
+int kano_path_shard_words(kano_ctx* src, int64_t* words);
+int kano_path_shard(kano_ctx* src, uint64_t* t_dev);
+int kano_path_combine(kano_ctx* src, kano_ctx* dst, const uint64_t* gathered_dev, int32_t nranks,
+                      int hops, int mode, int64_t* info);
+
 /* The on-disk / tooling row format: rows of M as
  * kano_py holds them, bitarray bytes in bitarray's default big-endian bit
  * order (kano_py/kano/model.py:136-139,158-160; bitarray.tobytes(): bit j of

@@ -2606,7 +2606,34 @@ int path_mfma_launch(kano_ctx* ctx, const PathMfmaArgs& a, i64 tiles) {
   return 0;
 }
 
-int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
+// this context's rows' part of T (all of T for a full build): T[b] = OR of
+// Mc[rc(j)] over the members j of column class b in [r0, r1)
+int path_t_local(kano_ctx* src, kano_ctx* ctx, u64* Tout) {
+  const i64 n = src->n, Ua = src->cc.U, ldR = src->ldC, KW = (Ua + 63) / 64;
+  const u64* base = P_<u64>(src->Mc);
+  const i64 nch = (ldR + 255) / 256;
+  if (KW <= 4 && Ua <= 65536) {
+    // narrow class rows: slices of the column classes' member lists
+    KTRY(dalloc(ctx, ctx->pB, sizeof(int32_t) * (Ua + 1)));
+    KCHK(hipMemsetAsync(Tout, 0, sizeof(u64) * Ua * ldR, ctx->stream));
+    hipLaunchKernelGGL(k_path_t_items, dim3(1), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(src->cc.moff), Ua, P_<int32_t>(ctx->pB));
+    KLAUNCH();
+    const i64 nitems = (n + 64 * NT_SLICE - 1) / (64 * NT_SLICE) + Ua;   // upper bound
+    hipLaunchKernelGGL(k_path_t_narrow, dim3(nblk(nitems, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                       base, ldR, P_<int32_t>(src->rc.cls), P_<int32_t>(src->cc.moff),
+                       P_<int32_t>(src->cc.mem), Ua, KW, P_<int32_t>(ctx->pB), nitems, src->r0,
+                       src->r1, Tout);
+  } else {
+    hipLaunchKernelGGL(k_path_t<4>, dim3(nblk(Ua * nch, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                       base, ldR, P_<int32_t>(src->rc.cls), P_<int32_t>(src->cc.moff),
+                       P_<int32_t>(src->cc.mem), Ua, KW, nch, src->r0, src->r1, Tout);
+  }
+  KLAUNCH();
+  return 0;
+}
+
+int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info, bool t_ready) {
   const i64 n = src->n, W = src->W, ldM = src->ldM;
   PathGeom g;
   g.identity = src->rows_dirty;
@@ -2628,26 +2655,7 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
   i64 steps = 0, used = 0, mfma_steps = 0;
   if (n > 0 && W > 0 && hops != 1 && g.rows > 0 && g.Ua > 0) {
     if (!g.identity) {
-      KTRY(dalloc(ctx, ctx->pT, sizeof(u64) * g.Ua * g.ldR));
-      const i64 nch = (g.ldR + 255) / 256;
-      if (g.KW <= 4 && g.Ua <= 65536) {
-        // narrow class rows: slices of the column classes' member lists
-        KTRY(dalloc(ctx, ctx->pB, sizeof(int32_t) * (g.Ua + 1)));
-        KCHK(hipMemsetAsync(ctx->pT.p, 0, sizeof(u64) * g.Ua * g.ldR, ctx->stream));
-        hipLaunchKernelGGL(k_path_t_items, dim3(1), dim3(TPB), 0, ctx->stream,
-                           P_<int32_t>(src->cc.moff), g.Ua, P_<int32_t>(ctx->pB));
-        KLAUNCH();
-        const i64 nitems = (n + 64 * NT_SLICE - 1) / (64 * NT_SLICE) + g.Ua;   // upper bound
-        hipLaunchKernelGGL(k_path_t_narrow, dim3(nblk(nitems, TPB / 64)), dim3(TPB), 0,
-                           ctx->stream, g.base, g.ldR, P_<int32_t>(src->rc.cls),
-                           P_<int32_t>(src->cc.moff), P_<int32_t>(src->cc.mem), g.Ua, g.KW,
-                           P_<int32_t>(ctx->pB), nitems, P_<u64>(ctx->pT));
-      } else
-        hipLaunchKernelGGL(k_path_t<4>, dim3(nblk(g.Ua * nch, TPB / 64)), dim3(TPB), 0,
-                           ctx->stream, g.base, g.ldR, P_<int32_t>(src->rc.cls),
-                           P_<int32_t>(src->cc.moff), P_<int32_t>(src->cc.mem), g.Ua, g.KW, nch,
-                           P_<u64>(ctx->pT));
-      KLAUNCH();
+      if (!t_ready) KTRY(path_t_local(src, ctx, P_<u64>(ctx->pT)));
       g.T = P_<u64>(ctx->pT);
     }
     // R[0] (the identity case writes the destination matrix in place), R[1]
@@ -2777,7 +2785,7 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
       auto launch = [&](auto kern, size_t shm) {
         hipLaunchKernelGGL(kern, grid, dim3(TPB), shm, ctx->stream, rt16, g.Ua, g.rows,
                            P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
-                           P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM);
+                           P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM, src->r0);
       };
       if (use_lds && staged) launch(k_path_expand16<SUB, true, true>, lds);
       else if (use_lds) launch(k_path_expand16<SUB, true, false>, lds);
@@ -2787,8 +2795,8 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info) {
     }
   } else if (n > 0 && W > 0) {
     // one hop (or an empty class set): the matrix itself
-    KCHK(hipMemcpyAsync(ctx->M.p, src->M.p, sizeof(u64) * n * ldM, hipMemcpyDeviceToDevice,
-                        ctx->stream));
+    KCHK(hipMemcpyAsync(ctx->M.p, src->M.p, sizeof(u64) * rows_local(src) * ldM,
+                        hipMemcpyDeviceToDevice, ctx->stream));
   }
   KTRY(sync(ctx));
   ctx->cols_valid = false;
@@ -2830,7 +2838,61 @@ int kano_path(kano_ctx* src, kano_ctx* dst, int hops, int mode, int64_t* info) {
     const int rc = sync(src);   // the source's matrix and classes are complete
     if (rc) return fail(dst, rc, "kano_path: source: " + src->err);
   }
-  return path_impl(src, dst, hops, mode, info);
+  KTRY(dalloc(ctx, ctx->pT, sizeof(u64) * std::max<i64>(1, src->cc.U * src->ldC)));
+  return path_impl(src, dst, hops, mode, info, false);
+}
+
+int kano_path_shard_words(kano_ctx* src, int64_t* words) {
+  if (!src || !words) return -EINVAL;
+  KTRY(ensure_matrix(src));
+  *words = src->rows_dirty ? 0 : src->cc.U * src->ldC;
+  return 0;
+}
+
+int kano_path_shard(kano_ctx* src, uint64_t* t_dev) {
+  if (!src) return -EINVAL;
+  kano_ctx* ctx = src;
+  KCHK(hipSetDevice(src->device));
+  KTRY(ensure_matrix(src));
+  if (src->rows_dirty)
+    return fail(src, -ENOTSUP, "kano_path_shard: an edited row shard (needs every row)");
+  if (src->cc.U * src->ldC > 0) {
+    if (!t_dev) return fail(src, -EINVAL, "kano_path_shard: t_dev is NULL");
+    KTRY(path_t_local(src, src, reinterpret_cast<u64*>(t_dev)));
+  }
+  return sync(src);
+}
+
+int kano_path_combine(kano_ctx* src, kano_ctx* dst, const uint64_t* gathered_dev, int32_t nranks,
+                      int hops, int mode, int64_t* info) {
+  if (!src || !dst || src == dst) return -EINVAL;
+  kano_ctx* ctx = dst;
+  if (hops < 0 || nranks < 1 || mode < KANO_PATH_AUTO || mode > KANO_PATH_MFMA)
+    return fail(dst, -EINVAL, "kano_path_combine: bad arguments");
+  if (src->device != dst->device) return fail(dst, -EINVAL, "kano_path_combine: two devices");
+  KCHK(hipSetDevice(dst->device));
+  {
+    const int rc = ensure_matrix(src);
+    if (rc) return fail(dst, rc, "kano_path_combine: source: " + src->err);
+  }
+  if (src->rows_dirty) return fail(dst, -ENOTSUP, "kano_path_combine: an edited row shard");
+  KTRY(ensure_matrix(dst));
+  if (dst->n != src->n || dst->r0 != src->r0 || dst->r1 != src->r1 || dst->ldM != src->ldM)
+    return fail(dst, -EINVAL, "kano_path_combine: the destination must hold the same rows");
+  {
+    const int rc = sync(src);
+    if (rc) return fail(dst, rc, "kano_path_combine: source: " + src->err);
+  }
+  const i64 nw = src->cc.U * src->ldC;
+  KTRY(dalloc(ctx, ctx->pT, sizeof(u64) * std::max<i64>(1, nw)));
+  if (nw > 0) {
+    if (!gathered_dev) return fail(dst, -EINVAL, "kano_path_combine: gathered_dev is NULL");
+    hipLaunchKernelGGL(k_or_parts, dim3(std::min<i64>(4096, nblk(nw))), dim3(TPB), 0,
+                       ctx->stream, reinterpret_cast<const u64*>(gathered_dev), nranks, nw,
+                       P_<u64>(ctx->pT));
+    KLAUNCH();
+  }
+  return path_impl(src, dst, hops, mode, info, true);
 }
 
 

@@ -38,7 +38,8 @@ __global__ __launch_bounds__(TPB) void k_path_t(const u64* __restrict__ Mc, i64 
                                                 const int32_t* __restrict__ rcls,
                                                 const int32_t* __restrict__ moff,
                                                 const int32_t* __restrict__ mem, i64 Ua,
-                                                i64 KW, i64 nch, u64* __restrict__ T) {
+                                                i64 KW, i64 nch, i64 r0, i64 r1,
+                                                u64* __restrict__ T) {
   const int lane = threadIdx.x & 63;
   const i64 item = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   if (item >= Ua * nch) return;                       // wave-uniform
@@ -48,7 +49,9 @@ __global__ __launch_bounds__(TPB) void k_path_t(const u64* __restrict__ Mc, i64 
   for (int k = 0; k < CW; ++k) acc[k] = 0;
   int32_t prev = -1;
   for (int32_t m = moff[b]; m < moff[b + 1]; ++m) {
-    const int32_t r = rcls[mem[m]];
+    const int32_t j = mem[m];
+    if (j < r0 || j >= r1) continue;                  // a row shard: its own pods only
+    const int32_t r = rcls[j];
     if (r == prev) continue;
     prev = r;
     const u64* src = Mc + (i64)r * ldC;
@@ -76,7 +79,8 @@ __global__ __launch_bounds__(TPB) void k_path_t_narrow(const u64* __restrict__ M
                                                        const int32_t* __restrict__ moff,
                                                        const int32_t* __restrict__ mem, i64 Ua,
                                                        i64 KW, const int32_t* __restrict__ ioff,
-                                                       i64 nitems, u64* __restrict__ T) {
+                                                       i64 nitems, i64 r0, i64 r1,
+                                                       u64* __restrict__ T) {
   const int lane = threadIdx.x & 63;
   const i64 item = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   if (item >= nitems) return;                         // wave-uniform
@@ -92,7 +96,9 @@ __global__ __launch_bounds__(TPB) void k_path_t_narrow(const u64* __restrict__ M
   u64 acc[4] = {0, 0, 0, 0};
   int32_t prev = -1;
   for (int32_t m = mb + lane; m < me; m += 64) {
-    const int32_t r = rcls[mem[m]];
+    const int32_t j = mem[m];
+    if (j < r0 || j >= r1) continue;
+    const int32_t r = rcls[j];
     if (r == prev) continue;
     prev = r;
 #pragma unroll
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
                                                        i64 rows, const int32_t* __restrict__ ccls,
                                                        i64 n, const int32_t* __restrict__ moff,
                                                        const int32_t* __restrict__ mem,
-                                                       u64* __restrict__ M, i64 ldM) {
+                                                       u64* __restrict__ M, i64 ldM, i64 r0) {
   const int32_t Z = (int32_t)gridDim.z, z = (int32_t)blockIdx.z;
   extern __shared__ uint16_t tab[];
   __shared__ u64 cw[STAGED ? 16 : 1][TPB];
@@ -449,12 +455,12 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
         int32_t m = moff[c] + z;
         for (; m + 3 * Z < m1; m += 4 * Z) {   // four member rows' stores in flight
           const int32_t a0 = mem[m], a1 = mem[m + Z], a2 = mem[m + 2 * Z], a3 = mem[m + 3 * Z];
-          M[(i64)a0 * ldM + w] = word;
-          M[(i64)a1 * ldM + w] = word;
-          M[(i64)a2 * ldM + w] = word;
-          M[(i64)a3 * ldM + w] = word;
+          M[(a0 - r0) * ldM + w] = word;
+          M[(a1 - r0) * ldM + w] = word;
+          M[(a2 - r0) * ldM + w] = word;
+          M[(a3 - r0) * ldM + w] = word;
         }
-        for (; m < m1; m += Z) M[(i64)mem[m] * ldM + w] = word;
+        for (; m < m1; m += Z) M[(mem[m] - r0) * ldM + w] = word;
       }
     }
     if (!STAGED) continue;
@@ -467,7 +473,7 @@ __global__ __launch_bounds__(TPB) void k_path_expand16(const uint16_t* __restric
       const int32_t m1 = moff[c + 1];
       for (int32_t m = moff[c] + z; m < m1; m += Z, ++q) {
         if ((q & 3) != wv) continue;
-        u64* dst = M + (i64)mem[m] * ldM + cb;
+        u64* dst = M + (mem[m] - r0) * ldM + cb;
 #pragma unroll
         for (int h = 0; h < TPB / 128; ++h) {
           const int k = 2 * (h * 64 + lane);
@@ -521,6 +527,16 @@ __global__ __launch_bounds__(TPB) void k_bytes_to_words(const uint8_t* __restric
   const i64 j0 = w * 64;
   if (j0 + 64 > nbits) x = j0 >= nbits ? 0ull : x & ((1ull << (nbits - j0)) - 1ull);
   M[r * ldM + w] = x;
+}
+
+// T = OR of the ranks' parts (gathered rank-major, nw words each)
+__global__ __launch_bounds__(TPB) void k_or_parts(const u64* __restrict__ parts, int32_t nranks,
+                                                  i64 nw, u64* __restrict__ out) {
+  for (i64 w = (i64)blockIdx.x * TPB + threadIdx.x; w < nw; w += (i64)gridDim.x * TPB) {
+    u64 x = 0;
+    for (int32_t r = 0; r < nranks; ++r) x |= parts[(i64)r * nw + w];
+    out[w] = x;
+  }
 }
 
 }  // namespace kano

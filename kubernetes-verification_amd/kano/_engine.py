@@ -125,13 +125,13 @@ class DeviceBuild:
         return (self.tables.n + 63) >> 6
 
     @staticmethod
-    def empty(n: int, device: int = 0) -> "DeviceBuild":
-        """A context holding an n x n matrix and no policies (the target of
-        put_rows or of path_from)."""
+    def empty(n: int, device: int = 0, rows: Optional[Tuple[int, int]] = None) -> "DeviceBuild":
+        """A context holding an n x n matrix (or its rows [r0, r1)) and no
+        policies (the target of put_rows or of path_from / path_combine)."""
         z64 = np.zeros(1, np.int64)
         e = np.zeros(0, np.int32)
         t = Tables(int(n), 0, np.zeros((0, int(n)), np.int32), z64, e, e, z64, e, e)
-        return DeviceBuild(t, device=device)
+        return DeviceBuild(t, device=device, rows=rows)
 
     def path_from(self, src: "DeviceBuild", hops: int = 2, mode: str = "auto") -> dict:
         """This context's matrix := the multi-hop reachability of src's
@@ -155,6 +155,26 @@ class DeviceBuild:
         rows = np.ascontiguousarray(rows, dtype=np.uint8)
         self._chk(self.lib.kano_import_rows(self.ctx, int(r0), int(rows.shape[0]), _ptr(rows)),
                   "kano_import_rows")
+
+    def path_shard_words(self) -> int:
+        w = c_int64(0)
+        self._chk(self.lib.kano_path_shard_words(self.ctx, byref(w)), "kano_path_shard_words")
+        return int(w.value)
+
+    def path_shard(self, t_dev_ptr: int) -> None:
+        """This row shard's part of the path's one-hop table (device memory)."""
+        self._chk(self.lib.kano_path_shard(self.ctx, c_void_p(t_dev_ptr)), "kano_path_shard")
+
+    def path_combine(self, src: "DeviceBuild", gathered_dev_ptr: int, nranks: int,
+                     hops: int = 2, mode: str = "auto") -> dict:
+        """This context's rows := src's shard of the path matrix, from the
+        ranks' gathered parts."""
+        info = np.zeros(6, dtype=np.int64)
+        self._chk(self.lib.kano_path_combine(src.ctx, self.ctx, c_void_p(gathered_dev_ptr),
+                                             int(nranks), int(hops), nat.PATHS[mode],
+                                             _ptr(info)), "kano_path_combine")
+        keys = ("steps", "steps_run", "mfma_steps", "row_classes", "col_classes", "identity")
+        return {k: int(v) for k, v in zip(keys, info)}
 
     # -- incremental updates (SURVEY.md §8(f) rank 4) ---------------------
     def add_policies(self, xval: np.ndarray, sel_csr, alw_csr) -> int:

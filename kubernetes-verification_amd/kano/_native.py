@@ -53,6 +53,10 @@ SIGNATURES = {
                                     c_int64, POINTER(c_int64)]),
     "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "kano_path_shard_words": (c_int, [c_void_p, POINTER(c_int64)]),
+    "kano_path_shard": (c_int, [c_void_p, c_void_p]),
+    "kano_path_combine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_int, c_int,
+                                  c_void_p]),
     "kano_export_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_add_policies": (c_int, [c_void_p, c_int64, c_int32, c_void_p] + [c_void_p] * 6 +
                           [POINTER(c_int64)]),

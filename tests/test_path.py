@@ -174,3 +174,39 @@ def test_path_expand_table_from_l2(monkeypatch):
     dst.path_from(eng, 2, "bitwise")
     M = eng.rows(0, cl.n)
     assert np.array_equal(dst.rows(0, cl.n), orc.path_c(M, cl.n, 2)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spans", [[(0, 700), (700, 1500)], [(0, 0), (0, 1), (1, 900), (900, 1500)]])
+@pytest.mark.parametrize("hops", [2, 0])
+def test_path_row_shards(spans, hops):
+    """The multi-GPU path on one device: every shard writes its part of T into
+    its slot of one gathered buffer (what the RCCL all-gather builds), then
+    kano_path_combine writes the shard's rows; the rows concatenate to the
+    single-device path matrix."""
+    import torch
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.synth import make_cluster
+    from oracle import kano_oracle as orc
+    cl = make_cluster(1500, 150, "sparse", seed=107)
+    t = tables_from_cluster(cl)
+    n = cl.n
+    full = DeviceBuild(t)
+    ref, _ = orc.path_c(full.rows(0, n), n, hops)
+    engs = [DeviceBuild(t, rows=s) for s in spans]
+    nw = engs[0].path_shard_words()
+    assert all(e.path_shard_words() == nw for e in engs)   # column classes agree
+    gathered = torch.zeros(len(spans) * max(nw, 1), dtype=torch.int64, device="cuda")
+    for k, e in enumerate(engs):
+        e.path_shard(gathered.data_ptr() + 8 * nw * k)
+    torch.cuda.synchronize()
+    rows = []
+    for e, (r0, r1) in zip(engs, spans):
+        dst = DeviceBuild.empty(n, rows=(r0, r1))
+        dst.path_combine(e, gathered.data_ptr(), len(spans), hops, "auto")
+        if r1 > r0:
+            rows.append(dst.rows(r0, r1 - r0))
+        dst.close()
+        e.close()
+    assert np.array_equal(np.concatenate(rows), ref)
