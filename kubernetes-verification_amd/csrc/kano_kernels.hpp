@@ -748,6 +748,45 @@ __global__ __launch_bounds__(TPB) void k_mc_scatter(i64 nnz, const int32_t* __re
   }
 }
 
+// The same rows written whole: one wave per row class builds its row in LDS
+// (the allowed-class lists of S(c), LDS atomic OR) and stores every word, so
+// Mc needs no zero fill and the global atomics go.  Heavy rows: skipped
+// (k_heavy_mc_or writes them whole) or, for the MFMA path that ORs into them,
+// written as zero.  LDS: NW rows of ldMc words per block.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_mc_rows(i64 U, const i64* __restrict__ soffc,
+                                                     const int32_t* __restrict__ slist,
+                                                     const i64* __restrict__ alcoff,
+                                                     const int32_t* __restrict__ alc,
+                                                     const int32_t* __restrict__ hflag,
+                                                     int heavy_zero, u64* __restrict__ Mc,
+                                                     i64 ldMc) {
+  extern __shared__ u64 mrow[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const i64 c = (i64)blockIdx.x * NW + wv;
+  if (c >= U) return;                                 // wave-uniform; no block barrier below
+  u64* row = mrow + (i64)wv * ldMc;
+  const bool heavy = hflag && hflag[c];
+  if (heavy && !heavy_zero) return;
+  for (i64 w = lane; w < ldMc; w += 64) row[w] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  if (!heavy) {
+    const i64 e1 = soffc[c + 1];
+    for (i64 e = soffc[c]; e < e1; ++e) {
+      const int32_t p = slist[e];
+      for (i64 k = alcoff[p] + lane; k < alcoff[p + 1]; k += 64) {
+        const int32_t ca = alc[k];
+        atomicOr(&row[ca >> 6], 1ull << (ca & 63));
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  u64* dst = Mc + c * ldMc;
+  for (i64 w = lane; w < ldMc; w += 64) dst[w] = row[w];
+}
+
 // column OR and NAND over the classes with local members, at class level
 // block: 64 words x (4 waves x 32 classes)
 __global__ __launch_bounds__(TPB) void k_mc_cols(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
