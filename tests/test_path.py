@@ -210,3 +210,39 @@ def test_path_row_shards(spans, hops):
         dst.close()
         e.close()
     assert np.array_equal(np.concatenate(rows), ref)
+
+
+@pytest.mark.gpu
+def test_path_c2_scale():
+    """C2 (10k pods / 1k policies, BASELINE configs[1]): the two-hop matrix
+    against the oracle; the closure through size-independent properties --
+    every mode gives the same matrix, it contains the two-hop matrix, and it is
+    closed (the closure of the closure is itself)."""
+    from kano import algorithm as alg
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.model import ReachabilityMatrix
+    from kano.synth import make_config
+    from oracle import kano_oracle as orc
+    cl = make_config("C2")
+    n = cl.n
+    eng = DeviceBuild(tables_from_cluster(cl))
+    m = ReachabilityMatrix.__new__(ReachabilityMatrix)
+    m.container_size, m._engine = n, eng
+    m._containers = m._policies = m._lists = None
+    m._ncontainers = n
+    M = eng.rows(0, n)
+    p2 = alg.two_hop(m)
+    P2 = p2.engine.rows(0, n)
+    assert np.array_equal(P2, orc.path_c(M, n, 2)[0])
+    closures = [alg.transitive_closure(m, mode).engine.rows(0, n)
+                for mode in ("auto", "bitwise", "mfma")]
+    C = closures[0]
+    assert all(np.array_equal(C, x) for x in closures[1:])
+    assert np.array_equal(C | P2, C)
+    # closed: one more composition adds nothing (the closure of C as a matrix)
+    dst = DeviceBuild.empty(n)
+    dst.put_rows(0, C)
+    again = DeviceBuild.empty(n)
+    again.path_from(dst, 0, "auto")
+    assert np.array_equal(again.rows(0, n), C)
