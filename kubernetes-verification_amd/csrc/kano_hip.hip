@@ -687,6 +687,12 @@ int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
 
 // classes of both sides, both matchings, allow counts, select counts and the
 // per-class plan; two host syncs (class counts, list sizes)
+// policies per block of k_pol_counts / k_sel_place: combine the per-class
+// atomics in LDS when many policies share few row classes (broad selectors)
+int sel_spb(const kano_ctx* ctx) {
+  return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
+}
+
 int do_front(kano_ctx* ctx, int path) {
   ctx->rc.m0 = ctx->r0;
   ctx->rc.m1 = ctx->r1;
@@ -744,12 +750,12 @@ int do_front(kano_ctx* ctx, int path) {
   // (one wave per policy, both sides)
   if (P > 0) {
     const bool sel = Ur > 0;
-    hipLaunchKernelGGL(k_pol_counts, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
+    hipLaunchKernelGGL(k_pol_counts, dim3(nblk(P, sel_spb(ctx))), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                        P_<int32_t>(ctx->am.gmem), P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca),
                        P_<int32_t>(ctx->acnt), P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                        sel ? P_<int32_t>(ctx->sm.gmem) : (const int32_t*)nullptr,
-                       P_<int32_t>(ctx->scnt), P_<unsigned long long>(ctx->cost));
+                       P_<int32_t>(ctx->scnt), P_<unsigned long long>(ctx->cost), sel_spb(ctx));
     KLAUNCH();
   }
   if (Ur > 0) {
@@ -890,10 +896,10 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   if (U > 0) {
     if (P > 0) {
-      hipLaunchKernelGGL(k_sel_place, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
+      hipLaunchKernelGGL(k_sel_place, dim3(nblk(P, sel_spb(ctx))), dim3(TPB), 0, ctx->stream, P,
                          P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                          P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
-                         P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls));
+                         P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), sel_spb(ctx));
       KLAUNCH();
     }
     // S(c) sorted, heavy list and work-item map in one launch

@@ -41,32 +41,101 @@ struct ClsPair {
   ClsSide s[2];
 };
 
+// Block-level combining (the packed mode): the block's pods first meet in an
+// LDS table keyed by the packed tuple, so only one thread per distinct tuple
+// per block probes the global table and posts the block's smallest member to
+// smin -- with few, large classes (broad selectors: C4 has ~100 row classes)
+// thousands of pods otherwise send their CAS / atomicMin to the same slot.
+constexpr int CLS_LDS = 512;   // LDS slots per block (2 x TPB)
+
+// LDS table of a block's classes (int32 keys, CLS_LDS slots, -1 empty):
+// the slot of c, inserting it if absent; -1 when the table is full and c is
+// not in it (the caller then goes to global memory directly; once full the
+// table stays full, so a later probe for c fails the same way).
+__device__ __forceinline__ int lds_class_slot(int32_t* lkey, int32_t c, bool insert) {
+  uint32_t h = hfin(hmix(0x2545f491u, (uint32_t)c)) & (CLS_LDS - 1);
+  for (int probe = 0; probe < CLS_LDS; ++probe) {
+    int32_t cur = lkey[h];
+    if (cur == -1 && insert) {
+      cur = atomicCAS(&lkey[h], -1, c);
+      if (cur == -1) return (int)h;
+    }
+    if (cur == c) return (int)h;
+    if (cur == -1) return -1;            // (lookup only) absent
+    h = (h + 1) & (CLS_LDS - 1);
+  }
+  return -1;
+}
+
+// Policies per block (spb) of the select-side kernels below that combine
+// their per-class atomics in LDS (k_pol_counts, k_sel_place): waves take the
+// block's policies in turn.  With spb == WPB (one policy per wave) they post
+// their atomics directly.  At C4 ~10,000 policies select one of ~100 classes
+// each, so the per-class counters otherwise see thousands of atomics; at C3
+// a class sees ~3 and the direct form is faster (more blocks).
+
+__device__ __forceinline__ uint32_t cls_packed_slot(const u64* tab, uint32_t tmask, u64 key) {
+  uint32_t s = hfin(hmix(hmix(0x9747b28cu, (uint32_t)key), (uint32_t)(key >> 32))) & tmask;
+  u64* t = const_cast<u64*>(tab);
+  for (;;) {
+    u64 cur = t[s];   // plain read: slots only go from empty to a key
+    if (cur == ~0ull) {
+      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&t[s]), ~0ull,
+                                 (unsigned long long)key);
+      if (prev == ~0ull) break;
+      cur = prev;
+    }
+    if (cur == key) break;
+    s = (s + 1) & tmask;
+  }
+  return s;
+}
+
 __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ pv, i64 n,
                                                     ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;   // pods [m0, m1) of the side
-  if (i >= a.m1) return;
-  uint32_t s;
-  if (a.packed) {
-    // the key tuple as one word, (value + 3) per key (ids are >= -3): compare
-    // words, no gathers of the occupant's pod values
-    u64 key = 0;
-    for (int k = 0; k < a.KS; ++k)
-      key = (key << a.keys[a.KS + k]) | (u64)(uint32_t)(pv[(i64)a.keys[k] * n + i] + 3);
-    s = hfin(hmix(hmix(0x9747b28cu, (uint32_t)key), (uint32_t)(key >> 32))) & a.tmask;
-    u64* tab = reinterpret_cast<u64*>(a.table);
-    for (;;) {
-      u64 cur = tab[s];   // plain read, as below
-      if (cur == ~0ull) {
-        const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tab[s]), ~0ull,
-                                   (unsigned long long)key);
-        if (prev == ~0ull) break;
-        cur = prev;
-      }
-      if (cur == key) break;
-      s = (s + 1) & a.tmask;
+  const bool act = i < a.m1;
+  if (a.packed) {                                  // block-uniform branch (one side per block)
+    __shared__ u64 lkey[CLS_LDS];
+    __shared__ int32_t lmin[CLS_LDS], lslot[CLS_LDS];
+    for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+      lkey[t] = ~0ull;
+      lmin[t] = INT32_MAX;
     }
-  } else {
+    __syncthreads();
+    // the key tuple as one word, (value + 3) per key (ids are >= -3)
+    u64 key = 0;
+    int t = -1;
+    bool lead = false;
+    if (act) {
+      for (int k = 0; k < a.KS; ++k)
+        key = (key << a.keys[a.KS + k]) | (u64)(uint32_t)(pv[(i64)a.keys[k] * n + i] + 3);
+      // 256 pods in 512 slots: the probe always ends
+      uint32_t h = hfin(hmix(hmix(0x2545f491u, (uint32_t)key), (uint32_t)(key >> 32))) &
+                   (CLS_LDS - 1);
+      for (;;) {
+        const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h]), ~0ull,
+                                   (unsigned long long)key);
+        if (prev == ~0ull) { lead = true; break; }
+        if (prev == key) break;
+        h = (h + 1) & (CLS_LDS - 1);
+      }
+      t = (int)h;
+      atomicMin(&lmin[t], (int32_t)i);
+    }
+    __syncthreads();
+    if (lead) {
+      const uint32_t s = cls_packed_slot(reinterpret_cast<const u64*>(a.table), a.tmask, key);
+      lslot[t] = (int32_t)s;
+      if (lmin[t] < a.smin[s]) atomicMin(&a.smin[s], lmin[t]);
+    }
+    __syncthreads();
+    if (act) a.slot_of[i] = lslot[t];
+    return;
+  }
+  if (!act) return;
+  uint32_t s;
   uint32_t h = 0x9747b28cu;
   for (int k = 0; k < a.KS; ++k) h = hmix(h, (uint32_t)pv[(i64)a.keys[k] * n + i]);
   s = hfin(h) & a.tmask;
@@ -87,7 +156,6 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
     }
     if (eq) break;
     s = (s + 1) & a.tmask;
-  }
   }
   a.slot_of[i] = (int32_t)s;
   // smallest member per slot (the class representative); smin only falls.
@@ -132,17 +200,37 @@ __global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
   const bool act = i < a.m1;
-  int32_t c = 0;
-  if (act) {
-    const int32_t r = a.smin[a.slot_of[i]];
-    c = a.cid[r - a.m0];
-    a.cls[i] = c;
-    if (r == (int32_t)i) a.rep[c] = (int32_t)i;
+  // the block's pods are counted per class in LDS; one atomic per distinct
+  // class per block reserves the block's places in the class's member list
+  // (the counter's old value + the pod's LDS rank is its place: k_cls_mfill
+  // then scatters without atomics)
+  __shared__ int32_t lkey[CLS_LDS], lcnt[CLS_LDS], lbase[CLS_LDS];
+  for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+    lkey[t] = -1;
+    lcnt[t] = 0;
   }
-  // the counter's old value + rank in the wave is the pod's place in its
-  // class's member list: k_cls_mfill then scatters without atomics
-  const int32_t r = wave_agg_inc(a.mcnt, c, act);
-  if (act) a.mcur[i - a.m0] = r;
+  __syncthreads();
+  int32_t c = 0, t = -1, r = 0;
+  bool lead = false;
+  if (act) {
+    const int32_t rp = a.smin[a.slot_of[i]];
+    c = a.cid[rp - a.m0];
+    a.cls[i] = c;
+    if (rp == (int32_t)i) a.rep[c] = (int32_t)i;
+    uint32_t h = hfin(hmix(0x2545f491u, (uint32_t)c)) & (CLS_LDS - 1);
+    for (;;) {
+      const int32_t prev = atomicCAS(&lkey[h], -1, c);
+      if (prev == -1) { lead = true; break; }
+      if (prev == c) break;
+      h = (h + 1) & (CLS_LDS - 1);
+    }
+    t = (int)h;
+    r = atomicAdd(&lcnt[t], 1);
+  }
+  __syncthreads();
+  if (lead) lbase[t] = atomicAdd(&a.mcnt[c], lcnt[t]);
+  __syncthreads();
+  if (act) a.mcur[i - a.m0] = lbase[t] + r;
 }
 
 // member counts of the pods [m0, m1) of each side
@@ -518,21 +606,70 @@ __global__ __launch_bounds__(TPB) void k_sel_count(i64 P, const i64* __restrict_
   }
 }
 
+// S(c) placement (model.py:161 appends p to select_policies): the block's
+// entries are counted per class in LDS, one atomic per distinct class per
+// block reserves their places, then the entries are walked again and placed
+// with LDS cursors (order inside S(c) is fixed by the sort that follows).
 __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict__ pstart,
                                                    const int32_t* __restrict__ plen,
                                                    const int32_t* __restrict__ pcls,
                                                    const i64* __restrict__ soffc, int32_t* scur,
                                                    int32_t* __restrict__ slist,
-                                                   int32_t* __restrict__ ecls) {
-  const i64 p = wave_policy();
-  if (p >= P) return;
-  const int32_t* L = pcls + pstart[p];
-  const int32_t len = plen[p];
-  for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
-    const int32_t c = L[k];
-    const i64 e = soffc[c] + atomicAdd(&scur[c], 1);
-    slist[e] = (int32_t)p;
-    ecls[e] = c;
+                                                   int32_t* __restrict__ ecls, int spb) {
+  __shared__ int32_t lkey[CLS_LDS], lcnt[CLS_LDS], lbase[CLS_LDS];
+  const bool comb = spb > WPB;                        // block-uniform
+  if (comb) {
+    for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+      lkey[t] = -1;
+      lcnt[t] = 0;
+    }
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // one policy per wave (q), or per lane when spb == TPB (short lists)
+  const bool lp = spb == TPB;
+  const int q0 = lp ? threadIdx.x : wv, qs = lp ? TPB : TPB / 64;
+  const int k0 = lp ? 0 : lane, ks = lp ? 1 : 64;
+  for (int q = q0; q < spb; q += qs) {                // pass 1: count, or place directly
+    const i64 p = (i64)blockIdx.x * spb + q;
+    if (p >= P) break;
+    const int32_t* L = pcls + pstart[p];
+    const int32_t len = plen[p];
+    for (int32_t k = k0; k < len; k += ks) {
+      const int32_t c = L[k];
+      const int t = comb ? lds_class_slot(lkey, c, true) : -1;
+      if (t >= 0) {
+        atomicAdd(&lcnt[t], 1);
+      } else {
+        const i64 e = soffc[c] + atomicAdd(&scur[c], 1);
+        slist[e] = (int32_t)p;
+        ecls[e] = c;
+      }
+    }
+  }
+  if (!comb) return;
+  __syncthreads();
+  for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+    const int32_t c = lkey[t];
+    if (c >= 0) {
+      lbase[t] = atomicAdd(&scur[c], lcnt[t]);
+      lcnt[t] = 0;
+    }
+  }
+  __syncthreads();
+  for (int q = q0; q < spb; q += qs) {                // pass 2: the counted entries
+    const i64 p = (i64)blockIdx.x * spb + q;
+    if (p >= P) break;
+    const int32_t* L = pcls + pstart[p];
+    const int32_t len = plen[p];
+    for (int32_t k = k0; k < len; k += ks) {
+      const int32_t c = L[k];
+      const int t = lds_class_slot(lkey, c, false);
+      if (t < 0) continue;                            // placed in pass 1
+      const i64 e = soffc[c] + lbase[t] + atomicAdd(&lcnt[t], 1);
+      slist[e] = (int32_t)p;
+      ecls[e] = c;
+    }
   }
 }
 
@@ -651,27 +788,83 @@ __global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict
                                                     const i64* __restrict__ spstart,
                                                     const int32_t* __restrict__ splen,
                                                     const int32_t* __restrict__ spcls,
-                                                    int32_t* scnt, unsigned long long* cost) {
-  const i64 p = wave_policy();
-  if (p >= P) return;
-  const int lane = threadIdx.x & 63;
-  const int32_t* L = apcls + apstart[p];
-  const int32_t len = aplen[p];
-  i64 pods = 0;
-  for (int32_t k = lane; k < len; k += 64) pods += csize[L[k]];
-  pods = wave_sum(pods);
-  if (lane == 0) {
-    nca[p] = len;
-    acnt[p] = (int32_t)pods;
+                                                    int32_t* scnt, unsigned long long* cost,
+                                                    int spb) {
+  __shared__ int32_t lkey[CLS_LDS], lcnt[CLS_LDS];
+  __shared__ unsigned long long lcost[CLS_LDS];
+  const bool comb = spb > WPB;                        // block-uniform
+  if (comb) {
+    for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+      lkey[t] = -1;
+      lcnt[t] = 0;
+      lcost[t] = 0;
+    }
+    __syncthreads();
   }
-  if (!spcls) return;
-  const int32_t* S = spcls + spstart[p];
-  const int32_t slen = splen[p];
-  const unsigned long long a = (unsigned long long)(int32_t)pods;
-  for (int32_t k = lane; k < slen; k += 64) {
-    const int32_t c = S[k];
-    atomicAdd(&scnt[c], 1);
-    if (a) atomicAdd(&cost[c], a);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (spb == TPB) {   // one policy per lane (short lists: broad selectors)
+    const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
+    if (p < P) {
+      const int32_t* L = apcls + apstart[p];
+      const int32_t len = aplen[p];
+      i64 pods = 0;
+      for (int32_t k = 0; k < len; ++k) pods += csize[L[k]];
+      nca[p] = len;
+      acnt[p] = (int32_t)pods;
+      if (spcls) {
+        const int32_t* S = spcls + spstart[p];
+        const int32_t slen = splen[p];
+        const unsigned long long a = (unsigned long long)(int32_t)pods;
+        for (int32_t k = 0; k < slen; ++k) {
+          const int32_t c = S[k];
+          const int t = lds_class_slot(lkey, c, true);
+          if (t >= 0) {
+            atomicAdd(&lcnt[t], 1);
+            if (a) atomicAdd(&lcost[t], a);
+          } else {
+            atomicAdd(&scnt[c], 1);
+            if (a) atomicAdd(&cost[c], a);
+          }
+        }
+      }
+    }
+  }
+  for (int q = wv; q < spb && spb != TPB; q += TPB / 64) {
+    const i64 p = (i64)blockIdx.x * spb + q;
+    if (p >= P) break;                               // wave-uniform
+    const int32_t* L = apcls + apstart[p];
+    const int32_t len = aplen[p];
+    i64 pods = 0;
+    for (int32_t k = lane; k < len; k += 64) pods += csize[L[k]];
+    pods = wave_sum(pods);
+    if (lane == 0) {
+      nca[p] = len;
+      acnt[p] = (int32_t)pods;
+    }
+    if (!spcls) continue;
+    const int32_t* S = spcls + spstart[p];
+    const int32_t slen = splen[p];
+    const unsigned long long a = (unsigned long long)(int32_t)pods;
+    for (int32_t k = lane; k < slen; k += 64) {
+      const int32_t c = S[k];
+      const int t = comb ? lds_class_slot(lkey, c, true) : -1;
+      if (t >= 0) {
+        atomicAdd(&lcnt[t], 1);
+        if (a) atomicAdd(&lcost[t], a);
+      } else {
+        atomicAdd(&scnt[c], 1);
+        if (a) atomicAdd(&cost[c], a);
+      }
+    }
+  }
+  if (!comb) return;
+  __syncthreads();
+  for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+    const int32_t c = lkey[t];
+    if (c >= 0) {
+      atomicAdd(&scnt[c], lcnt[t]);
+      if (lcost[t]) atomicAdd(&cost[c], lcost[t]);
+    }
   }
 }
 
