@@ -258,6 +258,17 @@ int kano_add_policies(kano_ctx* ctx, int64_t Pn, int32_t ncols_x, const int32_t*
 int kano_remove_policies(kano_ctx* ctx, int64_t count, const int64_t* ids);
 int kano_added_policy_sets(kano_ctx* ctx, int64_t id, uint64_t* sel, uint64_t* allow);
 
+/* Kubernetes matchExpressions requirements (an
+ * extension of kano_py's equality selectors; semantics of the requirements
+ * kubesv adapts, kubesv/kubesv/model.py:127-160).  Appends E pod columns
+ * ncols .. ncols+E-1 computed on the device: 1 where pod i meets requirement
+ * e, else 0 -- op 0 In (the key's value id listed in vals[off[e]..off[e+1]),
+ * sorted), 1 NotIn (absent or not listed), 2 Exists, 3 DoesNotExist; col[e]
+ * is the key's column (-1: no pod carries it).  Policies then use the term
+ * (ncols + e, 1).  Call after kano_set_pods, before kano_set_policies. */
+int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int32_t* op,
+                         const int64_t* off, const int32_t* vals);
+
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);
 void kano_host_free(void* p);

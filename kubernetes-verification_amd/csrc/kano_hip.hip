@@ -1628,6 +1628,56 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
 // keys of that side (slots); each policy's terms are sorted by slot and
 // deduplicated (two different values for one slot match nothing); the
 // distinct slot sets become the masks of the hash join.
+int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int32_t* op,
+                         const int64_t* off, const int32_t* vals) {
+  if (!ctx) return -EINVAL;
+  if (!ctx->have_pods) return fail(ctx, -EINVAL, "kano_set_expressions before kano_set_pods");
+  if (E < 0 || (E > 0 && (!col || !op || !off))) return fail(ctx, -EINVAL, "kano_set_expressions");
+  if (E == 0) return 0;
+  KCHK(hipSetDevice(ctx->device));
+  const i64 n = ctx->n, nc = ctx->ncols;
+  for (int32_t e = 0; e < E; ++e) {
+    if (col[e] >= nc || op[e] < 0 || op[e] > 3 || off[e + 1] < off[e])
+      return fail(ctx, -EINVAL, "kano_set_expressions: bad requirement");
+    for (i64 k = off[e] + 1; k < off[e + 1]; ++k)
+      if (vals[k - 1] >= vals[k]) return fail(ctx, -EINVAL, "kano_set_expressions: unsorted set");
+  }
+  // the pod table grows by E columns, computed on the device
+  DBuf grown;
+  KTRY(dalloc(ctx, grown, sizeof(int32_t) * std::max<i64>(1, n * (nc + E))));
+  if (n * nc > 0)
+    KCHK(hipMemcpyAsync(grown.p, ctx->pv.p, sizeof(int32_t) * n * nc, hipMemcpyDeviceToDevice,
+                        ctx->stream));
+  const i64 nv = off[E];
+  std::vector<uint8_t> h(sizeof(int32_t) * 2 * E + sizeof(i64) * (E + 1) +
+                         sizeof(int32_t) * std::max<i64>(1, nv) + 16);
+  std::memcpy(h.data(), off, sizeof(i64) * (E + 1));
+  int32_t* hb = reinterpret_cast<int32_t*>(h.data() + sizeof(i64) * (E + 1));
+  std::memcpy(hb, col, sizeof(int32_t) * E);
+  std::memcpy(hb + E, op, sizeof(int32_t) * E);
+  if (nv) std::memcpy(hb + 2 * E, vals, sizeof(int32_t) * nv);
+  DBuf args;
+  KTRY(dalloc(ctx, args, h.size()));
+  KCHK(hipMemcpyAsync(args.p, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+  if (n > 0) {
+    const i64* d_off = P_<i64>(args);
+    const int32_t* d_b = reinterpret_cast<const int32_t*>(d_off + E + 1);
+    hipLaunchKernelGGL(k_expr_cols, dim3(nblk(n), (unsigned)E), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(grown), n, d_b, d_b + E, d_off, d_b + 2 * E,
+                       P_<int32_t>(grown) + n * nc);
+    KLAUNCH();
+  }
+  KTRY(sync(ctx));
+  dfree(args);
+  dfree(ctx->pv);
+  ctx->pv = grown;
+  ctx->ncols = (int32_t)(nc + E);
+  ctx->colbits.resize((size_t)ctx->ncols, 3);   // values 0 / 1 pack as 3 / 4
+  ctx->have_pols = false;
+  ctx->built = false;
+  return 0;
+}
+
 static constexpr int MAX_MASKS = 64;
 
 static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t* col,

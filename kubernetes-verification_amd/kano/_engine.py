@@ -98,6 +98,12 @@ class DeviceBuild:
         self.tables = t
         pv = np.ascontiguousarray(t.pod_val, dtype=np.int32)
         self._chk(self.lib.kano_set_pods(self.ctx, t.n, t.ncols, _ptr(pv)), "kano_set_pods")
+        if getattr(t, "expr_col", None) is not None and len(t.expr_col):
+            ex = [np.ascontiguousarray(a, dtype=d) for a, d in (
+                (t.expr_col, np.int32), (t.expr_op, np.int32), (t.expr_off, np.int64),
+                (t.expr_val, np.int32))]
+            self._chk(self.lib.kano_set_expressions(self.ctx, len(ex[0]), *[_ptr(a) for a in ex]),
+                      "kano_set_expressions")
         arrs = [np.ascontiguousarray(a, dtype=d) for a, d in (
             (t.sel_off, np.int64), (t.sel_col, np.int32), (t.sel_val, np.int32),
             (t.alw_off, np.int64), (t.alw_col, np.int32), (t.alw_val, np.int32))]

@@ -49,6 +49,13 @@ class Tables:
     # interning state of intern(): lets intern_more() put later policies in
     # the same id space (incremental updates)
     state: Any = None
+    # matchExpressions requirements (model.LabelExpression): E columns the
+    # engine appends after the ncols above (kano_set_expressions): base pod
+    # column (-1: no container carries the key), operator, sorted value ids
+    expr_col: Any = None
+    expr_op: Any = None
+    expr_off: Any = None
+    expr_val: Any = None
 
     @property
     def P(self) -> int:
@@ -134,6 +141,8 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
             col_specs.append(("key", k))
         return c
 
+    from .model import LabelExpression
+    exprs: List[tuple] = []              # (key, LabelExpression)
     raw_terms = []                       # per policy: ([(col, rule|None)], [(col, rule|None)])
     for ws, wa, matcher in sides:
         default = is_default_matcher(matcher)
@@ -141,6 +150,14 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
         for side in (ws, wa):
             terms = []
             for k, rule in side.items():
+                if isinstance(rule, LabelExpression):
+                    # evaluated on the device from the key's column, whether or
+                    # not a container carries the key (no quirk Q1)
+                    if k in keys:
+                        key_col(k)
+                    terms.append((None, len(exprs), "expr"))
+                    exprs.append((k, rule))
+                    continue
                 if k not in keys:
                     continue                 # quirk Q1
                 if default:
@@ -176,6 +193,10 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
         vals: List[int] = []
         for p, per_side in enumerate(raw_terms):
             for col, rule, custom in per_side[which]:
+                if custom == "expr":
+                    cols.append(ncols + rule)    # the engine's expression column
+                    vals.append(1)
+                    continue
                 cols.append(col)
                 vals.append(1 if custom else indexes[col].rule_id(rule))
             off[p + 1] = len(cols)
@@ -183,8 +204,27 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
 
     so, sc, sv = csr(0)
     ao, ac, av = csr(1)
-    st = _InternState(labels, keys, col_of_key, indexes, ncols)
-    return Tables(n, ncols, pod_val, so, sc, sv, ao, ac, av, st)
+    st = _InternState(labels, keys, col_of_key, indexes, ncols + len(exprs))
+    t = Tables(n, ncols, pod_val, so, sc, sv, ao, ac, av, st)
+    if exprs:
+        ecol, eop, eoff, evals = [], [], [0], []
+        for k, rule in exprs:
+            c = col_of_key.get(k, -1) if k in keys else -1
+            ecol.append(c)
+            eop.append(rule.op)
+            ids = set()
+            if c >= 0:
+                for v in getattr(rule, "values", ()):
+                    vid = indexes[c].rule_id(v)
+                    if vid >= 0:
+                        ids.add(vid)
+            evals.extend(sorted(ids))
+            eoff.append(len(evals))
+        t.expr_col = np.asarray(ecol, np.int32)
+        t.expr_op = np.asarray(eop, np.int32)
+        t.expr_off = np.asarray(eoff, np.int64)
+        t.expr_val = np.asarray(evals, np.int32)
+    return t
 
 
 class _InternState:
@@ -201,6 +241,7 @@ def intern_more(t: Tables, policies: Sequence):
     where xval (ncols_x, n) holds the pod columns these policies add (keys no
     earlier policy used, custom-matcher columns), numbered after every column
     so far.  KEYS stay the build's (kano_py's labelMap, model.py:127-133)."""
+    from .model import LabelExpression
     st = t.state
     if st is None:
         raise ValueError("tables without interning state (use intern())")
@@ -229,6 +270,14 @@ def intern_more(t: Tables, policies: Sequence):
         for which, side in enumerate((pol.working_selector.labels, pol.working_allow.labels)):
             terms = []
             for k, rule in side.items():
+                if isinstance(rule, LabelExpression):
+                    c = st.ncols
+                    st.ncols += 1
+                    row = np.fromiter((1 if rule.matches(lab, k) else 0 for lab in labels),
+                                      dtype=np.int32, count=n)
+                    new_cols.append(row)
+                    terms.append((c, 1))
+                    continue
                 if k not in st.keys:
                     continue                 # quirk Q1
                 if default:

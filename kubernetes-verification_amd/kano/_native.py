@@ -52,6 +52,7 @@ SIGNATURES = {
     "kano_verify_combine": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                     c_int64, POINTER(c_int64)]),
     "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
+    "kano_set_expressions": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kano_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "kano_path_shard_words": (c_int, [c_void_p, POINTER(c_int64)]),
     "kano_path_shard": (c_int, [c_void_p, c_void_p]),

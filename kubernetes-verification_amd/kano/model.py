@@ -38,6 +38,7 @@ __all__ = [
     "Container", "PolicySelect", "PolicyAllow", "PolicyDirection", "PolicyIngress",
     "PolicyEgress", "PolicyProtocol", "LabelRelation", "DefaultEqualityLabelRelation",
     "Policy", "ReachabilityMatrix", "BitArray", "bitarray", "KanoNativeError",
+    "LabelExpression", "In", "NotIn", "Exists", "DoesNotExist",
 ]
 
 bitarray = BitArray
@@ -165,6 +166,71 @@ class Container:
     __hash__ = None
 
 
+class LabelExpression:
+    """Kubernetes matchExpressions requirement as a PolicySelect / PolicyAllow
+    value (not in kano_py).  Semantics follow the
+    label-selector requirements kubesv adapts (kubesv/kubesv/model.py:127-160,
+    operators In / NotIn / Exists / DoesNotExist): In needs the key with a
+    listed value, NotIn matches an absent key or an unlisted value, Exists
+    needs the key, DoesNotExist its absence.  Unlike a plain value, the term
+    is evaluated whether or not any container carries the key (no quirk Q1).
+    Values compare by Python ==, like the default matcher."""
+
+    op = -1
+
+    def matches(self, labels: Dict, key) -> bool:
+        raise NotImplementedError
+
+    def __eq__(self, other):
+        return type(other) is type(self) and getattr(other, "values", None) == getattr(
+            self, "values", None)
+
+    def __hash__(self):
+        return hash((type(self).__name__, tuple(getattr(self, "values", ()))))
+
+    def __repr__(self):
+        v = getattr(self, "values", None)
+        return f"{type(self).__name__}({v!r})" if v is not None else f"{type(self).__name__}()"
+
+
+def _listed(v, values) -> bool:
+    return any(v == x for x in values)
+
+
+class In(LabelExpression):
+    op = 0
+
+    def __init__(self, values):
+        self.values = list(values)
+
+    def matches(self, labels, key):
+        return key in labels and _listed(labels[key], self.values)
+
+
+class NotIn(LabelExpression):
+    op = 1
+
+    def __init__(self, values):
+        self.values = list(values)
+
+    def matches(self, labels, key):
+        return key not in labels or not _listed(labels[key], self.values)
+
+
+class Exists(LabelExpression):
+    op = 2
+
+    def matches(self, labels, key):
+        return key in labels
+
+
+class DoesNotExist(LabelExpression):
+    op = 3
+
+    def matches(self, labels, key):
+        return key not in labels
+
+
 @dataclass
 class PolicySelect:
     labels: Dict[str, str]
@@ -255,17 +321,20 @@ class Policy:
 
     # Per-container predicates kept for API parity (model.py:95-111); the build
     # evaluates the same predicate on the GPU over interned labels.
+    # (LabelExpression values, an extension, are evaluated on their own)
     def select_policy(self, container: Container) -> bool:
-        sl = self.working_selector.labels
-        for k, v in container.labels.items():
-            if k in sl.keys() and not self.matcher.match(sl[k], v):
-                return False
-        return True
+        return self._pred(self.working_selector.labels, container)
 
     def allow_policy(self, container: Container) -> bool:
-        al = self.working_allow.labels
+        return self._pred(self.working_allow.labels, container)
+
+    def _pred(self, sl, container) -> bool:
+        for k, rule in sl.items():
+            if isinstance(rule, LabelExpression) and not rule.matches(container.labels, k):
+                return False
         for k, v in container.labels.items():
-            if k in al.keys() and not self.matcher.match(al[k], v):
+            if k in sl.keys() and not isinstance(sl[k], LabelExpression) and \
+                    not self.matcher.match(sl[k], v):
                 return False
         return True
 

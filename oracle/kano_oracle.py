@@ -219,17 +219,39 @@ def ref_py(containers, policies, label="app", sys_idx=0) -> dict:
     sel_lists = [[] for _ in range(n)]
     alw_lists = [[] for _ in range(n)]
 
-    def pred(pol_labels, cl, matcher):                      # model.py:95-111
-        for k, v in cl.items():
-            if k in pol_labels.keys() and not matcher.match(pol_labels[k], v):
+    def is_expr(rule):   # a matchExpressions requirement (extension)
+        return hasattr(rule, "matches")
+
+    def expr_ok(pol_labels, cl):
+        # K8s label-selector requirements (kubesv/kubesv/model.py:127-160):
+        # In: key present, value listed; NotIn: absent or unlisted; Exists;
+        # DoesNotExist.  Python == for values.
+        for k, r in pol_labels.items():
+            if not is_expr(r):
+                continue
+            name = type(r).__name__
+            present = k in cl
+            listed = present and any(cl[k] == x for x in getattr(r, "values", ()))
+            ok = {"In": listed, "NotIn": not listed, "Exists": present,
+                  "DoesNotExist": not present}[name]
+            if not ok:
                 return False
         return True
+
+    def pred(pol_labels, cl, matcher):                      # model.py:95-111
+        for k, v in cl.items():
+            if k in pol_labels.keys() and not is_expr(pol_labels[k]) and \
+                    not matcher.match(pol_labels[k], v):
+                return False
+        return expr_ok(pol_labels, cl)
 
     for p, pol in enumerate(policies):
         ws = pol.working_selector.labels                    # model.py:82-93
         wa = pol.working_allow.labels
-        s = [int(all(k in c.labels for k in ws if k in keys)) for c in containers]
-        a = [int(all(k in c.labels for k in wa if k in keys)) for c in containers]
+        s = [int(all(k in c.labels for k in ws if k in keys and not is_expr(ws[k])))
+             for c in containers]
+        a = [int(all(k in c.labels for k in wa if k in keys and not is_expr(wa[k])))
+             for c in containers]
         for i, c in enumerate(containers):                  # model.py:150-154
             if s[i] and not pred(ws, c.labels, pol.matcher):
                 s[i] = 0
