@@ -269,6 +269,24 @@ int kano_added_policy_sets(kano_ctx* ctx, int64_t id, uint64_t* sel, uint64_t* a
 int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int32_t* op,
                          const int64_t* off, const int32_t* vals);
 
+/* kubesv's edge relation (kubesv/kubesv/
+ * constraint.py:191-231, which replaces kano's M with a K8s reading of the
+ * policies: namespaces, namespaceSelector, per-direction rules).  in_t and
+ * eg_t hold full n x n builds, in_t[sel][src] = ingress_traffic(src, sel) and
+ * eg_t[sel][dst] = egress_traffic(dst, sel) (one kano policy per (policy,
+ * peer), built by the host from the K8s objects); dst (an n x n context, e.g.
+ * kano_create + kano_set_pods with no policies) receives
+ *   edge[src][dst] = OR_sel in_t[sel][src] AND eg_t[sel][dst]
+ *                    | eg_t[src][dst]          if flags & KANO_K8S_SELF
+ * (check_self_ingress_traffic: ingress_traffic(sel, sel)), or every pair if
+ * flags & KANO_K8S_ALL (check_select_by_no_policy with a pod selected by no
+ * policy: that pod receives from and sends to everyone).  dst then reads as
+ * an edited matrix (every check, kano_path for kubesv's path relation).
+ * info (nullable): [0] the bits the product added beyond the self term. */
+#define KANO_K8S_SELF 1
+#define KANO_K8S_ALL  2
+int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int64_t* info);
+
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);
 void kano_host_free(void* p);

@@ -43,6 +43,7 @@
 #include "kano_kernels.hpp"
 #include "kano_path.hpp"
 #include "kano_inc.hpp"
+#include "kano_k8s.hpp"
 
 using namespace kano;
 
@@ -3185,6 +3186,78 @@ int kano_added_policy_sets(kano_ctx* ctx, int64_t id, uint64_t* sel, uint64_t* a
     KCHK(hipMemcpyAsync(allow, P_<u64>(ctx->aalw) + q * W, sizeof(u64) * W,
                         hipMemcpyDeviceToHost, ctx->stream));
   return sync(ctx);
+}
+
+// kubesv's edge relation (kubesv/kubesv/constraint.py:191-231) from the two
+// per-direction kano matrices: see kano_k8s.hpp.
+int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int64_t* info) {
+  if (!in_t || !eg_t || !dst) return -EINVAL;
+  if (dst == in_t || dst == eg_t)
+    return fail(dst, -EINVAL, "kano_k8s_edge: the destination must be another context");
+  if (in_t->device != dst->device || eg_t->device != dst->device)
+    return fail(dst, -EINVAL, "kano_k8s_edge: contexts on two devices");
+  kano_ctx* ctx = dst;
+  KCHK(hipSetDevice(dst->device));
+  for (kano_ctx* s : {in_t, eg_t}) {
+    const int rc = ensure_matrix(s);
+    if (rc) return fail(dst, rc, "kano_k8s_edge: source: " + s->err);
+    if (s->r0 != 0 || s->r1 != s->n)
+      return fail(dst, -ENOTSUP, "kano_k8s_edge: a source holds a row shard (needs every row)");
+  }
+  KTRY(ensure_matrix(dst));
+  const i64 n = dst->n, W = dst->W, ldM = dst->ldM;
+  if (in_t->n != n || eg_t->n != n || dst->r0 != 0 || dst->r1 != n || in_t->ldM != ldM ||
+      eg_t->ldM != ldM)
+    return fail(dst, -EINVAL, "kano_k8s_edge: the three matrices must have the same size");
+  for (kano_ctx* s : {in_t, eg_t}) {
+    const int rc = sync(s);   // the sources' matrices are complete
+    if (rc) return fail(dst, rc, "kano_k8s_edge: source: " + s->err);
+  }
+  u64* E = P_<u64>(dst->M);
+  u64 added = 0;
+  if (n > 0 && W > 0) {
+    if (flags & KANO_K8S_ALL) {
+      hipLaunchKernelGGL(k_k8s_ones, dim3(nblk(n * ldM)), dim3(TPB), 0, ctx->stream, E, ldM, n, W);
+      KLAUNCH();
+    } else {
+      // edge starts as EgT (self ingress traffic: sel = src) or empty
+      if (flags & KANO_K8S_SELF)
+        KCHK(hipMemcpyAsync(E, eg_t->M.p, sizeof(u64) * n * ldM, hipMemcpyDeviceToDevice,
+                            ctx->stream));
+      else
+        KCHK(hipMemsetAsync(E, 0, sizeof(u64) * n * ldM, ctx->stream));
+      // In = InT transposed (row src: the sel pods src may send to)
+      KTRY(dalloc(ctx, ctx->pA, sizeof(u64) * n * ldM));
+      KTRY(dalloc(ctx, ctx->pB, sizeof(u64) * n * ldM));
+      KTRY(dalloc(ctx, ctx->pcnt, sizeof(u64) * PATH_CNT_SLOTS * PATH_CNT_STRIDE));
+      KCHK(hipMemsetAsync(ctx->pcnt.p, 0, sizeof(u64) * PATH_CNT_SLOTS * PATH_CNT_STRIDE,
+                          ctx->stream));
+      const i64 CG = (W + 15) / 16;
+      hipLaunchKernelGGL(k_k8s_transpose, dim3(nblk(W * CG, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                         P_<u64>(in_t->M), ldM, n, W, CG, n, P_<u64>(ctx->pA), ldM);
+      KLAUNCH();
+      // edge[src] |= OR_{sel in In[src]} EgT[sel]
+      PathGeom g;
+      g.identity = true;
+      g.rows = n;
+      g.Ua = n;
+      g.KW = W;
+      g.ldR = ldM;
+      g.T = P_<u64>(eg_t->M);
+      if (ldM <= 128) KTRY(path_or_launch<2>(ctx, P_<u64>(ctx->pA), E, P_<u64>(ctx->pB), g));
+      else KTRY(path_or_launch<4>(ctx, P_<u64>(ctx->pA), E, P_<u64>(ctx->pB), g));
+      std::vector<u64> slots(PATH_CNT_SLOTS * PATH_CNT_STRIDE);
+      KCHK(hipMemcpyAsync(slots.data(), ctx->pcnt.p, sizeof(u64) * slots.size(),
+                          hipMemcpyDeviceToHost, ctx->stream));
+      KTRY(sync(ctx));
+      for (int k = 0; k < PATH_CNT_SLOTS; ++k) added += slots[(size_t)k * PATH_CNT_STRIDE];
+    }
+  }
+  KTRY(sync(ctx));
+  ctx->cols_valid = false;
+  ctx->rows_dirty = true;
+  if (info) info[0] = (int64_t)added;
+  return 0;
 }
 
 }  // extern "C"

@@ -339,3 +339,122 @@ def path_py(edges: set, n: int, hops: int = 2) -> set:
             break
         path = new
     return path
+
+
+# ---------------------------------------------------------------------------
+# kubesv's Kubernetes relations, restated on Python
+# sets straight from the Datalog rules -- independent of kano/k8s.py's
+# compilation to kano policies.  Unpinned: kubesv needs z3 and the kubernetes
+# client, both absent.  Inputs are the kano.k8s objects (name / namespace /
+# labels, NetworkPolicy.spec dicts).
+# ---------------------------------------------------------------------------
+
+def _k8s_selector(selector, known: set):
+    """LabelSelectorAdapter.define_label_selector (kubesv/kubesv/model.py:
+    178-233) as a predicate over a labels dict, or None on a quick fail."""
+    if selector is None:
+        return lambda lab: True
+    reqs = []
+    exprs = selector.get("matchExpressions")
+    if exprs is not None:
+        for e in exprs:                                   # model.py:139-158
+            op = str(e.get("operator", "")).lower()
+            if op not in ("in", "notin", "exists", "doesnotexists"):
+                continue
+            if e.get("key") not in known:
+                return None
+            reqs.append((op, e["key"], list(e.get("values") or [])))
+    labels = selector.get("matchLabels")
+    if labels is not None:
+        for k, v in labels.items():
+            if k not in known:
+                return None
+            reqs.append(("in", k, [v]))
+
+    def pred(lab):
+        for op, k, vals in reqs:
+            has = k in lab
+            listed = has and any(lab[k] == v for v in vals)
+            if op == "in" and not listed:
+                return False
+            if op == "notin" and listed:
+                return False
+            if op == "exists" and not has:
+                return False
+            if op == "doesnotexists" and has:
+                return False
+        return True
+    return pred
+
+
+def kubesv_edge_py(pods, policies, namespaces, check_self_ingress_traffic=True,
+                   check_select_by_no_policy=False):
+    """edge(src, dst) as a set of pairs (kubesv/kubesv/constraint.py:168-231),
+    with the facts of define_pod_facts (:242-275) and define_pol_facts
+    (:278-282, model.py:420-514)."""
+    nam_map = {ns.name: i for i, ns in enumerate(namespaces)}
+    ns_lab = {ns.name: ns.labels for ns in namespaces}
+    pod_ns = [nam_map[p.namespace] for p in pods]       # KeyError as :251
+    del pod_ns
+    pod_keys = {k for p in pods for k in p.labels}
+    ns_keys = {k for ns in namespaces for k in ns.labels}
+    n = len(pods)
+    selected_by_pol = set()                             # (pod, pol)
+    ingress_allow, egress_allow = set(), set()          # (pod, pol)
+    for idx, pol in enumerate(policies):
+        spec = pol.spec
+        # define_pod_selector (model.py:496-514)
+        if pol.namespace in nam_map:
+            pred = _k8s_selector(spec.get("podSelector"), pod_keys)
+            if pred is not None:
+                for i, p in enumerate(pods):
+                    if p.namespace == pol.namespace and pred(p.labels):
+                        selected_by_pol.add((i, idx))
+
+        def rules(direction, key, out):
+            for rule in spec.get(direction):
+                for peer in (rule or {}).get(key):
+                    peer = peer or {}
+                    nsp = _k8s_selector(peer.get("namespaceSelector"), ns_keys)
+                    if nsp is None:
+                        continue
+                    pp = _k8s_selector(peer.get("podSelector"), pod_keys)
+                    if pp is None:
+                        continue
+                    for i, p in enumerate(pods):   # namespace(pod, ns), ns free
+                        if nsp(ns_lab[p.namespace]) and pp(p.labels):
+                            out.add((i, idx))
+        # define_egress_rules (model.py:420-437)
+        if spec.get("egress") is not None:
+            rules("egress", "to", egress_allow)
+        # define_ingress_rules (model.py:466-483): guarded by egress
+        if spec.get("egress") is not None:
+            rules("ingress", "from", ingress_allow)
+    pols_of = {}
+    for (i, q) in selected_by_pol:
+        pols_of.setdefault(i, set()).add(q)
+    ing_by = {}
+    for (i, q) in ingress_allow:
+        ing_by.setdefault(q, set()).add(i)
+    eg_by = {}
+    for (i, q) in egress_allow:
+        eg_by.setdefault(q, set()).add(i)
+    # ingress_traffic(src, sel), egress_traffic(dst, sel) (constraint.py:191-227)
+    ingress = {s: set() for s in range(n)}              # sel -> srcs
+    egress = {s: set() for s in range(n)}               # sel -> dsts
+    for s in range(n):
+        for q in pols_of.get(s, ()):
+            ingress[s] |= ing_by.get(q, set())
+            egress[s] |= eg_by.get(q, set())
+        if check_self_ingress_traffic:
+            ingress[s].add(s)
+        if check_select_by_no_policy and s not in pols_of:
+            ingress[s] = set(range(n))
+            egress[s] = set(range(n))
+    # edge(src, dst) :- ingress_traffic(src, sel), egress_traffic(dst, sel)
+    edge = set()
+    for s in range(n):
+        for src in ingress[s]:
+            for dst in egress[s]:
+                edge.add((src, dst))
+    return edge, ingress, egress
