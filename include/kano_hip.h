@@ -282,9 +282,15 @@ int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int
  * flags & KANO_K8S_ALL (check_select_by_no_policy with a pod selected by no
  * policy: that pod receives from and sends to everyone).  dst then reads as
  * an edited matrix (every check, kano_path for kubesv's path relation).
- * info (nullable): [0] the bits the product added beyond the self term. */
+ * Two forms: class level when both sources are unedited builds (edge[src]
+ * [dst] = Ec[cc_i(src)][cc_e(dst)] | Mc_e[rc_e(src)][cc_e(dst)], Ec from two
+ * OR-products over the builds' classes, then one expansion to pods), else --
+ * or with KANO_K8S_PODS -- pod level (InT transposed, one OR-product).
+ * info (nullable): [0] the bits the pod-level product added beyond the self
+ * term (-1 for the class-level form). */
 #define KANO_K8S_SELF 1
 #define KANO_K8S_ALL  2
+#define KANO_K8S_PODS 4
 int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int64_t* info);
 
 /* Page-locked host buffers for fast device-to-host result copies. */

@@ -3219,8 +3219,60 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
     if (flags & KANO_K8S_ALL) {
       hipLaunchKernelGGL(k_k8s_ones, dim3(nblk(n * ldM)), dim3(TPB), 0, ctx->stream, E, ldM, n, W);
       KLAUNCH();
+    } else if (!in_t->rows_dirty && !eg_t->rows_dirty && in_t->rc.U > 0 && eg_t->rc.U > 0 &&
+               in_t->cc.U > 0 && eg_t->cc.U > 0 && !(flags & KANO_K8S_PODS)) {
+      // class level (kano_k8s.hpp): B, EgA, Mc_i transposed, Ec, expansion
+      const i64 Ui = in_t->rc.U, Xi = in_t->cc.U, Ue = eg_t->rc.U, Ye = eg_t->cc.U;
+      const i64 ldCe = eg_t->ldC, ldCi = in_t->ldC;
+      const i64 KWb = (Ue + 63) / 64, KWa = (Ui + 63) / 64, NWe = (Ye + 63) / 64;
+      KTRY(dalloc(ctx, ctx->pA, sizeof(u64) * Ui * KWb));
+      KTRY(dalloc(ctx, ctx->pB, sizeof(u64) * Ui * ldCe));
+      KTRY(dalloc(ctx, ctx->pT, sizeof(u64) * Xi * KWa));
+      KTRY(dalloc(ctx, ctx->pR[0], sizeof(u64) * Xi * ldCe));
+      KCHK(hipMemsetAsync(ctx->pA.p, 0, sizeof(u64) * Ui * KWb, ctx->stream));
+      hipLaunchKernelGGL(k_k8s_pairs, dim3(nblk(n)), dim3(TPB), 0, ctx->stream,
+                         P_<int32_t>(in_t->rc.cls), P_<int32_t>(eg_t->rc.cls), n,
+                         P_<u64>(ctx->pA), KWb);
+      KLAUNCH();
+      const i64 nch = (ldCe + 255) / 256;
+      hipLaunchKernelGGL(k_k8s_or_rows<4>, dim3(nblk(Ui * nch, TPB / 64)), dim3(TPB), 0,
+                         ctx->stream, P_<u64>(ctx->pA), KWb, KWb, P_<u64>(eg_t->Mc), ldCe, NWe,
+                         P_<u64>(ctx->pB), ldCe, Ui, nch);
+      KLAUNCH();
+      const i64 CGi = ((Xi + 63) / 64 + 15) / 16;
+      hipLaunchKernelGGL(k_k8s_transpose, dim3(nblk(KWa * CGi, TPB / 64)), dim3(TPB), 0,
+                         ctx->stream, P_<u64>(in_t->Mc), ldCi, Ui, KWa, CGi, Xi,
+                         P_<u64>(ctx->pT), KWa);
+      KLAUNCH();
+      hipLaunchKernelGGL(k_k8s_or_rows<4>, dim3(nblk(Xi * nch, TPB / 64)), dim3(TPB), 0,
+                         ctx->stream, P_<u64>(ctx->pT), KWa, KWa, P_<u64>(ctx->pB), ldCe, NWe,
+                         P_<u64>(ctx->pR[0]), ldCe, Xi, nch);
+      KLAUNCH();
+      const int self = (flags & KANO_K8S_SELF) ? 1 : 0;
+      if (Xi * 2 <= n && ldM % 2 == 0) {
+        // expand the Xi class rows once, then stream them (and the self
+        // term, eg_t's own rows) to the pod rows
+        KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * Xi * ldM));
+        hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
+                           ctx->stream, P_<u64>(ctx->pR[0]), ldCe, (const int32_t*)nullptr,
+                           P_<u64>(eg_t->Mc), ldCe, P_<int32_t>(eg_t->rc.cls),
+                           P_<int32_t>(eg_t->cc.cls), 0, Xi, n, W, P_<u64>(ctx->pR[1]), ldM);
+        KLAUNCH();
+        hipLaunchKernelGGL(k_k8s_rows, dim3(nblk(n * (ldM / 2))), dim3(TPB), 0, ctx->stream,
+                           P_<u64>(ctx->pR[1]), P_<int32_t>(in_t->cc.cls), P_<u64>(eg_t->M), self,
+                           n, ldM, E);
+        KLAUNCH();
+      } else {
+        hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(n, K8S_XR)), dim3(TPB), 0,
+                           ctx->stream, P_<u64>(ctx->pR[0]), ldCe, P_<int32_t>(in_t->cc.cls),
+                           P_<u64>(eg_t->Mc), ldCe, P_<int32_t>(eg_t->rc.cls),
+                           P_<int32_t>(eg_t->cc.cls), self, n, n, W, E, ldM);
+        KLAUNCH();
+      }
+      added = (u64)-1;
     } else {
-      // edge starts as EgT (self ingress traffic: sel = src) or empty
+      // pod level (edited sources): edge starts as EgT (self ingress
+      // traffic: sel = src) or empty
       if (flags & KANO_K8S_SELF)
         KCHK(hipMemcpyAsync(E, eg_t->M.p, sizeof(u64) * n * ldM, hipMemcpyDeviceToDevice,
                             ctx->stream));

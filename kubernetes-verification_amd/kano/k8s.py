@@ -15,8 +15,10 @@ kubesv (kubesv/kubesv/model.py, constraint.py) reads Kubernetes objects:
   and ``path`` (constraint.py:168-237).
 
 Here each (policy, peer) becomes one kano policy: select = the policy's pod
-selector and namespace, allow = the peer's terms, all as requirement columns
-(``model.In`` etc.: kubesv has no quirk Q1).  Two device builds give
+selector and namespace, allow = the peer's terms -- matchLabels as plain kano
+values (the quick fail guarantees some pod carries the key, so kano's quirk
+Q1 cannot fire), matchExpressions as requirement columns (``model.In``
+etc.).  Two device builds give
 InT[sel][src] and EgT[sel][dst]; ``kano_k8s_edge`` forms the edge matrix on
 the device (kano_k8s.hpp).  Every check of ``kano.algorithm`` and the path
 functions then read it like any matrix.
@@ -57,7 +59,7 @@ from typing import Any, Dict, List, Optional
 import numpy as np
 
 from .model import (ReachabilityMatrix, Container, Policy, PolicySelect, PolicyAllow,
-                    PolicyEgress, In, NotIn, Exists, DoesNotExist)
+                    PolicyEgress, In, NotIn, Exists, DoesNotExist, LabelExpression)
 
 _NS = ("__k8s_namespace__",)
 
@@ -129,7 +131,10 @@ def _terms(selector: Optional[Dict[str, Any]], known: set) -> Optional[List[tupl
         for k, v in labels.items():
             if k not in known:
                 return None                               # K2
-            out.append((k, In([v])))
+            # a plain kano value: key present and equal (Python ==), one
+            # shared value column per key rather than a requirement column
+            # per term; kano's quirk Q1 cannot fire, some pod carries the key
+            out.append((k, v))
     return out
 
 
@@ -201,6 +206,10 @@ def compile_policies(pods: List[Pod], policies: List[NetworkPolicy],
         pod_keys.update(p.labels.keys())
     for ns in namespaces:
         ns_keys.update(ns.labels.keys())
+    # namespace label keys some pod sees (through its namespace)
+    ns_pod_keys = set()
+    for name in {p.namespace for p in pods}:
+        ns_pod_keys.update(by_name[name].labels.keys())
 
     aliases: Dict[Any, Any] = {}
     ing, egr, sel_only = [], [], []
@@ -214,7 +223,7 @@ def compile_policies(pods: List[Pod], policies: List[NetworkPolicy],
             t = _terms(spec.get("podSelector"), pod_keys)
             if t is not None:
                 sel = _TermDict(aliases)
-                sel.add(_NS, In([pol.namespace]))
+                sel.add(_NS, pol.namespace)
                 for k, r in t:
                     sel.add(k, r)
         # define_egress_rules, then define_ingress_rules (constraint.py:278-282)
@@ -240,6 +249,9 @@ def compile_policies(pods: List[Pod], policies: List[NetworkPolicy],
                         continue                          # K2
                     if sel is None:
                         continue                          # selects nothing
+                    if any(not isinstance(r, LabelExpression) and k not in ns_pod_keys
+                           for k, r in nst):
+                        continue      # no pod lives in a namespace with the key
                     alw = _TermDict(aliases)
                     for k, r in nst:
                         alw.add(("__k8s_ns_label__", k), r)
@@ -268,9 +280,11 @@ def compile_policies(pods: List[Pod], policies: List[NetworkPolicy],
 
 def build(pods: List[Pod], policies: List[NetworkPolicy], namespaces: List[Namespace],
           check_self_ingress_traffic: bool = True, check_select_by_no_policy: bool = False,
-          device: int = 0, path: str = "auto") -> K8sReachability:
+          device: int = 0, path: str = "auto", form: str = "classes") -> K8sReachability:
     """kubesv's ``build`` (constraint.py:285-299) on the device: the edge
-    relation as an n x n matrix (rows src, columns dst)."""
+    relation as an n x n matrix (rows src, columns dst).  ``form``: the
+    product over the builds' row / column classes ("classes") or over pods
+    ("pods"); both give the same matrix."""
     from ._engine import DeviceBuild
     from ._intern import intern
     containers, ing, egr, sel_only = compile_policies(pods, policies, namespaces)
@@ -288,7 +302,8 @@ def build(pods: List[Pod], policies: List[NetworkPolicy], namespaces: List[Names
             selected = np.array([bool(col[i]) for i in range(n)], dtype=bool)
         all_pairs = bool(n) and not bool(selected.all())
     out = DeviceBuild.empty(n, device=device)
-    added = out.k8s_edge_from(in_t, eg_t, bool(check_self_ingress_traffic), all_pairs)
+    added = out.k8s_edge_from(in_t, eg_t, bool(check_self_ingress_traffic), all_pairs,
+                              pods=(form == "pods"))
     info = {"ingress_policies": len(ing), "egress_policies": len(egr),
             "product_bits": added, "all_pairs": all_pairs}
     return K8sReachability(_wrap(out, n), _wrap(in_t, n), _wrap(eg_t, n), selected, info)

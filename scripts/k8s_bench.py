@@ -1,0 +1,101 @@
+"""kubesv's edge relation at scale (kano.k8s): a
+synthetic Kubernetes cluster -- pods spread over namespaces (Zipf), apps per
+namespace, one NetworkPolicy per (namespace, app) that admits ingress from a
+few apps of its namespace and of namespaces with a team label, and sends
+egress to a few apps -- timed per stage.  One JSON line per size.
+
+Usage: python scripts/k8s_bench.py [--pods 10000 100000] [--reps 3]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-verification_amd")]
+
+
+def cluster(n, seed=0):
+    from kano import k8s
+    rng = np.random.default_rng(seed)
+    nns = max(4, n // 500)
+    teams = ["a", "b", "c", "d"]
+    nss = [k8s.Namespace(f"ns{i}", {"team": teams[i % 4], **({"env": "prod"} if i % 3 else {})})
+           for i in range(nns)]
+    z = 1.0 / np.arange(1, nns + 1) ** 1.1
+    ns_of = rng.choice(nns, size=n, p=z / z.sum())
+    apps_per_ns = 20
+    app_of = rng.integers(0, apps_per_ns, size=n)
+    tier = rng.integers(0, 3, size=n)
+    pods = [k8s.Pod(f"p{i}", f"ns{ns_of[i]}", {"app": f"a{app_of[i]}", "tier": f"t{tier[i]}"})
+            for i in range(n)]
+    pols = []
+    for ns in range(nns):
+        for a in range(apps_per_ns):
+            if rng.random() < 0.5:
+                continue
+            ing = [{"podSelector": {"matchLabels": {"app": f"a{int(b)}"}}}
+                   for b in rng.choice(apps_per_ns, size=2, replace=False)]
+            if rng.random() < 0.2:
+                ing.append({"namespaceSelector": {"matchLabels": {"team": teams[ns % 4]}},
+                            "podSelector": {"matchLabels": {"tier": "t0"}}})
+            egr = [{"podSelector": {"matchLabels": {"app": f"a{int(b)}"}},
+                    "namespaceSelector": {"matchLabels": {"team": teams[ns % 4]}}}
+                   for b in rng.choice(apps_per_ns, size=2, replace=False)]
+            pols.append(k8s.NetworkPolicy(f"np{ns}-{a}", f"ns{ns}", {
+                "podSelector": {"matchLabels": {"app": f"a{a}"}},
+                "ingress": [{"from": ing}], "egress": [{"to": egr}]}))
+    return pods, pols, nss
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pods", type=int, nargs="+", default=[10000, 100000])
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--form", default="classes", choices=["classes", "pods"])
+    args = ap.parse_args()
+    import torch  # noqa: F401  (HIP runtime first, as the bench does)
+    from kano import k8s
+    from kano._engine import DeviceBuild
+    from kano._intern import intern
+    for n in args.pods:
+        pods, pols, nss = cluster(n)
+        t = time.perf_counter()
+        cs, ing, egr, _ = k8s.compile_policies(pods, pols, nss)
+        t_compile = time.perf_counter() - t
+        t = time.perf_counter()
+        ti, te = intern(cs, ing), intern(cs, egr)
+        t_intern = time.perf_counter() - t
+        best = None
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            in_t = DeviceBuild(ti)
+            eg_t = DeviceBuild(te)
+            t1 = time.perf_counter()
+            out = DeviceBuild.empty(n)
+            t2 = time.perf_counter()
+            added = out.k8s_edge_from(in_t, eg_t, True, False, pods=args.form == "pods")
+            t3 = time.perf_counter()
+            r = (t1 - t0, t3 - t2)
+            best = r if best is None or sum(r) < sum(best) else best
+            del in_t, eg_t
+        W = (n + 63) // 64
+        # edge density from the matrix itself
+        from kano import algorithm as alg
+        from kano.k8s import _wrap
+        em = _wrap(out, n)
+        iso = len(alg.all_isolated(em))
+        print(json.dumps({
+            "workload": "kubesv edge relation (kano.k8s), synthetic K8s cluster",
+            "form": args.form, "pods": n, "namespaces": len(nss), "policies": len(pols),
+            "ingress_peers": len(ing), "egress_peers": len(egr),
+            "host_compile_s": round(t_compile, 3), "host_intern_s": round(t_intern, 3),
+            "builds_ms": round(best[0] * 1e3, 3), "edge_ms": round(best[1] * 1e3, 3),
+            "product_bits": added, "edge_matrix_bytes": 8 * n * W,
+            "all_isolated": iso, "all_reachable": len(alg.all_reachable(em))}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -145,7 +145,7 @@ def test_compiled_terms_cover_quirks():
         {"key": "app", "operator": "NotIn", "values": ["b"]},
         {"key": "tier", "operator": "Exists"}], "matchLabels": {"app": "web"}}, known)
     assert [(k, type(r)) for k, r in t] == [("app", In), ("tier", DoesNotExist),
-                                           ("app", NotIn), ("tier", Exists), ("app", In)]
+                                           ("app", NotIn), ("tier", Exists), ("app", str)]
 
 
 def _ref_rows(cs, ps, n):
@@ -185,13 +185,14 @@ def test_compilation_matches_oracle(seed, self_traffic):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(12))
 @pytest.mark.parametrize("self_traffic,by_none", [(True, False), (False, False), (True, True)])
-def test_edge_matches_oracle(seed, self_traffic, by_none):
+@pytest.mark.parametrize("form", ["classes", "pods"])
+def test_edge_matches_oracle(seed, self_traffic, by_none, form):
     from kano import k8s
     from oracle import kano_oracle as orc
     pods, pols, nss = _cluster(seed)
     n = len(pods)
     r = k8s.build(pods, pols, nss, check_self_ingress_traffic=self_traffic,
-                  check_select_by_no_policy=by_none)
+                  check_select_by_no_policy=by_none, form=form)
     edge, ing, eg = orc.kubesv_edge_py(pods, pols, nss, self_traffic, by_none)
     assert _bits(r.edge.engine.rows(0, n), n) == edge
     # the product's operands: ingress_traffic [sel][src] without the self
@@ -226,14 +227,16 @@ def test_edge_checks_and_path(seed):
 
 
 @pytest.mark.gpu
-def test_edge_larger_cluster():
-    """A few thousand pods: the product runs many words per row."""
+@pytest.mark.parametrize("form", ["classes", "pods"])
+@pytest.mark.parametrize("seed,self_traffic", [(99, True), (5, False)])
+def test_edge_larger_cluster(form, seed, self_traffic):
+    """A few thousand pods: many words per row, both product forms."""
     from kano import k8s
     from oracle import kano_oracle as orc
-    pods, pols, nss = _cluster(99, n=1500, P=20, nns=5)
+    pods, pols, nss = _cluster(seed, n=1500, P=20, nns=5)
     n = len(pods)
-    r = k8s.build(pods, pols, nss)
-    edge, _, _ = orc.kubesv_edge_py(pods, pols, nss)
+    r = k8s.build(pods, pols, nss, check_self_ingress_traffic=self_traffic, form=form)
+    edge, _, _ = orc.kubesv_edge_py(pods, pols, nss, self_traffic)
     M = r.edge.engine.rows(0, n)
     ref = np.zeros_like(M)
     for i, j in edge:
