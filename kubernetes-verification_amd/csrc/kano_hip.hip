@@ -1703,7 +1703,9 @@ static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t*
     kd.push_back(ctx->colbits[c]);
     tb += ctx->colbits[c];
   }
-  cs.packed = (cs.KS > 0 && tb <= 63 && ctx->cls_packed) ? 1 : 0;
+  // (KS = 0 -- no policy, or only empty selectors -- is one class: packed
+  // too, so its pods meet in LDS instead of CAS-ing one global slot)
+  cs.packed = (tb <= 63 && ctx->cls_packed) ? 1 : 0;
   KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, kd.size())));
   if (cs.KS > 0)   // uploaded once per policy set, not per build
     KCHK(hipMemcpy(cs.keys_d.p, kd.data(), sizeof(int32_t) * kd.size(), hipMemcpyHostToDevice));
