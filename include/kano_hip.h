@@ -282,6 +282,9 @@ int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int
  * flags & KANO_K8S_ALL (check_select_by_no_policy with a pod selected by no
  * policy: that pod receives from and sends to everyone).  dst then reads as
  * an edited matrix (every check, kano_path for kubesv's path relation).
+ * dst may hold a row shard [r0, r1) (kano_set_shard): only its rows are
+ * written (class-level form; the sources are full builds, typically made
+ * with kano_build_classes so their own matrices are never written).
  * Two forms: class level when both sources are unedited builds (edge[src]
  * [dst] = Ec[cc_i(src)][cc_e(dst)] | Mc_e[rc_e(src)][cc_e(dst)], Ec from two
  * OR-products over the builds' classes, then one expansion to pods), else --
@@ -292,6 +295,12 @@ int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int
 #define KANO_K8S_ALL  2
 #define KANO_K8S_PODS 4
 int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int64_t* info);
+
+/* kano_build without the matrix write (model.py:125-165 up to the class-level
+ * matrix Mc, the lists and the column checks): M is written on first use
+ * (kano_get_rows, kano_path, ...).  For sources of kano_k8s_edge, which reads
+ * only Mc and the classes. */
+int kano_build_classes(kano_ctx* ctx, int path);
 
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);

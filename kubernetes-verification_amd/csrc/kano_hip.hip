@@ -99,6 +99,10 @@ struct kano_ctx {
   bool lists_mode = false;   // kano_shadow_lists context: no matrix
   bool cols_valid = false;   // color/colnand describe M
   bool rows_dirty = false;   // M edited: classes no longer describe it
+  bool rows_deferred = false;  // kano_build_classes: M is written on first use
+  int k8s_rows_cls = 0;      // kano_k8s_edge: stream pod rows per class (measured slower at
+                             // 100k pods: 0.61 vs 0.48 ms -- one block walks a class's
+                             // members serially), else per row
   bool rows_timed = false;
   bool alist_valid = false;
   bool cols_deferred = false;
@@ -1103,6 +1107,10 @@ int join_rows(kano_ctx* ctx) {
 int ensure_matrix(kano_ctx* ctx) {
   KTRY(ensure_built(ctx));
   if (ctx->lists_mode) return fail(ctx, -EINVAL, "context holds policy lists, not a matrix");
+  if (ctx->rows_deferred) {    // kano_build_classes: the matrix write, now
+    ctx->rows_deferred = false;
+    KTRY(launch_rows(ctx, false));
+  }
   return join_rows(ctx);
 }
 
@@ -1436,6 +1444,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "kmin" && v >= 1) ctx->mfma_kmin = v;
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
+        if (k == "k8srows") ctx->k8s_rows_cls = v;
         if (k == "store") ctx->rows_store = v;
         if (k == "hosttime") ctx->host_timing = v;
         if (k == "fork") ctx->fork_checks = v;
@@ -1849,6 +1858,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KCHK(hipSetDevice(ctx->device));
   KTRY(join_rows(ctx));  // the previous matrix write still reads the class lists
   ctx->built = false;
+  ctx->rows_deferred = false;
   ctx->lists_mode = false;
   ctx->rows_timed = false;
   ctx->rows_dirty = false;
@@ -1886,6 +1896,12 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
 extern "C" {
 
 int kano_build(kano_ctx* ctx, int path) { return build_impl(ctx, path, true); }
+
+int kano_build_classes(kano_ctx* ctx, int path) {
+  KTRY(build_impl(ctx, path, false));
+  ctx->rows_deferred = true;
+  return 0;
+}
 
 int kano_info(kano_ctx* ctx, int64_t* out) {
   if (!ctx || !out) return -EINVAL;
@@ -3201,29 +3217,43 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
   kano_ctx* ctx = dst;
   KCHK(hipSetDevice(dst->device));
   for (kano_ctx* s : {in_t, eg_t}) {
-    const int rc = ensure_matrix(s);
+    const int rc = ensure_built(s);
     if (rc) return fail(dst, rc, "kano_k8s_edge: source: " + s->err);
+    if (s->lists_mode) return fail(dst, -EINVAL, "kano_k8s_edge: a source holds policy lists");
     if (s->r0 != 0 || s->r1 != s->n)
       return fail(dst, -ENOTSUP, "kano_k8s_edge: a source holds a row shard (needs every row)");
   }
   KTRY(ensure_matrix(dst));
-  const i64 n = dst->n, W = dst->W, ldM = dst->ldM;
-  if (in_t->n != n || eg_t->n != n || dst->r0 != 0 || dst->r1 != n || in_t->ldM != ldM ||
-      eg_t->ldM != ldM)
+  const i64 n = dst->n, W = dst->W, ldM = dst->ldM, r0 = dst->r0, rl = rows_local(dst);
+  if (in_t->n != n || eg_t->n != n || in_t->ldM != ldM || eg_t->ldM != ldM)
     return fail(dst, -EINVAL, "kano_k8s_edge: the three matrices must have the same size");
+  const bool classes = !in_t->rows_dirty && !eg_t->rows_dirty && in_t->rc.U > 0 &&
+                       eg_t->rc.U > 0 && in_t->cc.U > 0 && eg_t->cc.U > 0 &&
+                       !(flags & KANO_K8S_PODS);
+  const bool pod_form = !(flags & KANO_K8S_ALL) && !classes;
+  if (pod_form) {
+    if (r0 != 0 || rl != n)
+      return fail(dst, -ENOTSUP, "kano_k8s_edge: the pod-level form needs every row");
+    for (kano_ctx* s : {in_t, eg_t}) {
+      const int rc = ensure_matrix(s);   // (a deferred matrix write runs now)
+      if (rc) return fail(dst, rc, "kano_k8s_edge: source: " + s->err);
+    }
+  }
   for (kano_ctx* s : {in_t, eg_t}) {
-    const int rc = sync(s);   // the sources' matrices are complete
+    const int rc = sync(s);   // the sources' classes / matrices are complete
     if (rc) return fail(dst, rc, "kano_k8s_edge: source: " + s->err);
   }
   u64* E = P_<u64>(dst->M);
   u64 added = 0;
-  if (n > 0 && W > 0) {
+  const int self = (flags & KANO_K8S_SELF) ? 1 : 0;
+  if (rl > 0 && W > 0) {
     if (flags & KANO_K8S_ALL) {
-      hipLaunchKernelGGL(k_k8s_ones, dim3(nblk(n * ldM)), dim3(TPB), 0, ctx->stream, E, ldM, n, W);
+      hipLaunchKernelGGL(k_k8s_ones, dim3(nblk(rl * ldM)), dim3(TPB), 0, ctx->stream, E, ldM, rl,
+                         n, W);
       KLAUNCH();
-    } else if (!in_t->rows_dirty && !eg_t->rows_dirty && in_t->rc.U > 0 && eg_t->rc.U > 0 &&
-               in_t->cc.U > 0 && eg_t->cc.U > 0 && !(flags & KANO_K8S_PODS)) {
-      // class level (kano_k8s.hpp): B, EgA, Mc_i transposed, Ec, expansion
+    } else if (classes) {
+      // class level (kano_k8s.hpp): B, EgA, Mc_i transposed, Ec, expansion;
+      // only Mc and the class ids of the two builds are read
       const i64 Ui = in_t->rc.U, Xi = in_t->cc.U, Ue = eg_t->rc.U, Ye = eg_t->cc.U;
       const i64 ldCe = eg_t->ldC, ldCi = in_t->ldC;
       const i64 KWb = (Ue + 63) / 64, KWa = (Ui + 63) / 64, NWe = (Ye + 63) / 64;
@@ -3250,37 +3280,60 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
                          ctx->stream, P_<u64>(ctx->pT), KWa, KWa, P_<u64>(ctx->pB), ldCe, NWe,
                          P_<u64>(ctx->pR[0]), ldCe, Xi, nch);
       KLAUNCH();
-      const int self = (flags & KANO_K8S_SELF) ? 1 : 0;
-      if (Xi * 2 <= n && ldM % 2 == 0) {
-        // expand the Xi class rows once, then stream them (and the self
-        // term, eg_t's own rows) to the pod rows
-        KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * Xi * ldM));
+      const int32_t* cci = P_<int32_t>(in_t->cc.cls);
+      const int32_t* rce = P_<int32_t>(eg_t->rc.cls);
+      const int32_t* cce = P_<int32_t>(eg_t->cc.cls);
+      if (Xi + (self ? Ue : 0) <= std::max<i64>(rl / 2, 1) && ldM % 2 == 0) {
+        // expand the class rows once (Ec's Xi rows; for self traffic Mc_e's
+        // Ue rows, i.e. EgT by egress row class), then stream them to the
+        // shard's pod rows
+        KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * (Xi + (self ? Ue : 0)) * ldM));
+        u64* Xe = P_<u64>(ctx->pR[1]);
+        u64* Se = Xe + Xi * ldM;
         hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
                            ctx->stream, P_<u64>(ctx->pR[0]), ldCe, (const int32_t*)nullptr,
-                           P_<u64>(eg_t->Mc), ldCe, P_<int32_t>(eg_t->rc.cls),
-                           P_<int32_t>(eg_t->cc.cls), 0, Xi, n, W, P_<u64>(ctx->pR[1]), ldM);
+                           (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0, Xi,
+                           n, W, Xe, ldM);
         KLAUNCH();
-        hipLaunchKernelGGL(k_k8s_rows, dim3(nblk(n * (ldM / 2))), dim3(TPB), 0, ctx->stream,
-                           P_<u64>(ctx->pR[1]), P_<int32_t>(in_t->cc.cls), P_<u64>(eg_t->M), self,
-                           n, ldM, E);
+        if (self) {
+          hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Ue, K8S_XR)), dim3(TPB),
+                             0, ctx->stream, P_<u64>(eg_t->Mc), ldCe, (const int32_t*)nullptr,
+                             (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0,
+                             Ue, n, W, Se, ldM);
+          KLAUNCH();
+        }
+        const unsigned nq = nblk(ldM / 2);
+        if (ctx->k8s_rows_cls) {
+          // by class: self -> egress row classes (base Se, gather Xe by
+          // cc_i), else in-build column classes (base Xe)
+          if (self)
+            hipLaunchKernelGGL(k_k8s_rows_cls, dim3((unsigned)Ue, nq), dim3(TPB), 0, ctx->stream,
+                               Se, Xe, cci, P_<int32_t>(eg_t->rc.moff), P_<int32_t>(eg_t->rc.mem),
+                               r0, r0 + rl, ldM, E);
+          else
+            hipLaunchKernelGGL(k_k8s_rows_cls, dim3((unsigned)Xi, nq), dim3(TPB), 0, ctx->stream,
+                               Xe, (const u64*)nullptr, cci, P_<int32_t>(in_t->cc.moff),
+                               P_<int32_t>(in_t->cc.mem), r0, r0 + rl, ldM, E);
+        } else {
+          hipLaunchKernelGGL(k_k8s_rows, dim3(nblk(rl * (ldM / 2))), dim3(TPB), 0, ctx->stream,
+                             Xe, cci, Se, rce, self, r0, rl, ldM, E);
+        }
         KLAUNCH();
       } else {
-        hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(n, K8S_XR)), dim3(TPB), 0,
-                           ctx->stream, P_<u64>(ctx->pR[0]), ldCe, P_<int32_t>(in_t->cc.cls),
-                           P_<u64>(eg_t->Mc), ldCe, P_<int32_t>(eg_t->rc.cls),
-                           P_<int32_t>(eg_t->cc.cls), self, n, n, W, E, ldM);
+        hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(rl, K8S_XR)), dim3(TPB), 0,
+                           ctx->stream, P_<u64>(ctx->pR[0]), ldCe, cci, P_<u64>(eg_t->Mc), ldCe,
+                           rce, cce, self, r0, rl, n, W, E, ldM);
         KLAUNCH();
       }
       added = (u64)-1;
     } else {
-      // pod level (edited sources): edge starts as EgT (self ingress
-      // traffic: sel = src) or empty
-      if (flags & KANO_K8S_SELF)
+      // pod level: edge starts as EgT (self ingress traffic: sel = src) or
+      // empty, then edge[src] |= OR_{sel in In[src]} EgT[sel], In = InT^T
+      if (self)
         KCHK(hipMemcpyAsync(E, eg_t->M.p, sizeof(u64) * n * ldM, hipMemcpyDeviceToDevice,
                             ctx->stream));
       else
         KCHK(hipMemsetAsync(E, 0, sizeof(u64) * n * ldM, ctx->stream));
-      // In = InT transposed (row src: the sel pods src may send to)
       KTRY(dalloc(ctx, ctx->pA, sizeof(u64) * n * ldM));
       KTRY(dalloc(ctx, ctx->pB, sizeof(u64) * n * ldM));
       KTRY(dalloc(ctx, ctx->pcnt, sizeof(u64) * PATH_CNT_SLOTS * PATH_CNT_STRIDE));
@@ -3290,7 +3343,6 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
       hipLaunchKernelGGL(k_k8s_transpose, dim3(nblk(W * CG, TPB / 64)), dim3(TPB), 0, ctx->stream,
                          P_<u64>(in_t->M), ldM, n, W, CG, n, P_<u64>(ctx->pA), ldM);
       KLAUNCH();
-      // edge[src] |= OR_{sel in In[src]} EgT[sel]
       PathGeom g;
       g.identity = true;
       g.rows = n;

@@ -45,9 +45,10 @@ __global__ __launch_bounds__(TPB) void k_k8s_transpose(const u64* __restrict__ X
 // M := every pair (kubesv's edge when check_select_by_no_policy holds and some
 // pod is selected by no policy: constraint.py:207-212,222-227); pad bits and
 // pad words zero.
-__global__ __launch_bounds__(TPB) void k_k8s_ones(u64* __restrict__ M, i64 ldM, i64 n, i64 W) {
+__global__ __launch_bounds__(TPB) void k_k8s_ones(u64* __restrict__ M, i64 ldM, i64 rows, i64 n,
+                                                 i64 W) {
   const i64 t = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (t >= n * ldM) return;
+  if (t >= rows * ldM) return;
   const i64 w = t % ldM;
   const int tail = (int)(n & 63);
   u64 v = 0;
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(TPB) void k_k8s_or_rows(const u64* __restrict__ D, 
 }
 
 // Pod rows from class rows: a block is 16 words (1024 dst pods) x 64 src
-// rows.  The 1024 column-class ids sit in LDS; per src row each lane gathers
+// rows (local row r is pod g0 + r; cci == nullptr: row r is class r).  The 1024 column-class ids sit in LDS; per src row each lane gathers
 // its pod's bit from the src's class row(s), a ballot packs 64 pods into one
 // word, and lanes 0-15 store the row's 16 contiguous words (128 B).
 constexpr int K8S_XW = 16, K8S_XR = 64;
@@ -126,8 +127,8 @@ __global__ __launch_bounds__(TPB) void k_k8s_expand(const u64* __restrict__ Ec, 
                                                     const u64* __restrict__ Mce, i64 ldCe,
                                                     const int32_t* __restrict__ rce,
                                                     const int32_t* __restrict__ cce, int self,
-                                                    i64 rows, i64 n, i64 W, u64* __restrict__ M,
-                                                    i64 ldM) {
+                                                    i64 g0, i64 rows, i64 n, i64 W,
+                                                    u64* __restrict__ M, i64 ldM) {
   __shared__ int32_t cid[K8S_XW * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const i64 w0 = (i64)blockIdx.x * K8S_XW, r0 = (i64)blockIdx.y * K8S_XR;
@@ -139,8 +140,8 @@ __global__ __launch_bounds__(TPB) void k_k8s_expand(const u64* __restrict__ Ec, 
   const i64 r1 = r0 + K8S_XR < rows ? r0 + K8S_XR : rows;
   // wave wv takes rows r0 + wv, r0 + wv + 4, ...: all 16 words of each
   for (i64 r = r0 + wv; r < r1; r += TPB / 64) {
-    const u64* er = Ec + (cci ? (i64)cci[r] : r) * ldE;
-    const u64* sr = self ? Mce + (i64)rce[r] * ldCe : nullptr;
+    const u64* er = Ec + (cci ? (i64)cci[g0 + r] : r) * ldE;
+    const u64* sr = self ? Mce + (i64)rce[g0 + r] * ldCe : nullptr;
     u64 mine = 0;
 #pragma unroll 4
     for (int k = 0; k < K8S_XW; ++k) {
@@ -161,21 +162,48 @@ __global__ __launch_bounds__(TPB) void k_k8s_expand(const u64* __restrict__ Ec, 
   }
 }
 
-// M[r] = X[cci[r]] | EgM[r] (self) -- the expanded class rows streamed to
-// the pod rows, 16 bytes per lane; EgM is the egress build's own matrix (its
-// row r is EgT[r], the self term).
+// M[r] = X[cci[g0 + r]] | S[rce[g0 + r]] (self) -- the expanded class rows
+// streamed to the pod rows of a shard, 16 bytes per lane; S holds EgT by
+// egress row class (the self term, ingress_traffic(sel, sel)).
 __global__ __launch_bounds__(TPB) void k_k8s_rows(const u64* __restrict__ X,
                                                   const int32_t* __restrict__ cci,
-                                                  const u64* __restrict__ EgM, int self, i64 n,
-                                                  i64 ldM, u64* __restrict__ M) {
+                                                  const u64* __restrict__ S,
+                                                  const int32_t* __restrict__ rce, int self,
+                                                  i64 g0, i64 rows, i64 ldM,
+                                                  u64* __restrict__ M) {
   const i64 h = ldM / 2;                                  // ldM is a multiple of 16
   const i64 t = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (t >= n * h) return;
+  if (t >= rows * h) return;
   const i64 r = t / h, q = t % h;
   typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-  u64x2 v = reinterpret_cast<const u64x2*>(X + (i64)cci[r] * ldM)[q];
-  if (self) v |= reinterpret_cast<const u64x2*>(EgM + r * ldM)[q];
+  u64x2 v = reinterpret_cast<const u64x2*>(X + (i64)cci[g0 + r] * ldM)[q];
+  if (self) v |= reinterpret_cast<const u64x2*>(S + (i64)rce[g0 + r] * ldM)[q];
   reinterpret_cast<u64x2*>(M + r * ldM)[q] = v;
+}
+
+// The same stream, one block per (class c, 512-word chunk): the class's
+// expanded row base[c] is loaded once and each member pod m of c in [g0, g1)
+// gets base[c] | X[xid[m]] (X nullable) -- HBM then sees the writes and one
+// read of each class row; the gathered X rows (few) stay in L2.
+__global__ __launch_bounds__(TPB) void k_k8s_rows_cls(const u64* __restrict__ base,
+                                                      const u64* __restrict__ X,
+                                                      const int32_t* __restrict__ xid,
+                                                      const int32_t* __restrict__ moff,
+                                                      const int32_t* __restrict__ mem, i64 g0,
+                                                      i64 g1, i64 ldM, u64* __restrict__ M) {
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const i64 h = ldM / 2, c = blockIdx.x;
+  const i64 q = (i64)blockIdx.y * TPB + threadIdx.x;
+  if (q >= h) return;
+  const u64x2 b = reinterpret_cast<const u64x2*>(base + c * ldM)[q];
+  const int32_t k1 = moff[c + 1];
+  for (int32_t k = moff[c]; k < k1; ++k) {
+    const i64 m = mem[k];
+    if (m < g0 || m >= g1) continue;
+    u64x2 v = b;
+    if (X) v |= reinterpret_cast<const u64x2*>(X + (i64)xid[m] * ldM)[q];
+    reinterpret_cast<u64x2*>(M + (m - g0) * ldM)[q] = v;
+  }
 }
 
 }  // namespace kano

@@ -117,6 +117,12 @@ class DeviceBuild:
         p = nat.PATHS[path or self.path]
         self._chk(self.lib.kano_build(self.ctx, p), "kano_build")
 
+    def build_classes(self, path: Optional[str] = None) -> None:
+        """kano_build_classes: the build up to the class-level matrix; M is
+        written on first use."""
+        p = nat.PATHS[path or self.path]
+        self._chk(self.lib.kano_build_classes(self.ctx, p), "kano_build_classes")
+
     def info(self) -> dict:
         out = np.zeros(nat.INFO_SLOTS, dtype=np.int64)
         self._chk(self.lib.kano_info(self.ctx, _ptr(out)), "kano_info")

@@ -55,6 +55,7 @@ SIGNATURES = {
     "kano_set_expressions": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kano_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "kano_k8s_edge": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "kano_build_classes": (c_int, [c_void_p, c_int]),
     "kano_path_shard_words": (c_int, [c_void_p, POINTER(c_int64)]),
     "kano_path_shard": (c_int, [c_void_p, c_void_p]),
     "kano_path_combine": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_int, c_int,

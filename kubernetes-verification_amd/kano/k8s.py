@@ -280,17 +280,25 @@ def compile_policies(pods: List[Pod], policies: List[NetworkPolicy],
 
 def build(pods: List[Pod], policies: List[NetworkPolicy], namespaces: List[Namespace],
           check_self_ingress_traffic: bool = True, check_select_by_no_policy: bool = False,
-          device: int = 0, path: str = "auto", form: str = "classes") -> K8sReachability:
+          device: int = 0, path: str = "auto", form: str = "classes",
+          rows: Optional[tuple] = None) -> K8sReachability:
     """kubesv's ``build`` (constraint.py:285-299) on the device: the edge
     relation as an n x n matrix (rows src, columns dst).  ``form``: the
     product over the builds' row / column classes ("classes") or over pods
-    ("pods"); both give the same matrix."""
+    ("pods"); both give the same matrix.  ``rows=(r0, r1)``: only those rows
+    of the edge matrix (a multi-GPU rank's shard; the class form)."""
     from ._engine import DeviceBuild
     from ._intern import intern
     containers, ing, egr, sel_only = compile_policies(pods, policies, namespaces)
     n = len(pods)
-    in_t = DeviceBuild(intern(containers, ing), device=device, path=path)
-    eg_t = DeviceBuild(intern(containers, egr), device=device, path=path)
+
+    def operand(pols):
+        b = DeviceBuild(intern(containers, pols), device=device, path=path, build=False)
+        b.build_classes(path)          # Mc and classes; M written only if read
+        return b
+
+    in_t = operand(ing)
+    eg_t = operand(egr)
     selected = None
     all_pairs = False
     if check_select_by_no_policy:
@@ -301,9 +309,9 @@ def build(pods: List[Pod], policies: List[NetworkPolicy], namespaces: List[Names
             col = _wrap(ms, n).getcol(0)
             selected = np.array([bool(col[i]) for i in range(n)], dtype=bool)
         all_pairs = bool(n) and not bool(selected.all())
-    out = DeviceBuild.empty(n, device=device)
+    out = DeviceBuild.empty(n, device=device, rows=rows)
     added = out.k8s_edge_from(in_t, eg_t, bool(check_self_ingress_traffic), all_pairs,
                               pods=(form == "pods"))
     info = {"ingress_policies": len(ing), "egress_policies": len(egr),
-            "product_bits": added, "all_pairs": all_pairs}
+            "product_bits": added, "all_pairs": all_pairs, "rows": rows}
     return K8sReachability(_wrap(out, n), _wrap(in_t, n), _wrap(eg_t, n), selected, info)

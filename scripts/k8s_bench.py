@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--pods", type=int, nargs="+", default=[10000, 100000])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--form", default="classes", choices=["classes", "pods"])
+    ap.add_argument("--ranks", type=int, default=1,
+                    help="time rank 0's row shard of an N-rank split (the edge rows [0, n/N))")
     args = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime first, as the bench does)
     from kano import k8s
@@ -71,10 +73,15 @@ def main():
         best = None
         for _ in range(args.reps):
             t0 = time.perf_counter()
-            in_t = DeviceBuild(ti)
-            eg_t = DeviceBuild(te)
+            in_t = DeviceBuild(ti, build=False)
+            in_t.build_classes()      # Mc and classes only (kano.k8s.build's operands)
+            eg_t = DeviceBuild(te, build=False)
+            eg_t.build_classes()
+            if args.form == "pods":   # the pod-level product reads both matrices
+                in_t.rows(0, 1)
+                eg_t.rows(0, 1)
             t1 = time.perf_counter()
-            out = DeviceBuild.empty(n)
+            out = DeviceBuild.empty(n, rows=(0, n // args.ranks) if args.ranks > 1 else None)
             t2 = time.perf_counter()
             added = out.k8s_edge_from(in_t, eg_t, True, False, pods=args.form == "pods")
             t3 = time.perf_counter()
@@ -86,7 +93,7 @@ def main():
         from kano import algorithm as alg
         from kano.k8s import _wrap
         em = _wrap(out, n)
-        iso = len(alg.all_isolated(em))
+        iso = len(alg.all_isolated(em)) if args.ranks == 1 else None
         print(json.dumps({
             "workload": "kubesv edge relation (kano.k8s), synthetic K8s cluster",
             "form": args.form, "pods": n, "namespaces": len(nss), "policies": len(pols),
@@ -94,7 +101,9 @@ def main():
             "host_compile_s": round(t_compile, 3), "host_intern_s": round(t_intern, 3),
             "builds_ms": round(best[0] * 1e3, 3), "edge_ms": round(best[1] * 1e3, 3),
             "product_bits": added, "edge_matrix_bytes": 8 * n * W,
-            "all_isolated": iso, "all_reachable": len(alg.all_reachable(em))}), flush=True)
+            "ranks": args.ranks, "rows": n // args.ranks, "all_isolated": iso,
+            "all_reachable": len(alg.all_reachable(em)) if args.ranks == 1 else None}),
+            flush=True)
 
 
 if __name__ == "__main__":

@@ -242,3 +242,40 @@ def test_edge_larger_cluster(form, seed, self_traffic):
     for i, j in edge:
         ref[i, j >> 6] |= np.uint64(1) << np.uint64(j & 63)
     assert np.array_equal(M, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cuts", [[0, 30, 60], [0, 1, 59, 60], [0, 20, 20, 45, 60]])
+@pytest.mark.parametrize("self_traffic", [True, False])
+def test_edge_row_shards(cuts, self_traffic):
+    """A rank's rows of the edge matrix (rows=(r0, r1)), recombined, equal
+    the whole matrix and the restated rules (the multi-GPU split)."""
+    from kano import k8s
+    from oracle import kano_oracle as orc
+    pods, pols, nss = _cluster(5)
+    n = len(pods)
+    edge, _, _ = orc.kubesv_edge_py(pods, pols, nss, self_traffic)
+    parts = []
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        r = k8s.build(pods, pols, nss, check_self_ingress_traffic=self_traffic, rows=(r0, r1))
+        parts.append(r.edge.engine.rows(r0, r1 - r0))
+    M = np.concatenate(parts, axis=0)
+    assert M.shape[0] == n
+    assert _bits(M, n) == edge
+
+
+@pytest.mark.gpu
+def test_build_classes_defers_the_matrix():
+    """kano_build_classes: the same classes and checks as kano_build, and the
+    same matrix once it is read (written on first use)."""
+    from kano import model
+    from kano._engine import DeviceBuild
+    from kano._intern import intern
+    from kano.synth import make_cluster, cluster_objects
+    cs, ps = cluster_objects(make_cluster(800, 80, seed=4), model)
+    t = intern(cs, ps)
+    a = DeviceBuild(t)
+    b = DeviceBuild(t, build=False)
+    b.build_classes()
+    assert a.info() == b.info()
+    assert np.array_equal(a.rows(0, 800), b.rows(0, 800))
