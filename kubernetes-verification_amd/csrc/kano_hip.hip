@@ -100,6 +100,7 @@ struct kano_ctx {
   bool cols_valid = false;   // color/colnand describe M
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_deferred = false;  // kano_build_classes: M is written on first use
+  bool defer_alloc = false;    // (inside kano_build_classes: no M allocation)
   int k8s_rows_cls = 0;      // kano_k8s_edge: stream pod rows per class (measured slower at
                              // 100k pods: 0.61 vs 0.48 ms -- one block walks a class's
                              // members serially), else per row
@@ -1107,8 +1108,10 @@ int join_rows(kano_ctx* ctx) {
 int ensure_matrix(kano_ctx* ctx) {
   KTRY(ensure_built(ctx));
   if (ctx->lists_mode) return fail(ctx, -EINVAL, "context holds policy lists, not a matrix");
-  if (ctx->rows_deferred) {    // kano_build_classes: the matrix write, now
+  if (ctx->rows_deferred) {    // kano_build_classes: the matrix, now
     ctx->rows_deferred = false;
+    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM) *
+                                 ctx->m_over));
     KTRY(launch_rows(ctx, false));
   }
   return join_rows(ctx);
@@ -1865,7 +1868,8 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->cols_valid = false;
   ctx->shadow_total = -1;
   const i64 rl = rows_local(ctx);
-  KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over));
+  if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
+    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KTRY(stage_mark(ctx, 0, ctx->stream));
@@ -1898,9 +1902,12 @@ extern "C" {
 int kano_build(kano_ctx* ctx, int path) { return build_impl(ctx, path, true); }
 
 int kano_build_classes(kano_ctx* ctx, int path) {
-  KTRY(build_impl(ctx, path, false));
-  ctx->rows_deferred = true;
-  return 0;
+  if (!ctx) return -EINVAL;
+  ctx->defer_alloc = true;
+  const int rc = build_impl(ctx, path, false);
+  ctx->defer_alloc = false;
+  if (rc == 0) ctx->rows_deferred = true;
+  return rc;
 }
 
 int kano_info(kano_ctx* ctx, int64_t* out) {

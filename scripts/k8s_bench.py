@@ -74,8 +74,9 @@ def main():
         for _ in range(args.reps):
             t0 = time.perf_counter()
             in_t = DeviceBuild(ti, build=False)
-            in_t.build_classes()      # Mc and classes only (kano.k8s.build's operands)
             eg_t = DeviceBuild(te, build=False)
+            tu = time.perf_counter()
+            in_t.build_classes()      # Mc and classes only (kano.k8s.build's operands)
             eg_t.build_classes()
             if args.form == "pods":   # the pod-level product reads both matrices
                 in_t.rows(0, 1)
@@ -85,8 +86,8 @@ def main():
             t2 = time.perf_counter()
             added = out.k8s_edge_from(in_t, eg_t, True, False, pods=args.form == "pods")
             t3 = time.perf_counter()
-            r = (t1 - t0, t3 - t2)
-            best = r if best is None or sum(r) < sum(best) else best
+            r = (t1 - t0, t3 - t2, tu - t0)
+            best = r if best is None or r[0] + r[1] < best[0] + best[1] else best
             del in_t, eg_t
         W = (n + 63) // 64
         # edge density from the matrix itself
@@ -99,7 +100,7 @@ def main():
             "form": args.form, "pods": n, "namespaces": len(nss), "policies": len(pols),
             "ingress_peers": len(ing), "egress_peers": len(egr),
             "host_compile_s": round(t_compile, 3), "host_intern_s": round(t_intern, 3),
-            "builds_ms": round(best[0] * 1e3, 3), "edge_ms": round(best[1] * 1e3, 3),
+            "builds_ms": round(best[0] * 1e3, 3), "of_which_upload_ms": round(best[2] * 1e3, 3), "edge_ms": round(best[1] * 1e3, 3),
             "product_bits": added, "edge_matrix_bytes": 8 * n * W,
             "ranks": args.ranks, "rows": n // args.ranks, "all_isolated": iso,
             "all_reachable": len(alg.all_reachable(em)) if args.ranks == 1 else None}),
