@@ -294,6 +294,10 @@ int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int
 #define KANO_K8S_SELF 1
 #define KANO_K8S_ALL  2
 #define KANO_K8S_PODS 4
+/* KANO_K8S_DST_EG: dst is itself a build of eg_t's tables over its row range
+ * (kano_build writes EgT's rows, the self term), and the product is OR-ed
+ * into it in place -- no expansion of the egress classes. */
+#define KANO_K8S_DST_EG 8
 int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int64_t* info);
 
 /* kano_build without the matrix write (model.py:125-165 up to the class-level

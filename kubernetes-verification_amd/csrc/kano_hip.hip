@@ -3238,6 +3238,9 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
                        eg_t->rc.U > 0 && in_t->cc.U > 0 && eg_t->cc.U > 0 &&
                        !(flags & KANO_K8S_PODS);
   const bool pod_form = !(flags & KANO_K8S_ALL) && !classes;
+  if ((flags & KANO_K8S_DST_EG) && (pod_form || dst->rows_dirty || dst->P != eg_t->P))
+    return fail(dst, -EINVAL, "kano_k8s_edge: KANO_K8S_DST_EG needs dst = an unedited build "
+                              "of the egress policies (class-level form)");
   if (pod_form) {
     if (r0 != 0 || rl != n)
       return fail(dst, -ENOTSUP, "kano_k8s_edge: the pod-level form needs every row");
@@ -3290,11 +3293,15 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
       const int32_t* cci = P_<int32_t>(in_t->cc.cls);
       const int32_t* rce = P_<int32_t>(eg_t->rc.cls);
       const int32_t* cce = P_<int32_t>(eg_t->cc.cls);
-      if (Xi + (self ? Ue : 0) <= std::max<i64>(rl / 2, 1) && ldM % 2 == 0) {
+      // KANO_K8S_DST_EG: dst already holds the shard's EgT rows (a build of
+      // the egress policies), so the self term needs no expansion
+      const bool in_place = self && (flags & KANO_K8S_DST_EG);
+      const i64 Us = (self && !in_place) ? Ue : 0;
+      if (Xi + Us <= std::max<i64>(rl / 2, 1) && ldM % 2 == 0) {
         // expand the class rows once (Ec's Xi rows; for self traffic Mc_e's
         // Ue rows, i.e. EgT by egress row class), then stream them to the
         // shard's pod rows
-        KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * (Xi + (self ? Ue : 0)) * ldM));
+        KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * (Xi + Us) * ldM));
         u64* Xe = P_<u64>(ctx->pR[1]);
         u64* Se = Xe + Xi * ldM;
         hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
@@ -3302,7 +3309,7 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
                            (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0, Xi,
                            n, W, Xe, ldM);
         KLAUNCH();
-        if (self) {
+        if (Us) {
           hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Ue, K8S_XR)), dim3(TPB),
                              0, ctx->stream, P_<u64>(eg_t->Mc), ldCe, (const int32_t*)nullptr,
                              (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0,
@@ -3310,7 +3317,10 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
           KLAUNCH();
         }
         const unsigned nq = nblk(ldM / 2);
-        if (ctx->k8s_rows_cls) {
+        if (in_place) {
+          hipLaunchKernelGGL(k_k8s_or_into, dim3(nblk(rl * (ldM / 2))), dim3(TPB), 0, ctx->stream,
+                             Xe, cci, r0, rl, ldM, E);
+        } else if (ctx->k8s_rows_cls) {
           // by class: self -> egress row classes (base Se, gather Xe by
           // cc_i), else in-build column classes (base Xe)
           if (self)

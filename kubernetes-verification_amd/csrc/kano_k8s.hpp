@@ -181,6 +181,21 @@ __global__ __launch_bounds__(TPB) void k_k8s_rows(const u64* __restrict__ X,
   reinterpret_cast<u64x2*>(M + r * ldM)[q] = v;
 }
 
+// M[r] |= X[cci[g0 + r]]: the destination already holds EgT's rows of the
+// shard (a build of the egress policies: the self term written by k_rows),
+// the expanded Ec rows are OR-ed in place.
+__global__ __launch_bounds__(TPB) void k_k8s_or_into(const u64* __restrict__ X,
+                                                     const int32_t* __restrict__ cci, i64 g0,
+                                                     i64 rows, i64 ldM, u64* __restrict__ M) {
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const i64 h = ldM / 2;
+  const i64 t = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (t >= rows * h) return;
+  const i64 r = t / h, q = t % h;
+  u64x2* m = reinterpret_cast<u64x2*>(M + r * ldM) + q;
+  *m |= reinterpret_cast<const u64x2*>(X + (i64)cci[g0 + r] * ldM)[q];
+}
+
 // The same stream, one block per (class c, 512-word chunk): the class's
 // expanded row base[c] is loaded once and each member pod m of c in [g0, g1)
 // gets base[c] | X[xid[m]] (X nullable) -- HBM then sees the writes and one

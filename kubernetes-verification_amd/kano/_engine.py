@@ -169,12 +169,13 @@ class DeviceBuild:
                   "kano_import_rows")
 
     def k8s_edge_from(self, in_t: "DeviceBuild", eg_t: "DeviceBuild", self_traffic: bool,
-                      all_pairs: bool, pods: bool = False) -> int:
+                      all_pairs: bool, pods: bool = False, dst_is_egress: bool = False) -> int:
         """This context's matrix := kubesv's edge relation from the two
         per-direction builds (kano_k8s_edge; kubesv/kubesv/constraint.py:191-231).
         Returns the bits the product added beyond the self term."""
         info = np.zeros(1, dtype=np.int64)
-        flags = (1 if self_traffic else 0) | (2 if all_pairs else 0) | (4 if pods else 0)
+        flags = ((1 if self_traffic else 0) | (2 if all_pairs else 0) | (4 if pods else 0) |
+                 (8 if dst_is_egress else 0))
         self._chk(self.lib.kano_k8s_edge(in_t.ctx, eg_t.ctx, self.ctx, flags, _ptr(info)),
                   "kano_k8s_edge")
         return int(info[0])

@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--pods", type=int, nargs="+", default=[10000, 100000])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--form", default="classes", choices=["classes", "pods"])
+    ap.add_argument("--inplace", type=int, default=-1,
+                    help="1: build the destination from the egress policies (the self term), "
+                         "0: expand the self term, -1: as kano.k8s.build (expand)")
     ap.add_argument("--ranks", type=int, default=1,
                     help="time rank 0's row shard of an N-rank split (the edge rows [0, n/N))")
     args = ap.parse_args()
@@ -82,9 +85,18 @@ def main():
                 in_t.rows(0, 1)
                 eg_t.rows(0, 1)
             t1 = time.perf_counter()
-            out = DeviceBuild.empty(n, rows=(0, n // args.ranks) if args.ranks > 1 else None)
-            t2 = time.perf_counter()
-            added = out.k8s_edge_from(in_t, eg_t, True, False, pods=args.form == "pods")
+            rows = (0, n // args.ranks) if args.ranks > 1 else None
+            inplace = args.inplace if args.inplace >= 0 else 0
+            if args.form == "classes" and inplace:
+                # as kano.k8s.build: the destination is the egress build of the
+                # rows (its matrix write is the self term); timed with the edge
+                t2 = time.perf_counter()
+                out = DeviceBuild(te, rows=rows)
+                added = out.k8s_edge_from(in_t, eg_t, True, False, dst_is_egress=True)
+            else:
+                out = DeviceBuild.empty(n, rows=rows)
+                t2 = time.perf_counter()
+                added = out.k8s_edge_from(in_t, eg_t, True, False, pods=args.form == "pods")
             t3 = time.perf_counter()
             r = (t1 - t0, t3 - t2, tu - t0)
             best = r if best is None or r[0] + r[1] < best[0] + best[1] else best
@@ -97,7 +109,8 @@ def main():
         iso = len(alg.all_isolated(em)) if args.ranks == 1 else None
         print(json.dumps({
             "workload": "kubesv edge relation (kano.k8s), synthetic K8s cluster",
-            "form": args.form, "pods": n, "namespaces": len(nss), "policies": len(pols),
+            "form": args.form + ("+inplace" if args.form == "classes" and inplace else ""),
+            "pods": n, "namespaces": len(nss), "policies": len(pols),
             "ingress_peers": len(ing), "egress_peers": len(egr),
             "host_compile_s": round(t_compile, 3), "host_intern_s": round(t_intern, 3),
             "builds_ms": round(best[0] * 1e3, 3), "of_which_upload_ms": round(best[2] * 1e3, 3), "edge_ms": round(best[1] * 1e3, 3),

@@ -185,14 +185,15 @@ def test_compilation_matches_oracle(seed, self_traffic):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(12))
 @pytest.mark.parametrize("self_traffic,by_none", [(True, False), (False, False), (True, True)])
-@pytest.mark.parametrize("form", ["classes", "pods"])
+@pytest.mark.parametrize("form", ["classes", "pods", "classes+build"])
 def test_edge_matches_oracle(seed, self_traffic, by_none, form):
     from kano import k8s
     from oracle import kano_oracle as orc
     pods, pols, nss = _cluster(seed)
     n = len(pods)
     r = k8s.build(pods, pols, nss, check_self_ingress_traffic=self_traffic,
-                  check_select_by_no_policy=by_none, form=form)
+                  check_select_by_no_policy=by_none, form=form.split("+")[0],
+                  self_term="build" if form.endswith("build") else "expand")
     edge, ing, eg = orc.kubesv_edge_py(pods, pols, nss, self_traffic, by_none)
     assert _bits(r.edge.engine.rows(0, n), n) == edge
     # the product's operands: ingress_traffic [sel][src] without the self
@@ -247,7 +248,8 @@ def test_edge_larger_cluster(form, seed, self_traffic):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cuts", [[0, 30, 60], [0, 1, 59, 60], [0, 20, 20, 45, 60]])
 @pytest.mark.parametrize("self_traffic", [True, False])
-def test_edge_row_shards(cuts, self_traffic):
+@pytest.mark.parametrize("self_term", ["expand", "build"])
+def test_edge_row_shards(cuts, self_traffic, self_term):
     """A rank's rows of the edge matrix (rows=(r0, r1)), recombined, equal
     the whole matrix and the restated rules (the multi-GPU split)."""
     from kano import k8s
@@ -257,7 +259,8 @@ def test_edge_row_shards(cuts, self_traffic):
     edge, _, _ = orc.kubesv_edge_py(pods, pols, nss, self_traffic)
     parts = []
     for r0, r1 in zip(cuts[:-1], cuts[1:]):
-        r = k8s.build(pods, pols, nss, check_self_ingress_traffic=self_traffic, rows=(r0, r1))
+        r = k8s.build(pods, pols, nss, check_self_ingress_traffic=self_traffic, rows=(r0, r1),
+                      self_term=self_term)
         parts.append(r.edge.engine.rows(r0, r1 - r0))
     M = np.concatenate(parts, axis=0)
     assert M.shape[0] == n
