@@ -101,6 +101,28 @@ class NetworkPolicy:
         return NetworkPolicy(md.get("name"), md.get("namespace"), obj.get("spec"))
 
 
+def from_dict(kind: str, data: Dict[str, Any]):
+    """kubesv.parser.from_dict (kubesv/kubesv/parser.py:9-18) without the
+    kubernetes client: a manifest dict as this module's Pod / Namespace /
+    NetworkPolicy (kind 'V1Pod', 'V1Namespace', 'V1NetworkPolicy'; the 'V1'
+    prefix is optional)."""
+    k = kind[2:] if kind.startswith("V1") else kind
+    md = (data or {}).get("metadata") or {}
+    if k == "Pod":
+        return Pod(md.get("name"), md.get("namespace"), md.get("labels"))
+    if k == "Namespace":
+        return Namespace(md.get("name"), md.get("labels"))
+    if k == "NetworkPolicy":
+        return NetworkPolicy.from_manifest(data)
+    raise ValueError(f"unsupported kind {kind!r}")
+
+
+def from_yaml(kind: str, yml: str):
+    """kubesv.parser.from_yaml (parser.py:21-22)."""
+    import yaml
+    return from_dict(kind, yaml.safe_load(yml))
+
+
 # ---------------------------------------------------------------------------
 # selectors -> requirement terms
 # ---------------------------------------------------------------------------

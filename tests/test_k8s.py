@@ -282,3 +282,37 @@ def test_build_classes_defers_the_matrix():
     b.build_classes()
     assert a.info() == b.info()
     assert np.array_equal(a.rows(0, 800), b.rows(0, 800))
+
+
+# kubesv's sample cluster (kubesv/sample/example.py:106-174; its test,
+# kubesv/tests/test_basic.py:13-30, queries egress_traffic with self ingress
+# traffic on).  Worked by hand from the rules: the policy selects the two db
+# pods of "default" (0, 1); egress goes to tomcat pods of namespaces without
+# "l" (8, 9); ingress comes from tomcat pods of nonsense=default namespaces
+# (8, 9) and, with self traffic, from the selected pod itself.
+PAPER_EGRESS = {(8, 0), (9, 0), (8, 1), (9, 1)}                   # (dst, sel)
+PAPER_EDGE = {(s, d) for s in (0, 1, 8, 9) for d in (8, 9)}            # (src, dst)
+
+
+def test_paper_example_oracle():
+    from sample.kubesv_example import paper_example
+    from oracle import kano_oracle as orc
+    pods, pols, nss = paper_example()
+    assert [p.name for p in pods][:2] == ["db_0", "db_1"] and pols[0].namespace == "default"
+    edge, ing, eg = orc.kubesv_edge_py(pods, pols, nss, True, False)
+    assert {(d, s) for s in range(len(pods)) for d in eg[s]} == PAPER_EGRESS
+    assert edge == PAPER_EDGE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("self_term", ["expand", "build"])
+def test_paper_example_gpu(self_term):
+    from kano import k8s, algorithm as alg
+    from sample.kubesv_example import paper_example
+    pods, pols, nss = paper_example()
+    n = len(pods)
+    r = k8s.build(pods, pols, nss, check_self_ingress_traffic=True,
+                  check_select_by_no_policy=False, self_term=self_term)
+    assert {(d, s) for s, d in _bits(r.egress_traffic.engine.rows(0, n), n)} == PAPER_EGRESS
+    assert _bits(r.edge.engine.rows(0, n), n) == PAPER_EDGE
+    assert alg.all_isolated(r.edge) == [j for j in range(n) if j not in (8, 9)]
