@@ -3290,6 +3290,8 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
                          ctx->stream, P_<u64>(ctx->pT), KWa, KWa, P_<u64>(ctx->pB), ldCe, NWe,
                          P_<u64>(ctx->pR[0]), ldCe, Xi, nch);
       KLAUNCH();
+      // class rows of <= K8S_STAGE_W words are staged in LDS by the expansion
+      auto K8S_EXPAND = ldCe <= K8S_STAGE_W ? k_k8s_expand<true> : k_k8s_expand<false>;
       const int32_t* cci = P_<int32_t>(in_t->cc.cls);
       const int32_t* rce = P_<int32_t>(eg_t->rc.cls);
       const int32_t* cce = P_<int32_t>(eg_t->cc.cls);
@@ -3304,13 +3306,13 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
         KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * (Xi + Us) * ldM));
         u64* Xe = P_<u64>(ctx->pR[1]);
         u64* Se = Xe + Xi * ldM;
-        hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
+        hipLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
                            ctx->stream, P_<u64>(ctx->pR[0]), ldCe, (const int32_t*)nullptr,
                            (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0, Xi,
                            n, W, Xe, ldM);
         KLAUNCH();
         if (Us) {
-          hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(Ue, K8S_XR)), dim3(TPB),
+          hipLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(Ue, K8S_XR)), dim3(TPB),
                              0, ctx->stream, P_<u64>(eg_t->Mc), ldCe, (const int32_t*)nullptr,
                              (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0,
                              Ue, n, W, Se, ldM);
@@ -3337,7 +3339,7 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
         }
         KLAUNCH();
       } else {
-        hipLaunchKernelGGL(k_k8s_expand, dim3(nblk(ldM, K8S_XW), nblk(rl, K8S_XR)), dim3(TPB), 0,
+        hipLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(rl, K8S_XR)), dim3(TPB), 0,
                            ctx->stream, P_<u64>(ctx->pR[0]), ldCe, cci, P_<u64>(eg_t->Mc), ldCe,
                            rce, cce, self, r0, rl, n, W, E, ldM);
         KLAUNCH();

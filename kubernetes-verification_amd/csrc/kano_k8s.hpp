@@ -121,7 +121,11 @@ __global__ __launch_bounds__(TPB) void k_k8s_or_rows(const u64* __restrict__ D, 
 // rows (local row r is pod g0 + r; cci == nullptr: row r is class r).  The 1024 column-class ids sit in LDS; per src row each lane gathers
 // its pod's bit from the src's class row(s), a ballot packs 64 pods into one
 // word, and lanes 0-15 store the row's 16 contiguous words (128 B).
-constexpr int K8S_XW = 16, K8S_XR = 64;
+constexpr int K8S_XW = 16, K8S_XR = 64, K8S_STAGE_W = 32;
+// STAGE (class rows of <= K8S_STAGE_W words): the block's 64 class rows,
+// OR-ed with their self-term rows, are staged in LDS first, so the per-pod
+// gathers read LDS; each lane keeps its 16 column-class ids in registers.
+template <bool STAGE>
 __global__ __launch_bounds__(TPB) void k_k8s_expand(const u64* __restrict__ Ec, i64 ldE,
                                                     const int32_t* __restrict__ cci,
                                                     const u64* __restrict__ Mce, i64 ldCe,
@@ -130,26 +134,42 @@ __global__ __launch_bounds__(TPB) void k_k8s_expand(const u64* __restrict__ Ec, 
                                                     i64 g0, i64 rows, i64 n, i64 W,
                                                     u64* __restrict__ M, i64 ldM) {
   __shared__ int32_t cid[K8S_XW * 64];
+  __shared__ u64 rowbuf[STAGE ? K8S_XR * K8S_STAGE_W : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const i64 w0 = (i64)blockIdx.x * K8S_XW, r0 = (i64)blockIdx.y * K8S_XR;
   for (int t = threadIdx.x; t < K8S_XW * 64; t += TPB) {
     const i64 j = w0 * 64 + t;
     cid[t] = j < n ? cce[j] : -1;
   }
-  __syncthreads();
   const i64 r1 = r0 + K8S_XR < rows ? r0 + K8S_XR : rows;
+  if (STAGE) {
+    for (int t = threadIdx.x; t < K8S_XR * ldE; t += TPB) {
+      const i64 rr = t / ldE, w = t % ldE, r = r0 + rr;
+      u64 v = 0;
+      if (r < r1) {
+        v = Ec[(cci ? (i64)cci[g0 + r] : r) * ldE + w];
+        if (self) v |= Mce[(i64)rce[g0 + r] * ldCe + w];
+      }
+      rowbuf[t] = v;
+    }
+  }
+  __syncthreads();
+  int cr[K8S_XW];
+#pragma unroll
+  for (int k = 0; k < K8S_XW; ++k) cr[k] = cid[k * 64 + lane];
   // wave wv takes rows r0 + wv, r0 + wv + 4, ...: all 16 words of each
   for (i64 r = r0 + wv; r < r1; r += TPB / 64) {
-    const u64* er = Ec + (cci ? (i64)cci[g0 + r] : r) * ldE;
-    const u64* sr = self ? Mce + (i64)rce[g0 + r] * ldCe : nullptr;
+    const u64* er = STAGE ? rowbuf + (r - r0) * ldE
+                          : Ec + (cci ? (i64)cci[g0 + r] : r) * ldE;
+    const u64* sr = (!STAGE && self) ? Mce + (i64)rce[g0 + r] * ldCe : nullptr;
     u64 mine = 0;
-#pragma unroll 4
+#pragma unroll
     for (int k = 0; k < K8S_XW; ++k) {
-      const int c = cid[k * 64 + lane];
+      const int c = cr[k];
       int bit = 0;
       if (c >= 0) {
         u64 v = er[c >> 6];
-        if (self) v |= sr[c >> 6];
+        if (!STAGE && self) v |= sr[c >> 6];
         bit = (int)((v >> (c & 63)) & 1ull);
       }
       const u64 b = __ballot(bit);
