@@ -330,8 +330,8 @@ def build(pods: List[Pod], policies: List[NetworkPolicy], namespaces: List[Names
         selected = np.zeros(n, dtype=bool)
         if n:
             # allow = {} matches every pod: column 0 of M is the selected flag
-            col = _wrap(ms, n).getcol(0)
-            selected = np.array([bool(col[i]) for i in range(n)], dtype=bool)
+            from ._bits import words_to_bool
+            selected = words_to_bool(_wrap(ms, n).getcol(0).words(), n)
         all_pairs = bool(n) and not bool(selected.all())
     # the self term: expanded from the egress classes ("expand", the
     # default), or the destination is a build of the egress policies over its
