@@ -316,3 +316,28 @@ def test_paper_example_gpu(self_term):
     assert {(d, s) for s, d in _bits(r.egress_traffic.engine.rows(0, n), n)} == PAPER_EGRESS
     assert _bits(r.edge.engine.rows(0, n), n) == PAPER_EDGE
     assert alg.all_isolated(r.edge) == [j for j in range(n) if j not in (8, 9)]
+
+
+def test_from_yaml_manifests():
+    """kano.k8s.from_yaml reads the manifests kubesv's parser deserialises
+    (kubesv/kubesv/parser.py:9-22): metadata name / namespace / labels, the
+    NetworkPolicy spec as written."""
+    from kano import k8s
+    pod = k8s.from_yaml("V1Pod", """
+apiVersion: v1
+kind: Pod
+metadata: {name: label-demo, labels: {environment: production, app: nginx}}
+spec: {containers: [{name: nginx, image: "nginx:1.14.2"}]}
+""")
+    assert (pod.name, pod.namespace, pod.labels) == (
+        "label-demo", "default", {"environment": "production", "app": "nginx"})
+    ns = k8s.from_yaml("Namespace", "kind: Namespace\nmetadata: {name: shop, labels: {team: a}}\n")
+    assert (ns.name, ns.labels) == ("shop", {"team": "a"})
+    pol = k8s.from_yaml("V1NetworkPolicy", """
+kind: NetworkPolicy
+metadata: {name: default-deny-all, namespace: default}
+spec: {podSelector: {}, ingress: []}
+""")
+    assert pol.namespace == "default" and pol.spec == {"podSelector": {}, "ingress": []}
+    with pytest.raises(ValueError):
+        k8s.from_dict("V1Service", {})
