@@ -106,6 +106,12 @@ int kano_get_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* dst);
 /* Overwrite rows (assignment to ReachabilityMatrix.matrix rows / the
  * ReachabilityMatrix(container_size, matrix) constructor, model.py:167-169). */
 int kano_put_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint64_t* src);
+/* Per-row 64-bit digests of rows [r0, r0 + nrows) (no reference counterpart:
+ * a full-size matrix does not fit the host; the tests compare digests of
+ * two builds of the same rows, e.g. bitwise vs MFMA, sharded vs unsharded).
+ * digest = sum_k mix64(row[k] ^ k * 0xD6E8FEB86659FD93) mod 2^64 over the W
+ * words, mix64 the splitmix64 finaliser. */
+int kano_rows_digest(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* out);
 int kano_get_col(kano_ctx* ctx, int64_t j, uint64_t* dst /* ceil(rows/64) */);
 int kano_get_bit(kano_ctx* ctx, int64_t i, int64_t j, int* value);
 int kano_set_bit(kano_ctx* ctx, int64_t i, int64_t j, int value);
@@ -160,7 +166,9 @@ int kano_conflict(kano_ctx* ctx, int* raises);
  * with kano_col_flags_dev / kano_crosscheck_dev across shards instead).
  * When shadow_count is non-NULL, policy_shadow runs too (kano_shadow) and
  * the pairs are copied to shadow_pairs if count <= shadow_cap (otherwise
- * fetch them with kano_shadow_fetch). */
+ * fetch them with kano_shadow_fetch).  shadow_cap < 0 asks for the count
+ * only: every subset test still runs, the pairs are not emitted (broad
+ * selectors give ~1e11 of them; kano_shadow_fetch then fails). */
 int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
                 int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count);

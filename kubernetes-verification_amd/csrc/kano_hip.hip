@@ -124,7 +124,10 @@ struct kano_ctx {
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
-  int rows_store = 0;        // k_rows store order (experiments)
+  int rows_store = 2;        // k_rows stores: 2 non-temporal (measured C3: 253 vs 263-270 us
+                             // for plain stores on one box, 232 vs 246-258 on another);
+                             // 0 plain, 1 word-major, 3 sc1 (no gain) are experiments
+  int rows_persist = 0;      // k_rows persistent grid: blocks per CU (0: one block per item)
   // kano_verify: policy_shadow's subset tests on stream2 beside the Mc
   // chain (set by verify_front around the build; called once the lists and
   // AC exist), joined through ev_join2 before the shadow scans
@@ -137,6 +140,8 @@ struct kano_ctx {
                              // 0.209-0.213 ms beside a normal-priority tail, 0.233-0.239
                              // beside a high-priority one; step 0.556 vs 0.582 ms)
   int side_tail = 1;         // kano_verify's tail on stream3 beside k_rows (else after it)
+  int s3_cus = 0;            // stream3 restricted to this many CUs (0: all), so that the
+                             // tail's short kernels take few CUs from k_rows
   std::function<int()> fork_hook;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   bool fork_pending = false;
@@ -1078,7 +1083,17 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
   int nt = ctx->rows_nt;
   if (nt == 0) nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   KCHK(hipEventRecord(ctx->ev[7], rs));
-  const dim3 grid((unsigned)ctx->wi_total, ncc);
+  dim3 grid((unsigned)ctx->wi_total, ncc);
+  a.nitems = 0;
+  if (ctx->rows_persist > 0) {
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    const i64 g = (i64)ncu * ctx->rows_persist;
+    if (g < ctx->wi_total) {
+      a.nitems = ctx->wi_total;
+      grid.x = (unsigned)g;
+    }
+  }
   const size_t lds = sizeof(u64) * cww;
   if (nt == 1024) hipLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, a);
   else if (nt == 512) hipLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, a);
@@ -1429,7 +1444,7 @@ int kano_create(int device, kano_ctx** out) {
         const std::string k = kv.substr(0, eq);
         const int v = atoi(kv.c_str() + eq + 1);
         if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
-        if (k == "cww" && v >= 256 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
+        if (k == "cww" && v >= 16 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
         if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
         if (k == "alist") ctx->rows_alist = v < 0 ? -1 : (v ? 1 : 0);
         if (k == "nt" && (v == 0 || v == 256 || v == 512 || v == 1024)) ctx->rows_nt = v;
@@ -1449,11 +1464,13 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "packed") ctx->cls_packed = v;
         if (k == "k8srows") ctx->k8s_rows_cls = v;
         if (k == "store") ctx->rows_store = v;
+        if (k == "persist" && v >= 0 && v <= 64) ctx->rows_persist = v;
         if (k == "hosttime") ctx->host_timing = v;
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
+        if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
         if (k == "pathtm" && (v == 1 || v == 2 || v == 4)) ctx->path_tm = v;
@@ -1479,9 +1496,20 @@ int kano_create(int device, kano_ctx** out) {
   {
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-    const hipError_t e3 =
-        ctx->s3_prio ? hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, hi)
-                     : hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking);
+    hipError_t e3;
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    if (ctx->s3_cus > 0 && ctx->s3_cus < ncu) {
+      // every (ncu / s3_cus)-th CU: the tail spread thinly over the chip
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      const int stride = std::max(1, ncu / ctx->s3_cus);
+      for (int c = 0, k = 0; c < ncu && k < ctx->s3_cus; c += stride, ++k)
+        mask[(size_t)c / 32] |= 1u << (c % 32);
+      e3 = hipExtStreamCreateWithCUMask(&ctx->stream3, (uint32_t)mask.size(), mask.data());
+    } else {
+      e3 = ctx->s3_prio ? hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, hi)
+                        : hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking);
+    }
     if (e3 != hipSuccess) {
       ctx->stream3 = nullptr;
       kano_destroy(ctx);
@@ -1991,6 +2019,31 @@ int kano_get_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* dst) {
                         sizeof(u64) * ctx->ldM, sizeof(u64) * ctx->W, (size_t)nrows,
                         hipMemcpyDeviceToHost, ctx->stream));
   return sync(ctx);
+}
+
+int kano_rows_digest(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* out) {
+  KTRY(ensure_matrix(ctx));
+  if (nrows < 0 || r0 < ctx->r0 || r0 + nrows > ctx->r1 || (!out && nrows > 0))
+    return fail(ctx, -EINVAL, "kano_rows_digest: rows outside this shard");
+  if (nrows == 0) return 0;
+  DBuf d;
+  KTRY(dalloc(ctx, d, sizeof(u64) * (size_t)nrows));
+  int rc = 0;
+  for (i64 q = 0; q < nrows && rc == 0; q += 1 << 30) {   // grid.x limit
+    const i64 cnt = std::min<i64>(nrows - q, 1 << 30);
+    hipLaunchKernelGGL(k_row_digest, dim3((unsigned)cnt), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->M) + (r0 - ctx->r0 + q) * ctx->ldM, ctx->ldM, ctx->W,
+                       P_<u64>(d) + q);
+    if (hipGetLastError() != hipSuccess) rc = fail(ctx, -EIO, "kano_rows_digest: launch");
+  }
+  if (rc == 0 &&
+      hipMemcpyAsync(out, d.p, sizeof(u64) * nrows, hipMemcpyDeviceToHost, ctx->stream) !=
+          hipSuccess)
+    rc = fail(ctx, -EIO, "kano_rows_digest: copy");
+  if (rc == 0) rc = sync(ctx);
+  else (void)sync(ctx);
+  dfree(d);
+  return rc;
 }
 
 int kano_put_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, const uint64_t* src) {
@@ -2555,8 +2608,14 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   i64 total = 0;
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
-    KTRY(shadow_back(ctx, v[0], total, cs));
-    ctx->shadow_total = total;
+    if (shadow_cap >= 0) {
+      KTRY(shadow_back(ctx, v[0], total, cs));
+      ctx->shadow_total = total;
+    } else {
+      // count only: every subset test ran (the flags and the per-pod counts
+      // above); the pairs are neither compacted nor emitted (C4: ~1e11)
+      ctx->shadow_total = -1;
+    }
     *shadow_count = total;
   }
   if (nidx > 0)

@@ -1538,7 +1538,8 @@ struct RowsArgs {
   int ch;
   int cww;
   int probe;             // experiments: 1 skip the row build, 2 skip the stores
-  int store_mode;        // experiments: 0 row-major stores, 1 word-major, 2 nontemporal
+  int store_mode;        // experiments: 0 row-major stores, 1 word-major, 2 nontemporal, 3 sc1
+  i64 nitems;            // 0: one work item per block; else the grid strides over nitems
   u64* color;
   u64* colnand;
 };
@@ -1548,11 +1549,17 @@ constexpr int ROWS_UNROLL = 4;
 // that the static LDS does not cost the wide (NT = 1024, 64 KB row) blocks
 // their second slot per CU
 constexpr int ROWS_SEG = 256;
+// 16-byte store that drops the line from the XCD's L2 (sc1: write-through
+// to memory, MI355X_MICROARCH.md "stores of each flavour"); a vector store
+__device__ __forceinline__ void store16_sc1(u64* dst, u64x2 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(v) : "memory");
+}
+
+// one work item (class c, <= ch member rows, column chunk blockIdx.y) of
+// k_rows; b = work item index.  Returns uniformly for the whole block.
 template <int NT>
-__global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) u64 row[];
+__device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   constexpr int NW = NT / 64;
-  const i64 b = blockIdx.x;
   const i64 c = a.wicls ? (i64)a.wicls[b] : upper_bound_i32(a.wioff, a.U + 1, b) - 1;
   if (c < 0 || c >= a.U) return;
   const i64 chunk = b - a.wioff[c];
@@ -1669,6 +1676,9 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
       if (a.store_mode == 2) {
         for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
           __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
+      } else if (a.store_mode == 3) {
+        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+          store16_sc1(&dst[w], *(const u64x2*)&row[w]);
       } else {
         for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
           *(u64x2*)&dst[w] = *(const u64x2*)&row[w];
@@ -1686,6 +1696,52 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
       const u64 nv = ~v & vm;
       if (nv & ~a.colnand[gw]) atomicOr(&a.colnand[gw], nv);
     }
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u64 row[];
+  if (a.nitems == 0) {            // one work item per block
+    rows_item<NT>(a, blockIdx.x, row);
+    return;
+  }
+  // persistent form: the grid strides over the work items; the LDS row is
+  // reused, so every item ends in a barrier (every thread reaches it: the
+  // loop bound is uniform)
+  for (i64 b = blockIdx.x; b < a.nitems; b += gridDim.x) {
+    rows_item<NT>(a, b, row);
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// Row digests (full-size property checks: a 1M-pod matrix is 125 GB, too big
+// to bring to the host).  digest(row) = sum over k < W of
+// mix64(row[k] ^ k * 0xD6E8FEB86659FD93) mod 2^64, mix64 = splitmix64's
+// finaliser; tests/_golden.py row_digest is the same on the host.
+// ===========================================================================
+__device__ __forceinline__ u64 mix64(u64 z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// one block per row
+__global__ __launch_bounds__(TPB) void k_row_digest(const u64* __restrict__ M, i64 ldM, i64 W,
+                                                    u64* __restrict__ out) {
+  const u64* r = M + (i64)blockIdx.x * ldM;
+  u64 h = 0;
+  for (i64 k = threadIdx.x; k < W; k += TPB) h += mix64(r[k] ^ ((u64)k * 0xD6E8FEB86659FD93ull));
+  __shared__ u64 part[TPB / 64];
+  h = wave_sum(h);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 t = 0;
+    for (int w = 0; w < TPB / 64; ++w) t += part[w];
+    out[blockIdx.x] = t;
   }
 }
 

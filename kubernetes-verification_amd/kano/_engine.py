@@ -261,6 +261,14 @@ class DeviceBuild:
                   "kano_get_rows")
         return out
 
+    def rows_digest(self, r0: int, nrows: int) -> np.ndarray:
+        """kano_rows_digest: one 64-bit digest per row (tests/_golden.py
+        row_digest computes the same on the host)."""
+        out = np.zeros(max(nrows, 1), dtype=np.uint64)
+        self._chk(self.lib.kano_rows_digest(self.ctx, int(r0), int(nrows), _ptr(out)),
+                  "kano_rows_digest")
+        return out[:nrows]
+
     def put_rows(self, r0: int, words: np.ndarray) -> None:
         words = np.ascontiguousarray(words, dtype=np.uint64).reshape(-1, self.W)
         self._chk(self.lib.kano_put_rows(self.ctx, int(r0), words.shape[0], _ptr(words)),
@@ -339,7 +347,8 @@ class DeviceBuild:
 
     def verify(self, gid=None, sys_row: int = 0, shadow: bool = True,
                pairs: Optional[np.ndarray] = None, idx: Optional[np.ndarray] = None,
-               ngroups: int = 0, path: Optional[str] = None) -> dict:
+               ngroups: int = 0, path: Optional[str] = None,
+               shadow_count_only: bool = False) -> dict:
         """kano_verify: build + every check in one call (three host syncs).
 
         Returns the reference's result lists as int32 index arrays
@@ -348,7 +357,9 @@ class DeviceBuild:
         and, with ``shadow``, ``shadow_count`` plus ``pairs`` (a (count, 2)
         view of the given buffer when it is large enough, else fetched
         afterwards).  ``idx`` (>= 4*n int32, e.g. pinned) receives the lists.
-        ``ngroups`` > 0 declares ``gid < ngroups`` (checked on the device)."""
+        ``ngroups`` > 0 declares ``gid < ngroups`` (checked on the device).
+        ``shadow_count_only``: policy_shadow's subset tests run and its pair
+        count is returned, the pairs are not emitted (``pairs`` is None)."""
         n = self.n
         if idx is None:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
@@ -369,6 +380,8 @@ class DeviceBuild:
             self._cnt_ref = byref(self._cnt)
         counts, cnt = self._counts, self._cnt
         cap = 0 if pairs is None else pairs.size // 2
+        if shadow_count_only:
+            cap = -1
         pth = nat.PATHS[path or self.path]
         rc = self.lib.kano_verify(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), _ptr(idx),
                                   counts.ctypes.data, _ptr(pairs), int(cap),
@@ -386,7 +399,9 @@ class DeviceBuild:
         if shadow:
             k = int(cnt.value)
             out["shadow_count"] = k
-            if pairs is not None and k <= cap:
+            if shadow_count_only:
+                out["pairs"] = None
+            elif pairs is not None and k <= cap:
                 out["pairs"] = pairs.reshape(-1)[:2 * k].reshape(k, 2)
             else:
                 out["pairs"] = self.shadow_fetch(k)

@@ -458,3 +458,62 @@ def kubesv_edge_py(pods, policies, namespaces, check_self_ingress_traffic=True,
             for dst in egress[s]:
                 edge.add((src, dst))
     return edge, ingress, egress
+
+
+# ---------------------------------------------------------------------------
+# policy_shadow's pair count where the list itself is out of reach
+def shadow_count_grouped(obj: dict) -> int:
+    """len(policy_shadow(m, policies, containers)) (kano_py/kano/
+    algorithm.py:58-80) without materialising the pairs: the reference
+    appends (j, k) for every pod i and every ordered pair j != k of
+    containers[i].select_policies with allow_k a subset of allow_j.  The
+    count is restated as
+
+        sum over row classes c of  m_c * sum_{j != k in S(c)} [allow_k <= allow_j]
+
+    where a row class is the set of pods with equal values on every key a
+    working selector names (the predicate of model.py:95-111 and the
+    presence AND of :142-147 read nothing else, so S is constant on it) and
+    policies with equal allow sets share one subset test.  Interning is the
+    oracle's own (intern_json); allow sets come from the predicate of
+    model.py:104-111 / :145-147 evaluated on the pod value table.  Pinned
+    against kano_py's own counts (tests/test_oracle_golden.py); used for C4,
+    whose ~1e11 pairs no list holds."""
+    n, K, lo, lk, lv, P, (so, sk, sv), (ao, ak, av) = intern_json(obj)
+    V = np.full((max(K, 1), n), -1, np.int32)
+    V[lk, np.repeat(np.arange(n), np.diff(lo))] = lv
+    W = (n + 63) // 64
+    A = np.zeros((P, W), np.uint64)
+    for p in range(P):
+        m = np.ones(n, bool)
+        for t in range(ao[p], ao[p + 1]):
+            if ak[t] >= 0:                       # unknown keys are ignored (Q1)
+                m &= V[ak[t]] == av[t]
+        buf = np.zeros(W * 64, np.uint8)
+        buf[:n] = m
+        A[p] = np.packbits(buf, bitorder="little").view("<u8")
+    R, g_of = np.unique(A, axis=0, return_inverse=True)
+    g_of = g_of.reshape(-1)
+    G = R.shape[0]
+    sub = np.full((G, G), -1, np.int8)          # sub[a, b] = R[b] <= R[a], filled lazily
+    keys = np.unique(sk[sk >= 0])
+    if keys.size:
+        _, rep, m_c = np.unique(V[keys].T, axis=0, return_index=True, return_counts=True)
+    else:
+        rep, m_c = np.array([0] if n else [], np.int64), np.array([n] if n else [], np.int64)
+    total = 0
+    for i, mc in zip(rep.tolist(), m_c.tolist()):
+        ok = (sk < 0) | (V[np.maximum(sk, 0), i] == sv)
+        cs = np.concatenate([[0], np.cumsum(~ok)])
+        S = np.flatnonzero(cs[so[1:]] - cs[so[:-1]] == 0)
+        if S.size < 2:
+            continue
+        gs, cnt = np.unique(g_of[S], return_counts=True)
+        blk = sub[np.ix_(gs, gs)]
+        for ai in np.flatnonzero((blk < 0).any(axis=1)):
+            a = gs[ai]
+            sub[a, gs] = ~np.any(R[gs] & ~R[a], axis=1)
+        blk = sub[np.ix_(gs, gs)].astype(np.int64)
+        cnt = cnt.astype(np.int64)
+        total += mc * (int(cnt @ blk @ cnt) - int(S.size))
+    return int(total)

@@ -22,11 +22,10 @@ for r in csv.DictReader(open(f)):
     if pat.search(r["Name"]):
         out.append(f"{r['Name'].split('(')[0][-40:]} {float(r['AverageNs'])/1000:.1f}us")
     tot += float(r["TotalDurationNs"])
-line = open("gpurun_out/kab.log").read().strip().splitlines()[-1]
-try:
-    ms = json.loads(line)["step_ms"]["median"]
-except Exception:
-    ms = None
+ms = None
+for line in open("gpurun_out/kab.log").read().splitlines():
+    if line.startswith('{"metric"'):
+        ms = json.loads(line)["step_ms"]["median"]
 print(os.environ["T"], "|", "; ".join(out), "| busy/step", round(tot / 12 / 1000, 1), "us | step", ms)
 EOF
 done

@@ -82,6 +82,20 @@ QUIRKS = {
                      pol("y_to_z", {"r": "y"}, {"r": "z"}, "egress"),
                      pol("z_to_x", {"r": "z"}, {"r": "x"}, "ingress")],
     },
+    # one light row class selected by more policies than k_rows' LDS segment
+    # table holds (ROWS_SEG = 256): 320 policies select the "hot" pods, each
+    # allowing one pod (duplicates every 300 -> shadow pairs), so the class
+    # stays light (its rebuild scatters 320 entries) and takes the
+    # non-segmented walk over the flat lists
+    "q_wide_select": {
+        "label": "grp",
+        "pods": [pod("p%d" % i, id="p%d" % i, grp="hot" if i % 120 == 7 else "g%d" % (i % 5),
+                     app="a%d" % (i % 9)) for i in range(1200)],
+        "policies": ([pol("w%d" % k, {"grp": "hot"}, {"id": "p%d" % (k % 300)}, "egress")
+                      for k in range(320)] +
+                     [pol("x%d" % k, {"app": "a%d" % (k % 9)}, {"grp": "g%d" % (k % 5)},
+                          "ingress" if k % 2 else "egress") for k in range(20)]),
+    },
     # every container selected by at most one policy: policy_conflict returns []
     "q_no_conflict": {
         "label": "app",
@@ -125,15 +139,19 @@ def main():
             json.dump(obj, f, separators=(",", ":"))
     print("wrote", len(QUIRKS) + len(SEEDED), "clusters to", OUT)
     if "--big" in sys.argv:
-        # C2 (BASELINE.json configs[1]): regenerated from its seed by the tests
+        # C2/C3/C4 (BASELINE.json configs[1..3]): regenerated from their seeds
+        # by the tests; only kano_py's outputs on them are committed
         from kano.synth import make_config
-        cl = make_config("C2")
-        obj = cl.to_json_obj()
-        obj["label"] = "tenant"
-        obj["seed"] = dict(n=cl.n, P=cl.P, mode=cl.mode, seed=cl.seed, fingerprint=cl.fingerprint())
-        with open("/tmp/kano_golden_C2.json", "w") as f:
-            json.dump(obj, f, separators=(",", ":"))
-        print("wrote /tmp/kano_golden_C2.json")
+        names = [a for a in sys.argv[1:] if not a.startswith("--")] or ["C2"]
+        for name in names:
+            cl = make_config(name)
+            obj = cl.to_json_obj()
+            obj["label"] = "tenant"
+            obj["seed"] = dict(n=cl.n, P=cl.P, mode=cl.mode, seed=cl.seed,
+                               fingerprint=cl.fingerprint())
+            with open(f"/tmp/kano_golden_{name}.json", "w") as f:
+                json.dump(obj, f, separators=(",", ":"))
+            print(f"wrote /tmp/kano_golden_{name}.json")
 
 
 if __name__ == "__main__":

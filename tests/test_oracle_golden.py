@@ -1,11 +1,16 @@
 """The oracle pinned against kano_py's own outputs (tests/golden/expected,
 produced by running the reference, tests/golden/make_golden.py).  CPU only."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
-from _golden import (cluster, cluster_names, csr_sha, expected, lists_to_csr, rows01_to_words,
-                     sha, words_to_rows01)
+from _golden import (GOLDEN, cluster, cluster_names, csr_sha, expected, lists_to_csr,
+                     rows01_to_words, sha, words_to_rows01)
 from oracle import kano_oracle as orc
+
+sys.path.insert(0, GOLDEN)
 
 
 def paper_json():
@@ -53,8 +58,9 @@ def test_cluster_c_oracle(name):
     check_record(res, exp)
 
 
-@pytest.mark.parametrize("name", [n for n in cluster_names() if n.startswith("q_")] +
-                         ["s_sparse_50"])
+@pytest.mark.parametrize("name", [n for n in cluster_names()
+                                  if n.startswith("q_") and n != "q_wide_select"] +
+                         ["s_sparse_50"])   # (pure Python: the small full-matrix records)
 def test_cluster_py_oracle(name):
     from kano.synth import objects_from_json
     from kano import model
@@ -107,3 +113,81 @@ def test_c2_c_oracle():
     obj = cl.to_json_obj()
     res = orc.run_c(obj, label="tenant")
     check_record(res, exp)
+
+
+# --- policy_shadow's count without the list (C4) ----------------------------
+def _count_cases():
+    out = [n for n in cluster_names()] + ["C2"]
+    out += sorted(f[:-5] for f in os.listdir(os.path.join(GOLDEN, "expected"))
+                  if f.startswith("gen_") and expected(f[:-5])["n"] <= 10000)
+    return out
+
+
+def _obj(name):
+    if name.startswith("gen_"):
+        from refgen import cluster_json
+        e = expected(name)
+        g = e["generator"]
+        return cluster_json(g["seed"], g["podN"], g["policyN"], e["walk_order"])
+    if name in ("C2", "C3", "C4"):
+        from kano.synth import make_config
+        return make_config(name).to_json_obj()
+    return cluster(name)
+
+
+@pytest.mark.parametrize("name", _count_cases())
+def test_shadow_count_grouped_vs_kano_py(name):
+    """The grouped count restatement equals len(policy_shadow(...)) as
+    kano_py computed it (algorithm.py:58-80)."""
+    assert orc.shadow_count_grouped(_obj(name)) == expected(name)["policy_shadow"]["count"]
+
+
+def test_big_config_counts_agree():
+    """C3: kano_py's count and the oracle's agree; C4's count is the
+    oracle's (make_golden.py --big + oracle_counts.py)."""
+    for name in ("C3", "C4"):
+        if not os.path.exists(os.path.join(GOLDEN, "expected", name + ".json")):
+            pytest.fail(f"{name} golden missing (tests/golden/make_golden.py --big {name})")
+        sh = expected(name)["policy_shadow"]
+        assert "oracle_count" in sh
+        if "count" in sh:
+            assert sh["count"] == sh["oracle_count"]
+
+
+# --- the reference generator (kano_py/tests/generate.py) --------------------
+GEN = sorted(f[:-5] for f in os.listdir(os.path.join(GOLDEN, "expected"))
+             if f.startswith("gen_"))
+
+
+@pytest.mark.parametrize("name", GEN)
+def test_refgen_reproduces_reference_generator(name):
+    """The seeded restatement writes the same pods and YAML text as the
+    reference's ConfigFiles after random.seed (digest recorded by
+    make_golden.py --gen, which compared them file by file)."""
+    from refgen import RefGen
+    e = expected(name)
+    g = e["generator"]
+    rg = RefGen(g["seed"], podN=g["podN"], policyN=g["policyN"])
+    assert rg.digest() == g["digest"]
+    assert sorted(e["walk_order"]) == sorted(f for f, _ in rg.files)
+
+
+@pytest.mark.parametrize("name", [n for n in GEN if expected(n)["n"] <= 1000])
+def test_refgen_parsed_by_drop_in_parser(name, tmp_path):
+    """The drop-in ConfigParser reads the generated files as kano_py's
+    ConfigParser did (same select / allow dicts and directions, walk order
+    replayed), and the C oracle on them reproduces kano_py's record."""
+    from refgen import RefGen, cluster_json
+    from kano.parser import ConfigParser
+    e = expected(name)
+    g = e["generator"]
+    RefGen(g["seed"], podN=g["podN"], policyN=g["policyN"]).write(str(tmp_path))
+    cp = ConfigParser()
+    for f in e["walk_order"]:
+        cp.parse(str(tmp_path / f))
+    obj = cluster_json(g["seed"], g["podN"], g["policyN"], e["walk_order"])
+    got = [(p.selector.labels, p.allow.labels, "ingress" if p.is_ingress() else "egress")
+           for p in cp.policies]
+    assert got == [(q["select"], q["allow"], q["direction"]) for q in obj["policies"]]
+    res = orc.run_c(obj, label="User")
+    check_record(res, e)
