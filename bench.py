@@ -59,8 +59,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--path", default="auto", choices=["auto", "bitwise", "mfma"])
-    ap.add_argument("--no-shadow", action="store_true",
-                    help="skip policy_shadow (its output is ~1e11 pairs on C4)")
+    ap.add_argument("--shadow", default="auto", choices=["auto", "pairs", "count", "off"],
+                    help="policy_shadow: the pairs to the host (C2/C3/C5), the count only "
+                         "(every subset test, no emission: C4's ~1e11 pairs), or off; "
+                         "auto = count for C4, pairs otherwise")
+    ap.add_argument("--no-shadow", action="store_true", help="same as --shadow off")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU sample")
     ap.add_argument("--shard-path", action="store_true",
@@ -79,7 +82,8 @@ class Step:
                  stream=None, emulate=0):
         self.eng, self.gid, self.n = eng, gid, n
         self.rank, self.world, self.r0, self.r1 = rank, world, r0, r1
-        self.shadow = shadow
+        self.shadow = shadow != "off"
+        self.count_only = shadow == "count"
         self.dist, self.torch, self.stream = dist, torch, stream
         self.W = (n + 63) >> 6
         self.emulate = emulate
@@ -106,7 +110,7 @@ class Step:
         eng, n = self.eng, self.n
         res = {}
         pairs = None
-        if self.shadow:
+        if self.shadow and not self.count_only:
             if self.pin is None:
                 self.pin_pairs = 1 << 20
                 self.pin = self.PinnedBuffer(self.pin_pairs * 8)
@@ -119,7 +123,8 @@ class Step:
         if not self.shard_path:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
-            r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=idx)
+            r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=idx,
+                           shadow_count_only=self.count_only)
         else:
             # this rank's rows and checks up to its column words, one RCCL
             # all-gather of 3*W words per rank over xGMI (on the engine's
@@ -132,7 +137,7 @@ class Step:
                 else:
                     self.dist.all_gather_into_tensor(self.gathered, self.words)
                 r = eng.verify_combine(self.gathered.data_ptr(), self.nranks, pairs=pairs,
-                                       idx=idx)
+                                       idx=idx, shadow_count_only=self.count_only)
         for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
             if r[k] is not None:
                 res[k] = r[k]
@@ -140,7 +145,7 @@ class Step:
             cnt = r["shadow_count"]
             res["policy_shadow"] = r["pairs"]
             res["policy_shadow_count"] = cnt
-            if cnt > self.pin_pairs:          # grow for the next step
+            if not self.count_only and cnt > self.pin_pairs:   # grow for the next step
                 self.pin.close()
                 self.pin_pairs = 2 * cnt
                 self.pin = self.PinnedBuffer(self.pin_pairs * 8)
@@ -149,7 +154,6 @@ class Step:
         st = eng.stage_times()
         self.host_stage_s += time.perf_counter() - t1
         self.k_rows_ms.append(st["k_rows"])
-        self.stages = st
         self.results = res
         return res
 
@@ -249,6 +253,9 @@ def main():
     from kano._intern import tables_from_cluster
     from kano.synth import make_config, KEY_NAMES
 
+    shadow = "off" if args.no_shadow else args.shadow
+    if shadow == "auto":
+        shadow = "count" if args.config == "C4" else "pairs"
     cl = make_config(args.config)
     tables = tables_from_cluster(cl)
     n = cl.n
@@ -257,11 +264,19 @@ def main():
     if args.rank_of > 1:
         r0, r1 = 0, n // args.rank_of
     stream = torch.cuda.Stream() if dist is not None or args.rank_of > 1 else None
-    eng = DeviceBuild(tables, device=torch.cuda.current_device(), rows=(r0, r1), path=args.path,
-                      build=False,
+    eng = DeviceBuild(None, device=torch.cuda.current_device(), path=args.path,
                       stream=stream.cuda_stream if stream is not None else None)
-    step = Step(eng, gid, n, rank, world, r0, r1, shadow=not args.no_shadow, dist=dist,
+    # host -> device upload of the resident inputs (label tables, policy
+    # terms, the tenant groups): reported apart from the step
+    torch.cuda.synchronize()
+    t_up = time.perf_counter()
+    eng.upload(tables)
+    eng.set_rows(r0, r1)
+    up_tables_ms = (time.perf_counter() - t_up) * 1e3
+    t_up = time.perf_counter()
+    step = Step(eng, gid, n, rank, world, r0, r1, shadow=shadow, dist=dist,
                 torch=torch, stream=stream, emulate=args.rank_of if args.rank_of > 1 else 0)
+    up_groups_ms = (time.perf_counter() - t_up) * 1e3
 
     def barrier():
         torch.cuda.synchronize()
@@ -302,6 +317,17 @@ def main():
         shadow_cnt = int(t.item())
     out = None
     traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
+    # the last step's results against kano_py's own outputs on this cluster
+    # (tests/golden/expected/<config>.json); on row shards rank 0 checks the
+    # combined column lists and the system row it owns
+    verified, vdetail = verify_against_golden(args.config, cl, step.results, world, rank,
+                                             args.rank_of, shadow)
+    if dist is not None:
+        t = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if int(t.item()) == 0 and verified is not False:
+            verified, vdetail = False, "another rank's results differ from the golden"
+    box_fill = box_store_rate(torch, eng.W * 8 * max(r1 - r0, 1)) if world == 1 else None
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "pod-pairs/s", "n_gpus": world,
@@ -316,13 +342,19 @@ def main():
                        "path": args.path,
                        "checks": "all_reachable, all_isolated, user_crosscheck(tenant), "
                                  "system_isolation(0)" +
-                                 ("" if args.no_shadow else ", policy_shadow")},
+                                 {"pairs": ", policy_shadow (pairs to the host)",
+                                  "count": ", policy_shadow (every subset test; pair count "
+                                           "only)",
+                                  "off": ""}[shadow]},
+            "verified": verified, "verified_against": vdetail,
+            "upload_ms": {"tables": round(up_tables_ms, 3), "groups": round(up_groups_ms, 3),
+                          "note": "host -> device input upload, once, outside the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rows", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes,
-                         "avg_launch_ms": k_rows_ms},
-            "stages_ms_last_step": {k: round(v, 4) for k, v in step.stages.items()},
+                         "avg_launch_ms": k_rows_ms,
+                         "box_fill_gbs": box_fill},
             "host_stage_times_ms_per_step": round(step.host_stage_s / args.steps * 1e3, 4),
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),
@@ -334,9 +366,12 @@ def main():
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},
         }
+        ref = kano_py_measured(args.config)
+        if ref:
+            out["kano_py_measured"] = ref
         if args.cpu_baseline and world == 1:
             sum_s2 = 0
-            if not args.no_shadow:
+            if shadow != "off":
                 off, _ = eng.select_csr()
                 cls = eng.classes()
                 s = np.diff(off)[cls].astype(np.int64)
@@ -348,6 +383,101 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if verified is False:
+        sys.exit(f"bench: results differ from the golden: {vdetail}")
+
+
+def _golden(config):
+    path = os.path.join(ROOT, "tests", "golden", "expected", f"{config}.json")
+    try:
+        with open(path) as f:
+            return json.load(f), os.path.relpath(path, ROOT)
+    except OSError:
+        return None, None
+
+
+def _list_ok(got, exp):
+    import hashlib
+    got = np.ascontiguousarray(np.asarray(got, dtype=np.int32))
+    if isinstance(exp, dict):
+        return (got.shape[0] == exp["count"] and
+                hashlib.sha256(got.tobytes()).hexdigest() == exp["sha256"])
+    return got.tolist() == exp
+
+
+def verify_against_golden(config, cl, res, world, rank, rank_of, shadow):
+    """True / False against kano_py's record of this exact cluster; None
+    when no such record exists (C5: out of kano_py's reach; its full-size
+    properties are tests/test_configs.py::test_c5_full_size_properties) or
+    the run is an emulated diagnostic."""
+    import hashlib
+    exp, src = _golden(config)
+    if exp is None:
+        return None, "no kano_py record for this config (C5: see tests/test_configs.py)"
+    if rank_of > 1:
+        return None, "emulated shard step (other ranks' words are zero): not checked"
+    if exp.get("seed", {}).get("fingerprint") != cl.fingerprint():
+        return False, f"{src}: cluster fingerprint differs"
+    bad = []
+    for k in ("all_reachable", "all_isolated"):
+        if not _list_ok(res[k], exp[k]):
+            bad.append(k)
+    if not _list_ok(res["user_crosscheck"], exp["user_crosscheck"]["result"]):
+        bad.append("user_crosscheck")
+    if "system_isolation" in res and not _list_ok(res["system_isolation"],
+                                                  exp["system_isolation"]["result"]):
+        bad.append("system_isolation")
+    sh = exp["policy_shadow"]
+    if shadow == "pairs" and world == 1:
+        if res["policy_shadow_count"] != sh["count"] or hashlib.sha256(
+                np.ascontiguousarray(res["policy_shadow"], dtype=np.int32).tobytes()
+        ).hexdigest() != sh["sha256"]:
+            bad.append("policy_shadow")
+    elif shadow != "off" and world == 1:
+        want = sh.get("count", sh.get("oracle_count"))
+        if res["policy_shadow_count"] != want:
+            bad.append("policy_shadow count")
+    if bad:
+        return False, f"{src}: {', '.join(bad)} differ"
+    what = "lists" + (", policy_shadow " + ("pairs sha256" if shadow == "pairs" else "count")
+                      if shadow != "off" and world == 1 else "")
+    return True, f"{src} (kano_py on the same seeded cluster): {what} equal"
+
+
+def kano_py_measured(config):
+    """kano_py's own times on this cluster, measured in the build container
+    by tests/golden/make_golden.py (single thread, bitarray 2.3.0)."""
+    exp, src = _golden(config)
+    if exp is None or "reference_seconds" not in exp:
+        return None
+    t = exp["reference_seconds"]
+    total = float(sum(t.values()))
+    n = exp["n"]
+    return {"seconds": {k: round(v, 2) for k, v in t.items()}, "total_s": round(total, 1),
+            "pod_pairs_per_s": n * n / total, "cores": 1,
+            "where": "build container (Intel Xeon, py3.9, bitarray 2.3.0), not the GPU box",
+            "complete": "policy_shadow" in t, "source": src}
+
+
+def box_store_rate(torch, nbytes):
+    """This box's plain device fill rate on a buffer of the matrix's size
+    (torch fill_, HIP events): context for the k_rows roofline fraction,
+    boxes differ by up to 20 %."""
+    try:
+        buf = torch.empty(int(nbytes) // 8, dtype=torch.int64, device="cuda")
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        buf.fill_(1)
+        ms = []
+        for _ in range(5):
+            ev[0].record()
+            buf.fill_(0)
+            ev[1].record()
+            torch.cuda.synchronize()
+            ms.append(ev[0].elapsed_time(ev[1]))
+        del buf
+        return round(nbytes / (min(ms) * 1e-3) / 1e9, 1)
+    except Exception:   # noqa: BLE001 (context only)
+        return None
 
 
 def pmc_traffic(config):

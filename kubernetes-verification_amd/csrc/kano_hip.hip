@@ -1123,6 +1123,10 @@ int join_rows(kano_ctx* ctx) {
 int ensure_matrix(kano_ctx* ctx) {
   KTRY(ensure_built(ctx));
   if (ctx->lists_mode) return fail(ctx, -EINVAL, "context holds policy lists, not a matrix");
+  if (ctx->vs_open)
+    return fail(ctx, -EINVAL,
+                "matrix read between kano_verify_shard and kano_verify_combine (the combine "
+                "writes the shard's rows)");
   if (ctx->rows_deferred) {    // kano_build_classes: the matrix, now
     ctx->rows_deferred = false;
     KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM) *

@@ -429,7 +429,8 @@ class DeviceBuild:
 
     def verify_combine(self, gathered_dev_ptr: int, nranks: int, cross: bool = True,
                        pairs: Optional[np.ndarray] = None,
-                       idx: Optional[np.ndarray] = None) -> dict:
+                       idx: Optional[np.ndarray] = None,
+                       shadow_count_only: bool = False) -> dict:
         """kano_verify_combine: OR the gathered word sets of ``nranks`` shards
         and return the results like ``verify`` (column lists global, the
         system row and the shadow pairs of this shard)."""
@@ -442,6 +443,8 @@ class DeviceBuild:
         cnt = c_int64(0)
         shadow = self._shard_shadow
         cap = 0 if pairs is None else pairs.size // 2
+        if shadow_count_only:
+            cap = -1
         self._chk(self.lib.kano_verify_combine(self.ctx, c_void_p(gathered_dev_ptr), int(nranks),
                                                _ptr(idx), _ptr(counts), _ptr(pairs), int(cap),
                                                byref(cnt) if shadow else None),
@@ -457,7 +460,9 @@ class DeviceBuild:
         if shadow:
             k = int(cnt.value)
             out["shadow_count"] = k
-            if pairs is not None and k <= cap:
+            if shadow_count_only:
+                out["pairs"] = None
+            elif pairs is not None and k <= cap:
                 out["pairs"] = pairs.reshape(-1)[:2 * k].reshape(k, 2)
             else:
                 out["pairs"] = self.shadow_fetch(k)
