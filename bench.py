@@ -90,10 +90,11 @@ class Step:
         self.nranks = emulate or world
         self.shard_path = self.nranks > 1 or dist is not None
         if self.shard_path:
-            # [OR | cross | NAND] words of this rank's rows, and all ranks'
-            self.words = torch.zeros(3 * self.W, dtype=torch.int64, device="cuda")
-            self.gathered = torch.zeros(self.nranks * 3 * self.W, dtype=torch.int64,
-                                        device="cuda")
+            # [OR | cross | NAND] words of this rank's rows, all ranks'
+            # gathered, the combine (kano/shard.py)
+            from kano.shard import ShardExchange
+            self.xchg = ShardExchange(torch, self.W, self.nranks,
+                                      dist=None if emulate else dist, stream=stream)
         from kano._engine import PinnedBuffer
         self.pin = None
         self.pin_idx = None
@@ -129,15 +130,8 @@ class Step:
             # this rank's rows and checks up to its column words, one RCCL
             # all-gather of 3*W words per rank over xGMI (on the engine's
             # stream), then the OR-combine and the lists on the device
-            with self.torch.cuda.stream(self.stream):
-                eng.verify_shard(self.words.data_ptr(), gid="stored", sys_row=0,
-                                 shadow=self.shadow)
-                if self.emulate:
-                    self.gathered[:3 * self.W].copy_(self.words)
-                else:
-                    self.dist.all_gather_into_tensor(self.gathered, self.words)
-                r = eng.verify_combine(self.gathered.data_ptr(), self.nranks, pairs=pairs,
-                                       idx=idx, shadow_count_only=self.count_only)
+            r = self.xchg.verify(eng, gid="stored", sys_row=0, shadow=self.shadow,
+                                 count_only=self.count_only, pairs=pairs, idx=idx)
         for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
             if r[k] is not None:
                 res[k] = r[k]
@@ -260,7 +254,8 @@ def main():
     tables = tables_from_cluster(cl)
     n = cl.n
     gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
-    r0, r1 = rank * n // world, (rank + 1) * n // world
+    from kano.shard import row_range
+    r0, r1 = row_range(n, world, rank)
     if args.rank_of > 1:
         r0, r1 = 0, n // args.rank_of
     stream = torch.cuda.Stream() if dist is not None or args.rank_of > 1 else None

@@ -1,77 +1,97 @@
-"""Row partition of the reachability matrix across ranks (one process per
-GPU) and the exchange step of the column checks.
+"""Row-sharded verification across ranks: one process per GPU (SURVEY.md
+§8(e)); what bench.py's N > 1 step runs.
 
 Rows of M (source pods) are independent: M[i] = OR_{p in S(i)} allow_p
-(kano_py/kano/model.py:158-160), so rank r builds rows [row_range(n, W, r)]
-with no communication.  The column checks are existentials / universals over
-rows, so they combine over shards:
+(kano_py/kano/model.py:158-160), so rank r builds rows row_range(n, N, r)
+with no communication (kano_verify_shard).  The column checks are
+existentials / universals over rows and combine over shards:
 
   all_isolated[j]    = NOT OR_r colOR_r[j]          (algorithm.py:12-17)
   all_reachable[j]   = NOT OR_r colNAND_r[j]        (algorithm.py:4-9)
   user_crosscheck[j] = OR_r cross_r[j]              (algorithm.py:27-42)
 
-RCCL has no bitwise reduction.  The bench's step (kano_verify_shard /
-kano_verify_combine) gathers every rank's three bit vectors as words,
-[or | cross | nand] (3 W u64 = n*3/8 bytes per rank), with one all-gather over
-xGMI and ORs them on the device; ``combine_words`` is the host statement of
-that combine.  The older byte form (``pack_flags``: one byte per column, one
-MAX all-reduce, MAX of 0/1 bytes = OR) stays for kano_col_flags_dev.
-system_isolation reads one row from the rank that owns it; policy_shadow's
-output is ordered by container, so each rank emits its own rows' pairs and
-rank order is the global order.
+RCCL has no bitwise reduction, so the one exchange is an all-gather of every
+rank's [OR | cross | NAND] words (3 W u64 = 3n/8 bytes per rank; 37.5 KB at
+100k pods) over xGMI, OR-ed on the device by kano_verify_combine, which also
+lists the results.  system_isolation comes from the rank owning the row;
+policy_shadow's output is ordered by container, so each rank emits its own
+rows' pairs and rank order is the global order.
+
+With the gloo backend (several ranks rehearsing on one device, or CPU-only
+collectives) the words travel through host memory: ``host_staged``.
 """
 from __future__ import annotations
 
-from typing import Dict, Tuple
-
-import numpy as np
+from typing import Optional, Tuple
 
 
 def row_range(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Rows [r0, r1) of rank ``rank`` of ``world`` (contiguous, balanced)."""
     return rank * n // world, (rank + 1) * n // world
 
 
 def owner_of_row(n: int, world: int, i: int) -> int:
-    for r in range(world):
-        a, b = row_range(n, world, r)
-        if a <= i < b:
-            return r
-    raise IndexError(i)
+    """The rank whose row_range holds row i."""
+    if not 0 <= i < n:
+        raise IndexError(i)
+    r = (i * world) // n
+    while row_range(n, world, r)[1] <= i:   # floor rounding: at most one step
+        r += 1
+    while row_range(n, world, r)[0] > i:
+        r -= 1
+    return r
 
 
-def pack_flags(col_or: np.ndarray, cross: np.ndarray, col_nand: np.ndarray, n: int) -> np.ndarray:
-    """Three LSB-first word vectors -> [or | cross | nand] bytes (host side of
-    kano_col_flags_dev / kano_crosscheck_dev)."""
-    out = np.empty(3 * n, np.uint8)
-    for k, w in enumerate((col_or, cross, col_nand)):
-        b = np.unpackbits(np.ascontiguousarray(w, dtype="<u8").view(np.uint8),
-                          bitorder="little")[:n]
-        out[k * n:(k + 1) * n] = b
-    return out
+class ShardExchange:
+    """The N > 1 verification step of one rank: kano_verify_shard, the
+    all-gather of the ranks' column words, kano_verify_combine.
 
+    ``eng`` is the rank's DeviceBuild (rows = row_range(...)), created on
+    ``stream`` (a torch.cuda.Stream) so that the collective is ordered after
+    the shard's kernels on the same stream.  ``dist`` None with ``nranks``
+    > 1 emulates rank 0 of nranks on one device (other ranks' words zero: a
+    timing diagnostic, results are partial)."""
 
-def decode_flags(flags: np.ndarray, n: int) -> Dict[str, np.ndarray]:
-    """Combined [or | cross | nand] bytes -> the three check results."""
-    f = np.asarray(flags)
-    return {
-        "all_isolated": np.flatnonzero(f[:n] == 0),
-        "user_crosscheck": np.flatnonzero(f[n:2 * n]),
-        "all_reachable": np.flatnonzero(f[2 * n:3 * n] == 0),
-    }
+    def __init__(self, torch, W: int, nranks: int, dist=None, stream=None,
+                 host_staged: Optional[bool] = None, device: str = "cuda"):
+        self.torch, self.W, self.nranks, self.dist, self.stream = torch, W, nranks, dist, stream
+        if host_staged is None:
+            host_staged = dist is not None and dist.get_backend() == "gloo"
+        self.host_staged = host_staged
+        self.words = torch.zeros(3 * W, dtype=torch.int64, device=device)
+        self.gathered = torch.zeros(nranks * 3 * W, dtype=torch.int64, device=device)
+        if host_staged:
+            self._hw = torch.zeros(3 * W, dtype=torch.int64)
+            self._hg = torch.zeros(nranks * 3 * W, dtype=torch.int64)
 
+    def gather(self) -> None:
+        """Every rank's words into ``gathered`` (rank order)."""
+        torch, dist = self.torch, self.dist
+        if dist is None:
+            self.gathered[:3 * self.W].copy_(self.words)
+        elif self.host_staged:
+            if self.words.is_cuda:
+                torch.cuda.synchronize()      # the shard's kernels wrote the words
+            self._hw.copy_(self.words)
+            dist.all_gather_into_tensor(self._hg, self._hw)
+            self.gathered.copy_(self._hg)
+            if self.gathered.is_cuda:
+                torch.cuda.synchronize()
+        else:
+            dist.all_gather_into_tensor(self.gathered, self.words)
 
-def combine_words(gathered: np.ndarray, n: int) -> Dict[str, np.ndarray]:
-    """Gathered [rank][or | cross | nand][W] u64 words -> the three check
-    results (host statement of k_combine_cols)."""
-    W = (n + 63) // 64
-    g = np.asarray(gathered, dtype=np.uint64).reshape(-1, 3, W)
-    o, c, na = (np.bitwise_or.reduce(g[:, k, :], axis=0) for k in range(3))
+    def _run(self, eng, gid, sys_row, shadow, count_only, pairs, idx):
+        eng.verify_shard(self.words.data_ptr(), gid=gid, sys_row=sys_row, shadow=shadow)
+        self.gather()
+        return eng.verify_combine(self.gathered.data_ptr(), self.nranks, pairs=pairs, idx=idx,
+                                  shadow_count_only=count_only)
 
-    def bits(w):
-        return np.unpackbits(np.ascontiguousarray(w, dtype="<u8").view(np.uint8),
-                             bitorder="little")[:n].astype(bool)
-    return {
-        "all_isolated": np.flatnonzero(~bits(o)),
-        "user_crosscheck": np.flatnonzero(bits(c)),
-        "all_reachable": np.flatnonzero(~bits(na)),
-    }
+    def verify(self, eng, gid="stored", sys_row: int = 0, shadow: bool = True,
+               count_only: bool = False, pairs=None, idx=None) -> dict:
+        """kano_py's checks for this rank (algorithm.py:4-80): the column
+        lists are global, system_isolation is None unless this rank owns
+        sys_row, the shadow pairs are this rank's rows' part."""
+        if self.stream is None:
+            return self._run(eng, gid, sys_row, shadow, count_only, pairs, idx)
+        with self.torch.cuda.stream(self.stream):
+            return self._run(eng, gid, sys_row, shadow, count_only, pairs, idx)

@@ -1,0 +1,110 @@
+"""The multi-GPU verification step across processes, on the product path:
+every rank builds its row shard (DeviceBuild(rows=row_range(...)),
+kano_verify_shard), the ranks all-gather their column words and
+kano_verify_combine ORs them and lists the results -- kano/shard.py's
+ShardExchange, exactly what bench.py's N > 1 step runs.  2 and 3 ranks share
+cuda:0 over gloo (RCCL refuses two ranks on one device, so the words are
+staged through host memory); results against kano_py's goldens."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from _golden import expected, index_list_matches, sha
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, name, count_only, q):
+    try:
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-verification_amd"), HERE]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch
+        import torch.distributed as dist
+        from kano._engine import DeviceBuild
+        from kano._intern import group_ids, intern, tables_from_cluster
+        from kano.shard import ShardExchange, row_range
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if name.startswith("C"):
+            from kano.synth import KEY_NAMES, make_config
+            cl = make_config(name)
+            t = tables_from_cluster(cl)
+            gid = np.unique(cl.vals[KEY_NAMES.index("tenant")],
+                            return_inverse=True)[1].astype(np.int32)
+        else:
+            from _golden import cluster
+            from kano import model
+            from kano.synth import objects_from_json
+            obj = cluster(name)
+            cs, ps = objects_from_json(obj, model)
+            t = intern(cs, ps)
+            gid = group_ids(cs, obj["label"])
+        n = t.n
+        stream = torch.cuda.Stream()
+        r0, r1 = row_range(n, world, rank)
+        eng = DeviceBuild(t, rows=(r0, r1), build=False, stream=stream.cuda_stream)
+        eng.set_groups(gid)
+        x = ShardExchange(torch, (n + 63) // 64, world, dist=dist, stream=stream)
+        out = []
+        for _ in range(2):    # twice: the step repeats on the same context
+            r = x.verify(eng, gid="stored", sys_row=0, shadow=True, count_only=count_only)
+            out.append({k: (None if v is None else np.array(v, copy=True))
+                        for k, v in r.items() if k != "shadow_count"})
+            out[-1]["shadow_count"] = r["shadow_count"]
+        eng.close()
+        dist.destroy_process_group()
+        q.put((rank, out, None))
+    except Exception as e:   # noqa: BLE001
+        import traceback
+        q.put((rank, None, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("count_only", [False, True])
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", ["s_sparse_2000", "C2", "q_wide_select"])
+def test_shard_exchange_across_processes(name, world, count_only):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, count_only, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [e for _, _, e in res if e]
+    assert not errs, errs[0]
+    exp = expected(name)
+    for step in range(2):
+        pairs, total = [], 0
+        for rank, out, _ in res:
+            r = out[step]
+            assert index_list_matches(r["all_reachable"], exp["all_reachable"])
+            assert index_list_matches(r["all_isolated"], exp["all_isolated"])
+            assert index_list_matches(r["user_crosscheck"], exp["user_crosscheck"]["result"])
+            if rank == 0:     # row 0's owner
+                assert index_list_matches(r["system_isolation"],
+                                          exp["system_isolation"]["result"])
+            else:
+                assert r["system_isolation"] is None
+            total += r["shadow_count"]
+            if not count_only:
+                pairs.append(r["pairs"].reshape(-1, 2))
+        assert total == exp["policy_shadow"]["count"]
+        if not count_only:
+            allp = np.ascontiguousarray(np.concatenate(pairs).astype(np.int32))
+            assert sha(allp) == exp["policy_shadow"]["sha256"]
