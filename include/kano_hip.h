@@ -193,6 +193,17 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
                         int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                         int64_t* shadow_count);
 
+/* The checks of kano_verify_shard over the matrix rows AS THEY STAND --
+ * after kano_add_policies / kano_remove_policies (or edits), which
+ * kano_verify, a rebuild from the tables, would undo: this shard's
+ * [OR | cross | NAND] column words to words_dev (3*W u64), the system row
+ * kept if owned.  Gather the ranks' words and finish with
+ * kano_verify_combine (shadow_count NULL); one rank: nranks = 1 with its own
+ * words.  Column checks of algorithm.py:4-42 and system_isolation (:45-55)
+ * on an incrementally updated, row-sharded matrix. */
+int kano_checks_shard(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                      uint64_t* words_dev);
+
 /* user_hashmap (algorithm.py:20-24) as resident input: the group id of
  * every pod uploaded once (like the label tables), for kano_verify with
  * gid = NULL, ngroups = KANO_STORED_GROUPS.  ngroups <= 0: max(gid) + 1. */

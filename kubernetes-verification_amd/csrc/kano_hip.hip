@@ -2684,6 +2684,62 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
                      shadow_pairs, shadow_cap, shadow_count);
 }
 
+int kano_checks_shard(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                      uint64_t* words_dev) {
+  KTRY(ensure_matrix(ctx));
+  if (!words_dev) return fail(ctx, -EINVAL, "kano_checks_shard: words_dev is NULL");
+  const i64 n = ctx->n, W = ctx->W;
+  const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
+  const bool want_cross = gid || stored;
+  // column OR / NAND of the rows as they stand (after incremental updates
+  // or edits: from M; otherwise the build's own)
+  if (!ctx->cols_valid) KTRY(recompute_cols(ctx));
+  bool cross_on = false;
+  if (want_cross) {
+    KTRY(crosscheck_impl(ctx, stored ? nullptr : gid, stored ? 0 : ngroups));
+    cross_on = n > 0 && rows_local(ctx) > 0 && W > 0;
+  }
+  const i64 nb = std::max<i64>(1, nblk(W * 64));
+  KTRY(dalloc(ctx, ctx->col_and, sizeof(u64) * std::max<i64>(1, W)));
+  KTRY(dalloc(ctx, ctx->sysrow, sizeof(u64) * std::max<i64>(1, W)));
+  KTRY(dalloc(ctx, ctx->icnt, sizeof(i64) * 4 * nb));
+  KTRY(dalloc(ctx, ctx->ioff, sizeof(i64) * 4 * (nb + 1)));
+  KTRY(dalloc(ctx, ctx->idxd, sizeof(int32_t) * std::max<i64>(1, 4 * n) + 16));
+  KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
+  if (W > 0) {
+    KCHK(hipMemcpyAsync(words_dev, ctx->color.p, sizeof(u64) * W, hipMemcpyDeviceToDevice,
+                        ctx->stream));
+    if (cross_on)
+      KCHK(hipMemcpyAsync(words_dev + W, ctx->cross.p, sizeof(u64) * W, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    else
+      KCHK(hipMemsetAsync(words_dev + W, 0, sizeof(u64) * W, ctx->stream));
+    KCHK(hipMemcpyAsync(words_dev + 2 * W, ctx->colnand.p, sizeof(u64) * W,
+                        hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
+  const bool sys_on = have_sys && W > 0;
+  if (sys_on)
+    KCHK(hipMemcpyAsync(ctx->sysrow.p, P_<u64>(ctx->M) + (sys_row - ctx->r0) * ctx->ldM,
+                        sizeof(u64) * W, hipMemcpyDeviceToDevice, ctx->stream));
+  // icnt rows 0-2 come from kano_verify_combine's k_combine_cols, row 3 here
+  hipLaunchKernelGGL(k_row_zero_counts, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream,
+                     sys_on ? P_<u64>(ctx->sysrow) : (const u64*)nullptr, n, W,
+                     P_<i64>(ctx->icnt) + 3 * nb);
+  KLAUNCH();
+  // the combine half is kano_verify_combine's: no rows to write, no shadow
+  ctx->vs_open = true;
+  ctx->vs_shadow = false;
+  ctx->vs_cross_want = want_cross;
+  ctx->vs_cross_on = cross_on;
+  ctx->vs_have_sys = have_sys;
+  ctx->vs_sys_on = sys_on;
+  ctx->vs_early = true;
+  ctx->vs_nb = nb;
+  ctx->vs_rl = rows_local(ctx);
+  return 0;
+}
+
 int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods) return fail(ctx, -EINVAL, "kano_set_groups before kano_set_pods");

@@ -2159,6 +2159,17 @@ __device__ __forceinline__ bool mc_bit(const u64* row, int32_t ca) {
   return (row[ca >> 6] >> (ca & 63)) & 1ull;
 }
 
+// per-block counts of a row's zero bits (system_isolation's list sizes,
+// icnt row 3) from a row of M; all zero when the row is not this shard's
+__global__ __launch_bounds__(TPB) void k_row_zero_counts(const u64* __restrict__ row, i64 n,
+                                                         i64 W, i64* __restrict__ icnt3) {
+  __shared__ i64 sm[4];
+  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;   // grid covers W * 64
+  const bool z = row && j < n && !((row[j >> 6] >> (j & 63)) & 1ull);
+  const i64 c = block_sum((i64)z, sm);
+  if (threadIdx.x == 0) icnt3[blockIdx.x] = c;
+}
+
 __global__ __launch_bounds__(TPB) void k_verify_cols(FinishArgs a) {
   __shared__ i64 sm[4];
   const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;   // grid covers W * 64

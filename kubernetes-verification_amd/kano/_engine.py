@@ -68,6 +68,7 @@ class DeviceBuild:
         self.device = device
         self.path = path
         self._counts = None
+        self.row_span = None          # (r0, r1) when this context holds a row shard
         if stream is not None:
             self._chk(self.lib.kano_set_stream(self.ctx, c_void_p(stream)), "kano_set_stream")
         self.tables = None
@@ -112,6 +113,12 @@ class DeviceBuild:
 
     def set_rows(self, r0: int, r1: int) -> None:
         self._chk(self.lib.kano_set_shard(self.ctx, int(r0), int(r1)), "kano_set_shard")
+        n = self.tables.n if self.tables is not None else None
+        self.row_span = None if (int(r0), int(r1)) == (0, n) else (int(r0), int(r1))
+
+    @property
+    def is_shard(self) -> bool:
+        return self.row_span is not None
 
     def build(self, path: Optional[str] = None) -> None:
         p = nat.PATHS[path or self.path]
@@ -426,6 +433,23 @@ class DeviceBuild:
         self._chk(self.lib.kano_verify_shard(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row),
                                              1 if shadow else 0, c_void_p(words_dev_ptr)),
                   "kano_verify_shard")
+
+    def checks_shard(self, words_dev_ptr: int, gid=None, sys_row: int = 0,
+                     ngroups: int = 0) -> None:
+        """kano_checks_shard: this shard's column words from the matrix as
+        it stands (after add_policies / remove_policies); finish with
+        ``verify_combine``."""
+        self._gid_keep = None
+        if isinstance(gid, str) and gid == "stored":
+            gid, ngroups = None, nat.STORED_GROUPS
+        elif gid is not None:
+            gid = np.ascontiguousarray(gid, dtype=np.int32)
+            if gid.shape[0] != self.n:
+                raise ValueError("gid must have one entry per pod")
+            self._gid_keep = gid
+        self._shard_shadow = False
+        self._chk(self.lib.kano_checks_shard(self.ctx, _ptr(gid), int(ngroups), int(sys_row),
+                                             c_void_p(words_dev_ptr)), "kano_checks_shard")
 
     def verify_combine(self, gathered_dev_ptr: int, nranks: int, cross: bool = True,
                        pairs: Optional[np.ndarray] = None,

@@ -34,6 +34,7 @@ SIGNATURES = {
     "kano_crosscheck_dev": (c_int, [c_void_p, c_void_p, c_void_p]),
     "kano_get_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_rows_digest": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
+    "kano_checks_shard": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p]),
     "kano_put_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_get_col": (c_int, [c_void_p, c_int64, c_void_p]),
     "kano_get_bit": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_int)]),

@@ -17,10 +17,20 @@ from ._bits import bool_to_words, set_bit_indices, words_to_bool
 from ._intern import group_ids
 
 
-def _engine(matrix: ReachabilityMatrix):
+def _engine(matrix: ReachabilityMatrix, whole: bool = True):
+    """The matrix's device context.  A context holding only a row shard
+    (a multi-GPU rank's rows) cannot answer a whole-matrix query on its own:
+    the column checks, getcol and policy_shadow need every row, so they raise
+    instead of returning the shard's part (combine shards with
+    kano.shard.ShardExchange)."""
     eng = getattr(matrix, "_engine", None)
     if eng is None:
         raise TypeError("expected a kano ReachabilityMatrix built by this package")
+    if whole and getattr(eng, "is_shard", False):
+        r0, r1 = eng.row_span
+        raise ValueError(f"matrix holds only rows [{r0}, {r1}) of {matrix.container_size}: "
+                         "whole-matrix checks need every row (combine the row shards "
+                         "with kano.shard.ShardExchange)")
     return eng
 
 
@@ -76,8 +86,9 @@ def user_crosscheck(matrix: ReachabilityMatrix, containers: List[Container],
 
 
 def system_isolation(matrix: ReachabilityMatrix, idx: int) -> List[int]:
-    """Containers j not reachable from container idx (algorithm.py:45-55)."""
-    eng = _engine(matrix)
+    """Containers j not reachable from container idx (algorithm.py:45-55).
+    On a row shard, idx must be one of the shard's rows."""
+    eng = _engine(matrix, whole=False)
     n = matrix.container_size
     i = int(idx)
     if i < 0:

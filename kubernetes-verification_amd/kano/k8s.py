@@ -48,6 +48,22 @@ kubesv's behaviour is kept where it departs from the Kubernetes documents
   namespace missing from the namespace list raises ``KeyError``
   (constraint.py:251).
 
+Two behaviours of kubesv's encoding are NOT reproduced (intentional
+departures, both z3 sort/name artefacts rather than readings of the rules):
+
+* K8 a ``namespaceSelector`` In / NotIn requirement: kubesv declares the
+  membership relation over ``pod_sort`` and applies it to a namespace
+  variable (model.py:211-221); z3 then raises a sort mismatch whenever the
+  pod and namespace bit-vector widths differ, and otherwise ranges over
+  namespace ids read as pod ids.  Here the requirement is evaluated on the
+  namespace's labels (the Kubernetes meaning).
+* K9 namespace label relations are declared as ``Function(k, nam_sort,
+  ...)`` under the pod relation's name ``k`` (constraint.py:270, not
+  ``k__namespace``); when the two sort widths match that is the same z3
+  function as the pod label relation ``k``, so pod and namespace facts on a
+  shared key mix.  Here the namespace's labels and the pods' labels stay
+  separate columns.
+
 Parity: against ``oracle/kano_oracle.py kubesv_edge_py``, a restatement of
 the Datalog rules on Python sets -- unpinned against kubesv itself (it needs
 z3 and the kubernetes client, both absent here).
@@ -326,12 +342,17 @@ def build(pods: List[Pod], policies: List[NetworkPolicy], namespaces: List[Names
     selected = None
     all_pairs = False
     if check_select_by_no_policy:
-        ms = DeviceBuild(intern(containers, sel_only), device=device, path=path)
+        # a pod is selected by some policy iff its row class's S(c) is not
+        # empty: the class-level build only (no matrix is written or
+        # allocated, whatever n and rows are)
         selected = np.zeros(n, dtype=bool)
         if n:
-            # allow = {} matches every pod: column 0 of M is the selected flag
-            from ._bits import words_to_bool
-            selected = words_to_bool(_wrap(ms, n).getcol(0).words(), n)
+            ms = DeviceBuild(intern(containers, sel_only), device=device, path=path,
+                             build=False)
+            ms.build_classes(path)
+            off, _ = ms.select_csr()
+            selected = np.diff(off)[ms.classes()] > 0
+            ms.close()
         all_pairs = bool(n) and not bool(selected.all())
     # the self term: expanded from the egress classes ("expand", the
     # default), or the destination is a build of the egress policies over its

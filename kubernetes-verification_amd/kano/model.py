@@ -29,6 +29,8 @@ try:                                    # the reference imports typing_extension
 except ImportError:                     # pragma: no cover
     from typing import Protocol
 
+import itertools
+
 import numpy as np
 
 from ._bits import BitArray, bool_to_words, words_to_bool
@@ -45,13 +47,19 @@ bitarray = BitArray
 KanoNativeError = _native.KanoNativeError
 
 
+_BUILD_IDS = itertools.count(1)
+
+
 class _BuildLists:
-    """Host-side, lazily fetched view of one build's per-container lists."""
+    """Host-side, lazily fetched view of one build's per-container lists.
+    ``bid`` names the build's segment of every container's accumulated
+    lists (quirk Q5: each build appends after the previous builds' entries)."""
 
     def __init__(self, engine):
         self._engine = engine
         self._sel = None
         self._alw = None
+        self.bid = next(_BUILD_IDS)
 
     def select_list(self, i: int) -> List[int]:
         if self._sel is None:
@@ -78,22 +86,35 @@ class _BuildLists:
 
 
 class _Renumber:
-    """ReachabilityMatrix.remove_policies on a container's lists: drop the
-    removed policy indices, renumber the rest (what a build over the updated
-    policy list would have appended)."""
+    """ReachabilityMatrix.remove_policies on a container's lists: within the
+    segment build ``bid`` appended, drop the removed policy indices and
+    renumber the rest (what that build over the updated policy list would
+    have appended); other builds' entries (Q5) are left alone."""
 
-    __slots__ = ("gone", "lo")
+    __slots__ = ("gone", "lo", "bid")
 
-    def __init__(self, gone: np.ndarray):
+    def __init__(self, gone: np.ndarray, bid: int):
         self.gone = gone
         self.lo = int(gone[0])
+        self.bid = bid
 
-    def apply(self, lst: List[int]) -> None:
+    def apply_list(self, lst: List[int]) -> None:
         lo = self.lo
         if any(x >= lo for x in lst):
             arr = np.asarray(lst, dtype=np.int64)
             keep = arr[~np.isin(arr, self.gone)]
             lst[:] = (keep - np.searchsorted(self.gone, keep, side="right")).tolist()
+
+    def apply(self, c: "Container") -> None:
+        seg = c._seg.get(self.bid)
+        if seg is None:
+            return
+        for which, lst in ((0, c._sel), (2, c._alw)):
+            a, b = seg[which], seg[which + 1]
+            part = lst[a:b]
+            self.apply_list(part)
+            lst[a:b] = part
+            c._shift(which, b, len(part) - (b - a), self.bid)
 
 
 class Container:
@@ -101,7 +122,7 @@ class Container:
     fields ``name, labels, select_policies, allow_policies``; the two lists
     receive each build's appends lazily (see module docstring)."""
 
-    __slots__ = ("name", "labels", "_sel", "_alw", "_pending", "__weakref__")
+    __slots__ = ("name", "labels", "_sel", "_alw", "_pending", "_seg", "__weakref__")
     __match_args__ = ("name", "labels", "select_policies", "allow_policies")
 
     def __init__(self, name: str, labels: Dict[str, str],
@@ -112,17 +133,46 @@ class Container:
         self._sel = [] if select_policies is None else select_policies
         self._alw = [] if allow_policies is None else allow_policies
         self._pending: List[tuple] = []
+        # build id -> [sel start, sel end, allow start, allow end]: where each
+        # build's appends sit in the accumulated lists
+        self._seg: Dict[int, List[int]] = {}
 
     def _flush(self) -> None:
         if self._pending:
             pend, self._pending = self._pending, []
             for lists, i in pend:
                 if isinstance(lists, _Renumber):   # a policy removal, applied lazily
-                    lists.apply(self._sel)
-                    lists.apply(self._alw)
+                    lists.apply(self)
                     continue
+                s0, a0 = len(self._sel), len(self._alw)
                 self._sel.extend(lists.select_list(i))
                 self._alw.extend(lists.allow_list(i))
+                self._seg[lists.bid] = [s0, len(self._sel), a0, len(self._alw)]
+
+    def _shift(self, which: int, at: int, delta: int, bid: int) -> None:
+        """Segment bid's list (0 select, 2 allow) grew by delta at position
+        at: move its end and every later segment."""
+        if delta == 0:
+            return
+        for k, seg in self._seg.items():
+            if k == bid:
+                seg[which + 1] += delta
+            elif seg[which] >= at:
+                seg[which] += delta
+                seg[which + 1] += delta
+
+    def _seg_append(self, bid: int, which: int, value: int) -> None:
+        """An incremental add: the build bid over the extended policy list
+        would have appended value at the end of its segment."""
+        self._flush()
+        lst = self._sel if which == 0 else self._alw
+        seg = self._seg.get(bid)
+        if seg is None:
+            lst.append(value)
+            return
+        at = seg[which + 1]
+        lst.insert(at, value)
+        self._shift(which, at, 1, bid)
 
     @property
     def select_policies(self) -> List[int]:
@@ -133,6 +183,7 @@ class Container:
     def select_policies(self, v: List[int]) -> None:
         self._flush()
         self._sel = v
+        self._seg = {}       # a replaced list has no build segments
 
     @property
     def allow_policies(self) -> List[int]:
@@ -143,6 +194,7 @@ class Container:
     def allow_policies(self, v: List[int]) -> None:
         self._flush()
         self._alw = v
+        self._seg = {}
 
     def getValueOrDefault(self, key: str, value: str):
         if key in self.labels:
@@ -435,6 +487,7 @@ class ReachabilityMatrix:
         m._policies = policies
         m._ncontainers = len(containers)
         m._lists = lists
+        m._bid = lists.bid
         return m
 
     def __init__(self, container_size: int, matrix: Any) -> None:
@@ -493,6 +546,10 @@ class ReachabilityMatrix:
         j = int(index)
         if not 0 <= j < n:
             raise IndexError("bitarray index out of range")
+        if getattr(self._engine, "is_shard", False):
+            r0, r1 = self._engine.row_span
+            raise ValueError(f"matrix holds only rows [{r0}, {r1}) of {n}: a column needs "
+                             "every row")
         return BitArray.from_words(self._engine.col(j), n)
 
     # engine access for kano.algorithm
@@ -533,9 +590,15 @@ class ReachabilityMatrix:
             s, a = eng.added_policy_sets(eid)
             pol.store_bcp(BitArray.from_words(s, n), BitArray.from_words(a, n))
             for i in set_bit_indices(s, n).tolist():
-                cs[i].select_policies.append(idx)
+                if isinstance(cs[i], Container):
+                    cs[i]._seg_append(self._bid, 0, idx)
+                else:
+                    cs[i].select_policies.append(idx)
             for j in set_bit_indices(a, n).tolist():
-                cs[j].allow_policies.append(idx)
+                if isinstance(cs[j], Container):
+                    cs[j]._seg_append(self._bid, 2, idx)
+                else:
+                    cs[j].allow_policies.append(idx)
             ps.append(pol)
             self._eids.append(eid)
         self._lists = None
@@ -551,13 +614,13 @@ class ReachabilityMatrix:
         self._engine.remove_policies([self._eids[k] for k in idx])
         # the lists drop the removed indices and renumber the rest (lazily,
         # in order with the build's own pending lists)
-        op = _Renumber(np.asarray(idx, dtype=np.int64))
+        op = _Renumber(np.asarray(idx, dtype=np.int64), self._bid)
         for c in cs:
             if isinstance(c, Container):
                 c._pending.append((op, -1))
             else:
-                op.apply(c.select_policies)
-                op.apply(c.allow_policies)
+                op.apply_list(c.select_policies)
+                op.apply_list(c.allow_policies)
         for k in reversed(idx):
             del ps[k]
             del self._eids[k]

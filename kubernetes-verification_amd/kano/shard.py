@@ -95,3 +95,16 @@ class ShardExchange:
             return self._run(eng, gid, sys_row, shadow, count_only, pairs, idx)
         with self.torch.cuda.stream(self.stream):
             return self._run(eng, gid, sys_row, shadow, count_only, pairs, idx)
+
+    def checks(self, eng, gid="stored", sys_row: int = 0, idx=None) -> dict:
+        """The same exchange over the rows as they stand after incremental
+        updates (kano_checks_shard; kano_verify would rebuild from the
+        tables): global column lists, the owner's system_isolation."""
+        def run():
+            eng.checks_shard(self.words.data_ptr(), gid=gid, sys_row=sys_row)
+            self.gather()
+            return eng.verify_combine(self.gathered.data_ptr(), self.nranks, idx=idx)
+        if self.stream is None:
+            return run()
+        with self.torch.cuda.stream(self.stream):
+            return run()
