@@ -143,6 +143,10 @@ struct kano_ctx {
   int s3_cus = 0;            // stream3 restricted to this many CUs (0: all), so that the
                              // tail's short kernels take few CUs from k_rows
   std::function<int()> fork_hook;
+  // kano_verify with rows_early == 2: called once the matrix write's inputs
+  // exist (the lists; Mc too when some class is heavy), to start k_rows on
+  // stream2 beside the class-level checks
+  std::function<int()> rows_hook;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   bool fork_pending = false;
   // host-time breakdown of kano_verify (KANO_TUNE=hosttime=1), printed at
@@ -942,6 +946,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     ua = ctx->light_cost * 16 > ctx->nnz_alw && ctx->nnz_alw * 4 <= (2ll << 30) ? 1 : 0;
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx));
+  if (ctx->rows_hook && H == 0) KTRY(ctx->rows_hook());   // no heavy rows: M needs no Mc
   if (U == 0) return 0;
   if (mc_rows_on(ctx)) {
     const bool four = 4 * ldMc * 8 <= 64 * 1024;
@@ -1008,6 +1013,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       KLAUNCH();
     }
   }
+  if (ctx->rows_hook && H > 0) KTRY(ctx->rows_hook());    // heavy rows copy from Mc
   if (!ctx->cols_deferred) KTRY(mc_cols(ctx));
   return 0;
 }
@@ -1452,7 +1458,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
         if (k == "alist") ctx->rows_alist = v < 0 ? -1 : (v ? 1 : 0);
         if (k == "nt" && (v == 0 || v == 256 || v == 512 || v == 1024)) ctx->rows_nt = v;
-        if (k == "probe" && v >= 0 && v <= 2) ctx->rows_probe = v;
+        if (k == "probe" && v >= 0 && v <= 3) ctx->rows_probe = v;
         if (k == "mover" && v >= 1 && v <= 64) ctx->m_over = v;
         if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
         if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
@@ -2435,23 +2441,40 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // policy_shadow's subset tests need only the lists and AC: they run on
   // stream2 beside the Mc chain (scatter, fold) and the flat-list build
   ctx->fork_pending = false;
+  // rows_early == 2: the matrix write starts on stream2 as soon as its
+  // inputs exist (rows_hook, inside the build), beside the class-level
+  // checks; policy_shadow's tests then take stream3 (the tail's stream,
+  // which runs after them anyway)
+  const bool rows_first = ctx->rows_early == 2 && rows_local(ctx) > 0;
+  hipStream_t tst = rows_first ? ctx->stream3 : ctx->stream2;
   if (want_shadow && ctx->fork_checks) {
-    ctx->fork_hook = [&]() -> int {
+    ctx->fork_hook = [&, tst]() -> int {
       KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));
-      KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
-      KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
-      KCHK(hipEventRecord(ctx->ev_join2, ctx->stream2));
+      KCHK(hipStreamWaitEvent(tst, ctx->ev_fork2, 0));
+      KTRY(shadow_test_launch(ctx, sp, tst));
+      KCHK(hipEventRecord(ctx->ev_join2, tst));
       ctx->fork_pending = true;
+      return 0;
+    };
+  }
+  bool early = false;
+  if (rows_first && !words_dev) {
+    ctx->rows_hook = [&]() -> int {
+      KTRY(launch_rows(ctx, true));
+      early = true;
       return 0;
     };
   }
   const int brc = build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run);
   ctx->fork_hook = nullptr;
+  ctx->rows_hook = nullptr;
   KTRY(brc);
   // the matrix write needs only the lists: with rows_early it starts here on
   // stream2, beside the class-level checks
-  bool early = ctx->rows_early && ctx->rows_overlap;
-  if (early) KTRY(launch_rows(ctx));
+  if (!early && ctx->rows_early == 1 && ctx->rows_overlap) {
+    KTRY(launch_rows(ctx));
+    early = true;
+  }
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   const bool cross_on = want_cross && cp.on;

@@ -1672,7 +1672,10 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   } else {
     for (int32_t m = m0; m < m1 && a.probe != 2; ++m) {
       if (heavy && m == m_begin) continue;
-      u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
+      // (probe 3, experiment: rows placed in member-list order, i.e. the
+      // grid's blocks write consecutive rows -- results are wrong)
+      const i64 drow = a.probe == 3 ? (i64)m : (i64)(a.mem[m] - a.r0);
+      u64* dst = a.M + drow * ldw + base;
       if (a.store_mode == 2) {
         for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
           __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
