@@ -128,6 +128,7 @@ struct kano_ctx {
                              // for plain stores on one box, 232 vs 246-258 on another);
                              // 0 plain, 1 word-major, 3 sc1 (no gain) are experiments
   int rows_persist = 0;      // k_rows persistent grid: blocks per CU (0: one block per item)
+  int rows_order = 0;        // matrix write in pod order (k_rows_ord) when no class is heavy
   // kano_verify: policy_shadow's subset tests on stream2 beside the Mc
   // chain (set by verify_front around the build; called once the lists and
   // AC exist), joined through ev_join2 before the shadow scans
@@ -179,6 +180,15 @@ struct kano_ctx {
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
+  // the side issue (SideIssue): the size-independent back-end work (zeroed
+  // AC / Mc, the crosscheck's group-key sort) on stream2 beside the join,
+  // with scan status regions of its own
+  DBuf scan_tmp_side;
+  i64 scan_cap_side = 0;
+  int scan_parity_side = 0;
+  int side_pre = 1;          // knob "sidepre": 0 = that work in order on the main stream
+  bool side_pending = false;
+  hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
@@ -406,6 +416,42 @@ int FillBatch::run() {
   hipLaunchKernelGGL(k_fill_many, dim3(grid), dim3(TPB), 0, ctx->stream, jobs);
   KLAUNCH();
   jobs.count = 0;
+  return 0;
+}
+
+// Issue the enclosed launches on stream2 (forked from the main stream at
+// construction, joined through ev_join3 at destruction; the main stream waits
+// for it with side_join): ctx->stream and the scan status buffers are swapped
+// for the duration, so every launch helper sends its work there unchanged.
+struct SideIssue {
+  kano_ctx* c;
+  bool on;
+  SideIssue(kano_ctx* ctx, bool enable) : c(ctx), on(enable && ctx->stream2) {
+    if (!on) return;
+    if (hipEventRecord(c->ev_fork3, c->stream) != hipSuccess ||
+        hipStreamWaitEvent(c->stream2, c->ev_fork3, 0) != hipSuccess) {
+      on = false;
+      return;
+    }
+    swap();
+  }
+  void swap() {
+    std::swap(c->stream, c->stream2);
+    std::swap(c->scan_tmp, c->scan_tmp_side);
+    std::swap(c->scan_cap, c->scan_cap_side);
+    std::swap(c->scan_parity, c->scan_parity_side);
+  }
+  ~SideIssue() {
+    if (!on) return;
+    swap();
+    if (hipEventRecord(c->ev_join3, c->stream2) == hipSuccess) c->side_pending = true;
+  }
+};
+
+int side_join(kano_ctx* ctx) {
+  if (!ctx->side_pending) return 0;
+  ctx->side_pending = false;
+  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join3, 0));
   return 0;
 }
 
@@ -708,7 +754,7 @@ int sel_spb(const kano_ctx* ctx) {
   return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
 }
 
-int do_front(kano_ctx* ctx, int path) {
+int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::function<int()>()) {
   ctx->rc.m0 = ctx->r0;
   ctx->rc.m1 = ctx->r1;
   ctx->cc.m0 = 0;
@@ -757,6 +803,10 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
     KTRY(fb.run());
+  }
+  if (side) {   // the size-independent back-end work, beside the join (stream2)
+    SideIssue si(ctx, true);
+    KTRY(side());
   }
   KTRY(classify_phase2b(ctx));
   KTRY(match_both(ctx));
@@ -1089,6 +1139,20 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
   int nt = ctx->rows_nt;
   if (nt == 0) nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   KCHK(hipEventRecord(ctx->ev[7], rs));
+  const size_t lds = sizeof(u64) * cww;
+  if (ctx->rows_order && ctx->heavy_count == 0 && rl <= (i64)INT32_MAX) {
+    // pod order: one row per block, consecutive blocks on consecutive rows
+    a.rcls = P_<int32_t>(ctx->rc.cls);
+    const dim3 g((unsigned)rl, ncc);
+    if (nt == 1024) hipLaunchKernelGGL(k_rows_ord<1024>, g, dim3(1024), lds, rs, a);
+    else if (nt == 512) hipLaunchKernelGGL(k_rows_ord<512>, g, dim3(512), lds, rs, a);
+    else hipLaunchKernelGGL(k_rows_ord<256>, g, dim3(256), lds, rs, a);
+    KLAUNCH();
+    KCHK(hipEventRecord(ctx->ev[8], rs));
+    if (rs != ctx->stream) KCHK(hipEventRecord(ctx->ev_rows, rs));
+    ctx->rows_timed = true;
+    return 0;
+  }
   dim3 grid((unsigned)ctx->wi_total, ncc);
   a.nitems = 0;
   if (ctx->rows_persist > 0) {
@@ -1100,7 +1164,6 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
       grid.x = (unsigned)g;
     }
   }
-  const size_t lds = sizeof(u64) * cww;
   if (nt == 1024) hipLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, a);
   else if (nt == 512) hipLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, a);
   else hipLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, a);
@@ -1475,11 +1538,13 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "k8srows") ctx->k8s_rows_cls = v;
         if (k == "store") ctx->rows_store = v;
         if (k == "persist" && v >= 0 && v <= 64) ctx->rows_persist = v;
+        if (k == "order") ctx->rows_order = v;
         if (k == "hosttime") ctx->host_timing = v;
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
+        if (k == "sidepre") ctx->side_pre = v;
         if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
@@ -1533,7 +1598,9 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sync, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork3, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join3, hipEventDisableTiming) != hipSuccess) {
     kano_destroy(ctx);
     return -EIO;
   }
@@ -1585,7 +1652,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->hoff,   &ctx->hlist,   &ctx->sq,      &ctx->pfoff,     &ctx->ACT,
                   &ctx->AC,     &ctx->nca,     &ctx->acnt,    &ctx->alcoff,    &ctx->alc,
                   &ctx->aloff,  &ctx->alist,   &ctx->M,       &ctx->Mc,        &ctx->color,
-                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp,
+                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp, &ctx->scan_tmp_side,
                   &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
                   &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
@@ -1608,6 +1675,8 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
   if (ctx->ev_sizes) (void)hipEventDestroy(ctx->ev_sizes);
   if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
+  if (ctx->ev_fork3) (void)hipEventDestroy(ctx->ev_fork3);
+  if (ctx->ev_join3) (void)hipEventDestroy(ctx->ev_join3);
   if (ctx->ev_fork2) (void)hipEventDestroy(ctx->ev_fork2);
   if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
   delete ctx;
@@ -1911,12 +1980,18 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KTRY(stage_mark(ctx, 0, ctx->stream));
-  KTRY(do_front(ctx, path));
-  // host sync 2 (the list sizes), overlapped with the size-independent part
-  // of the back end
+  // the size-independent part of the back end (zeroed AC / Mc, the
+  // crosscheck's group-key sort) needs only the class counts: with side_pre
+  // it runs on stream2 beside the join, else here, overlapped with host sync 2
+  ctx->side_pending = false;
+  const bool side = ctx->side_pre != 0;
+  std::function<int()> pre = [&]() -> int { return do_back_pre(ctx, pre_fill, pre_run); };
+  KTRY(do_front(ctx, path, side ? pre : std::function<int()>()));
+  // host sync 2 (the list sizes)
   KTRY(mirror_begin(ctx));
-  KTRY(do_back_pre(ctx, pre_fill, pre_run));
+  if (!side) KTRY(do_back_pre(ctx, pre_fill, pre_run));
   KTRY(read_sizes(ctx));
+  KTRY(side_join(ctx));
   KTRY(stage_mark(ctx, 3, ctx->stream));
   ctx->cols_deferred = defer_cols;
   KTRY(do_back(ctx, path, extra));

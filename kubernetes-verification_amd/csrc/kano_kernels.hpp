@@ -1540,6 +1540,7 @@ struct RowsArgs {
   int probe;             // experiments: 1 skip the row build, 2 skip the stores
   int store_mode;        // experiments: 0 row-major stores, 1 word-major, 2 nontemporal, 3 sc1
   i64 nitems;            // 0: one work item per block; else the grid strides over nitems
+  const int32_t* rcls;   // k_rows_ord: row class of every pod (global index)
   u64* color;
   u64* colnand;
 };
@@ -1553,6 +1554,92 @@ constexpr int ROWS_SEG = 256;
 // to memory, MI355X_MICROARCH.md "stores of each flavour"); a vector store
 __device__ __forceinline__ void store16_sc1(u64* dst, u64x2 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(v) : "memory");
+}
+
+// the row of light class c over columns [64*base, 64*(base + nw)) built in
+// LDS from the allowed-pod lists of S(c) (zeroed first; ends in a barrier)
+template <int NT>
+__device__ __forceinline__ void build_light_row(const RowsArgs& a, i64 c, i64 base, int nw,
+                                                u64* row) {
+  constexpr int NW = NT / 64;
+  for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
+  __syncthreads();
+  const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
+  const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
+  if (a.alist && s1 - s0 <= ROWS_SEG) {
+    // the allowed-pod lists of S(c) as one flat range: a segment table
+    // (start, prefix) in LDS, then every thread streams entries with
+    // ROWS_UNROLL loads in flight -- no per-policy round trips
+    __shared__ i64 seg_start[ROWS_SEG];
+    __shared__ i64 seg_pre[ROWS_SEG + 1];
+    __shared__ i64 sm_scan[NT / 64];
+    const int ns = (int)(s1 - s0);
+    i64 len = 0, st = 0;
+    if ((int)threadIdx.x < ns) {   // ns <= ROWS_SEG <= NT
+      const int32_t p = a.slist[s0 + threadIdx.x];
+      st = a.aloff[p];
+      len = a.aloff[p + 1] - st;
+    }
+    i64 total;
+    const i64 pre = block_excl_scan_nw<NT / 64>(len, sm_scan, total);
+    if ((int)threadIdx.x < ns) {
+      seg_start[threadIdx.x] = st;
+      seg_pre[threadIdx.x] = pre;
+    }
+    if (threadIdx.x == 0) seg_pre[ns] = total;
+    __syncthreads();
+    for (i64 i0 = threadIdx.x; i0 < total; i0 += (i64)NT * ROWS_UNROLL) {
+      int32_t jv[ROWS_UNROLL];
+#pragma unroll
+      for (int u = 0; u < ROWS_UNROLL; ++u) {
+        const i64 id = i0 + (i64)u * NT;
+        jv[u] = -1;
+        if (id < total) {
+          int lo = 0, hi = ns - 1;   // last segment with seg_pre <= id
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (seg_pre[mid] <= id) lo = mid; else hi = mid - 1;
+          }
+          jv[u] = a.alist[seg_start[lo] + (id - seg_pre[lo])];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < ROWS_UNROLL; ++u) {
+        const int32_t j = jv[u];
+        if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+      }
+    }
+  } else if (a.alist) {
+    // the flat allowed-pod list of each policy of S(c), across all threads
+    for (i64 e = s0; e < s1; ++e) {
+      const int32_t p = a.slist[e];
+      const int32_t* L = a.alist + a.aloff[p];
+      const i64 cnt = a.aloff[p + 1] - a.aloff[p];
+      for (i64 k = threadIdx.x; k < cnt; k += NT) {
+        const int32_t j = L[k];
+        if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+      }
+    }
+  } else {
+    // (policy, allowed column class) entries dealt round-robin to the
+    // waves, the class's members across the lanes
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int t = 0;
+    for (i64 e = s0; e < s1; ++e) {
+      const int32_t p = a.slist[e];
+      const i64 q1 = a.alcoff[p + 1];
+      for (i64 q = a.alcoff[p]; q < q1; ++q, ++t) {
+        if (t % NW != wid) continue;
+        const int32_t ca = a.alc[q];
+        const int32_t k1 = a.cmoff[ca + 1];
+        for (int32_t k = a.cmoff[ca] + lane; k < k1; k += 64) {
+          const int32_t j = a.cmem[k];
+          if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+        }
+      }
+    }
+  }
+  __syncthreads();
 }
 
 // one work item (class c, <= ch member rows, column chunk blockIdx.y) of
@@ -1581,84 +1668,7 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
       *(u64x2*)&row[w] = *(const u64x2*)&src[w];
     __syncthreads();
   } else {
-    for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
-    __syncthreads();
-    const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
-    const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
-    if (a.alist && s1 - s0 <= ROWS_SEG) {
-      // the allowed-pod lists of S(c) as one flat range: a segment table
-      // (start, prefix) in LDS, then every thread streams entries with
-      // ROWS_UNROLL loads in flight -- no per-policy round trips
-      __shared__ i64 seg_start[ROWS_SEG];
-      __shared__ i64 seg_pre[ROWS_SEG + 1];
-      __shared__ i64 sm_scan[NT / 64];
-      const int ns = (int)(s1 - s0);
-      i64 len = 0, st = 0;
-      if ((int)threadIdx.x < ns) {   // ns <= ROWS_SEG <= NT
-        const int32_t p = a.slist[s0 + threadIdx.x];
-        st = a.aloff[p];
-        len = a.aloff[p + 1] - st;
-      }
-      i64 total;
-      const i64 pre = block_excl_scan_nw<NT / 64>(len, sm_scan, total);
-      if ((int)threadIdx.x < ns) {
-        seg_start[threadIdx.x] = st;
-        seg_pre[threadIdx.x] = pre;
-      }
-      if (threadIdx.x == 0) seg_pre[ns] = total;
-      __syncthreads();
-      for (i64 i0 = threadIdx.x; i0 < total; i0 += (i64)NT * ROWS_UNROLL) {
-        int32_t jv[ROWS_UNROLL];
-#pragma unroll
-        for (int u = 0; u < ROWS_UNROLL; ++u) {
-          const i64 id = i0 + (i64)u * NT;
-          jv[u] = -1;
-          if (id < total) {
-            int lo = 0, hi = ns - 1;   // last segment with seg_pre <= id
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if (seg_pre[mid] <= id) lo = mid; else hi = mid - 1;
-            }
-            jv[u] = a.alist[seg_start[lo] + (id - seg_pre[lo])];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < ROWS_UNROLL; ++u) {
-          const int32_t j = jv[u];
-          if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
-        }
-      }
-    } else if (a.alist) {
-      // the flat allowed-pod list of each policy of S(c), across all threads
-      for (i64 e = s0; e < s1; ++e) {
-        const int32_t p = a.slist[e];
-        const int32_t* L = a.alist + a.aloff[p];
-        const i64 cnt = a.aloff[p + 1] - a.aloff[p];
-        for (i64 k = threadIdx.x; k < cnt; k += NT) {
-          const int32_t j = L[k];
-          if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
-        }
-      }
-    } else {
-      // (policy, allowed column class) entries dealt round-robin to the
-      // waves, the class's members across the lanes
-      const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-      int t = 0;
-      for (i64 e = s0; e < s1; ++e) {
-        const int32_t p = a.slist[e];
-        const i64 q1 = a.alcoff[p + 1];
-        for (i64 q = a.alcoff[p]; q < q1; ++q, ++t) {
-          if (t % NW != wid) continue;
-          const int32_t ca = a.alc[q];
-          const int32_t k1 = a.cmoff[ca + 1];
-          for (int32_t k = a.cmoff[ca] + lane; k < k1; k += 64) {
-            const int32_t j = a.cmem[k];
-            if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
-          }
-        }
-      }
-    }
-    __syncthreads();
+    build_light_row<NT>(a, c, base, nw, row);
   }
   if (a.store_mode == 1 && a.probe != 2) {
     // word-major: each thread's words go to every member row before the
@@ -1715,6 +1725,42 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   for (i64 b = blockIdx.x; b < a.nitems; b += gridDim.x) {
     rows_item<NT>(a, b, row);
     __syncthreads();
+  }
+}
+
+// The matrix write in pod order (light classes only): block b writes row
+// r0 + b, column chunk blockIdx.y, after building its class's row in LDS.
+// Consecutive blocks write consecutive rows and every lane stores 32
+// contiguous bytes (two 16-byte stores): measured 6.6 TB/s for that store
+// shape against 5.2-5.5 TB/s for 16 bytes per lane or rows in class order
+// (profiles/r02_store_ceiling.txt).  A class row is rebuilt for each member
+// (the list walk is cheap next to the 8*W-byte store).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_ord(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u64 row[];
+  const i64 li = blockIdx.x;
+  const i64 c = a.rcls[a.r0 + li];
+  const i64 base = (i64)blockIdx.y * a.cww;
+  const int nw = (int)min((i64)a.cww, a.wW - base);
+  if (nw <= 0) return;
+  if (c >= 0 && c < a.U) {
+    build_light_row<NT>(a, c, base, nw, row);
+  } else {
+    for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
+    __syncthreads();
+  }
+  u64* dst = a.M + li * a.ldM + base;
+  // nw is a multiple of 4 (ldM and the chunk width are multiples of 16)
+  for (int w = threadIdx.x * 4; w < nw; w += NT * 4) {
+    const u64x2 v0 = *(const u64x2*)&row[w];
+    const u64x2 v1 = *(const u64x2*)&row[w + 2];
+    if (a.store_mode == 2) {
+      __builtin_nontemporal_store(v0, (u64x2*)&dst[w]);
+      __builtin_nontemporal_store(v1, (u64x2*)&dst[w + 2]);
+    } else {
+      *(u64x2*)&dst[w] = v0;
+      *(u64x2*)&dst[w + 2] = v1;
+    }
   }
 }
 

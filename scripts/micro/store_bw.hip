@@ -93,6 +93,35 @@ __global__ __launch_bounds__(256) void k_rows_chunk(u64* M, const int* perm, lon
     }
   }
 }
+// torch's vectorized fill shape: one-shot blocks, 32 contiguous bytes per lane
+__global__ __launch_bounds__(256) void k_flat32(u64* M, long nw) {
+  const long w = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const u64x2 v = {1ull, 2ull};
+  if (w + 3 < nw) {
+    *(u64x2*)&M[w] = v;
+    *(u64x2*)&M[w + 2] = v;
+  }
+}
+// k_rows' shape with 32 bytes per lane: block per row
+__global__ __launch_bounds__(256) void k_rows32(u64* M, const int* perm, long ldw, int W) {
+  u64* dst = M + (long)perm[blockIdx.x] * ldw;
+  const u64x2 v = {(u64)blockIdx.x, 5ull};
+  for (int w = threadIdx.x * 4; w < W; w += 1024) {
+    *(u64x2*)&dst[w] = v;
+    if (w + 2 < W) *(u64x2*)&dst[w + 2] = v;
+  }
+}
+// one-shot blocks of CHUNK bytes each, 16 or 32 B per lane, chunks in
+// order or permuted
+template <int PER_LANE>
+__global__ __launch_bounds__(256) void k_chunks(u64* M, const int* cperm, long nchunks) {
+  const long c = cperm ? cperm[blockIdx.x] : (long)blockIdx.x;
+  constexpr int WPL = PER_LANE / 8;                     // words per lane
+  const long w = c * 256 * WPL + (long)threadIdx.x * WPL;
+  const u64x2 v = {(u64)c, 9ull};
+  *(u64x2*)&M[w] = v;
+  if (WPL == 4) *(u64x2*)&M[w + 2] = v;
+}
 int main() {
   const int n = 100000, W = 1563;
   const long ldw = 1568;
@@ -221,6 +250,47 @@ int main() {
       best = std::min(best, ms);
     }
     printf("rows random wave-per-row lane chunk %d x 16B: %.1f us  %.0f GB/s\n", ch, best * 1e3, bytes / (best * 1e-3) / 1e9);
+  }
+  for (int kind = 0; kind < 2; ++kind) {
+    float best = 1e9;
+    for (int rep = 0; rep < 6; ++rep) {
+      hipEventRecord(a);
+      if (kind == 0) hipLaunchKernelGGL(k_flat32, dim3((unsigned)(((long)W * n / 4 + 255) / 256)), dim3(256), 0, 0, M, (long)W * n);
+      else hipLaunchKernelGGL(k_rows32, dim3(n), dim3(256), 0, 0, M, dperm, ldw, W);
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      best = std::min(best, ms);
+    }
+    printf("%s: %.1f us  %.0f GB/s\n", kind ? "rows random 32B/lane" : "flat 32B/lane one-shot", best * 1e3, bytes / (best * 1e-3) / 1e9);
+  }
+  {
+    for (int per : {16, 32}) for (int permuted = 0; permuted < 2; ++permuted) {
+      const long chunk_words = 256L * per / 8;
+      const long nch = (long)W * n / chunk_words;
+      std::vector<int> cp(nch);
+      for (long i = 0; i < nch; ++i) cp[i] = (int)i;
+      if (permuted) std::shuffle(cp.begin(), cp.end(), std::mt19937(3));
+      int* dcp;
+      hipMalloc(&dcp, sizeof(int) * nch);
+      hipMemcpy(dcp, cp.data(), sizeof(int) * nch, hipMemcpyHostToDevice);
+      float best = 1e9;
+      for (int rep = 0; rep < 6; ++rep) {
+        hipEventRecord(a);
+        if (per == 16) hipLaunchKernelGGL(k_chunks<16>, dim3((unsigned)nch), dim3(256), 0, 0, M, dcp, nch);
+        else hipLaunchKernelGGL(k_chunks<32>, dim3((unsigned)nch), dim3(256), 0, 0, M, dcp, nch);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        best = std::min(best, ms);
+      }
+      hipFree(dcp);
+      const double by = 8.0 * chunk_words * nch;
+      printf("chunks %ld B, %d B/lane, %s: %.1f us  %.0f GB/s\n", chunk_words * 8, per,
+             permuted ? "random order" : "in order", best * 1e3, by / (best * 1e-3) / 1e9);
+    }
   }
   for (int rpb : {1, 4}) {
     float best = 1e9;
