@@ -186,7 +186,9 @@ struct kano_ctx {
   DBuf scan_tmp_side;
   i64 scan_cap_side = 0;
   int scan_parity_side = 0;
-  int side_pre = 1;          // knob "sidepre": 0 = that work in order on the main stream
+  int side_pre = 0;          // knob "sidepre": 1 = that work on stream2 (measured slower on
+                             // C3: 0.658 vs 0.624 ms -- the host issuing the side work
+                             // delays the join chain by ~30 us)
   bool side_pending = false;
   hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
