@@ -186,7 +186,9 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
  *     misses j (:4-9), user_crosscheck[j] = some shard crosses (:27-42) --
  *     then the same outputs as kano_verify: the three global lists, this
  *     shard's system_isolation row (-1 when sys_row is elsewhere), and this
- *     shard's policy_shadow pairs (rank order = the reference's order). */
+ *     shard's policy_shadow pairs (rank order = the reference's order).
+ * with_shadow: 0 no policy_shadow, 1 the pairs, 2 the pair count only (then
+ * kano_verify_combine takes shadow_cap < 0). */
 int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
                       int64_t sys_row, int with_shadow, uint64_t* words_dev);
 int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nranks,

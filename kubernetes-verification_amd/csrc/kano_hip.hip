@@ -209,6 +209,11 @@ struct kano_ctx {
   int path_tn = 2;           // k_path_mfma column tiles per wave (2 or 4)
   int path_lds = 1;          // k_path_expand16: the group table in LDS when it fits (tests: 0)
   i64 shadow_total = -1;
+  // policy_shadow count-only (kano_verify with shadow_cap < 0): the grouped
+  // count (k_shg_*) instead of the pair-by-pair flags
+  bool vs_count_only = false;
+  DBuf shg_h, shg_tkey, shg_trep, shg_slot, shg_isrep, shg_gidx, shg_gid, shg_reps, shg_sub,
+      shg_err;
   DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
   DBuf icnt, ioff, sysrow, idxd;
   u64* ghost = nullptr;      // pinned landing buffer for the size slots
@@ -1655,6 +1660,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->AC,     &ctx->nca,     &ctx->acnt,    &ctx->alcoff,    &ctx->alc,
                   &ctx->aloff,  &ctx->alist,   &ctx->M,       &ctx->Mc,        &ctx->color,
                   &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp, &ctx->scan_tmp_side,
+                  &ctx->shg_h,  &ctx->shg_tkey, &ctx->shg_trep, &ctx->shg_slot, &ctx->shg_isrep,
+                  &ctx->shg_gidx, &ctx->shg_gid, &ctx->shg_reps, &ctx->shg_sub, &ctx->shg_err,
                   &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
                   &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
@@ -2267,7 +2274,7 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   sp.nf = ctx->nflags;
   sp.nt = (sp.nf + SH_TILE - 1) / SH_TILE;
   KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
-  KTRY(dalloc(ctx, ctx->flags, sp.nf + 16));
+  KTRY(dalloc(ctx, ctx->flags, ctx->vs_count_only ? 16 : sp.nf + 16));
   KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, sp.U)));
   KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (sp.U + 1)));
   KTRY(dalloc(ctx, ctx->tp, sizeof(i64) * std::max<i64>(1, sp.rl)));
@@ -2278,9 +2285,75 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
 }
 
+// the grouped count (count-only policy_shadow): T[c] per row class
+int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
+  const i64 P = ctx->P, U = sp.U;
+  if (P == 0 || U == 0) return 0;
+  i64 Th = 64;
+  while (Th < 2 * P) Th <<= 1;
+  const i64 GW = (SHG_MAX + 63) / 64;
+  KTRY(dalloc(ctx, ctx->shg_h, sizeof(u64) * P));
+  KTRY(dalloc(ctx, ctx->shg_tkey, sizeof(u64) * Th));
+  KTRY(dalloc(ctx, ctx->shg_trep, sizeof(int32_t) * Th));
+  KTRY(dalloc(ctx, ctx->shg_slot, sizeof(int32_t) * P));
+  KTRY(dalloc(ctx, ctx->shg_isrep, sizeof(int32_t) * P));
+  KTRY(dalloc(ctx, ctx->shg_gidx, sizeof(int32_t) * (P + 1)));
+  KTRY(dalloc(ctx, ctx->shg_gid, sizeof(int32_t) * P));
+  KTRY(dalloc(ctx, ctx->shg_reps, sizeof(int32_t) * SHG_MAX));
+  KTRY(dalloc(ctx, ctx->shg_sub, sizeof(u64) * SHG_MAX * GW));
+  KTRY(dalloc(ctx, ctx->shg_err, sizeof(int32_t) * 4));
+  KCHK(hipMemsetAsync(ctx->shg_tkey.p, 0xff, sizeof(u64) * Th, st));
+  KCHK(hipMemsetAsync(ctx->shg_trep.p, 0x7f, sizeof(int32_t) * Th, st));
+  KCHK(hipMemsetAsync(ctx->shg_err.p, 0, sizeof(int32_t) * 4, st));
+  const u64* AC = P_<u64>(ctx->AC);
+  hipLaunchKernelGGL(k_shg_hash, dim3(nblk(P, WPB)), dim3(TPB), 0, st, P, AC, ctx->ldC, ctx->UAW,
+                     P_<u64>(ctx->shg_h));
+  KLAUNCH();
+  hipLaunchKernelGGL(k_shg_insert, dim3(nblk(P)), dim3(TPB), 0, st, P, P_<u64>(ctx->shg_h),
+                     P_<unsigned long long>(ctx->shg_tkey), P_<int32_t>(ctx->shg_trep),
+                     P_<int32_t>(ctx->shg_slot), (uint32_t)(Th - 1));
+  KLAUNCH();
+  hipLaunchKernelGGL(k_shg_verify, dim3(nblk(P, WPB)), dim3(TPB), 0, st, P,
+                     P_<int32_t>(ctx->shg_slot), P_<int32_t>(ctx->shg_trep), AC, ctx->ldC,
+                     ctx->UAW, P_<int32_t>(ctx->shg_isrep), P_<int32_t>(ctx->shg_err));
+  KLAUNCH();
+  hipLaunchKernelGGL(k_shg_scan, dim3(1), dim3(1024), 0, st, P, P_<int32_t>(ctx->shg_isrep),
+                     P_<int32_t>(ctx->shg_gidx));
+  KLAUNCH();
+  hipLaunchKernelGGL(k_shg_assign, dim3(nblk(P)), dim3(TPB), 0, st, P, P_<int32_t>(ctx->shg_slot),
+                     P_<int32_t>(ctx->shg_trep), P_<int32_t>(ctx->shg_isrep),
+                     P_<int32_t>(ctx->shg_gidx), P_<int32_t>(ctx->shg_gid),
+                     P_<int32_t>(ctx->shg_reps));
+  KLAUNCH();
+  const int32_t* Gp = P_<int32_t>(ctx->shg_gidx) + P;
+  hipLaunchKernelGGL(k_shg_sub, dim3(nblk(std::min<i64>(P, SHG_MAX), WPB)), dim3(TPB), 0, st, Gp,
+                     P_<int32_t>(ctx->shg_reps), AC, ctx->ldC, ctx->UAW, P_<u64>(ctx->shg_sub),
+                     GW);
+  KLAUNCH();
+  ShadowArgs a;
+  a.U = U;
+  a.soffc = P_<i64>(ctx->soffc);
+  a.slist = P_<int32_t>(ctx->slist);
+  a.mcnt = P_<int32_t>(ctx->rc.mcnt);
+  a.pfoff = P_<i64>(ctx->pfoff);
+  a.nca = P_<int32_t>(ctx->nca);
+  a.alcoff = P_<i64>(ctx->alcoff);
+  a.alc = P_<int32_t>(ctx->alc);
+  a.AC = AC;
+  a.ldC = ctx->ldC;
+  a.flags = nullptr;
+  a.T = P_<i64>(ctx->T);
+  hipLaunchKernelGGL(k_shg_count, dim3((unsigned)U), dim3(TPB), 0, st, a,
+                     P_<int32_t>(ctx->shg_gid), Gp, P_<u64>(ctx->shg_sub), GW,
+                     P_<int32_t>(ctx->shg_err));
+  KLAUNCH();
+  return 0;
+}
+
 // subset tests; the list-offset scans go to sb
 int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   KTRY(stage_mark(ctx, 5, st));
+  if (ctx->vs_count_only) return shadow_group_launch(ctx, sp, st);
   if (sp.nt > 0) {
     ShadowArgs a;
     a.U = sp.U;
@@ -2492,7 +2565,8 @@ namespace {
 // the gathered words of all shards,) list the results, the matrix write,
 // policy_shadow's pairs, the copies to the host.
 int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
-                 bool want_shadow, u64* words_dev) {
+                 bool want_shadow, u64* words_dev, bool count_only = false) {
+  ctx->vs_count_only = want_shadow && count_only;
   const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
   const bool want_cross = gid || stored;
   // the crosscheck and policy_shadow buffers are filled in the build's last
@@ -2710,6 +2784,11 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   hipStream_t cs = ctx->side_tail ? ctx->stream3 : ctx->stream;
   if (cs != ctx->stream) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
   i64 total = 0;
+  if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
+    (void)sync(ctx);
+    return fail(ctx, -EINVAL, "kano_verify_combine: the shard ran policy_shadow count-only "
+                              "(with_shadow = 2); pass shadow_cap < 0");
+  }
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
     if (shadow_cap >= 0) {
@@ -2749,7 +2828,8 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   ctx->ht_wait = 0;
-  KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr));
+  KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr,
+                    shadow_cap < 0));
   const auto t1 = clk::now();
   const int rc = verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count);
   if (ctx->host_timing) {
@@ -2769,7 +2849,7 @@ int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngrou
   if (!ctx) return -EINVAL;
   if (!words_dev) return fail(ctx, -EINVAL, "kano_verify_shard: words_dev is NULL");
   return verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0,
-                      reinterpret_cast<u64*>(words_dev));
+                      reinterpret_cast<u64*>(words_dev), with_shadow == 2);
 }
 
 int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nranks,

@@ -2094,6 +2094,169 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
     atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
 }
 
+// ---------------------------------------------------------------------------
+// policy_shadow's pair count without the pairs (kano_verify, shadow_cap < 0):
+// algorithm.py:58-80 counts, per pod i, the ordered pairs j != k of S(i) with
+// allow_k a subset of allow_j.  Policies with equal allow sets answer every
+// subset test alike, so the policies are grouped by their class-level allow
+// row AC[p] (hash, then a full-row check against the group's first policy);
+// sub[a][b] = allow(b) <= allow(a) is tested once per pair of groups, and a
+// row class with group counts n_c contributes  n_c' Sub n_c - |S(c)|  pairs
+// per member.  Broad selectors (C4): ~10^8 pair tests become ~10^4 group
+// tests.  On a hash collision or more than SHG_MAX groups every class falls
+// back to the pair-by-pair test (same result, slower).
+// ---------------------------------------------------------------------------
+constexpr int SHG_MAX = 4096;
+
+// one wave per policy: 64-bit hash of AC[p] (never the empty key ~0)
+__global__ __launch_bounds__(TPB) void k_shg_hash(i64 P, const u64* __restrict__ AC, i64 ldC,
+                                                  i64 UAW, u64* __restrict__ h) {
+  const i64 p = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= P) return;
+  const u64* r = AC + p * ldC;
+  u64 x = 0;
+  for (i64 w = lane; w < UAW; w += 64) x += mix64(r[w] ^ ((u64)w * 0xD6E8FEB86659FD93ull));
+  x = wave_sum(x);
+  if (lane == 0) h[p] = x == ~0ull ? 0ull : x;
+}
+
+// open-addressing insert keyed by the hash; the slot keeps its smallest policy
+__global__ __launch_bounds__(TPB) void k_shg_insert(i64 P, const u64* __restrict__ h,
+                                                    unsigned long long* __restrict__ tkey,
+                                                    int32_t* __restrict__ trep,
+                                                    int32_t* __restrict__ slot_of, uint32_t tmask) {
+  const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (p >= P) return;
+  const unsigned long long key = h[p];
+  uint32_t s = (uint32_t)(key ^ (key >> 29)) & tmask;
+  for (;;) {
+    const unsigned long long prev = atomicCAS(&tkey[s], ~0ull, key);
+    if (prev == ~0ull || prev == key) break;
+    s = (s + 1) & tmask;
+  }
+  atomicMin(&trep[s], (int32_t)p);
+  slot_of[p] = (int32_t)s;
+}
+
+// isrep[p] (the group's first policy); a policy whose row differs from its
+// representative's (a hash collision) sets err
+__global__ __launch_bounds__(TPB) void k_shg_verify(i64 P, const int32_t* __restrict__ slot_of,
+                                                    const int32_t* __restrict__ trep,
+                                                    const u64* __restrict__ AC, i64 ldC, i64 UAW,
+                                                    int32_t* __restrict__ isrep,
+                                                    int32_t* __restrict__ err) {
+  const i64 p = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= P) return;
+  const int32_t r = trep[slot_of[p]];
+  if (lane == 0) isrep[p] = r == p ? 1 : 0;
+  if (r == p) return;
+  const u64* a = AC + p * ldC;
+  const u64* b = AC + (i64)r * ldC;
+  bool diff = false;
+  for (i64 w = lane; w < UAW; w += 64) diff |= a[w] != b[w];
+  if (__any(diff) && lane == 0) atomicOr(err, 1);
+}
+
+// exclusive scan of isrep in one block (gidx[P] = the group count)
+__global__ __launch_bounds__(1024) void k_shg_scan(i64 P, const int32_t* __restrict__ isrep,
+                                                   int32_t* __restrict__ gidx) {
+  __shared__ int32_t sm[16];
+  const i64 per = (P + 1023) / 1024;
+  const i64 b0 = threadIdx.x * per, b1 = min(P, b0 + per);
+  int32_t s = 0;
+  for (i64 q = b0; q < b1; ++q) s += isrep[q];
+  int32_t tot;
+  int32_t pre = block_excl_scan_nw<16>(s, sm, tot);
+  for (i64 q = b0; q < b1; ++q) {
+    gidx[q] = pre;
+    pre += isrep[q];
+  }
+  if (threadIdx.x == 0) gidx[P] = tot;
+}
+
+// gid[p] = dense group of p; reps[g] = the group's first policy
+__global__ __launch_bounds__(TPB) void k_shg_assign(i64 P, const int32_t* __restrict__ slot_of,
+                                                    const int32_t* __restrict__ trep,
+                                                    const int32_t* __restrict__ isrep,
+                                                    const int32_t* __restrict__ gidx,
+                                                    int32_t* __restrict__ gid,
+                                                    int32_t* __restrict__ reps) {
+  const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (p >= P) return;
+  const int32_t g = gidx[trep[slot_of[p]]];
+  gid[p] = g;
+  if (isrep[p] && g < SHG_MAX) reps[g] = (int32_t)p;
+}
+
+// sub[a][b / 64] bit b = allow(reps[b]) <= allow(reps[a]); one wave per a
+__global__ __launch_bounds__(TPB) void k_shg_sub(const int32_t* __restrict__ Gp,
+                                                 const int32_t* __restrict__ reps,
+                                                 const u64* __restrict__ AC, i64 ldC, i64 UAW,
+                                                 u64* __restrict__ sub, i64 GW) {
+  const int32_t G = *Gp;
+  const i64 a = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (G > SHG_MAX || a >= G) return;
+  const u64* ra = AC + (i64)reps[a] * ldC;
+  for (i64 hb = 0; hb * 64 < G; ++hb) {
+    const i64 b = hb * 64 + lane;
+    bool ok = false;
+    if (b < G) {
+      const u64* rb = AC + (i64)reps[b] * ldC;
+      ok = true;
+      for (i64 w = 0; w < UAW && ok; ++w) ok = (rb[w] & ~ra[w]) == 0;
+    }
+    const u64 bits = __ballot(ok);
+    if (lane == 0) sub[a * GW + hb] = bits;
+  }
+}
+
+// T[c] = flagged pairs of row class c (one block per class)
+__global__ __launch_bounds__(TPB) void k_shg_count(ShadowArgs a, const int32_t* __restrict__ gid,
+                                                   const int32_t* __restrict__ Gp,
+                                                   const u64* __restrict__ sub, i64 GW,
+                                                   const int32_t* __restrict__ err) {
+  __shared__ int32_t hist[SHG_MAX];
+  __shared__ int32_t gl[SHG_MAX];
+  __shared__ int32_t ngl;
+  __shared__ i64 sm[4];
+  const i64 c = blockIdx.x;
+  if (a.mcnt[c] == 0) return;                    // no local member: T[c] stays 0
+  const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0;
+  if (s < 2) return;
+  const int32_t G = *Gp;
+  i64 acc = 0;
+  if (*err || G > SHG_MAX) {
+    // the pair-by-pair test (algorithm.py:76-79 at class level)
+    for (i64 q = threadIdx.x; q < s * s; q += TPB) {
+      const i64 x = q / s, y = q - x * s;
+      if (x == y) continue;
+      const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
+      acc += (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+    }
+    const i64 tot = block_sum(acc, sm);
+    if (threadIdx.x == 0) a.T[c] = tot;
+    return;
+  }
+  for (int g = threadIdx.x; g < G; g += TPB) hist[g] = 0;
+  if (threadIdx.x == 0) ngl = 0;
+  __syncthreads();
+  for (i64 e = threadIdx.x; e < s; e += TPB) {
+    const int32_t g = gid[a.slist[s0 + e]];
+    if (atomicAdd(&hist[g], 1) == 0) gl[atomicAdd(&ngl, 1)] = g;
+  }
+  __syncthreads();
+  const i64 m = ngl;
+  for (i64 q = threadIdx.x; q < m * m; q += TPB) {
+    const int32_t ga = gl[q / m], gb = gl[q % m];
+    if ((sub[(i64)ga * GW + (gb >> 6)] >> (gb & 63)) & 1ull) acc += (i64)hist[ga] * hist[gb];
+  }
+  const i64 tot = block_sum(acc, sm);
+  if (threadIdx.x == 0) a.T[c] = tot - s;
+}
+
 // the flagged pairs in flat order: L[tile_off[b] + rank] = (j, k)
 __global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ soffc, i64 U,
                                                         const int32_t* __restrict__ slist,

@@ -415,7 +415,8 @@ class DeviceBuild:
         return out
 
     def verify_shard(self, words_dev_ptr: int, gid=None, sys_row: int = 0, shadow: bool = True,
-                     ngroups: int = 0, path: Optional[str] = None) -> None:
+                     ngroups: int = 0, path: Optional[str] = None,
+                     shadow_count_only: bool = False) -> None:
         """kano_verify_shard: build this row shard and run its checks up to the
         column words, written (3*W u64, [OR | cross | NAND]) to the device
         buffer at ``words_dev_ptr``.  Asynchronous on the engine's stream;
@@ -430,8 +431,9 @@ class DeviceBuild:
             self._gid_keep = gid
         self._shard_shadow = bool(shadow)
         pth = nat.PATHS[path or self.path]
+        mode = (2 if shadow_count_only else 1) if shadow else 0
         self._chk(self.lib.kano_verify_shard(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row),
-                                             1 if shadow else 0, c_void_p(words_dev_ptr)),
+                                             mode, c_void_p(words_dev_ptr)),
                   "kano_verify_shard")
 
     def checks_shard(self, words_dev_ptr: int, gid=None, sys_row: int = 0,

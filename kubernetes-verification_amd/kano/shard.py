@@ -81,7 +81,8 @@ class ShardExchange:
             dist.all_gather_into_tensor(self.gathered, self.words)
 
     def _run(self, eng, gid, sys_row, shadow, count_only, pairs, idx):
-        eng.verify_shard(self.words.data_ptr(), gid=gid, sys_row=sys_row, shadow=shadow)
+        eng.verify_shard(self.words.data_ptr(), gid=gid, sys_row=sys_row, shadow=shadow,
+                         shadow_count_only=count_only)
         self.gather()
         return eng.verify_combine(self.gathered.data_ptr(), self.nranks, pairs=pairs, idx=idx,
                                   shadow_count_only=count_only)

@@ -296,3 +296,38 @@ def test_rows_variants_forced(name, tune, monkeypatch):
     check_verify(r, exp)
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     eng.close()
+
+
+# --- policy_shadow's count without the pairs (the grouped count) ----------
+@pytest.mark.parametrize("name", ["C2", "s_broad_1000", "s_broad_300", "s_sparse_2000", "q_shadow",
+                                  "q_wide_select", "gen_s5_10000", "gen_s4_4000"])
+def test_shadow_count_only_vs_kano_py(name, tmp_path):
+    """kano_verify's count-only policy_shadow (policies grouped by allow
+    set, one subset test per pair of groups) equals len(policy_shadow(...))
+    as kano_py computed it, whole and summed over row shards."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids, tables_from_cluster
+    from kano.synth import make_config, objects_from_json
+    from kano import model
+    exp = expected(name)
+    if name == "C2":
+        t = tables_from_cluster(make_config("C2"))
+    elif name.startswith("gen_"):
+        cs, ps = gen_objects(exp, tmp_path)
+        t = intern(cs, ps)
+    else:
+        cs, ps = objects_from_json(cluster(name), model)
+        t = intern(cs, ps)
+    eng = DeviceBuild(t, build=False)
+    r = eng.verify(None, sys_row=0, shadow=True, shadow_count_only=True)
+    assert r["shadow_count"] == exp["policy_shadow"]["count"]
+    assert r["pairs"] is None
+    assert index_list_matches(r["all_isolated"], exp["all_isolated"])
+    eng.close()
+    n = t.n
+    total = 0
+    for r0, r1 in [(0, n // 3), (n // 3, n)]:
+        e = DeviceBuild(t, rows=(r0, r1), build=False)
+        total += e.verify(None, sys_row=0, shadow=True, shadow_count_only=True)["shadow_count"]
+        e.close()
+    assert total == exp["policy_shadow"]["count"]
