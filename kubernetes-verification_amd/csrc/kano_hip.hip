@@ -2764,7 +2764,11 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // only, then queues policy_shadow's emission and the copies behind k_rows
   constexpr int NS = SZ_ERR - SZ_NL + 1;
   KTRY(mirror_begin(ctx));
-  if (!ctx->vs_early) KTRY(launch_rows(ctx));
+  // side_tail == 2: policy_shadow's compaction and emission run on the main
+  // stream before the matrix write (they crawl beside it: 60 + 40 us there
+  // against 10 + 4 us alone, and slow it), the copies beside it
+  const bool pre_tail = ctx->side_tail == 2 && !ctx->vs_early && want_shadow && shadow_cap >= 0;
+  if (!ctx->vs_early && !pre_tail) KTRY(launch_rows(ctx));
   i64 v[NS];
   KTRY(mirror_wait(ctx, SZ_NL, NS, v));
   if (ctx->vs_cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff)) {
@@ -2782,7 +2786,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // (the copies are blit kernels that crawl beside k_rows: the short
   // shadow kernels go first so that they do not queue behind them)
   hipStream_t cs = ctx->side_tail ? ctx->stream3 : ctx->stream;
-  if (cs != ctx->stream) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+  if (cs != ctx->stream && !pre_tail) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
   i64 total = 0;
   if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
     (void)sync(ctx);
@@ -2792,8 +2796,13 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
     if (shadow_cap >= 0) {
-      KTRY(shadow_back(ctx, v[0], total, cs));
+      KTRY(shadow_back(ctx, v[0], total, pre_tail ? ctx->stream : cs));
       ctx->shadow_total = total;
+      if (pre_tail) {     // the pairs exist: the matrix write, the copies beside it
+        KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
+        KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+        KTRY(launch_rows(ctx));
+      }
     } else {
       // count only: every subset test ran (the flags and the per-pod counts
       // above); the pairs are neither compacted nor emitted (C4: ~1e11)
