@@ -57,6 +57,9 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_UA      10   /* column classes (pods with equal allow keys) */
 #define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 int8 MFMA          */
 #define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the row kernel */
+#define KANO_INFO_GRAPH_HITS 13 /* kano_verify segments issued as a cached hipGraph */
+#define KANO_INFO_GRAPH_CAPTURES 14 /* ... captured into a new hipGraph       */
+#define KANO_INFO_GRAPH_DIRECT 15 /* ... issued operation by operation      */
 #define KANO_INFO_NSLOTS   16
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in

@@ -40,6 +40,7 @@
 #include <cstdio>
 
 #include "kano_hip.h"
+#include "kano_graph.hpp"     // records the HIP operations of kano_verify (see there)
 #include "kano_kernels.hpp"
 #include "kano_path.hpp"
 #include "kano_inc.hpp"
@@ -141,6 +142,18 @@ struct kano_ctx {
                              // 0.209-0.213 ms beside a normal-priority tail, 0.233-0.239
                              // beside a high-priority one; step 0.556 vs 0.582 ms)
   int side_tail = 1;         // kano_verify's tail on stream3 beside k_rows (else after it)
+  // kano_verify's operations recorded per segment (between host waits) and
+  // issued as cached hipGraphs (kano_graph.hpp); knob "graphs".  Measured
+  // slower, so off: C3 0.628 vs 0.587 ms a step, rank 0 of 8 0.426 vs 0.386 ms
+  // -- a segment reaches the GPU only once the host has recorded all of it,
+  // and replaying the graph is no faster on the GPU than direct dispatch
+  int graphs = 0;
+  bool seg_on = false;
+  kano_rec::Recorder rec;
+  std::vector<std::pair<uint64_t, hipGraphExec_t>> gcache;   // most recent last
+  std::vector<uint64_t> gseen;     // hashes issued directly once (capture on the 2nd)
+  std::vector<uint64_t> gbad;      // hashes whose capture failed
+  i64 g_hits = 0, g_captures = 0, g_direct = 0;
   int s3_cus = 0;            // stream3 restricted to this many CUs (0: all), so that the
                              // tail's short kernels take few CUs from k_rows
   std::function<int()> fork_hook;
@@ -273,10 +286,107 @@ int fail(kano_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
+// ---- segments: the recorded operations of kano_verify (kano_graph.hpp) ----
+constexpr size_t GCACHE_MAX = 48;
+
+void seg_begin(kano_ctx* ctx) {
+  if (!ctx->graphs || ctx->seg_on) return;
+  ctx->rec.clear();
+  ctx->seg_on = true;
+  kano_rec::g_rec = &ctx->rec;
+}
+
+bool contains(const std::vector<uint64_t>& v, uint64_t h) {
+  return std::find(v.begin(), v.end(), h) != v.end();
+}
+
+// issue the recorded segment: a cached graph, a new capture (the second time
+// the same sequence comes), or the operations one by one
+int seg_end(kano_ctx* ctx) {
+  if (!ctx->seg_on) return 0;
+  ctx->seg_on = false;
+  kano_rec::g_rec = nullptr;
+  kano_rec::Recorder& r = ctx->rec;
+  if (r.ops.empty()) return 0;
+  const uint64_t h = r.hash;
+  for (size_t i = 0; i < ctx->gcache.size(); ++i) {
+    if (ctx->gcache[i].first != h) continue;
+    hipGraphExec_t ge = ctx->gcache[i].second;
+    if (hipGraphLaunch(ge, ctx->stream) != hipSuccess) {
+      (void)hipGetLastError();
+      break;                                     // issue directly below
+    }
+    ++ctx->g_hits;
+    return 0;
+  }
+  if (r.capturable && contains(ctx->gseen, h) && !contains(ctx->gbad, h)) {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    bool ok = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed) == hipSuccess;
+    if (ok) {
+      const hipError_t ei = kano_rec::issue(r);
+      const hipError_t ee = hipStreamEndCapture(ctx->stream, &g);
+      ok = ei == hipSuccess && ee == hipSuccess && g &&
+           hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+    }
+    if (g) (void)hipGraphDestroy(g);
+    if (ok && hipGraphLaunch(ge, ctx->stream) == hipSuccess) {
+      if (ctx->gcache.size() >= GCACHE_MAX) {
+        (void)hipGraphExecDestroy(ctx->gcache.front().second);
+        ctx->gcache.erase(ctx->gcache.begin());
+      }
+      ctx->gcache.emplace_back(h, ge);
+      ++ctx->g_captures;
+      return 0;
+    }
+    if (ge) (void)hipGraphExecDestroy(ge);
+    (void)hipGetLastError();
+    ctx->gbad.push_back(h);                      // never again for this sequence
+  }
+  if (!contains(ctx->gseen, h)) {
+    if (ctx->gseen.size() >= 4 * GCACHE_MAX) ctx->gseen.erase(ctx->gseen.begin());
+    ctx->gseen.push_back(h);
+  }
+  ++ctx->g_direct;
+  const hipError_t e = kano_rec::issue(r);
+  if (e != hipSuccess) return fail(ctx, -EIO, std::string("issuing kernels: ") + hipGetErrorString(e));
+  return 0;
+}
+
+// the host is about to depend on the device (a wait, a free): issue what is
+// recorded so far and go on recording
+int seg_cut(kano_ctx* ctx) {
+  if (!ctx->seg_on) return 0;
+  const int rc = seg_end(ctx);
+  seg_begin(ctx);
+  return rc;
+}
+
+// operations issued directly for the scope (k_rows and its timing events)
+struct SegPause {
+  kano_ctx* c;
+  bool was;
+  int rc = 0;
+  explicit SegPause(kano_ctx* ctx) : c(ctx), was(ctx->seg_on) {
+    if (was) rc = seg_end(c);
+  }
+  ~SegPause() {
+    if (was) seg_begin(c);
+  }
+};
+
+// a recorded scope: kano_verify & co. (issued at the latest when it ends)
+struct SegScope {
+  kano_ctx* c;
+  explicit SegScope(kano_ctx* ctx) : c(ctx) { seg_begin(c); }
+  ~SegScope() { (void)seg_end(c); }
+};
+
 int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.p && b.bytes >= bytes) return 0;
   if (b.p) {
+    KTRY(seg_cut(ctx));   // recorded operations may still use the old buffer
     KCHK(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -466,6 +576,7 @@ int side_join(kano_ctx* ctx) {
 // of blocking in the runtime.  Measured on C3: +0.02 ms a step -- each
 // hipEventQuery costs more than the runtime's own wake-up -- so it is off.
 int wait_event(kano_ctx* ctx, hipEvent_t ev) {
+  KTRY(seg_cut(ctx));
   if (ctx->spin_wait) {
     hipError_t e;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
@@ -478,6 +589,7 @@ int wait_event(kano_ctx* ctx, hipEvent_t ev) {
 }
 
 int sync(kano_ctx* ctx) {
+  KTRY(seg_cut(ctx));
   if (ctx->spin_wait) {
     KCHK(hipEventRecord(ctx->ev_sync, ctx->stream));
     return wait_event(ctx, ctx->ev_sync);
@@ -500,6 +612,10 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 // event behind them now, queues more work, and later waits on the event and
 // reads the mirror -- no copy
 int mirror_begin(kano_ctx* ctx) {
+  // the host waits on this event: it is recorded outside any graph (an event
+  // recorded during a capture only orders the graph's own nodes)
+  SegPause pause(ctx);
+  KTRY(pause.rc);
   KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
   return 0;
 }
@@ -1095,6 +1211,10 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
   if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
+  // the matrix write and its timing events are issued directly (the events
+  // time k_rows for the bench's roofline); what was recorded before goes first
+  SegPause pause(ctx);
+  KTRY(pause.rc);
   // the matrix write saturates HBM and starves kernels beside it (measured:
   // overlapping it with the checks on stream2 was slower), so it runs in
   // order on the main stream unless rows_overlap is set
@@ -1552,6 +1672,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
         if (k == "sidepre") ctx->side_pre = v;
+        if (k == "graphs") ctx->graphs = v;
         if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
@@ -1629,6 +1750,12 @@ int kano_create(int device, kano_ctx** out) {
 }
 
 void kano_destroy(kano_ctx* ctx) {
+  if (ctx) {
+    ctx->seg_on = false;
+    kano_rec::g_rec = nullptr;
+    for (auto& e : ctx->gcache) (void)hipGraphExecDestroy(e.second);
+    ctx->gcache.clear();
+  }
   if (!ctx) return;
   if (ctx->host_timing && ctx->ht[0] > 1)
     fprintf(stderr,
@@ -2048,6 +2175,9 @@ int kano_info(kano_ctx* ctx, int64_t* out) {
   out[KANO_INFO_UA] = ctx->cc.U;
   out[KANO_INFO_HEAVY_PATH] = ctx->heavy_path;
   out[KANO_INFO_WORK_ITEMS] = ctx->wi_total;
+  out[KANO_INFO_GRAPH_HITS] = ctx->g_hits;
+  out[KANO_INFO_GRAPH_CAPTURES] = ctx->g_captures;
+  out[KANO_INFO_GRAPH_DIRECT] = ctx->g_direct;
   return 0;
 }
 
@@ -2837,6 +2967,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   ctx->ht_wait = 0;
+  SegScope seg(ctx);
   KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr,
                     shadow_cap < 0));
   const auto t1 = clk::now();
@@ -2857,8 +2988,10 @@ int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngrou
                       int64_t sys_row, int with_shadow, uint64_t* words_dev) {
   if (!ctx) return -EINVAL;
   if (!words_dev) return fail(ctx, -EINVAL, "kano_verify_shard: words_dev is NULL");
-  return verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0,
-                      reinterpret_cast<u64*>(words_dev), with_shadow == 2);
+  SegScope seg(ctx);
+  KTRY(verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0,
+                    reinterpret_cast<u64*>(words_dev), with_shadow == 2));
+  return seg_end(ctx);     // the words must be on their way when the caller gathers
 }
 
 int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nranks,
@@ -2869,6 +3002,7 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
     return fail(ctx, -EINVAL, "kano_verify_combine: bad arguments");
   if (ctx->vs_open && ctx->vs_shadow && !shadow_count)
     return fail(ctx, -EINVAL, "kano_verify_combine: shadow_count is NULL but the shard ran policy_shadow");
+  SegScope seg(ctx);
   return verify_back(ctx, reinterpret_cast<const u64*>(gathered_dev), nranks, idx, counts,
                      shadow_pairs, shadow_cap, shadow_count);
 }

@@ -58,7 +58,7 @@ def _worker(rank, world, port, name, count_only, q):
         eng.set_groups(gid)
         x = ShardExchange(torch, (n + 63) // 64, world, dist=dist, stream=stream)
         out = []
-        for _ in range(2):    # twice: the step repeats on the same context
+        for _ in range(4):    # the step repeats on the same context (graph capture, replay)
             r = x.verify(eng, gid="stored", sys_row=0, shadow=True, count_only=count_only)
             out.append({k: (None if v is None else np.array(v, copy=True))
                         for k, v in r.items() if k != "shadow_count"})
@@ -89,7 +89,7 @@ def test_shard_exchange_across_processes(name, world, count_only):
     errs = [e for _, _, e in res if e]
     assert not errs, errs[0]
     exp = expected(name)
-    for step in range(2):
+    for step in range(4):
         pairs, total = [], 0
         for rank, out, _ in res:
             r = out[step]
