@@ -225,6 +225,9 @@ struct kano_ctx {
   // policy_shadow count-only (kano_verify with shadow_cap < 0): the grouped
   // count (k_shg_*) instead of the pair-by-pair flags
   bool vs_count_only = false;
+  int shadow_count_mode = 0; // count-only policy_shadow: 0 auto (pairwise tests up to
+                             // SH_COUNT_PAIRWISE_MAX candidate pairs, else grouped),
+                             // 1 pairwise, 2 grouped
   DBuf shg_h, shg_tkey, shg_trep, shg_slot, shg_isrep, shg_gidx, shg_gid, shg_reps, shg_sub,
       shg_err;
   DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
@@ -1673,6 +1676,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "s3prio") ctx->s3_prio = v;
         if (k == "sidepre") ctx->side_pre = v;
         if (k == "graphs") ctx->graphs = v;
+        if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
         if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
@@ -2411,7 +2415,8 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (sp.rl + 1)));
   KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, sp.nt)));
   KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
-  if (ctx->sh_items == 1) KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));   // accumulated
+  if (ctx->sh_items == 1 || ctx->vs_count_only)   // accumulated
+    KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));
   return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
 }
 
@@ -2480,10 +2485,22 @@ int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   return 0;
 }
 
+// Count-only policy_shadow tests pair by pair (k_shadow_test1 without the
+// flags: only T[c]) up to this many candidate pairs, grouped beyond: C3's
+// 5.8e7 pairs take 29 us pairwise against 5.2 ms grouped (~10^4 distinct
+// allow sets, past SHG_MAX: every class falls back), C4's ~10^10 take
+// 0.1 ms grouped (a few hundred groups).
+constexpr i64 SH_COUNT_PAIRWISE_MAX = i64(1) << 28;
+
+bool shadow_count_grouped(const kano_ctx* ctx, const ShadowPlan& sp) {
+  if (ctx->shadow_count_mode) return ctx->shadow_count_mode == 2;
+  return sp.nf > SH_COUNT_PAIRWISE_MAX;
+}
+
 // subset tests; the list-offset scans go to sb
 int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   KTRY(stage_mark(ctx, 5, st));
-  if (ctx->vs_count_only) return shadow_group_launch(ctx, sp, st);
+  if (ctx->vs_count_only && shadow_count_grouped(ctx, sp)) return shadow_group_launch(ctx, sp, st);
   if (sp.nt > 0) {
     ShadowArgs a;
     a.U = sp.U;
@@ -2496,9 +2513,9 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     a.alc = P_<int32_t>(ctx->alc);
     a.AC = P_<u64>(ctx->AC);
     a.ldC = ctx->ldC;
-    a.flags = P_<uint8_t>(ctx->flags);
+    a.flags = ctx->vs_count_only ? nullptr : P_<uint8_t>(ctx->flags);   // count only: T[c]
     a.T = P_<i64>(ctx->T);
-    if (ctx->sh_items == 1)
+    if (ctx->sh_items == 1 || ctx->vs_count_only)
       hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)(sp.nt * SH_ITEMS)), dim3(TPB), 0, st, a,
                          sp.nf, P_<i64>(ctx->tcnt));
     else

@@ -2078,7 +2078,7 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
       const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
       f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
     }
-    a.flags[t] = (uint8_t)f;
+    if (a.flags) a.flags[t] = (uint8_t)f;   // null: count only (T[c])
   }
   // T[c] += f: one atomic per wave when the wave lies in one class
   const i64 c0 = __shfl(c, 0, 64);

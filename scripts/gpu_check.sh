@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 stop_if_fatal() {  # $1 = exit code of a GPU step
   case "$1" in 0|1) return 0 ;; *) echo "fatal rc=$1, stopping"; exit "$1" ;; esac
 }
-timeout -k 10 ${T_TEST:-480} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${T_TEST:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest_rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; stop_if_fatal $rc
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke_rc=$rc"; tail -2 gpurun_out/smoke.log; stop_if_fatal $rc

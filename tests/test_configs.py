@@ -86,6 +86,8 @@ def test_config_vs_kano_py(name):
     if full_shadow:
         r = eng.verify("stored", sys_row=0, shadow=True)
         check_verify(r, exp)
+        r = eng.verify("stored", sys_row=0, shadow=True, shadow_count_only=True)
+        assert r["shadow_count"] == exp["policy_shadow"]["count"]
     else:
         r = eng.verify("stored", sys_row=0, shadow=True, shadow_count_only=True)
         check_verify(r, exp, shadow=False)
@@ -298,17 +300,21 @@ def test_rows_variants_forced(name, tune, monkeypatch):
     eng.close()
 
 
-# --- policy_shadow's count without the pairs (the grouped count) ----------
+# --- policy_shadow's count without the pairs --------------------------------
+@pytest.mark.parametrize("mode", ["shcount=0", "shcount=1", "shcount=2"])
 @pytest.mark.parametrize("name", ["C2", "s_broad_1000", "s_broad_300", "s_sparse_2000", "q_shadow",
                                   "q_wide_select", "gen_s5_10000", "gen_s4_4000"])
-def test_shadow_count_only_vs_kano_py(name, tmp_path):
-    """kano_verify's count-only policy_shadow (policies grouped by allow
-    set, one subset test per pair of groups) equals len(policy_shadow(...))
-    as kano_py computed it, whole and summed over row shards."""
+def test_shadow_count_only_vs_kano_py(name, mode, tmp_path, monkeypatch):
+    """kano_verify's count-only policy_shadow -- the pairwise subset tests
+    without the flags (shcount=1), the policies grouped by allow set with one
+    subset test per pair of groups (shcount=2), or the automatic choice --
+    equals len(policy_shadow(...)) as kano_py computed it, whole and summed
+    over row shards."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids, tables_from_cluster
     from kano.synth import make_config, objects_from_json
     from kano import model
+    monkeypatch.setenv("KANO_TUNE", mode)
     exp = expected(name)
     if name == "C2":
         t = tables_from_cluster(make_config("C2"))
