@@ -83,7 +83,8 @@ struct SideMatch {
 // counters) and read by the host with one copy per sync
 enum {
   SZ_UR = 0, SZ_UA, SZ_NNZ_SEL, SZ_NNZ_ALC, SZ_NNZ_ALW, SZ_NFLAGS, SZ_WI, SZ_HEAVY, SZ_MAXSEL,
-  SZ_LIGHT, SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 17
+  SZ_LIGHT, SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 17,
+  SZ_SIGNAL = SZ_SLOTS   // host mirror only: the scans' host signal word
 };
 
 struct kano_ctx {
@@ -235,8 +236,25 @@ struct kano_ctx {
   u64* ghost = nullptr;      // pinned landing buffer for the size slots
   // pinned, coherent mirror of the size slots that the scans write directly
   // (slot-indexed): the overlapped syncs wait on an event, with no copy
-  u64* gmirror = nullptr;
+  u64* gmirror = nullptr;     // SZ_SLOTS slots + the host signal word (SZ_SIGNAL)
   u64* gmirror_dev = nullptr;
+  // host signal of the scans (ScanJobs::sig_host): the overlapped syncs poll
+  // gmirror[SZ_SIGNAL] for the value the last scan with host totals raises,
+  // instead of recording and waiting on an event (knob sig=0: events)
+  int mirror_sig = 1;
+  // kano_verify's crosscheck sort folded into the build's launches (xs_on,
+  // armed by verify_front): the group ranges in k_cls_mfill, the key
+  // histogram in k_cls_vals, its scan in the join's scan, the placement in
+  // k_join_fill -- four launches fewer (knob xfuse=0: separate launches)
+  int xfuse = 1;
+  bool xs_on = false, xs_done = false;
+  const int32_t* xs_gdev = nullptr;
+  int32_t xs_G = 0;
+  i64 xs_knb = 0, xs_kslots = 0;
+  DBuf sig_ctr;              // the scans' arrival counter (one u32, zero between launches)
+  u64 sig_seq = 0;           // last signal value handed to a scan
+  u64 sig_armed = 0;         // the value the latest scan with host totals will raise
+  u64 sig_wait = 0;          // what mirror_wait polls for (0: the event)
 
   hipEvent_t ev[10] = {};
   // the matrix write (k_rows) runs on its own stream beside the checks, which
@@ -483,6 +501,19 @@ struct ScanBatch {
   int run() {
     if (jobs.count == 0) return 0;
     KTRY(scan_reserve(ctx, slots));
+    // the host signal: raised once every host mirror of this launch is written
+    int writers = jobs.npub > 0 ? 1 : 0;
+    for (int q = 0; q < jobs.count; ++q) writers += jobs.j[q].total_host ? 1 : 0;
+    jobs.sig_host = nullptr;
+    if (writers > 0 && ctx->mirror_sig && !ctx->graphs && ctx->sig_ctr.p) {
+      jobs.sig_host = ctx->gmirror_dev + SZ_SIGNAL;
+      jobs.sig_val = ++ctx->sig_seq;
+      jobs.sig_ctr = reinterpret_cast<uint32_t*>(ctx->sig_ctr.p);
+      jobs.sig_n = writers;
+      ctx->sig_armed = jobs.sig_val;
+    } else if (writers > 0) {
+      ctx->sig_armed = 0;
+    }
     u64* st = P_<u64>(ctx->scan_tmp);
     u64* cur = st + (ctx->scan_parity ? ctx->scan_cap : 0);
     u64* nxt = st + (ctx->scan_parity ? 0 : ctx->scan_cap);
@@ -615,6 +646,13 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 // event behind them now, queues more work, and later waits on the event and
 // reads the mirror -- no copy
 int mirror_begin(kano_ctx* ctx) {
+  // the latest scan with host totals raises the host signal: nothing to queue
+  if (ctx->sig_armed) {
+    ctx->sig_wait = ctx->sig_armed;
+    ctx->sig_armed = 0;
+    return 0;
+  }
+  ctx->sig_wait = 0;
   // the host waits on this event: it is recorded outside any graph (an event
   // recorded during a capture only orders the graph's own nodes)
   SegPause pause(ctx);
@@ -623,9 +661,33 @@ int mirror_begin(kano_ctx* ctx) {
   return 0;
 }
 
+// poll the host signal word; past a second (a slow device, a failed
+// launch) the stream's own synchronisation decides
+int wait_signal(kano_ctx* ctx, u64 val) {
+  KTRY(seg_cut(ctx));
+  volatile u64* sig = ctx->gmirror + SZ_SIGNAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1; *sig != val; ++spin) {
+    __builtin_ia32_pause();
+    if ((spin & 0xfff) == 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      KCHK(hipStreamSynchronize(ctx->stream));
+      if (*sig != val) return fail(ctx, -EIO, "internal: host signal not raised");
+      break;
+    }
+  }
+  return 0;
+}
+
 int mirror_wait(kano_ctx* ctx, int first, int count, i64* out) {
   const auto t0 = std::chrono::steady_clock::now();
-  KTRY(wait_event(ctx, ctx->ev_sizes));
+  if (ctx->sig_wait) {
+    const u64 v = ctx->sig_wait;
+    ctx->sig_wait = 0;
+    KTRY(wait_signal(ctx, v));
+  } else {
+    KTRY(wait_event(ctx, ctx->ev_sizes));
+  }
   if (ctx->host_timing) {
     const double w =
         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
@@ -725,6 +787,23 @@ int classify_alloc2(kano_ctx* ctx, ClassSet& cs) {
   return dalloc(ctx, cs.cval, sizeof(int32_t) * std::max<i64>(1, (i64)cs.KS * cs.U));
 }
 
+// the fused crosscheck sort's arguments (nb = 0 when it is not armed)
+KeySort xs_sort(kano_ctx* ctx) {
+  KeySort k{};
+  if (!ctx->xs_on) return k;
+  k.U = ctx->rc.U;
+  k.nb = ctx->xs_knb;
+  k.mcnt = P_<int32_t>(ctx->rc.mcnt);
+  k.gmin = P_<int32_t>(ctx->gmin);
+  k.gmax = P_<int32_t>(ctx->gmax);
+  k.G = ctx->xs_G;
+  k.ckey = P_<int32_t>(ctx->ckey);
+  k.hist = P_<int32_t>(ctx->kcnt) + 2 * ((i64)ctx->xs_G + 1);
+  k.hoff = P_<int32_t>(ctx->koff);
+  k.order = P_<int32_t>(ctx->corder);
+  return k;
+}
+
 // phase 2a, both sides, without the class counts (the host reads them
 // meanwhile): ids, member counts, their offsets (scanned over the side's pod
 // count; the entries past U are zero), member lists of pods [m0, m1)
@@ -741,7 +820,12 @@ int classify_phase2a(kano_ctx* ctx) {
   KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ma, P_<int32_t>(ctx->cc.moff)));
   KTRY(sb.run());
   if (rl > 0) {
-    hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
+    const bool x = ctx->xs_on;
+    hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr,
+                       x ? ctx->xs_gdev : (const int32_t*)nullptr, ctx->xs_G,
+                       x ? P_<int32_t>(ctx->gmin) : (int32_t*)nullptr,
+                       x ? P_<int32_t>(ctx->gmax) : (int32_t*)nullptr,
+                       reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR));
     KLAUNCH();
   }
   return 0;
@@ -753,7 +837,7 @@ int classify_phase2b(kano_ctx* ctx) {
   const i64 U = std::max(ctx->rc.U, ctx->cc.U);
   if (U > 0) {
     hipLaunchKernelGGL(k_cls_vals, dim3(nblk(U), 2), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->pv), ctx->n, pr);
+                       P_<int32_t>(ctx->pv), ctx->n, pr, xs_sort(ctx));
     KLAUNCH();
   }
   return 0;
@@ -823,6 +907,10 @@ int match_both(kano_ctx* ctx) {
   const i64 maxU = std::max(a0.live ? a0.U : 0, a1.live ? a1.U : 0);
   const unsigned rows_i = (a0.live ? a0.NM : 0) + (a1.live ? a1.NM : 0);
   const unsigned rows_f = (a0.live ? a0.NM + 1 : 0) + (a1.live ? a1.NM + 1 : 0);
+  // the fused crosscheck sort: its histogram (k_cls_vals) is scanned with
+  // the join's group counts, its placement is k_join_fill's last grid row
+  KeySort ks = xs_sort(ctx);
+  bool hist_scanned = false;
   if (rows_i > 0) {
     hipLaunchKernelGGL(k_join_insert, dim3(nblk(maxU), rows_i), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
@@ -832,10 +920,27 @@ int match_both(kano_ctx* ctx) {
       if (pr.s[q].live && sx.NM > 0)
         KTRY(sb.add(P_<int32_t>(sx.gcnt), (i64)sx.NM * sx.T, P_<int32_t>(sx.goff)));
     }
+    if (ks.nb > 0) {
+      KTRY(sb.add(ks.hist, ctx->xs_kslots, P_<int32_t>(ctx->koff)));
+      hist_scanned = true;
+    }
     KTRY(sb.run());
   }
+  if (ks.nb > 0 && !hist_scanned) {
+    ScanBatch sb(ctx);
+    KTRY(sb.add(ks.hist, ctx->xs_kslots, P_<int32_t>(ctx->koff)));
+    KTRY(sb.run());
+  }
+  const bool place = ks.nb > 0 && rows_f > 0 && nblk(maxU) >= ks.nb;
+  if (ks.nb > 0 && !place) {
+    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)ks.nb), dim3(TPB), 0, ctx->stream, ks);
+    KLAUNCH();
+  }
+  if (ks.nb > 0) ctx->xs_done = true;
+  if (!place) ks.nb = 0;
   if (rows_f > 0) {
-    hipLaunchKernelGGL(k_join_fill, dim3(nblk(maxU), rows_f), dim3(TPB), 0, ctx->stream, pr);
+    hipLaunchKernelGGL(k_join_fill, dim3(nblk(maxU), rows_f + (place ? 1 : 0)), dim3(TPB), 0,
+                       ctx->stream, pr, ks);
     KLAUNCH();
     hipLaunchKernelGGL(k_join_match, dim3(nblk(ctx->P), 2), dim3(TPB), 0, ctx->stream, ctx->P, pr);
     KLAUNCH();
@@ -891,6 +996,13 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
     KTRY(fb.add(ctx->sizes, sizeof(u64) * SZ_SLOTS, 0u));
     KTRY(classify_alloc1(ctx, ctx->rc, fb));
     KTRY(classify_alloc1(ctx, ctx->cc, fb));
+    if (ctx->xs_on) {   // group ranges per row class (k_cls_mfill), <= one per local pod
+      const i64 m = std::max<i64>(1, ctx->rc.m1 - ctx->rc.m0);
+      KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * m));
+      KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * m));
+      KTRY(fb.add(ctx->gmin, sizeof(int32_t) * m, 0x7fffffffu));
+      KTRY(fb.add(ctx->gmax, sizeof(int32_t) * m, 0xffffffffu));
+    }
     KTRY(fb.run());
   }
   KTRY(classify_phase1(ctx));
@@ -928,6 +1040,15 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
     KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (Ur + 1)));
     KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
+    if (ctx->xs_on) {   // the fused crosscheck sort's buffers (as cross_prepare sizes them)
+      const i64 G = ctx->xs_G;
+      ctx->xs_knb = std::max<i64>(1, nblk(Ur, (i64)TPB * KEY_ITEMS));
+      ctx->xs_kslots = (G + 1) * ctx->xs_knb;
+      KTRY(dalloc(ctx, ctx->ckey, sizeof(int32_t) * std::max<i64>(1, Ur)));
+      KTRY(dalloc(ctx, ctx->corder, sizeof(int32_t) * std::max<i64>(1, Ur)));
+      KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * (G + 1) + sizeof(int32_t) * ctx->xs_kslots));
+      KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * (ctx->xs_kslots + 1)));
+    }
     KTRY(fb.run());
   }
   if (side) {   // the size-independent back-end work, beside the join (stream2)
@@ -1402,16 +1523,12 @@ struct CrossPlan {
   i64 knb = 0, kslots = 0;
 };
 
-// host checks, group upload, allocations; fills go to fb
-int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp,
-                  FillBatch& fb) {
+// host checks, group upload (no fills): cp.on, cp.gdev, cp.G
+int cross_setup(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
   KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
-  int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
-  KTRY(fb.add_raw(err, sizeof(u64), 0u));
-  KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
   cp.on = false;
   if (n == 0 || rows_local(ctx) == 0 || W == 0) return 0;
   int32_t G = ngroups;
@@ -1433,6 +1550,21 @@ int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan&
   }
   cp.G = G;
   cp.on = true;
+  return 0;
+}
+
+// cross_setup (unless done), allocations; fills go to fb.  With the fused
+// sort (ctx->xs_on) the build has filled gmin / gmax, found the group ranges
+// and may have flagged the error slot already: those fills are skipped.
+int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp,
+                  FillBatch& fb, bool setup_done = false) {
+  const i64 ldM = ctx->ldM;
+  if (!setup_done) KTRY(cross_setup(ctx, gid, ngroups, cp));
+  int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
+  if (!ctx->xs_on) KTRY(fb.add_raw(err, sizeof(u64), 0u));
+  KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
+  if (!cp.on) return 0;
+  const int32_t G = cp.G;
   if (ctx->rows_dirty) return 0;   // the M-based path allocates its own
   const i64 U = ctx->rc.U, ldC = ctx->ldC;
   KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * std::max<i64>(1, U)));
@@ -1448,8 +1580,10 @@ int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan&
   KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
   KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
   KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
-  KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
-  KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
+  if (!ctx->xs_on) {
+    KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
+    KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
+  }
   KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
   for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
   KTRY(fb.add(ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1), 0u));   // counts + cursors
@@ -1458,11 +1592,28 @@ int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan&
 
 // group range per class, group keys and their histogram; the key scan job
 // goes to sb
+KeySort cross_sort(kano_ctx* ctx, const CrossPlan& cp) {
+  KeySort k{};
+  k.U = ctx->rc.U;
+  k.nb = cp.knb;
+  k.mcnt = P_<int32_t>(ctx->rc.mcnt);
+  k.gmin = P_<int32_t>(ctx->gmin);
+  k.gmax = P_<int32_t>(ctx->gmax);
+  k.G = cp.G;
+  k.ckey = P_<int32_t>(ctx->ckey);
+  k.hist = P_<int32_t>(ctx->kcnt) + 2 * ((i64)cp.G + 1);
+  k.hoff = P_<int32_t>(ctx->koff);
+  k.order = P_<int32_t>(ctx->corder);
+  return k;
+}
+
 int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
   if (!cp.on) return 0;
   const i64 U = ctx->rc.U, G = cp.G, rl = rows_local(ctx);
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
-  if (ctx->grange_m)
+  if (ctx->xs_on) {
+    // (k_cls_mfill found the group ranges)
+  } else if (ctx->grange_m)
     hipLaunchKernelGGL(k_cls_group_range_m, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
                        (int32_t)G, P_<int32_t>(ctx->rc.cls), P_<int32_t>(ctx->rc.mem), rl,
                        P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
@@ -1473,12 +1624,10 @@ int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
   KLAUNCH();
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {   // classes in group order: per-block LDS histograms
-    int32_t* hist = kcnt + 2 * (G + 1);
-    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, U,
-                       P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
-                       (int32_t)G, P_<int32_t>(ctx->ckey), hist);
+    const KeySort ks = cross_sort(ctx, cp);
+    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, ks);
     KLAUNCH();
-    KTRY(sb.add(hist, cp.kslots, P_<int32_t>(ctx->koff)));
+    KTRY(sb.add(ks.hist, cp.kslots, P_<int32_t>(ctx->koff)));
   } else {
     hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
                        P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
@@ -1496,9 +1645,8 @@ int cross_stage_b1(kano_ctx* ctx, const CrossPlan& cp) {
   const i64 U = ctx->rc.U, G = cp.G;
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {
-    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, U,
-                       P_<int32_t>(ctx->ckey), (int32_t)G, P_<int32_t>(ctx->koff),
-                       P_<int32_t>(ctx->corder));
+    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream,
+                       cross_sort(ctx, cp));
   } else {
     hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
                        P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
@@ -1676,6 +1824,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "s3prio") ctx->s3_prio = v;
         if (k == "sidepre") ctx->side_pre = v;
         if (k == "graphs") ctx->graphs = v;
+        if (k == "sig") ctx->mirror_sig = v;
+        if (k == "xfuse") ctx->xfuse = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
         if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
@@ -1741,14 +1891,19 @@ int kano_create(int device, kano_ctx** out) {
     kano_destroy(ctx);
     return -ENOMEM;
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->gmirror), sizeof(u64) * SZ_SLOTS,
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->gmirror), sizeof(u64) * (SZ_SIGNAL + 1),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->gmirror_dev), ctx->gmirror, 0) !=
           hipSuccess) {
     kano_destroy(ctx);
     return -ENOMEM;
   }
-  for (int k = 0; k < SZ_SLOTS; ++k) ctx->gmirror[k] = 0;
+  for (int k = 0; k <= SZ_SIGNAL; ++k) ctx->gmirror[k] = 0;
+  if (dalloc(ctx, ctx->sig_ctr, sizeof(uint32_t) * 4) != 0 ||
+      hipMemset(ctx->sig_ctr.p, 0, sizeof(uint32_t) * 4) != hipSuccess) {
+    kano_destroy(ctx);
+    return -ENOMEM;
+  }
   *out = ctx;
   return 0;
 }
@@ -1792,7 +1947,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->aloff,  &ctx->alist,   &ctx->M,       &ctx->Mc,        &ctx->color,
                   &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp, &ctx->scan_tmp_side,
                   &ctx->shg_h,  &ctx->shg_tkey, &ctx->shg_trep, &ctx->shg_slot, &ctx->shg_isrep,
-                  &ctx->shg_gidx, &ctx->shg_gid, &ctx->shg_reps, &ctx->shg_sub, &ctx->shg_err,
+                  &ctx->shg_gidx, &ctx->shg_gid, &ctx->shg_reps, &ctx->shg_sub, &ctx->shg_err, &ctx->sig_ctr,
                   &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
                   &ctx->A2,     &ctx->own,     &ctx->cross,   &ctx->gmin,      &ctx->gmax,
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
@@ -2114,6 +2269,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->rows_dirty = false;
   ctx->cols_valid = false;
   ctx->shadow_total = -1;
+  ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
   const i64 rl = rows_local(ctx);
   if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
     KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over));
@@ -2720,13 +2876,26 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // fill launch
   CrossPlan cp;
   ShadowPlan sp;
-  // the crosscheck's fills and its group-key sort need only the class
-  // counts: they run while the list sizes travel (build sync 2)
+  // the crosscheck's group-key sort rides on the build's launches (xs_on):
+  // the groups go up first, the build's kernels do the rest
+  bool setup_done = false;
+  ctx->xs_on = ctx->xs_done = false;
+  if (want_cross && ctx->xfuse && ctx->grange_m && !ctx->side_pre) {
+    KTRY(cross_setup(ctx, gid, ngroups, cp));
+    setup_done = true;
+    if (cp.on && (i64)cp.G + 1 <= KEY_LDS_MAX) {
+      ctx->xs_on = true;
+      ctx->xs_gdev = cp.gdev;
+      ctx->xs_G = cp.G;
+    }
+  }
+  // the crosscheck's fills (and, unfused, its group-key sort) need only the
+  // class counts: they run while the list sizes travel (build sync 2)
   auto pre_fill = [&](FillBatch& fb) -> int {
-    return want_cross ? cross_prepare(ctx, gid, ngroups, cp, fb) : 0;
+    return want_cross ? cross_prepare(ctx, gid, ngroups, cp, fb, setup_done) : 0;
   };
   auto pre_run = [&]() -> int {
-    if (!want_cross || !cp.on) return 0;
+    if (!want_cross || !cp.on || ctx->xs_done) return 0;
     ScanBatch sb(ctx);
     KTRY(cross_stage_a(ctx, cp, sb));
     KTRY(sb.run());
@@ -2766,6 +2935,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   const int brc = build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run);
   ctx->fork_hook = nullptr;
   ctx->rows_hook = nullptr;
+  ctx->xs_on = false;
   KTRY(brc);
   // the matrix write needs only the lists: with rows_early it starts here on
   // stream2, beside the class-level checks
@@ -2889,6 +3059,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
                 SZ_IDX0 + r));
   sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
+  if (want_shadow) sb.publish(SZ_NL);   // (an earlier scan's total: one host signal for all)
   KTRY(sb.run());
   IdxRows ir{};
   ir.W = W;

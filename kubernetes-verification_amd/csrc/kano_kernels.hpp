@@ -41,6 +41,62 @@ struct ClsPair {
   ClsSide s[2];
 };
 
+// ---- user_crosscheck's group keys (a counting sort of the row classes) -----
+// Key of row class c: g when all its local members are in group g, G when
+// they mix groups (MULTI), -1 without local members.  Small key spaces
+// (G + 1 <= KEY_LDS_MAX): per-block histograms in LDS, no global atomics;
+// hist is bin-major, hist[k * nb + b], so its exclusive scan (hoff) is every
+// (bin, block) start.  Block b covers classes [b, b + 1) * TPB * KEY_ITEMS.
+// Standalone (k_key_hist, k_key_place_lds) or fused into k_cls_vals and
+// k_join_fill (kano_verify: two launches and a scan fewer).
+constexpr int KEY_LDS_MAX = 8192;
+constexpr int KEY_ITEMS = 8;   // classes per thread
+struct KeySort {
+  i64 U;                 // row classes
+  i64 nb;                // blocks of the sort (0: none)
+  const int32_t* mcnt;
+  const int32_t* gmin;
+  const int32_t* gmax;
+  int32_t G;
+  int32_t* ckey;
+  int32_t* hist;
+  const int32_t* hoff;
+  int32_t* order;
+};
+
+// (block-uniform: every thread of the block calls it)
+__device__ __forceinline__ void key_hist_block(const KeySort& k, i64 b) {
+  __shared__ int32_t h[KEY_LDS_MAX];
+  const int nk = k.G + 1;
+  for (int q = threadIdx.x; q < nk; q += TPB) h[q] = 0;
+  __syncthreads();
+  const i64 c0 = b * TPB * KEY_ITEMS;
+  for (int q = 0; q < KEY_ITEMS; ++q) {
+    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
+    if (c >= k.U) break;
+    int32_t key = -1;
+    if (k.mcnt[c] > 0 && k.gmin[c] <= k.gmax[c]) key = k.gmin[c] == k.gmax[c] ? k.gmin[c] : k.G;
+    k.ckey[c] = key;
+    if (key >= 0) atomicAdd(&h[key], 1);
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < nk; q += TPB) k.hist[(i64)q * k.nb + b] = h[q];
+}
+
+__device__ __forceinline__ void key_place_block(const KeySort& k, i64 b) {
+  __shared__ int32_t h[KEY_LDS_MAX];
+  const int nk = k.G + 1;
+  for (int q = threadIdx.x; q < nk; q += TPB) h[q] = k.hoff[(i64)q * k.nb + b];
+  __syncthreads();
+  const i64 c0 = b * TPB * KEY_ITEMS;
+  for (int q = 0; q < KEY_ITEMS; ++q) {
+    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
+    if (c >= k.U) break;
+    const int32_t key = k.ckey[c];
+    if (key >= 0) k.order[atomicAdd(&h[key], 1)] = (int32_t)c;
+  }
+}
+
 // Block-level combining (the packed mode): the block's pods first meet in an
 // LDS table keyed by the packed tuple, so only one thread per distinct tuple
 // per block probes the global table and posts the block's smallest member to
@@ -241,22 +297,41 @@ __global__ __launch_bounds__(TPB) void k_cls_mcount(ClsPair pr) {
   (void)wave_agg_inc(a.mcnt, act ? a.cls[i] : 0, act);
 }
 
-// member lists: pod i at its rank (from k_cls_assign_count) in its class
-__global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr) {
+// member lists: pod i at its rank (from k_cls_assign_count) in its class.
+// With gid (kano_verify's crosscheck), the row side also folds the group
+// range of every row class (gmin / gmax: k_cls_group_range's work, one
+// launch fewer); a group id outside [0, G) sets *err.
+__global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr, const int32_t* __restrict__ gid,
+                                                   int32_t G, int32_t* gmin, int32_t* gmax,
+                                                   int32_t* err) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= a.m1) return;
-  a.mem[a.moff[a.cls[i]] + a.mcur[i - a.m0]] = (int32_t)i;
+  const bool act = i < a.m1;
+  const int32_t c = act ? a.cls[i] : 0;
+  if (act) a.mem[a.moff[c] + a.mcur[i - a.m0]] = (int32_t)i;
+  if (blockIdx.y == 0 && gid) {                    // block-uniform
+    int32_t g = act ? gid[i] : 0;
+    bool ok = act;
+    if (act && (g < 0 || g >= G)) {                // caller-declared group count violated
+      atomicOr(err, 1);
+      ok = false;
+    }
+    wave_agg_minmax(gmin, gmax, c, g, ok);
+  }
 }
 
 // key values of each class's representative, slot-major: cval[k * U + c]
+// (ks.nb > 0: the row side's first ks.nb blocks also run the group-key
+// histogram, k_key_hist's work)
 __global__ __launch_bounds__(TPB) void k_cls_vals(const int32_t* __restrict__ pv, i64 n,
-                                                  ClsPair pr) {
+                                                  ClsPair pr, KeySort ks) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c >= a.U) return;
-  const int32_t r = a.rep[c];
-  for (int k = 0; k < a.KS; ++k) a.cval[(i64)k * a.U + c] = pv[(i64)a.keys[k] * n + r];
+  if (c < a.U) {
+    const int32_t r = a.rep[c];
+    for (int k = 0; k < a.KS; ++k) a.cval[(i64)k * a.U + c] = pv[(i64)a.keys[k] * n + r];
+  }
+  if (blockIdx.y == 0 && (i64)blockIdx.x < ks.nb) key_hist_block(ks, blockIdx.x);
 }
 
 // ===========================================================================
@@ -489,7 +564,13 @@ __global__ __launch_bounds__(TPB) void k_join_count(JoinPair pr) {
 
 // grouped class lists; the extra row per side writes the iota block (the
 // class list of policies without terms)
-__global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr) {
+// (ks.nb > 0: the grid's last row places the row classes by group key,
+// k_key_place_lds's work, its first ks.nb blocks)
+__global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr, KeySort ks) {
+  if (ks.nb > 0 && blockIdx.y == gridDim.y - 1) {   // block-uniform
+    if ((i64)blockIdx.x < ks.nb) key_place_block(ks, blockIdx.x);
+    return;
+  }
   int m;
   const JoinSide a = join_row(pr, blockIdx.y, 1, &m) ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
@@ -1109,50 +1190,10 @@ __global__ __launch_bounds__(TPB) void k_cls_key_place(i64 U, const int32_t* __r
   if (key >= 0) order[koff[key] + r] = (int32_t)c;
 }
 
-// Small key spaces (G + 1 <= KEY_LDS_MAX): a stable-free counting sort with
-// per-block histograms in LDS, no global atomics.  hist is bin-major,
-// hist[k * nb + b], so its exclusive scan is every (bin, block) start.
-constexpr int KEY_LDS_MAX = 8192;
-constexpr int KEY_ITEMS = 8;   // classes per thread
-__global__ __launch_bounds__(TPB) void k_key_hist(i64 U, const int32_t* __restrict__ mcnt,
-                                                  const int32_t* __restrict__ gmin,
-                                                  const int32_t* __restrict__ gmax, int32_t G,
-                                                  int32_t* __restrict__ ckey,
-                                                  int32_t* __restrict__ hist) {
-  __shared__ int32_t h[KEY_LDS_MAX];
-  const int nk = G + 1;
-  const i64 nb = gridDim.x;
-  for (int k = threadIdx.x; k < nk; k += TPB) h[k] = 0;
-  __syncthreads();
-  const i64 c0 = (i64)blockIdx.x * TPB * KEY_ITEMS;
-  for (int q = 0; q < KEY_ITEMS; ++q) {
-    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
-    if (c >= U) break;
-    int32_t key = -1;
-    if (mcnt[c] > 0 && gmin[c] <= gmax[c]) key = gmin[c] == gmax[c] ? gmin[c] : G;
-    ckey[c] = key;
-    if (key >= 0) atomicAdd(&h[key], 1);
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < nk; k += TPB) hist[(i64)k * nb + blockIdx.x] = h[k];
-}
-
-__global__ __launch_bounds__(TPB) void k_key_place_lds(i64 U, const int32_t* __restrict__ ckey,
-                                                       int32_t G,
-                                                       const int32_t* __restrict__ hoff,
-                                                       int32_t* __restrict__ order) {
-  __shared__ int32_t h[KEY_LDS_MAX];
-  const int nk = G + 1;
-  const i64 nb = gridDim.x;
-  for (int k = threadIdx.x; k < nk; k += TPB) h[k] = hoff[(i64)k * nb + blockIdx.x];
-  __syncthreads();
-  const i64 c0 = (i64)blockIdx.x * TPB * KEY_ITEMS;
-  for (int q = 0; q < KEY_ITEMS; ++q) {
-    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
-    if (c >= U) break;
-    const int32_t key = ckey[c];
-    if (key >= 0) order[atomicAdd(&h[key], 1)] = (int32_t)c;
-  }
+// the standalone launches of the group-key sort (KeySort above): grid = nb
+__global__ __launch_bounds__(TPB) void k_key_hist(KeySort k) { key_hist_block(k, blockIdx.x); }
+__global__ __launch_bounds__(TPB) void k_key_place_lds(KeySort k) {
+  key_place_block(k, blockIdx.x);
 }
 
 // One pass over Mc in group order: R[g] |= Mc[c] (g = key), MULTI for key G;
@@ -1646,7 +1687,6 @@ __device__ __forceinline__ void build_light_row(const RowsArgs& a, i64 c, i64 ba
 // k_rows; b = work item index.  Returns uniformly for the whole block.
 template <int NT>
 __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
-  constexpr int NW = NT / 64;
   const i64 c = a.wicls ? (i64)a.wicls[b] : upper_bound_i32(a.wioff, a.U + 1, b) - 1;
   if (c < 0 || c >= a.U) return;
   const i64 chunk = b - a.wioff[c];

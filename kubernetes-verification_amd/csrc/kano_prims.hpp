@@ -160,7 +160,29 @@ struct ScanJobs {
   int npub;
   const u64* pub_src[MAX_PUBLISH];
   u64* pub_dst[MAX_PUBLISH];
+  // host signal (nullable): after the sig_n writers of host mirrors (one per
+  // job with total_host, one for the publish list) have stored their values,
+  // the last of them stores sig_val to *sig_host -- the host polls that word
+  // instead of waiting on an event (an event record costs the stream ~6 us)
+  u64* sig_host;
+  u64 sig_val;
+  uint32_t* sig_ctr;   // arrivals (zero between launches: the last arrival resets it)
+  int sig_n;
 };
+
+// one writer of host mirrors is done: its stores are made visible system-wide
+// before it counts itself; the last writer raises the host signal
+__device__ __forceinline__ void scan_sig_arrive(const ScanJobs& jobs) {
+  if (!jobs.sig_host) return;
+  __threadfence_system();
+  const uint32_t old =
+      __hip_atomic_fetch_add(jobs.sig_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 == (uint32_t)jobs.sig_n) {
+    __hip_atomic_store(jobs.sig_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence_system();
+    __hip_atomic_store(jobs.sig_host, jobs.sig_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
                                                  u64* __restrict__ clear, i64 nclear) {
@@ -170,8 +192,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
   const i64 lin = (i64)blockIdx.y * gridDim.x + blockIdx.x;
   const i64 nthr = (i64)gridDim.x * gridDim.y * TPB;
   for (i64 i = lin * TPB + threadIdx.x; i < nclear; i += nthr) clear[i] = 0;
-  if (lin == 0 && threadIdx.x == 0)
+  if (lin == 0 && threadIdx.x == 0 && jobs.npub > 0) {
     for (int q = 0; q < jobs.npub; ++q) *jobs.pub_dst[q] = *jobs.pub_src[q];
+    scan_sig_arrive(jobs);
+  }
   ScanJob jb = jobs.j[0];   // select, not a dynamic index (kernarg stays in SGPRs)
 #pragma unroll
   for (int q = 1; q < MAX_SCAN_JOBS; ++q)
@@ -182,7 +206,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       if (jb.out64) static_cast<i64*>(jb.out)[0] = 0;
       else static_cast<int32_t*>(jb.out)[0] = 0;
       if (jb.total) *jb.total = 0;
-      if (jb.total_host) *jb.total_host = 0;
+      if (jb.total_host) {
+        *jb.total_host = 0;
+        scan_sig_arrive(jobs);
+      }
     }
     return;
   }
@@ -245,7 +272,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
     if (tile == tiles - 1 && threadIdx.x == TPB - 1) {
       o[jb.n] = pre;
       if (jb.total) *jb.total = (u64)pre;
-      if (jb.total_host) *jb.total_host = (u64)pre;
+      if (jb.total_host) {
+        *jb.total_host = (u64)pre;
+        scan_sig_arrive(jobs);
+      }
     }
   } else {
     int32_t* o = static_cast<int32_t*>(jb.out);
@@ -257,7 +287,10 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
     if (tile == tiles - 1 && threadIdx.x == TPB - 1) {
       o[jb.n] = (int32_t)pre;
       if (jb.total) *jb.total = (u64)pre;
-      if (jb.total_host) *jb.total_host = (u64)pre;
+      if (jb.total_host) {
+        *jb.total_host = (u64)pre;
+        scan_sig_arrive(jobs);
+      }
     }
   }
 }
