@@ -226,9 +226,9 @@ struct kano_ctx {
   // policy_shadow count-only (kano_verify with shadow_cap < 0): the grouped
   // count (k_shg_*) instead of the pair-by-pair flags
   bool vs_count_only = false;
-  int shadow_count_mode = 0; // count-only policy_shadow: 0 auto (pairwise tests up to
-                             // SH_COUNT_PAIRWISE_MAX candidate pairs, else grouped),
+  int shadow_count_mode = 0; // count-only policy_shadow: 0 the device picks (shg_grouped),
                              // 1 pairwise, 2 grouped
+  bool shg_ran = false;      // the grouped count was queued (its G / err exist)
   DBuf shg_h, shg_tkey, shg_trep, shg_slot, shg_isrep, shg_gidx, shg_gid, shg_reps, shg_sub,
       shg_err;
   DBuf sizes;                // SZ_* slots: list sizes the host reads at its syncs
@@ -245,8 +245,9 @@ struct kano_ctx {
   // kano_verify's crosscheck sort folded into the build's launches (xs_on,
   // armed by verify_front): the group ranges in k_cls_mfill, the key
   // histogram in k_cls_vals, its scan in the join's scan, the placement in
-  // k_join_fill -- four launches fewer (knob xfuse=0: separate launches)
-  int xfuse = 1;
+  // k_join_fill -- four launches fewer (knob xfuse; off by default: measured
+  // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
+  int xfuse = 0;
   bool xs_on = false, xs_done = false;
   const int32_t* xs_gdev = nullptr;
   int32_t xs_G = 0;
@@ -645,9 +646,16 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 // (totals) or by a scan's publish list (atomic slots); the host records an
 // event behind them now, queues more work, and later waits on the event and
 // reads the mirror -- no copy
-int mirror_begin(kano_ctx* ctx) {
+// order: also record ev_sizes here for other streams to wait on (the host
+// itself may poll the signal)
+int mirror_begin(kano_ctx* ctx, bool order = false) {
   // the latest scan with host totals raises the host signal: nothing to queue
   if (ctx->sig_armed) {
+    if (order) {
+      SegPause pause(ctx);
+      KTRY(pause.rc);
+      KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
+    }
     ctx->sig_wait = ctx->sig_armed;
     ctx->sig_armed = 0;
     return 0;
@@ -2579,6 +2587,7 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
 // the grouped count (count-only policy_shadow): T[c] per row class
 int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   const i64 P = ctx->P, U = sp.U;
+  ctx->shg_ran = false;
   if (P == 0 || U == 0) return 0;
   i64 Th = 64;
   while (Th < 2 * P) Th <<= 1;
@@ -2617,11 +2626,13 @@ int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
                      P_<int32_t>(ctx->shg_reps));
   KLAUNCH();
   const int32_t* Gp = P_<int32_t>(ctx->shg_gidx) + P;
+  const u64* nfp = P_<u64>(ctx->sizes) + SZ_NFLAGS;
+  const int force = ctx->shadow_count_mode == 2 ? 2 : 0;
   hipLaunchKernelGGL(k_shg_sub, dim3(nblk(std::min<i64>(P, SHG_MAX), WPB)), dim3(TPB), 0, st, Gp,
                      P_<int32_t>(ctx->shg_reps), AC, ctx->ldC, ctx->UAW, P_<u64>(ctx->shg_sub),
-                     GW);
+                     GW, P_<int32_t>(ctx->shg_err), nfp, force);
   KLAUNCH();
-  ShadowArgs a;
+  ShadowArgs a{};
   a.U = U;
   a.soffc = P_<i64>(ctx->soffc);
   a.slist = P_<int32_t>(ctx->slist);
@@ -2634,31 +2645,35 @@ int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   a.ldC = ctx->ldC;
   a.flags = nullptr;
   a.T = P_<i64>(ctx->T);
+  a.shg_nf = nfp;
+  a.shg_force = force;
   hipLaunchKernelGGL(k_shg_count, dim3((unsigned)U), dim3(TPB), 0, st, a,
                      P_<int32_t>(ctx->shg_gid), Gp, P_<u64>(ctx->shg_sub), GW,
                      P_<int32_t>(ctx->shg_err));
   KLAUNCH();
+  ctx->shg_ran = true;
   return 0;
 }
 
-// Count-only policy_shadow tests pair by pair (k_shadow_test1 without the
-// flags: only T[c]) up to this many candidate pairs, grouped beyond: C3's
-// 5.8e7 pairs take 29 us pairwise against 5.2 ms grouped (~10^4 distinct
-// allow sets, past SHG_MAX: every class falls back), C4's ~10^10 take
-// 0.1 ms grouped (a few hundred groups).
-constexpr i64 SH_COUNT_PAIRWISE_MAX = i64(1) << 28;
+constexpr i64 SH_YIELD_GRID = 8192;   // 32 blocks per CU
 
-bool shadow_count_grouped(const kano_ctx* ctx, const ShadowPlan& sp) {
-  if (ctx->shadow_count_mode) return ctx->shadow_count_mode == 2;
-  return sp.nf > SH_COUNT_PAIRWISE_MAX;
-}
-
-// subset tests; the list-offset scans go to sb
+// subset tests; the list-offset scans go to sb.  Count only: the grouped
+// count and the flag-free pairwise test are both queued, the device picks
+// one (shg_grouped) once the allow-set groups are known; knob shcount 1 / 2
+// forces the pairwise / grouped form.
 int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   KTRY(stage_mark(ctx, 5, st));
-  if (ctx->vs_count_only && shadow_count_grouped(ctx, sp)) return shadow_group_launch(ctx, sp, st);
+  const int mode = ctx->vs_count_only ? ctx->shadow_count_mode : -1;
+  ctx->shg_ran = false;
+  if (mode == 0 || mode == 2) KTRY(shadow_group_launch(ctx, sp, st));
+  if (mode == 2) return 0;
   if (sp.nt > 0) {
-    ShadowArgs a;
+    ShadowArgs a{};
+    if (mode == 0 && ctx->shg_ran) {   // the pairwise test yields to the grouped count
+      a.shg_G = P_<int32_t>(ctx->shg_gidx) + ctx->P;
+      a.shg_err = P_<int32_t>(ctx->shg_err);
+      a.shg_nf = P_<u64>(ctx->sizes) + SZ_NFLAGS;
+    }
     a.U = sp.U;
     a.soffc = P_<i64>(ctx->soffc);
     a.slist = P_<int32_t>(ctx->slist);
@@ -2671,9 +2686,13 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     a.ldC = ctx->ldC;
     a.flags = ctx->vs_count_only ? nullptr : P_<uint8_t>(ctx->flags);   // count only: T[c]
     a.T = P_<i64>(ctx->T);
+    // (one block per virtual block, or a capped striding grid when the test
+    // may yield to the grouped count)
+    const i64 nvb = sp.nt * SH_ITEMS;
+    const i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
     if (ctx->sh_items == 1 || ctx->vs_count_only)
-      hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)(sp.nt * SH_ITEMS)), dim3(TPB), 0, st, a,
-                         sp.nf, P_<i64>(ctx->tcnt));
+      hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
+                         P_<i64>(ctx->tcnt));
     else
       hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, st, a, sp.nf,
                          P_<i64>(ctx->tcnt));
@@ -3081,11 +3100,12 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // host while the matrix write runs: the host waits on the copy's event
   // only, then queues policy_shadow's emission and the copies behind k_rows
   constexpr int NS = SZ_ERR - SZ_NL + 1;
-  KTRY(mirror_begin(ctx));
   // side_tail == 2: policy_shadow's compaction and emission run on the main
   // stream before the matrix write (they crawl beside it: 60 + 40 us there
   // against 10 + 4 us alone, and slow it), the copies beside it
   const bool pre_tail = ctx->side_tail == 2 && !ctx->vs_early && want_shadow && shadow_cap >= 0;
+  // the tail on stream3 waits for everything queued so far (ev_sizes)
+  KTRY(mirror_begin(ctx, ctx->side_tail && !pre_tail));
   if (!ctx->vs_early && !pre_tail) KTRY(launch_rows(ctx));
   i64 v[NS];
   KTRY(mirror_wait(ctx, SZ_NL, NS, v));

@@ -310,13 +310,31 @@ __global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr, const int32_t* __
   const int32_t c = act ? a.cls[i] : 0;
   if (act) a.mem[a.moff[c] + a.mcur[i - a.m0]] = (int32_t)i;
   if (blockIdx.y == 0 && gid) {                    // block-uniform
-    int32_t g = act ? gid[i] : 0;
-    bool ok = act;
+    // the block's ranges meet in LDS first, then one check-before-atomic per
+    // distinct class: few, large classes (C4: ~100 for 100k pods) otherwise
+    // serialise every pod's atomics on a handful of addresses
+    __shared__ int32_t lk[CLS_LDS], lmn[CLS_LDS], lmx[CLS_LDS];
+    for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+      lk[t] = -1;
+      lmn[t] = INT32_MAX;
+      lmx[t] = INT32_MIN;
+    }
+    __syncthreads();
+    const int32_t g = act ? gid[i] : 0;
     if (act && (g < 0 || g >= G)) {                // caller-declared group count violated
       atomicOr(err, 1);
-      ok = false;
+    } else if (act) {
+      const int t = lds_class_slot(lk, c, true);   // TPB pods in 2 x TPB slots: always found
+      atomicMin(&lmn[t], g);
+      atomicMax(&lmx[t], g);
     }
-    wave_agg_minmax(gmin, gmax, c, g, ok);
+    __syncthreads();
+    for (int t = threadIdx.x; t < CLS_LDS; t += TPB) {
+      const int32_t k = lk[t];
+      if (k < 0) continue;
+      if (lmn[t] < gmin[k]) atomicMin(&gmin[k], lmn[t]);   // (a stale read only costs an atomic)
+      if (lmx[t] > gmax[k]) atomicMax(&gmax[k], lmx[t]);
+    }
   }
 }
 
@@ -2003,7 +2021,29 @@ struct ShadowArgs {
   i64 ldC;
   uint8_t* flags;
   i64* T;
+  // count only (flags null): the grouped count's verdict (shg_grouped),
+  // when set the pairwise test leaves T to it
+  const int32_t* shg_G;
+  const int32_t* shg_err;
+  const u64* shg_nf;
+  int shg_force;
 };
+
+// Count-only policy_shadow, decided on the device once the allow-set groups
+// are known: the grouped count (k_shg_sub's G^2 row compares + per class
+// m_c^2 bit tests) when G <= SHG_MAX, no hash collision and G^2 <= nf / 4
+// (nf = the pairwise candidate pairs), else the pairwise test (k_shadow_test1
+// without flags).  C3: G = 4,092, nf = 5.8e7 -> pairwise (29 us; grouped
+// 5.2 ms); C4: G = 111 -> grouped.  force 2: grouped whatever G (the count
+// falls back pair by pair per class past SHG_MAX or on a collision).
+constexpr int SHG_MAX = 4096;
+__device__ __forceinline__ bool shg_grouped(const int32_t* Gp, const int32_t* err, const u64* nfp,
+                                            int force) {
+  if (force == 2) return true;
+  const i64 G = *Gp;
+  if (*err || G > SHG_MAX) return false;
+  return (u64)(G * G) <= *nfp / 4;
+}
 
 // The candidate pairs of every row class c are (x, y) in [0, s_c)^2, laid out
 // flat at pfoff[c] (class-major, x-major).  Both kernels take SH_TILE
@@ -2100,38 +2140,46 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
                                                      i64* __restrict__ tile_cnt) {
   __shared__ i64 sm[4];
   __shared__ i64 rng[2];
-  const i64 tile = blockIdx.x / SH_ITEMS, part = blockIdx.x % SH_ITEMS;
-  const i64 b0 = tile * SH_TILE + part * TPB;
-  if (b0 >= nflags) return;                      // block-uniform
-  const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
-  if (threadIdx.x == 0) rng[0] = class_of_pair(a.pfoff, 0, a.U - 1, b0);
-  if (threadIdx.x == 64) rng[1] = class_of_pair(a.pfoff, 0, a.U - 1, b1);
-  __syncthreads();
-  const i64 t = b0 + threadIdx.x;
-  int f = 0;
-  i64 c = -1;
-  if (t < nflags) {
-    c = class_of_pair(a.pfoff, rng[0], rng[1], t);
-    const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
-    const i64 x = q / s, y = q - x * s;
-    if (a.mcnt[c] > 0 && x != y) {
-      const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
-      f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+  // count only: nothing to do when the grouped count holds (block-uniform);
+  // that launch strides over the virtual blocks with a capped grid, so that
+  // the yielding test costs little
+  if (a.shg_G && shg_grouped(a.shg_G, a.shg_err, a.shg_nf, a.shg_force)) return;
+  const i64 nvb = (nflags + SH_TILE - 1) / SH_TILE * SH_ITEMS;
+  for (i64 vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    const i64 tile = vb / SH_ITEMS, part = vb % SH_ITEMS;
+    const i64 b0 = tile * SH_TILE + part * TPB;
+    if (b0 >= nflags) break;                     // block-uniform (b0 rises with vb)
+    const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
+    if (threadIdx.x == 0) rng[0] = class_of_pair(a.pfoff, 0, a.U - 1, b0);
+    if (threadIdx.x == 64) rng[1] = class_of_pair(a.pfoff, 0, a.U - 1, b1);
+    __syncthreads();
+    const i64 t = b0 + threadIdx.x;
+    int f = 0;
+    i64 c = -1;
+    if (t < nflags) {
+      c = class_of_pair(a.pfoff, rng[0], rng[1], t);
+      const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
+      const i64 x = q / s, y = q - x * s;
+      if (a.mcnt[c] > 0 && x != y) {
+        const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
+        f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+      }
+      if (a.flags) a.flags[t] = (uint8_t)f;   // null: count only (T[c])
     }
-    if (a.flags) a.flags[t] = (uint8_t)f;   // null: count only (T[c])
+    // T[c] += f: one atomic per wave when the wave lies in one class
+    const i64 c0 = __shfl(c, 0, 64);
+    if (__all(c == c0 || c < 0)) {
+      const int r = wave_sum(f);
+      if ((threadIdx.x & 63) == 0 && r && c0 >= 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c0]), (unsigned long long)r);
+    } else if (f) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
+    }
+    const i64 tot = block_sum((i64)f, sm);
+    if (threadIdx.x == 0 && tot)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
+    __syncthreads();                             // rng / sm reused by the next virtual block
   }
-  // T[c] += f: one atomic per wave when the wave lies in one class
-  const i64 c0 = __shfl(c, 0, 64);
-  if (__all(c == c0 || c < 0)) {
-    const int r = wave_sum(f);
-    if ((threadIdx.x & 63) == 0 && r && c0 >= 0)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c0]), (unsigned long long)r);
-  } else if (f) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
-  }
-  const i64 tot = block_sum((i64)f, sm);
-  if (threadIdx.x == 0 && tot)
-    atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
 }
 
 // ---------------------------------------------------------------------------
@@ -2146,8 +2194,6 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
 // tests.  On a hash collision or more than SHG_MAX groups every class falls
 // back to the pair-by-pair test (same result, slower).
 // ---------------------------------------------------------------------------
-constexpr int SHG_MAX = 4096;
-
 // one wave per policy: 64-bit hash of AC[p] (never the empty key ~0)
 __global__ __launch_bounds__(TPB) void k_shg_hash(i64 P, const u64* __restrict__ AC, i64 ldC,
                                                   i64 UAW, u64* __restrict__ h) {
@@ -2234,11 +2280,13 @@ __global__ __launch_bounds__(TPB) void k_shg_assign(i64 P, const int32_t* __rest
 __global__ __launch_bounds__(TPB) void k_shg_sub(const int32_t* __restrict__ Gp,
                                                  const int32_t* __restrict__ reps,
                                                  const u64* __restrict__ AC, i64 ldC, i64 UAW,
-                                                 u64* __restrict__ sub, i64 GW) {
+                                                 u64* __restrict__ sub, i64 GW,
+                                                 const int32_t* __restrict__ err,
+                                                 const u64* __restrict__ nfp, int force) {
   const int32_t G = *Gp;
   const i64 a = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (G > SHG_MAX || a >= G) return;
+  if (G > SHG_MAX || a >= G || !shg_grouped(Gp, err, nfp, force)) return;
   const u64* ra = AC + (i64)reps[a] * ldC;
   for (i64 hb = 0; hb * 64 < G; ++hb) {
     const i64 b = hb * 64 + lane;
@@ -2254,6 +2302,7 @@ __global__ __launch_bounds__(TPB) void k_shg_sub(const int32_t* __restrict__ Gp,
 }
 
 // T[c] = flagged pairs of row class c (one block per class)
+// (not shg_grouped: T is the pairwise test's)
 __global__ __launch_bounds__(TPB) void k_shg_count(ShadowArgs a, const int32_t* __restrict__ gid,
                                                    const int32_t* __restrict__ Gp,
                                                    const u64* __restrict__ sub, i64 GW,
@@ -2262,6 +2311,7 @@ __global__ __launch_bounds__(TPB) void k_shg_count(ShadowArgs a, const int32_t* 
   __shared__ int32_t gl[SHG_MAX];
   __shared__ int32_t ngl;
   __shared__ i64 sm[4];
+  if (!shg_grouped(Gp, err, a.shg_nf, a.shg_force)) return;
   const i64 c = blockIdx.x;
   if (a.mcnt[c] == 0) return;                    // no local member: T[c] stays 0
   const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0;

@@ -15,6 +15,7 @@ for line in open("gpurun_out/bab.log"):
         d = json.loads(line)
         print(os.environ["T"] or "(default)", "| step", round(d["ms_per_step"], 4), "median",
               d["step_ms"]["median"], "| k_rows", round(d["roofline"]["avg_launch_ms"], 4),
+              "| front", round(d["step_ms"]["median"] - d["roofline"]["avg_launch_ms"], 4),
               "| verified", d.get("verified"))
 PY
 done

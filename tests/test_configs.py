@@ -271,13 +271,15 @@ def _lists(cs, which):
 # --- k_rows variants that only fire on wide matrices ------------------------
 @pytest.mark.parametrize("tune", [
     "nt=512", "nt=1024", "cww=64", "cww=16", "nt=1024,cww=32", "cww=16,ch=3",
-    "persist=8", "store=0", "store=3",
+    "persist=8", "store=0", "store=3", "xfuse=1", "sig=0",
 ])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
     """k_rows<512> / <1024> (chosen for n > 131k / 262k), several column
     chunks (n > 524k), other work-item sizes, the persistent grid and the
-    store flavours, forced at small n, against kano_py's matrix and lists."""
+    store flavours, forced at small n; the crosscheck's sort folded into the
+    build's launches (xfuse) and event-based host syncs (sig=0): against
+    kano_py's matrix and lists."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids, tables_from_cluster
     from kano.synth import make_config, objects_from_json

@@ -192,8 +192,11 @@ def test_verify_fused_c2(cap):
     pin.close()
 
 
-def test_verify_declared_groups_checked():
-    """A group id outside the declared [0, ngroups) is an error, not a fault."""
+@pytest.mark.parametrize("tune", ["xfuse=0", "xfuse=1"])
+def test_verify_declared_groups_checked(tune, monkeypatch):
+    """A group id outside the declared [0, ngroups) is an error, not a fault
+    (the check in k_cls_group_range_m, or in k_cls_mfill with xfuse)."""
+    monkeypatch.setenv("KANO_TUNE", tune)
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids
     from kano._native import KanoNativeError

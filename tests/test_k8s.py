@@ -268,6 +268,29 @@ def test_edge_row_shards(cuts, self_traffic, self_term):
 
 
 @pytest.mark.gpu
+def test_edge_row_shard_checks_refuse_and_by_none():
+    """A row shard's edge is not a whole matrix: kano.algorithm's column
+    checks refuse it (they would fold only the rank's rows) instead of
+    answering for the shard; with check_select_by_no_policy the shards,
+    recombined, still equal the restated rules."""
+    from kano import k8s, algorithm
+    from oracle import kano_oracle as orc
+    pods, pols, nss = _cluster(5)
+    n = len(pods)
+    r = k8s.build(pods, pols, nss, rows=(20, 45))
+    with pytest.raises(ValueError):
+        algorithm.all_isolated(r.edge)
+    with pytest.raises(ValueError):
+        algorithm.all_reachable(r.edge)
+    edge, _, _ = orc.kubesv_edge_py(pods, pols, nss, True, True)
+    parts = []
+    for r0, r1 in [(0, 25), (25, n)]:
+        rr = k8s.build(pods, pols, nss, rows=(r0, r1), check_select_by_no_policy=True)
+        parts.append(rr.edge.engine.rows(r0, r1 - r0))
+    assert _bits(np.concatenate(parts, axis=0), n) == edge
+
+
+@pytest.mark.gpu
 def test_build_classes_defers_the_matrix():
     """kano_build_classes: the same classes and checks as kano_build, and the
     same matrix once it is read (written on first use)."""
