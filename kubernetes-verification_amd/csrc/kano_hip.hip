@@ -248,6 +248,8 @@ struct kano_ctx {
   // k_join_fill -- four launches fewer (knob xfuse; off by default: measured
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
+  int fork_late = 1;         // policy_shadow's side-stream tests issued after the build's
+                             // last launches (0: at the fork point)
   bool xs_on = false, xs_done = false;
   const int32_t* xs_gdev = nullptr;
   int32_t xs_G = 0;
@@ -1834,6 +1836,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "graphs") ctx->graphs = v;
         if (k == "sig") ctx->mirror_sig = v;
         if (k == "xfuse") ctx->xfuse = v;
+        if (k == "forklate") ctx->fork_late = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
         if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
@@ -2933,16 +2936,29 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // which runs after them anyway)
   const bool rows_first = ctx->rows_early == 2 && rows_local(ctx) > 0;
   hipStream_t tst = rows_first ? ctx->stream3 : ctx->stream2;
+  // The fork point is marked (ev_fork2) where the lists and AC are complete;
+  // the side stream's wait, the tests and the join event are issued after
+  // the build's remaining launches (flat lists, Mc scatter), so that the
+  // host's ~15 us of fork calls overlap those kernels instead of leaving the
+  // main stream idle (it ran ahead of the host there)
+  bool fork_marked = false;
+  std::function<int()> fork_issue;
   if (want_shadow && ctx->fork_checks) {
-    ctx->fork_hook = [&, tst]() -> int {
+    ctx->fork_hook = [&]() -> int {
       KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));
-      KCHK(hipStreamWaitEvent(tst, ctx->ev_fork2, 0));
-      KTRY(shadow_test_launch(ctx, sp, tst));
-      KCHK(hipEventRecord(ctx->ev_join2, tst));
-      ctx->fork_pending = true;
-      return 0;
+      fork_marked = true;
+      return ctx->fork_late ? 0 : fork_issue();
     };
   }
+  fork_issue = [&, tst]() -> int {
+    if (!fork_marked) return 0;
+    fork_marked = false;
+    KCHK(hipStreamWaitEvent(tst, ctx->ev_fork2, 0));
+    KTRY(shadow_test_launch(ctx, sp, tst));
+    KCHK(hipEventRecord(ctx->ev_join2, tst));
+    ctx->fork_pending = true;
+    return 0;
+  };
   bool early = false;
   if (rows_first && !words_dev) {
     ctx->rows_hook = [&]() -> int {
@@ -2956,6 +2972,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   ctx->rows_hook = nullptr;
   ctx->xs_on = false;
   KTRY(brc);
+  KTRY(fork_issue());
   // the matrix write needs only the lists: with rows_early it starts here on
   // stream2, beside the class-level checks
   if (!early && ctx->rows_early == 1 && ctx->rows_overlap) {
