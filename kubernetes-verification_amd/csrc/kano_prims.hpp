@@ -170,17 +170,25 @@ struct ScanJobs {
   int sig_n;
 };
 
-// one writer of host mirrors is done: its stores are made visible system-wide
-// before it counts itself; the last writer raises the host signal
+// A host mirror word: a system-scope (write-through) store, so that once the
+// store is acknowledged the host sees it -- no cache write-back needed.
+__device__ __forceinline__ void mirror_store(u64* p, u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One writer of host mirrors is done.  Its mirror stores are acknowledged
+// (s_waitcnt on every counter) before it counts itself, and the last writer
+// raises the host signal after seeing every other count: the host, seeing
+// the signal, sees every mirror word.  (A system-scope fence here wrote back
+// the XCD's L2 per writer: ~5 us on the scan that carries the signal.)
 __device__ __forceinline__ void scan_sig_arrive(const ScanJobs& jobs) {
   if (!jobs.sig_host) return;
-  __threadfence_system();
+  __builtin_amdgcn_s_waitcnt(0);
   const uint32_t old =
-      __hip_atomic_fetch_add(jobs.sig_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(jobs.sig_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old + 1 == (uint32_t)jobs.sig_n) {
     __hip_atomic_store(jobs.sig_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence_system();
-    __hip_atomic_store(jobs.sig_host, jobs.sig_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    mirror_store(jobs.sig_host, jobs.sig_val);
   }
 }
 
@@ -193,7 +201,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
   const i64 nthr = (i64)gridDim.x * gridDim.y * TPB;
   for (i64 i = lin * TPB + threadIdx.x; i < nclear; i += nthr) clear[i] = 0;
   if (lin == 0 && threadIdx.x == 0 && jobs.npub > 0) {
-    for (int q = 0; q < jobs.npub; ++q) *jobs.pub_dst[q] = *jobs.pub_src[q];
+    for (int q = 0; q < jobs.npub; ++q) mirror_store(jobs.pub_dst[q], *jobs.pub_src[q]);
     scan_sig_arrive(jobs);
   }
   ScanJob jb = jobs.j[0];   // select, not a dynamic index (kernarg stays in SGPRs)
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       else static_cast<int32_t*>(jb.out)[0] = 0;
       if (jb.total) *jb.total = 0;
       if (jb.total_host) {
-        *jb.total_host = 0;
+        mirror_store(jb.total_host, 0);
         scan_sig_arrive(jobs);
       }
     }
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       o[jb.n] = pre;
       if (jb.total) *jb.total = (u64)pre;
       if (jb.total_host) {
-        *jb.total_host = (u64)pre;
+        mirror_store(jb.total_host, (u64)pre);
         scan_sig_arrive(jobs);
       }
     }
@@ -288,7 +296,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
       o[jb.n] = (int32_t)pre;
       if (jb.total) *jb.total = (u64)pre;
       if (jb.total_host) {
-        *jb.total_host = (u64)pre;
+        mirror_store(jb.total_host, (u64)pre);
         scan_sig_arrive(jobs);
       }
     }
