@@ -648,16 +648,9 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 // (totals) or by a scan's publish list (atomic slots); the host records an
 // event behind them now, queues more work, and later waits on the event and
 // reads the mirror -- no copy
-// order: also record ev_sizes here for other streams to wait on (the host
-// itself may poll the signal)
-int mirror_begin(kano_ctx* ctx, bool order = false) {
+int mirror_begin(kano_ctx* ctx) {
   // the latest scan with host totals raises the host signal: nothing to queue
   if (ctx->sig_armed) {
-    if (order) {
-      SegPause pause(ctx);
-      KTRY(pause.rc);
-      KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
-    }
     ctx->sig_wait = ctx->sig_armed;
     ctx->sig_armed = 0;
     return 0;
@@ -3121,9 +3114,22 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // stream before the matrix write (they crawl beside it: 60 + 40 us there
   // against 10 + 4 us alone, and slow it), the copies beside it
   const bool pre_tail = ctx->side_tail == 2 && !ctx->vs_early && want_shadow && shadow_cap >= 0;
-  // the tail on stream3 waits for everything queued so far (ev_sizes)
-  KTRY(mirror_begin(ctx, ctx->side_tail && !pre_tail));
-  if (!ctx->vs_early && !pre_tail) KTRY(launch_rows(ctx));
+  // the tail on stream3 waits for everything queued so far: the host's own
+  // sync event when there is one, else k_rows' start event (recorded at the
+  // same point of the main stream: one marker instead of two), else ev_sizes
+  const bool signalled = ctx->sig_armed != 0;
+  KTRY(mirror_begin(ctx));
+  hipEvent_t tail_ev = signalled ? nullptr : ctx->ev_sizes;
+  if (!ctx->vs_early && !pre_tail) {
+    KTRY(launch_rows(ctx));
+    if (!tail_ev && ctx->rows_timed && !ctx->rows_overlap) tail_ev = ctx->ev[7];
+  }
+  if (!tail_ev && ctx->side_tail && !pre_tail) {
+    SegPause pause(ctx);
+    KTRY(pause.rc);
+    KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
+    tail_ev = ctx->ev_sizes;
+  }
   i64 v[NS];
   KTRY(mirror_wait(ctx, SZ_NL, NS, v));
   if (ctx->vs_cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff)) {
@@ -3141,7 +3147,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // (the copies are blit kernels that crawl beside k_rows: the short
   // shadow kernels go first so that they do not queue behind them)
   hipStream_t cs = ctx->side_tail ? ctx->stream3 : ctx->stream;
-  if (cs != ctx->stream && !pre_tail) KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
+  if (cs != ctx->stream && !pre_tail) KCHK(hipStreamWaitEvent(cs, tail_ev, 0));
   i64 total = 0;
   if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
     (void)sync(ctx);
