@@ -2178,6 +2178,7 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
     const i64 tot = block_sum((i64)f, sm);
     if (threadIdx.x == 0 && tot)
       atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
+    if ((i64)gridDim.x >= nvb) break;           // one virtual block per block (uniform)
     __syncthreads();                             // rng / sm reused by the next virtual block
   }
 }
