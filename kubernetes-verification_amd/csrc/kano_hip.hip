@@ -248,6 +248,9 @@ struct kano_ctx {
   // k_join_fill -- four launches fewer (knob xfuse; off by default: measured
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
+  int alist_side = 1;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
+                             // side stream beside the Mc chain (0: in order)
+  bool alist_side_ok = false, alist_pending = false;
   int fork_late = 1;         // policy_shadow's side-stream tests issued after the build's
                              // last launches (0: at the fork point)
   bool xs_on = false, xs_done = false;
@@ -1131,11 +1134,11 @@ int mc_cols(kano_ctx* ctx) {
 }
 
 // allowed-pod lists per policy (members of its allowed column classes)
-int build_alist(kano_ctx* ctx) {
+int build_alist(kano_ctx* ctx, hipStream_t st = nullptr) {
   const i64 P = ctx->P;
   KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
   if (P > 0 && ctx->cc.U > 0) {
-    hipLaunchKernelGGL(k_pol_pods, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
+    hipLaunchKernelGGL(k_pol_pods, dim3(nblk(P, WPB)), dim3(TPB), 0, st ? st : ctx->stream, P,
                        P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
                        P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
     KLAUNCH();
@@ -1245,7 +1248,12 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   if (ua < 0)
     ua = ctx->light_cost * 16 > ctx->nnz_alw && ctx->nnz_alw * 4 <= (2ll << 30) ? 1 : 0;
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
-  if (ctx->rows_use_alist) KTRY(build_alist(ctx));
+  // (alist_side: kano_verify builds the flat lists on the side stream with
+  // policy_shadow's tests, joined before the matrix write)
+  if (ctx->rows_use_alist) {
+    if (ctx->alist_side_ok && !(ctx->rows_hook && H == 0)) ctx->alist_pending = true;
+    else KTRY(build_alist(ctx));
+  }
   if (ctx->rows_hook && H == 0) KTRY(ctx->rows_hook());   // no heavy rows: M needs no Mc
   if (U == 0) return 0;
   if (mc_rows_on(ctx)) {
@@ -1830,6 +1838,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sig") ctx->mirror_sig = v;
         if (k == "xfuse") ctx->xfuse = v;
         if (k == "forklate") ctx->fork_late = v;
+        if (k == "alistside") ctx->alist_side = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
         if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
         if (k == "shardearly") ctx->shard_rows_early = v;
@@ -2947,6 +2956,10 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     if (!fork_marked) return 0;
     fork_marked = false;
     KCHK(hipStreamWaitEvent(tst, ctx->ev_fork2, 0));
+    if (ctx->alist_pending) {   // the flat lists first: the matrix write needs them
+      ctx->alist_pending = false;
+      KTRY(build_alist(ctx, tst));
+    }
     KTRY(shadow_test_launch(ctx, sp, tst));
     KCHK(hipEventRecord(ctx->ev_join2, tst));
     ctx->fork_pending = true;
@@ -2960,7 +2973,11 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
       return 0;
     };
   }
+  ctx->alist_pending = false;
+  ctx->alist_side_ok = want_shadow && ctx->fork_checks && ctx->fork_late && ctx->alist_side &&
+                       !rows_first;
   const int brc = build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run);
+  ctx->alist_side_ok = false;
   ctx->fork_hook = nullptr;
   ctx->rows_hook = nullptr;
   ctx->xs_on = false;
