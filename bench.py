@@ -55,8 +55,9 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # (many short steps: one host hiccup of a few ms must not move the mean)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--path", default="auto", choices=["auto", "bitwise", "mfma"])
     ap.add_argument("--shadow", default="auto", choices=["auto", "pairs", "count", "off"],

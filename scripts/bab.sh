@@ -7,7 +7,9 @@ mkdir -p gpurun_out
 for t in "$@"; do
   KANO_TUNE="$t" timeout -k 10 150 python3 bench.py --steps ${STEPS:-50} --warmup 5 --cpu-baseline 0 \
     --config ${CFG:-C3} ${EXTRA:-} > gpurun_out/bab.log 2>&1
-  rc=$?; [ $rc -eq 0 ] || { echo "$t rc=$rc"; tail -5 gpurun_out/bab.log; exit $rc; }
+  rc=$?
+  # rc 1: the line printed, results differ from the golden (experiments)
+  case $rc in 0|1) ;; *) echo "$t rc=$rc"; tail -5 gpurun_out/bab.log; exit $rc ;; esac
   T="$t" python3 - <<'PY'
 import json, os
 for line in open("gpurun_out/bab.log"):
@@ -16,6 +18,6 @@ for line in open("gpurun_out/bab.log"):
         print(os.environ["T"] or "(default)", "| step", round(d["ms_per_step"], 4), "median",
               d["step_ms"]["median"], "| k_rows", round(d["roofline"]["avg_launch_ms"], 4),
               "| front", round(d["step_ms"]["median"] - d["roofline"]["avg_launch_ms"], 4),
-              "| verified", d.get("verified"))
+              "| max", d["step_ms"]["max"], "| verified", d.get("verified"))
 PY
 done
