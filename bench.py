@@ -55,9 +55,11 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # (many short steps: one host hiccup of a few ms must not move the mean)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # (many short steps: the boxes show a 7-8 ms host stall about every 0.5 s
+    # of wall time inside an engine call -- no HIP call spans it, the thread
+    # is off the CPU; over 1000 steps it adds 1-3% to the mean, see median)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--path", default="auto", choices=["auto", "bitwise", "mfma"])
     ap.add_argument("--shadow", default="auto", choices=["auto", "pairs", "count", "off"],
@@ -107,6 +109,7 @@ class Step:
         self.results = {}
         self.k_rows_ms = []
         self.host_stage_s = 0.0
+        self.verify_max_ms = 0.0    # the slowest engine call (host hiccups show here or not)
 
     def __call__(self):
         eng, n = self.eng, self.n
@@ -122,6 +125,7 @@ class Step:
             self.pin_idx = self.PinnedBuffer(4 * 4 * max(n, 1))
             self.idx_view = self.pin_idx.view(np.int32, 4 * max(n, 1))
         idx = self.idx_view
+        tv = time.perf_counter()
         if not self.shard_path:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
@@ -133,6 +137,8 @@ class Step:
             # stream), then the OR-combine and the lists on the device
             r = self.xchg.verify(eng, gid="stored", sys_row=0, shadow=self.shadow,
                                  count_only=self.count_only, pairs=pairs, idx=idx)
+        dv = time.perf_counter() - tv
+        self.verify_max_ms = max(self.verify_max_ms, dv * 1e3)
         for k in ("all_reachable", "all_isolated", "user_crosscheck", "system_isolation"):
             if r[k] is not None:
                 res[k] = r[k]
@@ -284,6 +290,12 @@ def main():
         step()
     step.k_rows_ms.clear()
     step.host_stage_s = 0.0
+    step.verify_max_ms = 0.0
+    # Python's cyclic GC off in the timed region (as timeit does): a full
+    # collection over torch's objects took ~7 ms between two steps
+    import gc
+    gc.collect()
+    gc.disable()
     barrier()
     t0 = time.perf_counter()
     marks = []
@@ -292,6 +304,7 @@ def main():
         marks.append(time.perf_counter())   # each step ends in a host sync
     barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     step_ms = np.diff(np.array([t0] + marks)) * 1e3
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -357,7 +370,8 @@ def main():
                         "p90": round(float(np.percentile(step_ms, 90)), 4),
                         "max": round(float(step_ms.max()), 4),
                         "worst5": [round(float(v), 3) for v in np.sort(step_ms)[-5:]],
-                        "worst5_at": [int(i) for i in np.argsort(step_ms)[-5:]]},
+                        "worst5_at": [int(i) for i in np.argsort(step_ms)[-5:]],
+                        "engine_call_max": round(step.verify_max_ms, 4)},
             "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},

@@ -37,6 +37,7 @@
 #include <string>
 #include <vector>
 #include <chrono>
+#include <ctime>
 #include <cstdio>
 
 #include "kano_hip.h"
@@ -248,6 +249,7 @@ struct kano_ctx {
   // k_join_fill -- four launches fewer (knob xfuse; off by default: measured
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
+  int m_contig = 0;          // the matrix in physically contiguous memory (experiment)
   int alist_side = 1;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
                              // side stream beside the Mc chain (0: in order)
   bool alist_side_ok = false, alist_pending = false;
@@ -261,6 +263,8 @@ struct kano_ctx {
   u64 sig_seq = 0;           // last signal value handed to a scan
   u64 sig_armed = 0;         // the value the latest scan with host totals will raise
   u64 sig_wait = 0;          // what mirror_wait polls for (0: the event)
+  i64 sig_long[2] = {0, 0};  // (hosttime) waits past 1 ms: stream busy / stream idle
+  int sig_spin_us = 200;     // host signal: spin this long, then sleep between polls (-1: spin)
 
   hipEvent_t ev[10] = {};
   // the matrix write (k_rows) runs on its own stream beside the checks, which
@@ -409,7 +413,9 @@ struct SegScope {
   ~SegScope() { (void)seg_end(c); }
 };
 
-int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes) {
+// contig: ask for physically contiguous memory first (the matrix: knob
+// mcontig), plain hipMalloc when that fails
+int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes, bool contig = false) {
   if (bytes == 0) bytes = 16;
   if (b.p && b.bytes >= bytes) return 0;
   if (b.p) {
@@ -418,7 +424,15 @@ int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes) {
     b.p = nullptr;
     b.bytes = 0;
   }
-  hipError_t e = hipMalloc(&b.p, bytes);
+  hipError_t e = hipErrorOutOfMemory;
+  if (contig) {
+    e = hipExtMallocWithFlags(&b.p, bytes, hipDeviceMallocContiguous);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+    }
+  }
+  if (e != hipSuccess) e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) {
     b.p = nullptr;
     return fail(ctx, -ENOMEM, "hipMalloc(" + std::to_string(bytes) + " bytes) -> " +
@@ -667,16 +681,32 @@ int mirror_begin(kano_ctx* ctx) {
   return 0;
 }
 
-// poll the host signal word; past a second (a slow device, a failed
-// launch) the stream's own synchronisation decides
+// Poll the host signal word: spin for sig_spin_us (the syncs' usual waits
+// are 30-100 us), then poll between short sleeps, so that a long wait does
+// not hold a core (knob sigspin); past a second (a slow device, a failed
+// launch) the stream's own synchronisation decides.
 int wait_signal(kano_ctx* ctx, u64 val) {
   KTRY(seg_cut(ctx));
   volatile u64* sig = ctx->gmirror + SZ_SIGNAL;
-  const auto t0 = std::chrono::steady_clock::now();
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  bool noted = false, sleepy = false;
   for (uint32_t spin = 1; *sig != val; ++spin) {
-    __builtin_ia32_pause();
-    if ((spin & 0xfff) == 0 &&
-        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+    if (sleepy) {
+      struct timespec ts = {0, 10000};
+      nanosleep(&ts, nullptr);
+    } else {
+      __builtin_ia32_pause();
+    }
+    if ((spin & 0xff) != 0 && !sleepy) continue;
+    const auto dt = clk::now() - t0;
+    if (!sleepy && ctx->sig_spin_us >= 0 && dt > std::chrono::microseconds(ctx->sig_spin_us))
+      sleepy = true;
+    if (ctx->host_timing && !noted && dt > std::chrono::milliseconds(1)) {
+      noted = true;   // (diagnostic) a long wait: is the stream still busy?
+      ctx->sig_long[hipStreamQuery(ctx->stream) == hipSuccess ? 1 : 0] += 1;
+    }
+    if (dt > std::chrono::seconds(1)) {
       KCHK(hipStreamSynchronize(ctx->stream));
       if (*sig != val) return fail(ctx, -EIO, "internal: host signal not raised");
       break;
@@ -1361,8 +1391,9 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
     rs = ctx->stream2;
   }
   if (ctx->heavy_count > 0) {
-    hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), (unsigned)ctx->heavy_count), dim3(TPB),
-                       0, rs, P_<int32_t>(ctx->hlist), P_<u64>(ctx->Mc), ctx->ldC,
+    hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(ctx->heavy_count, HEXP_CLS)),
+                       dim3(TPB), 0, rs, P_<int32_t>(ctx->hlist), (i64)ctx->heavy_count,
+                       P_<u64>(ctx->Mc), ctx->ldC,
                        P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
@@ -1461,7 +1492,7 @@ int ensure_matrix(kano_ctx* ctx) {
   if (ctx->rows_deferred) {    // kano_build_classes: the matrix, now
     ctx->rows_deferred = false;
     KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM) *
-                                 ctx->m_over));
+                                 ctx->m_over, ctx->m_contig != 0));
     KTRY(launch_rows(ctx, false));
   }
   return join_rows(ctx);
@@ -1836,7 +1867,9 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sidepre") ctx->side_pre = v;
         if (k == "graphs") ctx->graphs = v;
         if (k == "sig") ctx->mirror_sig = v;
+        if (k == "sigspin") ctx->sig_spin_us = v;
         if (k == "xfuse") ctx->xfuse = v;
+        if (k == "mcontig") ctx->m_contig = v;
         if (k == "forklate") ctx->fork_late = v;
         if (k == "alistside") ctx->alist_side = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
@@ -1936,6 +1969,9 @@ void kano_destroy(kano_ctx* ctx) {
             ctx->ht[1] / (ctx->ht[0] - 1), ctx->ht[2] / ctx->ht[0], ctx->ht[3] / ctx->ht[0],
             ctx->ht[4] / ctx->ht[0], ctx->ht[5] / ctx->ht[0], ctx->ht[6] / ctx->ht[0],
             ctx->ht[7] / ctx->ht[0], ctx->ht[0]);
+  if (ctx->host_timing)
+    fprintf(stderr, "kano host signal waits past 1 ms: %lld with the stream busy, %lld idle\n",
+            (long long)ctx->sig_long[0], (long long)ctx->sig_long[1]);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
@@ -2285,7 +2321,8 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
   const i64 rl = rows_local(ctx);
   if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
-    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over));
+    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over,
+                ctx->m_contig != 0));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KTRY(stage_mark(ctx, 0, ctx->stream));

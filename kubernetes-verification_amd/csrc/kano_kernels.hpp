@@ -1545,24 +1545,28 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
 }
 
 // expansion: M[first member of heavy class h] bit j = Mc[h][cla[j]]; one wave
-// per 64-pod word, the whole padded row is written
-__global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict__ hlist,
+// per 64-pod word, the whole padded row is written.  A block takes HEXP_CLS
+// heavy classes (grid.y = ceil(H / HEXP_CLS)): the pods' column classes are
+// read once per block, not once per class (C5: 1,027 heavy classes x 1M pods)
+constexpr int HEXP_CLS = 16;
+__global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict__ hlist, i64 H,
                                                       const u64* __restrict__ Mc, i64 ldMc,
                                                       const int32_t* __restrict__ cla, i64 n,
                                                       const int32_t* __restrict__ moff,
                                                       const int32_t* __restrict__ mem,
                                                       u64* __restrict__ M, i64 ldM, i64 r0) {
-  const int32_t c = hlist[blockIdx.y];
   const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
   const i64 w = j >> 6;
   if ((w << 6) >= ldM * 64) return;                 // wave-uniform
-  bool bit = false;
-  if (j < n) {
-    const int32_t ca = cla[j];
-    bit = (Mc[(i64)c * ldMc + (ca >> 6)] >> (ca & 63)) & 1ull;
+  const int32_t ca = j < n ? cla[j] : -1;
+  const i64 h0 = (i64)blockIdx.y * HEXP_CLS;
+  const int nh = (int)min((i64)HEXP_CLS, H - h0);
+  for (int q = 0; q < nh; ++q) {
+    const int32_t c = hlist[h0 + q];
+    const bool bit = ca >= 0 && ((Mc[(i64)c * ldMc + (ca >> 6)] >> (ca & 63)) & 1ull);
+    const u64 bal = __ballot(bit);
+    if ((threadIdx.x & 63) == 0 && w < ldM) M[(i64)(mem[moff[c]] - r0) * ldM + w] = bal;
   }
-  const u64 bal = __ballot(bit);
-  if ((threadIdx.x & 63) == 0 && w < ldM) M[(i64)(mem[moff[c]] - r0) * ldM + w] = bal;
 }
 
 // ===========================================================================

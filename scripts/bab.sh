@@ -18,6 +18,6 @@ for line in open("gpurun_out/bab.log"):
         print(os.environ["T"] or "(default)", "| step", round(d["ms_per_step"], 4), "median",
               d["step_ms"]["median"], "| k_rows", round(d["roofline"]["avg_launch_ms"], 4),
               "| front", round(d["step_ms"]["median"] - d["roofline"]["avg_launch_ms"], 4),
-              "| max", d["step_ms"]["max"], "| verified", d.get("verified"))
+              "| max", d["step_ms"]["max"], "engine", d["step_ms"].get("engine_call_max"), "at", d["step_ms"]["worst5_at"][-1], "| verified", d.get("verified"))
 PY
 done
