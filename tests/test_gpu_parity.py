@@ -498,3 +498,38 @@ def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
     assert r["system_isolation"].tolist() == ref["system_isolation"]
     assert np.array_equal(np.ascontiguousarray(r["pairs"]).reshape(-1, 2), ref["shadow"])
     eng.close()
+
+
+@pytest.mark.parametrize("tune", ["", "sig=0", "xfuse=1,forklate=0,alistside=0"])
+@pytest.mark.parametrize("n,P", [(1, 0), (1, 1), (2, 3), (5, 1), (63, 7), (64, 64), (65, 9),
+                                 (130, 40)])
+def test_verify_small_shapes_vs_oracle(n, P, tune, monkeypatch):
+    """kano_verify on tiny and word-boundary shapes (1, 63, 64, 65 pods; no
+    policy; more policies than pods) under each host-sync form and the
+    launch-order variants: every list, the pairs and the count-only count
+    equal the C oracle's (a restatement of algorithm.py:4-80)."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids
+    from kano.synth import make_cluster, objects_from_json
+    from kano import model
+    from oracle import kano_oracle as orc
+    monkeypatch.setenv("KANO_TUNE", tune)
+    obj = make_cluster(n, P, "sparse", seed=n * 1000 + P).to_json_obj()
+    ref = orc.run_c(obj, label="tenant")
+    cs, ps = objects_from_json(obj, model)
+    gid = group_ids(cs, "tenant")
+    eng = DeviceBuild(intern(cs, ps), build=False)
+    for sys_row in sorted({0, n - 1}):
+        r = eng.verify(gid, sys_row=sys_row, shadow=True)
+        assert r["all_reachable"].tolist() == ref["all_reachable"]
+        assert r["all_isolated"].tolist() == ref["all_isolated"]
+        assert r["user_crosscheck"].tolist() == ref["user_crosscheck"]
+        row = ref["M"][sys_row]
+        bits = np.unpackbits(row.view(np.uint8), bitorder="little")[:n]
+        assert r["system_isolation"].tolist() == np.flatnonzero(bits == 0).tolist()
+        assert r["shadow_count"] == ref["shadow_count"]
+        assert np.array_equal(np.asarray(r["pairs"]).reshape(-1, 2), ref["shadow"].reshape(-1, 2))
+        assert np.array_equal(eng.rows(0, n), ref["M"])
+        c = eng.verify(gid, sys_row=sys_row, shadow=True, shadow_count_only=True)
+        assert c["shadow_count"] == ref["shadow_count"] and c["pairs"] is None
+    eng.close()
