@@ -250,8 +250,9 @@ struct kano_ctx {
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
   int m_contig = 0;          // the matrix in physically contiguous memory (experiment)
-  int alist_side = 1;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
-                             // side stream beside the Mc chain (0: in order)
+  int alist_side = 0;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
+                             // side stream beside the Mc chain (measured: front end +4-14 us,
+                             // the side stream then outlasts the Mc chain; off)
   bool alist_side_ok = false, alist_pending = false;
   int fork_late = 1;         // policy_shadow's side-stream tests issued after the build's
                              // last launches (0: at the fork point)
