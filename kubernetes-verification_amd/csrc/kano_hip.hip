@@ -249,6 +249,7 @@ struct kano_ctx {
   // k_join_fill -- four launches fewer (knob xfuse; off by default: measured
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
+  int hfuse = 1;             // independent launches merged (k_lists_allow, k_pods_scatter)
   int m_contig = 0;          // the matrix in physically contiguous memory (experiment)
   int alist_side = 0;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
                              // side stream beside the Mc chain (measured: front end +4-14 us,
@@ -1165,13 +1166,20 @@ int mc_cols(kano_ctx* ctx) {
 }
 
 // allowed-pod lists per policy (members of its allowed column classes)
-int build_alist(kano_ctx* ctx, hipStream_t st = nullptr) {
+PolPodsArgs pol_pods_args(kano_ctx* ctx) {
+  return PolPodsArgs{ctx->P, P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
+                     P_<int32_t>(ctx->cc.moff), P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff),
+                     P_<int32_t>(ctx->alist)};
+}
+
+// launch: false -- allocate only (the caller launches k_pol_pods' blocks
+// inside k_pods_scatter)
+int build_alist(kano_ctx* ctx, hipStream_t st = nullptr, bool launch = true) {
   const i64 P = ctx->P;
   KTRY(dalloc(ctx, ctx->alist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_alw)));
-  if (P > 0 && ctx->cc.U > 0) {
-    hipLaunchKernelGGL(k_pol_pods, dim3(nblk(P, WPB)), dim3(TPB), 0, st ? st : ctx->stream, P,
-                       P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->cc.moff),
-                       P_<int32_t>(ctx->cc.mem), P_<i64>(ctx->aloff), P_<int32_t>(ctx->alist));
+  if (launch && P > 0 && ctx->cc.U > 0) {
+    hipLaunchKernelGGL(k_pol_pods, dim3(nblk(P, WPB)), dim3(TPB), 0, st ? st : ctx->stream,
+                       pol_pods_args(ctx));
     KLAUNCH();
   }
   ctx->alist_valid = true;
@@ -1251,21 +1259,33 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                          P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), sel_spb(ctx));
       KLAUNCH();
     }
-    // S(c) sorted, heavy list and work-item map in one launch
-    const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
-                           ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
-    hipLaunchKernelGGL(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream,
-                       P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), P > 0 ? 1 : 0,
-                       P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), P_<int32_t>(ctx->hlist),
-                       P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls));
-    KLAUNCH();
   }
-  if (P > 0 && ctx->cc.U > 0) {
-    hipLaunchKernelGGL(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, P,
-                       P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
-                       P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
-                       P_<u64>(ctx->AC), ctx->ldC);
+  // S(c) sorted, heavy list and work-item map (k_class_lists) and the
+  // allowed classes + bits per policy (k_pol_allow_fill): independent, one
+  // launch when both run (hfuse)
+  const bool lists_on = U > 0, allow_on = P > 0 && ctx->cc.U > 0;
+  const ClassListsArgs cla{P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), P > 0 ? 1 : 0,
+                           P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), P_<int32_t>(ctx->hlist),
+                           P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls)};
+  const PolAllowArgs paa{P, P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
+                         P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
+                         P_<u64>(ctx->AC), ctx->ldC};
+  const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
+                         ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
+  if (lists_on && allow_on && ctx->hfuse) {
+    const unsigned nb1 = nblk(U, TPB / 64);
+    hipLaunchKernelGGL(k_lists_allow, dim3(nb1 + nblk(P, WPB)), dim3(TPB), lds, ctx->stream, cla,
+                       paa, nb1);
     KLAUNCH();
+  } else {
+    if (lists_on) {
+      hipLaunchKernelGGL(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, cla);
+      KLAUNCH();
+    }
+    if (allow_on) {
+      hipLaunchKernelGGL(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, paa);
+      KLAUNCH();
+    }
   }
   if (ctx->fork_hook) KTRY(ctx->fork_hook());   // lists and AC are complete here
   // light rows read either the flat allowed-pod lists (materialised here,
@@ -1281,9 +1301,21 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   ctx->rows_use_alist = ua && ctx->light_cost > 0;
   // (alist_side: kano_verify builds the flat lists on the side stream with
   // policy_shadow's tests, joined before the matrix write)
+  // (k_pol_pods' blocks ride in the Mc scatter's launch when both run)
+  const McScatterArgs msa{ctx->nnz_sel, P_<int32_t>(ctx->ecls), P_<int32_t>(ctx->slist),
+                          P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
+                          H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr,
+                          P_<u64>(ctx->Mc), ldMc};
+  const bool scatter_on = U > 0 && !mc_rows_on(ctx) && ctx->nnz_sel > 0;
+  bool pods_in_scatter = false;
   if (ctx->rows_use_alist) {
-    if (ctx->alist_side_ok && !(ctx->rows_hook && H == 0)) ctx->alist_pending = true;
-    else KTRY(build_alist(ctx));
+    if (ctx->alist_side_ok && !(ctx->rows_hook && H == 0)) {
+      ctx->alist_pending = true;
+    } else {
+      pods_in_scatter = ctx->hfuse && scatter_on && !(ctx->rows_hook && H == 0) && P > 0 &&
+                        ctx->cc.U > 0;
+      KTRY(build_alist(ctx, nullptr, !pods_in_scatter));
+    }
   }
   if (ctx->rows_hook && H == 0) KTRY(ctx->rows_hook());   // no heavy rows: M needs no Mc
   if (U == 0) return 0;
@@ -1299,12 +1331,14 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       hipLaunchKernelGGL(k_mc_rows<1>, dim3((unsigned)U), dim3(64), lds, ctx->stream, U,
                          P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
                          P_<int32_t>(ctx->alc), hf, mfma ? 1 : 0, P_<u64>(ctx->Mc), ldMc);
-  } else if (ctx->nnz_sel > 0)
-  hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                     ctx->nnz_sel, P_<int32_t>(ctx->ecls), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
-                     P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
-                     H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr, P_<u64>(ctx->Mc),
-                     ldMc);
+  } else if (pods_in_scatter) {
+    const unsigned nb1 = nblk(P, WPB);
+    hipLaunchKernelGGL(k_pods_scatter, dim3(nb1 + nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
+                       ctx->stream, pol_pods_args(ctx), msa, nb1);
+  } else if (scatter_on) {
+    hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0, ctx->stream,
+                       msa);
+  }
   KLAUNCH();
   if (H > 0) {
     if (mfma) {
@@ -1870,6 +1904,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sig") ctx->mirror_sig = v;
         if (k == "sigspin") ctx->sig_spin_us = v;
         if (k == "xfuse") ctx->xfuse = v;
+        if (k == "hfuse") ctx->hfuse = v;
         if (k == "mcontig") ctx->m_contig = v;
         if (k == "forklate") ctx->fork_late = v;
         if (k == "alistside") ctx->alist_side = v;

@@ -448,16 +448,29 @@ __device__ __forceinline__ i64 wave_policy() {
 
 // allowed pods of policy p: members of its allowed column classes, streamed
 // 64 classes at a time as one flat range (no per-class round trips)
-__global__ __launch_bounds__(TPB) void k_pol_pods(i64 P, const i64* __restrict__ alcoff,
-                                                  const int32_t* __restrict__ alc,
-                                                  const int32_t* __restrict__ cmoff,
-                                                  const int32_t* __restrict__ cmem,
-                                                  const i64* __restrict__ aloff,
-                                                  int32_t* __restrict__ alist) {
+struct PolPodsArgs {
+  i64 P;
+  const i64* alcoff;
+  const int32_t* alc;
+  const int32_t* cmoff;
+  const int32_t* cmem;
+  const i64* aloff;
+  int32_t* alist;
+};
+// (vb: the block index within this job, so that a launch can carry other
+// jobs' blocks too -- k_pods_scatter; no block barrier)
+__device__ __forceinline__ void pol_pods_item(const PolPodsArgs& a, i64 vb) {
+  const i64 P = a.P;
+  const i64* __restrict__ alcoff = a.alcoff;
+  const int32_t* __restrict__ alc = a.alc;
+  const int32_t* __restrict__ cmoff = a.cmoff;
+  const int32_t* __restrict__ cmem = a.cmem;
+  const i64* __restrict__ aloff = a.aloff;
+  int32_t* __restrict__ alist = a.alist;
   __shared__ int32_t seg_m0[WPB][64];
   __shared__ int32_t seg_pre[WPB][65];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const i64 p = wave_policy();
+  const i64 p = vb * WPB + wid;
   if (p >= P) return;                      // wave-uniform
   i64 out = aloff[p];
   const i64 e1 = alcoff[p + 1];
@@ -487,6 +500,8 @@ __global__ __launch_bounds__(TPB) void k_pol_pods(i64 P, const i64* __restrict__
     __builtin_amdgcn_wave_barrier();
   }
 }
+
+__global__ __launch_bounds__(TPB) void k_pol_pods(PolPodsArgs a) { pol_pods_item(a, blockIdx.x); }
 
 // ===========================================================================
 // Policy -> class matching by hash join.  The terms of a policy fix the values
@@ -796,16 +811,30 @@ __global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soff
 // sorted ascending (with sort != 0): a rank sort in registers for s <= 64,
 // else the wave's own LDS bitmap of all P policies (dynamic LDS: WPB x
 // ceil(P/64) words, passed only when some list is longer than 64).
-__global__ __launch_bounds__(TPB) void k_class_lists(const i64* __restrict__ soffc, i64 U, i64 P,
-                                                     int32_t* __restrict__ slist, int sort,
-                                                     const int32_t* __restrict__ hflag,
-                                                     const int32_t* __restrict__ hoff,
-                                                     int32_t* __restrict__ hlist,
-                                                     const int32_t* __restrict__ wioff,
-                                                     int32_t* __restrict__ wicls) {
+struct ClassListsArgs {
+  const i64* soffc;
+  i64 U, P;
+  int32_t* slist;
+  int sort;
+  const int32_t* hflag;
+  const int32_t* hoff;
+  int32_t* hlist;
+  const int32_t* wioff;
+  int32_t* wicls;
+};
+__device__ __forceinline__ void class_lists_item(const ClassListsArgs& a, i64 vb) {
+  const i64* __restrict__ soffc = a.soffc;
+  const i64 U = a.U, P = a.P;
+  int32_t* __restrict__ slist = a.slist;
+  const int sort = a.sort;
+  const int32_t* __restrict__ hflag = a.hflag;
+  const int32_t* __restrict__ hoff = a.hoff;
+  int32_t* __restrict__ hlist = a.hlist;
+  const int32_t* __restrict__ wioff = a.wioff;
+  int32_t* __restrict__ wicls = a.wicls;
   extern __shared__ __attribute__((aligned(16))) u64 lds_bm[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + wid;
+  const i64 c = vb * (TPB / 64) + wid;
   if (c >= U) return;                       // wave-uniform; waves never meet at a barrier
   if (lane == 0 && hflag[c]) hlist[hoff[c]] = (int32_t)c;
   for (int32_t w = wioff[c] + lane; w < wioff[c + 1]; w += 64) wicls[w] = (int32_t)c;
@@ -841,6 +870,10 @@ __global__ __launch_bounds__(TPB) void k_class_lists(const i64* __restrict__ sof
     }
     base += tot;
   }
+}
+
+__global__ __launch_bounds__(TPB) void k_class_lists(ClassListsArgs a) {
+  class_lists_item(a, blockIdx.x);
 }
 
 // block per class with s > SORT_WAVE_MAX: bitmap of all P policies in LDS
@@ -987,22 +1020,38 @@ __global__ __launch_bounds__(TPB) void k_pol_allow_count(i64 P, const i64* __res
 }
 
 // block per policy: allowed class list (alc) and its bits AC[p]
-__global__ __launch_bounds__(TPB) void k_pol_allow_fill(i64 P, const i64* __restrict__ pstart,
-                                                        const int32_t* __restrict__ plen,
-                                                        const int32_t* __restrict__ pcls,
-                                                        const i64* __restrict__ alcoff,
-                                                        int32_t* __restrict__ alc, u64* AC,
-                                                        i64 ldC) {
-  const i64 p = wave_policy();
-  if (p >= P) return;
-  const int32_t* L = pcls + pstart[p];
-  const int32_t len = plen[p];
-  int32_t* out = alc + alcoff[p];
+struct PolAllowArgs {
+  i64 P;
+  const i64* pstart;
+  const int32_t* plen;
+  const int32_t* pcls;
+  const i64* alcoff;
+  int32_t* alc;
+  u64* AC;
+  i64 ldC;
+};
+__device__ __forceinline__ void pol_allow_item(const PolAllowArgs& a, i64 vb) {
+  const i64 p = vb * WPB + (threadIdx.x >> 6);
+  if (p >= a.P) return;
+  const int32_t* L = a.pcls + a.pstart[p];
+  const int32_t len = a.plen[p];
+  int32_t* out = a.alc + a.alcoff[p];
   for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
     const int32_t ca = L[k];
     out[k] = ca;
-    atomicOr(&AC[p * ldC + (ca >> 6)], 1ull << (ca & 63));
+    atomicOr(&a.AC[p * a.ldC + (ca >> 6)], 1ull << (ca & 63));
   }
+}
+__global__ __launch_bounds__(TPB) void k_pol_allow_fill(PolAllowArgs a) {
+  pol_allow_item(a, blockIdx.x);
+}
+
+// k_class_lists and k_pol_allow_fill in one launch (independent; both one
+// wave per item, no block barrier): blocks [0, nb1) take the class lists
+__global__ __launch_bounds__(TPB) void k_lists_allow(ClassListsArgs a, PolAllowArgs b,
+                                                     unsigned nb1) {
+  if (blockIdx.x < nb1) class_lists_item(a, blockIdx.x);
+  else pol_allow_item(b, blockIdx.x - nb1);
 }
 
 // class-major policy bits for the MFMA path: out[pb][c] bit p%64 = policy p
@@ -1020,24 +1069,40 @@ __global__ __launch_bounds__(TPB) void k_classbits(const i64* __restrict__ pstar
 // ---- compressed matrix Mc[c] over column classes (row classes x col classes)
 // light classes: one wave per select entry (c, p) scatters p's allowed-class
 // list into row c (balanced over entries, not classes)
-__global__ __launch_bounds__(TPB) void k_mc_scatter(i64 nnz, const int32_t* __restrict__ ecls,
-                                                    const int32_t* __restrict__ slist,
-                                                    const i64* __restrict__ alcoff,
-                                                    const int32_t* __restrict__ alc,
-                                                    const int32_t* __restrict__ mcnt,
-                                                    const int32_t* __restrict__ hflag,
-                                                    u64* Mc, i64 ldMc) {
-  const i64 e = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+struct McScatterArgs {
+  i64 nnz;
+  const int32_t* ecls;
+  const int32_t* slist;
+  const i64* alcoff;
+  const int32_t* alc;
+  const int32_t* mcnt;
+  const int32_t* hflag;
+  u64* Mc;
+  i64 ldMc;
+};
+__device__ __forceinline__ void mc_scatter_item(const McScatterArgs& a, i64 vb) {
+  const i64 e = vb * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (e >= nnz) return;
-  const int32_t c = ecls[e];
-  if (mcnt[c] == 0 || (hflag && hflag[c])) return;
-  u64* row = Mc + (i64)c * ldMc;
-  const int32_t p = slist[e];
-  for (i64 k = alcoff[p] + lane; k < alcoff[p + 1]; k += 64) {
-    const int32_t ca = alc[k];
+  if (e >= a.nnz) return;
+  const int32_t c = a.ecls[e];
+  if (a.mcnt[c] == 0 || (a.hflag && a.hflag[c])) return;
+  u64* row = a.Mc + (i64)c * a.ldMc;
+  const int32_t p = a.slist[e];
+  for (i64 k = a.alcoff[p] + lane; k < a.alcoff[p + 1]; k += 64) {
+    const int32_t ca = a.alc[k];
     atomicOr(&row[ca >> 6], 1ull << (ca & 63));
   }
+}
+__global__ __launch_bounds__(TPB) void k_mc_scatter(McScatterArgs a) {
+  mc_scatter_item(a, blockIdx.x);
+}
+
+// k_pol_pods and k_mc_scatter in one launch (independent; one wave per
+// item): blocks [0, nb1) build the flat allowed-pod lists
+__global__ __launch_bounds__(TPB) void k_pods_scatter(PolPodsArgs a, McScatterArgs b,
+                                                      unsigned nb1) {
+  if (blockIdx.x < nb1) pol_pods_item(a, blockIdx.x);
+  else mc_scatter_item(b, blockIdx.x - nb1);
 }
 
 // The same rows written whole: one wave per row class builds its row in LDS
