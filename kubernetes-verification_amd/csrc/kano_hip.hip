@@ -571,7 +571,21 @@ struct FillBatch {
     return 0;
   }
   int run();
+  // the pending jobs, for a launch that carries them (fill_item); none left
+  FillJobs take() {
+    FillJobs j = jobs;
+    jobs.count = 0;
+    return j;
+  }
 };
+
+// blocks a launch adds for carried fills (0 when there are none)
+unsigned fill_ride_blocks(const FillJobs& fj) {
+  if (fj.count == 0) return 0;
+  i64 most = 0;
+  for (int q = 0; q < fj.count; ++q) most = std::max(most, fj.j[q].words);
+  return (unsigned)std::max<i64>(1, std::min<i64>(FILL_RIDE_BLOCKS, (most + TPB - 1) / TPB));
+}
 
 int FillBatch::add(DBuf& b, size_t bytes, uint32_t value) {
   if (bytes == 0) return 0;
@@ -869,13 +883,18 @@ int classify_phase2a(kano_ctx* ctx) {
   return 0;
 }
 
-// phase 2b (U known): representative values, slot-major cval[k * U + c]
-int classify_phase2b(kano_ctx* ctx) {
+// phase 2b (U known): representative values, slot-major cval[k * U + c];
+// fj: fills that need not precede it, carried by the same launch
+int classify_phase2b(kano_ctx* ctx, FillJobs fj) {
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   const i64 U = std::max(ctx->rc.U, ctx->cc.U);
   if (U > 0) {
-    hipLaunchKernelGGL(k_cls_vals, dim3(nblk(U), 2), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->pv), ctx->n, pr, xs_sort(ctx));
+    const unsigned nbv = nblk(U), nbf = fill_ride_blocks(fj);
+    hipLaunchKernelGGL(k_cls_vals, dim3(nbv + nbf, 2), dim3(TPB), 0, ctx->stream,
+                       P_<int32_t>(ctx->pv), ctx->n, pr, xs_sort(ctx), fj, nbv);
+    KLAUNCH();
+  } else if (fj.count > 0) {
+    hipLaunchKernelGGL(k_fill_many, dim3(fill_ride_blocks(fj)), dim3(TPB), 0, ctx->stream, fj);
     KLAUNCH();
   }
   return 0;
@@ -1057,6 +1076,7 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
   const i64 P = ctx->P, Ur = ctx->rc.U, Ua = ctx->cc.U;
   ctx->UAW = (Ua + 63) / 64;
   ctx->ldC = std::max<i64>(2, (ctx->UAW + 1) & ~(i64)1);
+  FillJobs carried{};
   {
     FillBatch fb(ctx);
     KTRY(classify_alloc2(ctx, ctx->rc));
@@ -1078,6 +1098,7 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
     KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (Ur + 1)));
     KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
+    // (carried by k_cls_vals' launch unless side work sits between)
     if (ctx->xs_on) {   // the fused crosscheck sort's buffers (as cross_prepare sizes them)
       const i64 G = ctx->xs_G;
       ctx->xs_knb = std::max<i64>(1, nblk(Ur, (i64)TPB * KEY_ITEMS));
@@ -1087,13 +1108,14 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
       KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * (G + 1) + sizeof(int32_t) * ctx->xs_kslots));
       KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * (ctx->xs_kslots + 1)));
     }
-    KTRY(fb.run());
+    if (side || !ctx->hfuse) KTRY(fb.run());
+    else carried = fb.take();
   }
   if (side) {   // the size-independent back-end work, beside the join (stream2)
     SideIssue si(ctx, true);
     KTRY(side());
   }
-  KTRY(classify_phase2b(ctx));
+  KTRY(classify_phase2b(ctx, carried));
   KTRY(match_both(ctx));
   KTRY(stage_mark(ctx, 2, ctx->stream));
   // allowed classes / pods per policy, then |S(c)| and the rebuild cost
@@ -1235,6 +1257,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     }
     ctx->heavy_path = mfma ? 2 : 1;
   }
+  FillJobs carried{};
   {
     FillBatch fb(ctx);
     KTRY(dalloc(ctx, ctx->slist, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
@@ -1249,16 +1272,17 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
     }
     if (extra) KTRY(extra(fb));   // the caller's fills (kano_verify: crosscheck, shadow)
-    KTRY(fb.run());
+    // (carried by k_sel_place's launch: it neither reads nor writes them)
+    if (U > 0 && P > 0 && ctx->hfuse) carried = fb.take();
+    else KTRY(fb.run());
   }
-  if (U > 0) {
-    if (P > 0) {
-      hipLaunchKernelGGL(k_sel_place, dim3(nblk(P, sel_spb(ctx))), dim3(TPB), 0, ctx->stream, P,
-                         P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
-                         P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
-                         P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), sel_spb(ctx));
-      KLAUNCH();
-    }
+  if (U > 0 && P > 0) {
+    const unsigned nbs = nblk(P, sel_spb(ctx)), nbf = fill_ride_blocks(carried);
+    hipLaunchKernelGGL(k_sel_place, dim3(nbs + nbf), dim3(TPB), 0, ctx->stream, P,
+                       P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                       P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
+                       P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), sel_spb(ctx), carried, nbs);
+    KLAUNCH();
   }
   // S(c) sorted, heavy list and work-item map (k_class_lists) and the
   // allowed classes + bits per policy (k_pol_allow_fill): independent, one

@@ -341,8 +341,14 @@ __global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr, const int32_t* __
 // key values of each class's representative, slot-major: cval[k * U + c]
 // (ks.nb > 0: the row side's first ks.nb blocks also run the group-key
 // histogram, k_key_hist's work)
+// (blocks x >= nbv carry the fills fj: row y = 0 only)
 __global__ __launch_bounds__(TPB) void k_cls_vals(const int32_t* __restrict__ pv, i64 n,
-                                                  ClsPair pr, KeySort ks) {
+                                                  ClsPair pr, KeySort ks, FillJobs fj,
+                                                  unsigned nbv) {
+  if (blockIdx.x >= nbv) {                         // block-uniform
+    if (blockIdx.y == 0) fill_item(fj, blockIdx.x - nbv, gridDim.x - nbv);
+    return;
+  }
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
   if (c < a.U) {
@@ -724,12 +730,18 @@ __global__ __launch_bounds__(TPB) void k_sel_count(i64 P, const i64* __restrict_
 // entries are counted per class in LDS, one atomic per distinct class per
 // block reserves their places, then the entries are walked again and placed
 // with LDS cursors (order inside S(c) is fixed by the sort that follows).
+// (blocks >= nbs carry the fills fj)
 __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict__ pstart,
                                                    const int32_t* __restrict__ plen,
                                                    const int32_t* __restrict__ pcls,
                                                    const i64* __restrict__ soffc, int32_t* scur,
                                                    int32_t* __restrict__ slist,
-                                                   int32_t* __restrict__ ecls, int spb) {
+                                                   int32_t* __restrict__ ecls, int spb,
+                                                   FillJobs fj, unsigned nbs) {
+  if (blockIdx.x >= nbs) {                         // block-uniform
+    fill_item(fj, blockIdx.x - nbs, gridDim.x - nbs);
+    return;
+  }
   __shared__ int32_t lkey[CLS_LDS], lcnt[CLS_LDS], lbase[CLS_LDS];
   const bool comb = spb > WPB;                        // block-uniform
   if (comb) {

@@ -314,15 +314,22 @@ struct FillJobs {
   FillJob j[MAX_FILLS];
   int count;
 };
-__global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
-  const i64 stride = (i64)gridDim.x * TPB;
+// the fills on blocks [0, nvb) of whatever launch carries them (vb = the
+// block's index among them): k_fill_many, or extra blocks of a kernel that
+// runs independently of the fills (k_cls_vals, k_sel_place)
+__device__ __forceinline__ void fill_item(const FillJobs& jobs, i64 vb, i64 nvb) {
+  const i64 stride = nvb * TPB;
   for (int q = 0; q < jobs.count; ++q) {
     uint32_t* p = jobs.j[q].ptr;
     const uint32_t v = jobs.j[q].value;
     const i64 nw = jobs.j[q].words;
-    for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < nw; i += stride) p[i] = v;
+    for (i64 i = vb * TPB + threadIdx.x; i < nw; i += stride) p[i] = v;
   }
 }
+__global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
+  fill_item(jobs, blockIdx.x, gridDim.x);
+}
+constexpr int FILL_RIDE_BLOCKS = 512;   // blocks a carried fill gets (grid-stride)
 
 // atomicAdd(&ctr[key], 1) for every active lane, lanes with equal keys merged
 // into one atomic: up to AGG_ROUNDS rounds each take the first remaining
