@@ -88,6 +88,9 @@ struct Recorder {
 
 // the recorder of the segment being recorded on this thread (null: issue now)
 inline thread_local Recorder* g_rec = nullptr;
+// device-writing operations issued on this thread (launches, memsets,
+// copies): lets a context tell that nothing ran since it last did
+inline thread_local uint64_t g_ops = 0;
 
 template <typename Tup, size_t... I>
 inline hipError_t launch_tuple(const void* f, dim3 g, dim3 b, size_t shm, hipStream_t st, Tup& t,
@@ -109,6 +112,7 @@ template <typename... P, typename... A>
 inline void launch(void (*f)(P...), dim3 g, dim3 b, size_t shm, hipStream_t st, A&&... a) {
   static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
   std::tuple<std::decay_t<P>...> t(static_cast<std::decay_t<P>>(std::forward<A>(a))...);
+  ++g_ops;
   if (!g_rec) {
     (void)launch_tuple(reinterpret_cast<const void*>(f), g, b, shm, st, t,
                        std::index_sequence_for<P...>{});
@@ -133,6 +137,7 @@ inline void launch(void (*f)(P...), dim3 g, dim3 b, size_t shm, hipStream_t st, 
 }
 
 inline hipError_t memsetAsync(void* p, int v, size_t n, hipStream_t st) {
+  ++g_ops;
   if (!g_rec) return ::hipMemsetAsync(p, v, n, st);
   Op op;
   op.kind = OP_MEMSET;
@@ -146,6 +151,7 @@ inline hipError_t memsetAsync(void* p, int v, size_t n, hipStream_t st) {
 }
 
 inline hipError_t memcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind k, hipStream_t st) {
+  ++g_ops;
   if (!g_rec) return ::hipMemcpyAsync(d, s, n, k, st);
   Op op;
   op.kind = OP_MEMCPY;
@@ -163,6 +169,7 @@ inline hipError_t memcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind k,
 
 inline hipError_t memcpy2DAsync(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h,
                                 hipMemcpyKind k, hipStream_t st) {
+  ++g_ops;
   if (!g_rec) return ::hipMemcpy2DAsync(d, dp, s, sp, w, h, k, st);
   Op op;
   op.kind = OP_MEMCPY2D;

@@ -36,6 +36,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <array>
 #include <chrono>
 #include <ctime>
 #include <cstdio>
@@ -250,6 +251,10 @@ struct kano_ctx {
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
   int hfuse = 1;             // independent launches merged (k_lists_allow, k_pods_scatter)
+  int preclean = 1;          // kano_verify resets the next front end's tables on its tail
+  bool front_clean = false;
+  std::array<i64, 6> fc_dims{};
+  uint64_t fc_ops = 0;       // kano_rec::g_ops after the reset: nothing may run in between
   int m_contig = 0;          // the matrix in physically contiguous memory (experiment)
   int alist_side = 0;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
                              // side stream beside the Mc chain (measured: front end +4-14 us,
@@ -785,8 +790,7 @@ int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   KTRY(dalloc(ctx, cs.mcur, sizeof(int32_t) * m));
   KTRY(dalloc(ctx, cs.moff, sizeof(int32_t) * (m + 1)));
   KTRY(dalloc(ctx, cs.mem, sizeof(int32_t) * m));
-  KTRY(fb.add(cs.mcnt, sizeof(int32_t) * m, 0u));
-  return 0;
+  return 0;   // (mcnt is zeroed by k_cls_insert, one entry per pod)
 }
 
 ClsSide cls_side(kano_ctx* ctx, ClassSet& cs) {
@@ -1042,17 +1046,34 @@ int sel_spb(const kano_ctx* ctx) {
   return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
 }
 
+// The front end's first fills (size slots, both sides' hash tables and
+// smallest-member slots) and their shape (front_dims: re-used only if equal)
+int front_fills(kano_ctx* ctx, FillBatch& fb) {
+  KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
+  KTRY(fb.add(ctx->sizes, sizeof(u64) * SZ_SLOTS, 0u));
+  KTRY(classify_alloc1(ctx, ctx->rc, fb));
+  KTRY(classify_alloc1(ctx, ctx->cc, fb));
+  return 0;
+}
+std::array<i64, 6> front_dims(const kano_ctx* ctx) {
+  return {ctx->n, ctx->r0, ctx->r1, ctx->rc.packed, ctx->cc.packed,
+          (i64)reinterpret_cast<uintptr_t>(ctx->rc.table.p)};
+}
+
 int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::function<int()>()) {
   ctx->rc.m0 = ctx->r0;
   ctx->rc.m1 = ctx->r1;
   ctx->cc.m0 = 0;
   ctx->cc.m1 = ctx->n;
+  // the size slots and hash tables arrive clean when the previous kano_verify
+  // reset them on its tail stream beside its matrix write (front_clean)
+  const bool clean = ctx->front_clean && ctx->fc_dims == front_dims(ctx) &&
+                     ctx->fc_ops == kano_rec::g_ops;
+  ctx->front_clean = false;
   {
     FillBatch fb(ctx);
-    KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
-    KTRY(fb.add(ctx->sizes, sizeof(u64) * SZ_SLOTS, 0u));
-    KTRY(classify_alloc1(ctx, ctx->rc, fb));
-    KTRY(classify_alloc1(ctx, ctx->cc, fb));
+    KTRY(front_fills(ctx, fb));
+    if (clean) (void)fb.take();
     if (ctx->xs_on) {   // group ranges per row class (k_cls_mfill), <= one per local pod
       const i64 m = std::max<i64>(1, ctx->rc.m1 - ctx->rc.m0);
       KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * m));
@@ -1929,6 +1950,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sigspin") ctx->sig_spin_us = v;
         if (k == "xfuse") ctx->xfuse = v;
         if (k == "hfuse") ctx->hfuse = v;
+        if (k == "preclean") ctx->preclean = v;
         if (k == "mcontig") ctx->m_contig = v;
         if (k == "forklate") ctx->fork_late = v;
         if (k == "alistside") ctx->alist_side = v;
@@ -3290,6 +3312,18 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         cs));
+  // the next front end's first fills, beside the matrix write (the next
+  // build checks front_dims before skipping them)
+  if (cs != ctx->stream && ctx->preclean && !ctx->graphs) {
+    FillBatch fb(ctx);
+    KTRY(front_fills(ctx, fb));
+    const FillJobs fj = fb.take();
+    hipLaunchKernelGGL(k_fill_many, dim3(fill_ride_blocks(fj)), dim3(TPB), 0, cs, fj);
+    KLAUNCH();
+    ctx->front_clean = true;
+    ctx->fc_dims = front_dims(ctx);
+    ctx->fc_ops = kano_rec::g_ops;
+  }
   // later work on the main stream (a fetch of the pairs, the next build)
   // follows the tail
   if (cs != ctx->stream) {

@@ -152,6 +152,7 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
   const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;   // pods [m0, m1) of the side
   const bool act = i < a.m1;
+  if (act) a.mcnt[i - a.m0] = 0;                   // the member counts of k_cls_assign_count
   if (a.packed) {                                  // block-uniform branch (one side per block)
     __shared__ u64 lkey[CLS_LDS];
     __shared__ int32_t lmin[CLS_LDS], lslot[CLS_LDS];
