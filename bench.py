@@ -349,6 +349,8 @@ def main():
                                        f"rank 0 of {args.rank_of} emulated on one GPU, "
                                        "no collective (diagnostic, not a bench line)"),
                        "path": args.path,
+                       "exchange": (step.xchg.mode if step.shard_path else "none (one rank, "
+                                    "fused kano_verify)"),
                        "checks": "all_reachable, all_isolated, user_crosscheck(tenant), "
                                  "system_isolation(0)" +
                                  {"pairs": ", policy_shadow (pairs to the host)",

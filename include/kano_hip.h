@@ -198,6 +198,21 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
                         int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                         int64_t* shadow_count);
 
+/* kano_verify_shard, the exchange and kano_verify_combine in ONE call, the
+ * exchange being an RCCL all-gather issued by the engine itself on the
+ * context stream: comm is the caller's ncclComm_t (e.g. torch's
+ * ProcessGroupNCCL._comm_ptr()) over nranks ranks, this context's rank
+ * among them being the comm's own.  No host code runs between the shard's
+ * checks and the combine (the caller's per-collective overhead is gone).
+ * The RCCL symbols are resolved at the first call from the process (the
+ * library that created comm, e.g. torch's bundled librccl), else
+ * librccl.so; without them the call fails (-ENOSYS) and nothing runs.
+ * Outputs as kano_verify_combine; with_shadow as kano_verify_shard. */
+int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
+                       int64_t sys_row, int with_shadow, void* comm, int32_t nranks,
+                       int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                       int64_t* shadow_count);
+
 /* The checks of kano_verify_shard over the matrix rows AS THEY STAND --
  * after kano_add_policies / kano_remove_policies (or edits), which
  * kano_verify, a rebuild from the tables, would undo: this shard's

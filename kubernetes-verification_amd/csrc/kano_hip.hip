@@ -40,6 +40,8 @@
 #include <chrono>
 #include <ctime>
 #include <cstdio>
+#include <dlfcn.h>
+#include <link.h>
 
 #include "kano_hip.h"
 #include "kano_graph.hpp"     // records the HIP operations of kano_verify (see there)
@@ -210,6 +212,7 @@ struct kano_ctx {
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
+  DBuf xw, xg;               // kano_verify_gather: this shard's words, all ranks' words
   // kano_path (in the destination context): T, R / delta ping-pong buffers,
   // the MFMA operands, the step counter
   DBuf pT, pR[2], pD[2], pA, pB, pcnt;
@@ -2090,7 +2093,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
-                  &ctx->irows};
+                  &ctx->irows,  &ctx->xw,      &ctx->xg};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -3010,6 +3013,41 @@ namespace {
 // [OR | cross | NAND] words for the ranks' gather).  verify_back: (combine
 // the gathered words of all shards,) list the results, the matrix write,
 // policy_shadow's pairs, the copies to the host.
+// ncclAllGather, resolved once: from the process first (the library that
+// created the caller's communicator -- torch ships its own librccl), else
+// librccl.so.  The engine does not link RCCL: without it only
+// kano_verify_gather is unavailable.
+typedef int (*RcclAllGather)(const void*, void*, size_t, int, void*, hipStream_t);
+constexpr int RCCL_UINT64 = 5;   // ncclUint64 (rccl.h)
+int rccl_find_loaded(struct dl_phdr_info* info, size_t, void* out) {
+  const char* name = info->dlpi_name;
+  if (name && std::strstr(name, "librccl")) {
+    *static_cast<std::string*>(out) = name;
+    return 1;
+  }
+  return 0;
+}
+RcclAllGather rccl_all_gather() {
+  static RcclAllGather fn = [] {
+    // a librccl already mapped into the process (torch's, loaded RTLD_LOCAL
+    // as a dependency: not visible to RTLD_DEFAULT)
+    std::string path;
+    dl_iterate_phdr(rccl_find_loaded, &path);
+    void* f = nullptr;
+    if (!path.empty()) {
+      if (void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_NOLOAD)) f = dlsym(h, "ncclAllGather");
+    }
+    if (!f) f = dlsym(RTLD_DEFAULT, "ncclAllGather");
+    if (!f) {
+      void* h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (h) f = dlsym(h, "ncclAllGather");
+    }
+    return reinterpret_cast<RcclAllGather>(f);
+  }();
+  return fn;
+}
+
 int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
                  bool want_shadow, u64* words_dev, bool count_only = false) {
   ctx->vs_count_only = want_shadow && count_only;
@@ -3384,6 +3422,38 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
   SegScope seg(ctx);
   return verify_back(ctx, reinterpret_cast<const u64*>(gathered_dev), nranks, idx, counts,
                      shadow_pairs, shadow_cap, shadow_count);
+}
+
+int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
+                       int64_t sys_row, int with_shadow, void* comm, int32_t nranks,
+                       int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
+                       int64_t* shadow_count) {
+  if (!ctx) return -EINVAL;
+  if (!comm || nranks < 1) return fail(ctx, -EINVAL, "kano_verify_gather: bad communicator");
+  if (!counts || (!idx && ctx->n > 0))
+    return fail(ctx, -EINVAL, "kano_verify_gather: idx / counts must not be NULL");
+  if (with_shadow && !shadow_count)
+    return fail(ctx, -EINVAL, "kano_verify_gather: shadow_count is NULL but with_shadow is set");
+  const RcclAllGather ag = rccl_all_gather();
+  if (!ag)
+    return fail(ctx, -ENOSYS, "kano_verify_gather: no RCCL in the process (ncclAllGather)");
+  SegScope seg(ctx);
+  const i64 nw = 3 * ctx->W;     // [OR | cross | NAND] words of a shard (same W on every rank)
+  KTRY(dalloc(ctx, ctx->xw, sizeof(u64) * std::max<i64>(1, nw)));
+  KTRY(dalloc(ctx, ctx->xg, sizeof(u64) * std::max<i64>(1, nw * nranks)));
+  KTRY(verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0, P_<u64>(ctx->xw),
+                    with_shadow == 2));
+  // the shard's launches reach the stream before the collective does
+  KTRY(seg_cut(ctx));
+  if (nw > 0) {
+    const int rc = ag(ctx->xw.p, ctx->xg.p, (size_t)nw, RCCL_UINT64, comm, ctx->stream);
+    if (rc != 0) {
+      (void)sync(ctx);
+      return fail(ctx, -EIO, "kano_verify_gather: ncclAllGather returned " + std::to_string(rc));
+    }
+  }
+  return verify_back(ctx, P_<u64>(ctx->xg), nranks, idx, counts, shadow_pairs, shadow_cap,
+                     shadow_count);
 }
 
 int kano_checks_shard(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, int64_t sys_row,

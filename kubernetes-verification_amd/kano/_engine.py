@@ -436,6 +436,30 @@ class DeviceBuild:
                                              mode, c_void_p(words_dev_ptr)),
                   "kano_verify_shard")
 
+    def verify_gather(self, comm_ptr: int, nranks: int, gid=None, sys_row: int = 0,
+                      shadow: bool = True, pairs: Optional[np.ndarray] = None,
+                      idx: Optional[np.ndarray] = None, ngroups: int = 0,
+                      path: Optional[str] = None, shadow_count_only: bool = False) -> dict:
+        """kano_verify_gather: ``verify_shard``, the ranks' all-gather and
+        ``verify_combine`` in one engine call, the all-gather issued by the
+        engine on its stream through the RCCL communicator ``comm_ptr``
+        (an ncclComm_t over ``nranks`` ranks, e.g. torch's
+        ``ProcessGroupNCCL._comm_ptr()``).  Results as ``verify_combine``."""
+        if isinstance(gid, str) and gid == "stored":
+            gid, ngroups = None, nat.STORED_GROUPS
+        elif gid is not None:
+            gid = np.ascontiguousarray(gid, dtype=np.int32)
+            if gid.shape[0] != self.n:
+                raise ValueError("gid must have one entry per pod")
+        self._shard_shadow = bool(shadow)
+        pth = nat.PATHS[path or self.path]
+        mode = (2 if shadow_count_only else 1) if shadow else 0
+        return self._combine_call(
+            lambda idx_p, cnt_p, pairs_p, cap, cnt_ref: self.lib.kano_verify_gather(
+                self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), mode, c_void_p(comm_ptr),
+                int(nranks), idx_p, cnt_p, pairs_p, cap, cnt_ref),
+            "kano_verify_gather", pairs, idx, shadow_count_only)
+
     def checks_shard(self, words_dev_ptr: int, gid=None, sys_row: int = 0,
                      ngroups: int = 0) -> None:
         """kano_checks_shard: this shard's column words from the matrix as
@@ -460,6 +484,17 @@ class DeviceBuild:
         """kano_verify_combine: OR the gathered word sets of ``nranks`` shards
         and return the results like ``verify`` (column lists global, the
         system row and the shadow pairs of this shard)."""
+        out = self._combine_call(
+            lambda idx_p, cnt_p, pairs_p, cap, cnt_ref: self.lib.kano_verify_combine(
+                self.ctx, c_void_p(gathered_dev_ptr), int(nranks), idx_p, cnt_p, pairs_p, cap,
+                cnt_ref),
+            "kano_verify_combine", pairs, idx, shadow_count_only)
+        if not cross:
+            out["user_crosscheck"] = None
+        return out
+
+    def _combine_call(self, call, what, pairs, idx, shadow_count_only) -> dict:
+        """The combine half's outputs (verify_combine, verify_gather)."""
         n = self.n
         if idx is None:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
@@ -471,18 +506,14 @@ class DeviceBuild:
         cap = 0 if pairs is None else pairs.size // 2
         if shadow_count_only:
             cap = -1
-        self._chk(self.lib.kano_verify_combine(self.ctx, c_void_p(gathered_dev_ptr), int(nranks),
-                                               _ptr(idx), _ptr(counts), _ptr(pairs), int(cap),
-                                               byref(cnt) if shadow else None),
-                  "kano_verify_combine")
+        self._chk(call(_ptr(idx), _ptr(counts), _ptr(pairs), int(cap),
+                       byref(cnt) if shadow else None), what)
         out, o = {}, 0
         for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
                                   "system_isolation")):
             k = int(counts[r])
             out[name] = idx[o:o + k] if k >= 0 else None
             o += max(k, 0)
-        if not cross:
-            out["user_crosscheck"] = None
         if shadow:
             k = int(cnt.value)
             out["shadow_count"] = k

@@ -53,6 +53,9 @@ SIGNATURES = {
     "kano_verify_shard": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_int, c_void_p]),
     "kano_verify_combine": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                     c_int64, POINTER(c_int64)]),
+    "kano_verify_gather": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_int, c_void_p,
+                                   c_int32, c_void_p, c_void_p, c_void_p, c_int64,
+                                   POINTER(c_int64)]),
     "kano_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_set_expressions": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kano_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),

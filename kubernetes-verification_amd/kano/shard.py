@@ -17,10 +17,18 @@ lists the results.  system_isolation comes from the rank owning the row;
 policy_shadow's output is ordered by container, so each rank emits its own
 rows' pairs and rank order is the global order.
 
-With the gloo backend (several ranks rehearsing on one device, or CPU-only
-collectives) the words travel through host memory: ``host_staged``.
+With the nccl (RCCL) backend the exchange is native by default: the engine
+runs the shard's checks, the all-gather and the combine in one call
+(kano_verify_gather), issuing ncclAllGather itself on its stream through
+torch's communicator (``ProcessGroupNCCL._comm_ptr()``), so no Python or
+c10d work sits between the shard's last kernel and the combine
+(KANO_NATIVE_EXCHANGE=0 keeps the torch collective).  With the gloo backend
+(several ranks rehearsing on one device, or CPU-only collectives) the words
+travel through host memory: ``host_staged``.
 """
 from __future__ import annotations
+
+import os
 
 from typing import Optional, Tuple
 
@@ -53,7 +61,8 @@ class ShardExchange:
     timing diagnostic, results are partial)."""
 
     def __init__(self, torch, W: int, nranks: int, dist=None, stream=None,
-                 host_staged: Optional[bool] = None, device: str = "cuda"):
+                 host_staged: Optional[bool] = None, device: str = "cuda",
+                 native: Optional[bool] = None):
         self.torch, self.W, self.nranks, self.dist, self.stream = torch, W, nranks, dist, stream
         if host_staged is None:
             host_staged = dist is not None and dist.get_backend() == "gloo"
@@ -63,6 +72,35 @@ class ShardExchange:
         if host_staged:
             self._hw = torch.zeros(3 * W, dtype=torch.int64)
             self._hg = torch.zeros(nranks * 3 * W, dtype=torch.int64)
+        self.comm = None   # ncclComm_t of the native exchange
+        if native is None:
+            native = (dist is not None and not host_staged
+                      and os.environ.get("KANO_NATIVE_EXCHANGE", "1") != "0")
+        if native:
+            self.comm = self._rccl_comm()
+        self.mode = ("emulated" if dist is None else "rccl-native" if self.comm
+                     else "host-staged" if host_staged else "torch-collective")
+
+    def _rccl_comm(self) -> Optional[int]:
+        """torch's RCCL communicator for this device (created by one
+        all-gather, as the first collective on the device does)."""
+        torch, dist = self.torch, self.dist
+        try:
+            if dist.get_backend() != "nccl" or dist.get_world_size() != self.nranks:
+                return None
+            ctx = torch.cuda.stream(self.stream) if self.stream is not None else None
+            if ctx is not None:
+                with ctx:
+                    dist.all_gather_into_tensor(self.gathered, self.words)
+            else:
+                dist.all_gather_into_tensor(self.gathered, self.words)
+            torch.cuda.synchronize()
+            pg = dist.distributed_c10d._get_default_group()
+            be = pg._get_backend(torch.device("cuda", torch.cuda.current_device()))
+            ptr = int(be._comm_ptr())
+            return ptr or None
+        except Exception:   # noqa: BLE001 (no raw communicator: the torch collective)
+            return None
 
     def gather(self) -> None:
         """Every rank's words into ``gathered`` (rank order)."""
@@ -81,6 +119,10 @@ class ShardExchange:
             dist.all_gather_into_tensor(self.gathered, self.words)
 
     def _run(self, eng, gid, sys_row, shadow, count_only, pairs, idx):
+        if self.comm:
+            return eng.verify_gather(self.comm, self.nranks, gid=gid, sys_row=sys_row,
+                                     shadow=shadow, shadow_count_only=count_only, pairs=pairs,
+                                     idx=idx)
         eng.verify_shard(self.words.data_ptr(), gid=gid, sys_row=sys_row, shadow=shadow,
                          shadow_count_only=count_only)
         self.gather()

@@ -27,7 +27,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, name, count_only, q):
+def _worker(rank, world, port, name, count_only, q, backend="gloo", native=None):
     try:
         sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-verification_amd"), HERE]
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -36,7 +36,9 @@ def _worker(rank, world, port, name, count_only, q):
         from kano._engine import DeviceBuild
         from kano._intern import group_ids, intern, tables_from_cluster
         from kano.shard import ShardExchange, row_range
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if backend == "nccl":
+            torch.cuda.set_device(0)
+        dist.init_process_group(backend, rank=rank, world_size=world)
         if name.startswith("C"):
             from kano.synth import KEY_NAMES, make_config
             cl = make_config(name)
@@ -56,7 +58,9 @@ def _worker(rank, world, port, name, count_only, q):
         r0, r1 = row_range(n, world, rank)
         eng = DeviceBuild(t, rows=(r0, r1), build=False, stream=stream.cuda_stream)
         eng.set_groups(gid)
-        x = ShardExchange(torch, (n + 63) // 64, world, dist=dist, stream=stream)
+        x = ShardExchange(torch, (n + 63) // 64, world, dist=dist, stream=stream, native=native)
+        if native and x.mode != "rccl-native":
+            raise RuntimeError(f"native exchange not engaged: {x.mode}")
         out = []
         for _ in range(4):    # the step repeats on the same context (graph capture, replay)
             r = x.verify(eng, gid="stored", sys_row=0, shadow=True, count_only=count_only)
@@ -108,3 +112,29 @@ def test_shard_exchange_across_processes(name, world, count_only):
         if not count_only:
             allp = np.ascontiguousarray(np.concatenate(pairs).astype(np.int32))
             assert sha(allp) == exp["policy_shadow"]["sha256"]
+
+
+@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("name", ["s_sparse_2000", "C2"])
+def test_rccl_exchange_one_rank(name, native):
+    """The nccl (RCCL) backend on the device, one rank (RCCL refuses two
+    ranks on one device): the native exchange (kano_verify_gather: the
+    engine issues ncclAllGather through torch's communicator) and torch's
+    collective, against kano_py's goldens."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), name, False, q, "nccl", native))
+    p.start()
+    rank, out, err = q.get(timeout=300)
+    p.join(timeout=60)
+    assert not err, err
+    exp = expected(name)
+    for r in out:
+        assert index_list_matches(r["all_reachable"], exp["all_reachable"])
+        assert index_list_matches(r["all_isolated"], exp["all_isolated"])
+        assert index_list_matches(r["user_crosscheck"], exp["user_crosscheck"]["result"])
+        assert index_list_matches(r["system_isolation"], exp["system_isolation"]["result"])
+        assert r["shadow_count"] == exp["policy_shadow"]["count"]
+        allp = np.ascontiguousarray(r["pairs"].reshape(-1, 2).astype(np.int32))
+        assert sha(allp) == exp["policy_shadow"]["sha256"]
