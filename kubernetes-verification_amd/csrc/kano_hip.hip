@@ -254,6 +254,8 @@ struct kano_ctx {
   // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
   int xfuse = 0;
   int hfuse = 1;             // independent launches merged (k_lists_allow, k_pods_scatter)
+  int mc_own = 1;            // light Mc rows by their owner (k_mc_own: a thread per row class,
+                             // plain stores) instead of the select-entry scatter (atomics)
   int preclean = 1;          // kano_verify resets the next front end's tables on its tail
   bool front_clean = false;
   std::array<i64, 6> fc_dims{};
@@ -1379,6 +1381,20 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       hipLaunchKernelGGL(k_mc_rows<1>, dim3((unsigned)U), dim3(64), lds, ctx->stream, U,
                          P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
                          P_<int32_t>(ctx->alc), hf, mfma ? 1 : 0, P_<u64>(ctx->Mc), ldMc);
+  } else if (ctx->mc_own && (pods_in_scatter || scatter_on) &&
+             (size_t)ldMc * 8 * (TPB / 64) <= 64 * 1024) {
+    const size_t lds = sizeof(u64) * (size_t)ldMc * (TPB / 64);
+    const McOwnArgs moa{U, P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
+                        P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
+                        H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr,
+                        P_<u64>(ctx->Mc), ldMc};
+    if (pods_in_scatter) {
+      const unsigned nb1 = nblk(P, WPB);
+      hipLaunchKernelGGL(k_pods_own, dim3(nb1 + nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream,
+                         pol_pods_args(ctx), moa, nb1);
+    } else {
+      hipLaunchKernelGGL(k_mc_own, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, moa);
+    }
   } else if (pods_in_scatter) {
     const unsigned nb1 = nblk(P, WPB);
     hipLaunchKernelGGL(k_pods_scatter, dim3(nb1 + nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
@@ -1945,6 +1961,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hosttime") ctx->host_timing = v;
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
+        if (k == "mcown") ctx->mc_own = v;
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
         if (k == "sidepre") ctx->side_pre = v;

@@ -1110,12 +1110,70 @@ __global__ __launch_bounds__(TPB) void k_mc_scatter(McScatterArgs a) {
   mc_scatter_item(a, blockIdx.x);
 }
 
+// The light rows of Mc by their OWNER: one wave per row class ORs the
+// allowed-class lists of S(c) into an LDS row (lanes over the entries of
+// S(c), each walking its policy's list) and stores only the nonzero words
+// (Mc is zeroed before) -- no global atomics: the select-entry scatter's
+// 57,644 device-scope atomics cost 25-28 us at C3, and writing whole rows
+// (k_mc_rows) stores the 58 MB of mostly-zero words.
+struct McOwnArgs {
+  i64 U;
+  const i64* soffc;
+  const int32_t* slist;
+  const i64* alcoff;
+  const int32_t* alc;
+  const int32_t* mcnt;
+  const int32_t* hflag;
+  u64* Mc;
+  i64 ldMc;
+};
+// vb: the block index within this job; NW = TPB / 64 rows of ldMc words of
+// dynamic LDS (mrow) per block
+__device__ __forceinline__ void mc_own_item(const McOwnArgs& a, i64 vb, u64* mrow) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const i64 c = vb * (TPB / 64) + wv;
+  if (c >= a.U) return;                               // wave-uniform; no block barrier below
+  if (a.mcnt[c] == 0 || (a.hflag && a.hflag[c])) return;
+  const i64 e0 = a.soffc[c], e1 = a.soffc[c + 1];
+  if (e1 == e0) return;
+  u64* row = mrow + (i64)wv * a.ldMc;
+  for (i64 w = lane; w < a.ldMc; w += 64) row[w] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  for (i64 e = e0 + lane; e < e1; e += 64) {
+    const int32_t p = a.slist[e];
+    const i64 q1 = a.alcoff[p + 1];
+    for (i64 q = a.alcoff[p]; q < q1; ++q) {
+      const int32_t ca = a.alc[q];
+      atomicOr(&row[ca >> 6], 1ull << (ca & 63));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  u64* dst = a.Mc + c * a.ldMc;
+  for (i64 w = lane; w < a.ldMc; w += 64) {
+    const u64 v = row[w];
+    if (v) dst[w] = v;
+  }
+}
+__global__ __launch_bounds__(TPB) void k_mc_own(McOwnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u64 mrow[];
+  mc_own_item(a, blockIdx.x, mrow);
+}
+
 // k_pol_pods and k_mc_scatter in one launch (independent; one wave per
 // item): blocks [0, nb1) build the flat allowed-pod lists
 __global__ __launch_bounds__(TPB) void k_pods_scatter(PolPodsArgs a, McScatterArgs b,
                                                       unsigned nb1) {
   if (blockIdx.x < nb1) pol_pods_item(a, blockIdx.x);
   else mc_scatter_item(b, blockIdx.x - nb1);
+}
+// k_pol_pods and k_mc_own in one launch: blocks [0, nb1) build the flat
+// allowed-pod lists, the rest one thread per row class
+__global__ __launch_bounds__(TPB) void k_pods_own(PolPodsArgs a, McOwnArgs b, unsigned nb1) {
+  extern __shared__ __attribute__((aligned(16))) u64 mrow[];
+  if (blockIdx.x < nb1) pol_pods_item(a, blockIdx.x);
+  else mc_own_item(b, blockIdx.x - nb1, mrow);
 }
 
 // The same rows written whole: one wave per row class builds its row in LDS
