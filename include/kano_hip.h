@@ -171,7 +171,14 @@ int kano_conflict(kano_ctx* ctx, int* raises);
  * the pairs are copied to shadow_pairs if count <= shadow_cap (otherwise
  * fetch them with kano_shadow_fetch).  shadow_cap < 0 asks for the count
  * only: every subset test still runs, the pairs are not emitted (broad
- * selectors give ~1e11 of them; kano_shadow_fetch then fails). */
+ * selectors give ~1e11 of them; kano_shadow_fetch then fails).
+ * Completion: the call returns once idx, counts and the pairs are in host
+ * memory.  The matrix write (model.py:158-160) may still be running on the
+ * context's stream then (KANO_TUNE=async=0 waits for it): every later call
+ * on the context is ordered after it, and every entry point other than
+ * kano_verify / kano_verify_shard / kano_verify_combine / kano_verify_gather /
+ * kano_info waits for it first, so no
+ * caller can observe an unfinished matrix. */
 int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
                 int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count);
@@ -236,6 +243,13 @@ int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups);
  * when the context was created with KANO_TUNE=timing=1 (each event costs
  * host time on the launch path); slot 6 always. */
 int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
+
+/* k_rows launch times (the matrix write of model.py:158-160; HIP events on
+ * its stream) accumulated over the launches since the last reset: out[4] =
+ * [sum ms, launches, min ms, max ms]; reset != 0 zeroes the sums after
+ * reading.  Waits for the context's work first (a benchmark reads it after
+ * its timed region, kano_verify's own launches stay asynchronous). */
+int kano_rows_timing(kano_ctx* ctx, double* out /* 4 */, int reset);
 
 /* Multi-hop reachability, replacing kubesv's
  * `path` relation (kubesv/kubesv/constraint.py:233-237: path :- edge;

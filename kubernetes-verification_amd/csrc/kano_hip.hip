@@ -27,6 +27,7 @@
 //            allowed-pod lists (light) or a copy (heavy), streamed to the
 //            member rows; column OR / NAND folded in
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <functional>
@@ -128,6 +129,7 @@ struct kano_ctx {
   int rows_early = 0;        // kano_verify: launch k_rows right after the lists (on stream2)
   int prio = 0;              // checks stream high priority, matrix-write stream low
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
+  int sh_stage = 1;          // the pairwise test with the block's lists staged in LDS
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
   int rows_store = 2;        // k_rows stores: 2 non-temporal (measured C3: 253 vs 263-270 us
@@ -290,6 +292,25 @@ struct kano_ctx {
   bool rows_overlap = false;
   hipEvent_t ev_sizes = nullptr;
   hipEvent_t ev_sync = nullptr;    // sync() with spin_wait
+  // asynchronous completion (knob async, default on): kano_verify returns once
+  // its host results (index lists, pairs) are in host memory; the matrix
+  // write ends on the engine stream, behind which every later engine
+  // operation queues, and every other entry point settles it first
+  int async_rows = 1;
+  bool async_pending = false;
+  hipEvent_t ev_tail = nullptr;    // the result copies of kano_verify's tail
+  // k_rows' launch times (ev[7] -> ev[8]), resolved once the launch is known
+  // to be complete: the last one, and sums since kano_rows_timing's reset
+  bool rows_time_pending = false;
+  // k_rows timed by its own dispatch (hipExtLaunchKernel's start / stop
+  // events: no marker packets around the launch; knob extev); the tail's
+  // fork point is then a marker of its own
+  int rows_extev = 1;
+  hipEvent_t ev_rows_fork = nullptr;
+  hipEvent_t rows_fork = nullptr;    // what the tail waits on (ev[7] or ev_rows_fork)
+  float rows_ms_last = 0.f;
+  double rows_ms_sum = 0.0, rows_ms_min = 0.0, rows_ms_max = 0.0;
+  i64 rows_ms_n = 0;
   int spin_wait = 0;   // kano_verify: the size slots reached the host buffer
   // kano_verify halves (kano_verify_shard -> kano_verify_combine)
   bool vs_open = false, vs_shadow = false, vs_cross_want = false, vs_cross_on = false;
@@ -675,6 +696,30 @@ int sync(kano_ctx* ctx) {
     return wait_event(ctx, ctx->ev_sync);
   }
   KCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// an asynchronously completing kano_verify's matrix write, finished
+int settle(kano_ctx* ctx) {
+  if (!ctx->async_pending) return 0;
+  ctx->async_pending = false;
+  KCHK(hipSetDevice(ctx->device));
+  return sync(ctx);
+}
+
+// the last k_rows launch's time, once its end event is complete (blocks
+// until it is)
+int resolve_rows_time(kano_ctx* ctx) {
+  if (!ctx->rows_time_pending) return 0;
+  ctx->rows_time_pending = false;
+  KCHK(hipEventSynchronize(ctx->ev[8]));
+  float ms = 0.f;
+  KCHK(hipEventElapsedTime(&ms, ctx->ev[7], ctx->ev[8]));
+  ctx->rows_ms_last = ms;
+  if (ctx->rows_ms_n == 0 || ms < ctx->rows_ms_min) ctx->rows_ms_min = ms;
+  if (ctx->rows_ms_n == 0 || ms > ctx->rows_ms_max) ctx->rows_ms_max = ms;
+  ctx->rows_ms_sum += ms;
+  ctx->rows_ms_n += 1;
   return 0;
 }
 
@@ -1530,7 +1575,10 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
   int nt = ctx->rows_nt;
   if (nt == 0) nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
-  KCHK(hipEventRecord(ctx->ev[7], rs));
+  KTRY(resolve_rows_time(ctx));   // the previous launch's pair is reused
+  const bool ext = ctx->rows_extev && !ctx->rows_order;
+  ctx->rows_fork = ext ? ctx->ev_rows_fork : ctx->ev[7];
+  KCHK(hipEventRecord(ctx->rows_fork, rs));
   const size_t lds = sizeof(u64) * cww;
   if (ctx->rows_order && ctx->heavy_count == 0 && rl <= (i64)INT32_MAX) {
     // pod order: one row per block, consecutive blocks on consecutive rows
@@ -1543,6 +1591,7 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
     KCHK(hipEventRecord(ctx->ev[8], rs));
     if (rs != ctx->stream) KCHK(hipEventRecord(ctx->ev_rows, rs));
     ctx->rows_timed = true;
+    ctx->rows_time_pending = true;
     return 0;
   }
   dim3 grid((unsigned)ctx->wi_total, ncc);
@@ -1556,13 +1605,22 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
       grid.x = (unsigned)g;
     }
   }
-  if (nt == 1024) hipLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, a);
-  else if (nt == 512) hipLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, a);
-  else hipLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, a);
-  KLAUNCH();
-  KCHK(hipEventRecord(ctx->ev[8], rs));
+  if (ext) {   // timed by the dispatch itself
+    hipEvent_t e0 = ctx->ev[7], e1 = ctx->ev[8];
+    if (nt == 1024) hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, a);
+    else if (nt == 512) hipExtLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, e0, e1, 0, a);
+    else hipExtLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, e0, e1, 0, a);
+    KLAUNCH();
+  } else {
+    if (nt == 1024) hipLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, a);
+    else if (nt == 512) hipLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, a);
+    else hipLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, a);
+    KLAUNCH();
+    KCHK(hipEventRecord(ctx->ev[8], rs));
+  }
   if (rs != ctx->stream) KCHK(hipEventRecord(ctx->ev_rows, rs));
   ctx->rows_timed = true;
+  ctx->rows_time_pending = true;
   return 0;
 }
 
@@ -1570,7 +1628,7 @@ int ensure_built(kano_ctx* ctx) {
   if (!ctx) return -EINVAL;
   if (!ctx->built) return fail(ctx, -EINVAL, "matrix not built");
   KCHK(hipSetDevice(ctx->device));
-  return 0;
+  return settle(ctx);
 }
 
 // order the main stream after the matrix write
@@ -1948,6 +2006,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "early") ctx->rows_early = v;
         if (k == "prio") ctx->prio = v;
         if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
+        if (k == "shstage") ctx->sh_stage = v;
         if (k == "grm") ctx->grange_m = v;
         if (k == "fold") ctx->fold_mode = v;
         if (k == "mcrows") ctx->mc_rows = v;
@@ -1961,6 +2020,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hosttime") ctx->host_timing = v;
         if (k == "fork") ctx->fork_checks = v;
         if (k == "spin") ctx->spin_wait = v;
+        if (k == "async") ctx->async_rows = v;
+        if (k == "extev") ctx->rows_extev = v;
         if (k == "mcown") ctx->mc_own = v;
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
@@ -2027,6 +2088,8 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sync, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rows_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork3, hipEventDisableTiming) != hipSuccess ||
@@ -2119,6 +2182,8 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
+  if (ctx->ev_tail) (void)hipEventDestroy(ctx->ev_tail);
+  if (ctx->ev_rows_fork) (void)hipEventDestroy(ctx->ev_rows_fork);
   if (ctx->ev_sizes) (void)hipEventDestroy(ctx->ev_sizes);
   if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
   if (ctx->ev_fork3) (void)hipEventDestroy(ctx->ev_fork3);
@@ -2133,6 +2198,7 @@ const char* kano_last_error(const kano_ctx* ctx) { return ctx ? ctx->err.c_str()
 int kano_set_stream(kano_ctx* ctx, void* s) {
   if (!ctx) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   KCHK(hipStreamSynchronize(ctx->stream2));
   ctx->rows_pending = false;
   if (ctx->own_stream && ctx->stream) {
@@ -2155,6 +2221,7 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   if (n < 0 || ncols < 0 || n >= (int64_t)INT32_MAX / 2 || (n * ncols > 0 && !pod_val))
     return fail(ctx, -EINVAL, "kano_set_pods: bad arguments");
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   ctx->n = n;
   ctx->W = (n + 63) / 64;
   ctx->ldM = (std::max<i64>(ctx->ld_align,
@@ -2201,6 +2268,7 @@ int kano_set_expressions(kano_ctx* ctx, int32_t E, const int32_t* col, const int
   if (E < 0 || (E > 0 && (!col || !op || !off))) return fail(ctx, -EINVAL, "kano_set_expressions");
   if (E == 0) return 0;
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   const i64 n = ctx->n, nc = ctx->ncols;
   for (int32_t e = 0; e < E; ++e) {
     if (col[e] >= nc || op[e] < 0 || op[e] > 3 || off[e + 1] < off[e])
@@ -2380,6 +2448,7 @@ int kano_set_policies(kano_ctx* ctx, int64_t P, const int64_t* sel_off, const in
   if (!ctx->have_pods) return fail(ctx, -EINVAL, "kano_set_policies before kano_set_pods");
   if (P < 0 || !sel_off || !alw_off) return fail(ctx, -EINVAL, "kano_set_policies: bad arguments");
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   ctx->P = P;
   ctx->PB = (P + 63) / 64;
   KTRY(prepare_side(ctx, P, sel_off, sel_col, sel_val, ctx->rc, ctx->sm));
@@ -2834,7 +2903,10 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     // may yield to the grouped count)
     const i64 nvb = sp.nt * SH_ITEMS;
     const i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
-    if (ctx->sh_items == 1 || ctx->vs_count_only)
+    if ((ctx->sh_items == 1 || ctx->vs_count_only) && ctx->sh_stage)
+      hipLaunchKernelGGL(k_shadow_test1s, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
+                         P_<i64>(ctx->tcnt));
+    else if (ctx->sh_items == 1 || ctx->vs_count_only)
       hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
                          P_<i64>(ctx->tcnt));
     else
@@ -2940,6 +3012,7 @@ int kano_shadow_lists(kano_ctx* ctx, int64_t n_lists, int64_t nbits, int64_t P,
   if (n_lists < 0 || nbits < 0 || P < 0 || !soff || n_lists >= (int64_t)INT32_MAX / 2)
     return fail(ctx, -EINVAL, "kano_shadow_lists: bad arguments");
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   const i64 nnz = soff[n_lists];
   for (i64 e = 0; e < nnz; ++e)
     if (slist[e] < 0 || slist[e] >= P)
@@ -3255,7 +3328,8 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
 }
 
 int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx, int64_t* counts,
-                int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count) {
+                int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count,
+                bool may_async = false) {
   if (!ctx->vs_open) return fail(ctx, -EINVAL, "kano_verify_combine without kano_verify_shard");
   ctx->vs_open = false;
   const i64 n = ctx->n, W = ctx->W, nb = ctx->vs_nb;
@@ -3313,7 +3387,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   hipEvent_t tail_ev = signalled ? nullptr : ctx->ev_sizes;
   if (!ctx->vs_early && !pre_tail) {
     KTRY(launch_rows(ctx));
-    if (!tail_ev && ctx->rows_timed && !ctx->rows_overlap) tail_ev = ctx->ev[7];
+    if (!tail_ev && ctx->rows_timed && !ctx->rows_overlap) tail_ev = ctx->rows_fork;
   }
   if (!tail_ev && ctx->side_tail && !pre_tail) {
     SegPause pause(ctx);
@@ -3367,6 +3441,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         cs));
+  // asynchronous completion: the host waits for the result copies only; the
+  // matrix write (and the next front end's fills) end on the engine streams
+  const bool async = may_async && ctx->async_rows && cs != ctx->stream && !ctx->graphs;
+  if (async) KCHK(hipEventRecord(ctx->ev_tail, cs));
   // the next front end's first fills, beside the matrix write (the next
   // build checks front_dims before skipping them)
   if (cs != ctx->stream && ctx->preclean && !ctx->graphs) {
@@ -3386,6 +3464,11 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
   }
   KTRY(join_rows(ctx));  // the matrix is part of the result
+  if (async) {
+    KTRY(wait_event(ctx, ctx->ev_tail));
+    ctx->async_pending = true;
+    return 0;
+  }
   return sync(ctx);
 }
 }  // namespace
@@ -3405,7 +3488,8 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr,
                     shadow_cap < 0));
   const auto t1 = clk::now();
-  const int rc = verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count);
+  const int rc =
+      verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count, true);
   if (ctx->host_timing) {
     const auto t2 = clk::now();
     auto us = [](clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
@@ -3437,8 +3521,10 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
   if (ctx->vs_open && ctx->vs_shadow && !shadow_count)
     return fail(ctx, -EINVAL, "kano_verify_combine: shadow_count is NULL but the shard ran policy_shadow");
   SegScope seg(ctx);
+  // (gathered_dev is written on the context's stream: the combine may
+  // complete asynchronously like kano_verify)
   return verify_back(ctx, reinterpret_cast<const u64*>(gathered_dev), nranks, idx, counts,
-                     shadow_pairs, shadow_cap, shadow_count);
+                     shadow_pairs, shadow_cap, shadow_count, true);
 }
 
 int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
@@ -3470,7 +3556,7 @@ int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngro
     }
   }
   return verify_back(ctx, P_<u64>(ctx->xg), nranks, idx, counts, shadow_pairs, shadow_cap,
-                     shadow_count);
+                     shadow_count, true);
 }
 
 int kano_checks_shard(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, int64_t sys_row,
@@ -3535,6 +3621,7 @@ int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups) {
   const i64 n = ctx->n;
   if (n > 0 && !gid) return fail(ctx, -EINVAL, "kano_set_groups: gid is NULL");
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   int32_t G = 0;
   for (i64 i = 0; i < n; ++i) {
     if (gid[i] < 0) return fail(ctx, -EINVAL, "kano_set_groups: negative group id");
@@ -3567,6 +3654,7 @@ void kano_host_free(void* p) {
 int kano_stage_times(kano_ctx* ctx, float* ms) {
   if (!ctx || !ms) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
   KTRY(join_rows(ctx));
   KTRY(sync(ctx));
   for (int k = 0; k < 8; ++k) ms[k] = 0.f;
@@ -3575,10 +3663,29 @@ int kano_stage_times(kano_ctx* ctx, float* ms) {
       for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&ms[k], ctx->ev[k], ctx->ev[k + 1]);
       (void)hipEventElapsedTime(&ms[5], ctx->ev[0], ctx->ev[4]);
     }
-    if (ctx->rows_timed) (void)hipEventElapsedTime(&ms[6], ctx->ev[7], ctx->ev[8]);
+    KTRY(resolve_rows_time(ctx));
+    if (ctx->rows_timed) ms[6] = ctx->rows_ms_last;
   }
   if (ctx->stage_timing && ctx->shadow_total >= 0)
     (void)hipEventElapsedTime(&ms[4], ctx->ev[5], ctx->ev[6]);
+  return 0;
+}
+
+int kano_rows_timing(kano_ctx* ctx, double* out, int reset) {
+  if (!ctx || !out) return -EINVAL;
+  KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
+  KTRY(join_rows(ctx));
+  KTRY(sync(ctx));
+  KTRY(resolve_rows_time(ctx));
+  out[0] = ctx->rows_ms_sum;
+  out[1] = (double)ctx->rows_ms_n;
+  out[2] = ctx->rows_ms_min;
+  out[3] = ctx->rows_ms_max;
+  if (reset) {
+    ctx->rows_ms_sum = ctx->rows_ms_min = ctx->rows_ms_max = 0.0;
+    ctx->rows_ms_n = 0;
+  }
   return 0;
 }
 

@@ -2323,6 +2323,133 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
   }
 }
 
+// The same test with the block's select-list data staged in LDS first: the
+// classes of the block's 256 pairs (pfoff, soffc, mcnt), then their S(c)
+// entries (policy, allowed-class count, list offset, first allowed class) --
+// one short dependent chain per block instead of ~10 dependent loads per
+// thread.  A thread then reads its pair's class and policies from LDS and
+// usually decides with one global load (the first allowed class of k missing
+// from AC[j]).  Blocks whose class range or S(c) segment does not fit fall
+// back to the global form.
+constexpr int SHS_CLS = TPB + 2;
+constexpr int SHS_SEG = 1024;
+constexpr int SHS_U = 8;
+__global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
+                                                      i64* __restrict__ tile_cnt) {
+  __shared__ i64 sm[4];
+  __shared__ i64 rng[2];
+  __shared__ i64 s_pf[SHS_CLS];
+  __shared__ i64 s_so[SHS_CLS];
+  __shared__ int32_t s_mc[SHS_CLS];
+  __shared__ i64 s_ao[SHS_SEG];
+  __shared__ int32_t s_pol[SHS_SEG];
+  __shared__ int32_t s_nca[SHS_SEG];
+  __shared__ int32_t s_x0[SHS_SEG];
+  if (a.shg_G && shg_grouped(a.shg_G, a.shg_err, a.shg_nf, a.shg_force)) return;
+  const i64 nvb = (nflags + SH_TILE - 1) / SH_TILE * SH_ITEMS;
+  for (i64 vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    const i64 tile = vb / SH_ITEMS, part = vb % SH_ITEMS;
+    const i64 b0 = tile * SH_TILE + part * TPB;
+    if (b0 >= nflags) break;                     // block-uniform (b0 rises with vb)
+    const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
+    if (threadIdx.x == 0) rng[0] = class_of_pair(a.pfoff, 0, a.U - 1, b0);
+    if (threadIdx.x == 64) rng[1] = class_of_pair(a.pfoff, 0, a.U - 1, b1);
+    __syncthreads();
+    const i64 c0 = rng[0], c1 = rng[1];
+    const i64 ncls = c1 - c0 + 1;
+    const bool staged_cls = ncls + 1 <= SHS_CLS;
+    i64 seg0 = 0, nseg = SHS_SEG + 1;
+    if (staged_cls) {
+      for (i64 k = threadIdx.x; k <= ncls; k += TPB) {
+        s_pf[k] = a.pfoff[c0 + k];
+        s_so[k] = a.soffc[c0 + k];
+        if (k < ncls) s_mc[k] = a.mcnt[c0 + k];
+      }
+      __syncthreads();
+      seg0 = s_so[0];
+      nseg = s_so[ncls] - seg0;
+    }
+    const bool staged = staged_cls && nseg <= SHS_SEG;   // block-uniform
+    if (staged) {
+      for (i64 e = threadIdx.x; e < nseg; e += TPB) {
+        const int32_t p = a.slist[seg0 + e];
+        const int32_t cnt = a.nca[p];
+        const i64 ao = a.alcoff[p];
+        s_pol[e] = p;
+        s_nca[e] = cnt;
+        s_ao[e] = ao;
+        s_x0[e] = cnt > 0 ? a.alc[ao] : 0;
+      }
+      __syncthreads();
+    }
+    const i64 t = b0 + threadIdx.x;
+    int f = 0;
+    i64 c = -1;
+    if (t < nflags) {
+      if (staged) {
+        i64 lo = 0, hi = ncls - 1;               // last class with pfoff <= t
+        while (lo < hi) {
+          const i64 mid = (lo + hi + 1) >> 1;
+          if (s_pf[mid] <= t) lo = mid; else hi = mid - 1;
+        }
+        c = c0 + lo;
+        const i64 e0 = s_so[lo] - seg0, s = s_so[lo + 1] - s_so[lo], q = t - s_pf[lo];
+        const i64 x = q / s, y = q - x * s;
+        if (s_mc[lo] > 0 && x != y) {
+          const int32_t j = s_pol[e0 + x], kk = s_pol[e0 + y];
+          const int32_t ck = s_nca[e0 + y];
+          if (j != kk) {
+            if (ck == 0) {
+              f = 1;
+            } else if (ck <= s_nca[e0 + x]) {
+              const u64* aj = a.AC + (i64)j * a.ldC;
+              int32_t xe = s_x0[e0 + y];
+              bool ok = (aj[xe >> 6] >> (xe & 63)) & 1ull;
+              // the rest of k's list SHS_U entries at a time: the loads of
+              // a round are independent (a subset's full walk is the long
+              // pole of a wave)
+              const int32_t* L = a.alc + s_ao[e0 + y];
+              for (int32_t e = 1; ok && e < ck; e += SHS_U) {
+                int32_t xs[SHS_U];
+#pragma unroll
+                for (int u = 0; u < SHS_U; ++u) xs[u] = e + u < ck ? L[e + u] : xe;
+                u64 ws[SHS_U];
+#pragma unroll
+                for (int u = 0; u < SHS_U; ++u) ws[u] = aj[xs[u] >> 6];
+#pragma unroll
+                for (int u = 0; u < SHS_U; ++u) ok = ok && ((ws[u] >> (xs[u] & 63)) & 1ull);
+              }
+              f = ok;
+            }
+          }
+        }
+      } else {
+        c = class_of_pair(a.pfoff, c0, c1, t);
+        const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
+        const i64 x = q / s, y = q - x * s;
+        if (a.mcnt[c] > 0 && x != y) {
+          const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
+          f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+        }
+      }
+      if (a.flags) a.flags[t] = (uint8_t)f;   // null: count only (T[c])
+    }
+    const i64 cw = __shfl(c, 0, 64);
+    if (__all(c == cw || c < 0)) {
+      const int r = wave_sum(f);
+      if ((threadIdx.x & 63) == 0 && r && cw >= 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[cw]), (unsigned long long)r);
+    } else if (f) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
+    }
+    const i64 tot = block_sum((i64)f, sm);
+    if (threadIdx.x == 0 && tot)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
+    if ((i64)gridDim.x >= nvb) break;           // one virtual block per block (uniform)
+    __syncthreads();                             // LDS reused by the next virtual block
+  }
+}
+
 // ---------------------------------------------------------------------------
 // policy_shadow's pair count without the pairs (kano_verify, shadow_cap < 0):
 // algorithm.py:58-80 counts, per pod i, the ordered pairs j != k of S(i) with

@@ -530,6 +530,15 @@ class DeviceBuild:
         self._chk(self.lib.kano_conflict(self.ctx, byref(v)), "kano_conflict")
         return bool(v.value)
 
+    def rows_timing(self, reset: bool = False) -> dict:
+        """k_rows launch times (HIP events) since the last reset: sum, count,
+        min, max (ms); waits for the context's work."""
+        out = np.zeros(4, dtype=np.float64)
+        self._chk(self.lib.kano_rows_timing(self.ctx, _ptr(out), int(bool(reset))),
+                  "kano_rows_timing")
+        return dict(sum_ms=float(out[0]), launches=int(out[1]), min_ms=float(out[2]),
+                    max_ms=float(out[3]))
+
     def stage_times(self) -> dict:
         ms = np.zeros(8, dtype=np.float32)
         self._chk(self.lib.kano_stage_times(self.ctx, _ptr(ms)), "kano_stage_times")

@@ -72,6 +72,7 @@ SIGNATURES = {
     "kano_added_policy_sets": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "kano_import_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
+    "kano_rows_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),
 }

@@ -271,7 +271,7 @@ def _lists(cs, which):
 # --- k_rows variants that only fire on wide matrices ------------------------
 @pytest.mark.parametrize("tune", [
     "nt=512", "nt=1024", "cww=64", "cww=16", "nt=1024,cww=32", "cww=16,ch=3",
-    "persist=8", "store=0", "store=3", "xfuse=1", "sig=0", "hfuse=0",
+    "persist=8", "store=0", "store=3", "xfuse=1", "sig=0", "hfuse=0", "shstage=0", "extev=0",
 ])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):

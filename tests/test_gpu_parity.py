@@ -192,6 +192,52 @@ def test_verify_fused_c2(cap):
     pin.close()
 
 
+@pytest.mark.parametrize("tune", ["async=1", "async=0"])
+def test_verify_async_completion(tune, monkeypatch):
+    """kano_verify returns once its host results are in host memory, its
+    matrix write still queued (async=1, the default): back-to-back calls, a
+    matrix read right after, an upload between calls, a two-hop product
+    reading the source's matrix from another context and the k_rows timing
+    all see the finished matrix."""
+    monkeypatch.setenv("KANO_TUNE", tune)
+    from kano._engine import DeviceBuild, PinnedBuffer
+    from kano._intern import tables_from_cluster
+    from kano.synth import make_config, KEY_NAMES
+    exp = expected("C2")
+    cl = make_config("C2")
+    n = cl.n
+    _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
+    tables = tables_from_cluster(cl)
+    eng = DeviceBuild(tables, build=False)
+    pin = PinnedBuffer((1 << 22) * 8)
+    pairs = pin.view(np.int32, 2 << 22)
+    eng.set_groups(gid)
+    eng.rows_timing(reset=True)
+    for k in range(4):
+        r = eng.verify("stored", sys_row=0, shadow=True, pairs=pairs)
+        assert r["all_isolated"].tolist() == exp["all_isolated"]
+        assert r["shadow_count"] == exp["policy_shadow"]["count"]
+        assert sha(np.ascontiguousarray(r["pairs"])) == exp["policy_shadow"]["sha256"]
+        if k == 1:
+            assert sha(eng.rows(0, n)) == exp["M_sha256"]
+        if k == 2:
+            eng.upload(tables)          # an upload between two calls
+            eng.set_groups(gid)
+    rt = eng.rows_timing()
+    assert rt["launches"] == 4 and 0 < rt["min_ms"] <= rt["max_ms"]
+    assert sha(eng.rows(0, n)) == exp["M_sha256"]
+    r = eng.verify("stored", sys_row=0, shadow=True, pairs=pairs)
+    # another context reads this one's matrix right after the call (one hop
+    # of kano_path: the matrix itself)
+    dst = DeviceBuild.empty(n)
+    info = np.zeros(8, dtype=np.int64)
+    assert eng.lib.kano_path(eng.ctx, dst.ctx, 1, 0, info.ctypes.data) == 0
+    assert sha(dst.rows(0, n)) == exp["M_sha256"]
+    dst.close()
+    eng.close()
+    pin.close()
+
+
 @pytest.mark.parametrize("tune", ["xfuse=0", "xfuse=1"])
 def test_verify_declared_groups_checked(tune, monkeypatch):
     """A group id outside the declared [0, ngroups) is an error, not a fault
@@ -500,7 +546,8 @@ def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("tune", ["", "sig=0", "xfuse=1,forklate=0", "alistside=1", "hfuse=0,preclean=0"])
+@pytest.mark.parametrize("tune", ["", "sig=0", "xfuse=1,forklate=0", "alistside=1", "hfuse=0,preclean=0",
+                                  "shstage=0,async=0,extev=0"])
 @pytest.mark.parametrize("n,P", [(1, 0), (1, 1), (2, 3), (5, 1), (63, 7), (64, 64), (65, 9),
                                  (130, 40)])
 def test_verify_small_shapes_vs_oracle(n, P, tune, monkeypatch):
