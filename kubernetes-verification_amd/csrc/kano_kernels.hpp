@@ -2202,14 +2202,35 @@ __device__ __forceinline__ i64 class_of_pair(const i64* __restrict__ pfoff, i64 
   return lo;
 }
 
+// last class c in [lo, hi] with pfoff[c] <= t (pfoff[lo] <= t), searched by
+// one whole wave (uniform arguments): 64 pivots per round, so the 21.5k
+// classes of C3 take 3 dependent loads instead of the 15 of a binary search
+// (the block's first loads, before any test can start)
+__device__ __forceinline__ i64 wave_class_of(const i64* __restrict__ pfoff, i64 lo, i64 hi,
+                                             i64 t) {
+  const int lane = threadIdx.x & 63;
+  while (hi > lo) {
+    const i64 step = (hi - lo + 64) / 64;
+    const i64 idx = lo + (i64)lane * step;
+    const bool ok = idx <= hi && pfoff[idx] <= t;
+    const u64 m = __ballot(ok);                 // a prefix of the lanes (lane 0 set)
+    lo += (i64)(63 - __builtin_clzll(m)) * step;
+    hi = min(hi, lo + step - 1);
+  }
+  return lo;
+}
+
 // the class range of this block's tile: two searches over all classes, by
 // two waves, then every thread searches only inside the range
 __device__ __forceinline__ void tile_class_range(const i64* __restrict__ pfoff, i64 U,
                                                  i64 nflags, i64* s_rng) {
   const i64 b0 = (i64)blockIdx.x * SH_TILE;
   const i64 b1 = min(b0 + SH_TILE, nflags) - 1;
-  if (threadIdx.x == 0) s_rng[0] = class_of_pair(pfoff, 0, U - 1, b0);
-  if (threadIdx.x == 64) s_rng[1] = class_of_pair(pfoff, 0, U - 1, b1);
+  const int wv = threadIdx.x >> 6;
+  if (wv < 2) {
+    const i64 c = wave_class_of(pfoff, 0, U - 1, wv == 0 ? b0 : b1);
+    if ((threadIdx.x & 63) == 0) s_rng[wv] = c;
+  }
   __syncthreads();
 }
 
@@ -2290,8 +2311,11 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
     const i64 b0 = tile * SH_TILE + part * TPB;
     if (b0 >= nflags) break;                     // block-uniform (b0 rises with vb)
     const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
-    if (threadIdx.x == 0) rng[0] = class_of_pair(a.pfoff, 0, a.U - 1, b0);
-    if (threadIdx.x == 64) rng[1] = class_of_pair(a.pfoff, 0, a.U - 1, b1);
+    if ((threadIdx.x >> 6) < 2) {
+      const int wv = threadIdx.x >> 6;
+      const i64 cr = wave_class_of(a.pfoff, 0, a.U - 1, wv == 0 ? b0 : b1);
+      if ((threadIdx.x & 63) == 0) rng[wv] = cr;
+    }
     __syncthreads();
     const i64 t = b0 + threadIdx.x;
     int f = 0;
@@ -2352,8 +2376,11 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
     const i64 b0 = tile * SH_TILE + part * TPB;
     if (b0 >= nflags) break;                     // block-uniform (b0 rises with vb)
     const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
-    if (threadIdx.x == 0) rng[0] = class_of_pair(a.pfoff, 0, a.U - 1, b0);
-    if (threadIdx.x == 64) rng[1] = class_of_pair(a.pfoff, 0, a.U - 1, b1);
+    if ((threadIdx.x >> 6) < 2) {
+      const int wv = threadIdx.x >> 6;
+      const i64 cr = wave_class_of(a.pfoff, 0, a.U - 1, wv == 0 ? b0 : b1);
+      if ((threadIdx.x & 63) == 0) rng[wv] = cr;
+    }
     __syncthreads();
     const i64 c0 = rng[0], c1 = rng[1];
     const i64 ncls = c1 - c0 + 1;
