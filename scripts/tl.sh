@@ -9,7 +9,7 @@ for t in "$@"; do
   rm -rf gpurun_out/tl
   KANO_TUNE="$t" timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/tl -o run \
     --output-format csv -- python3 bench.py --steps 6 --warmup 2 --cpu-baseline 0 \
-    --config ${CFG:-C3} > gpurun_out/tl.log 2>&1
+    --config ${CFG:-C3} ${EXTRA:-} > gpurun_out/tl.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "$t rc=$rc"; tail -5 gpurun_out/tl.log; exit $rc; }
   echo "== $t"
   python3 scripts/timeline.py $(find gpurun_out/tl -name "*kernel_trace.csv" | head -1) $nk
