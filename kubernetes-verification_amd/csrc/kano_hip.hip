@@ -1583,7 +1583,9 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
   if (ctx->rows_order && ctx->heavy_count == 0 && rl <= (i64)INT32_MAX) {
     // pod order: one row per block, consecutive blocks on consecutive rows
     a.rcls = P_<int32_t>(ctx->rc.cls);
-    const dim3 g((unsigned)rl, ncc);
+    a.nitems = rl;
+    if (ctx->rows_order == 2) a.probe = 4;   // XCD-local sweeps
+    const dim3 g((unsigned)(ctx->rows_order == 2 ? (rl + 7) / 8 * 8 : rl), ncc);
     if (nt == 1024) hipLaunchKernelGGL(k_rows_ord<1024>, g, dim3(1024), lds, rs, a);
     else if (nt == 512) hipLaunchKernelGGL(k_rows_ord<512>, g, dim3(512), lds, rs, a);
     else hipLaunchKernelGGL(k_rows_ord<256>, g, dim3(256), lds, rs, a);

@@ -1926,17 +1926,25 @@ __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   }
 }
 
-// The matrix write in pod order (light classes only): block b writes row
-// r0 + b, column chunk blockIdx.y, after building its class's row in LDS.
-// Consecutive blocks write consecutive rows and every lane stores 32
-// contiguous bytes (two 16-byte stores): measured 6.6 TB/s for that store
-// shape against 5.2-5.5 TB/s for 16 bytes per lane or rows in class order
-// (profiles/r02_store_ceiling.txt).  A class row is rebuilt for each member
-// (the list walk is cheap next to the 8*W-byte store).
+// The matrix write in pod order (light classes only): block b writes one
+// row, column chunk blockIdx.y, after building its class's row in LDS.
+// Rows in order measured 5.2-5.6 TB/s against 4.7-5.0 for k_rows' class
+// order (profiles/r02_store_xcd_local.txt); xcd != 0 deals the rows so that
+// the blocks of one XCD (b mod 8 under the round-robin dispatch, speed only)
+// sweep one eighth of M in order (5.4-5.6 TB/s).  The class row is rebuilt
+// for each row (its allowed-pod lists, L2 / MALL resident).  16-byte lanes,
+// consecutive across the wave: 32 bytes per lane as two stores collapses to
+// ~2 TB/s with non-temporal stores.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rows_ord(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
-  const i64 li = blockIdx.x;
+  const i64 rl = a.nitems;                 // rows of the shard
+  i64 li = blockIdx.x;
+  if (a.probe == 4) {                      // XCD-local sweeps
+    const i64 R = (rl + 7) / 8;
+    li = (i64)(blockIdx.x & 7) * R + (blockIdx.x >> 3);
+  }
+  if (li >= rl) return;                    // block-uniform
   const i64 c = a.rcls[a.r0 + li];
   const i64 base = (i64)blockIdx.y * a.cww;
   const int nw = (int)min((i64)a.cww, a.wW - base);
@@ -1948,17 +1956,10 @@ __global__ __launch_bounds__(NT) void k_rows_ord(RowsArgs a) {
     __syncthreads();
   }
   u64* dst = a.M + li * a.ldM + base;
-  // nw is a multiple of 4 (ldM and the chunk width are multiples of 16)
-  for (int w = threadIdx.x * 4; w < nw; w += NT * 4) {
-    const u64x2 v0 = *(const u64x2*)&row[w];
-    const u64x2 v1 = *(const u64x2*)&row[w + 2];
-    if (a.store_mode == 2) {
-      __builtin_nontemporal_store(v0, (u64x2*)&dst[w]);
-      __builtin_nontemporal_store(v1, (u64x2*)&dst[w + 2]);
-    } else {
-      *(u64x2*)&dst[w] = v0;
-      *(u64x2*)&dst[w + 2] = v1;
-    }
+  for (int w = threadIdx.x * 2; w < nw; w += NT * 2) {
+    const u64x2 v = *(const u64x2*)&row[w];
+    if (a.store_mode == 2) __builtin_nontemporal_store(v, (u64x2*)&dst[w]);
+    else *(u64x2*)&dst[w] = v;
   }
 }
 
