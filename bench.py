@@ -363,7 +363,13 @@ def main():
                          "avg_launch_ms": k_rows_ms,
                          "launches_timed": rt["launches"],
                          "min_launch_ms": rt["min_ms"], "max_launch_ms": rt["max_ms"],
-                         "box_fill_gbs": box_fill},
+                         "box_fill_gbs": box_fill,
+                         "placement": {"candidates": info["MPROBE_TRIED"],
+                                       "kept_probe_ms": info["MPROBE_BEST_NS"] / 1e6,
+                                       "slowest_probe_ms": info["MPROBE_WORST_NS"] / 1e6,
+                                       "note": "the matrix allocation kept is the fastest of "
+                                               "the candidates under a probe write of k_rows' "
+                                               "store shape (DESIGN.md, alloc_matrix)"}},
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),
                         "p90": round(float(np.percentile(step_ms, 90)), 4),

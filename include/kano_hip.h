@@ -60,7 +60,10 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_GRAPH_HITS 13 /* kano_verify segments issued as a cached hipGraph */
 #define KANO_INFO_GRAPH_CAPTURES 14 /* ... captured into a new hipGraph       */
 #define KANO_INFO_GRAPH_DIRECT 15 /* ... issued operation by operation      */
-#define KANO_INFO_NSLOTS   16
+#define KANO_INFO_MPROBE_TRIED 16 /* matrix allocation: candidates probed (0: plain) */
+#define KANO_INFO_MPROBE_BEST_NS 17 /* ... the kept one's probe write, ns       */
+#define KANO_INFO_MPROBE_WORST_NS 18 /* ... the slowest candidate's, ns         */
+#define KANO_INFO_NSLOTS   19
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in
  * Python objects (kano_py/kano/model.py:167-169 ReachabilityMatrix.__init__). */

@@ -306,6 +306,14 @@ struct kano_ctx {
   // events: no marker packets around the launch; knob extev); the tail's
   // fork point is then a marker of its own
   int rows_extev = 1;
+  // placement-probed matrix allocation (alloc_matrix): candidates, and the
+  // matrix sizes (MB) it applies to
+  int mprobe = 8;
+  i64 mprobe_budget_mb = 16384;   // candidate bytes held at once
+  i64 mprobe_min_mb = 64, mprobe_max_mb = 16384;
+  float mprobe_best_ms = 0.f, mprobe_worst_ms = 0.f;
+  int mprobe_tried = 0;
+  DBuf mprobe_perm;
   hipEvent_t ev_rows_fork = nullptr;
   hipEvent_t rows_fork = nullptr;    // what the tail waits on (ev[7] or ev_rows_fork)
   float rows_ms_last = 0.f;
@@ -472,6 +480,85 @@ int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes, bool contig = false) {
                                   hipGetErrorString(e));
   }
   b.bytes = bytes;
+  return 0;
+}
+
+// The matrix write's store rate depends on where the allocation lands:
+// eight 1.25 GB allocations in one process took k_rows' store shape (random
+// rows, 16-B non-temporal lanes) at 4.6-4.9 TB/s on five and 5.4-5.5 TB/s
+// on three, each steadily (profiles/r02_store_alloc.txt).  So a matrix of
+// mprobe_min_mb..mprobe_max_mb is the best of up to mprobe candidate
+// allocations, each timed by a write of its own shape (k_place_probe, two
+// launches, the faster counts); the others are freed.  Once per allocation;
+// the matrix stays allocated across builds.
+int alloc_matrix(kano_ctx* ctx, size_t bytes, bool contig) {
+  DBuf& b = ctx->M;
+  if (bytes == 0) bytes = 16;
+  if (b.p && b.bytes >= bytes) return 0;
+  const i64 mb = (i64)(bytes >> 20);
+  const i64 ldM = std::max<i64>(1, ctx->ldM);
+  const i64 rows = (i64)(bytes / (sizeof(u64) * ldM));
+  if (ctx->mprobe < 2 || contig || mb < ctx->mprobe_min_mb || mb > ctx->mprobe_max_mb ||
+      rows < 1 || rows > (i64)UINT32_MAX)
+    return dalloc(ctx, b, bytes, contig);
+  if (b.p) {
+    KTRY(seg_cut(ctx));
+    KCHK(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  const i64 wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
+  // the probe's row order: a seeded random permutation (xorshift Fisher-Yates)
+  std::vector<int32_t> perm((size_t)rows);
+  for (i64 i = 0; i < rows; ++i) perm[(size_t)i] = (int32_t)i;
+  u64 x = 0x9e3779b97f4a7c15ull;
+  for (i64 i = rows - 1; i > 0; --i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    std::swap(perm[(size_t)i], perm[(size_t)(x % (u64)(i + 1))]);
+  }
+  KTRY(dalloc(ctx, ctx->mprobe_perm, sizeof(int32_t) * (size_t)rows));
+  KCHK(hipMemcpy(ctx->mprobe_perm.p, perm.data(), sizeof(int32_t) * (size_t)rows,
+                 hipMemcpyHostToDevice));
+  std::vector<void*> cand;
+  std::vector<float> ms;
+  SegPause pause(ctx);
+  KTRY(pause.rc);
+  const int ncand = (int)std::max<i64>(2, std::min<i64>(ctx->mprobe,
+                                                        ctx->mprobe_budget_mb / std::max<i64>(1, mb)));
+  for (int k = 0; k < ncand; ++k) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      break;
+    }
+    float t3[3];
+    for (int rep = 0; rep < 3; ++rep) {
+      KCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+      hipLaunchKernelGGL(k_place_probe, dim3((unsigned)rows), dim3(TPB), 0, ctx->stream,
+                         static_cast<u64*>(p), ldM, static_cast<const int32_t*>(ctx->mprobe_perm.p), wW);
+      KLAUNCH();
+      KCHK(hipEventRecord(ctx->ev[8], ctx->stream));
+      KCHK(hipEventSynchronize(ctx->ev[8]));
+      KCHK(hipEventElapsedTime(&t3[rep], ctx->ev[7], ctx->ev[8]));
+    }
+    std::sort(t3, t3 + 3);
+    cand.push_back(p);
+    ms.push_back(t3[1]);   // the median of three
+  }
+  ctx->rows_time_pending = false;   // ev[7] / ev[8] were reused
+  if (cand.empty()) return dalloc(ctx, b, bytes, contig);
+  size_t kb = 0;
+  for (size_t k = 1; k < cand.size(); ++k)
+    if (ms[k] < ms[kb]) kb = k;
+  for (size_t k = 0; k < cand.size(); ++k)
+    if (k != kb) KCHK(hipFree(cand[k]));
+  b.p = cand[kb];
+  b.bytes = bytes;
+  ctx->mprobe_tried = (int)cand.size();
+  ctx->mprobe_best_ms = ms[kb];
+  ctx->mprobe_worst_ms = *std::max_element(ms.begin(), ms.end());
   return 0;
 }
 
@@ -1650,7 +1737,7 @@ int ensure_matrix(kano_ctx* ctx) {
                 "writes the shard's rows)");
   if (ctx->rows_deferred) {    // kano_build_classes: the matrix, now
     ctx->rows_deferred = false;
-    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM) *
+    KTRY(alloc_matrix(ctx, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM) *
                                  ctx->m_over, ctx->m_contig != 0));
     KTRY(launch_rows(ctx, false));
   }
@@ -2024,6 +2111,9 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "spin") ctx->spin_wait = v;
         if (k == "async") ctx->async_rows = v;
         if (k == "extev") ctx->rows_extev = v;
+        if (k == "mprobe" && v >= 0 && v <= 16) ctx->mprobe = v;
+        if (k == "mprobemin" && v >= 0) ctx->mprobe_min_mb = v;
+        if (k == "mprobemax" && v >= 0) ctx->mprobe_max_mb = v;
         if (k == "mcown") ctx->mc_own = v;
         if (k == "tail") ctx->side_tail = v;
         if (k == "s3prio") ctx->s3_prio = v;
@@ -2169,7 +2259,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->sizes,   &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd,
+                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd,    &ctx->mprobe_perm,
                   &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff,
                   &ctx->gids,
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
@@ -2494,7 +2584,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
   const i64 rl = rows_local(ctx);
   if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
-    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over,
+    KTRY(alloc_matrix(ctx, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over,
                 ctx->m_contig != 0));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
@@ -2561,6 +2651,9 @@ int kano_info(kano_ctx* ctx, int64_t* out) {
   out[KANO_INFO_GRAPH_HITS] = ctx->g_hits;
   out[KANO_INFO_GRAPH_CAPTURES] = ctx->g_captures;
   out[KANO_INFO_GRAPH_DIRECT] = ctx->g_direct;
+  out[KANO_INFO_MPROBE_TRIED] = ctx->mprobe_tried;
+  out[KANO_INFO_MPROBE_BEST_NS] = (int64_t)(ctx->mprobe_best_ms * 1e6);
+  out[KANO_INFO_MPROBE_WORST_NS] = (int64_t)(ctx->mprobe_worst_ms * 1e6);
   return 0;
 }
 

@@ -1963,6 +1963,18 @@ __global__ __launch_bounds__(NT) void k_rows_ord(RowsArgs a) {
   }
 }
 
+// Placement probe of a matrix allocation (alloc_matrix): block b writes row
+// perm[b] (a random permutation: every row once, scattered like k_rows'
+// class order), 16-byte non-temporal lanes.
+__global__ __launch_bounds__(TPB) void k_place_probe(u64* __restrict__ M, i64 ldM,
+                                                     const int32_t* __restrict__ perm, i64 wW) {
+  const i64 r = perm[blockIdx.x];
+  u64* dst = M + r * ldM;
+  const u64x2 z = {0ull, 0ull};
+  for (i64 w = (i64)threadIdx.x * 2; w + 1 < wW; w += TPB * 2)
+    __builtin_nontemporal_store(z, (u64x2*)&dst[w]);
+}
+
 // ===========================================================================
 // Row digests (full-size property checks: a 1M-pod matrix is 125 GB, too big
 // to bring to the host).  digest(row) = sum over k < W of
