@@ -308,8 +308,8 @@ struct kano_ctx {
   int rows_extev = 1;
   // placement-probed matrix allocation (alloc_matrix): candidates, and the
   // matrix sizes (MB) it applies to
-  int mprobe = 8;
-  i64 mprobe_budget_mb = 16384;   // candidate bytes held at once
+  int mprobe = 16;
+  i64 mprobe_budget_mb = 24576;   // candidate bytes held at once
   i64 mprobe_min_mb = 64, mprobe_max_mb = 16384;
   float mprobe_best_ms = 0.f, mprobe_worst_ms = 0.f;
   int mprobe_tried = 0;
