@@ -15,7 +15,7 @@ timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench_rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-600; stop_if_fatal $rc
 if [ "${PROFILE:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
   rc=$?; echo "prof_rc=$rc"; stop_if_fatal $rc
   find gpurun_out/prof -name "*stats*" | head
 fi
