@@ -212,6 +212,9 @@ struct kano_ctx {
   bool side_pending = false;
   hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
+  DBuf kempty;               // the fold's "a live class has an empty select list"
+  int fold_skip_empty = 1;   // knob foldskip
+  int scan_slots = 1;        // knob scanslots: scans pass only their used job slots
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   DBuf xw, xg;               // kano_verify_gather: this shard's words, all ranks' words
@@ -638,6 +641,23 @@ struct ScanBatch {
     j.gm0 = m0;
     return 0;
   }
+  // the launch with only the used job slots in its kernel argument
+  template <int NJ>
+  void launch_n(dim3 g, u64* cur, u64* nxt) {
+    ScanJobsN<NJ> a;
+    for (int q = 0; q < NJ; ++q) a.j[q] = jobs.j[q];
+    a.count = jobs.count;
+    a.npub = jobs.npub;
+    for (int q = 0; q < MAX_PUBLISH; ++q) {
+      a.pub_src[q] = jobs.pub_src[q];
+      a.pub_dst[q] = jobs.pub_dst[q];
+    }
+    a.sig_host = jobs.sig_host;
+    a.sig_val = jobs.sig_val;
+    a.sig_ctr = jobs.sig_ctr;
+    a.sig_n = jobs.sig_n;
+    hipLaunchKernelGGL(k_scan_lb<NJ>, g, dim3(TPB), 0, ctx->stream, a, cur, nxt, ctx->scan_cap);
+  }
   int run() {
     if (jobs.count == 0) return 0;
     KTRY(scan_reserve(ctx, slots));
@@ -657,8 +677,17 @@ struct ScanBatch {
     u64* st = P_<u64>(ctx->scan_tmp);
     u64* cur = st + (ctx->scan_parity ? ctx->scan_cap : 0);
     u64* nxt = st + (ctx->scan_parity ? 0 : ctx->scan_cap);
-    hipLaunchKernelGGL(k_scan_lb, dim3((unsigned)maxt, (unsigned)jobs.count), dim3(TPB), 0,
-                       ctx->stream, jobs, cur, nxt, ctx->scan_cap);
+    const dim3 g((unsigned)maxt, (unsigned)jobs.count);
+    switch (ctx->scan_slots ? jobs.count : MAX_SCAN_JOBS) {
+      case 1: launch_n<1>(g, cur, nxt); break;
+      case 2: launch_n<2>(g, cur, nxt); break;
+      case 3: launch_n<3>(g, cur, nxt); break;
+      case 4: launch_n<4>(g, cur, nxt); break;
+      case 5: launch_n<5>(g, cur, nxt); break;
+      case 6: launch_n<6>(g, cur, nxt); break;
+      case 7: launch_n<7>(g, cur, nxt); break;
+      default: launch_n<MAX_SCAN_JOBS>(g, cur, nxt); break;
+    }
     KLAUNCH();
     ctx->scan_parity ^= 1;
     jobs.count = 0;
@@ -1875,6 +1904,8 @@ int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan&
   KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
   for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
   KTRY(fb.add(ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1), 0u));   // counts + cursors
+  KTRY(dalloc(ctx, ctx->kempty, sizeof(int32_t)));
+  KTRY(fb.add(ctx->kempty, sizeof(int32_t), 0u));
   return 0;
 }
 
@@ -1892,6 +1923,12 @@ KeySort cross_sort(kano_ctx* ctx, const CrossPlan& cp) {
   k.hist = P_<int32_t>(ctx->kcnt) + 2 * ((i64)cp.G + 1);
   k.hoff = P_<int32_t>(ctx->koff);
   k.order = P_<int32_t>(ctx->corder);
+  // classes with an empty select list skip the fold (their Mc rows are zero;
+  // the select counts exist once the build's front end ran)
+  if (ctx->fold_skip_empty && ctx->scnt.p && !ctx->rows_dirty) {
+    k.scnt = P_<int32_t>(ctx->scnt);
+    k.empty = P_<int32_t>(ctx->kempty);
+  }
   return k;
 }
 
@@ -1956,11 +1993,14 @@ int cross_stage_b2(kano_ctx* ctx, const CrossPlan& cp) {
     u64* cn = cols ? P_<u64>(ctx->col_nand_c) : nullptr;
     const int fm = ctx->fold_mode;   // 0 serial 16; 1 batched 16; 2 batched 32; +10 skip
     const int pw = (fm % 10) == 2 ? 32 : 16;
+    const KeySort ksx = cross_sort(ctx, cp);
+    const int32_t* ks_empty = cp.key_lds ? ksx.empty : nullptr;
     const dim3 g(nblk(UAW, 64), nblk(U, (TPB / 64) * pw));
 #define KANO_FOLD(PW, B, S)                                                                 \
   hipLaunchKernelGGL((k_mc_fold<PW, B, S>), g, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), \
                      ldC, UAW, ctx->cc.U, ord, nlive, ck, (int32_t)G, P_<u64>(ctx->R),     \
-                     P_<u64>(ctx->multi), co, cn)
+                     P_<u64>(ctx->multi), co, cn,                                           \
+                     ks_empty)
     switch (fm) {
       case 1: KANO_FOLD(16, true, false); break;
       case 2: KANO_FOLD(32, true, false); break;
@@ -2111,6 +2151,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "spin") ctx->spin_wait = v;
         if (k == "async") ctx->async_rows = v;
         if (k == "extev") ctx->rows_extev = v;
+        if (k == "foldskip") ctx->fold_skip_empty = v;
+        if (k == "scanslots") ctx->scan_slots = v;
         if (k == "mprobe" && v >= 0 && v <= 16) ctx->mprobe = v;
         if (k == "mprobemin" && v >= 0) ctx->mprobe_min_mb = v;
         if (k == "mprobemax" && v >= 0) ctx->mprobe_max_mb = v;

@@ -62,6 +62,10 @@ struct KeySort {
   int32_t* hist;
   const int32_t* hoff;
   int32_t* order;
+  // (nullable) |S(c)|: a class whose select list is empty has an all-zero Mc
+  // row, so it is left out of the fold (key -1) and only raises *empty
+  const int32_t* scnt;
+  int32_t* empty;
 };
 
 // (block-uniform: every thread of the block calls it)
@@ -76,6 +80,10 @@ __device__ __forceinline__ void key_hist_block(const KeySort& k, i64 b) {
     if (c >= k.U) break;
     int32_t key = -1;
     if (k.mcnt[c] > 0 && k.gmin[c] <= k.gmax[c]) key = k.gmin[c] == k.gmax[c] ? k.gmin[c] : k.G;
+    if (key >= 0 && k.scnt && k.scnt[c] == 0) {
+      key = -1;
+      *k.empty = 1;
+    }
     k.ckey[c] = key;
     if (key >= 0) atomicAdd(&h[key], 1);
   }
@@ -1365,7 +1373,8 @@ __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64
                                                  const int32_t* __restrict__ nlive_p,
                                                  const int32_t* __restrict__ ckey,
                                                  int32_t G, u64* R, u64* multi, u64* col_or,
-                                                 u64* col_nand) {
+                                                 u64* col_nand,
+                                                 const int32_t* __restrict__ empty_live) {
   __shared__ u64 red[2][TPB / 64][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const i64 w = (i64)blockIdx.x * 64 + lane;
@@ -1420,6 +1429,9 @@ __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64
   }
   if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
   if (col_or) {
+    // a live class with an empty select list (left out of the order) has an
+    // all-zero row: every column misses it
+    if (empty_live && *empty_live) na = vm;
     red[0][wid][lane] = o;
     red[1][wid][lane] = na;
     __syncthreads();

@@ -152,8 +152,12 @@ struct ScanJob {
 };
 constexpr int MAX_SCAN_JOBS = 8;
 constexpr int MAX_PUBLISH = 4;
-struct ScanJobs {
-  ScanJob j[MAX_SCAN_JOBS];
+// NJ job slots: the launch passes only the slots it uses (the kernel
+// argument of an 8-slot batch is ~800 B, and a launch costs the host ~1.4 us
+// more at 768 B than at 40 B: scripts/micro/launch_cost.hip)
+template <int NJ>
+struct ScanJobsN {
+  ScanJob j[NJ];
   int count;
   // size slots produced by earlier kernels (atomics), copied by one thread
   // to their host mirrors: they travel with the scan's own totals
@@ -169,6 +173,7 @@ struct ScanJobs {
   uint32_t* sig_ctr;   // arrivals (zero between launches: the last arrival resets it)
   int sig_n;
 };
+using ScanJobs = ScanJobsN<MAX_SCAN_JOBS>;
 
 // A host mirror word: a system-scope (write-through) store, so that once the
 // store is acknowledged the host sees it -- no cache write-back needed.
@@ -181,7 +186,8 @@ __device__ __forceinline__ void mirror_store(u64* p, u64 v) {
 // raises the host signal after seeing every other count: the host, seeing
 // the signal, sees every mirror word.  (A system-scope fence here wrote back
 // the XCD's L2 per writer: ~5 us on the scan that carries the signal.)
-__device__ __forceinline__ void scan_sig_arrive(const ScanJobs& jobs) {
+template <class J>
+__device__ __forceinline__ void scan_sig_arrive(const J& jobs) {
   if (!jobs.sig_host) return;
   __builtin_amdgcn_s_waitcnt(0);
   const uint32_t old =
@@ -192,7 +198,8 @@ __device__ __forceinline__ void scan_sig_arrive(const ScanJobs& jobs) {
   }
 }
 
-__global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
+template <int NJ>
+__global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status,
                                                  u64* __restrict__ clear, i64 nclear) {
   __shared__ i64 sm[4];
   __shared__ i64 s_tile;
@@ -206,7 +213,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobs jobs, u64* status,
   }
   ScanJob jb = jobs.j[0];   // select, not a dynamic index (kernarg stays in SGPRs)
 #pragma unroll
-  for (int q = 1; q < MAX_SCAN_JOBS; ++q)
+  for (int q = 1; q < NJ; ++q)
     if ((int)blockIdx.y == q) jb = jobs.j[q];
   const i64 tiles = (jb.n + SCAN_TILE - 1) / SCAN_TILE;
   if (jb.n == 0) {
