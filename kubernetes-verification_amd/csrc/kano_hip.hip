@@ -213,7 +213,7 @@ struct kano_ctx {
   hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf kempty;               // the fold's "a live class has an empty select list"
-  int fold_skip_empty = 1;   // knob foldskip
+  int fold_skip_empty = 0;   // knob foldskip (measured: the fold gains ~5 us, k_key_hist loses ~3 us on the critical path and the post-sync-2 issue absorbs the rest)
   int scan_slots = 1;        // knob scanslots: scans pass only their used job slots
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
@@ -1256,6 +1256,9 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
   KTRY(classify_phase2a(ctx));
   i64 u[2] = {0, 0};
   KTRY(mirror_wait(ctx, SZ_UR, 2, u));
+  // the previous matrix write ended before this build's first scan: its
+  // time is read here, off the host's path to the next k_rows launch
+  KTRY(resolve_rows_time(ctx));
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KTRY(stage_mark(ctx, 1, ctx->stream));

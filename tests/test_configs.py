@@ -273,7 +273,7 @@ def _lists(cs, which):
     "nt=512", "nt=1024", "cww=64", "cww=16", "nt=1024,cww=32", "cww=16,ch=3",
     "persist=8", "store=0", "store=3", "xfuse=1", "sig=0", "hfuse=0", "shstage=0", "extev=0",
     "order=1", "order=2", "order=2,nt=512,cww=64", "mprobe=3,mprobemin=0", "mprobe=0",
-    "foldskip=0",
+    "foldskip=1",
 ])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
