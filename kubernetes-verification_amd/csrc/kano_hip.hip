@@ -130,6 +130,7 @@ struct kano_ctx {
   int prio = 0;              // checks stream high priority, matrix-write stream low
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
   int sh_stage = 1;          // the pairwise test with the block's lists staged in LDS
+  int sh_seg = 1024;         // its staged S(c) entries per block (1024 or 512; knob shseg: 512 measured +3 us step median)
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
   int rows_store = 2;        // k_rows stores: 2 non-temporal (measured C3: 253 vs 263-270 us
@@ -2139,6 +2140,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "prio") ctx->prio = v;
         if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
         if (k == "shstage") ctx->sh_stage = v;
+        if (k == "shseg" && (v == 512 || v == 1024)) ctx->sh_seg = v;
         if (k == "grm") ctx->grange_m = v;
         if (k == "fold") ctx->fold_mode = v;
         if (k == "mcrows") ctx->mc_rows = v;
@@ -3044,8 +3046,14 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     const i64 nvb = sp.nt * SH_ITEMS;
     const i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
     if ((ctx->sh_items == 1 || ctx->vs_count_only) && ctx->sh_stage)
-      hipLaunchKernelGGL(k_shadow_test1s, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
-                         P_<i64>(ctx->tcnt));
+    {
+      if (ctx->sh_seg == 1024)
+        hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
+                           P_<i64>(ctx->tcnt));
+      else
+        hipLaunchKernelGGL(k_shadow_test1s<512>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
+                           P_<i64>(ctx->tcnt));
+    }
     else if (ctx->sh_items == 1 || ctx->vs_count_only)
       hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
                          P_<i64>(ctx->tcnt));

@@ -2381,8 +2381,10 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
 // from AC[j]).  Blocks whose class range or S(c) segment does not fit fall
 // back to the global form.
 constexpr int SHS_CLS = TPB + 2;
-constexpr int SHS_SEG = 1024;
+// SEG: staged S(c) entries per block (1024: ~25 KB of LDS; 512, ten blocks
+// per CU, measured slightly slower beside the main stream's kernels)
 constexpr int SHS_U = 8;
+template <int SHS_SEG>
 __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
                                                       i64* __restrict__ tile_cnt) {
   __shared__ i64 sm[4];
