@@ -130,6 +130,7 @@ struct kano_ctx {
   int prio = 0;              // checks stream high priority, matrix-write stream low
   int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
   int sh_stage = 1;          // the pairwise test with the block's lists staged in LDS
+  int sh_scan_side = 0;      // policy_shadow's scans on the side stream after its tests (knob shscanside: measured neutral)
   int sh_seg = 1024;         // its staged S(c) entries per block (1024 or 512; knob shseg: 512 measured +3 us step median)
   int grange_m = 1;          // crosscheck group ranges along the member lists
   int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
@@ -2141,6 +2142,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
         if (k == "shstage") ctx->sh_stage = v;
         if (k == "shseg" && (v == 512 || v == 1024)) ctx->sh_seg = v;
+        if (k == "shscanside") ctx->sh_scan_side = v;
         if (k == "grm") ctx->grange_m = v;
         if (k == "fold") ctx->fold_mode = v;
         if (k == "mcrows") ctx->mc_rows = v;
@@ -3339,6 +3341,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // host's ~15 us of fork calls overlap those kernels instead of leaving the
   // main stream idle (it ran ahead of the host there)
   bool fork_marked = false;
+  bool sh_scanned = false;
   std::function<int()> fork_issue;
   if (want_shadow && ctx->fork_checks) {
     ctx->fork_hook = [&]() -> int {
@@ -3356,6 +3359,25 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
       KTRY(build_alist(ctx, tst));
     }
     KTRY(shadow_test_launch(ctx, sp, tst));
+    // policy_shadow's scans follow its tests on the side stream (their own
+    // scan status buffers): one launch fewer on the main stream, which joins
+    // before k_verify_cols reads their offsets
+    sh_scanned = false;
+    if (ctx->sh_scan_side && tst == ctx->stream2) {
+      auto swap = [&]() {
+        std::swap(ctx->stream, ctx->stream2);
+        std::swap(ctx->scan_tmp, ctx->scan_tmp_side);
+        std::swap(ctx->scan_cap, ctx->scan_cap_side);
+        std::swap(ctx->scan_parity, ctx->scan_parity_side);
+      };
+      swap();
+      ScanBatch sbs(ctx);
+      int rc = shadow_stage_a_scans(ctx, sp, sbs);
+      if (rc == 0) rc = sbs.run();
+      swap();
+      KTRY(rc);
+      sh_scanned = true;
+    }
     KCHK(hipEventRecord(ctx->ev_join2, tst));
     ctx->fork_pending = true;
     return 0;
@@ -3395,7 +3417,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     if (ctx->fork_pending) {
       KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join2, 0));
       ctx->fork_pending = false;
-      KTRY(shadow_stage_a_scans(ctx, sp, sb));
+      if (!sh_scanned) KTRY(shadow_stage_a_scans(ctx, sp, sb));
     } else {
       KTRY(shadow_stage_a(ctx, sp, sb));
     }

@@ -547,7 +547,8 @@ def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
 
 
 @pytest.mark.parametrize("tune", ["", "sig=0", "xfuse=1,forklate=0", "alistside=1", "hfuse=0,preclean=0",
-                                  "shstage=0,async=0,extev=0", "foldskip=1", "shseg=512"])
+                                  "shstage=0,async=0,extev=0", "foldskip=1", "shseg=512",
+                                  "shscanside=1"])
 @pytest.mark.parametrize("n,P", [(1, 0), (1, 1), (2, 3), (5, 1), (63, 7), (64, 64), (65, 9),
                                  (130, 40)])
 def test_verify_small_shapes_vs_oracle(n, P, tune, monkeypatch):
