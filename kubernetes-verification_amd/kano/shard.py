@@ -134,7 +134,10 @@ class ShardExchange:
         """kano_py's checks for this rank (algorithm.py:4-80): the column
         lists are global, system_isolation is None unless this rank owns
         sys_row, the shadow pairs are this rank's rows' part."""
-        if self.stream is None:
+        if self.stream is None or self.comm:
+            # (the native exchange issues everything on the engine's own
+            # stream: no torch stream context needed, a few us less host time
+            # per step)
             return self._run(eng, gid, sys_row, shadow, count_only, pairs, idx)
         with self.torch.cuda.stream(self.stream):
             return self._run(eng, gid, sys_row, shadow, count_only, pairs, idx)
