@@ -459,6 +459,8 @@ struct SegScope {
   ~SegScope() { (void)seg_end(c); }
 };
 
+int settle(kano_ctx* ctx);
+
 // contig: ask for physically contiguous memory first (the matrix: knob
 // mcontig), plain hipMalloc when that fails
 int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes, bool contig = false) {
@@ -466,6 +468,7 @@ int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes, bool contig = false) {
   if (b.p && b.bytes >= bytes) return 0;
   if (b.p) {
     KTRY(seg_cut(ctx));   // recorded operations may still use the old buffer
+    KTRY(settle(ctx));    // ... and an asynchronously completing matrix write
     KCHK(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -508,6 +511,7 @@ int alloc_matrix(kano_ctx* ctx, size_t bytes, bool contig) {
     return dalloc(ctx, b, bytes, contig);
   if (b.p) {
     KTRY(seg_cut(ctx));
+    KTRY(settle(ctx));    // the previous matrix write may still run
     KCHK(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -2603,6 +2607,7 @@ int kano_set_shard(kano_ctx* ctx, int64_t row_begin, int64_t row_end) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods || row_begin < 0 || row_end < row_begin || row_end > ctx->n)
     return fail(ctx, -EINVAL, "kano_set_shard: bad row range");
+  KTRY(settle(ctx));
   ctx->r0 = row_begin;
   ctx->r1 = row_end;
   ctx->built = false;

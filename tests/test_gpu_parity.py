@@ -234,6 +234,24 @@ def test_verify_async_completion(tune, monkeypatch):
     assert eng.lib.kano_path(eng.ctx, dst.ctx, 1, 0, info.ctypes.data) == 0
     assert sha(dst.rows(0, n)) == exp["M_sha256"]
     dst.close()
+    # other clusters on the same context right behind an asynchronously
+    # completing call: their builds reallocate buffers the previous matrix
+    # write may still read (2k pods, then C2's 10k again)
+    from kano._intern import intern, group_ids
+    r = eng.verify("stored", sys_row=0, shadow=True, pairs=pairs)
+    obj = cluster("s_sparse_2000")
+    cs, ps = api_objects(obj)
+    eng.upload(intern(cs, ps))
+    rb = eng.verify(group_ids(cs, obj["label"]), sys_row=0, shadow=True, pairs=pairs)
+    e2 = expected("s_sparse_2000")
+    assert rb["all_isolated"].tolist() == e2["all_isolated"]
+    assert rb["user_crosscheck"].tolist() == e2["user_crosscheck"]["result"]
+    assert rb["shadow_count"] == e2["policy_shadow"]["count"]
+    eng.upload(tables)
+    eng.set_groups(gid)
+    r = eng.verify("stored", sys_row=0, shadow=True, pairs=pairs)
+    assert r["all_isolated"].tolist() == exp["all_isolated"]
+    assert sha(eng.rows(0, n)) == exp["M_sha256"]
     eng.close()
     pin.close()
 
