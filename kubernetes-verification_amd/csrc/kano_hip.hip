@@ -313,8 +313,8 @@ struct kano_ctx {
   int rows_extev = 1;
   // placement-probed matrix allocation (alloc_matrix): candidates, and the
   // matrix sizes (MB) it applies to
-  int mprobe = 16;
-  i64 mprobe_budget_mb = 24576;   // candidate bytes held at once
+  int mprobe = 32;
+  i64 mprobe_budget_mb = 40960;   // candidate bytes held at once
   i64 mprobe_min_mb = 64, mprobe_max_mb = 16384;
   float mprobe_best_ms = 0.f, mprobe_worst_ms = 0.f;
   int mprobe_tried = 0;
@@ -2164,7 +2164,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "extev") ctx->rows_extev = v;
         if (k == "foldskip") ctx->fold_skip_empty = v;
         if (k == "scanslots") ctx->scan_slots = v;
-        if (k == "mprobe" && v >= 0 && v <= 16) ctx->mprobe = v;
+        if (k == "mprobe" && v >= 0 && v <= 64) ctx->mprobe = v;
         if (k == "mprobemin" && v >= 0) ctx->mprobe_min_mb = v;
         if (k == "mprobemax" && v >= 0) ctx->mprobe_max_mb = v;
         if (k == "mcown") ctx->mc_own = v;
