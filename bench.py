@@ -285,6 +285,7 @@ def main():
     # k_rows' HIP-event times accumulate in the engine over the timed steps
     # (read once afterwards: kano_verify returns before its matrix write ends)
     eng.rows_timing(reset=True)
+    eng.host_times(reset=True)
     step.verify_max_ms = 0.0
     # Python's cyclic GC off in the timed region (as timeit does): a full
     # collection over torch's objects took ~7 ms between two steps
@@ -310,6 +311,8 @@ def main():
     value = float(n) * n / (elapsed / args.steps)
     rt = eng.rows_timing()
     k_rows_ms = rt["sum_ms"] / rt["launches"] if rt["launches"] else float("nan")
+    rows_kernel = {1: "k_rows_mc", 2: "k_rows"}.get(info["ROWS_KERNEL"], "none")
+    host = eng.host_times()
     rows_local = r1 - r0
     W = (n + 63) // 64
     alg_bytes = 8.0 * rows_local * W
@@ -356,20 +359,14 @@ def main():
             "verified": verified, "verified_against": vdetail,
             "upload_ms": {"tables": round(up_tables_ms, 3), "groups": round(up_groups_ms, 3),
                           "note": "host -> device input upload, once, outside the step"},
-            "roofline": {"bound": "hbm", "kernel": "k_rows", "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": rows_kernel, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": k_rows_ms,
                          "launches_timed": rt["launches"],
                          "min_launch_ms": rt["min_ms"], "max_launch_ms": rt["max_ms"],
-                         "box_fill_gbs": box_fill,
-                         "placement": {"candidates": info["MPROBE_TRIED"],
-                                       "kept_probe_ms": info["MPROBE_BEST_NS"] / 1e6,
-                                       "slowest_probe_ms": info["MPROBE_WORST_NS"] / 1e6,
-                                       "note": "the matrix allocation kept is the fastest of "
-                                               "the candidates under a probe write of k_rows' "
-                                               "store shape (DESIGN.md, alloc_matrix)"}},
+                         "box_fill_gbs": box_fill},
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),
                         "p90": round(float(np.percentile(step_ms, 90)), 4),
@@ -377,6 +374,14 @@ def main():
                         "worst5": [round(float(v), 3) for v in np.sort(step_ms)[-5:]],
                         "worst5_at": [int(i) for i in np.argsort(step_ms)[-5:]],
                         "engine_call_max": round(step.verify_max_ms, 4)},
+            # kano_verify's host time by phase over the timed steps (us): a
+            # stall names its phase (front = build + checks up to the column
+            # words, back = lists + matrix-write launch + wait for the host
+            # results, waits = the overlapped size syncs)
+            "host_us": ({k: round(v, 1) for k, v in host.items() if k.endswith("_max")} |
+                        {"front_mean": round(host["front_sum"] / max(1.0, host["calls"]), 1),
+                         "back_mean": round(host["back_sum"] / max(1.0, host["calls"]), 1)}
+                        if host["calls"] > 0 else None),
             "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},

@@ -56,14 +56,10 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_MAXSEL   9   /* max over classes of |S(c)|                  */
 #define KANO_INFO_UA      10   /* column classes (pods with equal allow keys) */
 #define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 int8 MFMA          */
-#define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the row kernel */
-#define KANO_INFO_GRAPH_HITS 13 /* kano_verify segments issued as a cached hipGraph */
-#define KANO_INFO_GRAPH_CAPTURES 14 /* ... captured into a new hipGraph       */
-#define KANO_INFO_GRAPH_DIRECT 15 /* ... issued operation by operation      */
-#define KANO_INFO_MPROBE_TRIED 16 /* matrix allocation: candidates probed (0: plain) */
-#define KANO_INFO_MPROBE_BEST_NS 17 /* ... the kept one's probe write, ns       */
-#define KANO_INFO_MPROBE_WORST_NS 18 /* ... the slowest candidate's, ns         */
-#define KANO_INFO_NSLOTS   19
+#define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the list-based row kernel */
+#define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 1 k_rows_mc (class table, address
+                                    order), 2 k_rows (allowed-pod lists), 0 none */
+#define KANO_INFO_NSLOTS   14
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in
  * Python objects (kano_py/kano/model.py:167-169 ReachabilityMatrix.__init__). */
@@ -361,6 +357,16 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
  * (kano_get_rows, kano_path, ...).  For sources of kano_k8s_edge, which reads
  * only Mc and the classes. */
 int kano_build_classes(kano_ctx* ctx, int path);
+
+/* Host time of kano_verify (no reference counterpart; diagnostics for the
+ * benchmark, always recorded: a few clock reads per call), microseconds:
+ * out[12] = [calls, front sum, back sum, size-wait sum, gap between calls sum,
+ *            front max, back max, size-wait max, call max,
+ *            size wait 1 max, size wait 2 max, size wait 3 max];
+ * "front" is the build and checks up to the column words, "back" the result
+ * lists, the matrix write's launch and the wait for the host results.
+ * reset != 0 zeroes them after reading. */
+int kano_host_times(kano_ctx* ctx, double* out /* 12 */, int reset);
 
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);

@@ -45,17 +45,23 @@
 #include <link.h>
 
 #include "kano_hip.h"
-#include "kano_graph.hpp"     // records the HIP operations of kano_verify (see there)
 #include "kano_kernels.hpp"
 #include "kano_path.hpp"
 #include "kano_inc.hpp"
 #include "kano_k8s.hpp"
+#include "kano_expand.hpp"
 
 using namespace kano;
 
 namespace {
 constexpr int MAX_CWW = 8192;   // column-chunk width in words (64 KB of LDS)
 constexpr int HT_ROWS = 128;    // heavy rows per MFMA launch (HT = 4)
+constexpr int ROWS_CH = 16;     // member rows per k_rows work item
+constexpr int LD_ALIGN = 16;    // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
+constexpr int MFMA_KMIN = 8;    // min policy blocks (64 policies each) per MFMA wave
+// k_rows_mc's LDS table (4 bytes per column class) must leave a block on a
+// CU: 160 KiB per CU
+constexpr size_t ROWS_MC_LDS_MAX = 152 * 1024;
 }  // namespace
 
 struct DBuf {
@@ -108,83 +114,29 @@ struct kano_ctx {
   bool rows_dirty = false;   // M edited: classes no longer describe it
   bool rows_deferred = false;  // kano_build_classes: M is written on first use
   bool defer_alloc = false;    // (inside kano_build_classes: no M allocation)
-  int k8s_rows_cls = 0;      // kano_k8s_edge: stream pod rows per class (measured slower at
-                             // 100k pods: 0.61 vs 0.48 ms -- one block walks a class's
-                             // members serially), else per row
   bool rows_timed = false;
   bool alist_valid = false;
   bool cols_deferred = false;
   int32_t cross_G = 0;         // group count of the last class-level crosscheck
   i64 groups_n = -1;           // kano_set_groups: pods covered (-1: none stored)
   int32_t groups_G = 0;      // group count of the stored groups
-  int ch = 16;               // member rows per k_rows work item
-  int cww_max = MAX_CWW;     // k_rows column chunk (words of LDS per block)
-  int ld_align = 16;         // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
-  int pitch_mul = 1;         // experiment: spread rows over pitch_mul x the memory
-  int rows_alist = -1;       // k_rows build from allowed-pod lists: -1 auto, 0 no, 1 yes
-  int rows_nt = 0;           // k_rows block size: 0 auto, 256 / 512 / 1024
-  int rows_probe = 0;        // experiments only (KANO_TUNE probe=1|2): results are wrong
-  int m_over = 1;            // experiment: over-allocate M by this factor
-  int pitch_pad = 0;         // experiment: extra words per M row
-  int rows_early = 0;        // kano_verify: launch k_rows right after the lists (on stream2)
-  int prio = 0;              // checks stream high priority, matrix-write stream low
-  int sh_items = 1;          // policy_shadow subset tests per thread: 1 or SH_ITEMS
-  int sh_stage = 1;          // the pairwise test with the block's lists staged in LDS
-  int sh_scan_side = 0;      // policy_shadow's scans on the side stream after its tests (knob shscanside: measured neutral)
-  int sh_seg = 1024;         // its staged S(c) entries per block (1024 or 512; knob shseg: 512 measured +3 us step median)
-  int grange_m = 1;          // crosscheck group ranges along the member lists
-  int stage_timing = 0;      // record the stage events of kano_stage_times (slots 0-5)
-  int rows_store = 2;        // k_rows stores: 2 non-temporal (measured C3: 253 vs 263-270 us
-                             // for plain stores on one box, 232 vs 246-258 on another);
-                             // 0 plain, 1 word-major, 3 sc1 (no gain) are experiments
-  int rows_persist = 0;      // k_rows persistent grid: blocks per CU (0: one block per item)
-  int rows_order = 0;        // matrix write in pod order (k_rows_ord) when no class is heavy
-  // kano_verify: policy_shadow's subset tests on stream2 beside the Mc
-  // chain (set by verify_front around the build; called once the lists and
-  // AC exist), joined through ev_join2 before the shadow scans
-  int fork_checks = 1;
-  int shard_rows_early = 0;  // kano_verify_shard: k_rows before the exchange, on stream2
-                             // (measured slower: +18 us over RCCL at one rank, +32 us
-                             // emulated at 1/8 -- the small combine kernels queue
-                             // behind k_rows' blocks)
-  int s3_prio = 0;           // the tail stream at high priority (measured: k_rows
-                             // 0.209-0.213 ms beside a normal-priority tail, 0.233-0.239
-                             // beside a high-priority one; step 0.556 vs 0.582 ms)
-  int side_tail = 1;         // kano_verify's tail on stream3 beside k_rows (else after it)
-  // kano_verify's operations recorded per segment (between host waits) and
-  // issued as cached hipGraphs (kano_graph.hpp); knob "graphs".  Measured
-  // slower, so off: C3 0.628 vs 0.587 ms a step, rank 0 of 8 0.426 vs 0.386 ms
-  // -- a segment reaches the GPU only once the host has recorded all of it,
-  // and replaying the graph is no faster on the GPU than direct dispatch
-  int graphs = 0;
-  bool seg_on = false;
-  kano_rec::Recorder rec;
-  std::vector<std::pair<uint64_t, hipGraphExec_t>> gcache;   // most recent last
-  std::vector<uint64_t> gseen;     // hashes issued directly once (capture on the 2nd)
-  std::vector<uint64_t> gbad;      // hashes whose capture failed
-  i64 g_hits = 0, g_captures = 0, g_direct = 0;
-  int s3_cus = 0;            // stream3 restricted to this many CUs (0: all), so that the
-                             // tail's short kernels take few CUs from k_rows
-  std::function<int()> fork_hook;
-  // kano_verify with rows_early == 2: called once the matrix write's inputs
-  // exist (the lists; Mc too when some class is heavy), to start k_rows on
-  // stream2 beside the class-level checks
-  std::function<int()> rows_hook;
-  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
-  bool fork_pending = false;
-  // host-time breakdown of kano_verify (KANO_TUNE=hosttime=1), printed at
-  // kano_destroy: [calls, gap since the previous return, front, back, waits]
-  int host_timing = 0;
-  double ht[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // + [5..7] the three size waits apart
-  int ht_wait = 0;
-  std::chrono::steady_clock::time_point ht_last{};
-  int cls_packed = 1;        // packed-key classification where the tuple fits 63 bits
-  int mfma_kmin = 8;         // min policy blocks (64 policies each) per MFMA wave
-  int mc_rows = 0;           // Mc rows written whole by k_mc_rows (else zero fill + scatter;
-                             // measured C3: k_mc_rows 35.6 us vs scatter 18.8 us + 2.3 us
-                             // of zero fill -- a wave per class walks S(c) serially)
-  int fold_mode = 2;         // k_mc_fold variant: 2 = 32 classes per wave, batched loads
-                             // (measured C3: 16.9 us vs 24-27 us for the serial walk)
+  // Test hooks (KANO_TUNE, parsed in kano_create).  Each selects between
+  // shipped forms that compute the same results; none changes a result.
+  int stage_timing = 0;      // timing=1: the stage events of kano_stage_times (slots 0-5)
+  int cls_packed = 1;        // packed=0: classification without packed keys (the wide-key form)
+  int rows_from = 0;         // rows=1: the matrix write from the allowed-pod lists (k_rows)
+                             // even where the class-level table fits (k_rows_mc)
+  int async_rows = 1;        // async=0: kano_verify waits for its matrix write
+  int shadow_count_mode = 0; // shcount=1|2: count-only policy_shadow pairwise | grouped
+                             // (0: the device picks, shg_grouped)
+  int path_dens = 8;         // pathdens: kano_path auto takes an MFMA step when the delta
+                             // holds more than path_dens % of the class-level bits
+  int path_tm = 2;           // pathtm / pathtn: k_path_mfma tiles per wave
+  int path_tn = 2;
+  int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
+  int rows_mc_nt = 512;      // rowsnt: k_rows_mc block size (256 / 512 / 1024)
+  int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
+                             // (n > 524k) take, forced at small n
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -194,6 +146,7 @@ struct kano_ctx {
   bool rows_use_alist = false;
   int max_sel = 0;
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
+  int rows_kernel = 0;       // the last matrix write: 1 k_rows_mc (class table), 2 k_rows (lists)
 
   DBuf pv;
   DBuf scnt, cost, soffc, scur, slist, ecls, wicls, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
@@ -202,21 +155,7 @@ struct kano_ctx {
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
-  // the side issue (SideIssue): the size-independent back-end work (zeroed
-  // AC / Mc, the crosscheck's group-key sort) on stream2 beside the join,
-  // with scan status regions of its own
-  DBuf scan_tmp_side;
-  i64 scan_cap_side = 0;
-  int scan_parity_side = 0;
-  int side_pre = 0;          // knob "sidepre": 1 = that work on stream2 (measured slower on
-                             // C3: 0.658 vs 0.624 ms -- the host issuing the side work
-                             // delays the join chain by ~30 us)
-  bool side_pending = false;
-  hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
-  DBuf kempty;               // the fold's "a live class has an empty select list"
-  int fold_skip_empty = 0;   // knob foldskip (measured: the fold gains ~5 us, k_key_hist loses ~3 us on the critical path and the post-sync-2 issue absorbs the rest)
-  int scan_slots = 1;        // knob scanslots: scans pass only their used job slots
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   DBuf xw, xg;               // kano_verify_gather: this shard's words, all ranks' words
@@ -229,17 +168,10 @@ struct kano_ctx {
   i64 inc_A = 0, inc_acap = 0, inc_xcols = 0;
   std::vector<uint8_t> dead;       // P + inc_A entries
   bool user_edited = false;        // put_rows / set_bit / import: removal cannot rewrite rows
-  int path_dens = 8;         // kano_path auto: MFMA step when the delta holds more than
-                             // path_dens % of the class-level bits
-  int path_tm = 2;           // k_path_mfma rows tiles per wave (1, 2 or 4)
-  int path_tn = 2;           // k_path_mfma column tiles per wave (2 or 4)
-  int path_lds = 1;          // k_path_expand16: the group table in LDS when it fits (tests: 0)
   i64 shadow_total = -1;
   // policy_shadow count-only (kano_verify with shadow_cap < 0): the grouped
   // count (k_shg_*) instead of the pair-by-pair flags
   bool vs_count_only = false;
-  int shadow_count_mode = 0; // count-only policy_shadow: 0 the device picks (shg_grouped),
-                             // 1 pairwise, 2 grouped
   bool shg_ran = false;      // the grouped count was queued (its G / err exist)
   DBuf shg_h, shg_tkey, shg_trep, shg_slot, shg_isrep, shg_gidx, shg_gid, shg_reps, shg_sub,
       shg_err;
@@ -247,87 +179,53 @@ struct kano_ctx {
   DBuf icnt, ioff, sysrow, idxd;
   u64* ghost = nullptr;      // pinned landing buffer for the size slots
   // pinned, coherent mirror of the size slots that the scans write directly
-  // (slot-indexed): the overlapped syncs wait on an event, with no copy
+  // (slot-indexed): the overlapped syncs poll the host signal word the last
+  // scan with host totals raises (or wait on an event when no scan does)
   u64* gmirror = nullptr;     // SZ_SLOTS slots + the host signal word (SZ_SIGNAL)
   u64* gmirror_dev = nullptr;
-  // host signal of the scans (ScanJobs::sig_host): the overlapped syncs poll
-  // gmirror[SZ_SIGNAL] for the value the last scan with host totals raises,
-  // instead of recording and waiting on an event (knob sig=0: events)
-  int mirror_sig = 1;
-  // kano_verify's crosscheck sort folded into the build's launches (xs_on,
-  // armed by verify_front): the group ranges in k_cls_mfill, the key
-  // histogram in k_cls_vals, its scan in the join's scan, the placement in
-  // k_join_fill -- four launches fewer (knob xfuse; off by default: measured
-  // C3 front end +13 us, the separate launches ran inside the sync-2 wait)
-  int xfuse = 0;
-  int hfuse = 1;             // independent launches merged (k_lists_allow, k_pods_scatter)
-  int mc_own = 1;            // light Mc rows by their owner (k_mc_own: a thread per row class,
-                             // plain stores) instead of the select-entry scatter (atomics)
-  int preclean = 1;          // kano_verify resets the next front end's tables on its tail
-  bool front_clean = false;
-  std::array<i64, 6> fc_dims{};
-  uint64_t fc_ops = 0;       // kano_rec::g_ops after the reset: nothing may run in between
-  int m_contig = 0;          // the matrix in physically contiguous memory (experiment)
-  int alist_side = 0;        // kano_verify: the flat allowed-pod lists (k_pol_pods) on the
-                             // side stream beside the Mc chain (measured: front end +4-14 us,
-                             // the side stream then outlasts the Mc chain; off)
-  bool alist_side_ok = false, alist_pending = false;
-  int fork_late = 1;         // policy_shadow's side-stream tests issued after the build's
-                             // last launches (0: at the fork point)
-  bool xs_on = false, xs_done = false;
-  const int32_t* xs_gdev = nullptr;
-  int32_t xs_G = 0;
-  i64 xs_knb = 0, xs_kslots = 0;
   DBuf sig_ctr;              // the scans' arrival counter (one u32, zero between launches)
   u64 sig_seq = 0;           // last signal value handed to a scan
   u64 sig_armed = 0;         // the value the latest scan with host totals will raise
   u64 sig_wait = 0;          // what mirror_wait polls for (0: the event)
-  i64 sig_long[2] = {0, 0};  // (hosttime) waits past 1 ms: stream busy / stream idle
-  int sig_spin_us = 200;     // host signal: spin this long, then sleep between polls (-1: spin)
+  // kano_verify's host time per call (always on: a few clock reads), read by
+  // kano_host_times: [calls, front sum, back sum, wait sum, gap sum,
+  // front max, back max, wait max, call max, size waits 1..3 max]
+  double ht[12] = {};
+  double ht_wait_cur = 0.0;
+  int ht_wait = 0;
+  std::chrono::steady_clock::time_point ht_last{};
 
   hipEvent_t ev[10] = {};
-  // the matrix write (k_rows) runs on its own stream beside the checks, which
-  // only need class-level data; ev_rows marks its end
+  // policy_shadow's subset tests run on stream2 beside the Mc chain (forked
+  // at ev_fork2 once the lists and AC exist, joined through ev_join2)
   hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
+  bool fork_pending = false;
+  std::function<int()> fork_hook;
   // kano_verify's tail (result copies, policy_shadow's emission) beside the
   // matrix write (normal priority: a high-priority tail slowed k_rows 10%)
   hipStream_t stream3 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_rows = nullptr;
-  bool rows_pending = false;
-  bool rows_overlap = false;
+  hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_sizes = nullptr;
-  hipEvent_t ev_sync = nullptr;    // sync() with spin_wait
-  // asynchronous completion (knob async, default on): kano_verify returns once
-  // its host results (index lists, pairs) are in host memory; the matrix
-  // write ends on the engine stream, behind which every later engine
-  // operation queues, and every other entry point settles it first
-  int async_rows = 1;
+  // asynchronous completion: kano_verify returns once its host results
+  // (index lists, pairs) are in host memory; the matrix write ends on the
+  // engine stream, behind which every later engine operation queues, and
+  // every other entry point settles it first
   bool async_pending = false;
   hipEvent_t ev_tail = nullptr;    // the result copies of kano_verify's tail
-  // k_rows' launch times (ev[7] -> ev[8]), resolved once the launch is known
-  // to be complete: the last one, and sums since kano_rows_timing's reset
+  // the matrix write's launch times (ev[7] -> ev[8], recorded by its own
+  // dispatch), resolved once the launch is known to be complete: the last
+  // one, and sums since kano_rows_timing's reset
   bool rows_time_pending = false;
-  // k_rows timed by its own dispatch (hipExtLaunchKernel's start / stop
-  // events: no marker packets around the launch; knob extev); the tail's
-  // fork point is then a marker of its own
-  int rows_extev = 1;
-  // placement-probed matrix allocation (alloc_matrix): candidates, and the
-  // matrix sizes (MB) it applies to
-  int mprobe = 32;
-  i64 mprobe_budget_mb = 40960;   // candidate bytes held at once
-  i64 mprobe_min_mb = 64, mprobe_max_mb = 16384;
-  float mprobe_best_ms = 0.f, mprobe_worst_ms = 0.f;
-  int mprobe_tried = 0;
-  DBuf mprobe_perm;
+  hipEvent_t rows_fork = nullptr;    // what the tail waits on (a marker before the write)
   hipEvent_t ev_rows_fork = nullptr;
-  hipEvent_t rows_fork = nullptr;    // what the tail waits on (ev[7] or ev_rows_fork)
   float rows_ms_last = 0.f;
   double rows_ms_sum = 0.0, rows_ms_min = 0.0, rows_ms_max = 0.0;
   i64 rows_ms_n = 0;
-  int spin_wait = 0;   // kano_verify: the size slots reached the host buffer
   // kano_verify halves (kano_verify_shard -> kano_verify_combine)
   bool vs_open = false, vs_shadow = false, vs_cross_want = false, vs_cross_on = false;
-  bool vs_have_sys = false, vs_sys_on = false, vs_early = false;
+  bool vs_have_sys = false, vs_sys_on = false;
+  bool vs_rows = false;      // the combine writes the shard's rows (not after kano_checks_shard)
   i64 vs_nb = 0, vs_rl = 0;
 };
 
@@ -363,211 +261,24 @@ int fail(kano_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
-// ---- segments: the recorded operations of kano_verify (kano_graph.hpp) ----
-constexpr size_t GCACHE_MAX = 48;
-
-void seg_begin(kano_ctx* ctx) {
-  if (!ctx->graphs || ctx->seg_on) return;
-  ctx->rec.clear();
-  ctx->seg_on = true;
-  kano_rec::g_rec = &ctx->rec;
-}
-
-bool contains(const std::vector<uint64_t>& v, uint64_t h) {
-  return std::find(v.begin(), v.end(), h) != v.end();
-}
-
-// issue the recorded segment: a cached graph, a new capture (the second time
-// the same sequence comes), or the operations one by one
-int seg_end(kano_ctx* ctx) {
-  if (!ctx->seg_on) return 0;
-  ctx->seg_on = false;
-  kano_rec::g_rec = nullptr;
-  kano_rec::Recorder& r = ctx->rec;
-  if (r.ops.empty()) return 0;
-  const uint64_t h = r.hash;
-  for (size_t i = 0; i < ctx->gcache.size(); ++i) {
-    if (ctx->gcache[i].first != h) continue;
-    hipGraphExec_t ge = ctx->gcache[i].second;
-    if (hipGraphLaunch(ge, ctx->stream) != hipSuccess) {
-      (void)hipGetLastError();
-      break;                                     // issue directly below
-    }
-    ++ctx->g_hits;
-    return 0;
-  }
-  if (r.capturable && contains(ctx->gseen, h) && !contains(ctx->gbad, h)) {
-    hipGraph_t g = nullptr;
-    hipGraphExec_t ge = nullptr;
-    bool ok = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed) == hipSuccess;
-    if (ok) {
-      const hipError_t ei = kano_rec::issue(r);
-      const hipError_t ee = hipStreamEndCapture(ctx->stream, &g);
-      ok = ei == hipSuccess && ee == hipSuccess && g &&
-           hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
-    }
-    if (g) (void)hipGraphDestroy(g);
-    if (ok && hipGraphLaunch(ge, ctx->stream) == hipSuccess) {
-      if (ctx->gcache.size() >= GCACHE_MAX) {
-        (void)hipGraphExecDestroy(ctx->gcache.front().second);
-        ctx->gcache.erase(ctx->gcache.begin());
-      }
-      ctx->gcache.emplace_back(h, ge);
-      ++ctx->g_captures;
-      return 0;
-    }
-    if (ge) (void)hipGraphExecDestroy(ge);
-    (void)hipGetLastError();
-    ctx->gbad.push_back(h);                      // never again for this sequence
-  }
-  if (!contains(ctx->gseen, h)) {
-    if (ctx->gseen.size() >= 4 * GCACHE_MAX) ctx->gseen.erase(ctx->gseen.begin());
-    ctx->gseen.push_back(h);
-  }
-  ++ctx->g_direct;
-  const hipError_t e = kano_rec::issue(r);
-  if (e != hipSuccess) return fail(ctx, -EIO, std::string("issuing kernels: ") + hipGetErrorString(e));
-  return 0;
-}
-
-// the host is about to depend on the device (a wait, a free): issue what is
-// recorded so far and go on recording
-int seg_cut(kano_ctx* ctx) {
-  if (!ctx->seg_on) return 0;
-  const int rc = seg_end(ctx);
-  seg_begin(ctx);
-  return rc;
-}
-
-// operations issued directly for the scope (k_rows and its timing events)
-struct SegPause {
-  kano_ctx* c;
-  bool was;
-  int rc = 0;
-  explicit SegPause(kano_ctx* ctx) : c(ctx), was(ctx->seg_on) {
-    if (was) rc = seg_end(c);
-  }
-  ~SegPause() {
-    if (was) seg_begin(c);
-  }
-};
-
-// a recorded scope: kano_verify & co. (issued at the latest when it ends)
-struct SegScope {
-  kano_ctx* c;
-  explicit SegScope(kano_ctx* ctx) : c(ctx) { seg_begin(c); }
-  ~SegScope() { (void)seg_end(c); }
-};
-
 int settle(kano_ctx* ctx);
 
-// contig: ask for physically contiguous memory first (the matrix: knob
-// mcontig), plain hipMalloc when that fails
-int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes, bool contig = false) {
+int dalloc(kano_ctx* ctx, DBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.p && b.bytes >= bytes) return 0;
   if (b.p) {
-    KTRY(seg_cut(ctx));   // recorded operations may still use the old buffer
-    KTRY(settle(ctx));    // ... and an asynchronously completing matrix write
+    KTRY(settle(ctx));    // an asynchronously completing matrix write may still use it
     KCHK(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
   }
-  hipError_t e = hipErrorOutOfMemory;
-  if (contig) {
-    e = hipExtMallocWithFlags(&b.p, bytes, hipDeviceMallocContiguous);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      b.p = nullptr;
-    }
-  }
-  if (e != hipSuccess) e = hipMalloc(&b.p, bytes);
+  const hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) {
     b.p = nullptr;
     return fail(ctx, -ENOMEM, "hipMalloc(" + std::to_string(bytes) + " bytes) -> " +
                                   hipGetErrorString(e));
   }
   b.bytes = bytes;
-  return 0;
-}
-
-// The matrix write's store rate depends on where the allocation lands:
-// eight 1.25 GB allocations in one process took k_rows' store shape (random
-// rows, 16-B non-temporal lanes) at 4.6-4.9 TB/s on five and 5.4-5.5 TB/s
-// on three, each steadily (profiles/r02_store_alloc.txt).  So a matrix of
-// mprobe_min_mb..mprobe_max_mb is the best of up to mprobe candidate
-// allocations, each timed by a write of its own shape (k_place_probe, two
-// launches, the faster counts); the others are freed.  Once per allocation;
-// the matrix stays allocated across builds.
-int alloc_matrix(kano_ctx* ctx, size_t bytes, bool contig) {
-  DBuf& b = ctx->M;
-  if (bytes == 0) bytes = 16;
-  if (b.p && b.bytes >= bytes) return 0;
-  const i64 mb = (i64)(bytes >> 20);
-  const i64 ldM = std::max<i64>(1, ctx->ldM);
-  const i64 rows = (i64)(bytes / (sizeof(u64) * ldM));
-  if (ctx->mprobe < 2 || contig || mb < ctx->mprobe_min_mb || mb > ctx->mprobe_max_mb ||
-      rows < 1 || rows > (i64)UINT32_MAX)
-    return dalloc(ctx, b, bytes, contig);
-  if (b.p) {
-    KTRY(seg_cut(ctx));
-    KTRY(settle(ctx));    // the previous matrix write may still run
-    KCHK(hipFree(b.p));
-    b.p = nullptr;
-    b.bytes = 0;
-  }
-  const i64 wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
-  // the probe's row order: a seeded random permutation (xorshift Fisher-Yates)
-  std::vector<int32_t> perm((size_t)rows);
-  for (i64 i = 0; i < rows; ++i) perm[(size_t)i] = (int32_t)i;
-  u64 x = 0x9e3779b97f4a7c15ull;
-  for (i64 i = rows - 1; i > 0; --i) {
-    x ^= x << 13;
-    x ^= x >> 7;
-    x ^= x << 17;
-    std::swap(perm[(size_t)i], perm[(size_t)(x % (u64)(i + 1))]);
-  }
-  KTRY(dalloc(ctx, ctx->mprobe_perm, sizeof(int32_t) * (size_t)rows));
-  KCHK(hipMemcpy(ctx->mprobe_perm.p, perm.data(), sizeof(int32_t) * (size_t)rows,
-                 hipMemcpyHostToDevice));
-  std::vector<void*> cand;
-  std::vector<float> ms;
-  SegPause pause(ctx);
-  KTRY(pause.rc);
-  const int ncand = (int)std::max<i64>(2, std::min<i64>(ctx->mprobe,
-                                                        ctx->mprobe_budget_mb / std::max<i64>(1, mb)));
-  for (int k = 0; k < ncand; ++k) {
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      break;
-    }
-    float t3[3];
-    for (int rep = 0; rep < 3; ++rep) {
-      KCHK(hipEventRecord(ctx->ev[7], ctx->stream));
-      hipLaunchKernelGGL(k_place_probe, dim3((unsigned)rows), dim3(TPB), 0, ctx->stream,
-                         static_cast<u64*>(p), ldM, static_cast<const int32_t*>(ctx->mprobe_perm.p), wW);
-      KLAUNCH();
-      KCHK(hipEventRecord(ctx->ev[8], ctx->stream));
-      KCHK(hipEventSynchronize(ctx->ev[8]));
-      KCHK(hipEventElapsedTime(&t3[rep], ctx->ev[7], ctx->ev[8]));
-    }
-    std::sort(t3, t3 + 3);
-    cand.push_back(p);
-    ms.push_back(t3[1]);   // the median of three
-  }
-  ctx->rows_time_pending = false;   // ev[7] / ev[8] were reused
-  if (cand.empty()) return dalloc(ctx, b, bytes, contig);
-  size_t kb = 0;
-  for (size_t k = 1; k < cand.size(); ++k)
-    if (ms[k] < ms[kb]) kb = k;
-  for (size_t k = 0; k < cand.size(); ++k)
-    if (k != kb) KCHK(hipFree(cand[k]));
-  b.p = cand[kb];
-  b.bytes = bytes;
-  ctx->mprobe_tried = (int)cand.size();
-  ctx->mprobe_best_ms = ms[kb];
-  ctx->mprobe_worst_ms = *std::max_element(ms.begin(), ms.end());
   return 0;
 }
 
@@ -671,7 +382,7 @@ struct ScanBatch {
     int writers = jobs.npub > 0 ? 1 : 0;
     for (int q = 0; q < jobs.count; ++q) writers += jobs.j[q].total_host ? 1 : 0;
     jobs.sig_host = nullptr;
-    if (writers > 0 && ctx->mirror_sig && !ctx->graphs && ctx->sig_ctr.p) {
+    if (writers > 0 && ctx->sig_ctr.p) {
       jobs.sig_host = ctx->gmirror_dev + SZ_SIGNAL;
       jobs.sig_val = ++ctx->sig_seq;
       jobs.sig_ctr = reinterpret_cast<uint32_t*>(ctx->sig_ctr.p);
@@ -684,7 +395,7 @@ struct ScanBatch {
     u64* cur = st + (ctx->scan_parity ? ctx->scan_cap : 0);
     u64* nxt = st + (ctx->scan_parity ? 0 : ctx->scan_cap);
     const dim3 g((unsigned)maxt, (unsigned)jobs.count);
-    switch (ctx->scan_slots ? jobs.count : MAX_SCAN_JOBS) {
+    switch (jobs.count) {
       case 1: launch_n<1>(g, cur, nxt); break;
       case 2: launch_n<2>(g, cur, nxt); break;
       case 3: launch_n<3>(g, cur, nxt); break;
@@ -759,64 +470,7 @@ int FillBatch::run() {
   return 0;
 }
 
-// Issue the enclosed launches on stream2 (forked from the main stream at
-// construction, joined through ev_join3 at destruction; the main stream waits
-// for it with side_join): ctx->stream and the scan status buffers are swapped
-// for the duration, so every launch helper sends its work there unchanged.
-struct SideIssue {
-  kano_ctx* c;
-  bool on;
-  SideIssue(kano_ctx* ctx, bool enable) : c(ctx), on(enable && ctx->stream2) {
-    if (!on) return;
-    if (hipEventRecord(c->ev_fork3, c->stream) != hipSuccess ||
-        hipStreamWaitEvent(c->stream2, c->ev_fork3, 0) != hipSuccess) {
-      on = false;
-      return;
-    }
-    swap();
-  }
-  void swap() {
-    std::swap(c->stream, c->stream2);
-    std::swap(c->scan_tmp, c->scan_tmp_side);
-    std::swap(c->scan_cap, c->scan_cap_side);
-    std::swap(c->scan_parity, c->scan_parity_side);
-  }
-  ~SideIssue() {
-    if (!on) return;
-    swap();
-    if (hipEventRecord(c->ev_join3, c->stream2) == hipSuccess) c->side_pending = true;
-  }
-};
-
-int side_join(kano_ctx* ctx) {
-  if (!ctx->side_pending) return 0;
-  ctx->side_pending = false;
-  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join3, 0));
-  return 0;
-}
-
-// host waits: with spin_wait (experiment) the host polls the event instead
-// of blocking in the runtime.  Measured on C3: +0.02 ms a step -- each
-// hipEventQuery costs more than the runtime's own wake-up -- so it is off.
-int wait_event(kano_ctx* ctx, hipEvent_t ev) {
-  KTRY(seg_cut(ctx));
-  if (ctx->spin_wait) {
-    hipError_t e;
-    while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
-    }
-    KCHK(e);
-    return 0;
-  }
-  KCHK(hipEventSynchronize(ev));
-  return 0;
-}
-
 int sync(kano_ctx* ctx) {
-  KTRY(seg_cut(ctx));
-  if (ctx->spin_wait) {
-    KCHK(hipEventRecord(ctx->ev_sync, ctx->stream));
-    return wait_event(ctx, ctx->ev_sync);
-  }
   KCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -856,8 +510,8 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 
 // the overlapped syncs: the slots reach their host mirror inside the scans
 // (totals) or by a scan's publish list (atomic slots); the host records an
-// event behind them now, queues more work, and later waits on the event and
-// reads the mirror -- no copy
+// event behind them now (unless a scan raises the host signal), queues more
+// work, and later waits and reads the mirror -- no copy
 int mirror_begin(kano_ctx* ctx) {
   // the latest scan with host totals raises the host signal: nothing to queue
   if (ctx->sig_armed) {
@@ -866,42 +520,25 @@ int mirror_begin(kano_ctx* ctx) {
     return 0;
   }
   ctx->sig_wait = 0;
-  // the host waits on this event: it is recorded outside any graph (an event
-  // recorded during a capture only orders the graph's own nodes)
-  SegPause pause(ctx);
-  KTRY(pause.rc);
   KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
   return 0;
 }
 
-// Poll the host signal word: spin for sig_spin_us (the syncs' usual waits
-// are 30-100 us), then poll between short sleeps, so that a long wait does
-// not hold a core (knob sigspin); past a second (a slow device, a failed
-// launch) the stream's own synchronisation decides.
+// Poll the host signal word (the syncs' waits are 30-100 us: the host spins,
+// it does not sleep -- a sleeping host's wake-up is at the scheduler's
+// mercy).  The sequence numbers only grow, so any value >= val means the
+// slots arrived.  Past a second (a slow device, a failed launch) the
+// stream's own synchronisation decides.
 int wait_signal(kano_ctx* ctx, u64 val) {
-  KTRY(seg_cut(ctx));
   volatile u64* sig = ctx->gmirror + SZ_SIGNAL;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
-  bool noted = false, sleepy = false;
-  for (uint32_t spin = 1; *sig != val; ++spin) {
-    if (sleepy) {
-      struct timespec ts = {0, 10000};
-      nanosleep(&ts, nullptr);
-    } else {
-      __builtin_ia32_pause();
-    }
-    if ((spin & 0xff) != 0 && !sleepy) continue;
-    const auto dt = clk::now() - t0;
-    if (!sleepy && ctx->sig_spin_us >= 0 && dt > std::chrono::microseconds(ctx->sig_spin_us))
-      sleepy = true;
-    if (ctx->host_timing && !noted && dt > std::chrono::milliseconds(1)) {
-      noted = true;   // (diagnostic) a long wait: is the stream still busy?
-      ctx->sig_long[hipStreamQuery(ctx->stream) == hipSuccess ? 1 : 0] += 1;
-    }
-    if (dt > std::chrono::seconds(1)) {
+  for (uint32_t spin = 1; *sig < val; ++spin) {
+    __builtin_ia32_pause();
+    if ((spin & 0xfff) != 0) continue;
+    if (clk::now() - t0 > std::chrono::seconds(1)) {
       KCHK(hipStreamSynchronize(ctx->stream));
-      if (*sig != val) return fail(ctx, -EIO, "internal: host signal not raised");
+      if (*sig < val) return fail(ctx, -EIO, "internal: host signal not raised");
       break;
     }
   }
@@ -915,15 +552,14 @@ int mirror_wait(kano_ctx* ctx, int first, int count, i64* out) {
     ctx->sig_wait = 0;
     KTRY(wait_signal(ctx, v));
   } else {
-    KTRY(wait_event(ctx, ctx->ev_sizes));
+    KCHK(hipEventSynchronize(ctx->ev_sizes));
   }
-  if (ctx->host_timing) {
-    const double w =
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    ctx->ht[4] += w;
-    ctx->ht[5 + std::min(ctx->ht_wait++, 2)] += w;
-  }
-  for (int k = 0; k < count; ++k) out[k] = (i64)((volatile u64*)ctx->gmirror)[first + k];
+  const double w =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  ctx->ht_wait_cur += w;
+  const int k = 9 + std::min(ctx->ht_wait++, 2);
+  ctx->ht[k] = std::max(ctx->ht[k], w);
+  for (int q = 0; q < count; ++q) out[q] = (i64)((volatile u64*)ctx->gmirror)[first + q];
   return 0;
 }
 
@@ -1015,23 +651,6 @@ int classify_alloc2(kano_ctx* ctx, ClassSet& cs) {
   return dalloc(ctx, cs.cval, sizeof(int32_t) * std::max<i64>(1, (i64)cs.KS * cs.U));
 }
 
-// the fused crosscheck sort's arguments (nb = 0 when it is not armed)
-KeySort xs_sort(kano_ctx* ctx) {
-  KeySort k{};
-  if (!ctx->xs_on) return k;
-  k.U = ctx->rc.U;
-  k.nb = ctx->xs_knb;
-  k.mcnt = P_<int32_t>(ctx->rc.mcnt);
-  k.gmin = P_<int32_t>(ctx->gmin);
-  k.gmax = P_<int32_t>(ctx->gmax);
-  k.G = ctx->xs_G;
-  k.ckey = P_<int32_t>(ctx->ckey);
-  k.hist = P_<int32_t>(ctx->kcnt) + 2 * ((i64)ctx->xs_G + 1);
-  k.hoff = P_<int32_t>(ctx->koff);
-  k.order = P_<int32_t>(ctx->corder);
-  return k;
-}
-
 // phase 2a, both sides, without the class counts (the host reads them
 // meanwhile): ids, member counts, their offsets (scanned over the side's pod
 // count; the entries past U are zero), member lists of pods [m0, m1)
@@ -1048,11 +667,8 @@ int classify_phase2a(kano_ctx* ctx) {
   KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ma, P_<int32_t>(ctx->cc.moff)));
   KTRY(sb.run());
   if (rl > 0) {
-    const bool x = ctx->xs_on;
     hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr,
-                       x ? ctx->xs_gdev : (const int32_t*)nullptr, ctx->xs_G,
-                       x ? P_<int32_t>(ctx->gmin) : (int32_t*)nullptr,
-                       x ? P_<int32_t>(ctx->gmax) : (int32_t*)nullptr,
+                       (const int32_t*)nullptr, 0, (int32_t*)nullptr, (int32_t*)nullptr,
                        reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR));
     KLAUNCH();
   }
@@ -1067,7 +683,7 @@ int classify_phase2b(kano_ctx* ctx, FillJobs fj) {
   if (U > 0) {
     const unsigned nbv = nblk(U), nbf = fill_ride_blocks(fj);
     hipLaunchKernelGGL(k_cls_vals, dim3(nbv + nbf, 2), dim3(TPB), 0, ctx->stream,
-                       P_<int32_t>(ctx->pv), ctx->n, pr, xs_sort(ctx), fj, nbv);
+                       P_<int32_t>(ctx->pv), ctx->n, pr, fj, nbv);
     KLAUNCH();
   } else if (fj.count > 0) {
     hipLaunchKernelGGL(k_fill_many, dim3(fill_ride_blocks(fj)), dim3(TPB), 0, ctx->stream, fj);
@@ -1140,10 +756,6 @@ int match_both(kano_ctx* ctx) {
   const i64 maxU = std::max(a0.live ? a0.U : 0, a1.live ? a1.U : 0);
   const unsigned rows_i = (a0.live ? a0.NM : 0) + (a1.live ? a1.NM : 0);
   const unsigned rows_f = (a0.live ? a0.NM + 1 : 0) + (a1.live ? a1.NM + 1 : 0);
-  // the fused crosscheck sort: its histogram (k_cls_vals) is scanned with
-  // the join's group counts, its placement is k_join_fill's last grid row
-  KeySort ks = xs_sort(ctx);
-  bool hist_scanned = false;
   if (rows_i > 0) {
     hipLaunchKernelGGL(k_join_insert, dim3(nblk(maxU), rows_i), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
@@ -1153,27 +765,10 @@ int match_both(kano_ctx* ctx) {
       if (pr.s[q].live && sx.NM > 0)
         KTRY(sb.add(P_<int32_t>(sx.gcnt), (i64)sx.NM * sx.T, P_<int32_t>(sx.goff)));
     }
-    if (ks.nb > 0) {
-      KTRY(sb.add(ks.hist, ctx->xs_kslots, P_<int32_t>(ctx->koff)));
-      hist_scanned = true;
-    }
     KTRY(sb.run());
   }
-  if (ks.nb > 0 && !hist_scanned) {
-    ScanBatch sb(ctx);
-    KTRY(sb.add(ks.hist, ctx->xs_kslots, P_<int32_t>(ctx->koff)));
-    KTRY(sb.run());
-  }
-  const bool place = ks.nb > 0 && rows_f > 0 && nblk(maxU) >= ks.nb;
-  if (ks.nb > 0 && !place) {
-    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)ks.nb), dim3(TPB), 0, ctx->stream, ks);
-    KLAUNCH();
-  }
-  if (ks.nb > 0) ctx->xs_done = true;
-  if (!place) ks.nb = 0;
   if (rows_f > 0) {
-    hipLaunchKernelGGL(k_join_fill, dim3(nblk(maxU), rows_f + (place ? 1 : 0)), dim3(TPB), 0,
-                       ctx->stream, pr, ks);
+    hipLaunchKernelGGL(k_join_fill, dim3(nblk(maxU), rows_f), dim3(TPB), 0, ctx->stream, pr);
     KLAUNCH();
     hipLaunchKernelGGL(k_join_match, dim3(nblk(ctx->P), 2), dim3(TPB), 0, ctx->stream, ctx->P, pr);
     KLAUNCH();
@@ -1218,8 +813,8 @@ int sel_spb(const kano_ctx* ctx) {
   return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
 }
 
-// The front end's first fills (size slots, both sides' hash tables and
-// smallest-member slots) and their shape (front_dims: re-used only if equal)
+// The front end's first fills: size slots, both sides' hash tables and
+// smallest-member slots
 int front_fills(kano_ctx* ctx, FillBatch& fb) {
   KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
   KTRY(fb.add(ctx->sizes, sizeof(u64) * SZ_SLOTS, 0u));
@@ -1227,32 +822,15 @@ int front_fills(kano_ctx* ctx, FillBatch& fb) {
   KTRY(classify_alloc1(ctx, ctx->cc, fb));
   return 0;
 }
-std::array<i64, 6> front_dims(const kano_ctx* ctx) {
-  return {ctx->n, ctx->r0, ctx->r1, ctx->rc.packed, ctx->cc.packed,
-          (i64)reinterpret_cast<uintptr_t>(ctx->rc.table.p)};
-}
 
-int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::function<int()>()) {
+int do_front(kano_ctx* ctx, int path) {
   ctx->rc.m0 = ctx->r0;
   ctx->rc.m1 = ctx->r1;
   ctx->cc.m0 = 0;
   ctx->cc.m1 = ctx->n;
-  // the size slots and hash tables arrive clean when the previous kano_verify
-  // reset them on its tail stream beside its matrix write (front_clean)
-  const bool clean = ctx->front_clean && ctx->fc_dims == front_dims(ctx) &&
-                     ctx->fc_ops == kano_rec::g_ops;
-  ctx->front_clean = false;
   {
     FillBatch fb(ctx);
     KTRY(front_fills(ctx, fb));
-    if (clean) (void)fb.take();
-    if (ctx->xs_on) {   // group ranges per row class (k_cls_mfill), <= one per local pod
-      const i64 m = std::max<i64>(1, ctx->rc.m1 - ctx->rc.m0);
-      KTRY(dalloc(ctx, ctx->gmin, sizeof(int32_t) * m));
-      KTRY(dalloc(ctx, ctx->gmax, sizeof(int32_t) * m));
-      KTRY(fb.add(ctx->gmin, sizeof(int32_t) * m, 0x7fffffffu));
-      KTRY(fb.add(ctx->gmax, sizeof(int32_t) * m, 0xffffffffu));
-    }
     KTRY(fb.run());
   }
   KTRY(classify_phase1(ctx));
@@ -1294,22 +872,7 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
     KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (Ur + 1)));
     KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
-    // (carried by k_cls_vals' launch unless side work sits between)
-    if (ctx->xs_on) {   // the fused crosscheck sort's buffers (as cross_prepare sizes them)
-      const i64 G = ctx->xs_G;
-      ctx->xs_knb = std::max<i64>(1, nblk(Ur, (i64)TPB * KEY_ITEMS));
-      ctx->xs_kslots = (G + 1) * ctx->xs_knb;
-      KTRY(dalloc(ctx, ctx->ckey, sizeof(int32_t) * std::max<i64>(1, Ur)));
-      KTRY(dalloc(ctx, ctx->corder, sizeof(int32_t) * std::max<i64>(1, Ur)));
-      KTRY(dalloc(ctx, ctx->kcnt, sizeof(int32_t) * 2 * (G + 1) + sizeof(int32_t) * ctx->xs_kslots));
-      KTRY(dalloc(ctx, ctx->koff, sizeof(int32_t) * (ctx->xs_kslots + 1)));
-    }
-    if (side || !ctx->hfuse) KTRY(fb.run());
-    else carried = fb.take();
-  }
-  if (side) {   // the size-independent back-end work, beside the join (stream2)
-    SideIssue si(ctx, true);
-    KTRY(side());
+    carried = fb.take();   // (carried by k_cls_vals' launch)
   }
   KTRY(classify_phase2b(ctx, carried));
   KTRY(match_both(ctx));
@@ -1333,7 +896,7 @@ int do_front(kano_ctx* ctx, int path, const std::function<int()>& side = std::fu
     a.cost = P_<unsigned long long>(ctx->cost);
     a.mcnt = P_<int32_t>(ctx->rc.mcnt);
     a.W = ctx->W;
-    a.ch = ctx->ch;
+    a.ch = ROWS_CH;
     a.force = path == KANO_PATH_MFMA ? 2 : 0;
     a.wicnt = P_<int32_t>(ctx->wicnt);
     a.hflag = P_<int32_t>(ctx->hflag);
@@ -1404,9 +967,11 @@ int build_alist(kano_ctx* ctx, hipStream_t st = nullptr, bool launch = true) {
   return 0;
 }
 
-// Mc rows written whole (k_mc_rows) when a wave's row fits LDS
-bool mc_rows_on(const kano_ctx* ctx) {
-  return ctx->mc_rows && ctx->ldC > 0 && ctx->ldC * 8 <= 64 * 1024;
+// the matrix write from the class-level table (k_rows_mc): its LDS table
+// holds 4 bytes per column class
+bool rows_mc_fits(const kano_ctx* ctx) {
+  return !ctx->rows_from && ctx->Mc.p &&
+         sizeof(uint32_t) * (size_t)std::max<i64>(1, ctx->cc.U) <= ROWS_MC_LDS_MAX;
 }
 
 // the part of the back end that needs only the class counts: zeroed AC,
@@ -1425,7 +990,7 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const std::function<in
     KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
     KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
     KTRY(fb.add(ctx->scur, sizeof(int32_t) * U, 0u));
-    if (!mc_rows_on(ctx)) KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
+    KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
     KTRY(fb.add(ctx->col_or_c, sizeof(u64) * ldMc, 0u));
     KTRY(fb.add(ctx->col_nand_c, sizeof(u64) * ldMc, 0u));
     if (pre_fill) KTRY(pre_fill(fb));
@@ -1469,7 +1034,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     }
     if (extra) KTRY(extra(fb));   // the caller's fills (kano_verify: crosscheck, shadow)
     // (carried by k_sel_place's launch: it neither reads nor writes them)
-    if (U > 0 && P > 0 && ctx->hfuse) carried = fb.take();
+    if (U > 0 && P > 0) carried = fb.take();
     else KTRY(fb.run());
   }
   if (U > 0 && P > 0) {
@@ -1482,7 +1047,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   // S(c) sorted, heavy list and work-item map (k_class_lists) and the
   // allowed classes + bits per policy (k_pol_allow_fill): independent, one
-  // launch when both run (hfuse)
+  // launch when both run
   const bool lists_on = U > 0, allow_on = P > 0 && ctx->cc.U > 0;
   const ClassListsArgs cla{P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), P > 0 ? 1 : 0,
                            P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), P_<int32_t>(ctx->hlist),
@@ -1492,67 +1057,43 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                          P_<u64>(ctx->AC), ctx->ldC};
   const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
                          ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
-  if (lists_on && allow_on && ctx->hfuse) {
+  if (lists_on && allow_on) {
     const unsigned nb1 = nblk(U, TPB / 64);
     hipLaunchKernelGGL(k_lists_allow, dim3(nb1 + nblk(P, WPB)), dim3(TPB), lds, ctx->stream, cla,
                        paa, nb1);
     KLAUNCH();
-  } else {
-    if (lists_on) {
-      hipLaunchKernelGGL(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, cla);
-      KLAUNCH();
-    }
-    if (allow_on) {
-      hipLaunchKernelGGL(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, paa);
-      KLAUNCH();
-    }
+  } else if (lists_on) {
+    hipLaunchKernelGGL(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, cla);
+    KLAUNCH();
+  } else if (allow_on) {
+    hipLaunchKernelGGL(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, paa);
+    KLAUNCH();
   }
   if (ctx->fork_hook) KTRY(ctx->fork_hook());   // lists and AC are complete here
-  // light rows read either the flat allowed-pod lists (materialised here,
-  // one pass over nnz_alw entries) or the column-class member lists (n
-  // entries, cache-resident).  With the flattened walk in k_rows the flat
-  // lists win wherever the light rows read them at all (measured: C3 at 1/8
-  // of the rows k_rows 99 -> 49 us; C5 21.8 -> 20.9 ms); where nearly every
-  // class is heavy (C4) building them is pure cost (+0.45 ms a step)
+  // The matrix write reads the class-level table (k_rows_mc) when it fits
+  // LDS; otherwise (very many column classes, C5) it rebuilds rows from the
+  // allowed-pod lists (k_rows): the flat lists (materialised here, one pass
+  // over nnz_alw entries) or the column-class member lists (n entries,
+  // cache-resident).  The flat lists win wherever the light rows read them
+  // at all (measured: C3 at 1/8 of the rows k_rows 99 -> 49 us; C5 21.8 ->
+  // 20.9 ms); where nearly every class is heavy (C4) building them is pure
+  // cost (+0.45 ms a step)
   ctx->alist_valid = false;
-  int ua = ctx->rows_alist;
-  if (ua < 0)
-    ua = ctx->light_cost * 16 > ctx->nnz_alw && ctx->nnz_alw * 4 <= (2ll << 30) ? 1 : 0;
-  ctx->rows_use_alist = ua && ctx->light_cost > 0;
-  // (alist_side: kano_verify builds the flat lists on the side stream with
-  // policy_shadow's tests, joined before the matrix write)
-  // (k_pol_pods' blocks ride in the Mc scatter's launch when both run)
+  const bool lists_rows = !rows_mc_fits(ctx);
+  ctx->rows_use_alist = lists_rows && ctx->light_cost > 0 && ctx->light_cost * 16 > ctx->nnz_alw &&
+                        ctx->nnz_alw * 4 <= (2ll << 30);
+  // (k_pol_pods' blocks ride in the Mc launch when both run)
   const McScatterArgs msa{ctx->nnz_sel, P_<int32_t>(ctx->ecls), P_<int32_t>(ctx->slist),
                           P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
                           H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr,
                           P_<u64>(ctx->Mc), ldMc};
-  const bool scatter_on = U > 0 && !mc_rows_on(ctx) && ctx->nnz_sel > 0;
-  bool pods_in_scatter = false;
-  if (ctx->rows_use_alist) {
-    if (ctx->alist_side_ok && !(ctx->rows_hook && H == 0)) {
-      ctx->alist_pending = true;
-    } else {
-      pods_in_scatter = ctx->hfuse && scatter_on && !(ctx->rows_hook && H == 0) && P > 0 &&
-                        ctx->cc.U > 0;
-      KTRY(build_alist(ctx, nullptr, !pods_in_scatter));
-    }
-  }
-  if (ctx->rows_hook && H == 0) KTRY(ctx->rows_hook());   // no heavy rows: M needs no Mc
+  const bool scatter_on = U > 0 && ctx->nnz_sel > 0;
+  const bool pods_in_scatter = ctx->rows_use_alist && scatter_on && P > 0 && ctx->cc.U > 0;
+  if (ctx->rows_use_alist) KTRY(build_alist(ctx, nullptr, !pods_in_scatter));
   if (U == 0) return 0;
-  if (mc_rows_on(ctx)) {
-    const bool four = 4 * ldMc * 8 <= 64 * 1024;
-    const size_t lds = sizeof(u64) * (size_t)ldMc * (four ? 4 : 1);
-    const int32_t* hf = H > 0 ? P_<int32_t>(ctx->hflag) : (const int32_t*)nullptr;
-    if (four)
-      hipLaunchKernelGGL(k_mc_rows<4>, dim3(nblk(U, 4)), dim3(256), lds, ctx->stream, U,
-                         P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
-                         P_<int32_t>(ctx->alc), hf, mfma ? 1 : 0, P_<u64>(ctx->Mc), ldMc);
-    else
-      hipLaunchKernelGGL(k_mc_rows<1>, dim3((unsigned)U), dim3(64), lds, ctx->stream, U,
-                         P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
-                         P_<int32_t>(ctx->alc), hf, mfma ? 1 : 0, P_<u64>(ctx->Mc), ldMc);
-  } else if (ctx->mc_own && (pods_in_scatter || scatter_on) &&
-             (size_t)ldMc * 8 * (TPB / 64) <= 64 * 1024) {
+  if (scatter_on && (size_t)ldMc * 8 * (TPB / 64) <= 64 * 1024) {
+    // light Mc rows by their owner (a wave per row class, the row in LDS,
+    // plain stores)
     const size_t lds = sizeof(u64) * (size_t)ldMc * (TPB / 64);
     const McOwnArgs moa{U, P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), P_<i64>(ctx->alcoff),
                         P_<int32_t>(ctx->alc), P_<int32_t>(ctx->rc.mcnt),
@@ -1565,15 +1106,20 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     } else {
       hipLaunchKernelGGL(k_mc_own, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, moa);
     }
-  } else if (pods_in_scatter) {
-    const unsigned nb1 = nblk(P, WPB);
-    hipLaunchKernelGGL(k_pods_scatter, dim3(nb1 + nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
-                       ctx->stream, pol_pods_args(ctx), msa, nb1);
+    KLAUNCH();
   } else if (scatter_on) {
-    hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0, ctx->stream,
-                       msa);
+    // very wide class-level rows: the select entries' allowed classes OR-ed
+    // into Mc with atomics (one wave per select entry)
+    if (pods_in_scatter) {
+      const unsigned nb1 = nblk(P, WPB);
+      hipLaunchKernelGGL(k_pods_scatter, dim3(nb1 + nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
+                         ctx->stream, pol_pods_args(ctx), msa, nb1);
+    } else {
+      hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
+                         ctx->stream, msa);
+    }
+    KLAUNCH();
   }
-  KLAUNCH();
   if (H > 0) {
     if (mfma) {
       const i64 Ua = ctx->cc.U;
@@ -1594,8 +1140,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       // (at least MFMA_KMIN policy blocks per wave: the epilogue, 16 ballots
       // and OR-atomics per 32-row tile, must not dominate)
       const i64 ksplit = std::max<i64>(
-          1, std::min<i64>((ctx->PB + ctx->mfma_kmin - 1) / ctx->mfma_kmin,
-                           2048 / std::max<i64>(1, tiles)));
+          1, std::min<i64>((ctx->PB + MFMA_KMIN - 1) / MFMA_KMIN, 2048 / std::max<i64>(1, tiles)));
       const i64 kchunk = (ctx->PB + ksplit - 1) / ksplit;
       const unsigned gy = (unsigned)((ctx->PB + kchunk - 1) / kchunk);
       for (i64 h0 = 0; h0 < H; h0 += HT_ROWS) {
@@ -1620,7 +1165,6 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       KLAUNCH();
     }
   }
-  if (ctx->rows_hook && H > 0) KTRY(ctx->rows_hook());    // heavy rows copy from Mc
   if (!ctx->cols_deferred) KTRY(mc_cols(ctx));
   return 0;
 }
@@ -1640,25 +1184,61 @@ int do_rows(kano_ctx* ctx) {
   return 0;
 }
 
-// the matrix write (heavy rows from Mc, then k_rows) on stream2
-int launch_rows(kano_ctx* ctx, bool side = false) {
+// The matrix write, timed by its own dispatch (hipExtLaunchKernelGGL's start
+// / stop events ev[7] -> ev[8]: no marker packets around it; the bench's
+// roofline reads them through kano_rows_timing).  k_rows_mc (address order,
+// from Mc and the column classes) wherever its LDS table fits, else k_rows
+// (heavy rows expanded from Mc first, then every class row rebuilt from the
+// allowed-pod lists and streamed to its members).
+int launch_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
-  if (rl == 0 || W == 0 || ctx->wi_total == 0) return 0;
-  // the matrix write and its timing events are issued directly (the events
-  // time k_rows for the bench's roofline); what was recorded before goes first
-  SegPause pause(ctx);
-  KTRY(pause.rc);
-  // the matrix write saturates HBM and starves kernels beside it (measured:
-  // overlapping it with the checks on stream2 was slower), so it runs in
-  // order on the main stream unless rows_overlap is set
+  ctx->rows_kernel = 0;
+  if (rl == 0 || W == 0) return 0;
   hipStream_t rs = ctx->stream;
-  if (ctx->rows_overlap || side) {
-    KCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
-    KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-    ctx->rows_pending = true;
-    rs = ctx->stream2;
+  KTRY(resolve_rows_time(ctx));   // the previous launch's pair is reused
+  ctx->rows_fork = ctx->ev_rows_fork;
+  KCHK(hipEventRecord(ctx->rows_fork, rs));
+  hipEvent_t e0 = ctx->ev[7], e1 = ctx->ev[8];
+  if (rows_mc_fits(ctx)) {
+    RowsMcArgs m{};
+    m.Mc = P_<u64>(ctx->Mc);
+    m.ldC = ctx->ldC;
+    m.UAW = ctx->UAW;
+    m.Ua = ctx->cc.U;
+    m.rcls = P_<int32_t>(ctx->rc.cls);
+    m.ccls = P_<int32_t>(ctx->cc.cls);
+    m.n = n;
+    m.ldM = ldM;
+    m.r0 = ctx->r0;
+    m.rl = rl;
+    m.M = P_<u64>(ctx->M);
+    const size_t lds = sizeof(uint32_t) * (size_t)std::max<i64>(1, ctx->cc.U);
+    const dim3 grid((unsigned)((rl + XR - 1) / XR));
+    static bool attr_set = false;
+    if (!attr_set) {   // dynamic LDS beyond 64 KiB
+      (void)hipFuncSetAttribute((const void*)k_rows_mc<256>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
+      (void)hipFuncSetAttribute((const void*)k_rows_mc<512>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
+      (void)hipFuncSetAttribute((const void*)k_rows_mc<1024>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
+      (void)hipGetLastError();
+      attr_set = true;
+    }
+    if (ctx->rows_mc_nt == 1024)
+      hipExtLaunchKernelGGL(k_rows_mc<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, m);
+    else if (ctx->rows_mc_nt == 256)
+      hipExtLaunchKernelGGL(k_rows_mc<256>, grid, dim3(256), lds, rs, e0, e1, 0, m);
+    else
+      hipExtLaunchKernelGGL(k_rows_mc<512>, grid, dim3(512), lds, rs, e0, e1, 0, m);
+    KLAUNCH();
+    ctx->rows_kernel = 1;
+    ctx->rows_timed = true;
+    ctx->rows_time_pending = true;
+    return 0;
   }
+  if (ctx->wi_total == 0) return 0;
   if (ctx->heavy_count > 0) {
     hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(ctx->heavy_count, HEXP_CLS)),
                        dim3(TPB), 0, rs, P_<int32_t>(ctx->hlist), (i64)ctx->heavy_count,
@@ -1667,9 +1247,8 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
                        P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     KLAUNCH();
   }
-  const i64 wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
-  const int cww = (int)std::min<i64>(wW, ctx->cww_max);
-  const unsigned ncc = (unsigned)((wW + cww - 1) / cww);
+  const int cww = (int)std::min<i64>(ldM, ctx->rows_cww);
+  const unsigned ncc = (unsigned)((ldM + cww - 1) / cww);
   RowsArgs a{};
   a.wioff = P_<int32_t>(ctx->wioff);
   a.wicls = P_<int32_t>(ctx->wicls);
@@ -1687,65 +1266,23 @@ int launch_rows(kano_ctx* ctx, bool side = false) {
   a.hflag = ctx->heavy_count > 0 ? P_<int32_t>(ctx->hflag) : nullptr;
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
-  a.wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
+  a.wW = ldM;
   a.r0 = ctx->r0;
   a.n = n;
   a.W = W;
-  a.ch = ctx->ch;
+  a.ch = ROWS_CH;
   a.cww = cww;
-  a.probe = ctx->rows_probe;
-  a.store_mode = ctx->rows_store;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
-  int nt = ctx->rows_nt;
-  if (nt == 0) nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
-  KTRY(resolve_rows_time(ctx));   // the previous launch's pair is reused
-  const bool ext = ctx->rows_extev && !ctx->rows_order;
-  ctx->rows_fork = ext ? ctx->ev_rows_fork : ctx->ev[7];
-  KCHK(hipEventRecord(ctx->rows_fork, rs));
+  const int nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   const size_t lds = sizeof(u64) * cww;
-  if (ctx->rows_order && ctx->heavy_count == 0 && rl <= (i64)INT32_MAX) {
-    // pod order: one row per block, consecutive blocks on consecutive rows
-    a.rcls = P_<int32_t>(ctx->rc.cls);
-    a.nitems = rl;
-    if (ctx->rows_order == 2) a.probe = 4;   // XCD-local sweeps
-    const dim3 g((unsigned)(ctx->rows_order == 2 ? (rl + 7) / 8 * 8 : rl), ncc);
-    if (nt == 1024) hipLaunchKernelGGL(k_rows_ord<1024>, g, dim3(1024), lds, rs, a);
-    else if (nt == 512) hipLaunchKernelGGL(k_rows_ord<512>, g, dim3(512), lds, rs, a);
-    else hipLaunchKernelGGL(k_rows_ord<256>, g, dim3(256), lds, rs, a);
-    KLAUNCH();
-    KCHK(hipEventRecord(ctx->ev[8], rs));
-    if (rs != ctx->stream) KCHK(hipEventRecord(ctx->ev_rows, rs));
-    ctx->rows_timed = true;
-    ctx->rows_time_pending = true;
-    return 0;
-  }
-  dim3 grid((unsigned)ctx->wi_total, ncc);
-  a.nitems = 0;
-  if (ctx->rows_persist > 0) {
-    int ncu = 256;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const i64 g = (i64)ncu * ctx->rows_persist;
-    if (g < ctx->wi_total) {
-      a.nitems = ctx->wi_total;
-      grid.x = (unsigned)g;
-    }
-  }
-  if (ext) {   // timed by the dispatch itself
-    hipEvent_t e0 = ctx->ev[7], e1 = ctx->ev[8];
-    if (nt == 1024) hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, a);
-    else if (nt == 512) hipExtLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, e0, e1, 0, a);
-    else hipExtLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, e0, e1, 0, a);
-    KLAUNCH();
-  } else {
-    if (nt == 1024) hipLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, a);
-    else if (nt == 512) hipLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, a);
-    else hipLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, a);
-    KLAUNCH();
-    KCHK(hipEventRecord(ctx->ev[8], rs));
-  }
-  if (rs != ctx->stream) KCHK(hipEventRecord(ctx->ev_rows, rs));
+  const dim3 grid((unsigned)ctx->wi_total, ncc);
+  if (nt == 1024) hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, a);
+  else if (nt == 512) hipExtLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, e0, e1, 0, a);
+  else hipExtLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, e0, e1, 0, a);
+  KLAUNCH();
+  ctx->rows_kernel = 2;
   ctx->rows_timed = true;
   ctx->rows_time_pending = true;
   return 0;
@@ -1758,14 +1295,6 @@ int ensure_built(kano_ctx* ctx) {
   return settle(ctx);
 }
 
-// order the main stream after the matrix write
-int join_rows(kano_ctx* ctx) {
-  if (!ctx->rows_pending) return 0;
-  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows, 0));
-  ctx->rows_pending = false;
-  return 0;
-}
-
 int ensure_matrix(kano_ctx* ctx) {
   KTRY(ensure_built(ctx));
   if (ctx->lists_mode) return fail(ctx, -EINVAL, "context holds policy lists, not a matrix");
@@ -1775,11 +1304,10 @@ int ensure_matrix(kano_ctx* ctx) {
                 "writes the shard's rows)");
   if (ctx->rows_deferred) {    // kano_build_classes: the matrix, now
     ctx->rows_deferred = false;
-    KTRY(alloc_matrix(ctx, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM) *
-                                 ctx->m_over, ctx->m_contig != 0));
-    KTRY(launch_rows(ctx, false));
+    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rows_local(ctx) * ctx->ldM)));
+    KTRY(launch_rows(ctx));
   }
-  return join_rows(ctx);
+  return 0;
 }
 
 // identity "classes" over the local rows (after an edit of M): row r is its
@@ -1820,7 +1348,7 @@ int recompute_cols(kano_ctx* ctx) {
   a.hflag = mem + rl;  // every row "prebuilt": copy + column fold, no writes
   a.M = P_<u64>(ctx->M);
   a.ldM = ldM;
-  a.wW = ldM / ctx->pitch_mul - ctx->pitch_pad;
+  a.wW = ldM;
   a.r0 = ctx->r0;
   a.n = ctx->n;
   a.W = W;
@@ -1879,15 +1407,13 @@ int cross_setup(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& c
   return 0;
 }
 
-// cross_setup (unless done), allocations; fills go to fb.  With the fused
-// sort (ctx->xs_on) the build has filled gmin / gmax, found the group ranges
-// and may have flagged the error slot already: those fills are skipped.
+// cross_setup (unless done), allocations; fills go to fb
 int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp,
                   FillBatch& fb, bool setup_done = false) {
   const i64 ldM = ctx->ldM;
   if (!setup_done) KTRY(cross_setup(ctx, gid, ngroups, cp));
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
-  if (!ctx->xs_on) KTRY(fb.add_raw(err, sizeof(u64), 0u));
+  KTRY(fb.add_raw(err, sizeof(u64), 0u));
   KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
   if (!cp.on) return 0;
   const int32_t G = cp.G;
@@ -1906,15 +1432,11 @@ int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan&
   KTRY(dalloc(ctx, ctx->multi, sizeof(u64) * ldC));
   KTRY(dalloc(ctx, ctx->A1, sizeof(u64) * ldC));
   KTRY(dalloc(ctx, ctx->A2, sizeof(u64) * ldC));
-  if (!ctx->xs_on) {
-    KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
-    KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
-  }
+  KTRY(fb.add(ctx->gmin, sizeof(int32_t) * U, 0x7fffffffu));
+  KTRY(fb.add(ctx->gmax, sizeof(int32_t) * U, 0xffffffffu));
   KTRY(fb.add(ctx->R, sizeof(u64) * (i64)G * ldC, 0u));
   for (DBuf* b : {&ctx->multi, &ctx->A1, &ctx->A2}) KTRY(fb.add(*b, sizeof(u64) * ldC, 0u));
   KTRY(fb.add(ctx->kcnt, sizeof(int32_t) * 2 * ((i64)G + 1), 0u));   // counts + cursors
-  KTRY(dalloc(ctx, ctx->kempty, sizeof(int32_t)));
-  KTRY(fb.add(ctx->kempty, sizeof(int32_t), 0u));
   return 0;
 }
 
@@ -1932,12 +1454,6 @@ KeySort cross_sort(kano_ctx* ctx, const CrossPlan& cp) {
   k.hist = P_<int32_t>(ctx->kcnt) + 2 * ((i64)cp.G + 1);
   k.hoff = P_<int32_t>(ctx->koff);
   k.order = P_<int32_t>(ctx->corder);
-  // classes with an empty select list skip the fold (their Mc rows are zero;
-  // the select counts exist once the build's front end ran)
-  if (ctx->fold_skip_empty && ctx->scnt.p && !ctx->rows_dirty) {
-    k.scnt = P_<int32_t>(ctx->scnt);
-    k.empty = P_<int32_t>(ctx->kempty);
-  }
   return k;
 }
 
@@ -1945,16 +1461,10 @@ int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
   if (!cp.on) return 0;
   const i64 U = ctx->rc.U, G = cp.G, rl = rows_local(ctx);
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
-  if (ctx->xs_on) {
-    // (k_cls_mfill found the group ranges)
-  } else if (ctx->grange_m)
-    hipLaunchKernelGGL(k_cls_group_range_m, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
-                       (int32_t)G, P_<int32_t>(ctx->rc.cls), P_<int32_t>(ctx->rc.mem), rl,
-                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
-  else
-    hipLaunchKernelGGL(k_cls_group_range, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
-                       (int32_t)G, P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1,
-                       P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
+  // group range of every row class along its member list
+  hipLaunchKernelGGL(k_cls_group_range_m, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
+                     (int32_t)G, P_<int32_t>(ctx->rc.cls), P_<int32_t>(ctx->rc.mem), rl,
+                     P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
   KLAUNCH();
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {   // classes in group order: per-block LDS histograms
@@ -2000,25 +1510,12 @@ int cross_stage_b2(kano_ctx* ctx, const CrossPlan& cp) {
     const int32_t* ck = P_<int32_t>(ctx->ckey);
     u64* co = cols ? P_<u64>(ctx->col_or_c) : nullptr;
     u64* cn = cols ? P_<u64>(ctx->col_nand_c) : nullptr;
-    const int fm = ctx->fold_mode;   // 0 serial 16; 1 batched 16; 2 batched 32; +10 skip
-    const int pw = (fm % 10) == 2 ? 32 : 16;
-    const KeySort ksx = cross_sort(ctx, cp);
-    const int32_t* ks_empty = cp.key_lds ? ksx.empty : nullptr;
-    const dim3 g(nblk(UAW, 64), nblk(U, (TPB / 64) * pw));
-#define KANO_FOLD(PW, B, S)                                                                 \
-  hipLaunchKernelGGL((k_mc_fold<PW, B, S>), g, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), \
-                     ldC, UAW, ctx->cc.U, ord, nlive, ck, (int32_t)G, P_<u64>(ctx->R),     \
-                     P_<u64>(ctx->multi), co, cn,                                           \
-                     ks_empty)
-    switch (fm) {
-      case 1: KANO_FOLD(16, true, false); break;
-      case 2: KANO_FOLD(32, true, false); break;
-      case 10: KANO_FOLD(16, false, true); break;
-      case 11: KANO_FOLD(16, true, true); break;
-      case 12: KANO_FOLD(32, true, true); break;
-      default: KANO_FOLD(16, false, false); break;
-    }
-#undef KANO_FOLD
+    // 32 row classes per wave, their Mc words loaded together (measured C3:
+    // 16.9 us vs 24-27 us for a serial walk of 16)
+    const dim3 g(nblk(UAW, 64), nblk(U, (TPB / 64) * FOLD_PER_WAVE));
+    hipLaunchKernelGGL(k_mc_fold, g, dim3(TPB), 0, ctx->stream, P_<u64>(ctx->Mc), ldC, UAW,
+                       ctx->cc.U, ord, nlive, ck, (int32_t)G, P_<u64>(ctx->R),
+                       P_<u64>(ctx->multi), co, cn);
   }
   KLAUNCH();
   ctx->cols_deferred = false;
@@ -2119,7 +1616,8 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
-  // tuning overrides for experiments: KANO_TUNE="ch=32,align=16"
+  // test hooks (KANO_TUNE="key=value,..."): forms that compute the same
+  // results, forced for the parity tests (see kano_ctx)
   if (const char* t = getenv("KANO_TUNE")) {
     std::string spec(t);
     size_t pos = 0;
@@ -2131,58 +1629,13 @@ int kano_create(int device, kano_ctx** out) {
       if (eq != std::string::npos) {
         const std::string k = kv.substr(0, eq);
         const int v = atoi(kv.c_str() + eq + 1);
-        if (k == "ch" && v >= 1 && v <= 1024) ctx->ch = v;
-        if (k == "cww" && v >= 16 && v <= MAX_CWW && v % 16 == 0) ctx->cww_max = v;
-        if (k == "pitch" && v >= 1 && v <= 64) ctx->pitch_mul = v;
-        if (k == "alist") ctx->rows_alist = v < 0 ? -1 : (v ? 1 : 0);
-        if (k == "nt" && (v == 0 || v == 256 || v == 512 || v == 1024)) ctx->rows_nt = v;
-        if (k == "probe" && v >= 0 && v <= 3) ctx->rows_probe = v;
-        if (k == "mover" && v >= 1 && v <= 64) ctx->m_over = v;
-        if (k == "pad" && v >= 0 && v <= 1 << 16 && v % 16 == 0) ctx->pitch_pad = v;
-        if (k == "align" && (v == 2 || v == 4 || v == 8 || v == 16 || v == 32)) ctx->ld_align = v;
-        if (k == "overlap") ctx->rows_overlap = v != 0;
-        if (k == "early") ctx->rows_early = v;
-        if (k == "prio") ctx->prio = v;
-        if (k == "sh") ctx->sh_items = v == 1 ? 1 : 8;
-        if (k == "shstage") ctx->sh_stage = v;
-        if (k == "shseg" && (v == 512 || v == 1024)) ctx->sh_seg = v;
-        if (k == "shscanside") ctx->sh_scan_side = v;
-        if (k == "grm") ctx->grange_m = v;
-        if (k == "fold") ctx->fold_mode = v;
-        if (k == "mcrows") ctx->mc_rows = v;
-        if (k == "kmin" && v >= 1) ctx->mfma_kmin = v;
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
-        if (k == "k8srows") ctx->k8s_rows_cls = v;
-        if (k == "store") ctx->rows_store = v;
-        if (k == "persist" && v >= 0 && v <= 64) ctx->rows_persist = v;
-        if (k == "order") ctx->rows_order = v;
-        if (k == "hosttime") ctx->host_timing = v;
-        if (k == "fork") ctx->fork_checks = v;
-        if (k == "spin") ctx->spin_wait = v;
+        if (k == "rows") ctx->rows_from = v;
+        if (k == "rowsnt" && (v == 256 || v == 512 || v == 1024)) ctx->rows_mc_nt = v;
+        if (k == "cww" && v >= 16 && v <= MAX_CWW && v % 16 == 0) ctx->rows_cww = v;
         if (k == "async") ctx->async_rows = v;
-        if (k == "extev") ctx->rows_extev = v;
-        if (k == "foldskip") ctx->fold_skip_empty = v;
-        if (k == "scanslots") ctx->scan_slots = v;
-        if (k == "mprobe" && v >= 0 && v <= 64) ctx->mprobe = v;
-        if (k == "mprobemin" && v >= 0) ctx->mprobe_min_mb = v;
-        if (k == "mprobemax" && v >= 0) ctx->mprobe_max_mb = v;
-        if (k == "mcown") ctx->mc_own = v;
-        if (k == "tail") ctx->side_tail = v;
-        if (k == "s3prio") ctx->s3_prio = v;
-        if (k == "sidepre") ctx->side_pre = v;
-        if (k == "graphs") ctx->graphs = v;
-        if (k == "sig") ctx->mirror_sig = v;
-        if (k == "sigspin") ctx->sig_spin_us = v;
-        if (k == "xfuse") ctx->xfuse = v;
-        if (k == "hfuse") ctx->hfuse = v;
-        if (k == "preclean") ctx->preclean = v;
-        if (k == "mcontig") ctx->m_contig = v;
-        if (k == "forklate") ctx->fork_late = v;
-        if (k == "alistside") ctx->alist_side = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
-        if (k == "s3cus" && v >= 0 && v <= 1024) ctx->s3_cus = v;
-        if (k == "shardearly") ctx->shard_rows_early = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
         if (k == "pathtm" && (v == 1 || v == 2 || v == 4)) ctx->path_tm = v;
         if (k == "pathlds") ctx->path_lds = v;
@@ -2191,54 +1644,18 @@ int kano_create(int device, kano_ctx** out) {
       pos = end + 1;
     }
   }
-  // priorities: the checks' stream high, the matrix write's low, so that the
-  // short check kernels get CUs while k_rows streams
-  int prio_lo = 0, prio_hi = 0;
-  const bool use_prio = ctx->prio && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) ==
-                                         hipSuccess && prio_lo != prio_hi;
-  if (use_prio) {
-    (void)hipStreamDestroy(ctx->stream);
-    if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
-      ctx->stream = nullptr;
-      kano_destroy(ctx);
-      return -EIO;
-    }
+  if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
+    ctx->stream3 = nullptr;
+    kano_destroy(ctx);
+    return -EIO;
   }
-  {
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-    hipError_t e3;
-    int ncu = 0;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    if (ctx->s3_cus > 0 && ctx->s3_cus < ncu) {
-      // every (ncu / s3_cus)-th CU: the tail spread thinly over the chip
-      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-      const int stride = std::max(1, ncu / ctx->s3_cus);
-      for (int c = 0, k = 0; c < ncu && k < ctx->s3_cus; c += stride, ++k)
-        mask[(size_t)c / 32] |= 1u << (c % 32);
-      e3 = hipExtStreamCreateWithCUMask(&ctx->stream3, (uint32_t)mask.size(), mask.data());
-    } else {
-      e3 = ctx->s3_prio ? hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, hi)
-                        : hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking);
-    }
-    if (e3 != hipSuccess) {
-      ctx->stream3 = nullptr;
-      kano_destroy(ctx);
-      return -EIO;
-    }
-  }
-  if ((use_prio ? hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_lo)
-                : hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking)) != hipSuccess ||
+  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_sync, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_fork3, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_join3, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess) {
     kano_destroy(ctx);
     return -EIO;
   }
@@ -2265,23 +1682,7 @@ int kano_create(int device, kano_ctx** out) {
 }
 
 void kano_destroy(kano_ctx* ctx) {
-  if (ctx) {
-    ctx->seg_on = false;
-    kano_rec::g_rec = nullptr;
-    for (auto& e : ctx->gcache) (void)hipGraphExecDestroy(e.second);
-    ctx->gcache.clear();
-  }
   if (!ctx) return;
-  if (ctx->host_timing && ctx->ht[0] > 1)
-    fprintf(stderr,
-            "kano host us/verify: gap %.1f front %.1f back %.1f (waits %.1f = %.1f + %.1f + %.1f) "
-            "over %.0f calls\n",
-            ctx->ht[1] / (ctx->ht[0] - 1), ctx->ht[2] / ctx->ht[0], ctx->ht[3] / ctx->ht[0],
-            ctx->ht[4] / ctx->ht[0], ctx->ht[5] / ctx->ht[0], ctx->ht[6] / ctx->ht[0],
-            ctx->ht[7] / ctx->ht[0], ctx->ht[0]);
-  if (ctx->host_timing)
-    fprintf(stderr, "kano host signal waits past 1 ms: %lld with the stream busy, %lld idle\n",
-            (long long)ctx->sig_long[0], (long long)ctx->sig_long[1]);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
@@ -2304,7 +1705,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->hoff,   &ctx->hlist,   &ctx->sq,      &ctx->pfoff,     &ctx->ACT,
                   &ctx->AC,     &ctx->nca,     &ctx->acnt,    &ctx->alcoff,    &ctx->alc,
                   &ctx->aloff,  &ctx->alist,   &ctx->M,       &ctx->Mc,        &ctx->color,
-                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp, &ctx->scan_tmp_side,
+                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp,
                   &ctx->shg_h,  &ctx->shg_tkey, &ctx->shg_trep, &ctx->shg_slot, &ctx->shg_isrep,
                   &ctx->shg_gidx, &ctx->shg_gid, &ctx->shg_reps, &ctx->shg_sub, &ctx->shg_err, &ctx->sig_ctr,
                   &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
@@ -2312,7 +1713,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->flags,  &ctx->T,       &ctx->loff,    &ctx->L,         &ctx->tp,
                   &ctx->poff,   &ctx->out,     &ctx->scratch_words, &ctx->ident, &ctx->ecls,
                   &ctx->tcnt,   &ctx->toff,    &ctx->sizes,   &ctx->icnt,      &ctx->ioff,
-                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd,    &ctx->mprobe_perm,
+                  &ctx->sysrow, &ctx->wicls,   &ctx->idxd,
                   &ctx->ckey,   &ctx->corder,  &ctx->kcnt,    &ctx->koff,
                   &ctx->gids,
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
@@ -2325,16 +1726,9 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
-  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-  if (ctx->ev_rows) (void)hipEventDestroy(ctx->ev_rows);
-  if (ctx->ev_tail) (void)hipEventDestroy(ctx->ev_tail);
-  if (ctx->ev_rows_fork) (void)hipEventDestroy(ctx->ev_rows_fork);
-  if (ctx->ev_sizes) (void)hipEventDestroy(ctx->ev_sizes);
-  if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
-  if (ctx->ev_fork3) (void)hipEventDestroy(ctx->ev_fork3);
-  if (ctx->ev_join3) (void)hipEventDestroy(ctx->ev_join3);
-  if (ctx->ev_fork2) (void)hipEventDestroy(ctx->ev_fork2);
-  if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rows_fork, ctx->ev_sizes,
+                       ctx->ev_fork2, ctx->ev_join2})
+    if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
 
@@ -2345,7 +1739,7 @@ int kano_set_stream(kano_ctx* ctx, void* s) {
   KCHK(hipSetDevice(ctx->device));
   KTRY(settle(ctx));
   KCHK(hipStreamSynchronize(ctx->stream2));
-  ctx->rows_pending = false;
+  KCHK(hipStreamSynchronize(ctx->stream3));
   if (ctx->own_stream && ctx->stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -2369,10 +1763,7 @@ int kano_set_pods(kano_ctx* ctx, int64_t n, int32_t ncols, const int32_t* pod_va
   KTRY(settle(ctx));
   ctx->n = n;
   ctx->W = (n + 63) / 64;
-  ctx->ldM = (std::max<i64>(ctx->ld_align,
-                            (ctx->W + ctx->ld_align - 1) / ctx->ld_align * ctx->ld_align) +
-              ctx->pitch_pad) *
-             ctx->pitch_mul;
+  ctx->ldM = std::max<i64>(LD_ALIGN, (ctx->W + LD_ALIGN - 1) / LD_ALIGN * LD_ALIGN);
   ctx->ncols = ncols;
   // bit width of every column's (value id + 1): key tuples that fit 63 bits
   // are hashed and compared as one packed word (no gathers of pod values)
@@ -2627,7 +2018,6 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
   KCHK(hipSetDevice(ctx->device));
-  KTRY(join_rows(ctx));  // the previous matrix write still reads the class lists
   ctx->built = false;
   ctx->rows_deferred = false;
   ctx->lists_mode = false;
@@ -2638,23 +2028,16 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
   const i64 rl = rows_local(ctx);
   if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
-    KTRY(alloc_matrix(ctx, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM) * ctx->m_over,
-                ctx->m_contig != 0));
+    KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM)));
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KTRY(stage_mark(ctx, 0, ctx->stream));
-  // the size-independent part of the back end (zeroed AC / Mc, the
-  // crosscheck's group-key sort) needs only the class counts: with side_pre
-  // it runs on stream2 beside the join, else here, overlapped with host sync 2
-  ctx->side_pending = false;
-  const bool side = ctx->side_pre != 0;
-  std::function<int()> pre = [&]() -> int { return do_back_pre(ctx, pre_fill, pre_run); };
-  KTRY(do_front(ctx, path, side ? pre : std::function<int()>()));
-  // host sync 2 (the list sizes)
+  KTRY(do_front(ctx, path));
+  // host sync 2 (the list sizes), overlapped with the size-independent part
+  // of the back end (zeroed AC / Mc, the crosscheck's group-key sort)
   KTRY(mirror_begin(ctx));
-  if (!side) KTRY(do_back_pre(ctx, pre_fill, pre_run));
+  KTRY(do_back_pre(ctx, pre_fill, pre_run));
   KTRY(read_sizes(ctx));
-  KTRY(side_join(ctx));
   KTRY(stage_mark(ctx, 3, ctx->stream));
   ctx->cols_deferred = defer_cols;
   KTRY(do_back(ctx, path, extra));
@@ -2702,12 +2085,7 @@ int kano_info(kano_ctx* ctx, int64_t* out) {
   out[KANO_INFO_UA] = ctx->cc.U;
   out[KANO_INFO_HEAVY_PATH] = ctx->heavy_path;
   out[KANO_INFO_WORK_ITEMS] = ctx->wi_total;
-  out[KANO_INFO_GRAPH_HITS] = ctx->g_hits;
-  out[KANO_INFO_GRAPH_CAPTURES] = ctx->g_captures;
-  out[KANO_INFO_GRAPH_DIRECT] = ctx->g_direct;
-  out[KANO_INFO_MPROBE_TRIED] = ctx->mprobe_tried;
-  out[KANO_INFO_MPROBE_BEST_NS] = (int64_t)(ctx->mprobe_best_ms * 1e6);
-  out[KANO_INFO_MPROBE_WORST_NS] = (int64_t)(ctx->mprobe_worst_ms * 1e6);
+  out[KANO_INFO_ROWS_KERNEL] = ctx->rows_kernel;
   return 0;
 }
 
@@ -2941,8 +2319,7 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (sp.rl + 1)));
   KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, sp.nt)));
   KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
-  if (ctx->sh_items == 1 || ctx->vs_count_only)   // accumulated
-    KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));
+  KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));   // accumulated
   return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
 }
 
@@ -3052,21 +2429,9 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     // may yield to the grouped count)
     const i64 nvb = sp.nt * SH_ITEMS;
     const i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
-    if ((ctx->sh_items == 1 || ctx->vs_count_only) && ctx->sh_stage)
-    {
-      if (ctx->sh_seg == 1024)
-        hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
-                           P_<i64>(ctx->tcnt));
-      else
-        hipLaunchKernelGGL(k_shadow_test1s<512>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
-                           P_<i64>(ctx->tcnt));
-    }
-    else if (ctx->sh_items == 1 || ctx->vs_count_only)
-      hipLaunchKernelGGL(k_shadow_test1, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
-                         P_<i64>(ctx->tcnt));
-    else
-      hipLaunchKernelGGL(k_shadow_test, dim3((unsigned)sp.nt), dim3(TPB), 0, st, a, sp.nf,
-                         P_<i64>(ctx->tcnt));
+    // the block's S(c) entries staged in LDS, one candidate pair per thread
+    hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
+                       P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
   return 0;
@@ -3302,26 +2667,13 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // fill launch
   CrossPlan cp;
   ShadowPlan sp;
-  // the crosscheck's group-key sort rides on the build's launches (xs_on):
-  // the groups go up first, the build's kernels do the rest
-  bool setup_done = false;
-  ctx->xs_on = ctx->xs_done = false;
-  if (want_cross && ctx->xfuse && ctx->grange_m && !ctx->side_pre) {
-    KTRY(cross_setup(ctx, gid, ngroups, cp));
-    setup_done = true;
-    if (cp.on && (i64)cp.G + 1 <= KEY_LDS_MAX) {
-      ctx->xs_on = true;
-      ctx->xs_gdev = cp.gdev;
-      ctx->xs_G = cp.G;
-    }
-  }
-  // the crosscheck's fills (and, unfused, its group-key sort) need only the
-  // class counts: they run while the list sizes travel (build sync 2)
+  // the crosscheck's fills and group-key sort need only the class counts:
+  // they run while the list sizes travel (build sync 2)
   auto pre_fill = [&](FillBatch& fb) -> int {
-    return want_cross ? cross_prepare(ctx, gid, ngroups, cp, fb, setup_done) : 0;
+    return want_cross ? cross_prepare(ctx, gid, ngroups, cp, fb) : 0;
   };
   auto pre_run = [&]() -> int {
-    if (!want_cross || !cp.on || ctx->xs_done) return 0;
+    if (!want_cross || !cp.on) return 0;
     ScanBatch sb(ctx);
     KTRY(cross_stage_a(ctx, cp, sb));
     KTRY(sb.run());
@@ -3332,84 +2684,28 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   };
   ctx->vs_open = false;
   // policy_shadow's subset tests need only the lists and AC: they run on
-  // stream2 beside the Mc chain (scatter, fold) and the flat-list build
+  // stream2 beside the Mc chain (scatter, fold).  The fork point is marked
+  // (ev_fork2) where the lists and AC are complete; the side stream's wait,
+  // the tests and the join event are issued after the build's remaining
+  // launches, so that the host's fork calls overlap those kernels instead of
+  // leaving the main stream idle
   ctx->fork_pending = false;
-  // rows_early == 2: the matrix write starts on stream2 as soon as its
-  // inputs exist (rows_hook, inside the build), beside the class-level
-  // checks; policy_shadow's tests then take stream3 (the tail's stream,
-  // which runs after them anyway)
-  const bool rows_first = ctx->rows_early == 2 && rows_local(ctx) > 0;
-  hipStream_t tst = rows_first ? ctx->stream3 : ctx->stream2;
-  // The fork point is marked (ev_fork2) where the lists and AC are complete;
-  // the side stream's wait, the tests and the join event are issued after
-  // the build's remaining launches (flat lists, Mc scatter), so that the
-  // host's ~15 us of fork calls overlap those kernels instead of leaving the
-  // main stream idle (it ran ahead of the host there)
   bool fork_marked = false;
-  bool sh_scanned = false;
-  std::function<int()> fork_issue;
-  if (want_shadow && ctx->fork_checks) {
+  if (want_shadow) {
     ctx->fork_hook = [&]() -> int {
       KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));
       fork_marked = true;
-      return ctx->fork_late ? 0 : fork_issue();
-    };
-  }
-  fork_issue = [&, tst]() -> int {
-    if (!fork_marked) return 0;
-    fork_marked = false;
-    KCHK(hipStreamWaitEvent(tst, ctx->ev_fork2, 0));
-    if (ctx->alist_pending) {   // the flat lists first: the matrix write needs them
-      ctx->alist_pending = false;
-      KTRY(build_alist(ctx, tst));
-    }
-    KTRY(shadow_test_launch(ctx, sp, tst));
-    // policy_shadow's scans follow its tests on the side stream (their own
-    // scan status buffers): one launch fewer on the main stream, which joins
-    // before k_verify_cols reads their offsets
-    sh_scanned = false;
-    if (ctx->sh_scan_side && tst == ctx->stream2) {
-      auto swap = [&]() {
-        std::swap(ctx->stream, ctx->stream2);
-        std::swap(ctx->scan_tmp, ctx->scan_tmp_side);
-        std::swap(ctx->scan_cap, ctx->scan_cap_side);
-        std::swap(ctx->scan_parity, ctx->scan_parity_side);
-      };
-      swap();
-      ScanBatch sbs(ctx);
-      int rc = shadow_stage_a_scans(ctx, sp, sbs);
-      if (rc == 0) rc = sbs.run();
-      swap();
-      KTRY(rc);
-      sh_scanned = true;
-    }
-    KCHK(hipEventRecord(ctx->ev_join2, tst));
-    ctx->fork_pending = true;
-    return 0;
-  };
-  bool early = false;
-  if (rows_first && !words_dev) {
-    ctx->rows_hook = [&]() -> int {
-      KTRY(launch_rows(ctx, true));
-      early = true;
       return 0;
     };
   }
-  ctx->alist_pending = false;
-  ctx->alist_side_ok = want_shadow && ctx->fork_checks && ctx->fork_late && ctx->alist_side &&
-                       !rows_first;
   const int brc = build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run);
-  ctx->alist_side_ok = false;
   ctx->fork_hook = nullptr;
-  ctx->rows_hook = nullptr;
-  ctx->xs_on = false;
   KTRY(brc);
-  KTRY(fork_issue());
-  // the matrix write needs only the lists: with rows_early it starts here on
-  // stream2, beside the class-level checks
-  if (!early && ctx->rows_early == 1 && ctx->rows_overlap) {
-    KTRY(launch_rows(ctx));
-    early = true;
+  if (fork_marked) {
+    KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
+    KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
+    KCHK(hipEventRecord(ctx->ev_join2, ctx->stream2));
+    ctx->fork_pending = true;
   }
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
@@ -3422,7 +2718,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     if (ctx->fork_pending) {
       KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join2, 0));
       ctx->fork_pending = false;
-      if (!sh_scanned) KTRY(shadow_stage_a_scans(ctx, sp, sb));
+      KTRY(shadow_stage_a_scans(ctx, sp, sb));
     } else {
       KTRY(shadow_stage_a(ctx, sp, sb));
     }
@@ -3484,19 +2780,13 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   } else {
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
   }
-  // a row shard's matrix write needs nothing from the ranks' exchange: it
-  // starts now on stream2, so the all-gather and the combine run beside it
-  if (words_dev && !early && ctx->shard_rows_early) {
-    KTRY(launch_rows(ctx, true));
-    early = true;
-  }
   ctx->vs_open = true;
   ctx->vs_shadow = want_shadow;
   ctx->vs_cross_want = want_cross;
   ctx->vs_cross_on = cross_on;
   ctx->vs_have_sys = have_sys;
   ctx->vs_sys_on = sys_on;
-  ctx->vs_early = early;
+  ctx->vs_rows = true;
   ctx->vs_nb = nb;
   ctx->vs_rl = sp.rl;
   return 0;
@@ -3547,26 +2837,20 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KLAUNCH();
   }
   // the list sizes, policy_shadow's sizes and the group check travel to the
-  // host while the matrix write runs: the host waits on the copy's event
-  // only, then queues policy_shadow's emission and the copies behind k_rows
+  // host while the matrix write runs: the host waits on the signal (or the
+  // event) only, then queues policy_shadow's emission and the copies beside
+  // k_rows on stream3.  The tail waits for everything queued so far: the
+  // host's own sync event when there is one, else the marker recorded before
+  // the matrix write
   constexpr int NS = SZ_ERR - SZ_NL + 1;
-  // side_tail == 2: policy_shadow's compaction and emission run on the main
-  // stream before the matrix write (they crawl beside it: 60 + 40 us there
-  // against 10 + 4 us alone, and slow it), the copies beside it
-  const bool pre_tail = ctx->side_tail == 2 && !ctx->vs_early && want_shadow && shadow_cap >= 0;
-  // the tail on stream3 waits for everything queued so far: the host's own
-  // sync event when there is one, else k_rows' start event (recorded at the
-  // same point of the main stream: one marker instead of two), else ev_sizes
   const bool signalled = ctx->sig_armed != 0;
   KTRY(mirror_begin(ctx));
   hipEvent_t tail_ev = signalled ? nullptr : ctx->ev_sizes;
-  if (!ctx->vs_early && !pre_tail) {
+  if (ctx->vs_rows) {
     KTRY(launch_rows(ctx));
-    if (!tail_ev && ctx->rows_timed && !ctx->rows_overlap) tail_ev = ctx->rows_fork;
+    if (!tail_ev && ctx->rows_kernel) tail_ev = ctx->rows_fork;
   }
-  if (!tail_ev && ctx->side_tail && !pre_tail) {
-    SegPause pause(ctx);
-    KTRY(pause.rc);
+  if (!tail_ev) {
     KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
     tail_ev = ctx->ev_sizes;
   }
@@ -3583,11 +2867,11 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   }
   if (!ctx->vs_have_sys) counts[3] = -1;
   // everything the matrix write does not touch runs beside it on stream3:
-  // the list copies, policy_shadow's compaction and emission, the pairs copy
-  // (the copies are blit kernels that crawl beside k_rows: the short
-  // shadow kernels go first so that they do not queue behind them)
-  hipStream_t cs = ctx->side_tail ? ctx->stream3 : ctx->stream;
-  if (cs != ctx->stream && !pre_tail) KCHK(hipStreamWaitEvent(cs, tail_ev, 0));
+  // policy_shadow's compaction and emission, the list and pair copies (the
+  // copies are blit kernels that crawl beside k_rows: the short shadow
+  // kernels go first so that they do not queue behind them)
+  hipStream_t cs = ctx->stream3;
+  KCHK(hipStreamWaitEvent(cs, tail_ev, 0));
   i64 total = 0;
   if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
     (void)sync(ctx);
@@ -3597,13 +2881,8 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
     if (shadow_cap >= 0) {
-      KTRY(shadow_back(ctx, v[0], total, pre_tail ? ctx->stream : cs));
+      KTRY(shadow_back(ctx, v[0], total, cs));
       ctx->shadow_total = total;
-      if (pre_tail) {     // the pairs exist: the matrix write, the copies beside it
-        KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
-        KCHK(hipStreamWaitEvent(cs, ctx->ev_sizes, 0));
-        KTRY(launch_rows(ctx));
-      }
     } else {
       // count only: every subset test ran (the flags and the per-pod counts
       // above); the pairs are neither compacted nor emitted (C4: ~1e11)
@@ -3617,30 +2896,15 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
                         cs));
   // asynchronous completion: the host waits for the result copies only; the
-  // matrix write (and the next front end's fills) end on the engine streams
-  const bool async = may_async && ctx->async_rows && cs != ctx->stream && !ctx->graphs;
+  // matrix write ends on the engine stream
+  const bool async = may_async && ctx->async_rows;
   if (async) KCHK(hipEventRecord(ctx->ev_tail, cs));
-  // the next front end's first fills, beside the matrix write (the next
-  // build checks front_dims before skipping them)
-  if (cs != ctx->stream && ctx->preclean && !ctx->graphs) {
-    FillBatch fb(ctx);
-    KTRY(front_fills(ctx, fb));
-    const FillJobs fj = fb.take();
-    hipLaunchKernelGGL(k_fill_many, dim3(fill_ride_blocks(fj)), dim3(TPB), 0, cs, fj);
-    KLAUNCH();
-    ctx->front_clean = true;
-    ctx->fc_dims = front_dims(ctx);
-    ctx->fc_ops = kano_rec::g_ops;
-  }
   // later work on the main stream (a fetch of the pairs, the next build)
   // follows the tail
-  if (cs != ctx->stream) {
-    KCHK(hipEventRecord(ctx->ev_fork, cs));
-    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
-  }
-  KTRY(join_rows(ctx));  // the matrix is part of the result
+  KCHK(hipEventRecord(ctx->ev_fork, cs));
+  KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
   if (async) {
-    KTRY(wait_event(ctx, ctx->ev_tail));
+    KCHK(hipEventSynchronize(ctx->ev_tail));
     ctx->async_pending = true;
     return 0;
   }
@@ -3659,32 +2923,43 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   ctx->ht_wait = 0;
-  SegScope seg(ctx);
+  ctx->ht_wait_cur = 0.0;
   KTRY(verify_front(ctx, path, gid, ngroups, sys_row, shadow_count != nullptr, nullptr,
                     shadow_cap < 0));
   const auto t1 = clk::now();
   const int rc =
       verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count, true);
-  if (ctx->host_timing) {
-    const auto t2 = clk::now();
-    auto us = [](clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
-    if (ctx->ht[0] > 0) ctx->ht[1] += us(t0 - ctx->ht_last);
-    ctx->ht[0] += 1;
-    ctx->ht[2] += us(t1 - t0);
-    ctx->ht[3] += us(t2 - t1);
-    ctx->ht_last = t2;
-  }
+  // host time of the call by phase (kano_host_times): a stall names its phase
+  const auto t2 = clk::now();
+  auto us = [](clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
+  double* h = ctx->ht;
+  if (h[0] > 0) h[4] += us(t0 - ctx->ht_last);
+  h[0] += 1;
+  h[1] += us(t1 - t0);
+  h[2] += us(t2 - t1);
+  h[3] += ctx->ht_wait_cur;
+  h[5] = std::max(h[5], us(t1 - t0));
+  h[6] = std::max(h[6], us(t2 - t1));
+  h[7] = std::max(h[7], ctx->ht_wait_cur);
+  h[8] = std::max(h[8], us(t2 - t0));
+  ctx->ht_last = t2;
   return rc;
+}
+
+int kano_host_times(kano_ctx* ctx, double* out, int reset) {
+  if (!ctx || !out) return -EINVAL;
+  for (int k = 0; k < 12; ++k) out[k] = ctx->ht[k];
+  if (reset)
+    for (double& v : ctx->ht) v = 0.0;
+  return 0;
 }
 
 int kano_verify_shard(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
                       int64_t sys_row, int with_shadow, uint64_t* words_dev) {
   if (!ctx) return -EINVAL;
   if (!words_dev) return fail(ctx, -EINVAL, "kano_verify_shard: words_dev is NULL");
-  SegScope seg(ctx);
-  KTRY(verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0,
-                    reinterpret_cast<u64*>(words_dev), with_shadow == 2));
-  return seg_end(ctx);     // the words must be on their way when the caller gathers
+  return verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0,
+                      reinterpret_cast<u64*>(words_dev), with_shadow == 2);
 }
 
 int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nranks,
@@ -3695,7 +2970,6 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
     return fail(ctx, -EINVAL, "kano_verify_combine: bad arguments");
   if (ctx->vs_open && ctx->vs_shadow && !shadow_count)
     return fail(ctx, -EINVAL, "kano_verify_combine: shadow_count is NULL but the shard ran policy_shadow");
-  SegScope seg(ctx);
   // (gathered_dev is written on the context's stream: the combine may
   // complete asynchronously like kano_verify)
   return verify_back(ctx, reinterpret_cast<const u64*>(gathered_dev), nranks, idx, counts,
@@ -3715,14 +2989,11 @@ int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngro
   const RcclAllGather ag = rccl_all_gather();
   if (!ag)
     return fail(ctx, -ENOSYS, "kano_verify_gather: no RCCL in the process (ncclAllGather)");
-  SegScope seg(ctx);
   const i64 nw = 3 * ctx->W;     // [OR | cross | NAND] words of a shard (same W on every rank)
   KTRY(dalloc(ctx, ctx->xw, sizeof(u64) * std::max<i64>(1, nw)));
   KTRY(dalloc(ctx, ctx->xg, sizeof(u64) * std::max<i64>(1, nw * nranks)));
   KTRY(verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0, P_<u64>(ctx->xw),
                     with_shadow == 2));
-  // the shard's launches reach the stream before the collective does
-  KTRY(seg_cut(ctx));
   if (nw > 0) {
     const int rc = ag(ctx->xw.p, ctx->xg.p, (size_t)nw, RCCL_UINT64, comm, ctx->stream);
     if (rc != 0) {
@@ -3784,7 +3055,7 @@ int kano_checks_shard(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, int64_
   ctx->vs_cross_on = cross_on;
   ctx->vs_have_sys = have_sys;
   ctx->vs_sys_on = sys_on;
-  ctx->vs_early = true;
+  ctx->vs_rows = false;
   ctx->vs_nb = nb;
   ctx->vs_rl = rows_local(ctx);
   return 0;
@@ -3804,7 +3075,6 @@ int kano_set_groups(kano_ctx* ctx, const int32_t* gid, int32_t ngroups) {
   }
   if (ngroups > 0 && ngroups < G) return fail(ctx, -EINVAL, "kano_set_groups: id >= ngroups");
   if (ngroups > 0) G = ngroups;
-  KTRY(join_rows(ctx));
   KTRY(dalloc(ctx, ctx->gids, sizeof(int32_t) * std::max<i64>(1, n)));
   if (n > 0)
     KCHK(hipMemcpyAsync(ctx->gids.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice,
@@ -3830,7 +3100,6 @@ int kano_stage_times(kano_ctx* ctx, float* ms) {
   if (!ctx || !ms) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
   KTRY(settle(ctx));
-  KTRY(join_rows(ctx));
   KTRY(sync(ctx));
   for (int k = 0; k < 8; ++k) ms[k] = 0.f;
   if (ctx->built && !ctx->lists_mode) {
@@ -3850,7 +3119,6 @@ int kano_rows_timing(kano_ctx* ctx, double* out, int reset) {
   if (!ctx || !out) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
   KTRY(settle(ctx));
-  KTRY(join_rows(ctx));
   KTRY(sync(ctx));
   KTRY(resolve_rows_time(ctx));
   out[0] = ctx->rows_ms_sum;
@@ -4508,21 +3776,9 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
                              Ue, n, W, Se, ldM);
           KLAUNCH();
         }
-        const unsigned nq = nblk(ldM / 2);
         if (in_place) {
           hipLaunchKernelGGL(k_k8s_or_into, dim3(nblk(rl * (ldM / 2))), dim3(TPB), 0, ctx->stream,
                              Xe, cci, r0, rl, ldM, E);
-        } else if (ctx->k8s_rows_cls) {
-          // by class: self -> egress row classes (base Se, gather Xe by
-          // cc_i), else in-build column classes (base Xe)
-          if (self)
-            hipLaunchKernelGGL(k_k8s_rows_cls, dim3((unsigned)Ue, nq), dim3(TPB), 0, ctx->stream,
-                               Se, Xe, cci, P_<int32_t>(eg_t->rc.moff), P_<int32_t>(eg_t->rc.mem),
-                               r0, r0 + rl, ldM, E);
-          else
-            hipLaunchKernelGGL(k_k8s_rows_cls, dim3((unsigned)Xi, nq), dim3(TPB), 0, ctx->stream,
-                               Xe, (const u64*)nullptr, cci, P_<int32_t>(in_t->cc.moff),
-                               P_<int32_t>(in_t->cc.mem), r0, r0 + rl, ldM, E);
         } else {
           hipLaunchKernelGGL(k_k8s_rows, dim3(nblk(rl * (ldM / 2))), dim3(TPB), 0, ctx->stream,
                              Xe, cci, Se, rce, self, r0, rl, ldM, E);

@@ -216,29 +216,5 @@ __global__ __launch_bounds__(TPB) void k_k8s_or_into(const u64* __restrict__ X,
   *m |= reinterpret_cast<const u64x2*>(X + (i64)cci[g0 + r] * ldM)[q];
 }
 
-// The same stream, one block per (class c, 512-word chunk): the class's
-// expanded row base[c] is loaded once and each member pod m of c in [g0, g1)
-// gets base[c] | X[xid[m]] (X nullable) -- HBM then sees the writes and one
-// read of each class row; the gathered X rows (few) stay in L2.
-__global__ __launch_bounds__(TPB) void k_k8s_rows_cls(const u64* __restrict__ base,
-                                                      const u64* __restrict__ X,
-                                                      const int32_t* __restrict__ xid,
-                                                      const int32_t* __restrict__ moff,
-                                                      const int32_t* __restrict__ mem, i64 g0,
-                                                      i64 g1, i64 ldM, u64* __restrict__ M) {
-  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-  const i64 h = ldM / 2, c = blockIdx.x;
-  const i64 q = (i64)blockIdx.y * TPB + threadIdx.x;
-  if (q >= h) return;
-  const u64x2 b = reinterpret_cast<const u64x2*>(base + c * ldM)[q];
-  const int32_t k1 = moff[c + 1];
-  for (int32_t k = moff[c]; k < k1; ++k) {
-    const i64 m = mem[k];
-    if (m < g0 || m >= g1) continue;
-    u64x2 v = b;
-    if (X) v |= reinterpret_cast<const u64x2*>(X + (i64)xid[m] * ldM)[q];
-    reinterpret_cast<u64x2*>(M + (m - g0) * ldM)[q] = v;
-  }
-}
 
 }  // namespace kano

@@ -47,8 +47,6 @@ struct ClsPair {
 // (G + 1 <= KEY_LDS_MAX): per-block histograms in LDS, no global atomics;
 // hist is bin-major, hist[k * nb + b], so its exclusive scan (hoff) is every
 // (bin, block) start.  Block b covers classes [b, b + 1) * TPB * KEY_ITEMS.
-// Standalone (k_key_hist, k_key_place_lds) or fused into k_cls_vals and
-// k_join_fill (kano_verify: two launches and a scan fewer).
 constexpr int KEY_LDS_MAX = 8192;
 constexpr int KEY_ITEMS = 8;   // classes per thread
 struct KeySort {
@@ -62,10 +60,6 @@ struct KeySort {
   int32_t* hist;
   const int32_t* hoff;
   int32_t* order;
-  // (nullable) |S(c)|: a class whose select list is empty has an all-zero Mc
-  // row, so it is left out of the fold (key -1) and only raises *empty
-  const int32_t* scnt;
-  int32_t* empty;
 };
 
 // (block-uniform: every thread of the block calls it)
@@ -80,10 +74,6 @@ __device__ __forceinline__ void key_hist_block(const KeySort& k, i64 b) {
     if (c >= k.U) break;
     int32_t key = -1;
     if (k.mcnt[c] > 0 && k.gmin[c] <= k.gmax[c]) key = k.gmin[c] == k.gmax[c] ? k.gmin[c] : k.G;
-    if (key >= 0 && k.scnt && k.scnt[c] == 0) {
-      key = -1;
-      *k.empty = 1;
-    }
     k.ckey[c] = key;
     if (key >= 0) atomicAdd(&h[key], 1);
   }
@@ -241,23 +231,7 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
   if (first && (int32_t)i < a.smin[s]) atomicMin(&a.smin[s], (int32_t)i);
 }
 
-// flag / cid are indexed by i - m0
-__global__ __launch_bounds__(TPB) void k_cls_flag(ClsPair pr) {
-  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i < a.m1) a.flag[i - a.m0] = (a.smin[a.slot_of[i]] == (int32_t)i) ? 1 : 0;
-}
 
-// class ids ordered by their smallest member (deterministic)
-__global__ __launch_bounds__(TPB) void k_cls_assign(ClsPair pr) {
-  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= a.m1) return;
-  const int32_t r = a.smin[a.slot_of[i]];
-  const int32_t c = a.cid[r - a.m0];
-  a.cls[i] = c;
-  if (r == (int32_t)i) a.rep[c] = (int32_t)i;
-}
 
 // k_cls_assign and k_cls_mcount in one pass: the class id of every pod of
 // [m0, m1), the representatives, the member counts
@@ -298,13 +272,6 @@ __global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
   if (act) a.mcur[i - a.m0] = lbase[t] + r;
 }
 
-// member counts of the pods [m0, m1) of each side
-__global__ __launch_bounds__(TPB) void k_cls_mcount(ClsPair pr) {
-  const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool act = i < a.m1;
-  (void)wave_agg_inc(a.mcnt, act ? a.cls[i] : 0, act);
-}
 
 // member lists: pod i at its rank (from k_cls_assign_count) in its class.
 // With gid (kano_verify's crosscheck), the row side also folds the group
@@ -348,12 +315,9 @@ __global__ __launch_bounds__(TPB) void k_cls_mfill(ClsPair pr, const int32_t* __
 }
 
 // key values of each class's representative, slot-major: cval[k * U + c]
-// (ks.nb > 0: the row side's first ks.nb blocks also run the group-key
-// histogram, k_key_hist's work)
 // (blocks x >= nbv carry the fills fj: row y = 0 only)
 __global__ __launch_bounds__(TPB) void k_cls_vals(const int32_t* __restrict__ pv, i64 n,
-                                                  ClsPair pr, KeySort ks, FillJobs fj,
-                                                  unsigned nbv) {
+                                                  ClsPair pr, FillJobs fj, unsigned nbv) {
   if (blockIdx.x >= nbv) {                         // block-uniform
     if (blockIdx.y == 0) fill_item(fj, blockIdx.x - nbv, gridDim.x - nbv);
     return;
@@ -364,7 +328,6 @@ __global__ __launch_bounds__(TPB) void k_cls_vals(const int32_t* __restrict__ pv
     const int32_t r = a.rep[c];
     for (int k = 0; k < a.KS; ++k) a.cval[(i64)k * a.U + c] = pv[(i64)a.keys[k] * n + r];
   }
-  if (blockIdx.y == 0 && (i64)blockIdx.x < ks.nb) key_hist_block(ks, blockIdx.x);
 }
 
 // ===========================================================================
@@ -602,23 +565,10 @@ __global__ __launch_bounds__(TPB) void k_join_insert(JoinPair pr) {
   if (act) a.gcur[(i64)m * a.U + c] = r;   // place in the group (k_join_fill scatters)
 }
 
-__global__ __launch_bounds__(TPB) void k_join_count(JoinPair pr) {
-  int m;
-  const JoinSide a = join_row(pr, blockIdx.y, 0, &m) ? pr.s[1] : pr.s[0];
-  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool act = c < a.U;
-  (void)wave_agg_inc(a.gcnt, act ? (i64)m * a.T + a.pslot[(i64)m * a.U + c] : 0, act);
-}
 
 // grouped class lists; the extra row per side writes the iota block (the
 // class list of policies without terms)
-// (ks.nb > 0: the grid's last row places the row classes by group key,
-// k_key_place_lds's work, its first ks.nb blocks)
-__global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr, KeySort ks) {
-  if (ks.nb > 0 && blockIdx.y == gridDim.y - 1) {   // block-uniform
-    if ((i64)blockIdx.x < ks.nb) key_place_block(ks, blockIdx.x);
-    return;
-  }
+__global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr) {
   int m;
   const JoinSide a = join_row(pr, blockIdx.y, 1, &m) ? pr.s[1] : pr.s[0];
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
@@ -716,24 +666,6 @@ __global__ __launch_bounds__(TPB) void k_offsets_to_start(const i64* __restrict_
   if (p < P) pstart[p] = off[p];
 }
 
-// ---- select side: S(c) = ascending policies whose list holds c --------------
-// block per policy: |S(c)| and the rebuild cost sum_{p in S(c)} |allow_p|
-__global__ __launch_bounds__(TPB) void k_sel_count(i64 P, const i64* __restrict__ pstart,
-                                                   const int32_t* __restrict__ plen,
-                                                   const int32_t* __restrict__ pcls,
-                                                   const int32_t* __restrict__ acnt,
-                                                   int32_t* scnt, unsigned long long* cost) {
-  const i64 p = wave_policy();
-  if (p >= P) return;
-  const int32_t* L = pcls + pstart[p];
-  const int32_t len = plen[p];
-  const unsigned long long a = (unsigned long long)acnt[p];
-  for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
-    const int32_t c = L[k];
-    atomicAdd(&scnt[c], 1);
-    if (a) atomicAdd(&cost[c], a);
-  }
-}
 
 // S(c) placement (model.py:161 appends p to select_policies): the block's
 // entries are counted per class in LDS, one atomic per distinct class per
@@ -813,19 +745,6 @@ __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict_
 // rank sort in registers; larger lists are left to k_sort_lists_big (block
 // bitmap over all policies).
 constexpr int SORT_WAVE_MAX = 64;
-__global__ __launch_bounds__(TPB) void k_sort_lists(const i64* __restrict__ soffc, i64 U,
-                                                    int32_t* __restrict__ slist) {
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + wid;
-  if (c >= U) return;
-  const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
-  if (s <= 1 || s > SORT_WAVE_MAX) return;
-  int32_t* L = slist + s0;
-  const int32_t v = lane < s ? L[lane] : 0x7fffffff;
-  int r = 0;
-  for (int k = 0; k < s; ++k) r += __shfl(v, k, 64) < v;
-  if (lane < s) L[r] = v;
-}
 
 // One wave per class, three jobs in one launch: the class's entry in the
 // heavy list, its k_rows work items' owner map (k_flag_list), and S(c)
@@ -897,36 +816,6 @@ __global__ __launch_bounds__(TPB) void k_class_lists(ClassListsArgs a) {
   class_lists_item(a, blockIdx.x);
 }
 
-// block per class with s > SORT_WAVE_MAX: bitmap of all P policies in LDS
-__global__ __launch_bounds__(TPB) void k_sort_lists_big(const i64* __restrict__ soffc, i64 P,
-                                                        int32_t* __restrict__ slist) {
-  extern __shared__ __attribute__((aligned(16))) u64 lds[];
-  __shared__ int sm[4];
-  const i64 c = blockIdx.x;
-  const i64 s0 = soffc[c], s = soffc[c + 1] - s0;
-  if (s <= SORT_WAVE_MAX) return;
-  int32_t* L = slist + s0;
-  const i64 PW = (P + 63) / 64;
-  for (i64 w = threadIdx.x; w < PW; w += TPB) lds[w] = 0ull;
-  __syncthreads();
-  for (i64 k = threadIdx.x; k < s; k += TPB) {
-    const int32_t v = L[k];
-    atomicOr(&lds[v >> 6], 1ull << (v & 63));
-  }
-  __syncthreads();
-  i64 base = 0;
-  for (i64 w0 = 0; w0 < PW; w0 += TPB) {
-    const i64 w = w0 + threadIdx.x;
-    u64 v = w < PW ? lds[w] : 0ull;
-    int tot;
-    i64 pos = base + block_excl_scan((int)__popcll(v), sm, tot);
-    while (v) {
-      L[pos++] = (int32_t)(w * 64 + __builtin_ctzll(v));
-      v &= v - 1;
-    }
-    base += tot;
-  }
-}
 
 // ---- allow side: per policy the allowed column classes and pods -----------
 // k_pol_allow_count and k_sel_count in one pass: policy p's allowed classes
@@ -1021,24 +910,6 @@ __global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict
   }
 }
 
-__global__ __launch_bounds__(TPB) void k_pol_allow_count(i64 P, const i64* __restrict__ pstart,
-                                                         const int32_t* __restrict__ plen,
-                                                         const int32_t* __restrict__ pcls,
-                                                         const int32_t* __restrict__ csize,
-                                                         int32_t* __restrict__ nca,
-                                                         int32_t* __restrict__ acnt) {
-  const i64 p = wave_policy();
-  if (p >= P) return;
-  const int32_t* L = pcls + pstart[p];
-  const int32_t len = plen[p];
-  i64 pods = 0;
-  for (int32_t k = threadIdx.x & 63; k < len; k += 64) pods += csize[L[k]];
-  pods = wave_sum(pods);
-  if ((threadIdx.x & 63) == 0) {
-    nca[p] = len;
-    acnt[p] = (int32_t)pods;
-  }
-}
 
 // block per policy: allowed class list (alc) and its bits AC[p]
 struct PolAllowArgs {
@@ -1184,44 +1055,6 @@ __global__ __launch_bounds__(TPB) void k_pods_own(PolPodsArgs a, McOwnArgs b, un
   else mc_own_item(b, blockIdx.x - nb1, mrow);
 }
 
-// The same rows written whole: one wave per row class builds its row in LDS
-// (the allowed-class lists of S(c), LDS atomic OR) and stores every word, so
-// Mc needs no zero fill and the global atomics go.  Heavy rows: skipped
-// (k_heavy_mc_or writes them whole) or, for the MFMA path that ORs into them,
-// written as zero.  LDS: NW rows of ldMc words per block.
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_mc_rows(i64 U, const i64* __restrict__ soffc,
-                                                     const int32_t* __restrict__ slist,
-                                                     const i64* __restrict__ alcoff,
-                                                     const int32_t* __restrict__ alc,
-                                                     const int32_t* __restrict__ hflag,
-                                                     int heavy_zero, u64* __restrict__ Mc,
-                                                     i64 ldMc) {
-  extern __shared__ u64 mrow[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const i64 c = (i64)blockIdx.x * NW + wv;
-  if (c >= U) return;                                 // wave-uniform; no block barrier below
-  u64* row = mrow + (i64)wv * ldMc;
-  const bool heavy = hflag && hflag[c];
-  if (heavy && !heavy_zero) return;
-  for (i64 w = lane; w < ldMc; w += 64) row[w] = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  if (!heavy) {
-    const i64 e1 = soffc[c + 1];
-    for (i64 e = soffc[c]; e < e1; ++e) {
-      const int32_t p = slist[e];
-      for (i64 k = alcoff[p] + lane; k < alcoff[p + 1]; k += 64) {
-        const int32_t ca = alc[k];
-        atomicOr(&row[ca >> 6], 1ull << (ca & 63));
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  u64* dst = Mc + c * ldMc;
-  for (i64 w = lane; w < ldMc; w += 64) dst[w] = row[w];
-}
 
 // column OR and NAND over the classes with local members, at class level
 // block: 64 words x (4 waves x 32 classes)
@@ -1274,40 +1107,7 @@ __global__ __launch_bounds__(TPB) void k_cols_expand(const u64* __restrict__ col
   }
 }
 
-// row `row` of M straight from Mc: bit j = Mc[cls(row)] bit cla[j]
-// (system_isolation without waiting for the matrix write)
-__global__ __launch_bounds__(TPB) void k_row_from_mc(const u64* __restrict__ Mc, i64 ldMc,
-                                                     const int32_t* __restrict__ clr, i64 row,
-                                                     const int32_t* __restrict__ cla, i64 n,
-                                                     i64 W, u64* __restrict__ out) {
-  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (((j >> 6) << 6) >= W * 64) return;
-  const u64* mr = Mc + (i64)clr[row] * ldMc;
-  bool b = false;
-  if (j < n) {
-    const int32_t ca = cla[j];
-    b = (mr[ca >> 6] >> (ca & 63)) & 1ull;
-  }
-  const u64 bal = __ballot(b);
-  if ((threadIdx.x & 63) == 0) out[j >> 6] = bal;
-}
 
-// user_crosscheck at class level (kano_py/kano/algorithm.py:27-42).  Group
-// range of the local members of every row class:
-__global__ __launch_bounds__(TPB) void k_cls_group_range(const int32_t* __restrict__ gid,
-                                                         int32_t G,
-                                                         const int32_t* __restrict__ cls, i64 r0,
-                                                         i64 r1, int32_t* gmin, int32_t* gmax,
-                                                         int32_t* err) {
-  const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  bool act = i < r1;
-  const int32_t c = act ? cls[i] : 0, g = act ? gid[i] : 0;
-  if (act && (g < 0 || g >= G)) {   // caller-declared group count violated
-    atomicOr(err, 1);
-    act = false;
-  }
-  wave_agg_minmax(gmin, gmax, c, g, act);
-}
 
 // The same ranges read along the class-grouped member list (mem, moff over
 // the shard's pods): a wave's lanes hold mostly one class, so one atomic pair
@@ -1362,19 +1162,16 @@ __global__ __launch_bounds__(TPB) void k_key_place_lds(KeySort k) {
 // with col_or / col_nand non-null also the column OR / NAND of
 // all_reachable / all_isolated.  Block = 64 words x (4 waves x 16 sorted
 // classes); runs of equal key are OR-ed in registers, one atomic per run.
-constexpr int FOLD_PER_WAVE = 16;
-// PW classes per wave; BATCH: the wave's class ids and keys in one round trip
-// (lane q holds entry k0+q) and all its Mc words in flight together, else a
-// serial walk with wave-uniform index loads; SKIP: column atomics skipped
-// when saturated (or_if_new)
-template <int PW, bool BATCH, bool SKIP>
+constexpr int FOLD_PER_WAVE = 32;
+// FOLD_PER_WAVE classes per wave, their class ids and keys in one round trip
+// (lane q holds entry k0+q) and all their Mc words in flight together
 __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
                                                  i64 Ua, const int32_t* __restrict__ order,
                                                  const int32_t* __restrict__ nlive_p,
                                                  const int32_t* __restrict__ ckey,
                                                  int32_t G, u64* R, u64* multi, u64* col_or,
-                                                 u64* col_nand,
-                                                 const int32_t* __restrict__ empty_live) {
+                                                 u64* col_nand) {
+  constexpr int PW = FOLD_PER_WAVE;
   __shared__ u64 red[2][TPB / 64][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const i64 w = (i64)blockIdx.x * 64 + lane;
@@ -1385,89 +1182,46 @@ __global__ __launch_bounds__(TPB) void k_mc_fold(const u64* __restrict__ Mc, i64
   const u64 vm = wok ? valid_mask(w, Ua) : 0ull;
   u64 o = 0, na = 0, acc = 0;
   int32_t cur = -1;
-  if (BATCH) {
-    int32_t myc = 0, myk = 0;
-    if (lane < PW && k0 + lane < k1) {
-      myc = order[k0 + lane];
-      myk = ckey[myc];
-    }
-    const int cnt = (int)max((i64)0, k1 - k0);
-    u64 v[PW];
+  int32_t myc = 0, myk = 0;
+  if (lane < PW && k0 + lane < k1) {
+    myc = order[k0 + lane];
+    myk = ckey[myc];
+  }
+  const int cnt = (int)max((i64)0, k1 - k0);
+  u64 v[PW];
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-      const int32_t c = __shfl(myc, q, 64);
-      v[q] = (wok && q < cnt) ? Mc[(i64)c * ldMc + w] : 0ull;
-    }
+  for (int q = 0; q < PW; ++q) {
+    const int32_t c = __shfl(myc, q, 64);
+    v[q] = (wok && q < cnt) ? Mc[(i64)c * ldMc + w] : 0ull;
+  }
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-      const int32_t key = __shfl(myk, q, 64);
-      if (q < cnt) {
-        o |= v[q];
-        na |= ~v[q] & vm;
-        if (key != cur) {
-          if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
-          cur = key;
-          acc = 0;
-        }
-        acc |= v[q];
-      }
-    }
-  } else {
-    for (i64 k = k0; k < k1; ++k) {
-      const int32_t c = order[k];
-      const int32_t key = ckey[c];
-      const u64 v = wok ? Mc[(i64)c * ldMc + w] : 0ull;
-      o |= v;
-      na |= ~v & vm;
+  for (int q = 0; q < PW; ++q) {
+    const int32_t key = __shfl(myk, q, 64);
+    if (q < cnt) {
+      o |= v[q];
+      na |= ~v[q] & vm;
       if (key != cur) {
         if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
         cur = key;
         acc = 0;
       }
-      acc |= v;
+      acc |= v[q];
     }
   }
   if (acc) atomicOr(cur == G ? &multi[w] : &R[(i64)cur * ldMc + w], acc);
   if (col_or) {
-    // a live class with an empty select list (left out of the order) has an
-    // all-zero row: every column misses it
-    if (empty_live && *empty_live) na = vm;
     red[0][wid][lane] = o;
     red[1][wid][lane] = na;
     __syncthreads();
     if (wid == 0 && wok) {
       o = red[0][0][lane] | red[0][1][lane] | red[0][2][lane] | red[0][3][lane];
       na = red[1][0][lane] | red[1][1][lane] | red[1][2][lane] | red[1][3][lane];
-      if (SKIP) {
-        if (o) or_if_new(&col_or[w], o);
-        if (na) or_if_new(&col_nand[w], na);
-      } else {
-        if (o) atomicOr(&col_or[w], o);
-        if (na) atomicOr(&col_nand[w], na);
-      }
+      if (o) atomicOr(&col_or[w], o);
+      if (na) atomicOr(&col_nand[w], na);
     }
   }
 }
 
-// R[g] |= Mc[c] for single-group classes, MULTI |= Mc[c] otherwise (wave per
-// class).
-__global__ __launch_bounds__(TPB) void k_cross_mc(const u64* __restrict__ Mc, i64 ldMc, i64 UW,
-                                                  i64 U, const int32_t* __restrict__ mcnt,
-                                                  const int32_t* __restrict__ gmin,
-                                                  const int32_t* __restrict__ gmax, u64* R,
-                                                  u64* multi) {
-  const i64 c = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= U || mcnt[c] == 0) return;
-  const int32_t g = gmin[c];
-  if (g > gmax[c]) return;   // no valid member (error flagged)
-  u64* dst = (g == gmax[c]) ? R + (i64)g * ldMc : multi;
-  const u64* src = Mc + c * ldMc;
-  for (i64 w = lane; w < UW; w += 64) {
-    const u64 v = src[w];
-    if (v) atomicOr(&dst[w], v);
-  }
-}
 
 // cross[j] = MULTI(ca) | A2(ca) | (A1(ca) & ~R[g(j)](ca)),  ca = cla[j]
 __global__ __launch_bounds__(TPB) void k_cross_pod(const int32_t* __restrict__ gid, int32_t G,
@@ -1562,18 +1316,6 @@ __global__ __launch_bounds__(TPB) void k_sq_from_off(const i64* __restrict__ off
   if (c < U) sq[c] = (off[c + 1] - off[c]) * (off[c + 1] - off[c]);
 }
 
-// heavy list, and the owner class of every k_rows work item (so k_rows does
-// not binary-search wioff)
-__global__ __launch_bounds__(TPB) void k_flag_list(const int32_t* __restrict__ flag,
-                                                   const int32_t* __restrict__ off, i64 U,
-                                                   int32_t* __restrict__ list,
-                                                   const int32_t* __restrict__ wioff,
-                                                   int32_t* __restrict__ wicls) {
-  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (c >= U) return;
-  if (flag[c]) list[off[c]] = (int32_t)c;
-  for (int32_t w = wioff[c]; w < wioff[c + 1]; ++w) wicls[w] = (int32_t)c;
-}
 
 // ===========================================================================
 // Heavy rows: the row of the class over COLUMN classes, Mc[h] = OR_{p in S}
@@ -1748,10 +1490,6 @@ struct RowsArgs {
   i64 n, W;
   int ch;
   int cww;
-  int probe;             // experiments: 1 skip the row build, 2 skip the stores
-  int store_mode;        // experiments: 0 row-major stores, 1 word-major, 2 nontemporal, 3 sc1
-  i64 nitems;            // 0: one work item per block; else the grid strides over nitems
-  const int32_t* rcls;   // k_rows_ord: row class of every pod (global index)
   u64* color;
   u64* colnand;
 };
@@ -1761,12 +1499,6 @@ constexpr int ROWS_UNROLL = 4;
 // that the static LDS does not cost the wide (NT = 1024, 64 KB row) blocks
 // their second slot per CU
 constexpr int ROWS_SEG = 256;
-// 16-byte store that drops the line from the XCD's L2 (sc1: write-through
-// to memory, MI355X_MICROARCH.md "stores of each flavour"); a vector store
-__device__ __forceinline__ void store16_sc1(u64* dst, u64x2 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(v) : "memory");
-}
-
 // the row of light class c over columns [64*base, 64*(base + nw)) built in
 // LDS from the allowed-pod lists of S(c) (zeroed first; ends in a barrier)
 template <int NT>
@@ -1869,10 +1601,7 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   const int32_t m1 = min(m_end, m0 + a.ch);
   const bool heavy = a.hflag && a.hflag[c];
 
-  if (a.probe == 1) {
-    for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
-    __syncthreads();
-  } else if (heavy) {
+  if (heavy) {
     const u64* src = a.M + (i64)(a.mem[m_begin] - a.r0) * ldw + base;
     for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
       *(u64x2*)&row[w] = *(const u64x2*)&src[w];
@@ -1880,35 +1609,14 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   } else {
     build_light_row<NT>(a, c, base, nw, row);
   }
-  if (a.store_mode == 1 && a.probe != 2) {
-    // word-major: each thread's words go to every member row before the
-    // next words (all member rows' streams open at once)
-    const int32_t mfirst = heavy && m0 == m_begin ? m0 + 1 : m0;
-    for (int w = threadIdx.x * 2; w < nw; w += NT * 2) {
-      const u64x2 v = *(const u64x2*)&row[w];
-      for (int32_t m = mfirst; m < m1; ++m)
-        *(u64x2*)&a.M[(i64)(a.mem[m] - a.r0) * ldw + base + w] = v;
-    }
-  } else {
-    for (int32_t m = m0; m < m1 && a.probe != 2; ++m) {
-      if (heavy && m == m_begin) continue;
-      // (probe 3, experiment: rows placed in member-list order, i.e. the
-      // grid's blocks write consecutive rows -- results are wrong)
-      const i64 drow = a.probe == 3 ? (i64)m : (i64)(a.mem[m] - a.r0);
-      u64* dst = a.M + drow * ldw + base;
-      if (a.store_mode == 2) {
-        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-          __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
-      } else if (a.store_mode == 3) {
-        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-          store16_sc1(&dst[w], *(const u64x2*)&row[w]);
-      } else {
-        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-          *(u64x2*)&dst[w] = *(const u64x2*)&row[w];
-      }
-    }
+  // non-temporal 16-byte stores (measured C3: 253 vs 263-270 us for plain
+  // stores on one box, 232 vs 246-258 on another)
+  for (int32_t m = m0; m < m1; ++m) {
+    if (heavy && m == m_begin) continue;
+    u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
+    for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+      __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
   }
-  if (a.probe == 2 && threadIdx.x == 0 && row[0] == 0x5eed5eed5eed5eedull) a.M[0] = 1;
   if (chunk == 0 && a.color) {
     for (int w = threadIdx.x; w < nw; w += NT) {
       const i64 gw = base + w;
@@ -1925,67 +1633,10 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
-  if (a.nitems == 0) {            // one work item per block
-    rows_item<NT>(a, blockIdx.x, row);
-    return;
-  }
-  // persistent form: the grid strides over the work items; the LDS row is
-  // reused, so every item ends in a barrier (every thread reaches it: the
-  // loop bound is uniform)
-  for (i64 b = blockIdx.x; b < a.nitems; b += gridDim.x) {
-    rows_item<NT>(a, b, row);
-    __syncthreads();
-  }
+  rows_item<NT>(a, blockIdx.x, row);
 }
 
-// The matrix write in pod order (light classes only): block b writes one
-// row, column chunk blockIdx.y, after building its class's row in LDS.
-// Rows in order measured 5.2-5.6 TB/s against 4.7-5.0 for k_rows' class
-// order (profiles/r02_store_xcd_local.txt); xcd != 0 deals the rows so that
-// the blocks of one XCD (b mod 8 under the round-robin dispatch, speed only)
-// sweep one eighth of M in order (5.4-5.6 TB/s).  The class row is rebuilt
-// for each row (its allowed-pod lists, L2 / MALL resident).  16-byte lanes,
-// consecutive across the wave: 32 bytes per lane as two stores collapses to
-// ~2 TB/s with non-temporal stores.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_rows_ord(RowsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) u64 row[];
-  const i64 rl = a.nitems;                 // rows of the shard
-  i64 li = blockIdx.x;
-  if (a.probe == 4) {                      // XCD-local sweeps
-    const i64 R = (rl + 7) / 8;
-    li = (i64)(blockIdx.x & 7) * R + (blockIdx.x >> 3);
-  }
-  if (li >= rl) return;                    // block-uniform
-  const i64 c = a.rcls[a.r0 + li];
-  const i64 base = (i64)blockIdx.y * a.cww;
-  const int nw = (int)min((i64)a.cww, a.wW - base);
-  if (nw <= 0) return;
-  if (c >= 0 && c < a.U) {
-    build_light_row<NT>(a, c, base, nw, row);
-  } else {
-    for (int w = threadIdx.x; w < nw; w += NT) row[w] = 0ull;
-    __syncthreads();
-  }
-  u64* dst = a.M + li * a.ldM + base;
-  for (int w = threadIdx.x * 2; w < nw; w += NT * 2) {
-    const u64x2 v = *(const u64x2*)&row[w];
-    if (a.store_mode == 2) __builtin_nontemporal_store(v, (u64x2*)&dst[w]);
-    else *(u64x2*)&dst[w] = v;
-  }
-}
 
-// Placement probe of a matrix allocation (alloc_matrix): block b writes row
-// perm[b] (a random permutation: every row once, scattered like k_rows'
-// class order), 16-byte non-temporal lanes.
-__global__ __launch_bounds__(TPB) void k_place_probe(u64* __restrict__ M, i64 ldM,
-                                                     const int32_t* __restrict__ perm, i64 wW) {
-  const i64 r = perm[blockIdx.x];
-  u64* dst = M + r * ldM;
-  const u64x2 z = {0ull, 0ull};
-  for (i64 w = (i64)threadIdx.x * 2; w + 1 < wW; w += TPB * 2)
-    __builtin_nontemporal_store(z, (u64x2*)&dst[w]);
-}
 
 // ===========================================================================
 // Row digests (full-size property checks: a 1M-pod matrix is 125 GB, too big
@@ -2259,118 +1910,7 @@ __device__ __forceinline__ void tile_class_range(const i64* __restrict__ pfoff, 
   __syncthreads();
 }
 
-// flags[t] = pair t is a shadow (x != y, j != k, allow_k subset of allow_j);
-// T[c] += flagged pairs of c (T zeroed); tile_cnt[b] = flagged pairs of tile b
-__global__ __launch_bounds__(TPB) void k_shadow_test(ShadowArgs a, i64 nflags,
-                                                    i64* __restrict__ tile_cnt) {
-  __shared__ i64 sm[4];
-  __shared__ i64 rng[2];
-  tile_class_range(a.pfoff, a.U, nflags, rng);
-  const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
-  i64 c = -1;
-  int run = 0, mine = 0;
-  if (base < nflags) {
-    c = class_of_pair(a.pfoff, rng[0], rng[1], base);
-    i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, p0 = a.pfoff[c], p1 = a.pfoff[c + 1];
-    bool live = a.mcnt[c] > 0;
-    u64 packed = 0;
-#pragma unroll
-    for (int k = 0; k < SH_ITEMS; ++k) {
-      const i64 t = base + k;
-      if (t >= nflags) break;
-      while (t >= p1) {
-        if (run) atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), (unsigned long long)run);
-        run = 0;
-        ++c;
-        s0 = a.soffc[c];
-        s = a.soffc[c + 1] - s0;
-        p0 = p1;
-        p1 = a.pfoff[c + 1];
-        live = a.mcnt[c] > 0;
-      }
-      const i64 q = t - p0, x = q / s, y = q - x * s;
-      int f = 0;
-      if (live && x != y) {
-        const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
-        f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
-      }
-      packed |= (u64)f << (8 * k);
-      run += f;
-      mine += f;
-    }
-    if (base + SH_ITEMS <= nflags) {
-      *reinterpret_cast<u64*>(a.flags + base) = packed;
-    } else {
-      for (int k = 0; base + k < nflags; ++k) a.flags[base + k] = (uint8_t)(packed >> (8 * k));
-    }
-  }
-  // the last run: one atomic per wave when the whole wave ended in one class
-  const i64 c0 = __shfl(c, 0, 64);
-  const bool same = __all(c == c0 || c < 0);
-  if (same) {
-    const int r = wave_sum(run);
-    if ((threadIdx.x & 63) == 0 && r && c0 >= 0)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c0]), (unsigned long long)r);
-  } else if (run) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), (unsigned long long)run);
-  }
-  const i64 tot = block_sum((i64)mine, sm);
-  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
-}
 
-// The same test with one candidate pair per thread: the tile of SH_TILE
-// pairs is spread over SH_ITEMS blocks, so the chip holds enough waves to hide
-// the subset tests' dependent loads (the 8-pairs-per-thread form above leaves
-// about two waves per SIMD on C3).  tile_cnt accumulates (zeroed first).
-__global__ __launch_bounds__(TPB) void k_shadow_test1(ShadowArgs a, i64 nflags,
-                                                     i64* __restrict__ tile_cnt) {
-  __shared__ i64 sm[4];
-  __shared__ i64 rng[2];
-  // count only: nothing to do when the grouped count holds (block-uniform);
-  // that launch strides over the virtual blocks with a capped grid, so that
-  // the yielding test costs little
-  if (a.shg_G && shg_grouped(a.shg_G, a.shg_err, a.shg_nf, a.shg_force)) return;
-  const i64 nvb = (nflags + SH_TILE - 1) / SH_TILE * SH_ITEMS;
-  for (i64 vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-    const i64 tile = vb / SH_ITEMS, part = vb % SH_ITEMS;
-    const i64 b0 = tile * SH_TILE + part * TPB;
-    if (b0 >= nflags) break;                     // block-uniform (b0 rises with vb)
-    const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
-    if ((threadIdx.x >> 6) < 2) {
-      const int wv = threadIdx.x >> 6;
-      const i64 cr = wave_class_of(a.pfoff, 0, a.U - 1, wv == 0 ? b0 : b1);
-      if ((threadIdx.x & 63) == 0) rng[wv] = cr;
-    }
-    __syncthreads();
-    const i64 t = b0 + threadIdx.x;
-    int f = 0;
-    i64 c = -1;
-    if (t < nflags) {
-      c = class_of_pair(a.pfoff, rng[0], rng[1], t);
-      const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
-      const i64 x = q / s, y = q - x * s;
-      if (a.mcnt[c] > 0 && x != y) {
-        const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
-        f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
-      }
-      if (a.flags) a.flags[t] = (uint8_t)f;   // null: count only (T[c])
-    }
-    // T[c] += f: one atomic per wave when the wave lies in one class
-    const i64 c0 = __shfl(c, 0, 64);
-    if (__all(c == c0 || c < 0)) {
-      const int r = wave_sum(f);
-      if ((threadIdx.x & 63) == 0 && r && c0 >= 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c0]), (unsigned long long)r);
-    } else if (f) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
-    }
-    const i64 tot = block_sum((i64)f, sm);
-    if (threadIdx.x == 0 && tot)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
-    if ((i64)gridDim.x >= nvb) break;           // one virtual block per block (uniform)
-    __syncthreads();                             // rng / sm reused by the next virtual block
-  }
-}
 
 // The same test with the block's select-list data staged in LDS first: the
 // classes of the block's 256 pairs (pfoff, soffc, mcnt), then their S(c)

@@ -97,6 +97,7 @@ class DeviceBuild:
     # -- inputs / build -------------------------------------------------
     def upload(self, t: Tables) -> None:
         self.tables = t
+        self.row_span = None          # kano_set_pods resets the engine to every row
         pv = np.ascontiguousarray(t.pod_val, dtype=np.int32)
         self._chk(self.lib.kano_set_pods(self.ctx, t.n, t.ncols, _ptr(pv)), "kano_set_pods")
         if getattr(t, "expr_col", None) is not None and len(t.expr_col):
@@ -113,7 +114,7 @@ class DeviceBuild:
 
     def set_rows(self, r0: int, r1: int) -> None:
         self._chk(self.lib.kano_set_shard(self.ctx, int(r0), int(r1)), "kano_set_shard")
-        n = self.tables.n if self.tables is not None else None
+        n = self.info()["N"]          # the engine's own pod count (tables may be absent)
         self.row_span = None if (int(r0), int(r1)) == (0, n) else (int(r0), int(r1))
 
     @property
@@ -538,6 +539,16 @@ class DeviceBuild:
                   "kano_rows_timing")
         return dict(sum_ms=float(out[0]), launches=int(out[1]), min_ms=float(out[2]),
                     max_ms=float(out[3]))
+
+    def host_times(self, reset: bool = False) -> dict:
+        """kano_verify's host time by phase (us): sums and maxima since the
+        last reset (kano_host_times)."""
+        out = np.zeros(12, dtype=np.float64)
+        self._chk(self.lib.kano_host_times(self.ctx, _ptr(out), int(bool(reset))),
+                  "kano_host_times")
+        k = ("calls", "front_sum", "back_sum", "wait_sum", "gap_sum", "front_max", "back_max",
+             "wait_max", "call_max", "wait1_max", "wait2_max", "wait3_max")
+        return {name: float(v) for name, v in zip(k, out)}
 
     def stage_times(self) -> dict:
         ms = np.zeros(8, dtype=np.float32)

@@ -73,14 +73,14 @@ SIGNATURES = {
     "kano_import_rows": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_rows_timing": (c_int, [c_void_p, c_void_p, c_int]),
+    "kano_host_times": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),
 }
 
-INFO_SLOTS = 19
+INFO_SLOTS = 14
 INFO = dict(N=0, W=1, P=2, U=3, NNZ_SEL=4, NNZ_ALW=5, HEAVY=6, ROW0=7, ROW1=8, MAXSEL=9,
-            UA=10, HEAVY_PATH=11, WORK_ITEMS=12, GRAPH_HITS=13, GRAPH_CAPTURES=14, GRAPH_DIRECT=15,
-            MPROBE_TRIED=16, MPROBE_BEST_NS=17, MPROBE_WORST_NS=18)
+            UA=10, HEAVY_PATH=11, WORK_ITEMS=12, ROWS_KERNEL=13)
 PATHS = {"auto": 0, "bitwise": 1, "mfma": 2}
 STORED_GROUPS = -1   # KANO_STORED_GROUPS
 

@@ -268,20 +268,17 @@ def _lists(cs, which):
                          for c in cs])
 
 
-# --- k_rows variants that only fire on wide matrices ------------------------
+# --- matrix-write forms ------------------------------------------------------
 @pytest.mark.parametrize("tune", [
-    "nt=512", "nt=1024", "cww=64", "cww=16", "nt=1024,cww=32", "cww=16,ch=3",
-    "persist=8", "store=0", "store=3", "xfuse=1", "sig=0", "hfuse=0", "shstage=0", "extev=0",
-    "order=1", "order=2", "order=2,nt=512,cww=64", "mprobe=3,mprobemin=0", "mprobe=0",
-    "foldskip=1",
+    "", "rowsnt=256", "rowsnt=1024", "rows=1", "rows=1,cww=64", "rows=1,cww=16",
+    "async=0",
 ])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
-    """k_rows<512> / <1024> (chosen for n > 131k / 262k), several column
-    chunks (n > 524k), other work-item sizes, the persistent grid and the
-    store flavours, forced at small n; the crosscheck's sort folded into the
-    build's launches (xfuse) and event-based host syncs (sig=0): against
-    kano_py's matrix and lists."""
+    """The matrix write in address order from the class-level table
+    (k_rows_mc, every block size) and from the allowed-pod lists (k_rows,
+    which wide matrices take: column chunks forced at small n), with and
+    without asynchronous completion: against kano_py's matrix and lists."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids, tables_from_cluster
     from kano.synth import make_config, objects_from_json
@@ -300,6 +297,9 @@ def test_rows_variants_forced(name, tune, monkeypatch):
     eng = DeviceBuild(t, build=False)
     r = eng.verify(gid, sys_row=0, shadow=True)
     check_verify(r, exp)
+    assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
+    assert eng.info()["ROWS_KERNEL"] == (2 if "rows=1" in tune else 1)
+    eng.build()
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     eng.close()
 

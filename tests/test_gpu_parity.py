@@ -256,11 +256,9 @@ def test_verify_async_completion(tune, monkeypatch):
     pin.close()
 
 
-@pytest.mark.parametrize("tune", ["xfuse=0", "xfuse=1"])
-def test_verify_declared_groups_checked(tune, monkeypatch):
+def test_verify_declared_groups_checked():
     """A group id outside the declared [0, ngroups) is an error, not a fault
-    (the check in k_cls_group_range_m, or in k_cls_mfill with xfuse)."""
-    monkeypatch.setenv("KANO_TUNE", tune)
+    (the check in k_cls_group_range_m)."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids
     from kano._native import KanoNativeError
@@ -564,16 +562,15 @@ def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("tune", ["", "sig=0", "xfuse=1,forklate=0", "alistside=1", "hfuse=0,preclean=0",
-                                  "shstage=0,async=0,extev=0", "foldskip=1", "shseg=512",
-                                  "shscanside=1"])
+@pytest.mark.parametrize("tune", ["", "async=0", "rows=1", "packed=0"])
 @pytest.mark.parametrize("n,P", [(1, 0), (1, 1), (2, 3), (5, 1), (63, 7), (64, 64), (65, 9),
                                  (130, 40)])
 def test_verify_small_shapes_vs_oracle(n, P, tune, monkeypatch):
     """kano_verify on tiny and word-boundary shapes (1, 63, 64, 65 pods; no
-    policy; more policies than pods) under each host-sync form and the
-    launch-order variants: every list, the pairs and the count-only count
-    equal the C oracle's (a restatement of algorithm.py:4-80)."""
+    policy; more policies than pods) with synchronous and asynchronous
+    completion, both matrix-write forms and both classification forms: every
+    list, the pairs and the count-only count equal the C oracle's (a
+    restatement of algorithm.py:4-80)."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids
     from kano.synth import make_cluster, objects_from_json
