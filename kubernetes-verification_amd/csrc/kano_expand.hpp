@@ -42,18 +42,37 @@ __host__ __device__ __forceinline__ void transpose32(uint32_t* a) {
 
 constexpr int XR = 32;   // rows of M per tile (bits of a table entry)
 
+// LDS position of table entry b: one pad word per 64 entries, so that the
+// table build's lanes (64 consecutive entries each) write to distinct banks
+__device__ __forceinline__ uint32_t tpos(uint32_t b) { return b + (b >> 6); }
+inline size_t rows_mc_lds_bytes(int64_t Ua) {
+  return sizeof(uint32_t) * (size_t)(Ua + 1 + (Ua + 1) / 64 + 1);
+}
+
 struct RowsMcArgs {
   const u64* Mc;         // row classes x ldC words (column-class bits)
   i64 ldC;
   i64 UAW;               // words of a class-level row that hold column classes
-  i64 Ua;                // column classes
+  i64 Ua;                // column classes (entry Ua of the table is the all-zero sentinel)
   const int32_t* rcls;   // row class of pod i (global index; rows r0 .. r0+rl)
-  const int32_t* ccls;   // column class of pod j (all n pods)
-  i64 n;
-  i64 ldM;               // M row pitch (words); words W .. ldM-1 are written 0
+  const void* cct;       // column classes word-transposed: cct[j * ldM + w] = class of pod
+                         // 64w + j (Ua past the last pod); uint16_t when Ua < 65535, else int32
+  i64 ldM;               // M row pitch (words); words W .. ldM-1 come out 0
   i64 r0, rl;            // the rows held: [r0, r0 + rl)
   u64* M;                // local row r at M + r * ldM
 };
+
+// the column classes of every pod, word-transposed (k_rows_mc's lanes read
+// pod j of word w at cct[j * ldM + w]: 64 coalesced loads per lane)
+template <typename IdT>
+__global__ __launch_bounds__(TPB) void k_cc_transpose(const int32_t* __restrict__ ccls, i64 n,
+                                                      i64 ldM, int32_t Ua, IdT* __restrict__ cct) {
+  const i64 t = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (t >= 64 * ldM) return;
+  const i64 j = t / ldM, w = t - j * ldM;
+  const i64 pod = w * 64 + j;
+  cct[t] = (IdT)(pod < n ? ccls[pod] : Ua);
+}
 
 // the 32 x 32 bit transposes of one table word column: Mc words q of the
 // tile's rows -> T[64q .. 64q+63]
@@ -69,62 +88,49 @@ __device__ __forceinline__ void rows_mc_table_word(const RowsMcArgs& a, const in
   }
   transpose32(lo);
   transpose32(hi);
-  const i64 b0 = q * 64;
-  if (b0 + 64 <= a.Ua) {
+  const uint32_t b0 = (uint32_t)q * 64;
+  uint32_t* t0 = T + tpos(b0);   // entries b0 .. b0+63 are contiguous (one pad word after)
+  if (b0 + 64 <= (uint32_t)a.Ua) {
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-      T[b0 + k] = lo[k];
-      T[b0 + 32 + k] = hi[k];
+      t0[k] = lo[k];
+      t0[32 + k] = hi[k];
     }
   } else {
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-      if (b0 + k < a.Ua) T[b0 + k] = lo[k];
-      if (b0 + 32 + k < a.Ua) T[b0 + 32 + k] = hi[k];
+      if (b0 + k < (uint32_t)a.Ua) t0[k] = lo[k];
+      if (b0 + 32 + k < (uint32_t)a.Ua) t0[32 + k] = hi[k];
     }
   }
 }
 
-template <int NT>
+template <int NT, typename IdT>
 __global__ __launch_bounds__(NT) void k_rows_mc(RowsMcArgs a) {
-  extern __shared__ uint32_t T[];    // Ua table entries
+  extern __shared__ uint32_t T[];    // tpos(0 .. Ua) entries
   __shared__ int32_t rc[XR];
   const i64 t0 = (i64)blockIdx.x * XR;          // first local row of the tile
   const int nr = (int)min((i64)XR, a.rl - t0);  // block-uniform
   if (nr <= 0) return;
   if (threadIdx.x < XR) rc[threadIdx.x] = (int)threadIdx.x < nr ? a.rcls[a.r0 + t0 + threadIdx.x] : -1;
+  if (threadIdx.x == 0) T[tpos((uint32_t)a.Ua)] = 0u;   // the sentinel past the last pod
   __syncthreads();
   for (i64 q = threadIdx.x; q < a.UAW; q += NT) rows_mc_table_word(a, rc, q, T);
   __syncthreads();
+  const IdT* __restrict__ cct = static_cast<const IdT*>(a.cct);
   u64* __restrict__ out = a.M + t0 * a.ldM;
   for (i64 w = threadIdx.x; w < a.ldM; w += NT) {
-    const i64 j0 = w * 64;
     uint32_t lo[32], hi[32];
-    if (j0 + 64 <= a.n) {
-      const int4* src = reinterpret_cast<const int4*>(a.ccls + j0);
+    const IdT* col = cct + w;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int4 v = src[q];
-        lo[4 * q] = T[v.x];
-        lo[4 * q + 1] = T[v.y];
-        lo[4 * q + 2] = T[v.z];
-        lo[4 * q + 3] = T[v.w];
-      }
+    for (int k = 0; k < 32; ++k) {
+      lo[k] = (uint32_t)col[(i64)k * a.ldM];
+      hi[k] = (uint32_t)col[(i64)(k + 32) * a.ldM];
+    }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int4 v = src[8 + q];
-        hi[4 * q] = T[v.x];
-        hi[4 * q + 1] = T[v.y];
-        hi[4 * q + 2] = T[v.z];
-        hi[4 * q + 3] = T[v.w];
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 32; ++k) {
-        const i64 j = j0 + k, j2 = j0 + 32 + k;
-        lo[k] = j < a.n ? T[a.ccls[j]] : 0u;
-        hi[k] = j2 < a.n ? T[a.ccls[j2]] : 0u;
-      }
+    for (int k = 0; k < 32; ++k) {
+      lo[k] = T[tpos(lo[k])];
+      hi[k] = T[tpos(hi[k])];
     }
     transpose32(lo);
     transpose32(hi);

@@ -152,6 +152,7 @@ struct kano_ctx {
   DBuf scnt, cost, soffc, scur, slist, ecls, wicls, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
   DBuf ACT, AC, nca, acnt, alcoff, alc, aloff, alist;
   DBuf M, Mc, color, colnand, col_and, col_or_c, col_nand_c;
+  DBuf cct;                  // column classes word-transposed (k_rows_mc)
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
@@ -970,8 +971,7 @@ int build_alist(kano_ctx* ctx, hipStream_t st = nullptr, bool launch = true) {
 // the matrix write from the class-level table (k_rows_mc): its LDS table
 // holds 4 bytes per column class
 bool rows_mc_fits(const kano_ctx* ctx) {
-  return !ctx->rows_from && ctx->Mc.p &&
-         sizeof(uint32_t) * (size_t)std::max<i64>(1, ctx->cc.U) <= ROWS_MC_LDS_MAX;
+  return !ctx->rows_from && ctx->Mc.p && rows_mc_lds_bytes(ctx->cc.U) <= ROWS_MC_LDS_MAX;
 }
 
 // the part of the back end that needs only the class counts: zeroed AC,
@@ -1201,37 +1201,53 @@ int launch_rows(kano_ctx* ctx) {
   KCHK(hipEventRecord(ctx->rows_fork, rs));
   hipEvent_t e0 = ctx->ev[7], e1 = ctx->ev[8];
   if (rows_mc_fits(ctx)) {
+    // the column classes word-transposed (coalesced id loads in k_rows_mc),
+    // 16-bit when they fit
+    const i64 Ua = ctx->cc.U;
+    const bool id16 = Ua < 65535;
+    KTRY(dalloc(ctx, ctx->cct, (id16 ? 2 : 4) * (size_t)(64 * ldM)));
+    if (id16)
+      hipLaunchKernelGGL(k_cc_transpose<uint16_t>, dim3(nblk(64 * ldM)), dim3(TPB), 0, rs,
+                         P_<int32_t>(ctx->cc.cls), n, ldM, (int32_t)Ua, P_<uint16_t>(ctx->cct));
+    else
+      hipLaunchKernelGGL(k_cc_transpose<int32_t>, dim3(nblk(64 * ldM)), dim3(TPB), 0, rs,
+                         P_<int32_t>(ctx->cc.cls), n, ldM, (int32_t)Ua, P_<int32_t>(ctx->cct));
+    KLAUNCH();
     RowsMcArgs m{};
     m.Mc = P_<u64>(ctx->Mc);
     m.ldC = ctx->ldC;
     m.UAW = ctx->UAW;
-    m.Ua = ctx->cc.U;
+    m.Ua = Ua;
     m.rcls = P_<int32_t>(ctx->rc.cls);
-    m.ccls = P_<int32_t>(ctx->cc.cls);
-    m.n = n;
+    m.cct = ctx->cct.p;
     m.ldM = ldM;
     m.r0 = ctx->r0;
     m.rl = rl;
     m.M = P_<u64>(ctx->M);
-    const size_t lds = sizeof(uint32_t) * (size_t)std::max<i64>(1, ctx->cc.U);
+    const size_t lds = rows_mc_lds_bytes(Ua);
     const dim3 grid((unsigned)((rl + XR - 1) / XR));
     static bool attr_set = false;
     if (!attr_set) {   // dynamic LDS beyond 64 KiB
-      (void)hipFuncSetAttribute((const void*)k_rows_mc<256>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
-      (void)hipFuncSetAttribute((const void*)k_rows_mc<512>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
-      (void)hipFuncSetAttribute((const void*)k_rows_mc<1024>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
+      const void* fns[] = {(const void*)k_rows_mc<256, uint16_t>, (const void*)k_rows_mc<512, uint16_t>,
+                           (const void*)k_rows_mc<1024, uint16_t>, (const void*)k_rows_mc<256, int32_t>,
+                           (const void*)k_rows_mc<512, int32_t>, (const void*)k_rows_mc<1024, int32_t>};
+      for (const void* f : fns)
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
       (void)hipGetLastError();
       attr_set = true;
     }
-    if (ctx->rows_mc_nt == 1024)
-      hipExtLaunchKernelGGL(k_rows_mc<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, m);
-    else if (ctx->rows_mc_nt == 256)
-      hipExtLaunchKernelGGL(k_rows_mc<256>, grid, dim3(256), lds, rs, e0, e1, 0, m);
-    else
-      hipExtLaunchKernelGGL(k_rows_mc<512>, grid, dim3(512), lds, rs, e0, e1, 0, m);
+#define KANO_ROWS_MC(NT, IT) \
+  hipExtLaunchKernelGGL((k_rows_mc<NT, IT>), grid, dim3(NT), lds, rs, e0, e1, 0, m)
+    if (id16) {
+      if (ctx->rows_mc_nt == 1024) KANO_ROWS_MC(1024, uint16_t);
+      else if (ctx->rows_mc_nt == 256) KANO_ROWS_MC(256, uint16_t);
+      else KANO_ROWS_MC(512, uint16_t);
+    } else {
+      if (ctx->rows_mc_nt == 1024) KANO_ROWS_MC(1024, int32_t);
+      else if (ctx->rows_mc_nt == 256) KANO_ROWS_MC(256, int32_t);
+      else KANO_ROWS_MC(512, int32_t);
+    }
+#undef KANO_ROWS_MC
     KLAUNCH();
     ctx->rows_kernel = 1;
     ctx->rows_timed = true;
@@ -1719,7 +1735,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
-                  &ctx->irows,  &ctx->xw,      &ctx->xg};
+                  &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->cct};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
