@@ -68,7 +68,6 @@ def parse():
                          "auto = count for C4, pairs otherwise")
     ap.add_argument("--no-shadow", action="store_true", help="same as --shadow off")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU sample")
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: the N > 1 step (shard verify + RCCL all-gather + combine) "
                          "even at one rank, e.g. under torch.distributed.run --nproc-per-node 1")
@@ -153,14 +152,32 @@ class Step:
         return res
 
 
-def cpu_baseline(cl, tables, eng_info, shadow_pairs_total, budget):
-    """Oracle C port (1 core) on a bounded sample of the same cluster."""
+def _cpu_lib():
     import ctypes
-    from oracle import kano_oracle as orc
-    L = orc.lib()
-    obj = None
+    path = os.path.join(ROOT, "oracle", "libkano_cpu.so")
+    L = ctypes.CDLL(path)
+    vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    L.cpu_threads.argtypes = [i32]
+    L.cpu_build.argtypes = [i64, i64, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.cpu_col_reduce.argtypes = [i64, vp, i32, vp]
+    L.cpu_crosscheck.argtypes = [i64, vp, vp, vp]
+    L.cpu_lists.argtypes = [i64, i64, vp, vp, vp]
+    L.cpu_shadow.argtypes = [i64, i64, vp, vp, vp, i64, vp, ctypes.POINTER(i64)]
+    return L
+
+
+def cpu_baseline(cl, gid, config):
+    """The reference's algorithm (kano_py: build_matrix, all_reachable,
+    all_isolated, user_crosscheck, system_isolation, policy_shadow) over the
+    WHOLE cluster on the host's cores (oracle/kano_cpu.c, OpenMP; the same
+    per-element work as the single-threaded oracle/kano_oracle.c restatement),
+    timed end to end and checked against kano_py's record of the cluster."""
+    import ctypes
+    import hashlib
+    L = _cpu_lib()
     n, P = cl.n, cl.P
-    # integer tables the oracle understands: label CSR over ALL keys of the
+    p = lambda a: a.ctypes.data  # noqa: E731
+    # integer tables the port understands: label CSR over ALL keys of the
     # pods and working terms keyed by the same ids
     nk = cl.vals.shape[0]
     present = cl.vals >= 0
@@ -169,61 +186,74 @@ def cpu_baseline(cl, tables, eng_info, shadow_pairs_total, budget):
     np.cumsum(cnt, out=lab_off[1:])
     order = np.argsort(~present.T, axis=1, kind="stable")  # keys of each pod first
     lab_key = np.concatenate([order[i, :cnt[i]] for i in range(n)]).astype(np.int32)
-    # value ids must be unique per (key, value): offset by key
     lab_val = (cl.vals[lab_key, np.repeat(np.arange(n), cnt)].astype(np.int64)
-               + lab_key.astype(np.int64) * 10_000_000).astype(np.int64)
+               + lab_key.astype(np.int64) * 10_000_000)
     (so, sk, sv), (ao, ak, av) = cl.working_terms()
-    sv2 = (sv.astype(np.int64) + sk.astype(np.int64) * 10_000_000)
-    av2 = (av.astype(np.int64) + ak.astype(np.int64) * 10_000_000)
-    # compress ids into int32
+    sv2 = sv.astype(np.int64) + sk.astype(np.int64) * 10_000_000
+    av2 = av.astype(np.int64) + ak.astype(np.int64) * 10_000_000
     allv = np.unique(np.concatenate([lab_val, sv2, av2]))
     lab_val = np.searchsorted(allv, lab_val).astype(np.int32)
     sv2 = np.searchsorted(allv, sv2).astype(np.int32)
     av2 = np.searchsorted(allv, av2).astype(np.int32)
+    so = np.ascontiguousarray(so, np.int64)
+    ao = np.ascontiguousarray(ao, np.int64)
+    sk = np.ascontiguousarray(sk, np.int32)
+    ak = np.ascontiguousarray(ak, np.int32)
     W = (n + 63) // 64
-    p_s = max(1, min(P, int(P * 0.02)))
-    M = np.zeros(n * W, np.uint64)
-    alw = np.zeros(p_s * W, np.uint64)
-    sel = np.zeros(p_s * W, np.uint64)
+    threads = L.cpu_threads(0)
+    M = np.empty(n * W, np.uint64)
+    sel = np.empty(P * W, np.uint64)
+    alw = np.empty(P * W, np.uint64)
+    sec = {}
     t = time.perf_counter()
-    L.oracle_build(n, nk, orc._p(lab_off), orc._p(lab_key), orc._p(lab_val), p_s,
-                   orc._p(so), orc._p(sk.astype(np.int32)), orc._p(sv2), orc._p(ao),
-                   orc._p(ak.astype(np.int32)), orc._p(av2), orc._p(M), orc._p(sel), orc._p(alw))
-    t_build = (time.perf_counter() - t) * P / p_s
-    c_s = max(64, min(n, int(budget * 0.15 / 2e-4)))
-    reach = np.zeros(n, np.uint8)
-    isol = np.zeros(n, np.uint8)
+    L.cpu_build(n, nk, p(lab_off), p(lab_key), p(lab_val), P, p(so), p(sk), p(sv2), p(ao), p(ak),
+                p(av2), p(M), p(sel), p(alw))
+    sec["build_matrix"] = time.perf_counter() - t
+    reach = np.empty(n, np.uint8)
+    isol = np.empty(n, np.uint8)
     t = time.perf_counter()
-    L.oracle_column_checks(n, orc._p(M), 0, c_s, orc._p(reach), orc._p(isol))
-    t_cols = (time.perf_counter() - t) * n / c_s * 2      # two passes in the reference
-    gid = cl.vals[0].astype(np.int32)
-    cross = np.zeros(n, np.uint8)
-    c_x = max(32, c_s // 4)
+    L.cpu_col_reduce(n, p(M), 0, p(reach))
+    sec["all_reachable"] = time.perf_counter() - t
     t = time.perf_counter()
-    L.oracle_crosscheck(n, orc._p(M), orc._p(gid), 0, c_x, orc._p(cross))
-    t_cross = (time.perf_counter() - t) * n / c_x
-    # shadow: time per pair test (allow rows of W words), times the exact pair
-    # count sum_i |S(i)|(|S(i)|-1) (from the GPU build's class lists)
-    npairs_test = 20000
-    lists_off = np.arange(0, 2 * npairs_test + 1, 2, dtype=np.int64)
-    rng = np.random.default_rng(0)
-    lst = rng.integers(0, p_s, size=2 * npairs_test).astype(np.int32)
-    c = ctypes.c_int64()
+    L.cpu_col_reduce(n, p(M), 1, p(isol))
+    sec["all_isolated"] = time.perf_counter() - t
+    cross = np.empty(n, np.uint8)
+    g = np.ascontiguousarray(gid, np.int32)
     t = time.perf_counter()
-    L.oracle_shadow(npairs_test, n, orc._p(lists_off), orc._p(lst), orc._p(alw), 0, npairs_test,
-                    0, None, ctypes.byref(c))
-    per_test = (time.perf_counter() - t) / (2 * npairs_test)
-    t_shadow = per_test * shadow_pairs_total
-    total = t_build + t_cols + t_cross + t_shadow
+    L.cpu_crosscheck(n, p(M), p(g), p(cross))
+    sec["user_crosscheck"] = time.perf_counter() - t
+    t = time.perf_counter()
+    row0 = np.unpackbits(M[:W].view(np.uint8), bitorder="little")[:n]
+    sysiso = np.flatnonzero(row0 == 0).astype(np.int32)
+    sec["system_isolation"] = time.perf_counter() - t
+    t = time.perf_counter()
+    off = np.zeros(n + 1, np.int64)
+    L.cpu_lists(n, P, p(sel), p(off), None)
+    lst = np.empty(max(1, int(off[-1])), np.int32)
+    L.cpu_lists(n, P, p(sel), p(off), p(lst))
+    cnt_pairs = ctypes.c_int64()
+    cap = 1 << 24
+    pairs = np.empty(2 * cap, np.int32)
+    L.cpu_shadow(n, n, p(off), p(lst), p(alw), cap, p(pairs), ctypes.byref(cnt_pairs))
+    sec["policy_shadow"] = time.perf_counter() - t
+    total = sum(sec.values())
+    res = {"all_reachable": np.flatnonzero(reach).astype(np.int32),
+           "all_isolated": np.flatnonzero(isol).astype(np.int32),
+           "user_crosscheck": np.flatnonzero(cross).astype(np.int32),
+           "system_isolation": sysiso,
+           "policy_shadow": pairs[:2 * min(cnt_pairs.value, cap)].reshape(-1, 2),
+           "policy_shadow_count": cnt_pairs.value}
+    verified, _ = verify_against_golden(config, cl, res, 1, 0, 0, "pairs")
+    del M, sel, alw
     return {
-        "value": float(n) * n / total, "unit": "pod-pairs/s", "cores": 1, "kind": "port",
-        "sample": (f"oracle C port of kano_py on the same {n}-pod cluster: build_matrix over "
-                   f"{p_s}/{P} policies (x{P / p_s:.0f}), all_reachable+all_isolated over "
-                   f"{c_s}/{n} columns, user_crosscheck over {c_x}/{n} columns, policy_shadow "
-                   f"{2 * npairs_test} subset tests x {shadow_pairs_total} tests; extrapolated "
-                   f"total {total:.1f} s"),
-        "seconds": {"build": round(t_build, 2), "col_checks": round(t_cols, 2),
-                    "crosscheck": round(t_cross, 2), "shadow": round(t_shadow, 2)},
+        "value": float(n) * n / total, "unit": "pod-pairs/s", "cores": int(threads),
+        "kind": "port",
+        "sample": (f"the whole {n}-pod / {P}-policy cluster (no extrapolation): oracle/kano_cpu.c, "
+                   f"kano_py's algorithm (build_matrix, all_reachable, all_isolated, "
+                   f"user_crosscheck, system_isolation, policy_shadow) on {threads} OpenMP threads "
+                   f"(OMP_NUM_THREADS); {total:.1f} s"),
+        "seconds": {k: round(v, 3) for k, v in sec.items()},
+        "verified": verified,
     }
 
 
@@ -389,14 +419,8 @@ def main():
         ref = kano_py_measured(args.config)
         if ref:
             out["kano_py_measured"] = ref
-        if args.cpu_baseline and world == 1:
-            sum_s2 = 0
-            if shadow != "off":
-                off, _ = eng.select_csr()
-                cls = eng.classes()
-                s = np.diff(off)[cls].astype(np.int64)
-                sum_s2 = int((s * (s - 1)).sum())
-            out["cpu_baseline"] = cpu_baseline(cl, tables, info, sum_s2, args.cpu_budget)
+        if args.cpu_baseline and world == 1 and args.rank_of <= 1 and n <= 200_000:
+            out["cpu_baseline"] = cpu_baseline(cl, gid, args.config)
             out["cpu_baseline"]["cpu"] = _cpu_model()
         print(json.dumps(out), flush=True)
     eng.close()
