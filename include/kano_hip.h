@@ -368,6 +368,37 @@ int kano_build_classes(kano_ctx* ctx, int path);
  * reset != 0 zeroes them after reading. */
 int kano_host_times(kano_ctx* ctx, double* out /* 12 */, int reset);
 
+/* One process over G devices (SURVEY.md §8(b) kano_init(ngpu), §8(e) row
+ * sharding; no reference counterpart: kano_py is single-process).  The group
+ * owns G member contexts, member r on device devices[r] (NULL: r) with its
+ * own stream; the caller uploads the inputs to every member and gives member
+ * r its row shard (kano_set_shard) -- kano/multi.py does both.  The column
+ * checks exchange the members' [OR | cross | NAND] words: ncclAllGather over
+ * xGMI (communicators from ncclCommInitAll) when the devices are distinct
+ * and RCCL loads (mode 1), device-to-device copies otherwise (mode 2, e.g.
+ * G members on one device; env KANO_GROUP_COPY forces it); every member ORs
+ * the gathered words on its device.  Members run on one host thread each.
+ *   kano_group_verify: kano_verify over the whole matrix -- the three
+ *     column lists (all_reachable, all_isolated, user_crosscheck) of every
+ *     row, system_isolation(sys_row) from the row's owner, policy_shadow's
+ *     pairs concatenated in rank order (= the reference's container order);
+ *     arguments as kano_verify_shard / kano_verify_combine (with_shadow 0 /
+ *     1 pairs / 2 count only).
+ *   kano_group_checks: the same checks over the members' matrices as they
+ *     stand (kano_checks_shard), no policy_shadow.
+ * kano_group_info: out[0] = G, out[1] = exchange mode. */
+typedef struct kano_group kano_group;
+int  kano_group_create(int ngpu, const int* devices, kano_group** out);
+void kano_group_destroy(kano_group* g);
+const char* kano_group_last_error(const kano_group* g);
+int  kano_group_info(kano_group* g, int32_t* out /* 2 */);
+int  kano_group_member(kano_group* g, int r, kano_ctx** ctx);
+int  kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngroups,
+                       int64_t sys_row, int with_shadow, int32_t* idx, int64_t* counts,
+                       int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count);
+int  kano_group_checks(kano_group* g, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                       int32_t* idx, int64_t* counts);
+
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);
 void kano_host_free(void* p);

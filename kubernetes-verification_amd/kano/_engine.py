@@ -79,6 +79,20 @@ class DeviceBuild:
             if build:
                 self.build(path)
 
+    @classmethod
+    def adopt(cls, ctx: c_void_p, device: int = 0, path: str = "auto") -> "DeviceBuild":
+        """Wrap a context owned elsewhere (a kano_group member, kano/multi.py):
+        its owner destroys it."""
+        self = cls.__new__(cls)
+        self.lib = nat.load()
+        self.ctx = ctx
+        self.device = device
+        self.path = path
+        self._counts = None
+        self.row_span = None
+        self.tables = None
+        return self
+
     # -- plumbing -------------------------------------------------------
     def _chk(self, rc, what):
         nat.check(self.ctx, rc, what)

@@ -74,6 +74,14 @@ SIGNATURES = {
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_rows_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_host_times": (c_int, [c_void_p, c_void_p, c_int]),
+    "kano_group_create": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
+    "kano_group_destroy": (None, [c_void_p]),
+    "kano_group_last_error": (ctypes.c_char_p, [c_void_p]),
+    "kano_group_info": (c_int, [c_void_p, c_void_p]),
+    "kano_group_member": (c_int, [c_void_p, c_int, POINTER(c_void_p)]),
+    "kano_group_verify": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_int, c_void_p,
+                                  c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
+    "kano_group_checks": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),
 }

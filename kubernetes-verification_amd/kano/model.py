@@ -467,8 +467,13 @@ class ReachabilityMatrix:
     def build_matrix(containers: List[Container], policies: List[Policy]):
         from ._engine import DeviceBuild
         from ._intern import intern
+        from .multi import MultiBuild, requested_devices, requested_gpus
         tables = intern(containers, policies)
-        engine = DeviceBuild(tables)
+        G = requested_gpus()
+        if G > 1:   # one process over G devices: rows sharded (kano/multi.py)
+            engine = MultiBuild(tables, G, devices=requested_devices(G))
+        else:
+            engine = DeviceBuild(tables)
         for p, pol in enumerate(policies):
             pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
         lists = _BuildLists(engine)

@@ -1,0 +1,325 @@
+"""One process over G devices: the drop-in API on a row-sharded matrix.
+
+``ReachabilityMatrix.build_matrix`` uses this engine when ``KANO_NGPU`` = G
+> 1 (SURVEY.md §8(b) ``kano_init(ngpu)``, §8(e)): a ``kano_group`` (C ABI,
+include/kano_hip.h) owns G member contexts, member r on device r (or
+``KANO_DEVICES``, comma-separated) holding rows [r0_r, r1_r) of M.  The build
+needs no communication; the whole-matrix checks run on the device:
+
+  all_reachable, all_isolated,   each member's [OR | cross | NAND] column
+  user_crosscheck                words exchanged (ncclAllGather over xGMI when
+  (kano_py/kano/algorithm.py     the devices are distinct, device copies
+   :4-42)                        otherwise) and OR-ed on every member
+  system_isolation(idx) (:45-55) the row's owner, whichever member it is
+  policy_shadow (:58-80)         the members' pairs in rank order (= container
+                                 order: the shards are consecutive rows)
+  getrow / getcol / [i, j]       the owner / every member's part, in order
+  (model.py:171-184)
+
+Shard boundaries are multiples of 64 rows, so a column is the members' word
+arrays concatenated.  The engine offers the DeviceBuild methods the drop-in
+API calls; incremental updates and multi-hop products stay single-device.
+"""
+from __future__ import annotations
+
+import os
+from ctypes import byref, c_int64, c_void_p
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _native as nat
+from ._bits import bool_to_words
+from ._engine import DeviceBuild, _ptr
+from ._intern import Tables
+
+
+def shard_bounds(n: int, G: int) -> List[Tuple[int, int]]:
+    """Consecutive row ranges, boundaries at multiples of 64 rows."""
+    words = (n + 63) >> 6
+    out = []
+    for r in range(G):
+        a = min(n, (words * r // G) << 6)
+        b = min(n, (words * (r + 1) // G) << 6)
+        out.append((a, b))
+    return out
+
+
+def requested_gpus() -> int:
+    try:
+        return max(1, int(os.environ.get("KANO_NGPU", "1")))
+    except ValueError:
+        return 1
+
+
+def requested_devices(G: int) -> Optional[List[int]]:
+    spec = os.environ.get("KANO_DEVICES")
+    if not spec:
+        return None
+    devs = [int(x) for x in spec.split(",") if x.strip()]
+    if len(devs) != G:
+        raise ValueError(f"KANO_DEVICES lists {len(devs)} devices for KANO_NGPU={G}")
+    return devs
+
+
+class MultiBuild:
+    """A kano_group: G row-shard contexts in one process (see module doc)."""
+
+    def __init__(self, tables: Tables, ngpu: int, devices: Optional[List[int]] = None,
+                 path: str = "auto", build: bool = True):
+        self.lib = nat.load()
+        self.g = c_void_p()
+        G = int(ngpu)
+        devs = None
+        if devices is not None:
+            devs = np.ascontiguousarray(devices, dtype=np.int32)
+        rc = self.lib.kano_group_create(G, _ptr(devs), byref(self.g))
+        if rc != 0:
+            self.g = c_void_p()
+            raise nat.KanoNativeError(f"kano_group_create({G}) failed (rc={rc})")
+        self.G = G
+        self.path = path
+        self.tables = tables
+        self.row_span = None
+        self.bounds = shard_bounds(tables.n, G)
+        info = np.zeros(2, dtype=np.int32)
+        self.lib.kano_group_info(self.g, _ptr(info))
+        self.mode = {1: "rccl all-gather", 2: "device copies"}[int(info[1])]
+        self.members: List[DeviceBuild] = []
+        for r in range(G):
+            ctx = c_void_p()
+            self._chk(self.lib.kano_group_member(self.g, r, byref(ctx)), "kano_group_member")
+            m = DeviceBuild.adopt(ctx, device=int(devices[r]) if devices is not None else r,
+                                  path=path)
+            m.upload(tables)
+            m.set_rows(*self.bounds[r])
+            self.members.append(m)
+        self.device = self.members[0].device
+        self._idx = None
+        if build:
+            self.build(path)
+
+    # -- plumbing -------------------------------------------------------
+    def _chk(self, rc, what):
+        if rc != 0:
+            raw = self.lib.kano_group_last_error(self.g) if self.g else b""
+            raise nat.KanoNativeError(f"{what} failed (rc={rc}): "
+                                      f"{raw.decode(errors='replace') if raw else ''}")
+
+    def close(self):
+        if self.g:
+            for m in self.members:
+                m.ctx = c_void_p()          # owned by the group
+            self.lib.kano_group_destroy(self.g)
+            self.g = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n(self) -> int:
+        return self.tables.n
+
+    @property
+    def W(self) -> int:
+        return (self.tables.n + 63) >> 6
+
+    is_shard = False
+
+    def owner(self, i: int) -> int:
+        for r, (a, b) in enumerate(self.bounds):
+            if a <= i < b:
+                return r
+        raise IndexError("row out of range")
+
+    def build(self, path: Optional[str] = None) -> None:
+        for m in self.members:
+            m.build(path or self.path)
+
+    def info(self) -> dict:
+        infos = [m.info() for m in self.members]
+        out = dict(infos[0])
+        out["ROW0"], out["ROW1"] = 0, self.n
+        for k in ("U", "NNZ_SEL", "HEAVY", "WORK_ITEMS"):
+            out[k] = sum(i[k] for i in infos)
+        out["MAXSEL"] = max(i["MAXSEL"] for i in infos)
+        return out
+
+    # -- whole-matrix checks on the device ----------------------------------
+    def _lists(self, counts, idx):
+        out, o = {}, 0
+        for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
+                                  "system_isolation")):
+            k = int(counts[r])
+            out[name] = idx[o:o + k] if k >= 0 else None
+            o += max(k, 0)
+        return out
+
+    def _idx_buf(self):
+        if self._idx is None or self._idx.size < 4 * max(self.n, 1):
+            self._idx = np.empty(4 * max(self.n, 1), dtype=np.int32)
+        return self._idx
+
+    def checks(self, gid: Optional[np.ndarray] = None, sys_row: int = -1) -> dict:
+        """kano_group_checks: the column lists over every member's rows (and
+        the owner's system row when sys_row >= 0)."""
+        counts = np.zeros(4, dtype=np.int64)
+        idx = self._idx_buf()
+        g = None if gid is None else np.ascontiguousarray(gid, dtype=np.int32)
+        self._chk(self.lib.kano_group_checks(self.g, _ptr(g), 0, int(sys_row), _ptr(idx),
+                                             counts.ctypes.data), "kano_group_checks")
+        return {k: (None if v is None else v.copy()) for k, v in self._lists(counts, idx).items()}
+
+    def col_checks(self) -> Tuple[np.ndarray, np.ndarray]:
+        r = self.checks()
+        n = self.n
+        reach = np.zeros(n, bool)
+        reach[r["all_reachable"]] = True
+        reached = np.ones(n, bool)
+        reached[r["all_isolated"]] = False
+        return bool_to_words(reach), bool_to_words(reached)
+
+    def crosscheck(self, gid: np.ndarray) -> np.ndarray:
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        if gid.shape[0] != self.n:
+            raise ValueError("gid must have one entry per pod")
+        r = self.checks(gid)
+        bits = np.zeros(self.n, bool)
+        bits[r["user_crosscheck"]] = True
+        return bool_to_words(bits)
+
+    def verify(self, gid=None, sys_row: int = 0, shadow: bool = True,
+               pairs: Optional[np.ndarray] = None, idx: Optional[np.ndarray] = None,
+               path: Optional[str] = None, shadow_count_only: bool = False) -> dict:
+        """kano_group_verify: build + every check over all G members (as
+        DeviceBuild.verify)."""
+        n = self.n
+        if idx is None:
+            idx = np.empty(max(4 * n, 1), dtype=np.int32)
+        g = None if gid is None else np.ascontiguousarray(gid, dtype=np.int32)
+        counts = np.zeros(4, dtype=np.int64)
+        cnt = c_int64(0)
+        cap = 0 if pairs is None else pairs.size // 2
+        if shadow_count_only:
+            cap = -1
+        with_shadow = 0 if not shadow else (2 if shadow_count_only else 1)
+        pth = nat.PATHS[path or self.path]
+        self._chk(self.lib.kano_group_verify(self.g, pth, _ptr(g), 0, int(sys_row), with_shadow,
+                                             _ptr(idx), counts.ctypes.data, _ptr(pairs), int(cap),
+                                             byref(cnt) if shadow else None), "kano_group_verify")
+        out = self._lists(counts, idx)
+        if gid is None:
+            out["user_crosscheck"] = None
+        if shadow:
+            k = int(cnt.value)
+            out["shadow_count"] = k
+            if shadow_count_only:
+                out["pairs"] = None
+            elif pairs is not None and k <= cap:
+                out["pairs"] = pairs.reshape(-1)[:2 * k].reshape(k, 2)
+            else:
+                out["pairs"] = np.concatenate([m.shadow_fetch(m.shadow_count())
+                                               for m in self.members]).reshape(-1, 2)
+        return out
+
+    def shadow(self) -> np.ndarray:
+        """policy_shadow's pairs: each member's (its containers), rank order."""
+        parts = [m.shadow() for m in self.members]
+        return np.concatenate(parts).reshape(-1, 2) if parts else np.zeros((0, 2), np.int32)
+
+    def conflict_raises(self) -> bool:
+        return any(m.conflict_raises() for m in self.members)
+
+    # -- matrix access: owners --------------------------------------------
+    def rows(self, r0: int, nrows: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros((nrows, self.W), dtype=np.uint64)
+        for m, (a, b) in zip(self.members, self.bounds):
+            lo, hi = max(a, r0), min(b, r0 + nrows)
+            if lo < hi:
+                m.rows(lo, hi - lo, out[lo - r0:hi - r0])
+        return out
+
+    def put_rows(self, r0: int, words: np.ndarray) -> None:
+        words = np.ascontiguousarray(words, dtype=np.uint64).reshape(-1, self.W)
+        for m, (a, b) in zip(self.members, self.bounds):
+            lo, hi = max(a, r0), min(b, r0 + words.shape[0])
+            if lo < hi:
+                m.put_rows(lo, words[lo - r0:hi - r0])
+
+    def col(self, j: int) -> np.ndarray:
+        """Column j: every member's rows' bits (64-row aligned shards)."""
+        parts = [m.col(j) for m, (a, b) in zip(self.members, self.bounds) if b > a]
+        return np.concatenate(parts)[: self.W] if parts else np.zeros(self.W, np.uint64)
+
+    def get_bit(self, i: int, j: int) -> int:
+        return self.members[self.owner(int(i))].get_bit(i, j)
+
+    def set_bit(self, i: int, j: int, value) -> None:
+        self.members[self.owner(int(i))].set_bit(i, j, value)
+
+    def export_rows(self, r0: int, nrows: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        nb = (self.n + 7) >> 3
+        if out is None:
+            out = np.empty((max(nrows, 0), nb), dtype=np.uint8)
+        for m, (a, b) in zip(self.members, self.bounds):
+            lo, hi = max(a, r0), min(b, r0 + nrows)
+            if lo < hi:
+                m.export_rows(lo, hi - lo, out[lo - r0:hi - r0])
+        return out
+
+    def import_rows(self, r0: int, rows: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.uint8)
+        for m, (a, b) in zip(self.members, self.bounds):
+            lo, hi = max(a, r0), min(b, r0 + rows.shape[0])
+            if lo < hi:
+                m.import_rows(lo, rows[lo - r0:hi - r0])
+
+    # -- build side effects (Container / Policy lists) ------------------------
+    def classes(self) -> np.ndarray:
+        """Row class of every pod, ids made global (member r's classes offset
+        by the classes of members < r)."""
+        out = np.full(self.n, -1, dtype=np.int32)
+        base = 0
+        for m, (a, b) in zip(self.members, self.bounds):
+            c = m.classes()
+            out[a:b] = c[a:b] + base
+            base += m.info()["U"]
+        return out
+
+    def select_csr(self) -> Tuple[np.ndarray, np.ndarray]:
+        offs, pols, base = [np.zeros(1, np.int64)], [], 0
+        for m in self.members:
+            off, pol = m.select_csr()
+            offs.append(off[1:] + base)
+            pols.append(pol)
+            base += int(off[-1])
+        return np.concatenate(offs), (np.concatenate(pols) if pols else np.zeros(0, np.int32))
+
+    def allow_csr(self) -> Tuple[np.ndarray, np.ndarray]:
+        return self.members[0].allow_csr()   # the column side is whole on every member
+
+    def policy_sets(self, p: int, sel: bool = True, allow: bool = True):
+        s = None
+        if sel:
+            s = np.zeros(self.W, dtype=np.uint64)
+            for m in self.members:
+                s |= m.policy_sets(p, True, False)[0]
+        a = self.members[0].policy_sets(p, False, True)[1] if allow else None
+        return s, a
+
+    # -- single-device only -----------------------------------------------
+    def _single(self, what):
+        raise NotImplementedError(f"{what} runs on a single-device matrix (KANO_NGPU=1)")
+
+    def add_policies(self, *a, **k):
+        self._single("add_policies")
+
+    def remove_policies(self, *a, **k):
+        self._single("remove_policies")
+
+    def path_from(self, *a, **k):
+        self._single("multi-hop reachability")
