@@ -341,7 +341,7 @@ def main():
     value = float(n) * n / (elapsed / args.steps)
     rt = eng.rows_timing()
     k_rows_ms = rt["sum_ms"] / rt["launches"] if rt["launches"] else float("nan")
-    rows_kernel = {1: "k_rows_mc", 2: "k_rows"}.get(info["ROWS_KERNEL"], "none")
+    rows_kernel = {2: "k_rows"}.get(info["ROWS_KERNEL"], "none")
     host = eng.host_times()
     rows_local = r1 - r0
     W = (n + 63) // 64

@@ -57,8 +57,7 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_UA      10   /* column classes (pods with equal allow keys) */
 #define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 int8 MFMA          */
 #define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the list-based row kernel */
-#define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 1 k_rows_mc (class table, address
-                                    order), 2 k_rows (allowed-pod lists), 0 none */
+#define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 2 k_rows, 0 none yet */
 #define KANO_INFO_NSLOTS   14
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in

@@ -50,7 +50,6 @@
 #include "kano_path.hpp"
 #include "kano_inc.hpp"
 #include "kano_k8s.hpp"
-#include "kano_expand.hpp"
 
 using namespace kano;
 
@@ -60,9 +59,7 @@ constexpr int HT_ROWS = 128;    // heavy rows per MFMA launch (HT = 4)
 constexpr int ROWS_CH = 16;     // member rows per k_rows work item
 constexpr int LD_ALIGN = 16;    // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 constexpr int MFMA_KMIN = 8;    // min policy blocks (64 policies each) per MFMA wave
-// k_rows_mc's LDS table (4 bytes per column class) must leave a block on a
-// CU: 160 KiB per CU
-constexpr size_t ROWS_MC_LDS_MAX = 152 * 1024;
+
 }  // namespace
 
 struct DBuf {
@@ -125,8 +122,7 @@ struct kano_ctx {
   // shipped forms that compute the same results; none changes a result.
   int stage_timing = 0;      // timing=1: the stage events of kano_stage_times (slots 0-5)
   int cls_packed = 1;        // packed=0: classification without packed keys (the wide-key form)
-  int rows_from = 0;         // rows=1: the matrix write from the allowed-pod lists (k_rows)
-                             // even where the class-level table fits (k_rows_mc)
+  int rows_plain = 0;        // store=0: k_rows with plain stores (non-temporal by default)
   int async_rows = 1;        // async=0: kano_verify waits for its matrix write
   int shadow_count_mode = 0; // shcount=1|2: count-only policy_shadow pairwise | grouped
                              // (0: the device picks, shg_grouped)
@@ -135,7 +131,6 @@ struct kano_ctx {
   int path_tm = 2;           // pathtm / pathtn: k_path_mfma tiles per wave
   int path_tn = 2;
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
-  int rows_mc_nt = 512;      // rowsnt: k_rows_mc block size (256 / 512 / 1024)
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
 
@@ -147,13 +142,12 @@ struct kano_ctx {
   bool rows_use_alist = false;
   int max_sel = 0;
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
-  int rows_kernel = 0;       // the last matrix write: 1 k_rows_mc (class table), 2 k_rows (lists)
+  int rows_kernel = 0;       // the last matrix write: 2 k_rows, 0 none
 
   DBuf pv;
   DBuf scnt, cost, soffc, scur, slist, ecls, wicls, maxs, wicnt, wioff, hflag, hoff, hlist, sq, pfoff;
   DBuf ACT, AC, nca, acnt, alcoff, alc, aloff, alist;
   DBuf M, Mc, color, colnand, col_and, col_or_c, col_nand_c;
-  DBuf cct;                  // column classes word-transposed (k_rows_mc)
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
@@ -969,12 +963,6 @@ int build_alist(kano_ctx* ctx, hipStream_t st = nullptr, bool launch = true) {
   return 0;
 }
 
-// the matrix write from the class-level table (k_rows_mc): its LDS table
-// holds 4 bytes per column class
-bool rows_mc_fits(const kano_ctx* ctx) {
-  return !ctx->rows_from && ctx->Mc.p && rows_mc_lds_bytes(ctx->cc.U) <= ROWS_MC_LDS_MAX;
-}
-
 // the part of the back end that needs only the class counts: zeroed AC,
 // Mc, cursors and class-level column words, then the caller's fills and
 // launches (kano_verify: the crosscheck's group keys) -- queued while the
@@ -1071,17 +1059,14 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     KLAUNCH();
   }
   if (ctx->fork_hook) KTRY(ctx->fork_hook());   // lists and AC are complete here
-  // The matrix write reads the class-level table (k_rows_mc) when it fits
-  // LDS; otherwise (very many column classes, C5) it rebuilds rows from the
-  // allowed-pod lists (k_rows): the flat lists (materialised here, one pass
-  // over nnz_alw entries) or the column-class member lists (n entries,
-  // cache-resident).  The flat lists win wherever the light rows read them
-  // at all (measured: C3 at 1/8 of the rows k_rows 99 -> 49 us; C5 21.8 ->
-  // 20.9 ms); where nearly every class is heavy (C4) building them is pure
-  // cost (+0.45 ms a step)
+  // Light rows read either the flat allowed-pod lists (materialised here,
+  // one pass over nnz_alw entries) or the column-class member lists (n
+  // entries, cache-resident).  The flat lists win wherever the light rows
+  // read them at all (measured: C3 at 1/8 of the rows k_rows 99 -> 49 us; C5
+  // 21.8 -> 20.9 ms); where nearly every class is heavy (C4) building them
+  // is pure cost (+0.45 ms a step)
   ctx->alist_valid = false;
-  const bool lists_rows = !rows_mc_fits(ctx);
-  ctx->rows_use_alist = lists_rows && ctx->light_cost > 0 && ctx->light_cost * 16 > ctx->nnz_alw &&
+  ctx->rows_use_alist = ctx->light_cost > 0 && ctx->light_cost * 16 > ctx->nnz_alw &&
                         ctx->nnz_alw * 4 <= (2ll << 30);
   // (k_pol_pods' blocks ride in the Mc launch when both run)
   const McScatterArgs msa{ctx->nnz_sel, P_<int32_t>(ctx->ecls), P_<int32_t>(ctx->slist),
@@ -1187,10 +1172,9 @@ int do_rows(kano_ctx* ctx) {
 
 // The matrix write, timed by its own dispatch (hipExtLaunchKernelGGL's start
 // / stop events ev[7] -> ev[8]: no marker packets around it; the bench's
-// roofline reads them through kano_rows_timing).  k_rows_mc (address order,
-// from Mc and the column classes) wherever its LDS table fits, else k_rows
-// (heavy rows expanded from Mc first, then every class row rebuilt from the
-// allowed-pod lists and streamed to its members).
+// roofline reads them through kano_rows_timing): heavy rows expanded from
+// Mc first, then every light class row rebuilt from the allowed-pod lists
+// in LDS and streamed to its members (k_rows).
 int launch_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
@@ -1201,60 +1185,6 @@ int launch_rows(kano_ctx* ctx) {
   ctx->rows_fork = ctx->ev_rows_fork;
   KCHK(hipEventRecord(ctx->rows_fork, rs));
   hipEvent_t e0 = ctx->ev[7], e1 = ctx->ev[8];
-  if (rows_mc_fits(ctx)) {
-    // the column classes word-transposed (coalesced id loads in k_rows_mc),
-    // 16-bit when they fit
-    const i64 Ua = ctx->cc.U;
-    const bool id16 = Ua < 65535;
-    KTRY(dalloc(ctx, ctx->cct, (id16 ? 2 : 4) * (size_t)(64 * ldM)));
-    if (id16)
-      hipLaunchKernelGGL(k_cc_transpose<uint16_t>, dim3(nblk(64 * ldM)), dim3(TPB), 0, rs,
-                         P_<int32_t>(ctx->cc.cls), n, ldM, (int32_t)Ua, P_<uint16_t>(ctx->cct));
-    else
-      hipLaunchKernelGGL(k_cc_transpose<int32_t>, dim3(nblk(64 * ldM)), dim3(TPB), 0, rs,
-                         P_<int32_t>(ctx->cc.cls), n, ldM, (int32_t)Ua, P_<int32_t>(ctx->cct));
-    KLAUNCH();
-    RowsMcArgs m{};
-    m.Mc = P_<u64>(ctx->Mc);
-    m.ldC = ctx->ldC;
-    m.UAW = ctx->UAW;
-    m.Ua = Ua;
-    m.rcls = P_<int32_t>(ctx->rc.cls);
-    m.cct = ctx->cct.p;
-    m.ldM = ldM;
-    m.r0 = ctx->r0;
-    m.rl = rl;
-    m.M = P_<u64>(ctx->M);
-    const size_t lds = rows_mc_lds_bytes(Ua);
-    const dim3 grid((unsigned)((rl + XR - 1) / XR));
-    static bool attr_set = false;
-    if (!attr_set) {   // dynamic LDS beyond 64 KiB
-      const void* fns[] = {(const void*)k_rows_mc<256, uint16_t>, (const void*)k_rows_mc<512, uint16_t>,
-                           (const void*)k_rows_mc<1024, uint16_t>, (const void*)k_rows_mc<256, int32_t>,
-                           (const void*)k_rows_mc<512, int32_t>, (const void*)k_rows_mc<1024, int32_t>};
-      for (const void* f : fns)
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_MC_LDS_MAX);
-      (void)hipGetLastError();
-      attr_set = true;
-    }
-#define KANO_ROWS_MC(NT, IT) \
-  hipExtLaunchKernelGGL((k_rows_mc<NT, IT>), grid, dim3(NT), lds, rs, e0, e1, 0, m)
-    if (id16) {
-      if (ctx->rows_mc_nt == 1024) KANO_ROWS_MC(1024, uint16_t);
-      else if (ctx->rows_mc_nt == 256) KANO_ROWS_MC(256, uint16_t);
-      else KANO_ROWS_MC(512, uint16_t);
-    } else {
-      if (ctx->rows_mc_nt == 1024) KANO_ROWS_MC(1024, int32_t);
-      else if (ctx->rows_mc_nt == 256) KANO_ROWS_MC(256, int32_t);
-      else KANO_ROWS_MC(512, int32_t);
-    }
-#undef KANO_ROWS_MC
-    KLAUNCH();
-    ctx->rows_kernel = 1;
-    ctx->rows_timed = true;
-    ctx->rows_time_pending = true;
-    return 0;
-  }
   if (ctx->wi_total == 0) return 0;
   if (ctx->heavy_count > 0) {
     hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(ctx->heavy_count, HEXP_CLS)),
@@ -1291,6 +1221,7 @@ int launch_rows(kano_ctx* ctx) {
   a.cww = cww;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
+  a.plain = ctx->rows_plain;
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
   const int nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   const size_t lds = sizeof(u64) * cww;
@@ -1648,8 +1579,7 @@ int kano_create(int device, kano_ctx** out) {
         const int v = atoi(kv.c_str() + eq + 1);
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
-        if (k == "rows") ctx->rows_from = v;
-        if (k == "rowsnt" && (v == 256 || v == 512 || v == 1024)) ctx->rows_mc_nt = v;
+        if (k == "store") ctx->rows_plain = v == 0;
         if (k == "cww" && v >= 16 && v <= MAX_CWW && v % 16 == 0) ctx->rows_cww = v;
         if (k == "async") ctx->async_rows = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
@@ -1736,7 +1666,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
-                  &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->cct};
+                  &ctx->irows,  &ctx->xw,      &ctx->xg};
   for (DBuf* b : bufs) dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);

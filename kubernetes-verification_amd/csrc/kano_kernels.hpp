@@ -1490,6 +1490,7 @@ struct RowsArgs {
   i64 n, W;
   int ch;
   int cww;
+  int plain;             // plain 16-byte stores (else non-temporal)
   u64* color;
   u64* colnand;
 };
@@ -1609,13 +1610,18 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   } else {
     build_light_row<NT>(a, c, base, nw, row);
   }
-  // non-temporal 16-byte stores (measured C3: 253 vs 263-270 us for plain
-  // stores on one box, 232 vs 246-258 on another)
+  // 16-byte stores, non-temporal unless a.plain (round 2 measured non-
+  // temporal 5-7 % faster on two boxes; box to box the order varies)
   for (int32_t m = m0; m < m1; ++m) {
     if (heavy && m == m_begin) continue;
     u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
-    for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-      __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
+    if (a.plain) {
+      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+        *(u64x2*)&dst[w] = *(const u64x2*)&row[w];
+    } else {
+      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+        __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
+    }
   }
   if (chunk == 0 && a.color) {
     for (int w = threadIdx.x; w < nw; w += NT) {

@@ -269,16 +269,12 @@ def _lists(cs, which):
 
 
 # --- matrix-write forms ------------------------------------------------------
-@pytest.mark.parametrize("tune", [
-    "", "rowsnt=256", "rowsnt=1024", "rows=1", "rows=1,cww=64", "rows=1,cww=16",
-    "async=0",
-])
+@pytest.mark.parametrize("tune", ["", "store=0", "cww=64", "cww=16", "async=0"])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
-    """The matrix write in address order from the class-level table
-    (k_rows_mc, every block size) and from the allowed-pod lists (k_rows,
-    which wide matrices take: column chunks forced at small n), with and
-    without asynchronous completion: against kano_py's matrix and lists."""
+    """The matrix write (k_rows) with non-temporal and plain stores, in the
+    column chunks wide matrices take (forced at small n), with and without
+    asynchronous completion: against kano_py's matrix and lists."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids, tables_from_cluster
     from kano.synth import make_config, objects_from_json
@@ -298,7 +294,7 @@ def test_rows_variants_forced(name, tune, monkeypatch):
     r = eng.verify(gid, sys_row=0, shadow=True)
     check_verify(r, exp)
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
-    assert eng.info()["ROWS_KERNEL"] == (2 if "rows=1" in tune else 1)
+    assert eng.info()["ROWS_KERNEL"] == 2
     eng.build()
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     eng.close()
