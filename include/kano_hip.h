@@ -359,13 +359,16 @@ int kano_build_classes(kano_ctx* ctx, int path);
 
 /* Host time of kano_verify (no reference counterpart; diagnostics for the
  * benchmark, always recorded: a few clock reads per call), microseconds:
- * out[12] = [calls, front sum, back sum, size-wait sum, gap between calls sum,
+ * out[20] = [calls, front sum, back sum, size-wait sum, gap between calls sum,
  *            front max, back max, size-wait max, call max,
- *            size wait 1 max, size wait 2 max, size wait 3 max];
+ *            size wait 1 max, size wait 2 max, size wait 3 max,
+ *            back's parts max: lists + matrix-write launch, policy_shadow's
+ *            emission launches, wait for the tail's copies, list copy issue,
+ *            pair copy issue, event records, 0, 0];
  * "front" is the build and checks up to the column words, "back" the result
  * lists, the matrix write's launch and the wait for the host results.
  * reset != 0 zeroes them after reading. */
-int kano_host_times(kano_ctx* ctx, double* out /* 12 */, int reset);
+int kano_host_times(kano_ctx* ctx, double* out /* 20 */, int reset);
 
 /* One process over G devices (SURVEY.md §8(b) kano_init(ngpu), §8(e) row
  * sharding; no reference counterpart: kano_py is single-process).  The group

@@ -185,8 +185,10 @@ struct kano_ctx {
   u64 sig_wait = 0;          // what mirror_wait polls for (0: the event)
   // kano_verify's host time per call (always on: a few clock reads), read by
   // kano_host_times: [calls, front sum, back sum, wait sum, gap sum,
-  // front max, back max, wait max, call max, size waits 1..3 max]
-  double ht[12] = {};
+  // front max, back max, wait max, call max, size waits 1..3 max, back's
+  // parts max: lists + matrix-write launch, policy_shadow's emission launches,
+  // tail wait, list copy, pair copy, event records]
+  double ht[20] = {};
   double ht_wait_cur = 0.0;
   int ht_wait = 0;
   std::chrono::steady_clock::time_point ht_last{};
@@ -508,6 +510,32 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 // (totals) or by a scan's publish list (atomic slots); the host records an
 // event behind them now (unless a scan raises the host signal), queues more
 // work, and later waits and reads the mirror -- no copy
+// A device -> host copy of the results: a kernel storing straight into the
+// caller's page-locked buffer when it is one (hipHostMalloc'd, e.g.
+// kano_host_alloc), else the runtime's copy
+int copy_out(kano_ctx* ctx, void* host, const void* dev, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return 0;
+  hipPointerAttribute_t at{};
+  void* dptr = nullptr;
+  if (hipPointerGetAttributes(&at, host) == hipSuccess && at.type == hipMemoryTypeHost &&
+      at.devicePointer)
+    dptr = at.devicePointer;
+  (void)hipGetLastError();
+  if (!dptr || (reinterpret_cast<uintptr_t>(dptr) & 15) || (reinterpret_cast<uintptr_t>(dev) & 15)) {
+    KCHK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+    return 0;
+  }
+  const i64 n16 = (i64)(bytes / 16);
+  const int ntail = (int)((bytes % 16) / 4);
+  const unsigned grid = (unsigned)std::max<i64>(1, std::min<i64>(1024, nblk(std::max<i64>(1, n16))));
+  hipLaunchKernelGGL(k_copy_out, dim3(grid), dim3(TPB), 0, st, static_cast<const uint4*>(dev),
+                     static_cast<uint4*>(dptr), n16,
+                     reinterpret_cast<const uint32_t*>(static_cast<const char*>(dev) + n16 * 16),
+                     reinterpret_cast<uint32_t*>(static_cast<char*>(dptr) + n16 * 16), ntail);
+  KLAUNCH();
+  return 0;
+}
+
 int mirror_begin(kano_ctx* ctx) {
   // the latest scan with host totals raises the host signal: nothing to queue
   if (ctx->sig_armed) {
@@ -2790,6 +2818,13 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // host's own sync event when there is one, else the marker recorded before
   // the matrix write
   constexpr int NS = SZ_ERR - SZ_NL + 1;
+  using clk = std::chrono::steady_clock;
+  auto tmark = clk::now();
+  auto part = [&](int k) {   // max host time of back's parts (kano_host_times)
+    const auto t = clk::now();
+    ctx->ht[k] = std::max(ctx->ht[k], std::chrono::duration<double, std::micro>(t - tmark).count());
+    tmark = t;
+  };
   const bool signalled = ctx->sig_armed != 0;
   KTRY(mirror_begin(ctx));
   hipEvent_t tail_ev = signalled ? nullptr : ctx->ev_sizes;
@@ -2801,8 +2836,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
     tail_ev = ctx->ev_sizes;
   }
+  part(12);
   i64 v[NS];
   KTRY(mirror_wait(ctx, SZ_NL, NS, v));
+  tmark = clk::now();
   if (ctx->vs_cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff)) {
     (void)sync(ctx);
     return fail(ctx, -EINVAL, "kano_verify: a group id lies outside [0, ngroups)");
@@ -2829,6 +2866,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     total = v[SZ_PAIRS - SZ_NL];
     if (shadow_cap >= 0) {
       KTRY(shadow_back(ctx, v[0], total, cs));
+      part(13);
       ctx->shadow_total = total;
     } else {
       // count only: every subset test ran (the flags and the per-pod counts
@@ -2837,11 +2875,12 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     }
     *shadow_count = total;
   }
-  if (nidx > 0)
-    KCHK(hipMemcpyAsync(idx, idx_dev, sizeof(int32_t) * nidx, hipMemcpyDeviceToHost, cs));
+  tmark = clk::now();
+  if (nidx > 0) KTRY(copy_out(ctx, idx, idx_dev, sizeof(int32_t) * nidx, cs));
+  part(15);
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
-    KCHK(hipMemcpyAsync(shadow_pairs, ctx->out.p, sizeof(int2) * total, hipMemcpyDeviceToHost,
-                        cs));
+    KTRY(copy_out(ctx, shadow_pairs, ctx->out.p, sizeof(int2) * total, cs));
+  part(16);
   // asynchronous completion: the host waits for the result copies only; the
   // matrix write ends on the engine stream
   const bool async = may_async && ctx->async_rows;
@@ -2850,12 +2889,16 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // follows the tail
   KCHK(hipEventRecord(ctx->ev_fork, cs));
   KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fork, 0));
+  part(17);
   if (async) {
     KCHK(hipEventSynchronize(ctx->ev_tail));
+    part(14);
     ctx->async_pending = true;
     return 0;
   }
-  return sync(ctx);
+  KTRY(sync(ctx));
+  part(14);
+  return 0;
 }
 }  // namespace
 
@@ -2895,7 +2938,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
 
 int kano_host_times(kano_ctx* ctx, double* out, int reset) {
   if (!ctx || !out) return -EINVAL;
-  for (int k = 0; k < 12; ++k) out[k] = ctx->ht[k];
+  for (int k = 0; k < 20; ++k) out[k] = ctx->ht[k];
   if (reset)
     for (double& v : ctx->ht) v = 0.0;
   return 0;

@@ -463,4 +463,16 @@ __device__ __forceinline__ uint32_t hfin(uint32_t h) {
   return h;
 }
 
+// Device -> host result copy as a kernel writing the caller's page-locked
+// host buffer directly (16 bytes per lane, a grid-stride loop): the
+// runtime's copy of a D2H range into the same buffer occasionally stalled the
+// host ~7 ms inside hipMemcpyAsync (kano_verify's tail, MI355X).
+__global__ __launch_bounds__(TPB) void k_copy_out(const uint4* __restrict__ src, uint4* dst,
+                                                 i64 n16, const uint32_t* __restrict__ src_tail,
+                                                 uint32_t* dst_tail, int ntail) {
+  const i64 stride = (i64)gridDim.x * TPB;
+  for (i64 k = (i64)blockIdx.x * TPB + threadIdx.x; k < n16; k += stride) dst[k] = src[k];
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dst_tail[threadIdx.x] = src_tail[threadIdx.x];
+}
+
 }  // namespace kano

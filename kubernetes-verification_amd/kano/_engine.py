@@ -557,11 +557,13 @@ class DeviceBuild:
     def host_times(self, reset: bool = False) -> dict:
         """kano_verify's host time by phase (us): sums and maxima since the
         last reset (kano_host_times)."""
-        out = np.zeros(12, dtype=np.float64)
+        out = np.zeros(20, dtype=np.float64)
         self._chk(self.lib.kano_host_times(self.ctx, _ptr(out), int(bool(reset))),
                   "kano_host_times")
         k = ("calls", "front_sum", "back_sum", "wait_sum", "gap_sum", "front_max", "back_max",
-             "wait_max", "call_max", "wait1_max", "wait2_max", "wait3_max")
+             "wait_max", "call_max", "wait1_max", "wait2_max", "wait3_max", "back_launch_max",
+             "back_emit_max", "back_tailwait_max", "back_copy_idx_max", "back_copy_pairs_max",
+             "back_events_max")
         return {name: float(v) for name, v in zip(k, out)}
 
     def stage_times(self) -> dict:
