@@ -68,6 +68,8 @@ def parse():
                          "auto = count for C4, pairs otherwise")
     ap.add_argument("--no-shadow", action="store_true", help="same as --shadow off")
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cold", type=int, default=1,
+                    help="also time the drop-in API once on fresh objects (C2 / C3, one rank)")
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: the N > 1 step (shard verify + RCCL all-gather + combine) "
                          "even at one rank, e.g. under torch.distributed.run --nproc-per-node 1")
@@ -150,6 +152,48 @@ class Step:
                 self.pairs_view = self.pin.view(np.int32, 2 * self.pin_pairs)
         self.results = res
         return res
+
+
+def cold_drop_in(cl, config):
+    """The drop-in call a kano_py user makes once, on fresh objects, timed end
+    to end (outside the bench's timed region; the process's GPU runtime is
+    already up): ReachabilityMatrix.build_matrix(containers, policies) --
+    interning, context, upload, build (kano_py/kano/model.py:125-165) -- then
+    the five checks' lists through kano.algorithm (algorithm.py:4-80)."""
+    from kano import model, algorithm as alg
+    from kano.synth import cluster_objects
+    t = time.perf_counter()
+    cs, ps = cluster_objects(cl, model)
+    t_objects = time.perf_counter() - t
+    sec = {}
+    t = time.perf_counter()
+    m = model.ReachabilityMatrix.build_matrix(cs, ps)
+    m.engine.info()                   # the build has run (kano_build syncs on its own)
+    sec["build_matrix"] = time.perf_counter() - t
+    t0 = time.perf_counter()
+    res = {}
+    for name, fn in (("all_reachable", lambda: alg.all_reachable(m)),
+                     ("all_isolated", lambda: alg.all_isolated(m)),
+                     ("user_crosscheck", lambda: alg.user_crosscheck(m, cs, "tenant")),
+                     ("system_isolation", lambda: alg.system_isolation(m, 0)),
+                     ("policy_shadow", lambda: alg.policy_shadow(m, ps, cs))):
+        t = time.perf_counter()
+        res[name] = fn()
+        sec[name] = time.perf_counter() - t
+    sec["checks_total"] = time.perf_counter() - t0
+    total = sec["build_matrix"] + sec["checks_total"]
+    pairs = np.array(res.pop("policy_shadow"), np.int32).reshape(-1, 2)
+    res = {k: np.asarray(v, np.int32) for k, v in res.items()}
+    res["policy_shadow"] = pairs
+    res["policy_shadow_count"] = int(pairs.shape[0])
+    verified, _ = verify_against_golden(config, cl, res, 1, 0, 0, "pairs")
+    m.engine.close()
+    return {"seconds": {k: round(v, 4) for k, v in sec.items()}, "total_s": round(total, 4),
+            "objects_s": round(t_objects, 3), "verified": verified,
+            "note": "build_matrix on fresh Container / Policy objects, then all_reachable, "
+                    "all_isolated, user_crosscheck(tenant), system_isolation(0), policy_shadow "
+                    "through the drop-in API (lists as Python objects); the GPU runtime is "
+                    "already initialised; objects_s (creating the objects) is not included"}
 
 
 def _cpu_lib():
@@ -416,6 +460,8 @@ def main():
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},
         }
+        if args.cold and world == 1 and args.rank_of <= 1 and n <= 200_000:
+            out["cold_drop_in"] = cold_drop_in(cl, args.config)
         ref = kano_py_measured(args.config)
         if ref:
             out["kano_py_measured"] = ref

@@ -16,7 +16,7 @@ import json
 d = json.loads(open("gpurun_out/b20.json").read().strip().splitlines()[-1])
 print("b20", d["ms_per_step"], d["step_ms"], d["roofline"]["kernel"], d["roofline"]["avg_launch_ms"], d["roofline"]["frac"], d.get("host_us"), d["verified"])
 PY
-for t in ${AB:-"" "rowsnt=256" "rowsnt=1024" "rows=1"}; do
+for t in ${AB:-"" "store=0"}; do
   KANO_TUNE="$t" timeout -k 10 200 python3 bench.py --steps 300 --warmup 20 --cpu-baseline 0 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail gpurun_out/ab.err; exit 1; }
   python3 - "$t" <<'PY'
 import json, sys

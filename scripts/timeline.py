@@ -7,7 +7,8 @@ import sys
 
 path = sys.argv[1]
 nk = int(sys.argv[2]) if len(sys.argv) > 2 else 48
-rows = list(csv.DictReader(open(path)))
+rows = [r for r in csv.DictReader(open(path)) if "elementwise" not in r["Kernel_Name"]
+        and "FillFunctor" not in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 last = rows[-nk:]
 t0 = int(last[0]["Start_Timestamp"])
