@@ -44,6 +44,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "pod-pairs/sec for reachability build + all-checks latency, 100k pods, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_I8_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md: int8 MFMA 2x the BF16 rate (~2.5 PF dense)
 WORKLOADS = {
     "C2": "Synthetic 10k pods / 1k policies, Zipf labels (BASELINE configs[1])",
     "C3": "Synthetic 100k pods / 10k policies, sparse selectors (BASELINE configs[2])",
@@ -360,6 +361,7 @@ def main():
     # (read once afterwards: kano_verify returns before its matrix write ends)
     eng.rows_timing(reset=True)
     eng.host_times(reset=True)
+    eng.mfma_timing(reset=True)
     step.verify_max_ms = 0.0
     # Python's cyclic GC off in the timed region (as timeit does): a full
     # collection over torch's objects took ~7 ms between two steps
@@ -386,6 +388,7 @@ def main():
     rt = eng.rows_timing()
     k_rows_ms = rt["sum_ms"] / rt["launches"] if rt["launches"] else float("nan")
     rows_kernel = {2: "k_rows"}.get(info["ROWS_KERNEL"], "none")
+    mt = eng.mfma_timing()
     host = eng.host_times()
     rows_local = r1 - r0
     W = (n + 63) // 64
@@ -441,6 +444,18 @@ def main():
                          "launches_timed": rt["launches"],
                          "min_launch_ms": rt["min_ms"], "max_launch_ms": rt["max_ms"],
                          "box_fill_gbs": box_fill},
+            # the dense path's int8 MFMA contraction (k_heavy_mc_mfma; --path
+            # mfma or AUTO's dense choice): algorithmic ops / its event time
+            "mfma_roofline": ({"bound": "mfma", "kernel": "k_heavy_mc_mfma",
+                               "achieved": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12,
+                               "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
+                               "frac": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12 /
+                                       MFMA_I8_PEAK_TOPS,
+                               "ops_per_build": mt["ops_last"],
+                               "avg_ms": mt["sum_ms"] / mt["builds"], "builds_timed": mt["builds"],
+                               "heavy_classes": info["HEAVY"], "column_classes": info["UA"],
+                               "policies": cl.P}
+                              if mt["builds"] > 0 and mt["sum_ms"] > 0 else None),
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),
                         "p90": round(float(np.percentile(step_ms, 90)), 4),

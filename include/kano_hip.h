@@ -249,6 +249,14 @@ int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
  * its timed region, kano_verify's own launches stay asynchronous). */
 int kano_rows_timing(kano_ctx* ctx, double* out /* 4 */, int reset);
 
+/* The heavy classes' int8 MFMA contraction (k_heavy_mc_mfma, the dense
+ * path of build_matrix, model.py:158-160 as Sel x Allow thresholded > 0)
+ * timed per build (HIP events around its launches on the context stream):
+ * out[4] = [sum ms, builds timed, sum of algorithmic int8 ops (2 x heavy row
+ * classes x policies x column classes per build), the last build's ops];
+ * reset != 0 zeroes the sums after reading. */
+int kano_mfma_timing(kano_ctx* ctx, double* out /* 4 */, int reset);
+
 /* Multi-hop reachability, replacing kubesv's
  * `path` relation (kubesv/kubesv/constraint.py:233-237: path :- edge;
  * path :- edge o edge) with kano's matrix as `edge`.  Writes into dst's matrix

@@ -217,6 +217,12 @@ struct kano_ctx {
   bool rows_time_pending = false;
   hipEvent_t rows_fork = nullptr;    // what the tail waits on (a marker before the write)
   hipEvent_t ev_rows_fork = nullptr;
+  // the heavy classes' int8 MFMA contraction (k_heavy_mc_mfma, every launch
+  // of a build between one pair of events), for kano_mfma_timing
+  hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;
+  bool mfma_time_pending = false;
+  double mfma_ops_last = 0.0, mfma_ops_sum = 0.0, mfma_ms_sum = 0.0;
+  i64 mfma_n = 0;
   float rows_ms_last = 0.f;
   double rows_ms_sum = 0.0, rows_ms_min = 0.0, rows_ms_max = 0.0;
   i64 rows_ms_n = 0;
@@ -494,6 +500,19 @@ int resolve_rows_time(kano_ctx* ctx) {
   if (ctx->rows_ms_n == 0 || ms > ctx->rows_ms_max) ctx->rows_ms_max = ms;
   ctx->rows_ms_sum += ms;
   ctx->rows_ms_n += 1;
+  return 0;
+}
+
+// the last build's MFMA contraction time, once its end event is complete
+int resolve_mfma_time(kano_ctx* ctx) {
+  if (!ctx->mfma_time_pending) return 0;
+  ctx->mfma_time_pending = false;
+  KCHK(hipEventSynchronize(ctx->ev_m1));
+  float ms = 0.f;
+  KCHK(hipEventElapsedTime(&ms, ctx->ev_m0, ctx->ev_m1));
+  ctx->mfma_ms_sum += ms;
+  ctx->mfma_ops_sum += ctx->mfma_ops_last;
+  ctx->mfma_n += 1;
   return 0;
 }
 
@@ -1157,6 +1176,8 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
           1, std::min<i64>((ctx->PB + MFMA_KMIN - 1) / MFMA_KMIN, 2048 / std::max<i64>(1, tiles)));
       const i64 kchunk = (ctx->PB + ksplit - 1) / ksplit;
       const unsigned gy = (unsigned)((ctx->PB + kchunk - 1) / kchunk);
+      KTRY(resolve_mfma_time(ctx));
+      KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
       for (i64 h0 = 0; h0 < H; h0 += HT_ROWS) {
         const int hh = (int)std::min<i64>(HT_ROWS, H - h0);
         const int32_t* hl = P_<int32_t>(ctx->hlist) + h0;
@@ -1172,6 +1193,11 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                              P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc, kchunk);
         KLAUNCH();
       }
+      KCHK(hipEventRecord(ctx->ev_m1, ctx->stream));
+      ctx->mfma_time_pending = true;
+      // algorithmic work: the heavy rows' boolean product over every policy,
+      // 2 ops (multiply, add) per (row class, policy, column class)
+      ctx->mfma_ops_last = 2.0 * (double)H * (double)P * (double)Ua;
     } else {
       hipLaunchKernelGGL(k_heavy_mc_or, dim3((unsigned)H, nblk(ldMc, 64)), dim3(TPB), 0, ctx->stream,
                          P_<int32_t>(ctx->hlist), P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
@@ -1630,7 +1656,8 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&ctx->ev_m0) != hipSuccess || hipEventCreate(&ctx->ev_m1) != hipSuccess) {
     kano_destroy(ctx);
     return -EIO;
   }
@@ -1702,7 +1729,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rows_fork, ctx->ev_sizes,
-                       ctx->ev_fork2, ctx->ev_join2})
+                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_m0, ctx->ev_m1})
     if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -3102,6 +3129,23 @@ int kano_stage_times(kano_ctx* ctx, float* ms) {
   }
   if (ctx->stage_timing && ctx->shadow_total >= 0)
     (void)hipEventElapsedTime(&ms[4], ctx->ev[5], ctx->ev[6]);
+  return 0;
+}
+
+int kano_mfma_timing(kano_ctx* ctx, double* out, int reset) {
+  if (!ctx || !out) return -EINVAL;
+  KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));
+  KTRY(sync(ctx));
+  KTRY(resolve_mfma_time(ctx));
+  out[0] = ctx->mfma_ms_sum;
+  out[1] = (double)ctx->mfma_n;
+  out[2] = ctx->mfma_ops_sum;
+  out[3] = ctx->mfma_ops_last;
+  if (reset) {
+    ctx->mfma_ms_sum = ctx->mfma_ops_sum = 0.0;
+    ctx->mfma_n = 0;
+  }
   return 0;
 }
 

@@ -554,6 +554,15 @@ class DeviceBuild:
         return dict(sum_ms=float(out[0]), launches=int(out[1]), min_ms=float(out[2]),
                     max_ms=float(out[3]))
 
+    def mfma_timing(self, reset: bool = False) -> dict:
+        """k_heavy_mc_mfma per build since the last reset: sum ms, builds,
+        algorithmic int8 ops (kano_mfma_timing)."""
+        out = np.zeros(4, dtype=np.float64)
+        self._chk(self.lib.kano_mfma_timing(self.ctx, _ptr(out), int(bool(reset))),
+                  "kano_mfma_timing")
+        return dict(sum_ms=float(out[0]), builds=int(out[1]), ops_sum=float(out[2]),
+                    ops_last=float(out[3]))
+
     def host_times(self, reset: bool = False) -> dict:
         """kano_verify's host time by phase (us): sums and maxima since the
         last reset (kano_host_times)."""
