@@ -475,12 +475,15 @@ def main():
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},
         }
-        if args.cold and world == 1 and args.rank_of <= 1 and n <= 200_000:
+        # (C2 / C3: kano_py's own policy_shadow list; C4's ~2.7e10 pairs fit no
+        # host list, C5's matrix no host memory)
+        if args.cold and world == 1 and args.rank_of <= 1 and n <= 200_000 and shadow == "pairs":
             out["cold_drop_in"] = cold_drop_in(cl, args.config)
         ref = kano_py_measured(args.config)
         if ref:
             out["kano_py_measured"] = ref
-        if args.cpu_baseline and world == 1 and args.rank_of <= 1 and n <= 200_000:
+        if (args.cpu_baseline and world == 1 and args.rank_of <= 1 and n <= 200_000
+                and shadow == "pairs"):
             out["cpu_baseline"] = cpu_baseline(cl, gid, args.config)
             out["cpu_baseline"]["cpu"] = _cpu_model()
         print(json.dumps(out), flush=True)
