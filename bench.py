@@ -514,14 +514,15 @@ def _list_ok(got, exp):
 
 
 def verify_against_golden(config, cl, res, world, rank, rank_of, shadow):
-    """True / False against kano_py's record of this exact cluster; None
-    when no such record exists (C5: out of kano_py's reach; its full-size
-    properties are tests/test_configs.py::test_c5_full_size_properties) or
-    the run is an emulated diagnostic."""
+    """True / False against the record of this exact cluster: kano_py's own
+    (C2-C4, tests/golden/make_golden.py), or for C5, out of kano_py's reach,
+    the indexed restatement's (tests/golden/make_c5.py, oracle/kano_indexed.py,
+    pinned on C2-C4 against kano_py); None when there is no record or the run
+    is an emulated diagnostic."""
     import hashlib
     exp, src = _golden(config)
     if exp is None:
-        return None, "no kano_py record for this config (C5: see tests/test_configs.py)"
+        return None, "no record for this config"
     if rank_of > 1:
         return None, "emulated shard step (other ranks' words are zero): not checked"
     if exp.get("seed", {}).get("fingerprint") != cl.fingerprint():
@@ -549,7 +550,8 @@ def verify_against_golden(config, cl, res, world, rank, rank_of, shadow):
         return False, f"{src}: {', '.join(bad)} differ"
     what = "lists" + (", policy_shadow " + ("pairs sha256" if shadow == "pairs" else "count")
                       if shadow != "off" and world == 1 else "")
-    return True, f"{src} (kano_py on the same seeded cluster): {what} equal"
+    who = exp.get("source", "kano_py on the same seeded cluster")
+    return True, f"{src} ({who}): {what} equal"
 
 
 def kano_py_measured(config):

@@ -9,6 +9,7 @@ the k_rows variants that only fire on wide matrices forced at small n.
 All of it goes through the C ABI: kano_verify (the bench's step), the matrix
 rows, the class-level lists expanded to Container.select_policies /
 allow_policies, and the policies' working sets."""
+import hashlib
 import os
 import sys
 
@@ -131,7 +132,10 @@ def _pack(bits):
 
 
 def test_c5_full_size_properties():
-    """C5 at full size on one GPU: (1) sampled rows -- the largest row
+    """C5 at full size on one GPU: (0) every check list, policy_shadow's
+    pairs (count + sha256) and the digest of all 10^6 rows equal C5's record
+    (tests/golden/make_c5.py: oracle/kano_indexed.py, pinned on C2-C4 against
+    kano_py, tests/test_oracle_indexed.py); (1) sampled rows -- the largest row
     classes' first members, row 0, the last row and random rows -- equal
     OR_{p: sel_p[i]} allow_p recomputed on the host from the tables
     (model.py:158-160); the device digest of each equals the host digest
@@ -152,6 +156,14 @@ def test_c5_full_size_properties():
     full = eng.verify("stored", sys_row=0, shadow=True)
     full = {k: (np.array(v, copy=True) if v is not None else None) for k, v in full.items()}
     dig = eng.rows_digest(0, n)
+    # (0) the independent record
+    exp = expected("C5")
+    assert exp["seed"]["fingerprint"] == cl.fingerprint()
+    check_verify(full, exp)
+    assert hashlib.sha256(np.ascontiguousarray(dig, dtype="<u8").tobytes()).hexdigest() == \
+        exp["row_digests_sha256"]
+    smp = exp["row_digest_sample"]
+    assert [f"{int(d):016x}" for d in dig[smp["rows"]]] == smp["digest"]
     # (1) sampled rows against the host restatement
     cls = eng.classes()
     big = np.argsort(-np.bincount(cls))[:24]

@@ -1,0 +1,71 @@
+"""Pin oracle/kano_indexed.py -- the restatement that produces C5's expected
+outputs (tests/golden/make_c5.py) -- against kano_py's own records of C2, C3
+and C4 (tests/golden/make_golden.py), then check that the committed C5 record
+belongs to the seeded C5 cluster."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+
+from _golden import expected, index_list_matches, row_digest  # noqa: E402
+from kano.synth import K_TENANT, make_config  # noqa: E402
+from oracle import kano_indexed as K  # noqa: E402
+
+
+@pytest.fixture(scope="module", params=["C2", "C3", "C4"])
+def pinned(request):
+    name = request.param
+    cl = make_config(name)
+    return name, cl, K.build_cluster(cl, label_key=K_TENANT), expected(name)
+
+
+def test_lists(pinned):
+    name, cl, ix, exp = pinned
+    RT = K.column_classes(ix)
+    assert index_list_matches(K.all_reachable(ix, RT), exp["all_reachable"])
+    assert index_list_matches(K.all_isolated(ix, RT), exp["all_isolated"])
+    assert index_list_matches(K.user_crosscheck(ix, RT), exp["user_crosscheck"]["result"])
+    assert index_list_matches(K.system_isolation(ix, 0), exp["system_isolation"]["result"])
+
+
+def test_policy_shadow(pinned):
+    name, cl, ix, exp = pinned
+    sh = exp["policy_shadow"]
+    cnt, digest = K.policy_shadow(ix, want_sha="sha256" in sh)
+    assert cnt == sh.get("count", sh.get("oracle_count"))
+    if "sha256" in sh:
+        assert digest == sh["sha256"]
+
+
+def test_sets_and_lists(pinned):
+    name, cl, ix, exp = pinned
+    if name != "C2":
+        pytest.skip("P x n set words: C2 keeps the CPU suite short")
+    assert K.set_words_sha(ix, ix.Sel) == exp["sel_sha256"]
+    assert K.set_words_sha(ix, ix.Alw) == exp["allow_sha256"]
+    assert K.lists_sha(ix, ix.Sel) == exp["select_policies_sha256"]
+    assert K.lists_sha(ix, ix.Alw) == exp["allow_policies_sha256"]
+
+
+def test_matrix_and_digests(pinned):
+    name, cl, ix, exp = pinned
+    if name == "C4":
+        pytest.skip("C2 and C3 cover the row layout")
+    assert K.matrix_sha(ix) == exp["M_sha256"]
+    dig = K.row_digests(ix)
+    rng = np.random.default_rng(1)
+    for i in np.unique(np.concatenate([[0, cl.n - 1], rng.integers(0, cl.n, 16)])):
+        assert row_digest(ix.row_words(int(i)))[0] == dig[i]
+
+
+def test_c5_record_matches_cluster():
+    exp = expected("C5")
+    cl = make_config("C5")
+    assert exp["seed"]["fingerprint"] == cl.fingerprint()
+    assert exp["n"] == cl.n and exp["P"] == cl.P
+    s = exp["row_digest_sample"]
+    assert len(s["rows"]) == len(s["digest"]) >= 500
