@@ -79,6 +79,14 @@ struct ClassSet {
 // One side of the policies (working selector or working allow): terms sorted
 // by class-key slot, the distinct slot sets ("masks") and, after matching,
 // each policy's class list pcls[pstart[p] .. + plen[p]).
+// What the matrix write reads (launch_rows: k_heavy_expand, k_rows) -- held
+// twice: back-to-back kano_verify calls build into one set while the previous
+// call's k_rows still reads the other (swap_rows_inputs)
+struct RowsInputs {
+  DBuf wioff, wicls, soffc, slist, aloff, alist, alcoff, alc, rmoff, rmem, cmoff, cmem, ccls,
+      hflag, hlist, Mc;
+};
+
 struct SideMatch {
   i64 nterms = 0;
   int NM = 0;                     // distinct masks (hash join); 0 with dense
@@ -133,6 +141,7 @@ struct kano_ctx {
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
+  int stream_prio = 1;       // prio=0: every stream at normal priority
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -200,9 +209,19 @@ struct kano_ctx {
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   bool fork_pending = false;
   std::function<int()> fork_hook;
-  // kano_verify's tail (result copies, policy_shadow's emission) beside the
-  // matrix write (normal priority: a high-priority tail slowed k_rows 10%)
+  // kano_verify's tail (result copies, policy_shadow's emission) runs on
+  // stream2 too (after the shadow tests' join), beside the matrix write,
+  // which has stream3 to itself (normal priority: a high-priority tail slowed
+  // k_rows 10%): the next kano_verify's build runs on the engine stream
+  // while the previous matrix write ends
   hipStream_t stream3 = nullptr;
+  RowsInputs rin_alt;        // the other set of k_rows' inputs
+  int rows_set = 0;          // which physical set the ctx fields hold
+  bool rows_overlap = false; // launch_rows: leave the engine stream free of the write
+  hipEvent_t rows_after = nullptr;   // launch_rows: the write also waits for this
+  hipEvent_t ev_rin = nullptr;          // k_rows' inputs complete (engine stream)
+  hipEvent_t ev_rows_end[2] = {};       // set k's matrix write done (stream3)
+  bool rows_end_rec[2] = {false, false};
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_sizes = nullptr;
   // asynchronous completion: kano_verify returns once its host results
@@ -211,12 +230,11 @@ struct kano_ctx {
   // every other entry point settles it first
   bool async_pending = false;
   hipEvent_t ev_tail = nullptr;    // the result copies of kano_verify's tail
-  // the matrix write's launch times (ev[7] -> ev[8], recorded by its own
-  // dispatch), resolved once the launch is known to be complete: the last
-  // one, and sums since kano_rows_timing's reset
-  bool rows_time_pending = false;
-  hipEvent_t rows_fork = nullptr;    // what the tail waits on (a marker before the write)
-  hipEvent_t ev_rows_fork = nullptr;
+  // the matrix write's launch times (ev_rt[set][0] -> [1], recorded by its
+  // own dispatch), resolved once the launch is known to be complete: the
+  // last one, and sums since kano_rows_timing's reset
+  hipEvent_t ev_rt[2][2] = {};
+  bool rows_time_pending[2] = {false, false};
   // the heavy classes' int8 MFMA contraction (k_heavy_mc_mfma, every launch
   // of a build between one pair of events), for kano_mfma_timing
   hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;
@@ -484,22 +502,62 @@ int settle(kano_ctx* ctx) {
   if (!ctx->async_pending) return 0;
   ctx->async_pending = false;
   KCHK(hipSetDevice(ctx->device));
+  KCHK(hipStreamSynchronize(ctx->stream3));
   return sync(ctx);
 }
 
-// the last k_rows launch's time, once its end event is complete (blocks
-// until it is)
-int resolve_rows_time(kano_ctx* ctx) {
-  if (!ctx->rows_time_pending) return 0;
-  ctx->rows_time_pending = false;
-  KCHK(hipEventSynchronize(ctx->ev[8]));
+// a k_rows launch's time, once its end event is complete (block: wait for
+// it; else leave it pending while the launch still runs)
+int resolve_rows_slot(kano_ctx* ctx, int k, bool block) {
+  if (!ctx->rows_time_pending[k]) return 0;
+  if (!block) {
+    const hipError_t q = hipEventQuery(ctx->ev_rt[k][1]);
+    if (q == hipErrorNotReady) return 0;
+    KCHK(q);
+  }
+  ctx->rows_time_pending[k] = false;
+  KCHK(hipEventSynchronize(ctx->ev_rt[k][1]));
   float ms = 0.f;
-  KCHK(hipEventElapsedTime(&ms, ctx->ev[7], ctx->ev[8]));
+  KCHK(hipEventElapsedTime(&ms, ctx->ev_rt[k][0], ctx->ev_rt[k][1]));
   ctx->rows_ms_last = ms;
   if (ctx->rows_ms_n == 0 || ms < ctx->rows_ms_min) ctx->rows_ms_min = ms;
   if (ctx->rows_ms_n == 0 || ms > ctx->rows_ms_max) ctx->rows_ms_max = ms;
   ctx->rows_ms_sum += ms;
   ctx->rows_ms_n += 1;
+  return 0;
+}
+
+int resolve_rows_time(kano_ctx* ctx, bool block = true) {
+  for (int k = 0; k < 2; ++k) KTRY(resolve_rows_slot(ctx, k, block));
+  return 0;
+}
+
+// Back-to-back kano_verify: the previous call's matrix write may still read
+// its inputs; this build takes the other set (written once the write two
+// calls back, which last read it, has ended -- an event wait on the engine
+// stream, not on the host)
+int swap_rows_inputs(kano_ctx* ctx) {
+  RowsInputs& a = ctx->rin_alt;
+  std::swap(ctx->wioff, a.wioff);
+  std::swap(ctx->wicls, a.wicls);
+  std::swap(ctx->soffc, a.soffc);
+  std::swap(ctx->slist, a.slist);
+  std::swap(ctx->aloff, a.aloff);
+  std::swap(ctx->alist, a.alist);
+  std::swap(ctx->alcoff, a.alcoff);
+  std::swap(ctx->alc, a.alc);
+  std::swap(ctx->rc.moff, a.rmoff);
+  std::swap(ctx->rc.mem, a.rmem);
+  std::swap(ctx->cc.moff, a.cmoff);
+  std::swap(ctx->cc.mem, a.cmem);
+  std::swap(ctx->cc.cls, a.ccls);
+  std::swap(ctx->hflag, a.hflag);
+  std::swap(ctx->hlist, a.hlist);
+  std::swap(ctx->Mc, a.Mc);
+  ctx->rows_set ^= 1;
+  ctx->alist_valid = false;
+  if (ctx->rows_end_rec[ctx->rows_set])
+    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows_end[ctx->rows_set], 0));
   return 0;
 }
 
@@ -883,9 +941,9 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(classify_phase2a(ctx));
   i64 u[2] = {0, 0};
   KTRY(mirror_wait(ctx, SZ_UR, 2, u));
-  // the previous matrix write ended before this build's first scan: its
-  // time is read here, off the host's path to the next k_rows launch
-  KTRY(resolve_rows_time(ctx));
+  // an earlier matrix write's time, when it has ended (no wait: the
+  // previous kano_verify's write may still run beside this build)
+  KTRY(resolve_rows_time(ctx, false));
   ctx->rc.U = u[0];
   ctx->cc.U = u[1];
   KTRY(stage_mark(ctx, 1, ctx->stream));
@@ -1225,21 +1283,27 @@ int do_rows(kano_ctx* ctx) {
 }
 
 // The matrix write, timed by its own dispatch (hipExtLaunchKernelGGL's start
-// / stop events ev[7] -> ev[8]: no marker packets around it; the bench's
+// / stop events ev_rt[set]: no marker packets around it; the bench's
 // roofline reads them through kano_rows_timing): heavy rows expanded from
 // Mc first, then every light class row rebuilt from the allowed-pod lists
-// in LDS and streamed to its members (k_rows).
+// in LDS and streamed to its members (k_rows).  It runs on stream3 behind
+// the engine stream's marker ev_rin; unless rows_overlap (kano_verify's
+// asynchronous completion) the engine stream then waits for it.
 int launch_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
   ctx->rows_kernel = 0;
   if (rl == 0 || W == 0) return 0;
-  hipStream_t rs = ctx->stream;
-  KTRY(resolve_rows_time(ctx));   // the previous launch's pair is reused
-  ctx->rows_fork = ctx->ev_rows_fork;
-  KCHK(hipEventRecord(ctx->rows_fork, rs));
-  hipEvent_t e0 = ctx->ev[7], e1 = ctx->ev[8];
+  hipStream_t rs = ctx->stream3;
+  const int set = ctx->rows_set;
+  // this set's pair was last used two writes back (ended: the engine stream
+  // waited for it before this build wrote the set)
+  KTRY(resolve_rows_slot(ctx, set, true));
+  KCHK(hipEventRecord(ctx->ev_rin, ctx->stream));
   if (ctx->wi_total == 0) return 0;
+  KCHK(hipStreamWaitEvent(rs, ctx->ev_rin, 0));
+  if (ctx->rows_after) KCHK(hipStreamWaitEvent(rs, ctx->rows_after, 0));
+  hipEvent_t e0 = ctx->ev_rt[set][0], e1 = ctx->ev_rt[set][1];
   if (ctx->heavy_count > 0) {
     hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(ctx->heavy_count, HEXP_CLS)),
                        dim3(TPB), 0, rs, P_<int32_t>(ctx->hlist), (i64)ctx->heavy_count,
@@ -1286,7 +1350,10 @@ int launch_rows(kano_ctx* ctx) {
   KLAUNCH();
   ctx->rows_kernel = 2;
   ctx->rows_timed = true;
-  ctx->rows_time_pending = true;
+  ctx->rows_time_pending[set] = true;
+  KCHK(hipEventRecord(ctx->ev_rows_end[set], rs));
+  ctx->rows_end_rec[set] = true;
+  if (!ctx->rows_overlap) KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows_end[set], 0));
   return 0;
 }
 
@@ -1612,12 +1679,6 @@ int kano_create(int device, kano_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return -EIO;
   kano_ctx* ctx = new kano_ctx();
   ctx->device = device;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return -EIO;
-  }
-  ctx->own_stream = true;
-  for (auto& e : ctx->ev) (void)hipEventCreate(&e);
   // test hooks (KANO_TUNE="key=value,..."): forms that compute the same
   // results, forced for the parity tests (see kano_ctx)
   if (const char* t = getenv("KANO_TUNE")) {
@@ -1641,23 +1702,40 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathtm" && (v == 1 || v == 2 || v == 4)) ctx->path_tm = v;
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
+        if (k == "prio") ctx->stream_prio = v;
       }
       pos = end + 1;
     }
   }
+  // the engine stream and stream2 at the device's greatest priority: a
+  // build's short kernels take the CUs first that the previous call's matrix
+  // write (stream3, normal priority) frees
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  const int prio_main = ctx->stream_prio ? prio_hi : prio_lo;
+  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_main) != hipSuccess) {
+    delete ctx;
+    return -EIO;
+  }
+  ctx->own_stream = true;
+  for (auto& e : ctx->ev) (void)hipEventCreate(&e);
   if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
     ctx->stream3 = nullptr;
     kano_destroy(ctx);
     return -EIO;
   }
-  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+  if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_rows_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rin, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreate(&ctx->ev_m0) != hipSuccess || hipEventCreate(&ctx->ev_m1) != hipSuccess) {
+      hipEventCreate(&ctx->ev_m0) != hipSuccess || hipEventCreate(&ctx->ev_m1) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rows_end[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rows_end[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&ctx->ev_rt[0][0]) != hipSuccess || hipEventCreate(&ctx->ev_rt[0][1]) != hipSuccess ||
+      hipEventCreate(&ctx->ev_rt[1][0]) != hipSuccess || hipEventCreate(&ctx->ev_rt[1][1]) != hipSuccess) {
     kano_destroy(ctx);
     return -EIO;
   }
@@ -1723,13 +1801,20 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
                   &ctx->irows,  &ctx->xw,      &ctx->xg};
   for (DBuf* b : bufs) dfree(*b);
+  RowsInputs& ra = ctx->rin_alt;
+  for (DBuf* b : {&ra.wioff, &ra.wicls, &ra.soffc, &ra.slist, &ra.aloff, &ra.alist, &ra.alcoff,
+                  &ra.alc, &ra.rmoff, &ra.rmem, &ra.cmoff, &ra.cmem, &ra.ccls, &ra.hflag,
+                  &ra.hlist, &ra.Mc})
+    dfree(*b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
-  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rows_fork, ctx->ev_sizes,
-                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_m0, ctx->ev_m1})
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_sizes,
+                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
+                       ctx->ev_rows_end[1], ctx->ev_rt[0][0], ctx->ev_rt[0][1], ctx->ev_rt[1][0],
+                       ctx->ev_rt[1][1]})
     if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
@@ -2663,6 +2748,9 @@ RcclAllGather rccl_all_gather() {
 int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, int64_t sys_row,
                  bool want_shadow, u64* words_dev, bool count_only = false) {
   ctx->vs_count_only = want_shadow && count_only;
+  // the previous call's matrix write may still run: build into the other
+  // input set instead of waiting for it
+  if (ctx->async_pending) KTRY(swap_rows_inputs(ctx));
   const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
   const bool want_cross = gid || stored;
   // the crosscheck and policy_shadow buffers are filled in the build's last
@@ -2839,11 +2927,12 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KLAUNCH();
   }
   // the list sizes, policy_shadow's sizes and the group check travel to the
-  // host while the matrix write runs: the host waits on the signal (or the
-  // event) only, then queues policy_shadow's emission and the copies beside
-  // k_rows on stream3.  The tail waits for everything queued so far: the
-  // host's own sync event when there is one, else the marker recorded before
-  // the matrix write
+  // host: it waits on the signal (or the event) only, then queues the tail
+  // (policy_shadow's compaction and emission, the copies) on stream2 and the
+  // matrix write behind the tail on stream3.  The tail runs on a quiet
+  // device (beside a matrix write its short latency-bound kernels took ~3x
+  // longer); the write then overlaps the host's return and, under
+  // asynchronous completion, the next call's build
   constexpr int NS = SZ_ERR - SZ_NL + 1;
   using clk = std::chrono::steady_clock;
   auto tmark = clk::now();
@@ -2855,10 +2944,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   const bool signalled = ctx->sig_armed != 0;
   KTRY(mirror_begin(ctx));
   hipEvent_t tail_ev = signalled ? nullptr : ctx->ev_sizes;
-  if (ctx->vs_rows) {
-    KTRY(launch_rows(ctx));
-    if (!tail_ev && ctx->rows_kernel) tail_ev = ctx->rows_fork;
-  }
+  const bool async = may_async && ctx->async_rows;
   if (!tail_ev) {
     KCHK(hipEventRecord(ctx->ev_sizes, ctx->stream));
     tail_ev = ctx->ev_sizes;
@@ -2877,11 +2963,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     nidx += counts[r];
   }
   if (!ctx->vs_have_sys) counts[3] = -1;
-  // everything the matrix write does not touch runs beside it on stream3:
-  // policy_shadow's compaction and emission, the list and pair copies (the
-  // copies are blit kernels that crawl beside k_rows: the short shadow
-  // kernels go first so that they do not queue behind them)
-  hipStream_t cs = ctx->stream3;
+  // the tail on stream2 (the shadow tests there have joined the engine
+  // stream already): policy_shadow's compaction and emission, the list and
+  // pair copies
+  hipStream_t cs = ctx->stream2;
   KCHK(hipStreamWaitEvent(cs, tail_ev, 0));
   i64 total = 0;
   if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
@@ -2909,9 +2994,17 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KTRY(copy_out(ctx, shadow_pairs, ctx->out.p, sizeof(int2) * total, cs));
   part(16);
   // asynchronous completion: the host waits for the result copies only; the
-  // matrix write ends on the engine stream
-  const bool async = may_async && ctx->async_rows;
-  if (async) KCHK(hipEventRecord(ctx->ev_tail, cs));
+  // matrix write ends on stream3 (settle, or the next kano_verify's build
+  // beside it on the other input set)
+  KCHK(hipEventRecord(ctx->ev_tail, cs));
+  if (ctx->vs_rows) {
+    ctx->rows_overlap = async;
+    ctx->rows_after = ctx->ev_tail;
+    const int rc = launch_rows(ctx);
+    ctx->rows_overlap = false;
+    ctx->rows_after = nullptr;
+    KTRY(rc);
+  }
   // later work on the main stream (a fetch of the pairs, the next build)
   // follows the tail
   KCHK(hipEventRecord(ctx->ev_fork, cs));
