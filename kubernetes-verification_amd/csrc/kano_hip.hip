@@ -142,6 +142,7 @@ struct kano_ctx {
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
   int stream_prio = 1;       // prio=0: every stream at normal priority
+  int rows_cu_off = 0;       // rcu=K: the matrix write's stream leaves K CUs per XCD free
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -590,6 +591,18 @@ int read_slots(kano_ctx* ctx, int first, int count, i64* out) {
 // A device -> host copy of the results: a kernel storing straight into the
 // caller's page-locked buffer when it is one (hipHostMalloc'd, e.g.
 // kano_host_alloc), else the runtime's copy
+// the device address of a page-locked host buffer (16-byte aligned), else null
+void* pinned_dev(void* host) {
+  if (!host || (reinterpret_cast<uintptr_t>(host) & 15)) return nullptr;
+  hipPointerAttribute_t at{};
+  void* dptr = nullptr;
+  if (hipPointerGetAttributes(&at, host) == hipSuccess && at.type == hipMemoryTypeHost &&
+      at.devicePointer)
+    dptr = at.devicePointer;
+  (void)hipGetLastError();
+  return dptr;
+}
+
 int copy_out(kano_ctx* ctx, void* host, const void* dev, size_t bytes, hipStream_t st) {
   if (bytes == 0) return 0;
   hipPointerAttribute_t at{};
@@ -1703,6 +1716,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
         if (k == "prio") ctx->stream_prio = v;
+        if (k == "rcu" && (v == 0 || v == 1 || v == 2 || v == 4)) ctx->rows_cu_off = v;
       }
       pos = end + 1;
     }
@@ -1719,7 +1733,23 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
+  hipError_t e3;
+  if (ctx->rows_cu_off > 0) {
+    // bit i off when i % 8 == (i / 32) % 8 (and, for fewer, i % 32 < 8 * K / 4...):
+    // K CUs of every XCD whether CUs are numbered XCD-major or round-robin
+    uint32_t mask[8];
+    for (int w = 0; w < 8; ++w) {
+      mask[w] = 0xffffffffu;
+      for (int b = 0; b < 32; ++b) {
+        const int i = w * 32 + b;
+        if (i % 8 == (i / 32) % 8 && (i % 32) < 8 * ctx->rows_cu_off) mask[w] &= ~(1u << b);
+      }
+    }
+    e3 = hipExtStreamCreateWithCUMask(&ctx->stream3, 8, mask);
+  } else {
+    e3 = hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking);
+  }
+  if (e3 != hipSuccess) {
     ctx->stream3 = nullptr;
     kano_destroy(ctx);
     return -EIO;
@@ -2573,13 +2603,14 @@ int shadow_back(kano_ctx* ctx, i64 nl, i64 total, hipStream_t st = nullptr) {
   if (nt > 0 && nl > 0) {
     hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)nt), dim3(TPB), 0, st,
                        P_<i64>(ctx->soffc), U, P_<int32_t>(ctx->slist), P_<i64>(ctx->pfoff),
-                       P_<uint8_t>(ctx->flags), nf, P_<i64>(ctx->toff), P_<int2>(ctx->L));
+                       P_<uint8_t>(ctx->flags), nf, P_<i64>(ctx->toff), P_<int2>(ctx->L), nl);
     KLAUNCH();
   }
   if (rl > 0 && total > 0) {
     hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
                        P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
-                       P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out));
+                       P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out), total,
+                       (const i64*)nullptr, nl);
     KLAUNCH();
   }
   KTRY(stage_mark(ctx, 6, st));
@@ -2882,6 +2913,120 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   return 0;
 }
 
+// spin on an event (the syncs' waits are tens of microseconds: no sleep)
+int spin_event(kano_ctx* ctx, hipEvent_t e) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (uint32_t spin = 1;; ++spin) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) KCHK(q);
+    __builtin_ia32_pause();
+    if ((spin & 0xff) == 0 && clk::now() - t0 > std::chrono::seconds(1)) {
+      KCHK(hipEventSynchronize(e));
+      return 0;
+    }
+  }
+}
+
+int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts,
+                       int32_t* shadow_pairs, void* pairs_h, int64_t shadow_cap,
+                       int64_t* shadow_count, bool async) {
+  using clk = std::chrono::steady_clock;
+  auto tmark = clk::now();
+  auto part = [&](int k) {
+    const auto t = clk::now();
+    ctx->ht[k] = std::max(ctx->ht[k], std::chrono::duration<double, std::micro>(t - tmark).count());
+    tmark = t;
+  };
+  const i64 n = ctx->n, rl = ctx->vs_rl;
+  const bool want_shadow = ctx->vs_shadow;
+  const bool pairs_mode = want_shadow && shadow_cap >= 0;
+  hipStream_t st = ctx->stream;
+  const i64 nf = ctx->nflags, nt = (nf + SH_TILE - 1) / SH_TILE;
+  i64 out_cap = 0;
+  if (pairs_mode) {
+    // L never exceeds the candidate pairs; out keeps the largest total seen
+    KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nf)));
+    KTRY(dalloc(ctx, ctx->out, sizeof(int2) * 1024));
+    out_cap = (i64)(ctx->out.bytes / sizeof(int2));
+    if (nt > 0) {
+      hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)nt), dim3(TPB), 0, st,
+                         P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
+                         P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), nf, P_<i64>(ctx->toff),
+                         P_<int2>(ctx->L), nf);
+      KLAUNCH();
+    }
+    if (rl > 0) {
+      hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
+                         P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
+                         P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out), out_cap,
+                         nt > 0 ? P_<i64>(ctx->toff) + nt : (const i64*)nullptr, nf);
+      KLAUNCH();
+    }
+  }
+  CopyJobs cj{};
+  cj.j[0] = CopyJob{static_cast<const char*>(ctx->idxd.p), static_cast<char*>(idx_h),
+                    P_<u64>(ctx->sizes) + SZ_IDX0, 4, 4, 4 * n};
+  int njobs = 1;
+  if (pairs_mode && pairs_h && rl > 0) {
+    cj.j[1] = CopyJob{static_cast<const char*>(ctx->out.p), static_cast<char*>(pairs_h),
+                      reinterpret_cast<const u64*>(P_<i64>(ctx->poff) + rl), 1, 8,
+                      std::min<i64>(shadow_cap, out_cap)};
+    njobs = 2;
+  }
+  hipLaunchKernelGGL(k_copy_out_dev, dim3(256, njobs), dim3(TPB), 0, st, cj);
+  KLAUNCH();
+  KCHK(hipEventRecord(ctx->ev_tail, st));
+  if (ctx->vs_rows) {
+    ctx->rows_overlap = async;
+    const int rc = launch_rows(ctx);
+    ctx->rows_overlap = false;
+    KTRY(rc);
+  }
+  part(12);
+  KTRY(spin_event(ctx, ctx->ev_tail));
+  part(14);
+  ctx->sig_wait = 0;
+  constexpr int NS = SZ_ERR - SZ_NL + 1;
+  i64 v[NS];
+  for (int q = 0; q < NS; ++q) v[q] = (i64)((volatile u64*)ctx->gmirror)[SZ_NL + q];
+  if (ctx->vs_cross_on && (v[SZ_ERR - SZ_NL] & 0xffffffff)) {
+    (void)settle(ctx);
+    (void)sync(ctx);
+    return fail(ctx, -EINVAL, "kano_verify: a group id lies outside [0, ngroups)");
+  }
+  for (int r = 0; r < 4; ++r) counts[r] = v[SZ_IDX0 - SZ_NL + r];
+  if (!ctx->vs_have_sys) counts[3] = -1;
+  if (want_shadow) {
+    const i64 total = v[SZ_PAIRS - SZ_NL];
+    *shadow_count = total;
+    ctx->shadow_total = pairs_mode ? total : -1;
+    if (pairs_mode && total > out_cap) {
+      // past the emission buffer: the sized emission, then the copy
+      KTRY(dalloc(ctx, ctx->out, sizeof(int2) * (total + total / 4)));
+      if (rl > 0) {
+        hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
+                           P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
+                           P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out), total,
+                           (const i64*)nullptr, nf);
+        KLAUNCH();
+      }
+      if (shadow_pairs && total <= shadow_cap)
+        KTRY(copy_out(ctx, shadow_pairs, ctx->out.p, sizeof(int2) * total, st));
+      KCHK(hipEventRecord(ctx->ev_tail, st));
+      KCHK(hipEventSynchronize(ctx->ev_tail));
+    }
+  }
+  part(15);
+  if (async) {
+    ctx->async_pending = true;
+    return 0;
+  }
+  KTRY(sync(ctx));
+  return 0;
+}
+
 int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx, int64_t* counts,
                 int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count,
                 bool may_async = false) {
@@ -2926,6 +3071,24 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
                        P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
     KLAUNCH();
   }
+  const bool pairs_mode = want_shadow && shadow_cap >= 0;
+  if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
+    (void)sync(ctx);
+    return fail(ctx, -EINVAL, "kano_verify_combine: the shard ran policy_shadow count-only "
+                              "(with_shadow = 2); pass shadow_cap < 0");
+  }
+  // Page-locked result buffers (kano_host_alloc): the whole tail is queued
+  // at once on the engine stream, sized on the device -- policy_shadow's
+  // compaction and emission into buffers sized from the subset-test count and
+  // the last call, the copies of scan-total length -- and the host waits
+  // once, for the results; no host round trip between the scans and the
+  // tail.  A total past a buffer's capacity leaves that step undone and the
+  // host redoes it sized (first call, or a larger output).
+  void* idx_h = n > 0 ? pinned_dev(idx) : nullptr;
+  void* pairs_h = pairs_mode && shadow_pairs ? pinned_dev(shadow_pairs) : nullptr;
+  if (n > 0 && W > 0 && idx_h && (!pairs_mode || !shadow_pairs || pairs_h))
+    return verify_back_direct(ctx, idx, idx_h, counts, shadow_pairs, pairs_h, shadow_cap,
+                              shadow_count, may_async && ctx->async_rows);
   // the list sizes, policy_shadow's sizes and the group check travel to the
   // host: it waits on the signal (or the event) only, then queues the tail
   // (policy_shadow's compaction and emission, the copies) on stream2 and the
@@ -2969,11 +3132,6 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   hipStream_t cs = ctx->stream2;
   KCHK(hipStreamWaitEvent(cs, tail_ev, 0));
   i64 total = 0;
-  if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
-    (void)sync(ctx);
-    return fail(ctx, -EINVAL, "kano_verify_combine: the shard ran policy_shadow count-only "
-                              "(with_shadow = 2); pass shadow_cap < 0");
-  }
   if (want_shadow) {
     total = v[SZ_PAIRS - SZ_NL];
     if (shadow_cap >= 0) {

@@ -2222,9 +2222,12 @@ __global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ 
                                                         const uint8_t* __restrict__ flags,
                                                         i64 nflags,
                                                         const i64* __restrict__ tile_off,
-                                                        int2* __restrict__ L) {
+                                                        int2* __restrict__ L, i64 L_cap) {
   __shared__ i64 sm[4];
   __shared__ i64 rng[2];
+  // (sized before the list length is known: past L_cap nothing is written,
+  // the host sees the total and runs the sized launch)
+  if (tile_off[gridDim.x] > L_cap) return;        // grid-uniform
   tile_class_range(pfoff, U, nflags, rng);
   const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
   u64 packed = 0;
@@ -2268,9 +2271,11 @@ __global__ __launch_bounds__(TPB) void k_shadow_emit(const int32_t* __restrict__
                                                      i64 r1, const i64* __restrict__ loff,
                                                      const int2* __restrict__ L,
                                                      const i64* __restrict__ poff,
-                                                     int2* __restrict__ out) {
+                                                     int2* __restrict__ out, i64 out_cap,
+                                                     const i64* __restrict__ L_total, i64 L_cap) {
   const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
   if (i >= r1) return;
+  if (poff[r1 - r0] > out_cap || (L_total && *L_total > L_cap)) return;   // as k_shadow_compact
   const int32_t c = cls[i];
   const i64 l0 = loff[c], len = loff[c + 1] - l0;
   const i64 o = poff[i - r0];

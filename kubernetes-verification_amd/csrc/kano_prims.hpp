@@ -475,4 +475,35 @@ __global__ __launch_bounds__(TPB) void k_copy_out(const uint4* __restrict__ src,
   if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dst_tail[threadIdx.x] = src_tail[threadIdx.x];
 }
 
+// The same copy sized on the device: up to two jobs (blockIdx.y), each of
+// sum(cnt[0..ncnt)) elements of esize bytes (a scan total, no host round
+// trip); a job past its capacity copies nothing (the host sees the count and
+// takes the sized path).
+struct CopyJob {
+  const char* src;
+  char* dst;
+  const u64* cnt;
+  int ncnt;
+  int esize;
+  i64 cap;
+};
+struct CopyJobs {
+  CopyJob j[2];
+};
+__global__ __launch_bounds__(TPB) void k_copy_out_dev(CopyJobs jobs) {
+  const CopyJob a = jobs.j[blockIdx.y];
+  i64 cnt = 0;
+  for (int q = 0; q < a.ncnt; ++q) cnt += (i64)a.cnt[q];
+  if (cnt > a.cap) return;                          // block-uniform
+  const i64 bytes = cnt * a.esize, n16 = bytes >> 4;
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.src);
+  uint4* dst = reinterpret_cast<uint4*>(a.dst);
+  const i64 stride = (i64)gridDim.x * TPB;
+  for (i64 k = (i64)blockIdx.x * TPB + threadIdx.x; k < n16; k += stride) dst[k] = src[k];
+  const int ntail = (int)((bytes & 15) >> 2);
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail)
+    reinterpret_cast<uint32_t*>(a.dst + n16 * 16)[threadIdx.x] =
+        reinterpret_cast<const uint32_t*>(a.src + n16 * 16)[threadIdx.x];
+}
+
 }  // namespace kano
