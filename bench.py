@@ -443,7 +443,11 @@ def main():
                          "avg_launch_ms": k_rows_ms,
                          "launches_timed": rt["launches"],
                          "min_launch_ms": rt["min_ms"], "max_launch_ms": rt["max_ms"],
-                         "box_fill_gbs": box_fill},
+                         "box_fill_gbs": box_fill,
+                         # the write runs beside the next step's build on a
+                         # CU-masked stream when it is short enough to overlap
+                         # it ("Pipelined steps")
+                         "cus": info["ROWS_CUS"]},
             # the dense path's int8 MFMA contraction (k_heavy_mc_mfma; --path
             # mfma or AUTO's dense choice): algorithmic ops / its event time
             "mfma_roofline": ({"bound": "mfma", "kernel": "k_heavy_mc_mfma",

@@ -58,7 +58,8 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 int8 MFMA          */
 #define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the list-based row kernel */
 #define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 2 k_rows, 0 none yet */
-#define KANO_INFO_NSLOTS   14
+#define KANO_INFO_ROWS_CUS 14   /* CUs the last matrix write's stream may use  */
+#define KANO_INFO_NSLOTS   15
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in
  * Python objects (kano_py/kano/model.py:167-169 ReachabilityMatrix.__init__). */

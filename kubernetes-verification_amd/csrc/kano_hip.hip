@@ -142,7 +142,16 @@ struct kano_ctx {
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
   int stream_prio = 1;       // prio=0: every stream at normal priority
-  int rows_cu_off = 0;       // rcu=K: the matrix write's stream leaves K CUs per XCD free
+  // The matrix write shares the device with the next kano_verify's build
+  // (asynchronous completion): a write that saturates HBM starves the
+  // build's latency-bound kernels (fill 6 -> 62-107 us, class insert 25 ->
+  // 50-63 us beside it).  A write of at most rows_cu_bytes therefore runs on
+  // a CU-masked stream that leaves rows_cu_off CUs per XCD to the build
+  // (C3: 96 of 256 CUs, k_rows 0.26 -> 0.35 ms, step 0.52 -> 0.43 ms); a
+  // larger write, which outlasts any build (C5: 125 GB), takes every CU.
+  int rows_cu_off = 20;      // rcu=K (0: no masked stream)
+  i64 rows_cu_bytes = 8ll << 30;   // rcubytes=G (GiB)
+  int num_cus = 0, rows_cus = 0;   // the device's CUs; those of the last write's stream
 
   ClassSet rc, cc;           // row classes (selector keys), column classes (allow keys)
   SideMatch sm, am;          // selector side, allow side
@@ -216,6 +225,8 @@ struct kano_ctx {
   // k_rows 10%): the next kano_verify's build runs on the engine stream
   // while the previous matrix write ends
   hipStream_t stream3 = nullptr;
+  hipStream_t stream3m = nullptr;    // CU-masked (rows_cu_off), for writes <= rows_cu_bytes
+  hipStream_t rows_last = nullptr;   // the stream of the last matrix write
   RowsInputs rin_alt;        // the other set of k_rows' inputs
   int rows_set = 0;          // which physical set the ctx fields hold
   bool rows_overlap = false; // launch_rows: leave the engine stream free of the write
@@ -504,6 +515,7 @@ int settle(kano_ctx* ctx) {
   ctx->async_pending = false;
   KCHK(hipSetDevice(ctx->device));
   KCHK(hipStreamSynchronize(ctx->stream3));
+  if (ctx->stream3m) KCHK(hipStreamSynchronize(ctx->stream3m));
   return sync(ctx);
 }
 
@@ -1307,7 +1319,10 @@ int launch_rows(kano_ctx* ctx) {
   const i64 rl = rows_local(ctx);
   ctx->rows_kernel = 0;
   if (rl == 0 || W == 0) return 0;
-  hipStream_t rs = ctx->stream3;
+  const bool masked =
+      ctx->stream3m && (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
+  hipStream_t rs = masked ? ctx->stream3m : ctx->stream3;
+  ctx->rows_cus = ctx->num_cus - (masked ? 8 * ctx->rows_cu_off : 0);
   const int set = ctx->rows_set;
   // this set's pair was last used two writes back (ended: the engine stream
   // waited for it before this build wrote the set)
@@ -1315,6 +1330,10 @@ int launch_rows(kano_ctx* ctx) {
   KCHK(hipEventRecord(ctx->ev_rin, ctx->stream));
   if (ctx->wi_total == 0) return 0;
   KCHK(hipStreamWaitEvent(rs, ctx->ev_rin, 0));
+  // writes stay in order across the two write streams (M, the input sets)
+  if (ctx->rows_last && ctx->rows_last != rs && ctx->rows_end_rec[set ^ 1])
+    KCHK(hipStreamWaitEvent(rs, ctx->ev_rows_end[set ^ 1], 0));
+  ctx->rows_last = rs;
   if (ctx->rows_after) KCHK(hipStreamWaitEvent(rs, ctx->rows_after, 0));
   hipEvent_t e0 = ctx->ev_rt[set][0], e1 = ctx->ev_rt[set][1];
   if (ctx->heavy_count > 0) {
@@ -1692,6 +1711,7 @@ int kano_create(int device, kano_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return -EIO;
   kano_ctx* ctx = new kano_ctx();
   ctx->device = device;
+  (void)hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
   // test hooks (KANO_TUNE="key=value,..."): forms that compute the same
   // results, forced for the parity tests (see kano_ctx)
   if (const char* t = getenv("KANO_TUNE")) {
@@ -1716,7 +1736,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
         if (k == "prio") ctx->stream_prio = v;
-        if (k == "rcu" && (v == 0 || v == 1 || v == 2 || v == 4)) ctx->rows_cu_off = v;
+        if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
+        if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
       }
       pos = end + 1;
     }
@@ -1733,26 +1754,26 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
-  hipError_t e3;
-  if (ctx->rows_cu_off > 0) {
-    // bit i off when i % 8 == (i / 32) % 8 (and, for fewer, i % 32 < 8 * K / 4...):
-    // K CUs of every XCD whether CUs are numbered XCD-major or round-robin
-    uint32_t mask[8];
-    for (int w = 0; w < 8; ++w) {
-      mask[w] = 0xffffffffu;
-      for (int b = 0; b < 32; ++b) {
-        const int i = w * 32 + b;
-        if (i % 8 == (i / 32) % 8 && (i % 32) < 8 * ctx->rows_cu_off) mask[w] &= ~(1u << b);
-      }
-    }
-    e3 = hipExtStreamCreateWithCUMask(&ctx->stream3, 8, mask);
-  } else {
-    e3 = hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking);
-  }
-  if (e3 != hipSuccess) {
+  if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
     ctx->stream3 = nullptr;
     kano_destroy(ctx);
     return -EIO;
+  }
+  if (ctx->rows_cu_off > 0) {
+    // bit i = 32a + 8b + c off when (c - a) mod 8 < t and b < beta, K = t * beta:
+    // K CUs of every XCD whether the CUs are numbered XCD-major (XCD a) or
+    // round-robin (XCD c)
+    const int K = ctx->rows_cu_off, t = K < 4 ? 1 : K / 4, beta = K < 4 ? K : 4;
+    uint32_t mask[8];
+    for (int w = 0; w < 8; ++w) {
+      mask[w] = 0xffffffffu;
+      for (int bit = 0; bit < 32; ++bit) {
+        const int i = w * 32 + bit, a = i / 32, b = (i / 8) % 4, c = i % 8;
+        if (((c - a) & 7) < t && b < beta) mask[w] &= ~(1u << bit);
+      }
+    }
+    // (no masked stream: every write takes stream3)
+    if (hipExtStreamCreateWithCUMask(&ctx->stream3m, 8, mask) != hipSuccess) ctx->stream3m = nullptr;
   }
   if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -1797,6 +1818,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
+  if (ctx->stream3m) (void)hipStreamSynchronize(ctx->stream3m);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   if (ctx->gmirror) (void)hipHostFree(ctx->gmirror);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
@@ -1841,6 +1863,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
+  if (ctx->stream3m) (void)hipStreamDestroy(ctx->stream3m);
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_sizes,
                        ctx->ev_fork2, ctx->ev_join2, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
                        ctx->ev_rows_end[1], ctx->ev_rt[0][0], ctx->ev_rt[0][1], ctx->ev_rt[1][0],
@@ -1857,6 +1880,7 @@ int kano_set_stream(kano_ctx* ctx, void* s) {
   KTRY(settle(ctx));
   KCHK(hipStreamSynchronize(ctx->stream2));
   KCHK(hipStreamSynchronize(ctx->stream3));
+  if (ctx->stream3m) KCHK(hipStreamSynchronize(ctx->stream3m));
   if (ctx->own_stream && ctx->stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -2201,6 +2225,7 @@ int kano_info(kano_ctx* ctx, int64_t* out) {
   out[KANO_INFO_MAXSEL] = ctx->max_sel;
   out[KANO_INFO_UA] = ctx->cc.U;
   out[KANO_INFO_HEAVY_PATH] = ctx->heavy_path;
+  out[KANO_INFO_ROWS_CUS] = ctx->rows_cus;
   out[KANO_INFO_WORK_ITEMS] = ctx->wi_total;
   out[KANO_INFO_ROWS_KERNEL] = ctx->rows_kernel;
   return 0;

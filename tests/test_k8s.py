@@ -304,8 +304,9 @@ def test_build_classes_defers_the_matrix():
     b = DeviceBuild(t, build=False)
     b.build_classes()
     ia, ib = a.info(), b.info()
-    # (ROWS_KERNEL names the matrix write that ran: none yet in b)
+    # (ROWS_KERNEL / ROWS_CUS name the matrix write that ran: none yet in b)
     assert ia.pop("ROWS_KERNEL") == 2 and ib.pop("ROWS_KERNEL") == 0
+    assert ia.pop("ROWS_CUS") > 0 and ib.pop("ROWS_CUS") == 0
     assert ia == ib
     assert np.array_equal(a.rows(0, 800), b.rows(0, 800))
 
