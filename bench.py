@@ -334,7 +334,13 @@ def main():
     r0, r1 = row_range(n, world, rank)
     if args.rank_of > 1:
         r0, r1 = 0, n // args.rank_of
-    stream = torch.cuda.Stream() if dist is not None or args.rank_of > 1 else None
+    # The engine runs on its own (high-priority) streams: the N > 1 exchange
+    # is issued by the engine itself (native RCCL, or the emulated gather of
+    # --rank-of), so no torch stream needs to order it.  (A torch stream
+    # added a fifth queue beside the engine's four; GPU_MAX_HW_QUEUES is 4,
+    # and streams sharing a hardware queue time-sliced the rank's kernels:
+    # rank 0 of 8 took 0.61 ms a step instead of 0.46.)
+    stream = None
     eng = DeviceBuild(None, device=torch.cuda.current_device(), path=args.path,
                       stream=stream.cuda_stream if stream is not None else None)
     # host -> device upload of the resident inputs (label tables, policy

@@ -213,6 +213,9 @@ int kano_verify_combine(kano_ctx* ctx, const uint64_t* gathered_dev, int32_t nra
  * The RCCL symbols are resolved at the first call from the process (the
  * library that created comm, e.g. torch's bundled librccl), else
  * librccl.so; without them the call fails (-ENOSYS) and nothing runs.
+ * comm NULL emulates rank 0 of nranks on this device (a timing diagnostic,
+ * bench.py --rank-of: the all-gather becomes a device copy into rank 0's
+ * slot, the other ranks' words stay zero, so the lists are partial).
  * Outputs as kano_verify_combine; with_shadow as kano_verify_shard. */
 int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups,
                        int64_t sys_row, int with_shadow, void* comm, int32_t nranks,

@@ -170,10 +170,29 @@ struct kano_ctx {
   DBuf scan_tmp;
   i64 scan_cap = 0;          // tiles per status region of scan_tmp
   int scan_parity = 0;
+  // stream2's scans (the build's side work): their own status regions
+  DBuf scan_tmp2;
+  i64 scan_cap2 = 0;
+  int scan_parity2 = 0;
+  // The build's size-independent side work on stream2 beside the join chain:
+  // AC / Mc zero fills and the crosscheck's group-key sort, forked after the
+  // classes (ev_pre) and joined before the lists (ev_pre_done).  sidepre=0
+  // keeps them on the engine stream.
+  int side_pre = 1;
+  hipEvent_t ev_pre = nullptr, ev_pre_done = nullptr;
+  bool pre_forked = false, pre_side_pending = false;
+  // policy_shadow's offset scans and compaction on stream2 right after its
+  // tests (pairs mode), beside the crosscheck pass and the column checks;
+  // the emission stays on the engine stream behind the index lists
+  // (sidetail=0: scans and compaction on the engine stream too)
+  int side_tail = 1;
+  bool tail_compacted = false;
+  hipEvent_t ev_pairs = nullptr;   // the compaction done (stream2)
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
   DBuf flags, T, loff, L, tp, poff, out, tcnt, toff;
   DBuf scratch_words, ident;
   DBuf xw, xg;               // kano_verify_gather: this shard's words, all ranks' words
+  i64 xg_emul = -1;          // words of xg zeroed for the emulated gather (comm NULL)
   // kano_path (in the destination context): T, R / delta ping-pong buffers,
   // the MFMA operands, the step counter
   DBuf pT, pR[2], pD[2], pA, pB, pcnt;
@@ -333,14 +352,16 @@ inline unsigned nblk(i64 n, i64 per = TPB) { return (unsigned)((n + per - 1) / p
 inline i64 scan_tiles(i64 n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 // status slots per region >= slots (grows, zeroing both regions in order)
-int scan_reserve(kano_ctx* ctx, i64 slots) {
-  if (slots <= ctx->scan_cap) return 0;
-  slots = std::max<i64>(slots, 2 * ctx->scan_cap);
+int scan_reserve(kano_ctx* ctx, i64 slots, bool side = false) {
+  i64& cap = side ? ctx->scan_cap2 : ctx->scan_cap;
+  if (slots <= cap) return 0;
+  slots = std::max<i64>(slots, 2 * cap);
   const size_t bytes = sizeof(u64) * 2 * (size_t)slots;
-  KTRY(dalloc(ctx, ctx->scan_tmp, bytes));
-  KCHK(hipMemsetAsync(ctx->scan_tmp.p, 0, bytes, ctx->stream));
-  ctx->scan_cap = slots;
-  ctx->scan_parity = 0;
+  DBuf& tmp = side ? ctx->scan_tmp2 : ctx->scan_tmp;
+  KTRY(dalloc(ctx, tmp, bytes));
+  KCHK(hipMemsetAsync(tmp.p, 0, bytes, side ? ctx->stream2 : ctx->stream));
+  cap = slots;
+  (side ? ctx->scan_parity2 : ctx->scan_parity) = 0;
   return 0;
 }
 
@@ -349,7 +370,8 @@ struct ScanBatch {
   ScanJobs jobs{};
   kano_ctx* ctx;
   i64 slots = 0, maxt = 1;
-  explicit ScanBatch(kano_ctx* c) : ctx(c) {
+  bool side = false;   // on stream2 with its own status regions (no host totals)
+  explicit ScanBatch(kano_ctx* c, bool on_side = false) : ctx(c), side(on_side) {
     jobs.count = 0;
     jobs.npub = 0;
   }
@@ -407,15 +429,20 @@ struct ScanBatch {
     a.sig_val = jobs.sig_val;
     a.sig_ctr = jobs.sig_ctr;
     a.sig_n = jobs.sig_n;
-    hipLaunchKernelGGL(k_scan_lb<NJ>, g, dim3(TPB), 0, ctx->stream, a, cur, nxt, ctx->scan_cap);
+    hipLaunchKernelGGL(k_scan_lb<NJ>, g, dim3(TPB), 0, side ? ctx->stream2 : ctx->stream, a, cur,
+                       nxt, side ? ctx->scan_cap2 : ctx->scan_cap);
   }
   int run() {
     if (jobs.count == 0) return 0;
-    KTRY(scan_reserve(ctx, slots));
+    KTRY(scan_reserve(ctx, slots, side));
     // the host signal: raised once every host mirror of this launch is written
     int writers = jobs.npub > 0 ? 1 : 0;
     for (int q = 0; q < jobs.count; ++q) writers += jobs.j[q].total_host ? 1 : 0;
     jobs.sig_host = nullptr;
+    // (the signal and its arrival counter belong to the engine stream: a side
+    // scan's host totals are plain mirror stores, read once the engine
+    // stream has joined the side stream)
+    if (side) writers = 0;
     if (writers > 0 && ctx->sig_ctr.p) {
       jobs.sig_host = ctx->gmirror_dev + SZ_SIGNAL;
       jobs.sig_val = ++ctx->sig_seq;
@@ -425,9 +452,11 @@ struct ScanBatch {
     } else if (writers > 0) {
       ctx->sig_armed = 0;
     }
-    u64* st = P_<u64>(ctx->scan_tmp);
-    u64* cur = st + (ctx->scan_parity ? ctx->scan_cap : 0);
-    u64* nxt = st + (ctx->scan_parity ? 0 : ctx->scan_cap);
+    u64* st = P_<u64>(side ? ctx->scan_tmp2 : ctx->scan_tmp);
+    const i64 cap = side ? ctx->scan_cap2 : ctx->scan_cap;
+    int& parity = side ? ctx->scan_parity2 : ctx->scan_parity;
+    u64* cur = st + (parity ? cap : 0);
+    u64* nxt = st + (parity ? 0 : cap);
     const dim3 g((unsigned)maxt, (unsigned)jobs.count);
     switch (jobs.count) {
       case 1: launch_n<1>(g, cur, nxt); break;
@@ -440,7 +469,7 @@ struct ScanBatch {
       default: launch_n<MAX_SCAN_JOBS>(g, cur, nxt); break;
     }
     KLAUNCH();
-    ctx->scan_parity ^= 1;
+    parity ^= 1;
     jobs.count = 0;
     jobs.npub = 0;
     slots = 0;
@@ -460,7 +489,8 @@ int scan_excl(kano_ctx* ctx, const Tin* in, i64 n, Tout* out) {
 struct FillBatch {
   FillJobs jobs{};
   kano_ctx* ctx;
-  explicit FillBatch(kano_ctx* c) : ctx(c) { jobs.count = 0; }
+  hipStream_t st = nullptr;   // (nullptr: the engine stream)
+  explicit FillBatch(kano_ctx* c, hipStream_t s = nullptr) : ctx(c), st(s) { jobs.count = 0; }
   int add(DBuf& b, size_t bytes, uint32_t value);
   int add_raw(void* p, size_t bytes, uint32_t value) {
     if (bytes == 0) return 0;
@@ -498,7 +528,7 @@ int FillBatch::run() {
   i64 most = 0;
   for (int q = 0; q < jobs.count; ++q) most = std::max(most, jobs.j[q].words);
   const unsigned grid = (unsigned)std::max<i64>(1, std::min<i64>(2048, (most + TPB - 1) / TPB));
-  hipLaunchKernelGGL(k_fill_many, dim3(grid), dim3(TPB), 0, ctx->stream, jobs);
+  hipLaunchKernelGGL(k_fill_many, dim3(grid), dim3(TPB), 0, st ? st : ctx->stream, jobs);
   KLAUNCH();
   jobs.count = 0;
   return 0;
@@ -764,7 +794,11 @@ int classify_phase1(kano_ctx* ctx) {
                        P_<int32_t>(ctx->pv), n, pr);
     KLAUNCH();
   }
-  // class ids: a scan over the representative flags (generated in the scan)
+  // class ids: a scan over the representative flags (generated in the scan).
+  // (Atomic ids drawn by the inserting pod, without this scan, measured
+  // slower: the two counters serialise ~21k atomics each, k_cls_insert 25 ->
+  // 58 us, and ids in creation order cost k_rows ~10 % -- smallest-member
+  // order keeps its member rows closer to address order.)
   ScanBatch sb(ctx);
   KTRY(sb.add_rep_flags(P_<int32_t>(ctx->rc.smin), P_<int32_t>(ctx->rc.slot_of), ctx->rc.m0, nr,
                         P_<int32_t>(ctx->rc.cid), SZ_UR));
@@ -893,10 +927,10 @@ int match_both(kano_ctx* ctx) {
     }
     KTRY(sb.run());
   }
-  if (rows_f > 0) {
-    hipLaunchKernelGGL(k_join_fill, dim3(nblk(maxU), rows_f), dim3(TPB), 0, ctx->stream, pr);
-    KLAUNCH();
-    hipLaunchKernelGGL(k_join_match, dim3(nblk(ctx->P), 2), dim3(TPB), 0, ctx->stream, ctx->P, pr);
+  if (rows_f > 0) {   // the group members and every policy's group, one launch
+    const unsigned nbf = nblk(maxU), nbm = nblk(ctx->P);
+    hipLaunchKernelGGL(k_join_fill_match, dim3(std::max(nbf, nbm), rows_f + 2), dim3(TPB), 0,
+                       ctx->stream, ctx->P, pr, (int)rows_f, nbf, nbm);
     KLAUNCH();
   }
   if (ctx->P > 0 && ctx->cc.U > 0 && ctx->am.dense) KTRY(match_dense(ctx, ctx->am, ctx->cc));
@@ -964,6 +998,12 @@ int do_front(kano_ctx* ctx, int path) {
   // travel while phase 2a runs
   KTRY(mirror_begin(ctx));
   KTRY(classify_phase2a(ctx));
+  // the side work of do_back_pre needs the classes only: fork it here
+  ctx->pre_forked = false;
+  if (ctx->side_pre && ctx->stream2) {
+    KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
+    ctx->pre_forked = true;
+  }
   i64 u[2] = {0, 0};
   KTRY(mirror_wait(ctx, SZ_UR, 2, u));
   // an earlier matrix write's time, when it has ended (no wait: the
@@ -1098,10 +1138,17 @@ int build_alist(kano_ctx* ctx, hipStream_t st = nullptr, bool launch = true) {
 // launches (kano_verify: the crosscheck's group keys) -- queued while the
 // list sizes travel to the host
 using PreLaunch = std::function<int(FillBatch&)>;
-int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const std::function<int()>& pre_run) {
+using PreRun = std::function<int(hipStream_t)>;
+// With the side work forked (ev_pre, recorded after the classes), all of it
+// runs on stream2 beside the join chain and do_back joins it (ev_pre_done).
+int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run) {
   const i64 U = ctx->rc.U, P = ctx->P, ldMc = ctx->ldC;
+  const bool side = ctx->pre_forked;
+  ctx->pre_forked = false;
+  hipStream_t ss = side ? ctx->stream2 : nullptr;
+  if (side) KCHK(hipStreamWaitEvent(ss, ctx->ev_pre, 0));
   {
-    FillBatch fb(ctx);
+    FillBatch fb(ctx, ss);
     KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
     KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
     KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
@@ -1115,7 +1162,11 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const std::function<in
     if (pre_fill) KTRY(pre_fill(fb));
     KTRY(fb.run());
   }
-  if (pre_run) KTRY(pre_run());
+  if (pre_run) KTRY(pre_run(ss));
+  if (side) {
+    KCHK(hipEventRecord(ctx->ev_pre_done, ss));
+    ctx->pre_side_pending = true;
+  }
   return 0;
 }
 
@@ -1125,6 +1176,10 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const std::function<in
 // contraction; column checks at class level
 int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra) {
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
+  if (ctx->pre_side_pending) {   // the side work (zeroed AC / Mc, the key sort)
+    ctx->pre_side_pending = false;
+    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_done, 0));
+  }
   ctx->heavy_path = 0;
   bool mfma = false;
   if (H > 0) {
@@ -1479,7 +1534,8 @@ struct CrossPlan {
 };
 
 // host checks, group upload (no fills): cp.on, cp.gdev, cp.G
-int cross_setup(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp) {
+int cross_setup(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp,
+                hipStream_t st = nullptr) {
   const i64 n = ctx->n, W = ctx->W, ldM = ctx->ldM;
   KTRY(dalloc(ctx, ctx->gid, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ldM));
@@ -1501,7 +1557,7 @@ int cross_setup(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& c
       }
     }
     KCHK(hipMemcpyAsync(ctx->gid.p, gid, sizeof(int32_t) * n, hipMemcpyHostToDevice,
-                        ctx->stream));
+                        st ? st : ctx->stream));
   }
   cp.G = G;
   cp.on = true;
@@ -1512,7 +1568,7 @@ int cross_setup(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& c
 int cross_prepare(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, CrossPlan& cp,
                   FillBatch& fb, bool setup_done = false) {
   const i64 ldM = ctx->ldM;
-  if (!setup_done) KTRY(cross_setup(ctx, gid, ngroups, cp));
+  if (!setup_done) KTRY(cross_setup(ctx, gid, ngroups, cp, fb.st));
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
   KTRY(fb.add_raw(err, sizeof(u64), 0u));
   KTRY(fb.add(ctx->cross, sizeof(u64) * ldM, 0u));
@@ -1558,23 +1614,26 @@ KeySort cross_sort(kano_ctx* ctx, const CrossPlan& cp) {
   return k;
 }
 
-int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
+// (st: stream2 for the build's side work, with sb a side batch; the side
+// form of the LDS key sort has no scan: k_key_place_scan scans the histogram)
+int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb, hipStream_t st = nullptr) {
   if (!cp.on) return 0;
   const i64 U = ctx->rc.U, G = cp.G, rl = rows_local(ctx);
+  const hipStream_t s = st ? st : ctx->stream;
   int32_t* err = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR);
   // group range of every row class along its member list
-  hipLaunchKernelGGL(k_cls_group_range_m, dim3(nblk(rl)), dim3(TPB), 0, ctx->stream, cp.gdev,
+  hipLaunchKernelGGL(k_cls_group_range_m, dim3(nblk(rl)), dim3(TPB), 0, s, cp.gdev,
                      (int32_t)G, P_<int32_t>(ctx->rc.cls), P_<int32_t>(ctx->rc.mem), rl,
                      P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax), err);
   KLAUNCH();
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {   // classes in group order: per-block LDS histograms
     const KeySort ks = cross_sort(ctx, cp);
-    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream, ks);
+    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB), 0, s, ks);
     KLAUNCH();
-    KTRY(sb.add(ks.hist, cp.kslots, P_<int32_t>(ctx->koff)));
+    if (!st) KTRY(sb.add(ks.hist, cp.kslots, P_<int32_t>(ctx->koff)));
   } else {
-    hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+    hipLaunchKernelGGL(k_cls_key, dim3(nblk(U)), dim3(TPB), 0, s, U,
                        P_<int32_t>(ctx->rc.mcnt), P_<int32_t>(ctx->gmin), P_<int32_t>(ctx->gmax),
                        (int32_t)G, P_<int32_t>(ctx->ckey), kcnt);
     KLAUNCH();
@@ -1585,15 +1644,19 @@ int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb) {
 
 // classes placed in group order, one pass over Mc (R[g], MULTI, and the
 // column checks when the build deferred them), group overlaps A1 / A2
-int cross_stage_b1(kano_ctx* ctx, const CrossPlan& cp) {
+int cross_stage_b1(kano_ctx* ctx, const CrossPlan& cp, hipStream_t st = nullptr) {
   if (!cp.on) return 0;
   const i64 U = ctx->rc.U, G = cp.G;
+  const hipStream_t s = st ? st : ctx->stream;
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
-  if (cp.key_lds) {
-    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, ctx->stream,
+  if (cp.key_lds && st) {
+    hipLaunchKernelGGL(k_key_place_scan, dim3((unsigned)cp.knb), dim3(TPB), 0, s,
+                       cross_sort(ctx, cp));
+  } else if (cp.key_lds) {
+    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, s,
                        cross_sort(ctx, cp));
   } else {
-    hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, ctx->stream, U,
+    hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, s, U,
                        P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,
                        P_<int32_t>(ctx->corder));
   }
@@ -1736,6 +1799,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
         if (k == "prio") ctx->stream_prio = v;
+        if (k == "sidepre") ctx->side_pre = v;
+        if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
       }
@@ -1782,6 +1847,9 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_rin, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pre_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pairs, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&ctx->ev_m0) != hipSuccess || hipEventCreate(&ctx->ev_m1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows_end[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows_end[1], hipEventDisableTiming) != hipSuccess ||
@@ -1837,7 +1905,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->hoff,   &ctx->hlist,   &ctx->sq,      &ctx->pfoff,     &ctx->ACT,
                   &ctx->AC,     &ctx->nca,     &ctx->acnt,    &ctx->alcoff,    &ctx->alc,
                   &ctx->aloff,  &ctx->alist,   &ctx->M,       &ctx->Mc,        &ctx->color,
-                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp,
+                  &ctx->colnand, &ctx->col_and, &ctx->col_or_c, &ctx->col_nand_c, &ctx->scan_tmp, &ctx->scan_tmp2,
                   &ctx->shg_h,  &ctx->shg_tkey, &ctx->shg_trep, &ctx->shg_slot, &ctx->shg_isrep,
                   &ctx->shg_gidx, &ctx->shg_gid, &ctx->shg_reps, &ctx->shg_sub, &ctx->shg_err, &ctx->sig_ctr,
                   &ctx->gid,    &ctx->cgroup,  &ctx->R,       &ctx->multi,     &ctx->A1,
@@ -1865,7 +1933,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamDestroy(ctx->stream3m);
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_sizes,
-                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
+                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_pre, ctx->ev_pre_done, ctx->ev_pairs, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
                        ctx->ev_rows_end[1], ctx->ev_rt[0][0], ctx->ev_rt[0][1], ctx->ev_rt[1][0],
                        ctx->ev_rt[1][1]})
     if (e) (void)hipEventDestroy(e);
@@ -2154,7 +2222,7 @@ namespace {
 using ExtraFills = std::function<int(FillBatch&)>;
 int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
                const ExtraFills& extra = ExtraFills(), const ExtraFills& pre_fill = ExtraFills(),
-               const std::function<int()>& pre_run = std::function<int()>()) {
+               const PreRun& pre_run = PreRun()) {
   if (!ctx) return -EINVAL;
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
@@ -2818,12 +2886,12 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   auto pre_fill = [&](FillBatch& fb) -> int {
     return want_cross ? cross_prepare(ctx, gid, ngroups, cp, fb) : 0;
   };
-  auto pre_run = [&]() -> int {
+  auto pre_run = [&](hipStream_t st) -> int {
     if (!want_cross || !cp.on) return 0;
-    ScanBatch sb(ctx);
-    KTRY(cross_stage_a(ctx, cp, sb));
+    ScanBatch sb(ctx, st != nullptr);
+    KTRY(cross_stage_a(ctx, cp, sb, st));
     KTRY(sb.run());
-    return cross_stage_b1(ctx, cp);
+    return cross_stage_b1(ctx, cp, st);
   };
   auto extra = [&](FillBatch& fb) -> int {
     return want_shadow ? shadow_prepare(ctx, sp, fb) : 0;
@@ -2847,24 +2915,45 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   const int brc = build_impl(ctx, path, false, want_cross, extra, pre_fill, pre_run);
   ctx->fork_hook = nullptr;
   KTRY(brc);
-  if (fork_marked) {
-    KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
-    KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
-    KCHK(hipEventRecord(ctx->ev_join2, ctx->stream2));
-    ctx->fork_pending = true;
-  }
   const i64 n = ctx->n, W = ctx->W;
   const bool have_sys = sys_row >= ctx->r0 && sys_row < ctx->r1;
   const bool cross_on = want_cross && cp.on;
-  // the crosscheck's pass over Mc, then policy_shadow's scans (its tests ran
-  // beside the build on stream2, or run here)
+  // the crosscheck's pass over Mc first (the engine stream's next work: its
+  // launches go out before the side stream's), then policy_shadow's tests on
+  // stream2 and their scans (or here)
   if (cross_on) KTRY(cross_stage_b2(ctx, cp));
+  ctx->tail_compacted = false;
+  bool scans_side = false;
+  if (fork_marked) {
+    KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
+    KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
+    scans_side = ctx->side_tail && !ctx->vs_count_only;
+    if (scans_side) {   // the offset scans right behind the tests
+      ScanBatch sbs(ctx, true);
+      KTRY(shadow_stage_a_scans(ctx, sp, sbs));
+      KTRY(sbs.run());
+    }
+    KCHK(hipEventRecord(ctx->ev_join2, ctx->stream2));
+    ctx->fork_pending = true;
+    if (scans_side) {   // the compaction beside the column checks
+      KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, sp.nf)));
+      if (sp.nt > 0) {
+        hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)sp.nt), dim3(TPB), 0, ctx->stream2,
+                           P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
+                           P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), sp.nf,
+                           P_<i64>(ctx->toff), P_<int2>(ctx->L), sp.nf);
+        KLAUNCH();
+      }
+      KCHK(hipEventRecord(ctx->ev_pairs, ctx->stream2));
+      ctx->tail_compacted = true;
+    }
+  }
   if (want_shadow) {
     ScanBatch sb(ctx);
     if (ctx->fork_pending) {
       KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join2, 0));
       ctx->fork_pending = false;
-      KTRY(shadow_stage_a_scans(ctx, sp, sb));
+      if (!scans_side) KTRY(shadow_stage_a_scans(ctx, sp, sb));
     } else {
       KTRY(shadow_stage_a(ctx, sp, sb));
     }
@@ -2954,9 +3043,11 @@ int spin_event(kano_ctx* ctx, hipEvent_t e) {
   }
 }
 
+// compacted: policy_shadow's compaction ran on stream2 (verify_front; its
+// end is ev_pairs)
 int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts,
                        int32_t* shadow_pairs, void* pairs_h, int64_t shadow_cap,
-                       int64_t* shadow_count, bool async) {
+                       int64_t* shadow_count, bool async, bool compacted = false) {
   using clk = std::chrono::steady_clock;
   auto tmark = clk::now();
   auto part = [&](int k) {
@@ -2975,7 +3066,8 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
     KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nf)));
     KTRY(dalloc(ctx, ctx->out, sizeof(int2) * 1024));
     out_cap = (i64)(ctx->out.bytes / sizeof(int2));
-    if (nt > 0) {
+    if (compacted) KCHK(hipStreamWaitEvent(st, ctx->ev_pairs, 0));
+    if (nt > 0 && !compacted) {
       hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)nt), dim3(TPB), 0, st,
                          P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
                          P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), nf, P_<i64>(ctx->toff),
@@ -3091,16 +3183,22 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   ir.row[3] = ctx->vs_sys_on ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
-  if (n > 0 && W > 0) {
-    hipLaunchKernelGGL(k_idx_write, dim3((unsigned)nb, 4), dim3(TPB), 0, ctx->stream, ir,
-                       P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
-    KLAUNCH();
-  }
   const bool pairs_mode = want_shadow && shadow_cap >= 0;
   if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
     (void)sync(ctx);
     return fail(ctx, -EINVAL, "kano_verify_combine: the shard ran policy_shadow count-only "
                               "(with_shadow = 2); pass shadow_cap < 0");
+  }
+  void* idx_h = n > 0 ? pinned_dev(idx) : nullptr;
+  void* pairs_h = pairs_mode && shadow_pairs ? pinned_dev(shadow_pairs) : nullptr;
+  const bool direct = n > 0 && W > 0 && idx_h && (!pairs_mode || !shadow_pairs || pairs_h);
+  // policy_shadow compacted on stream2 already (verify_front)
+  const bool compacted = direct && pairs_mode && ctx->tail_compacted;
+  ctx->tail_compacted = false;
+  if (n > 0 && W > 0) {
+    hipLaunchKernelGGL(k_idx_write, dim3((unsigned)nb, 4), dim3(TPB), 0, ctx->stream, ir,
+                       P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
+    KLAUNCH();
   }
   // Page-locked result buffers (kano_host_alloc): the whole tail is queued
   // at once on the engine stream, sized on the device -- policy_shadow's
@@ -3109,11 +3207,9 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // once, for the results; no host round trip between the scans and the
   // tail.  A total past a buffer's capacity leaves that step undone and the
   // host redoes it sized (first call, or a larger output).
-  void* idx_h = n > 0 ? pinned_dev(idx) : nullptr;
-  void* pairs_h = pairs_mode && shadow_pairs ? pinned_dev(shadow_pairs) : nullptr;
-  if (n > 0 && W > 0 && idx_h && (!pairs_mode || !shadow_pairs || pairs_h))
+  if (direct)
     return verify_back_direct(ctx, idx, idx_h, counts, shadow_pairs, pairs_h, shadow_cap,
-                              shadow_count, may_async && ctx->async_rows);
+                              shadow_count, may_async && ctx->async_rows, compacted);
   // the list sizes, policy_shadow's sizes and the group check travel to the
   // host: it waits on the signal (or the event) only, then queues the tail
   // (policy_shadow's compaction and emission, the copies) on stream2 and the
@@ -3203,6 +3299,26 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   part(14);
   return 0;
 }
+// host time of one kano_verify / kano_verify_gather call by phase
+// (kano_host_times): a stall names its phase
+void host_time_record(kano_ctx* ctx, std::chrono::steady_clock::time_point t0,
+                      std::chrono::steady_clock::time_point t1,
+                      std::chrono::steady_clock::time_point t2) {
+  auto us = [](std::chrono::steady_clock::duration d) {
+    return std::chrono::duration<double, std::micro>(d).count();
+  };
+  double* h = ctx->ht;
+  if (h[0] > 0) h[4] += us(t0 - ctx->ht_last);
+  h[0] += 1;
+  h[1] += us(t1 - t0);
+  h[2] += us(t2 - t1);
+  h[3] += ctx->ht_wait_cur;
+  h[5] = std::max(h[5], us(t1 - t0));
+  h[6] = std::max(h[6], us(t2 - t1));
+  h[7] = std::max(h[7], ctx->ht_wait_cur);
+  h[8] = std::max(h[8], us(t2 - t0));
+  ctx->ht_last = t2;
+}
 }  // namespace
 
 extern "C" {
@@ -3222,20 +3338,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   const auto t1 = clk::now();
   const int rc =
       verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count, true);
-  // host time of the call by phase (kano_host_times): a stall names its phase
-  const auto t2 = clk::now();
-  auto us = [](clk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
-  double* h = ctx->ht;
-  if (h[0] > 0) h[4] += us(t0 - ctx->ht_last);
-  h[0] += 1;
-  h[1] += us(t1 - t0);
-  h[2] += us(t2 - t1);
-  h[3] += ctx->ht_wait_cur;
-  h[5] = std::max(h[5], us(t1 - t0));
-  h[6] = std::max(h[6], us(t2 - t1));
-  h[7] = std::max(h[7], ctx->ht_wait_cur);
-  h[8] = std::max(h[8], us(t2 - t0));
-  ctx->ht_last = t2;
+  host_time_record(ctx, t0, t1, clk::now());
   return rc;
 }
 
@@ -3274,28 +3377,46 @@ int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngro
                        int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                        int64_t* shadow_count) {
   if (!ctx) return -EINVAL;
-  if (!comm || nranks < 1) return fail(ctx, -EINVAL, "kano_verify_gather: bad communicator");
+  if (nranks < 1) return fail(ctx, -EINVAL, "kano_verify_gather: bad communicator");
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify_gather: idx / counts must not be NULL");
   if (with_shadow && !shadow_count)
     return fail(ctx, -EINVAL, "kano_verify_gather: shadow_count is NULL but with_shadow is set");
-  const RcclAllGather ag = rccl_all_gather();
-  if (!ag)
+  // comm NULL: rank 0 of nranks emulated on this device (a timing diagnostic:
+  // the other ranks' words are zero, the all-gather a device copy)
+  const RcclAllGather ag = comm ? rccl_all_gather() : nullptr;
+  if (comm && !ag)
     return fail(ctx, -ENOSYS, "kano_verify_gather: no RCCL in the process (ncclAllGather)");
   const i64 nw = 3 * ctx->W;     // [OR | cross | NAND] words of a shard (same W on every rank)
   KTRY(dalloc(ctx, ctx->xw, sizeof(u64) * std::max<i64>(1, nw)));
+  const void* xg_before = ctx->xg.p;
   KTRY(dalloc(ctx, ctx->xg, sizeof(u64) * std::max<i64>(1, nw * nranks)));
+  if (!comm && (ctx->xg.p != xg_before || ctx->xg_emul != nw * nranks)) {
+    KCHK(hipMemsetAsync(ctx->xg.p, 0, sizeof(u64) * std::max<i64>(1, nw * nranks), ctx->stream));
+    ctx->xg_emul = nw * nranks;
+  }
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  ctx->ht_wait = 0;
+  ctx->ht_wait_cur = 0.0;
   KTRY(verify_front(ctx, path, gid, ngroups, sys_row, with_shadow != 0, P_<u64>(ctx->xw),
                     with_shadow == 2));
-  if (nw > 0) {
+  if (comm) ctx->xg_emul = -1;
+  if (nw > 0 && comm) {
     const int rc = ag(ctx->xw.p, ctx->xg.p, (size_t)nw, RCCL_UINT64, comm, ctx->stream);
     if (rc != 0) {
       (void)sync(ctx);
       return fail(ctx, -EIO, "kano_verify_gather: ncclAllGather returned " + std::to_string(rc));
     }
+  } else if (nw > 0) {
+    KCHK(hipMemcpyAsync(ctx->xg.p, ctx->xw.p, sizeof(u64) * nw, hipMemcpyDeviceToDevice,
+                        ctx->stream));
   }
-  return verify_back(ctx, P_<u64>(ctx->xg), nranks, idx, counts, shadow_pairs, shadow_cap,
-                     shadow_count, true);
+  const auto t1 = clk::now();
+  const int rc = verify_back(ctx, P_<u64>(ctx->xg), nranks, idx, counts, shadow_pairs,
+                             shadow_cap, shadow_count, true);
+  host_time_record(ctx, t0, t1, clk::now());
+  return rc;
 }
 
 int kano_checks_shard(kano_ctx* ctx, const int32_t* gid, int32_t ngroups, int64_t sys_row,

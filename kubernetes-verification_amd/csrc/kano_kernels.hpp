@@ -568,10 +568,10 @@ __global__ __launch_bounds__(TPB) void k_join_insert(JoinPair pr) {
 
 // grouped class lists; the extra row per side writes the iota block (the
 // class list of policies without terms)
-__global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr) {
+__device__ __forceinline__ void join_fill_item(const JoinPair& pr, int y, i64 bx) {
   int m;
-  const JoinSide a = join_row(pr, blockIdx.y, 1, &m) ? pr.s[1] : pr.s[0];
-  const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
+  const JoinSide a = join_row(pr, y, 1, &m) ? pr.s[1] : pr.s[0];
+  const i64 c = bx * TPB + threadIdx.x;
   if (m == a.NM) {
     if (c < a.U) a.gmem[(i64)a.NM * a.U + c] = (int32_t)c;
     return;
@@ -584,9 +584,9 @@ __global__ __launch_bounds__(TPB) void k_join_fill(JoinPair pr) {
 // thread per policy: its matched classes = gmem[pstart, pstart + plen)
 //   pmask -1: contradictory terms (matches nothing); -2: no terms (all
 //   classes: the iota block); terms sorted by slot = mask order
-__global__ __launch_bounds__(TPB) void k_join_match(i64 P, JoinPair pr) {
-  const JoinSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 p = (i64)blockIdx.x * TPB + threadIdx.x;
+__device__ __forceinline__ void join_match_item(i64 P, const JoinPair& pr, int side, i64 bx) {
+  const JoinSide a = side ? pr.s[1] : pr.s[0];
+  const i64 p = bx * TPB + threadIdx.x;
   if (!a.live || p >= P) return;
   const int m = a.pmask[p];
   i64 st = 0;
@@ -627,6 +627,18 @@ __global__ __launch_bounds__(TPB) void k_join_match(i64 P, JoinPair pr) {
   }
   a.pstart[p] = st;
   a.plen[p] = len;
+}
+
+// k_join_fill and k_join_match in one launch (both need only the group
+// offsets): grid rows [0, rows_f) fill, the next two match (side 0, 1)
+__global__ __launch_bounds__(TPB) void k_join_fill_match(i64 P, JoinPair pr, int rows_f,
+                                                         unsigned nbf, unsigned nbm) {
+  const int y = blockIdx.y;
+  if (y < rows_f) {
+    if (blockIdx.x < nbf) join_fill_item(pr, y, blockIdx.x);
+  } else if (blockIdx.x < nbm) {
+    join_match_item(P, pr, y - rows_f, blockIdx.x);
+  }
 }
 
 // dense fallback (too many distinct masks): per-policy class lists from the
@@ -1156,6 +1168,48 @@ __global__ __launch_bounds__(TPB) void k_cls_key_place(i64 U, const int32_t* __r
 __global__ __launch_bounds__(TPB) void k_key_hist(KeySort k) { key_hist_block(k, blockIdx.x); }
 __global__ __launch_bounds__(TPB) void k_key_place_lds(KeySort k) {
   key_place_block(k, blockIdx.x);
+}
+
+// k_key_place_lds without the scan launch before it: every block scans the
+// (small, bin-major) histogram itself and keeps the exclusive offsets of its
+// own (bin, block) entries; block 0 writes the total to hoff[nk * nb] (the
+// live-class count k_mc_fold reads).  Used on the side stream, which has no
+// scan status region of its own.
+constexpr int KEY_SCAN_ITEMS = 8;
+__global__ __launch_bounds__(TPB) void k_key_place_scan(KeySort k) {
+  __shared__ int32_t h[KEY_LDS_MAX];
+  __shared__ i64 sm[TPB / 64];
+  const int nk = k.G + 1;
+  const i64 b = blockIdx.x, nb = k.nb, ns = (i64)nk * nb;
+  i64 carry = 0;
+  for (i64 t0 = 0; t0 < ns; t0 += (i64)TPB * KEY_SCAN_ITEMS) {
+    const i64 e0 = t0 + (i64)threadIdx.x * KEY_SCAN_ITEMS;
+    int32_t v[KEY_SCAN_ITEMS];
+    i64 sum = 0;
+#pragma unroll
+    for (int q = 0; q < KEY_SCAN_ITEMS; ++q) {
+      v[q] = e0 + q < ns ? k.hist[e0 + q] : 0;
+      sum += v[q];
+    }
+    i64 total;
+    i64 pre = carry + block_excl_scan_nw<TPB / 64>(sum, sm, total);
+#pragma unroll
+    for (int q = 0; q < KEY_SCAN_ITEMS; ++q) {
+      const i64 e = e0 + q;
+      if (e < ns && e % nb == b) h[e / nb] = (int32_t)pre;
+      pre += v[q];
+    }
+    carry += total;
+  }
+  if (b == 0 && threadIdx.x == 0) const_cast<int32_t*>(k.hoff)[ns] = (int32_t)carry;
+  __syncthreads();
+  const i64 c0 = b * TPB * KEY_ITEMS;
+  for (int q = 0; q < KEY_ITEMS; ++q) {
+    const i64 c = c0 + (i64)q * TPB + threadIdx.x;
+    if (c >= k.U) break;
+    const int32_t key = k.ckey[c];
+    if (key >= 0) k.order[atomicAdd(&h[key], 1)] = (int32_t)c;
+  }
 }
 
 // One pass over Mc in group order: R[g] |= Mc[c] (g = key), MULTI for key G;

@@ -78,6 +78,10 @@ class ShardExchange:
                       and os.environ.get("KANO_NATIVE_EXCHANGE", "1") != "0")
         if native:
             self.comm = self._rccl_comm()
+        # emulated rank 0 through the engine's own gather call (comm NULL);
+        # KANO_EMUL_NATIVE=0 keeps the shard / torch copy / combine form
+        self.emulate_native = (dist is None and nranks > 1
+                               and os.environ.get("KANO_EMUL_NATIVE", "1") != "0")
         self.mode = ("emulated" if dist is None else "rccl-native" if self.comm
                      else "host-staged" if host_staged else "torch-collective")
 
@@ -116,9 +120,21 @@ class ShardExchange:
             if self.gathered.is_cuda:
                 torch.cuda.synchronize()
         else:
+            # (the engine's kernels and the collective are on different streams
+            # when the engine has its own: order them through the device)
+            on_dev = self.stream is None and self.words.is_cuda
+            if on_dev:
+                torch.cuda.synchronize()
             dist.all_gather_into_tensor(self.gathered, self.words)
+            if on_dev:
+                torch.cuda.synchronize()
 
     def _run(self, eng, gid, sys_row, shadow, count_only, pairs, idx):
+        if self.dist is None and self.nranks > 1 and self.emulate_native:
+            # emulated rank 0 (a timing diagnostic): one engine call like the
+            # native exchange, the all-gather a device copy (comm NULL)
+            return eng.verify_gather(0, self.nranks, gid=gid, sys_row=sys_row, shadow=shadow,
+                                     shadow_count_only=count_only, pairs=pairs, idx=idx)
         if self.comm:
             return eng.verify_gather(self.comm, self.nranks, gid=gid, sys_row=sys_row,
                                      shadow=shadow, shadow_count_only=count_only, pairs=pairs,
@@ -134,7 +150,7 @@ class ShardExchange:
         """kano_py's checks for this rank (algorithm.py:4-80): the column
         lists are global, system_isolation is None unless this rank owns
         sys_row, the shadow pairs are this rank's rows' part."""
-        if self.stream is None or self.comm:
+        if self.stream is None or self.comm or (self.dist is None and self.emulate_native):
             # (the native exchange issues everything on the engine's own
             # stream: no torch stream context needed, a few us less host time
             # per step)
