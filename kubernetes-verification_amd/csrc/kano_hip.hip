@@ -237,7 +237,7 @@ struct kano_ctx {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;
   bool fork_pending = false;
-  std::function<int()> fork_hook;
+  std::function<int(bool)> fork_hook;   // (true: ev_fork2 marked by the lists' dispatch)
   // kano_verify's tail (result copies, policy_shadow's emission) runs on
   // stream2 too (after the shadow tests' join), beside the matrix write,
   // which has stream3 to itself (normal priority: a high-priority tail slowed
@@ -250,6 +250,9 @@ struct kano_ctx {
   int rows_set = 0;          // which physical set the ctx fields hold
   bool rows_overlap = false; // launch_rows: leave the engine stream free of the write
   hipEvent_t rows_after = nullptr;   // launch_rows: the write also waits for this
+  // launch_rows: the inputs' marker is this event, already recorded on the
+  // engine stream where the write may start (instead of recording ev_rin)
+  hipEvent_t rows_in = nullptr;
   hipEvent_t ev_rin = nullptr;          // k_rows' inputs complete (engine stream)
   hipEvent_t ev_rows_end[2] = {};       // set k's matrix write done (stream3)
   bool rows_end_rec[2] = {false, false};
@@ -348,6 +351,15 @@ T* P_(DBuf& b) {
 
 inline unsigned nblk(i64 n, i64 per = TPB) { return (unsigned)((n + per - 1) / per); }
 
+// A launch whose own dispatch marks ev (when given) -- a separate
+// hipEventRecord costs the stream ~4.5 us (scripts/micro/event_cost.hip)
+template <typename... KArgs, typename... Args>
+void launch_marked(void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                   hipEvent_t ev, Args... args) {
+  if (ev) hipExtLaunchKernelGGL(kernel, grid, block, lds, st, nullptr, ev, 0, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+}
+
 // ---- device-wide scans: batches of k_scan_lb jobs ------------------------
 inline i64 scan_tiles(i64 n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
 
@@ -416,7 +428,7 @@ struct ScanBatch {
   }
   // the launch with only the used job slots in its kernel argument
   template <int NJ>
-  void launch_n(dim3 g, u64* cur, u64* nxt) {
+  void launch_n(dim3 g, u64* cur, u64* nxt, hipEvent_t mark) {
     ScanJobsN<NJ> a;
     for (int q = 0; q < NJ; ++q) a.j[q] = jobs.j[q];
     a.count = jobs.count;
@@ -429,10 +441,11 @@ struct ScanBatch {
     a.sig_val = jobs.sig_val;
     a.sig_ctr = jobs.sig_ctr;
     a.sig_n = jobs.sig_n;
-    hipLaunchKernelGGL(k_scan_lb<NJ>, g, dim3(TPB), 0, side ? ctx->stream2 : ctx->stream, a, cur,
-                       nxt, side ? ctx->scan_cap2 : ctx->scan_cap);
+    launch_marked(k_scan_lb<NJ>, g, dim3(TPB), 0, side ? ctx->stream2 : ctx->stream, mark, a, cur,
+                  nxt, side ? ctx->scan_cap2 : ctx->scan_cap);
   }
-  int run() {
+  // mark: an event this launch's dispatch marks (none when no job is queued)
+  int run(hipEvent_t mark = nullptr) {
     if (jobs.count == 0) return 0;
     KTRY(scan_reserve(ctx, slots, side));
     // the host signal: raised once every host mirror of this launch is written
@@ -459,14 +472,14 @@ struct ScanBatch {
     u64* nxt = st + (parity ? 0 : cap);
     const dim3 g((unsigned)maxt, (unsigned)jobs.count);
     switch (jobs.count) {
-      case 1: launch_n<1>(g, cur, nxt); break;
-      case 2: launch_n<2>(g, cur, nxt); break;
-      case 3: launch_n<3>(g, cur, nxt); break;
-      case 4: launch_n<4>(g, cur, nxt); break;
-      case 5: launch_n<5>(g, cur, nxt); break;
-      case 6: launch_n<6>(g, cur, nxt); break;
-      case 7: launch_n<7>(g, cur, nxt); break;
-      default: launch_n<MAX_SCAN_JOBS>(g, cur, nxt); break;
+      case 1: launch_n<1>(g, cur, nxt, mark); break;
+      case 2: launch_n<2>(g, cur, nxt, mark); break;
+      case 3: launch_n<3>(g, cur, nxt, mark); break;
+      case 4: launch_n<4>(g, cur, nxt, mark); break;
+      case 5: launch_n<5>(g, cur, nxt, mark); break;
+      case 6: launch_n<6>(g, cur, nxt, mark); break;
+      case 7: launch_n<7>(g, cur, nxt, mark); break;
+      default: launch_n<MAX_SCAN_JOBS>(g, cur, nxt, mark); break;
     }
     KLAUNCH();
     parity ^= 1;
@@ -814,7 +827,10 @@ int classify_alloc2(kano_ctx* ctx, ClassSet& cs) {
 // phase 2a, both sides, without the class counts (the host reads them
 // meanwhile): ids, member counts, their offsets (scanned over the side's pod
 // count; the entries past U are zero), member lists of pods [m0, m1)
-int classify_phase2a(kano_ctx* ctx) {
+// mark: an event the member-list fill's dispatch marks (returns false, and
+// marks nothing, when there is no fill)
+int classify_phase2a(kano_ctx* ctx, hipEvent_t mark = nullptr, bool* marked = nullptr) {
+  if (marked) *marked = false;
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   const i64 mr = ctx->rc.m1 - ctx->rc.m0, ma = ctx->cc.m1 - ctx->cc.m0;
   const i64 rl = std::max(mr, ma);
@@ -827,10 +843,11 @@ int classify_phase2a(kano_ctx* ctx) {
   KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ma, P_<int32_t>(ctx->cc.moff)));
   KTRY(sb.run());
   if (rl > 0) {
-    hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr,
-                       (const int32_t*)nullptr, 0, (int32_t*)nullptr, (int32_t*)nullptr,
-                       reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR));
+    launch_marked(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, mark, pr,
+                  (const int32_t*)nullptr, 0, (int32_t*)nullptr, (int32_t*)nullptr,
+                  reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR));
     KLAUNCH();
+    if (marked) *marked = mark != nullptr;
   }
   return 0;
 }
@@ -997,11 +1014,14 @@ int do_front(kano_ctx* ctx, int path) {
   // host sync 1 of the build (the class counts), overlapped: the counts
   // travel while phase 2a runs
   KTRY(mirror_begin(ctx));
-  KTRY(classify_phase2a(ctx));
-  // the side work of do_back_pre needs the classes only: fork it here
+  // the side work of do_back_pre needs the classes only: it forks after the
+  // member lists (their fill's dispatch marks ev_pre)
   ctx->pre_forked = false;
-  if (ctx->side_pre && ctx->stream2) {
-    KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
+  const bool fork_pre = ctx->side_pre && ctx->stream2;
+  bool pre_marked = false;
+  KTRY(classify_phase2a(ctx, fork_pre ? ctx->ev_pre : nullptr, &pre_marked));
+  if (fork_pre) {
+    if (!pre_marked) KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
     ctx->pre_forked = true;
   }
   i64 u[2] = {0, 0};
@@ -1231,19 +1251,24 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                          P_<u64>(ctx->AC), ctx->ldC};
   const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
                          ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
+  // (the fork point of kano_verify's side stream, when it has one: marked by
+  // this dispatch itself, not by a separate event record)
+  hipEvent_t fev = ctx->fork_hook ? ctx->ev_fork2 : nullptr;
   if (lists_on && allow_on) {
     const unsigned nb1 = nblk(U, TPB / 64);
-    hipLaunchKernelGGL(k_lists_allow, dim3(nb1 + nblk(P, WPB)), dim3(TPB), lds, ctx->stream, cla,
-                       paa, nb1);
+    launch_marked(k_lists_allow, dim3(nb1 + nblk(P, WPB)), dim3(TPB), lds, ctx->stream, fev, cla,
+                  paa, nb1);
     KLAUNCH();
   } else if (lists_on) {
-    hipLaunchKernelGGL(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, cla);
+    launch_marked(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, fev, cla);
     KLAUNCH();
   } else if (allow_on) {
-    hipLaunchKernelGGL(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, paa);
+    launch_marked(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, fev, paa);
     KLAUNCH();
+  } else {
+    fev = nullptr;
   }
-  if (ctx->fork_hook) KTRY(ctx->fork_hook());   // lists and AC are complete here
+  if (ctx->fork_hook) KTRY(ctx->fork_hook(fev != nullptr));   // lists and AC are complete here
   // Light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
   // entries, cache-resident).  The flat lists win wherever the light rows
@@ -1382,9 +1407,15 @@ int launch_rows(kano_ctx* ctx) {
   // this set's pair was last used two writes back (ended: the engine stream
   // waited for it before this build wrote the set)
   KTRY(resolve_rows_slot(ctx, set, true));
-  KCHK(hipEventRecord(ctx->ev_rin, ctx->stream));
+  // (an event record costs the engine stream ~4.5 us: reuse one that stands
+  // at the same place, e.g. the tail's copy-done event)
+  hipEvent_t rin = ctx->rows_in;
+  if (!rin) {
+    KCHK(hipEventRecord(ctx->ev_rin, ctx->stream));
+    rin = ctx->ev_rin;
+  }
   if (ctx->wi_total == 0) return 0;
-  KCHK(hipStreamWaitEvent(rs, ctx->ev_rin, 0));
+  KCHK(hipStreamWaitEvent(rs, rin, 0));
   // writes stay in order across the two write streams (M, the input sets)
   if (ctx->rows_last && ctx->rows_last != rs && ctx->rows_end_rec[set ^ 1])
     KCHK(hipStreamWaitEvent(rs, ctx->ev_rows_end[set ^ 1], 0));
@@ -2898,16 +2929,20 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   };
   ctx->vs_open = false;
   // policy_shadow's subset tests need only the lists and AC: they run on
-  // stream2 beside the Mc chain (scatter, fold).  The fork point is marked
-  // (ev_fork2) where the lists and AC are complete; the side stream's wait,
-  // the tests and the join event are issued after the build's remaining
-  // launches, so that the host's fork calls overlap those kernels instead of
-  // leaving the main stream idle
+  // stream2 beside the Mc chain (scatter, fold), forked (ev_fork2) and issued
+  // where the lists and AC are complete.  In pairs mode (side_tail) the rest
+  // of policy_shadow up to its emission follows them there -- the offset
+  // scans, the compaction, the per-pod pair counts and their scan -- and the
+  // engine stream joins it (ev_pairs) only before the emission.
   ctx->fork_pending = false;
+  ctx->tail_compacted = false;
   bool fork_marked = false;
+  const bool side_sh = want_shadow && !count_only && ctx->side_tail;
   if (want_shadow) {
-    ctx->fork_hook = [&]() -> int {
-      KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));
+    ctx->fork_hook = [&](bool marked) -> int {
+      if (!marked) KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));
+      KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
+      KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
       fork_marked = true;
       return 0;
     };
@@ -2922,38 +2957,17 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   // launches go out before the side stream's), then policy_shadow's tests on
   // stream2 and their scans (or here)
   if (cross_on) KTRY(cross_stage_b2(ctx, cp));
-  ctx->tail_compacted = false;
-  bool scans_side = false;
-  if (fork_marked) {
-    KCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork2, 0));
-    KTRY(shadow_test_launch(ctx, sp, ctx->stream2));
-    scans_side = ctx->side_tail && !ctx->vs_count_only;
-    if (scans_side) {   // the offset scans right behind the tests
-      ScanBatch sbs(ctx, true);
-      KTRY(shadow_stage_a_scans(ctx, sp, sbs));
-      KTRY(sbs.run());
-    }
+  const bool side_run = fork_marked && side_sh;
+  if (!side_run && fork_marked) {
     KCHK(hipEventRecord(ctx->ev_join2, ctx->stream2));
     ctx->fork_pending = true;
-    if (scans_side) {   // the compaction beside the column checks
-      KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, sp.nf)));
-      if (sp.nt > 0) {
-        hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)sp.nt), dim3(TPB), 0, ctx->stream2,
-                           P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
-                           P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), sp.nf,
-                           P_<i64>(ctx->toff), P_<int2>(ctx->L), sp.nf);
-        KLAUNCH();
-      }
-      KCHK(hipEventRecord(ctx->ev_pairs, ctx->stream2));
-      ctx->tail_compacted = true;
-    }
   }
-  if (want_shadow) {
+  if (want_shadow && !side_run) {
     ScanBatch sb(ctx);
     if (ctx->fork_pending) {
       KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join2, 0));
       ctx->fork_pending = false;
-      if (!scans_side) KTRY(shadow_stage_a_scans(ctx, sp, sb));
+      KTRY(shadow_stage_a_scans(ctx, sp, sb));
     } else {
       KTRY(shadow_stage_a(ctx, sp, sb));
     }
@@ -3003,7 +3017,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     }
     fa.icnt = P_<i64>(ctx->icnt);
     fa.words = words_dev;
-    if (want_shadow && sp.rl > 0) {
+    if (want_shadow && sp.rl > 0 && !side_run) {
       fa.rcls = P_<int32_t>(ctx->rc.cls);
       fa.loff = P_<i64>(ctx->loff);
       fa.tp = P_<i64>(ctx->tp);
@@ -3014,6 +3028,37 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     KLAUNCH();
   } else {
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
+  }
+  // (issued after the column checks: the engine stream does not wait for it)
+  if (side_run) {
+    // the offset scans (toff: SZ_NL; loff), the compaction and the per-pod
+    // pair counts, then their offsets (poff: SZ_PAIRS), all behind the tests
+    hipStream_t s2 = ctx->stream2;
+    {
+      ScanBatch sbs(ctx, true);
+      KTRY(shadow_stage_a_scans(ctx, sp, sbs));
+      KTRY(sbs.run());
+    }
+    KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, sp.nf)));
+    if (sp.nt > 0) {
+      hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)sp.nt), dim3(TPB), 0, s2,
+                         P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
+                         P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), sp.nf,
+                         P_<i64>(ctx->toff), P_<int2>(ctx->L), sp.nf);
+      KLAUNCH();
+    }
+    if (sp.rl > 0) {
+      hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(sp.rl)), dim3(TPB), 0, s2,
+                         P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
+                         P_<i64>(ctx->tp));
+      KLAUNCH();
+    }
+    {   // (its dispatch marks ev_pairs)
+      ScanBatch sbs(ctx, true);
+      KTRY(sbs.add(P_<i64>(ctx->tp), sp.rl, P_<i64>(ctx->poff), SZ_PAIRS));
+      KTRY(sbs.run(ctx->ev_pairs));
+    }
+    ctx->tail_compacted = true;
   }
   ctx->vs_open = true;
   ctx->vs_shadow = want_shadow;
@@ -3092,13 +3137,17 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
                       std::min<i64>(shadow_cap, out_cap)};
     njobs = 2;
   }
-  hipLaunchKernelGGL(k_copy_out_dev, dim3(256, njobs), dim3(TPB), 0, st, cj);
+  // the copy's own dispatch marks ev_tail (no separate record: ~3 us less on
+  // the engine stream), which also starts the matrix write
+  hipExtLaunchKernelGGL(k_copy_out_dev, dim3(256, njobs), dim3(TPB), 0, st, nullptr, ctx->ev_tail,
+                        0, cj);
   KLAUNCH();
-  KCHK(hipEventRecord(ctx->ev_tail, st));
   if (ctx->vs_rows) {
     ctx->rows_overlap = async;
+    ctx->rows_in = ctx->ev_tail;
     const int rc = launch_rows(ctx);
     ctx->rows_overlap = false;
+    ctx->rows_in = nullptr;
     KTRY(rc);
   }
   part(12);
@@ -3154,8 +3203,25 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // a gathered combine lists the crosscheck whenever it was asked for (other
   // shards may hold its rows)
   const bool cross_row = gathered ? ctx->vs_cross_want : ctx->vs_cross_on;
+  const bool pairs_mode = want_shadow && shadow_cap >= 0;
+  if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
+    (void)sync(ctx);
+    return fail(ctx, -EINVAL, "kano_verify_combine: the shard ran policy_shadow count-only "
+                              "(with_shadow = 2); pass shadow_cap < 0");
+  }
+  void* idx_h = n > 0 ? pinned_dev(idx) : nullptr;
+  void* pairs_h = pairs_mode && shadow_pairs ? pinned_dev(shadow_pairs) : nullptr;
+  const bool direct = n > 0 && W > 0 && idx_h && (!pairs_mode || !shadow_pairs || pairs_h);
+  // policy_shadow's scans, per-pod counts and compaction ran on stream2
+  // (verify_front): the direct tail joins it before the emission; the host's
+  // sync below needs its sizes, so that path joins it here
+  const bool side_sh = want_shadow && ctx->tail_compacted;
+  const bool compacted = side_sh && direct && pairs_mode;
+  if (side_sh && !compacted) KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pairs, 0));
+  ctx->tail_compacted = false;
   ScanBatch sb(ctx);
-  if (want_shadow) KTRY(sb.add(P_<i64>(ctx->tp), ctx->vs_rl, P_<i64>(ctx->poff), SZ_PAIRS));
+  if (want_shadow && !side_sh)
+    KTRY(sb.add(P_<i64>(ctx->tp), ctx->vs_rl, P_<i64>(ctx->poff), SZ_PAIRS));
   if (gathered && n > 0 && W > 0) {
     if (cross_row) KTRY(dalloc(ctx, ctx->cross, sizeof(u64) * ctx->ldM));
     hipLaunchKernelGGL(k_combine_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, gathered,
@@ -3170,7 +3236,9 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
                 SZ_IDX0 + r));
   sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
-  if (want_shadow) sb.publish(SZ_NL);   // (an earlier scan's total: one host signal for all)
+  // (an earlier scan's total: one host signal for all; the side scans store
+  // their totals to the host directly)
+  if (want_shadow && !compacted) sb.publish(SZ_NL);
   KTRY(sb.run());
   IdxRows ir{};
   ir.W = W;
@@ -3183,18 +3251,6 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   ir.row[3] = ctx->vs_sys_on ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
-  const bool pairs_mode = want_shadow && shadow_cap >= 0;
-  if (want_shadow && ctx->vs_count_only && shadow_cap >= 0) {
-    (void)sync(ctx);
-    return fail(ctx, -EINVAL, "kano_verify_combine: the shard ran policy_shadow count-only "
-                              "(with_shadow = 2); pass shadow_cap < 0");
-  }
-  void* idx_h = n > 0 ? pinned_dev(idx) : nullptr;
-  void* pairs_h = pairs_mode && shadow_pairs ? pinned_dev(shadow_pairs) : nullptr;
-  const bool direct = n > 0 && W > 0 && idx_h && (!pairs_mode || !shadow_pairs || pairs_h);
-  // policy_shadow compacted on stream2 already (verify_front)
-  const bool compacted = direct && pairs_mode && ctx->tail_compacted;
-  ctx->tail_compacted = false;
   if (n > 0 && W > 0) {
     hipLaunchKernelGGL(k_idx_write, dim3((unsigned)nb, 4), dim3(TPB), 0, ctx->stream, ir,
                        P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
