@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: the N > 1 step (shard verify + RCCL all-gather + combine) "
                          "even at one rank, e.g. under torch.distributed.run --nproc-per-node 1")
+    ap.add_argument("--alone", type=int, default=5,
+                    help="k_rows launches timed alone (kano_build) after the timed region "
+                         "(roofline.alone; 0: none)")
     ap.add_argument("--rank-of", type=int, default=0,
                     help="diagnostic: time rank 0's shard step of an N-rank run on one GPU "
                          "(the all-gather replaced by a local copy; not a bench line)")
@@ -396,6 +399,15 @@ def main():
     rows_kernel = {2: "k_rows"}.get(info["ROWS_KERNEL"], "none")
     mt = eng.mfma_timing()
     host = eng.host_times()
+    # k_rows alone (untimed, after the timed region): the same matrix write of
+    # the same inputs with nothing beside it -- kano_build, which waits for its
+    # write, so the write takes every CU (in the timed steps it runs on a
+    # CU-masked stream beside the next step's build)
+    eng.rows_timing(reset=True)
+    for _ in range(args.alone):
+        eng.build()
+    ra = eng.rows_timing()
+    alone_ms = ra["sum_ms"] / ra["launches"] if ra["launches"] else float("nan")
     rows_local = r1 - r0
     W = (n + 63) // 64
     alg_bytes = 8.0 * rows_local * W
@@ -453,7 +465,15 @@ def main():
                          # the write runs beside the next step's build on a
                          # CU-masked stream when it is short enough to overlap
                          # it ("Pipelined steps")
-                         "cus": info["ROWS_CUS"]},
+                         "cus": info["ROWS_CUS"],
+                         # the same launch alone on the device, every CU (a
+                         # separate untimed measurement, see above)
+                         "alone": ({"avg_launch_ms": alone_ms,
+                                    "achieved": alg_bytes / (alone_ms * 1e-3) / 1e9,
+                                    "frac": alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "launches": ra["launches"],
+                                    "how": "kano_build x %d after the timed region" % args.alone}
+                                   if ra["launches"] else None)},
             # the dense path's int8 MFMA contraction (k_heavy_mc_mfma; --path
             # mfma or AUTO's dense choice): algorithmic ops / its event time
             "mfma_roofline": ({"bound": "mfma", "kernel": "k_heavy_mc_mfma",

@@ -1399,8 +1399,11 @@ int launch_rows(kano_ctx* ctx) {
   const i64 rl = rows_local(ctx);
   ctx->rows_kernel = 0;
   if (rl == 0 || W == 0) return 0;
-  const bool masked =
-      ctx->stream3m && (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
+  // (the CU mask only where the write overlaps the next call's build --
+  // kano_verify's asynchronous completion; a write the caller waits for
+  // takes every CU)
+  const bool masked = ctx->rows_overlap && ctx->stream3m &&
+                      (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
   hipStream_t rs = masked ? ctx->stream3m : ctx->stream3;
   ctx->rows_cus = ctx->num_cus - (masked ? 8 * ctx->rows_cu_off : 0);
   const int set = ctx->rows_set;
