@@ -426,6 +426,18 @@ struct ScanBatch {
     j.gm0 = m0;
     return 0;
   }
+  // policy_shadow's pair offsets over pods [m0, m0 + n): each pod's count is
+  // its class's segment length in loff, generated inside the scan
+  int add_class_lengths(const int32_t* cls, const i64* loff, i64 m0, i64 n, i64* out,
+                        int total_slot) {
+    KTRY(add(static_cast<const int32_t*>(nullptr), n, out, total_slot));
+    ScanJob& j = jobs.j[jobs.count - 1];
+    j.gen = 2;
+    j.gslot = cls;
+    j.gloff = loff;
+    j.gm0 = m0;
+    return 0;
+  }
   // the launch with only the used job slots in its kernel argument
   template <int NJ>
   void launch_n(dim3 g, u64* cur, u64* nxt, hipEvent_t mark) {
@@ -919,6 +931,13 @@ JoinSide join_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
   a.plen = P_<int32_t>(sx.plen);
   a.NM = sx.NM;
   a.live = (ctx->P > 0 && cs.U > 0 && !sx.dense) ? 1 : 0;
+  a.ctab = P_<u64>(cs.table);
+  a.ctmask = (uint32_t)(table_size(ctx->n) - 1);
+  a.csmin = P_<int32_t>(cs.smin);
+  a.ccid = P_<int32_t>(cs.cid);
+  a.cm0 = cs.m0;
+  a.kbits = P_<int32_t>(cs.keys_d) + cs.KS;
+  a.KS = cs.KS;
   return a;
 }
 
@@ -1268,7 +1287,8 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   } else {
     fev = nullptr;
   }
-  if (ctx->fork_hook) KTRY(ctx->fork_hook(fev != nullptr));   // lists and AC are complete here
+  const bool fork_marked = fev != nullptr;   // (the hook runs at the end: the
+                                             // engine stream's launches go first)
   // Light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
   // entries, cache-resident).  The flat lists win wherever the light rows
@@ -1286,7 +1306,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   const bool scatter_on = U > 0 && ctx->nnz_sel > 0;
   const bool pods_in_scatter = ctx->rows_use_alist && scatter_on && P > 0 && ctx->cc.U > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx, nullptr, !pods_in_scatter));
-  if (U == 0) return 0;
+  if (U == 0) return ctx->fork_hook ? ctx->fork_hook(fork_marked) : 0;
   if (scatter_on && (size_t)ldMc * 8 * (TPB / 64) <= 64 * 1024) {
     // light Mc rows by their owner (a wave per row class, the row in LDS,
     // plain stores)
@@ -1369,6 +1389,8 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     }
   }
   if (!ctx->cols_deferred) KTRY(mc_cols(ctx));
+  // kano_verify's side stream forks from the lists (ev_fork2)
+  if (ctx->fork_hook) KTRY(ctx->fork_hook(fork_marked));
   return 0;
 }
 
@@ -2190,6 +2212,22 @@ static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t*
     tval.swap(v2);
     sx.nterms = (i64)tslot.size();
   } else {
+    // A policy naming every class key of a packed side selects at most one
+    // class, found in the classification's own table (pmask -3): its mask
+    // needs no join table (C3: a quarter of the policies on each side)
+    if (cs.packed && cs.KS > 0) {
+      int f = -1;
+      for (size_t m = 0; m < masks.size(); ++m)
+        if ((int)masks[m].size() == cs.KS) f = (int)m;
+      if (f >= 0) {
+        for (i64 p = 0; p < P; ++p) {
+          if (pmask[p] == f) pmask[p] = -3;
+          else if (pmask[p] > f) --pmask[p];
+        }
+        masks.erase(masks.begin() + f);
+        sx.NM = (int)masks.size();
+      }
+    }
     for (auto& m : masks) {
       mslot.insert(mslot.end(), m.begin(), m.end());
       moff.push_back((int32_t)mslot.size());
@@ -2280,6 +2318,12 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   // of the back end (zeroed AC / Mc, the crosscheck's group-key sort)
   KTRY(mirror_begin(ctx));
   KTRY(do_back_pre(ctx, pre_fill, pre_run));
+  // (the engine stream's join of the side work goes out before the host's
+  // wait for the sizes, not after it)
+  if (ctx->pre_side_pending) {
+    ctx->pre_side_pending = false;
+    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_done, 0));
+  }
   KTRY(read_sizes(ctx));
   KTRY(stage_mark(ctx, 3, ctx->stream));
   ctx->cols_deferred = defer_cols;
@@ -3050,15 +3094,11 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
                          P_<i64>(ctx->toff), P_<int2>(ctx->L), sp.nf);
       KLAUNCH();
     }
-    if (sp.rl > 0) {
-      hipLaunchKernelGGL(k_shadow_podcount, dim3(nblk(sp.rl)), dim3(TPB), 0, s2,
-                         P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
-                         P_<i64>(ctx->tp));
-      KLAUNCH();
-    }
-    {   // (its dispatch marks ev_pairs)
+    {   // the pair offsets, each pod's count generated from loff in the scan
+        // (its dispatch marks ev_pairs)
       ScanBatch sbs(ctx, true);
-      KTRY(sbs.add(P_<i64>(ctx->tp), sp.rl, P_<i64>(ctx->poff), SZ_PAIRS));
+      KTRY(sbs.add_class_lengths(P_<int32_t>(ctx->rc.cls), P_<i64>(ctx->loff), ctx->r0, sp.rl,
+                                 P_<i64>(ctx->poff), SZ_PAIRS));
       KTRY(sbs.run(ctx->ev_pairs));
     }
     ctx->tail_compacted = true;

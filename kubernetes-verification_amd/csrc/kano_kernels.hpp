@@ -517,6 +517,16 @@ struct JoinSide {
   int32_t* plen;
   int NM;
   int live;
+  // pmask -3 (a policy naming every class key of a packed side): its one
+  // class comes straight from the classification's table -- the side's
+  // packed-key table, representatives and class ids
+  const u64* ctab;
+  uint32_t ctmask;
+  const int32_t* csmin;
+  const int32_t* ccid;
+  i64 cm0;
+  const int32_t* kbits;   // bits per key (keys_d + KS)
+  int KS;
 };
 struct JoinPair {
   JoinSide s[2];
@@ -582,7 +592,8 @@ __device__ __forceinline__ void join_fill_item(const JoinPair& pr, int y, i64 bx
 }
 
 // thread per policy: its matched classes = gmem[pstart, pstart + plen)
-//   pmask -1: contradictory terms (matches nothing); -2: no terms (all
+//   pmask -1: contradictory terms (matches nothing); -3: every class key
+//   (one class, from the classification's table); -2: no terms (all
 //   classes: the iota block); terms sorted by slot = mask order
 __device__ __forceinline__ void join_match_item(i64 P, const JoinPair& pr, int side, i64 bx) {
   const JoinSide a = side ? pr.s[1] : pr.s[0];
@@ -591,7 +602,31 @@ __device__ __forceinline__ void join_match_item(i64 P, const JoinPair& pr, int s
   const int m = a.pmask[p];
   i64 st = 0;
   int32_t len = 0;
-  if (m == -2) {
+  if (m == -3) {
+    // every class key named: the class whose packed key equals the terms'
+    // (k_cls_insert's packing and hash), if a pod of this side has it
+    const i64 t0 = a.toff[p];
+    bool possible = true;
+    u64 key = 0;
+    for (int k = 0; k < a.KS; ++k) {
+      const int32_t v = a.tval[t0 + k];
+      possible = possible && v >= 0;
+      key = (key << a.kbits[k]) | (u64)(uint32_t)(v + 3);
+    }
+    if (possible && a.U > 0) {
+      uint32_t s = hfin(hmix(hmix(0x9747b28cu, (uint32_t)key), (uint32_t)(key >> 32))) & a.ctmask;
+      for (;;) {
+        const u64 cur = a.ctab[s];
+        if (cur == ~0ull) break;
+        if (cur == key) {
+          st = (i64)a.NM * a.U + a.ccid[a.csmin[s] - a.cm0];   // (the iota block)
+          len = 1;
+          break;
+        }
+        s = (s + 1) & a.ctmask;
+      }
+    }
+  } else if (m == -2) {
     st = (i64)a.NM * a.U;
     len = (int32_t)a.U;
   } else if (m >= 0) {

@@ -142,12 +142,15 @@ struct ScanJob {
   i64 n;
   i64 st;
   int in64, out64;
-  // generated input instead of `in` (gen = 1): element x is 1 iff pod
+  // generated input instead of `in`.  gen = 1: element x is 1 iff pod
   // m0 + x is the smallest member of its hash slot (a class representative),
-  // smin[slot_of[m0 + x]] == m0 + x
+  // smin[slot_of[m0 + x]] == m0 + x.  gen = 2: element x is the length of
+  // pod m0 + x's class segment, loff[c + 1] - loff[c] with c = gslot[m0 + x]
+  // (policy_shadow's pairs per pod: gslot = the row classes)
   int gen;
   const int32_t* gsmin;
   const int32_t* gslot;
+  const i64* gloff;
   i64 gm0;
 };
 constexpr int MAX_SCAN_JOBS = 8;
@@ -241,7 +244,11 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const i64 x = base + k;
     if (x >= jb.n) v[k] = 0;
-    else if (jb.gen) v[k] = jb.gsmin[jb.gslot[jb.gm0 + x]] == (int32_t)(jb.gm0 + x) ? 1 : 0;
+    else if (jb.gen == 1) v[k] = jb.gsmin[jb.gslot[jb.gm0 + x]] == (int32_t)(jb.gm0 + x) ? 1 : 0;
+    else if (jb.gen == 2) {
+      const int32_t c = jb.gslot[jb.gm0 + x];
+      v[k] = jb.gloff[c + 1] - jb.gloff[c];
+    }
     else v[k] = jb.in64 ? static_cast<const i64*>(jb.in)[x]
                         : (i64) static_cast<const int32_t*>(jb.in)[x];
     s += v[k];
