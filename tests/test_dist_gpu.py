@@ -138,3 +138,55 @@ def test_rccl_exchange_one_rank(name, native):
         assert r["shadow_count"] == exp["policy_shadow"]["count"]
         allp = np.ascontiguousarray(r["pairs"].reshape(-1, 2).astype(np.int32))
         assert sha(allp) == exp["policy_shadow"]["sha256"]
+
+
+@pytest.mark.parametrize("name", ["s_sparse_2000", "C2"])
+def test_verify_gather_emulated_exchange(name):
+    """kano_verify_gather with comm NULL (bench.py --rank-of's emulated
+    exchange: the all-gather a device copy into rank 0's slot, the other
+    ranks' words zero).  With nranks = 1 that is the whole exchange, so the
+    lists equal kano_py's; rank 0 of 3 keeps its own rows' exact results
+    (its shadow pairs are the head of the full list, system_isolation(0) is
+    its row)."""
+    from kano._engine import DeviceBuild
+    from kano._intern import group_ids, intern, tables_from_cluster
+    from kano.shard import row_range
+    if name.startswith("C"):
+        from kano.synth import KEY_NAMES, make_config
+        cl = make_config(name)
+        t = tables_from_cluster(cl)
+        gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
+    else:
+        from _golden import cluster
+        from kano import model
+        from kano.synth import objects_from_json
+        obj = cluster(name)
+        cs, ps = objects_from_json(obj, model)
+        t = intern(cs, ps)
+        gid = group_ids(cs, obj["label"])
+    exp = expected(name)
+    n = t.n
+    eng = DeviceBuild(t)
+    eng.set_groups(gid)
+    for _ in range(2):   # twice: the second call reuses the zeroed slots
+        r = eng.verify_gather(0, 1, gid="stored", sys_row=0, shadow=True)
+        assert index_list_matches(r["all_reachable"], exp["all_reachable"])
+        assert index_list_matches(r["all_isolated"], exp["all_isolated"])
+        assert index_list_matches(r["user_crosscheck"], exp["user_crosscheck"]["result"])
+        assert index_list_matches(r["system_isolation"], exp["system_isolation"]["result"])
+        assert r["shadow_count"] == exp["policy_shadow"]["count"]
+        allp = np.ascontiguousarray(r["pairs"].reshape(-1, 2).astype(np.int32))
+        assert sha(allp) == exp["policy_shadow"]["sha256"]
+    ref = eng.verify("stored", sys_row=0, shadow=True)
+    ref_pairs = np.array(ref["pairs"].reshape(-1, 2), copy=True)
+    ref_sys = np.array(ref["system_isolation"], copy=True)
+    eng.close()
+    r0, r1 = row_range(n, 3, 0)
+    shard = DeviceBuild(t, rows=(r0, r1))
+    shard.set_groups(gid)
+    rs = shard.verify_gather(0, 3, gid="stored", sys_row=0, shadow=True)
+    head = ref_pairs[ref_pairs[:, 0] < r1]
+    assert rs["shadow_count"] == head.shape[0]
+    assert np.array_equal(rs["pairs"].reshape(-1, 2), head)
+    assert np.array_equal(rs["system_isolation"], ref_sys)
+    shard.close()
