@@ -624,8 +624,14 @@ int swap_rows_inputs(kano_ctx* ctx) {
   std::swap(ctx->Mc, a.Mc);
   ctx->rows_set ^= 1;
   ctx->alist_valid = false;
-  if (ctx->rows_end_rec[ctx->rows_set])
-    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows_end[ctx->rows_set], 0));
+  // (usually long over: then no wait packet on the engine stream)
+  if (ctx->rows_end_rec[ctx->rows_set]) {
+    const hipError_t q = hipEventQuery(ctx->ev_rows_end[ctx->rows_set]);
+    if (q == hipErrorNotReady)
+      KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows_end[ctx->rows_set], 0));
+    else
+      KCHK(q);
+  }
   return 0;
 }
 
