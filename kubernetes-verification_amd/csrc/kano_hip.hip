@@ -179,8 +179,11 @@ struct kano_ctx {
   // classes (ev_pre) and joined before the lists (ev_pre_done).  sidepre=0
   // keeps them on the engine stream.
   int side_pre = 1;
-  hipEvent_t ev_pre = nullptr, ev_pre_done = nullptr;
-  bool pre_forked = false, pre_side_pending = false;
+  // (ev_pre_ac: AC zeroed, joined before the lists; ev_pre_done: the rest,
+  // joined before the Mc writers -- each join well after its work ends, so
+  // the engine stream's barrier finds it complete)
+  hipEvent_t ev_pre = nullptr, ev_pre_done = nullptr, ev_pre_ac = nullptr;
+  bool pre_forked = false, pre_side_pending = false, pre_ac_pending = false;
   // policy_shadow's offset scans and compaction on stream2 right after its
   // tests (pairs mode), beside the crosscheck pass and the column checks;
   // the emission stays on the engine stream behind the index lists
@@ -1081,8 +1084,10 @@ int do_front(kano_ctx* ctx, int path) {
     KTRY(dalloc(ctx, ctx->wioff, sizeof(int32_t) * (Ur + 1)));
     KTRY(dalloc(ctx, ctx->hoff, sizeof(int32_t) * (Ur + 1)));
     KTRY(dalloc(ctx, ctx->pfoff, sizeof(i64) * (Ur + 1)));
+    KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, Ur)));
     KTRY(fb.add(ctx->scnt, sizeof(int32_t) * Ur, 0u));
     KTRY(fb.add(ctx->cost, sizeof(u64) * Ur, 0u));
+    KTRY(fb.add(ctx->scur, sizeof(int32_t) * Ur, 0u));   // (k_sel_place's cursors)
     carried = fb.take();   // (carried by k_cls_vals' launch)
   }
   KTRY(classify_phase2b(ctx, carried));
@@ -1192,15 +1197,20 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
   ctx->pre_forked = false;
   hipStream_t ss = side ? ctx->stream2 : nullptr;
   if (side) KCHK(hipStreamWaitEvent(ss, ctx->ev_pre, 0));
+  KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
+  KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
+  KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
+  KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
+  if (side) {   // AC first: the lists' launch needs it before anything else here
+    FillBatch fa(ctx, ss);
+    KTRY(fa.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
+    KTRY(fa.run());
+    KCHK(hipEventRecord(ctx->ev_pre_ac, ss));
+    ctx->pre_ac_pending = true;
+  }
   {
     FillBatch fb(ctx, ss);
-    KTRY(dalloc(ctx, ctx->scur, sizeof(int32_t) * std::max<i64>(1, U)));
-    KTRY(dalloc(ctx, ctx->AC, sizeof(u64) * std::max<i64>(1, P * ctx->ldC)));
-    KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
-    KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
-    KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
-    KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
-    KTRY(fb.add(ctx->scur, sizeof(int32_t) * U, 0u));
+    if (!side) KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
     KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
     KTRY(fb.add(ctx->col_or_c, sizeof(u64) * ldMc, 0u));
     KTRY(fb.add(ctx->col_nand_c, sizeof(u64) * ldMc, 0u));
@@ -1221,10 +1231,6 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
 // contraction; column checks at class level
 int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra) {
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
-  if (ctx->pre_side_pending) {   // the side work (zeroed AC / Mc, the key sort)
-    ctx->pre_side_pending = false;
-    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_done, 0));
-  }
   ctx->heavy_path = 0;
   bool mfma = false;
   if (H > 0) {
@@ -1276,6 +1282,12 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                          P_<u64>(ctx->AC), ctx->ldC};
   const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
                          ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
+  // the side work's joins: AC zeroed before the lists, the rest (Mc, the
+  // crosscheck's fills and key sort) before the Mc writers below
+  if (ctx->pre_ac_pending) {
+    ctx->pre_ac_pending = false;
+    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_ac, 0));
+  }
   // (the fork point of kano_verify's side stream, when it has one: marked by
   // this dispatch itself, not by a separate event record)
   hipEvent_t fev = ctx->fork_hook ? ctx->ev_fork2 : nullptr;
@@ -1295,6 +1307,10 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   const bool fork_marked = fev != nullptr;   // (the hook runs at the end: the
                                              // engine stream's launches go first)
+  if (ctx->pre_side_pending) {
+    ctx->pre_side_pending = false;
+    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_done, 0));
+  }
   // Light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
   // entries, cache-resident).  The flat lists win wherever the light rows
@@ -1911,6 +1927,7 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pre_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pre_ac, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pairs, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&ctx->ev_m0) != hipSuccess || hipEventCreate(&ctx->ev_m1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows_end[0], hipEventDisableTiming) != hipSuccess ||
@@ -1995,7 +2012,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamDestroy(ctx->stream3m);
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_sizes,
-                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_pre, ctx->ev_pre_done, ctx->ev_pairs, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
+                       ctx->ev_fork2, ctx->ev_join2, ctx->ev_pre, ctx->ev_pre_done, ctx->ev_pre_ac, ctx->ev_pairs, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
                        ctx->ev_rows_end[1], ctx->ev_rt[0][0], ctx->ev_rt[0][1], ctx->ev_rt[1][0],
                        ctx->ev_rt[1][1]})
     if (e) (void)hipEventDestroy(e);
@@ -2324,12 +2341,6 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   // of the back end (zeroed AC / Mc, the crosscheck's group-key sort)
   KTRY(mirror_begin(ctx));
   KTRY(do_back_pre(ctx, pre_fill, pre_run));
-  // (the engine stream's join of the side work goes out before the host's
-  // wait for the sizes, not after it)
-  if (ctx->pre_side_pending) {
-    ctx->pre_side_pending = false;
-    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_done, 0));
-  }
   KTRY(read_sizes(ctx));
   KTRY(stage_mark(ctx, 3, ctx->stream));
   ctx->cols_deferred = defer_cols;
