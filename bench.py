@@ -499,7 +499,14 @@ def main():
             # results, waits = the overlapped size syncs)
             "host_us": ({k: round(v, 1) for k, v in host.items() if k.endswith("_max")} |
                         {"front_mean": round(host["front_sum"] / max(1.0, host["calls"]), 1),
-                         "back_mean": round(host["back_sum"] / max(1.0, host["calls"]), 1)}
+                         "back_mean": round(host["back_sum"] / max(1.0, host["calls"]), 1),
+                         # the host's own time per call: the calls minus their
+                         # waits for the device (size signals, the tail)
+                         "waits_mean": round(host["wait_sum"] / max(1.0, host["calls"]), 1),
+                         "tailwait_mean": round(host["tailwait_sum"] / max(1.0, host["calls"]), 1),
+                         "issue_mean": round((host["front_sum"] + host["back_sum"] - host["wait_sum"]
+                                              - host["tailwait_sum"]) / max(1.0, host["calls"]), 1),
+                         "between_mean": round(host["gap_sum"] / max(1.0, host["calls"] - 1), 1)}
                         if host["calls"] > 0 else None),
             "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,

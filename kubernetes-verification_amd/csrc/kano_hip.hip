@@ -228,7 +228,8 @@ struct kano_ctx {
   // kano_host_times: [calls, front sum, back sum, wait sum, gap sum,
   // front max, back max, wait max, call max, size waits 1..3 max, back's
   // parts max: lists + matrix-write launch, policy_shadow's emission launches,
-  // tail wait, list copy, pair copy, event records]
+  // tail wait, list copy, pair copy, event records; the direct tail's wait
+  // sum]
   double ht[20] = {};
   double ht_wait_cur = 0.0;
   int ht_wait = 0;
@@ -355,12 +356,15 @@ T* P_(DBuf& b) {
 inline unsigned nblk(i64 n, i64 per = TPB) { return (unsigned)((n + per - 1) / per); }
 
 // A launch whose own dispatch marks ev (when given) -- a separate
-// hipEventRecord costs the stream ~4.5 us (scripts/micro/event_cost.hip)
+// hipEventRecord costs the stream ~4.5 us (scripts/micro/event_cost.hip).
+// Always through hipExtLaunchKernel with the kernel's handle: a triple-chevron
+// launch through the function-pointer parameter (hipLaunchKernelGGL's macro
+// form) launched nothing in the host-sanitizer build (tests/asan: the first
+// scan's host signal never came)
 template <typename... KArgs, typename... Args>
 void launch_marked(void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t st,
                    hipEvent_t ev, Args... args) {
-  if (ev) hipExtLaunchKernelGGL(kernel, grid, block, lds, st, nullptr, ev, 0, args...);
-  else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+  hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, nullptr, ev, 0, args...);
 }
 
 // ---- device-wide scans: batches of k_scan_lb jobs ------------------------
@@ -728,7 +732,10 @@ int wait_signal(kano_ctx* ctx, u64 val) {
     if ((spin & 0xfff) != 0) continue;
     if (clk::now() - t0 > std::chrono::seconds(1)) {
       KCHK(hipStreamSynchronize(ctx->stream));
-      if (*sig < val) return fail(ctx, -EIO, "internal: host signal not raised");
+      if (*sig < val)
+        return fail(ctx, -EIO, "internal: host signal not raised (wait " +
+                                   std::to_string(ctx->ht_wait) + ": want " + std::to_string(val) +
+                                   ", have " + std::to_string((u64)*sig) + ")");
       break;
     }
   }
@@ -3211,7 +3218,9 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
     KTRY(rc);
   }
   part(12);
+  const auto tw0 = clk::now();
   KTRY(spin_event(ctx, ctx->ev_tail));
+  ctx->ht[18] += std::chrono::duration<double, std::micro>(clk::now() - tw0).count();
   part(14);
   ctx->sig_wait = 0;
   constexpr int NS = SZ_ERR - SZ_NL + 1;
@@ -3890,8 +3899,9 @@ int path_impl(kano_ctx* src, kano_ctx* ctx, int hops, int mode, int64_t* info, b
       const uint16_t* rt16 = reinterpret_cast<const uint16_t*>(ctx->pA.p);
       const bool use_lds = lds <= 64 * 1024 && ctx->path_lds;
       const bool staged = avg_members >= 16;
-      auto launch = [&](auto kern, size_t shm) {
-        hipLaunchKernelGGL(kern, grid, dim3(TPB), shm, ctx->stream, rt16, g.Ua, g.rows,
+      auto launch = [&](auto kern, size_t shm) {   // (by handle: see launch_marked)
+        hipExtLaunchKernelGGL(kern, grid, dim3(TPB), (std::uint32_t)shm, ctx->stream, nullptr,
+                              nullptr, 0, rt16, g.Ua, g.rows,
                            P_<int32_t>(src->cc.cls), n, P_<int32_t>(src->rc.moff),
                            P_<int32_t>(src->rc.mem), P_<u64>(ctx->M), ldM, src->r0);
       };
@@ -4296,6 +4306,7 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
                          P_<u64>(ctx->pR[0]), ldCe, Xi, nch);
       KLAUNCH();
       // class rows of <= K8S_STAGE_W words are staged in LDS by the expansion
+      // (launched by handle: see launch_marked)
       auto K8S_EXPAND = ldCe <= K8S_STAGE_W ? k_k8s_expand<true> : k_k8s_expand<false>;
       const int32_t* cci = P_<int32_t>(in_t->cc.cls);
       const int32_t* rce = P_<int32_t>(eg_t->rc.cls);
@@ -4311,14 +4322,14 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
         KTRY(dalloc(ctx, ctx->pR[1], sizeof(u64) * (Xi + Us) * ldM));
         u64* Xe = P_<u64>(ctx->pR[1]);
         u64* Se = Xe + Xi * ldM;
-        hipLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
-                           ctx->stream, P_<u64>(ctx->pR[0]), ldCe, (const int32_t*)nullptr,
+        hipExtLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(Xi, K8S_XR)), dim3(TPB), 0,
+                           ctx->stream, nullptr, nullptr, 0, P_<u64>(ctx->pR[0]), ldCe, (const int32_t*)nullptr,
                            (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0, Xi,
                            n, W, Xe, ldM);
         KLAUNCH();
         if (Us) {
-          hipLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(Ue, K8S_XR)), dim3(TPB),
-                             0, ctx->stream, P_<u64>(eg_t->Mc), ldCe, (const int32_t*)nullptr,
+          hipExtLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(Ue, K8S_XR)), dim3(TPB),
+                              0, ctx->stream, nullptr, nullptr, 0, P_<u64>(eg_t->Mc), ldCe, (const int32_t*)nullptr,
                              (const u64*)nullptr, ldCe, (const int32_t*)nullptr, cce, 0, (i64)0,
                              Ue, n, W, Se, ldM);
           KLAUNCH();
@@ -4332,8 +4343,8 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
         }
         KLAUNCH();
       } else {
-        hipLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(rl, K8S_XR)), dim3(TPB), 0,
-                           ctx->stream, P_<u64>(ctx->pR[0]), ldCe, cci, P_<u64>(eg_t->Mc), ldCe,
+        hipExtLaunchKernelGGL(K8S_EXPAND, dim3(nblk(ldM, K8S_XW), nblk(rl, K8S_XR)), dim3(TPB), 0,
+                           ctx->stream, nullptr, nullptr, 0, P_<u64>(ctx->pR[0]), ldCe, cci, P_<u64>(eg_t->Mc), ldCe,
                            rce, cce, self, r0, rl, n, W, E, ldM);
         KLAUNCH();
       }

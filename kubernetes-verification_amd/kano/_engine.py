@@ -572,7 +572,7 @@ class DeviceBuild:
         k = ("calls", "front_sum", "back_sum", "wait_sum", "gap_sum", "front_max", "back_max",
              "wait_max", "call_max", "wait1_max", "wait2_max", "wait3_max", "back_launch_max",
              "back_emit_max", "back_tailwait_max", "back_copy_idx_max", "back_copy_pairs_max",
-             "back_events_max")
+             "back_events_max", "tailwait_sum")
         return {name: float(v) for name, v in zip(k, out)}
 
     def stage_times(self) -> dict:

@@ -19,7 +19,7 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["roofline"]
 print(sys.argv[2], "ms", round(d["ms_per_step"], 4), "med", d["step_ms"]["median"], "max", d["step_ms"]["max"],
       "k_rows", round(r["avg_launch_ms"], 4), "frac", round(r["frac"], 3), "cus", r.get("cus"), "alone", (round(r["alone"]["avg_launch_ms"], 4), round(r["alone"]["frac"], 3)) if r.get("alone") else None,
-      "host", {k: d["host_us"][k] for k in ("front_mean", "back_mean")} if d.get("host_us") else None, "ok", d["verified"])
+      "host", {k: d["host_us"][k] for k in ("front_mean", "back_mean", "waits_mean", "tailwait_mean", "issue_mean", "between_mean")} if d.get("host_us") else None, "ok", d["verified"])
 PY
 }
 if [ "${B20:-1}" = 1 ]; then

@@ -19,12 +19,14 @@
 
 typedef uint64_t u64;
 static int fails = 0;
-#define CHECK(c)                                                       \
-  do {                                                                 \
-    if (!(c)) {                                                        \
-      std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);          \
-      ++fails;                                                         \
-    }                                                                  \
+static kano_ctx* g_ctx = nullptr;   // the main context: its last error goes with a failure
+#define CHECK(c)                                                                    \
+  do {                                                                              \
+    if (!(c)) {                                                                     \
+      std::printf("FAIL %s:%d %s (last error: %s)\n", __FILE__, __LINE__, #c,       \
+                  g_ctx ? kano_last_error(g_ctx) : "");                             \
+      ++fails;                                                                      \
+    }                                                                               \
   } while (0)
 
 static uint64_t rs = 0x9E3779B97F4A7C15ull;
@@ -112,6 +114,7 @@ int main() {
     std::printf("kano_create rc=%d\n", rc);
     return 1;
   }
+  g_ctx = ctx;
   const Cluster c = make(3000, 300, 3);
   const int64_t n = c.n, W = (n + 63) / 64;
   std::vector<int32_t> gid((size_t)n);
@@ -237,6 +240,7 @@ int main() {
     CHECK(total == shadow);
     (void)hipFree(g);
   }
+  g_ctx = nullptr;
   kano_destroy(ctx);
   std::printf("%s: %d failed checks, shadow pairs %lld\n", fails ? "FAIL" : "ok", fails,
               (long long)shadow);
