@@ -71,6 +71,7 @@ struct ClassSet {
   std::vector<int32_t> keys;     // pod_val columns hashed
   int KS = 0;
   int packed = 0;                // the key tuple fits one u64 (bits per key: keys_d[KS..2KS))
+  int tbits = 0;                 // the packed key's bits
   i64 U = 0;
   i64 m0 = 0, m1 = 0;            // pods whose membership is listed
   DBuf keys_d, table, smin, slot_of, flag, cid, cls, rep, mcnt, mcur, moff, mem, cval;
@@ -130,6 +131,7 @@ struct kano_ctx {
   // shipped forms that compute the same results; none changes a result.
   int stage_timing = 0;      // timing=1: the stage events of kano_stage_times (slots 0-5)
   int cls_packed = 1;        // packed=0: classification without packed keys (the wide-key form)
+  int cls_podword = 1;       // podword=0: packed slots without the member (the smin form)
   int rows_plain = 0;        // store=0: k_rows with plain stores (non-temporal by default)
   int async_rows = 1;        // async=0: kano_verify waits for its matrix write
   int shadow_count_mode = 0; // shcount=1|2: count-only policy_shadow pairwise | grouped
@@ -423,14 +425,15 @@ struct ScanBatch {
   }
   // class-id scan over the representative flags of pods [m0, m0 + n), the
   // flags generated inside the scan (no flag pass)
-  int add_rep_flags(const int32_t* smin, const int32_t* slot_of, i64 m0, i64 n, int32_t* out,
-                    int total_slot) {
-    KTRY(add(static_cast<const int32_t*>(nullptr), n, out, total_slot));
+  int add_rep_flags(ClassSet& cs, int pbits, i64 n, int total_slot) {
+    KTRY(add(static_cast<const int32_t*>(nullptr), n, P_<int32_t>(cs.cid), total_slot));
     ScanJob& j = jobs.j[jobs.count - 1];
     j.gen = 1;
-    j.gsmin = smin;
-    j.gslot = slot_of;
-    j.gm0 = m0;
+    j.gsmin = P_<int32_t>(cs.smin);
+    j.gtab = P_<u64>(cs.table);
+    j.gpb = pbits;
+    j.gslot = P_<int32_t>(cs.slot_of);
+    j.gm0 = cs.m0;
     return 0;
   }
   // policy_shadow's pair offsets over pods [m0, m0 + n): each pod's count is
@@ -777,6 +780,17 @@ i64 table_size(i64 n) {
   return T;
 }
 
+// Packed sides whose key and smallest member fit one word together keep the
+// member in the slot itself, key << pbits | pod: a block's first probe of a
+// slot inserts or finds its class and lowers the member in one atomic
+// round trip (no smin array); 0 when they do not fit (the smin form)
+int cls_pod_bits(const kano_ctx* ctx, const ClassSet& cs) {
+  if (!cs.packed || !ctx->cls_podword) return 0;
+  int pb = 1;
+  while (pb < 31 && ((i64)1 << pb) < ctx->n) ++pb;
+  return cs.tbits + pb <= 63 ? pb : 0;
+}
+
 int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   const i64 n = ctx->n, T = table_size(n);
   KTRY(dalloc(ctx, cs.table, sizeof(u64) * T));   // int32 pods, or u64 packed keys
@@ -786,7 +800,7 @@ int classify_alloc1(kano_ctx* ctx, ClassSet& cs, FillBatch& fb) {
   KTRY(dalloc(ctx, cs.cid, sizeof(int32_t) * (n + 1)));
   KTRY(dalloc(ctx, cs.cls, sizeof(int32_t) * std::max<i64>(1, n)));
   KTRY(fb.add(cs.table, (cs.packed ? sizeof(u64) : sizeof(int32_t)) * T, 0xffffffffu));
-  KTRY(fb.add(cs.smin, sizeof(int32_t) * T, 0x7fffffffu));
+  if (!cls_pod_bits(ctx, cs)) KTRY(fb.add(cs.smin, sizeof(int32_t) * T, 0x7fffffffu));
   // per-class arrays of phase 2a, sized by the side's pods (>= its classes)
   // so that they need not wait for the class count
   const i64 m = std::max<i64>(1, cs.m1 - cs.m0);
@@ -803,6 +817,7 @@ ClsSide cls_side(kano_ctx* ctx, ClassSet& cs) {
   a.keys = P_<int32_t>(cs.keys_d);
   a.KS = cs.KS;
   a.packed = cs.packed;
+  a.pbits = cls_pod_bits(ctx, cs);
   a.tmask = (uint32_t)(table_size(ctx->n) - 1);
   a.table = P_<int32_t>(cs.table);
   a.slot_of = P_<int32_t>(cs.slot_of);
@@ -841,10 +856,8 @@ int classify_phase1(kano_ctx* ctx) {
   // 58 us, and ids in creation order cost k_rows ~10 % -- smallest-member
   // order keeps its member rows closer to address order.)
   ScanBatch sb(ctx);
-  KTRY(sb.add_rep_flags(P_<int32_t>(ctx->rc.smin), P_<int32_t>(ctx->rc.slot_of), ctx->rc.m0, nr,
-                        P_<int32_t>(ctx->rc.cid), SZ_UR));
-  KTRY(sb.add_rep_flags(P_<int32_t>(ctx->cc.smin), P_<int32_t>(ctx->cc.slot_of), ctx->cc.m0, na,
-                        P_<int32_t>(ctx->cc.cid), SZ_UA));
+  KTRY(sb.add_rep_flags(ctx->rc, cls_pod_bits(ctx, ctx->rc), nr, SZ_UR));
+  KTRY(sb.add_rep_flags(ctx->cc, cls_pod_bits(ctx, ctx->cc), na, SZ_UA));
   return sb.run();
 }
 
@@ -950,6 +963,7 @@ JoinSide join_side(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
   a.ctab = P_<u64>(cs.table);
   a.ctmask = (uint32_t)(table_size(ctx->n) - 1);
   a.csmin = P_<int32_t>(cs.smin);
+  a.cpb = cls_pod_bits(ctx, cs);
   a.ccid = P_<int32_t>(cs.cid);
   a.cm0 = cs.m0;
   a.kbits = P_<int32_t>(cs.keys_d) + cs.KS;
@@ -1875,6 +1889,7 @@ int kano_create(int device, kano_ctx** out) {
         const int v = atoi(kv.c_str() + eq + 1);
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
+        if (k == "podword") ctx->cls_podword = v;
         if (k == "store") ctx->rows_plain = v == 0;
         if (k == "cww" && v >= 16 && v <= MAX_CWW && v % 16 == 0) ctx->rows_cww = v;
         if (k == "async") ctx->async_rows = v;
@@ -2170,6 +2185,7 @@ static int prepare_side(kano_ctx* ctx, i64 P, const int64_t* off, const int32_t*
   // (KS = 0 -- no policy, or only empty selectors -- is one class: packed
   // too, so its pods meet in LDS instead of CAS-ing one global slot)
   cs.packed = (tb <= 63 && ctx->cls_packed) ? 1 : 0;
+  cs.tbits = tb;
   KTRY(dalloc(ctx, cs.keys_d, sizeof(int32_t) * std::max<size_t>(1, kd.size())));
   if (cs.KS > 0)   // uploaded once per policy set, not per build
     KCHK(hipMemcpy(cs.keys_d.p, kd.data(), sizeof(int32_t) * kd.size(), hipMemcpyHostToDevice));

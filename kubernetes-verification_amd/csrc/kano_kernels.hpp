@@ -22,6 +22,7 @@ struct ClsSide {
   const int32_t* keys;   // KS columns, then their bit widths (packed mode)
   int KS;
   int packed;
+  int pbits;             // > 0: packed slots hold key << pbits | smallest member (no smin)
   uint32_t tmask;
   int32_t* table;
   int32_t* slot_of;
@@ -180,7 +181,24 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
       atomicMin(&lmin[t], (int32_t)i);
     }
     __syncthreads();
-    if (lead) {
+    if (lead && a.pbits) {
+      // one atomic per probed slot: the CAS inserts the block's class with
+      // its smallest member, or returns the slot's word; a word of the same
+      // key with a larger member is lowered (no return value awaited)
+      unsigned long long* tb = reinterpret_cast<unsigned long long*>(a.table);
+      const u64 mine = (key << a.pbits) | (u64)(uint32_t)lmin[t];
+      uint32_t s = hfin(hmix(hmix(0x9747b28cu, (uint32_t)key), (uint32_t)(key >> 32))) & a.tmask;
+      for (;;) {
+        const u64 prev = atomicCAS(&tb[s], ~0ull, (unsigned long long)mine);
+        if (prev == ~0ull) break;
+        if ((prev >> a.pbits) == key) {
+          if (prev > mine) atomicMin(&tb[s], (unsigned long long)mine);
+          break;
+        }
+        s = (s + 1) & a.tmask;
+      }
+      lslot[t] = (int32_t)s;
+    } else if (lead) {
       const uint32_t s = cls_packed_slot(reinterpret_cast<const u64*>(a.table), a.tmask, key);
       lslot[t] = (int32_t)s;
       if (lmin[t] < a.smin[s]) atomicMin(&a.smin[s], lmin[t]);
@@ -252,7 +270,10 @@ __global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
   int32_t c = 0, t = -1, r = 0;
   bool lead = false;
   if (act) {
-    const int32_t rp = a.smin[a.slot_of[i]];
+    const int32_t sl = a.slot_of[i];
+    const int32_t rp = a.pbits ? (int32_t)(reinterpret_cast<const u64*>(a.table)[sl] &
+                                           ((1ull << a.pbits) - 1ull))
+                               : a.smin[sl];
     c = a.cid[rp - a.m0];
     a.cls[i] = c;
     if (rp == (int32_t)i) a.rep[c] = (int32_t)i;
@@ -523,6 +544,7 @@ struct JoinSide {
   const u64* ctab;
   uint32_t ctmask;
   const int32_t* csmin;
+  int cpb;               // the classification's pod bits (ClsSide::pbits)
   const int32_t* ccid;
   i64 cm0;
   const int32_t* kbits;   // bits per key (keys_d + KS)
@@ -618,8 +640,9 @@ __device__ __forceinline__ void join_match_item(i64 P, const JoinPair& pr, int s
       for (;;) {
         const u64 cur = a.ctab[s];
         if (cur == ~0ull) break;
-        if (cur == key) {
-          st = (i64)a.NM * a.U + a.ccid[a.csmin[s] - a.cm0];   // (the iota block)
+        if ((a.cpb ? cur >> a.cpb : cur) == key) {
+          const int32_t r = a.cpb ? (int32_t)(cur & ((1ull << a.cpb) - 1ull)) : a.csmin[s];
+          st = (i64)a.NM * a.U + a.ccid[r - a.cm0];   // (the iota block)
           len = 1;
           break;
         }

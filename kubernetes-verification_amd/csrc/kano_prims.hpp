@@ -148,7 +148,9 @@ struct ScanJob {
   // pod m0 + x's class segment, loff[c + 1] - loff[c] with c = gslot[m0 + x]
   // (policy_shadow's pairs per pod: gslot = the row classes)
   int gen;
+  int gpb;              // gen = 1 with pod-in-slot tables: the member is gtab[slot]'s low gpb bits
   const int32_t* gsmin;
+  const u64* gtab;
   const int32_t* gslot;
   const i64* gloff;
   i64 gm0;
@@ -244,7 +246,11 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
   for (int k = 0; k < SCAN_ITEMS; ++k) {
     const i64 x = base + k;
     if (x >= jb.n) v[k] = 0;
-    else if (jb.gen == 1) v[k] = jb.gsmin[jb.gslot[jb.gm0 + x]] == (int32_t)(jb.gm0 + x) ? 1 : 0;
+    else if (jb.gen == 1) {
+      const int32_t sl = jb.gslot[jb.gm0 + x];
+      const int32_t r = jb.gpb ? (int32_t)(jb.gtab[sl] & ((1ull << jb.gpb) - 1ull)) : jb.gsmin[sl];
+      v[k] = r == (int32_t)(jb.gm0 + x) ? 1 : 0;
+    }
     else if (jb.gen == 2) {
       const int32_t c = jb.gslot[jb.gm0 + x];
       v[k] = jb.gloff[c + 1] - jb.gloff[c];
