@@ -22,11 +22,14 @@ strong scaling (fixed cluster).
 
 Rank 0 prints ONE JSON line.  roofline: the dominant kernel is k_rows (the
 matrix write), algorithmic bytes = 8 * rows * W (the bit matrix it writes),
-timed with HIP events on the engine's stream.  cpu_baseline: the oracle's C
-port of the reference (oracle/kano_oracle.c, 1 core) timed on a bounded
-sample of the same cluster and extrapolated by the reference's own cost laws
-(build linear in policies, each column check linear in columns, shadow linear
-in pair tests).
+timed with HIP events recorded by its own dispatch on its stream.
+cpu_baseline: kano_py's algorithm over the WHOLE cluster (oracle/kano_cpu.c,
+OpenMP, on every host thread the process gets; its outputs checked against
+kano_py's record before the time counts), measured, not extrapolated.
+
+--gpus N > 1 without torch.distributed.run runs the N row shards as members of
+one kano_group in this process (KANO_DEVICES=0,0 puts two members on one
+device: the exchange is then device copies).
 """
 import argparse
 import json
@@ -310,9 +313,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus N > 1 needs torch.distributed.run with N processes")
+    # --gpus N > 1 without torch.distributed.run: one process over N devices
+    # (kano_group, SURVEY.md §8(b) kano_init(ngpu)): KANO_DEVICES (comma-
+    # separated) or devices 0..N-1
+    group = world == 1 and args.gpus > 1
     import torch
     dist = None
     if world > 1 or (args.shard_path and "RANK" in os.environ):
@@ -333,6 +337,8 @@ def main():
     tables = tables_from_cluster(cl)
     n = cl.n
     gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
+    if group:
+        return group_main(args, torch, cl, tables, gid, shadow)
     from kano.shard import row_range
     r0, r1 = row_range(n, world, rank)
     if args.rank_of > 1:
@@ -528,6 +534,128 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if verified is False:
+        sys.exit(f"bench: results differ from the golden: {vdetail}")
+
+
+class GroupStep:
+    """The hot path over N devices in ONE process: kano_group_verify (every
+    member's row shard built and checked at once on its own host thread, the
+    members' column words exchanged -- ncclAllGather over xGMI between
+    distinct devices, device copies between members sharing one -- and
+    combined on every member; kano/multi.py MultiBuild)."""
+
+    def __init__(self, eng, gid, n, shadow):
+        from kano._engine import PinnedBuffer
+        self.eng, self.n = eng, n
+        self.shadow = shadow != "off"
+        self.count_only = shadow == "count"
+        eng.set_groups(gid)
+        self.idx = np.empty(4 * max(n, 1), np.int32)
+        self.pin = None
+        self.pin_pairs = 0
+        self.PinnedBuffer = PinnedBuffer
+        self.results = {}
+        self.verify_max_ms = 0.0
+
+    def __call__(self):
+        pairs = None
+        if self.shadow and not self.count_only:
+            if self.pin is None:
+                self.pin_pairs = 1 << 20
+                self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+                self.pairs_view = self.pin.view(np.int32, 2 * self.pin_pairs)
+            pairs = self.pairs_view
+        tv = time.perf_counter()
+        r = self.eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=self.idx,
+                            shadow_count_only=self.count_only)
+        self.verify_max_ms = max(self.verify_max_ms, (time.perf_counter() - tv) * 1e3)
+        res = {k: r[k] for k in ("all_reachable", "all_isolated", "user_crosscheck",
+                                 "system_isolation") if r[k] is not None}
+        if self.shadow:
+            cnt = r["shadow_count"]
+            res["policy_shadow"] = r["pairs"]
+            res["policy_shadow_count"] = cnt
+            if not self.count_only and cnt > self.pin_pairs:
+                self.pin.close()
+                self.pin_pairs = 2 * cnt
+                self.pin = self.PinnedBuffer(self.pin_pairs * 8)
+                self.pairs_view = self.pin.view(np.int32, 2 * self.pin_pairs)
+        self.results = res
+        return res
+
+
+def group_main(args, torch, cl, tables, gid, shadow):
+    """bench.py --gpus N (N > 1) without torch.distributed.run: the N row
+    shards as members of one kano_group in this process; one JSON line."""
+    from kano.multi import MultiBuild, requested_devices
+    N = args.gpus
+    devices = requested_devices(N) or list(range(N))
+    n = cl.n
+    t_up = time.perf_counter()
+    eng = MultiBuild(tables, N, devices=devices, path=args.path, build=False)
+    up_ms = (time.perf_counter() - t_up) * 1e3
+    step = GroupStep(eng, gid, n, shadow)
+    for _ in range(args.warmup):
+        step()
+    for m in eng.members:
+        m.rows_timing(reset=True)
+    import gc
+    gc.collect()
+    gc.disable()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    marks = []
+    for _ in range(args.steps):
+        step()
+        marks.append(time.perf_counter())
+    for d in sorted(set(devices)):
+        torch.cuda.synchronize(d)
+    elapsed = time.perf_counter() - t0
+    gc.enable()
+    step_ms = np.diff(np.array([t0] + marks)) * 1e3
+    W = (n + 63) // 64
+    rows = []
+    for m, (a, b) in zip(eng.members, eng.bounds):
+        rt = m.rows_timing()
+        ms = rt["sum_ms"] / rt["launches"] if rt["launches"] else float("nan")
+        rows.append({"rows": [a, b], "avg_launch_ms": ms, "launches": rt["launches"],
+                     "achieved": 8.0 * (b - a) * W / (ms * 1e-3) / 1e9 if ms > 0 else 0.0})
+    # the dominant kernel's roofline: member 0's matrix write (its row shard)
+    r0 = rows[0]
+    verified, vdetail = verify_against_golden(args.config, cl, step.results, 1, 0, 0, shadow)
+    out = {
+        "metric": METRIC, "value": float(n) * n / (elapsed / args.steps), "unit": "pod-pairs/s",
+        "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": WORKLOADS[args.config], "name": args.config, "pods": n,
+                   "policies": cl.P, "mode": cl.mode, "seed": cl.seed,
+                   "parallelism": f"rows{N} in one process (kano_group, {eng.mode})",
+                   "devices": devices, "path": args.path,
+                   "exchange": eng.mode,
+                   "checks": "all_reachable, all_isolated, user_crosscheck(tenant), "
+                             "system_isolation(0)" +
+                             {"pairs": ", policy_shadow (pairs to the host)",
+                              "count": ", policy_shadow (pair count only)", "off": ""}[shadow]},
+        "verified": verified, "verified_against": vdetail,
+        "upload_ms": {"group_create_and_tables": round(up_ms, 3)},
+        "roofline": {"bound": "hbm", "kernel": "k_rows (member 0)", "achieved": r0["achieved"],
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": r0["achieved"] / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": 8.0 * (r0["rows"][1] - r0["rows"][0]) * W,
+                     "avg_launch_ms": r0["avg_launch_ms"], "launches_timed": r0["launches"],
+                     "members": rows},
+        "step_ms": {"min": round(float(step_ms.min()), 4),
+                    "median": round(float(np.median(step_ms)), 4),
+                    "p90": round(float(np.percentile(step_ms, 90)), 4),
+                    "max": round(float(step_ms.max()), 4),
+                    "engine_call_max": round(step.verify_max_ms, 4)},
+        "result_sizes": {k: int(len(v)) for k, v in step.results.items()
+                         if hasattr(v, "__len__")},
+    }
+    print(json.dumps(out), flush=True)
+    eng.close()
     if verified is False:
         sys.exit(f"bench: results differ from the golden: {vdetail}")
 

@@ -385,19 +385,29 @@ int kano_host_times(kano_ctx* ctx, double* out /* 20 */, int reset);
 /* One process over G devices (SURVEY.md §8(b) kano_init(ngpu), §8(e) row
  * sharding; no reference counterpart: kano_py is single-process).  The group
  * owns G member contexts, member r on device devices[r] (NULL: r) with its
- * own stream; the caller uploads the inputs to every member and gives member
- * r its row shard (kano_set_shard) -- kano/multi.py does both.  The column
- * checks exchange the members' [OR | cross | NAND] words: ncclAllGather over
- * xGMI (communicators from ncclCommInitAll) when the devices are distinct
- * and RCCL loads (mode 1), device-to-device copies otherwise (mode 2, e.g.
- * G members on one device; env KANO_GROUP_COPY forces it); every member ORs
- * the gathered words on its device.  Members run on one host thread each.
+ * own streams, each driven by its own persistent host thread (started with
+ * the group): a group call hands every member its part and returns when all
+ * are done, so the members' uploads, builds and host syncs overlap.  The
+ * column checks exchange the members' [OR | cross | NAND] words: ncclAllGather
+ * over xGMI (communicators from ncclCommInitAll) when the devices are
+ * distinct and RCCL loads (mode 1), device-to-device copies otherwise (mode
+ * 2, e.g. G members on one device; env KANO_GROUP_COPY forces it); every
+ * member ORs the gathered words on its device.
+ *   kano_group_upload: kano_set_pods (+ kano_set_expressions when E > 0) +
+ *     kano_set_policies on every member, member r's rows [bounds[2r],
+ *     bounds[2r+1]) (kano_set_shard) -- the inputs of ReachabilityMatrix.
+ *     build_matrix (kano_py/kano/model.py:125-165), all members at once.
+ *   kano_group_build: kano_build on every member at once (the whole matrix).
+ *   kano_group_set_groups: kano_set_groups on every member (user_hashmap's
+ *     groups, algorithm.py:20-24); kano_group_verify / _checks then take
+ *     gid = NULL, ngroups = KANO_STORED_GROUPS.
  *   kano_group_verify: kano_verify over the whole matrix -- the three
  *     column lists (all_reachable, all_isolated, user_crosscheck) of every
  *     row, system_isolation(sys_row) from the row's owner, policy_shadow's
  *     pairs concatenated in rank order (= the reference's container order);
  *     arguments as kano_verify_shard / kano_verify_combine (with_shadow 0 /
- *     1 pairs / 2 count only).
+ *     1 pairs / 2 count only).  One hand-off: every member's shard step, the
+ *     exchange between two barriers of the member threads, every combine.
  *   kano_group_checks: the same checks over the members' matrices as they
  *     stand (kano_checks_shard), no policy_shadow.
  * kano_group_info: out[0] = G, out[1] = exchange mode. */
@@ -407,6 +417,14 @@ void kano_group_destroy(kano_group* g);
 const char* kano_group_last_error(const kano_group* g);
 int  kano_group_info(kano_group* g, int32_t* out /* 2 */);
 int  kano_group_member(kano_group* g, int r, kano_ctx** ctx);
+int  kano_group_upload(kano_group* g, int64_t n, int32_t ncols, const int32_t* pod_val,
+                       int32_t E, const int32_t* ecol, const int32_t* eop, const int64_t* eoff,
+                       const int32_t* evals, int64_t P, const int64_t* sel_off,
+                       const int32_t* sel_col, const int32_t* sel_val, const int64_t* alw_off,
+                       const int32_t* alw_col, const int32_t* alw_val,
+                       const int64_t* bounds /* 2 G */);
+int  kano_group_build(kano_group* g, int path);
+int  kano_group_set_groups(kano_group* g, const int32_t* gid, int32_t ngroups);
 int  kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngroups,
                        int64_t sys_row, int with_shadow, int32_t* idx, int64_t* counts,
                        int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count);

@@ -1,0 +1,513 @@
+// kano_group.hip -- one process over G devices (SURVEY.md §8(b) kano_init(ngpu),
+// §8(e) row sharding; the C ABI of include/kano_hip.h, kano_group_*).
+//
+// A group owns G member contexts; member r holds rows [r0_r, r1_r) of M on
+// device dev[r] with its own streams.  The build needs no communication
+// (kano_py/kano/model.py:125-165 per row shard); the column checks
+// (algorithm.py:4-42) exchange each member's [OR | cross | NAND] words
+// (3 W u64): ncclAllGather over xGMI (communicators from ncclCommInitAll)
+// when the G devices are distinct and RCCL loads, else device-to-device
+// copies (G members on one device: the tests) -- and every member ORs the
+// gathered words on its device (kano_verify_combine).
+//
+// Every member runs on its own persistent host thread (a worker per member,
+// started with the group): a call hands the members one job and waits for
+// them, so the members' uploads, builds, host syncs and result copies
+// overlap and no thread is created per call.  A job with an exchange runs it
+// between two worker barriers inside the same hand-off.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kano_hip.h"
+#include "kano_internal.hpp"
+
+using i64 = int64_t;
+using u64 = uint64_t;
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// G workers meet here; sense by generation
+struct SpinBarrier {
+  std::atomic<int> count{0};
+  std::atomic<uint64_t> gen{0};
+  int n = 1;
+  void wait() {
+    const uint64_t g = gen.load(std::memory_order_acquire);
+    if (count.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
+      count.store(0, std::memory_order_relaxed);
+      gen.fetch_add(1, std::memory_order_acq_rel);
+      return;
+    }
+    for (uint32_t s = 1; gen.load(std::memory_order_acquire) == g; ++s) {
+      cpu_relax();
+      if ((s & 0xffff) == 0) std::this_thread::yield();
+    }
+  }
+};
+
+// one persistent host thread per member
+struct Pool {
+  int G = 0;
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<uint64_t> seq{0};
+  std::atomic<int> pending{0};
+  std::atomic<bool> quit{false};
+  const std::function<int(int)>* job = nullptr;
+  std::vector<int> rc;
+  SpinBarrier bar;
+
+  void worker(int r, int dev) {
+    (void)hipSetDevice(dev);
+    uint64_t seen = 0;
+    for (;;) {
+      // spin a little (back-to-back calls hand over within microseconds),
+      // then sleep on the condition variable
+      auto t0 = clk::now();
+      uint64_t s;
+      for (uint32_t k = 1; (s = seq.load(std::memory_order_acquire)) == seen &&
+                           !quit.load(std::memory_order_acquire);
+           ++k) {
+        cpu_relax();
+        if ((k & 0x3ff) == 0 && clk::now() - t0 > std::chrono::milliseconds(2)) {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait_for(lk, std::chrono::milliseconds(100), [&] {
+            return seq.load(std::memory_order_acquire) != seen || quit.load();
+          });
+          t0 = clk::now();
+        }
+      }
+      if (quit.load(std::memory_order_acquire)) return;
+      seen = s;
+      rc[(size_t)r] = (*job)(r);
+      pending.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+
+  void start(const std::vector<int>& dev) {
+    G = (int)dev.size();
+    rc.assign((size_t)G, 0);
+    bar.n = G;
+    for (int r = 0; r < G; ++r) th.emplace_back(&Pool::worker, this, r, dev[(size_t)r]);
+  }
+
+  // run f(r) on every member's worker; returns when all are done
+  void run(const std::function<int(int)>& f) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = &f;
+      pending.store(G, std::memory_order_relaxed);
+      seq.fetch_add(1, std::memory_order_acq_rel);
+    }
+    cv.notify_all();
+    const auto t0 = clk::now();
+    for (uint32_t k = 1; pending.load(std::memory_order_acquire) > 0; ++k) {
+      cpu_relax();
+      if ((k & 0xfff) == 0 && clk::now() - t0 > std::chrono::milliseconds(5))
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    job = nullptr;
+  }
+
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit.store(true, std::memory_order_release);
+    }
+    cv.notify_all();
+    for (auto& t : th)
+      if (t.joinable()) t.join();
+    th.clear();
+  }
+};
+
+typedef int (*NcclCommInitAll)(void**, int, const int*);
+typedef int (*NcclGroupFn)();
+typedef int (*NcclCommDestroy)(void*);
+typedef int (*NcclAllGather)(const void*, void*, size_t, int, void*, hipStream_t);
+constexpr int RCCL_UINT64 = 5;   // ncclUint64 (rccl.h)
+
+struct Rccl {
+  NcclCommInitAll init_all = nullptr;
+  NcclGroupFn group_start = nullptr, group_end = nullptr;
+  NcclCommDestroy destroy = nullptr;
+  NcclAllGather all_gather = nullptr;
+  bool ok() const { return init_all && group_start && group_end && destroy && all_gather; }
+};
+
+const Rccl& rccl_syms() {
+  static Rccl r = [] {
+    Rccl x;
+    x.init_all = reinterpret_cast<NcclCommInitAll>(kano_int::rccl_symbol("ncclCommInitAll"));
+    x.group_start = reinterpret_cast<NcclGroupFn>(kano_int::rccl_symbol("ncclGroupStart"));
+    x.group_end = reinterpret_cast<NcclGroupFn>(kano_int::rccl_symbol("ncclGroupEnd"));
+    x.destroy = reinterpret_cast<NcclCommDestroy>(kano_int::rccl_symbol("ncclCommDestroy"));
+    x.all_gather = reinterpret_cast<NcclAllGather>(kano_int::rccl_symbol("ncclAllGather"));
+    return x;
+  }();
+  return r;
+}
+
+}  // namespace
+
+struct kano_group {
+  int G = 0;
+  std::vector<int> dev;
+  std::vector<kano_ctx*> m;
+  int mode = 2;                       // 1 RCCL all-gather, 2 device copies
+  std::vector<void*> comms;
+  std::vector<hipEvent_t> ev;         // a member's words are written
+  std::vector<void*> xw, xg;          // members' exchange buffers (device)
+  std::string err;
+  std::vector<int32_t*> idx;          // per-member pinned scratch: 4n list entries
+  std::vector<int32_t*> pairs;        // per-member pinned pairs
+  std::vector<i64> pair_cap;
+  i64 idx_n = -1;
+  Pool pool;
+  std::atomic<int> failed{0};         // a member's step failed (inside one job)
+};
+
+#define KANO_GROUP_TRY(expr) \
+  do {                       \
+    const int rc_ = (expr);  \
+    if (rc_) return rc_;     \
+  } while (0)
+
+namespace {
+
+int gfail(kano_group* g, int code, const std::string& msg) {
+  g->err = msg;
+  return code;
+}
+
+// f(r) on every member's worker; the first error wins
+int group_each(kano_group* g, const std::function<int(int)>& f) {
+  g->failed.store(0);
+  g->pool.run(f);
+  // (the member whose step failed first, not the ones it cancelled)
+  for (int pass = 0; pass < 2; ++pass)
+    for (int r = 0; r < g->G; ++r) {
+      const int rc = g->pool.rc[(size_t)r];
+      if (rc && (pass == 1 || rc != -ECANCELED)) {
+        const char* e = kano_last_error(g->m[(size_t)r]);
+        return gfail(g, rc, "member " + std::to_string(r) + ": " + (e ? e : ""));
+      }
+    }
+  return 0;
+}
+
+// inside a job: every member's words are written (on its stream) -> every
+// member's gathered buffer holds all of them, rank-major.  Called by every
+// worker; the workers meet at the barriers even when one failed.
+int member_exchange(kano_group* g, int r, int rc) {
+  const i64 nw = 3 * kano_int::ctx_W(g->m[0]);
+  kano_ctx* c = g->m[(size_t)r];
+  if (rc) g->failed.store(1);
+  if (g->mode == 2 && !rc && nw > 0 && hipEventRecord(g->ev[(size_t)r], kano_int::ctx_stream(c)) != hipSuccess) {
+    g->failed.store(1);
+    rc = kano_int::ctx_fail(c, -EIO, "recording the member's words event failed");
+  }
+  g->pool.bar.wait();
+  if (g->failed.load()) return rc ? rc : -ECANCELED;
+  if (nw > 0 && g->mode == 1) {
+    // one thread issues the grouped all-gather over every communicator
+    if (r == 0) {
+      const Rccl& R = rccl_syms();
+      int e = R.group_start();
+      for (int s = 0; e == 0 && s < g->G; ++s)
+        e = R.all_gather(g->xw[(size_t)s], g->xg[(size_t)s], (size_t)nw, RCCL_UINT64,
+                         g->comms[(size_t)s], kano_int::ctx_stream(g->m[(size_t)s]));
+      const int e2 = R.group_end();
+      if (e || e2) {
+        g->failed.store(1);
+        rc = kano_int::ctx_fail(c, -EIO, "ncclAllGather over the group failed");
+      }
+    }
+  } else if (nw > 0) {
+    // device copies: this member pulls every member's words onto its stream
+    hipStream_t st = kano_int::ctx_stream(c);
+    for (int s = 0; s < g->G && !rc; ++s) {
+      if (hipStreamWaitEvent(st, g->ev[(size_t)s], 0) != hipSuccess ||
+          hipMemcpyAsync(static_cast<u64*>(g->xg[(size_t)r]) + (i64)s * nw, g->xw[(size_t)s],
+                         sizeof(u64) * nw, hipMemcpyDefault, st) != hipSuccess) {
+        g->failed.store(1);
+        rc = kano_int::ctx_fail(c, -EIO, "the words' device copy failed");
+      }
+    }
+  }
+  g->pool.bar.wait();
+  if (g->failed.load()) return rc ? rc : -ECANCELED;
+  return 0;
+}
+
+int group_buffers(kano_group* g) {
+  const i64 n = kano_int::ctx_n(g->m[0]);
+  g->xw.assign((size_t)g->G, nullptr);
+  g->xg.assign((size_t)g->G, nullptr);
+  for (int r = 0; r < g->G; ++r) {
+    kano_ctx* ctx = g->m[(size_t)r];
+    if (kano_int::ctx_n(ctx) != n) return gfail(g, -EINVAL, "members hold different pod counts");
+    if (kano_int::ctx_exchange_buffers(ctx, g->G, &g->xw[(size_t)r], &g->xg[(size_t)r]))
+      return gfail(g, -ENOMEM, "member " + std::to_string(r) + ": " + kano_last_error(ctx));
+  }
+  if (g->idx_n != n) {
+    for (auto p : g->idx) (void)hipHostFree(p);
+    g->idx.assign((size_t)g->G, nullptr);
+    for (int r = 0; r < g->G; ++r)
+      if (hipHostMalloc(reinterpret_cast<void**>(&g->idx[(size_t)r]),
+                        sizeof(int32_t) * (size_t)std::max<i64>(16, 4 * n)) != hipSuccess)
+        return gfail(g, -ENOMEM, "pinned list buffers");
+    g->idx_n = n;
+  }
+  if ((int)g->pairs.size() != g->G) {
+    g->pairs.assign((size_t)g->G, nullptr);
+    g->pair_cap.assign((size_t)g->G, 0);
+  }
+  return 0;
+}
+
+// the global lists from member 0, system_isolation from its owner
+void group_lists(kano_group* g, const std::vector<std::array<int64_t, 4>>& cnt, int32_t* idx,
+                 int64_t* counts) {
+  i64 o = 0;
+  for (int k = 0; k < 3; ++k) {
+    const i64 c = cnt[0][(size_t)k];
+    i64 src = 0;
+    for (int q = 0; q < k; ++q) src += cnt[0][(size_t)q];
+    if (c > 0) std::memcpy(idx + o, g->idx[0] + src, sizeof(int32_t) * (size_t)c);
+    counts[k] = c;
+    o += c;
+  }
+  counts[3] = -1;
+  for (int r = 0; r < g->G; ++r) {
+    const i64 c = cnt[(size_t)r][3];
+    if (c < 0) continue;
+    const i64 src = cnt[(size_t)r][0] + cnt[(size_t)r][1] + cnt[(size_t)r][2];
+    if (c > 0) std::memcpy(idx + o, g->idx[(size_t)r] + src, sizeof(int32_t) * (size_t)c);
+    counts[3] = c;
+    break;
+  }
+}
+
+// member r's page-locked pair buffer, at least cap pairs
+int member_pairs(kano_group* g, int r, i64 cap) {
+  if (g->pairs[(size_t)r] && g->pair_cap[(size_t)r] >= cap) return 0;
+  if (g->pairs[(size_t)r]) (void)hipHostFree(g->pairs[(size_t)r]);
+  g->pairs[(size_t)r] = nullptr;
+  g->pair_cap[(size_t)r] = std::max<i64>(cap, 1 << 16);
+  if (hipHostMalloc(reinterpret_cast<void**>(&g->pairs[(size_t)r]),
+                    sizeof(int32_t) * 2 * (size_t)g->pair_cap[(size_t)r]) != hipSuccess) {
+    g->pair_cap[(size_t)r] = 0;
+    return kano_int::ctx_fail(g->m[(size_t)r], -ENOMEM, "pinned pair buffer");
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kano_group_create(int ngpu, const int* devices, kano_group** out) {
+  if (!out || ngpu < 1) return -EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
+  kano_group* g = new kano_group();
+  g->G = ngpu;
+  for (int r = 0; r < ngpu; ++r) {
+    const int d = devices ? devices[r] : r;
+    if (d < 0 || d >= ndev) {
+      delete g;
+      return -EINVAL;
+    }
+    g->dev.push_back(d);
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (int r = 0; r < ngpu; ++r) {
+    kano_ctx* c = nullptr;
+    const int rc = kano_create(g->dev[(size_t)r], &c);
+    if (rc) {
+      kano_group_destroy(g);
+      (void)hipSetDevice(cur);
+      return rc;
+    }
+    g->m.push_back(c);
+    hipEvent_t e = nullptr;
+    (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    g->ev.push_back(e);
+  }
+  // RCCL over xGMI when the devices are distinct (one communicator per
+  // device, ncclCommInitAll); device copies otherwise
+  std::vector<int> sorted(g->dev);
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  if (ngpu > 1 && distinct && !getenv("KANO_GROUP_COPY")) {
+    const Rccl& R = rccl_syms();
+    if (R.ok()) {
+      g->comms.assign((size_t)ngpu, nullptr);
+      if (R.init_all(g->comms.data(), ngpu, g->dev.data()) == 0) g->mode = 1;
+      else g->comms.clear();
+    }
+  }
+  (void)hipSetDevice(cur);
+  g->pool.start(g->dev);
+  *out = g;
+  return 0;
+}
+
+void kano_group_destroy(kano_group* g) {
+  if (!g) return;
+  g->pool.stop();
+  for (kano_ctx* c : g->m) kano_destroy(c);
+  if (!g->comms.empty()) {
+    const Rccl& R = rccl_syms();
+    for (void* c : g->comms)
+      if (c && R.destroy) (void)R.destroy(c);
+  }
+  for (hipEvent_t e : g->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto p : g->idx) (void)hipHostFree(p);
+  for (auto p : g->pairs)
+    if (p) (void)hipHostFree(p);
+  delete g;
+}
+
+const char* kano_group_last_error(const kano_group* g) { return g ? g->err.c_str() : "null group"; }
+
+int kano_group_info(kano_group* g, int32_t* out /* 2 */) {
+  if (!g || !out) return -EINVAL;
+  out[0] = g->G;
+  out[1] = g->mode;
+  return 0;
+}
+
+int kano_group_member(kano_group* g, int r, kano_ctx** ctx) {
+  if (!g || !ctx || r < 0 || r >= g->G) return -EINVAL;
+  *ctx = g->m[(size_t)r];
+  return 0;
+}
+
+int kano_group_upload(kano_group* g, int64_t n, int32_t ncols, const int32_t* pod_val, int32_t E,
+                      const int32_t* ecol, const int32_t* eop, const int64_t* eoff,
+                      const int32_t* evals, int64_t P, const int64_t* sel_off,
+                      const int32_t* sel_col, const int32_t* sel_val, const int64_t* alw_off,
+                      const int32_t* alw_col, const int32_t* alw_val, const int64_t* bounds) {
+  if (!g) return -EINVAL;
+  if (!bounds) return gfail(g, -EINVAL, "kano_group_upload: bounds NULL");
+  for (int r = 0; r < g->G; ++r)
+    if (bounds[2 * r] < 0 || bounds[2 * r + 1] < bounds[2 * r] || bounds[2 * r + 1] > n)
+      return gfail(g, -EINVAL, "kano_group_upload: bad row range of member " + std::to_string(r));
+  return group_each(g, [&](int r) {
+    kano_ctx* c = g->m[(size_t)r];
+    int rc = kano_set_pods(c, n, ncols, pod_val);
+    if (!rc && E > 0) rc = kano_set_expressions(c, E, ecol, eop, eoff, evals);
+    if (!rc)
+      rc = kano_set_policies(c, P, sel_off, sel_col, sel_val, alw_off, alw_col, alw_val);
+    if (!rc) rc = kano_set_shard(c, bounds[2 * r], bounds[2 * r + 1]);
+    return rc;
+  });
+}
+
+int kano_group_build(kano_group* g, int path) {
+  if (!g) return -EINVAL;
+  return group_each(g, [&](int r) { return kano_build(g->m[(size_t)r], path); });
+}
+
+int kano_group_set_groups(kano_group* g, const int32_t* gid, int32_t ngroups) {
+  if (!g) return -EINVAL;
+  return group_each(g, [&](int r) { return kano_set_groups(g->m[(size_t)r], gid, ngroups); });
+}
+
+int kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngroups,
+                      int64_t sys_row, int with_shadow, int32_t* idx, int64_t* counts,
+                      int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count) {
+  if (!g) return -EINVAL;
+  if (!counts || !idx) return gfail(g, -EINVAL, "kano_group_verify: idx / counts NULL");
+  if (with_shadow && !shadow_count)
+    return gfail(g, -EINVAL, "kano_group_verify: shadow_count NULL with with_shadow");
+  KANO_GROUP_TRY(group_buffers(g));
+  const bool count_only = with_shadow == 2;
+  std::vector<std::array<int64_t, 4>> cnt((size_t)g->G);
+  std::vector<int64_t> sc((size_t)g->G, 0);
+  // one hand-off: every member's build and checks up to its column words,
+  // the exchange between two worker barriers, then every member's combine
+  // (the three global lists, its system row, its policy_shadow pairs)
+  KANO_GROUP_TRY(group_each(g, [&](int r) {
+    kano_ctx* c = g->m[(size_t)r];
+    int rc = kano_verify_shard(c, path, gid, ngroups, sys_row, with_shadow,
+                               static_cast<uint64_t*>(g->xw[(size_t)r]));
+    rc = member_exchange(g, r, rc);
+    if (rc) return rc;
+    int32_t* pp = nullptr;
+    i64 cap = -1;
+    if (with_shadow && !count_only) {
+      if (member_pairs(g, r, 0)) return -ENOMEM;
+      pp = g->pairs[(size_t)r];
+      cap = g->pair_cap[(size_t)r];
+    }
+    rc = kano_verify_combine(c, static_cast<const uint64_t*>(g->xg[(size_t)r]), g->G,
+                             g->idx[(size_t)r], cnt[(size_t)r].data(), pp, cap,
+                             with_shadow ? &sc[(size_t)r] : nullptr);
+    if (rc) return rc;
+    if (pp && sc[(size_t)r] > cap) {   // grow and fetch the member's pairs
+      if (member_pairs(g, r, 2 * sc[(size_t)r])) return -ENOMEM;
+      rc = kano_shadow_fetch(c, g->pairs[(size_t)r]);
+    }
+    return rc;
+  }));
+  group_lists(g, cnt, idx, counts);
+  if (with_shadow) {
+    i64 total = 0;
+    for (int r = 0; r < g->G; ++r) total += sc[(size_t)r];
+    *shadow_count = total;
+    if (!count_only && shadow_pairs && total <= shadow_cap) {
+      i64 o = 0;
+      for (int r = 0; r < g->G; ++r) {
+        if (sc[(size_t)r] > 0)
+          std::memcpy(shadow_pairs + 2 * o, g->pairs[(size_t)r],
+                      sizeof(int32_t) * 2 * (size_t)sc[(size_t)r]);
+        o += sc[(size_t)r];
+      }
+    }
+  }
+  return 0;
+}
+
+int kano_group_checks(kano_group* g, const int32_t* gid, int32_t ngroups, int64_t sys_row,
+                      int32_t* idx, int64_t* counts) {
+  if (!g) return -EINVAL;
+  if (!counts || !idx) return gfail(g, -EINVAL, "kano_group_checks: idx / counts NULL");
+  KANO_GROUP_TRY(group_buffers(g));
+  std::vector<std::array<int64_t, 4>> cnt((size_t)g->G);
+  KANO_GROUP_TRY(group_each(g, [&](int r) {
+    kano_ctx* c = g->m[(size_t)r];
+    int rc = kano_checks_shard(c, gid, ngroups, sys_row, static_cast<uint64_t*>(g->xw[(size_t)r]));
+    rc = member_exchange(g, r, rc);
+    if (rc) return rc;
+    return kano_verify_combine(c, static_cast<const uint64_t*>(g->xg[(size_t)r]), g->G,
+                               g->idx[(size_t)r], cnt[(size_t)r].data(), nullptr, -1, nullptr);
+  }));
+  group_lists(g, cnt, idx, counts);
+  return 0;
+}
+
+}  // extern "C"

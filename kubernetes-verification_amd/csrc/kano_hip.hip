@@ -46,6 +46,7 @@
 #include <thread>
 
 #include "kano_hip.h"
+#include "kano_internal.hpp"
 #include "kano_kernels.hpp"
 #include "kano_path.hpp"
 #include "kano_inc.hpp"
@@ -4408,337 +4409,44 @@ int kano_k8s_edge(kano_ctx* in_t, kano_ctx* eg_t, kano_ctx* dst, int flags, int6
 }  // extern "C"
 
 // ===========================================================================
-// One process, G devices (SURVEY.md §8(b) kano_init(ngpu), §8(e)): a group
-// of G member contexts, member r holding rows [r0_r, r1_r) of M on device
-// dev[r] with its own stream.  The build needs no communication; the column
-// checks exchange each member's [OR | cross | NAND] words (3 * W u64) --
-// ncclAllGather over xGMI (communicators from ncclCommInitAll) when the G
-// devices are distinct and RCCL loads, else device-to-device copies (G
-// members on one device: the tests) -- and every member ORs the gathered
-// words on its device (kano_verify_combine).  Members run on one host thread
-// each, so their host syncs overlap.
+// What the multi-device group (kano_group.hip, its own translation unit)
+// needs of a member context (kano_internal.hpp)
 // ===========================================================================
-struct kano_group {
-  int G = 0;
-  std::vector<int> dev;
-  std::vector<kano_ctx*> m;
-  int mode = 2;                       // 1 RCCL all-gather, 2 device copies
-  std::vector<void*> comms;
-  std::vector<hipEvent_t> ev;         // a member's words are written
-  std::string err;
-  std::vector<int32_t*> idx;          // per-member pinned scratch: 4n list entries
-  std::vector<int32_t*> pairs;        // per-member pinned pairs
-  std::vector<i64> pair_cap;
-  i64 idx_n = -1;
-};
+namespace kano_int {
 
-namespace {
-typedef int (*NcclCommInitAll)(void**, int, const int*);
-typedef int (*NcclGroupFn)();
-typedef int (*NcclCommDestroy)(void*);
-struct Rccl {
-  NcclCommInitAll init_all = nullptr;
-  NcclGroupFn group_start = nullptr, group_end = nullptr;
-  NcclCommDestroy destroy = nullptr;
-  RcclAllGather all_gather = nullptr;
-  bool ok() const { return init_all && group_start && group_end && destroy && all_gather; }
-};
-const Rccl& rccl_syms() {
-  static Rccl r = [] {
-    Rccl x;
+int ctx_device(const kano_ctx* ctx) { return ctx->device; }
+hipStream_t ctx_stream(const kano_ctx* ctx) { return ctx->stream; }
+int64_t ctx_n(const kano_ctx* ctx) { return ctx->n; }
+int64_t ctx_W(const kano_ctx* ctx) { return ctx->W; }
+
+int ctx_fail(kano_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
+
+// the member's exchange buffers: its [OR | cross | NAND] words (3 W u64) and
+// every rank's (3 W nranks), written by the group's exchange -- not an
+// emulated gather's zeros any more (the next comm-NULL kano_verify_gather
+// clears them again)
+int ctx_exchange_buffers(kano_ctx* ctx, int32_t nranks, void** xw, void** xg) {
+  const i64 nw = 3 * ctx->W;
+  KCHK(hipSetDevice(ctx->device));
+  KTRY(dalloc(ctx, ctx->xw, sizeof(u64) * std::max<i64>(1, nw)));
+  KTRY(dalloc(ctx, ctx->xg, sizeof(u64) * std::max<i64>(1, nw * nranks)));
+  ctx->xg_emul = -1;
+  *xw = ctx->xw.p;
+  *xg = ctx->xg.p;
+  return 0;
+}
+
+void* rccl_symbol(const char* name) {
+  static void* h = [] {
     std::string path;
     dl_iterate_phdr(rccl_find_loaded, &path);
-    void* h = nullptr;
-    if (!path.empty()) h = dlopen(path.c_str(), RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) return x;
-    x.init_all = reinterpret_cast<NcclCommInitAll>(dlsym(h, "ncclCommInitAll"));
-    x.group_start = reinterpret_cast<NcclGroupFn>(dlsym(h, "ncclGroupStart"));
-    x.group_end = reinterpret_cast<NcclGroupFn>(dlsym(h, "ncclGroupEnd"));
-    x.destroy = reinterpret_cast<NcclCommDestroy>(dlsym(h, "ncclCommDestroy"));
-    x.all_gather = reinterpret_cast<RcclAllGather>(dlsym(h, "ncclAllGather"));
+    void* x = nullptr;
+    if (!path.empty()) x = dlopen(path.c_str(), RTLD_NOW | RTLD_NOLOAD);
+    if (!x) x = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!x) x = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     return x;
   }();
-  return r;
+  return h ? dlsym(h, name) : nullptr;
 }
 
-int gfail(kano_group* g, int code, const std::string& msg) {
-  g->err = msg;
-  return code;
-}
-
-// run f(r) for every member on its own host thread; the first error wins
-int group_each(kano_group* g, const std::function<int(int)>& f) {
-  std::vector<int> rc((size_t)g->G, 0);
-  std::vector<std::thread> th;
-  th.reserve((size_t)g->G);
-  for (int r = 0; r < g->G; ++r)
-    th.emplace_back([&, r]() {
-      if (hipSetDevice(g->dev[(size_t)r]) != hipSuccess) {
-        rc[(size_t)r] = -EIO;
-        return;
-      }
-      rc[(size_t)r] = f(r);
-    });
-  for (auto& t : th) t.join();
-  for (int r = 0; r < g->G; ++r)
-    if (rc[(size_t)r]) {
-      const char* e = kano_last_error(g->m[(size_t)r]);
-      return gfail(g, rc[(size_t)r], "member " + std::to_string(r) + ": " + (e ? e : ""));
-    }
-  return 0;
-}
-
-// the members' words (xw, written on their streams) to every member's
-// gathered buffer (xg), rank-major
-int group_exchange(kano_group* g) {
-  const i64 nw = 3 * g->m[0]->W;
-  if (nw == 0) return 0;
-  if (g->mode == 1) {
-    const Rccl& R = rccl_syms();
-    if (R.group_start() != 0) return gfail(g, -EIO, "ncclGroupStart failed");
-    for (int r = 0; r < g->G; ++r) {
-      kano_ctx* c = g->m[(size_t)r];
-      if (R.all_gather(c->xw.p, c->xg.p, (size_t)nw, RCCL_UINT64, g->comms[(size_t)r], c->stream) != 0) {
-        (void)R.group_end();
-        return gfail(g, -EIO, "ncclAllGather failed");
-      }
-    }
-    if (R.group_end() != 0) return gfail(g, -EIO, "ncclGroupEnd failed");
-    return 0;
-  }
-  for (int s = 0; s < g->G; ++s) {
-    kano_ctx* c = g->m[(size_t)s];
-    if (hipSetDevice(c->device) != hipSuccess ||
-        hipEventRecord(g->ev[(size_t)s], c->stream) != hipSuccess)
-      return gfail(g, -EIO, "recording a member's words event failed");
-  }
-  for (int r = 0; r < g->G; ++r) {
-    kano_ctx* c = g->m[(size_t)r];
-    if (hipSetDevice(c->device) != hipSuccess) return gfail(g, -EIO, "hipSetDevice failed");
-    for (int s = 0; s < g->G; ++s) {
-      kano_ctx* cs = g->m[(size_t)s];
-      if (hipStreamWaitEvent(c->stream, g->ev[(size_t)s], 0) != hipSuccess ||
-          hipMemcpyAsync(P_<u64>(c->xg) + (i64)s * nw, cs->xw.p, sizeof(u64) * nw, hipMemcpyDefault,
-                         c->stream) != hipSuccess)
-        return gfail(g, -EIO, "the words' device copy failed");
-    }
-  }
-  return 0;
-}
-
-int group_buffers(kano_group* g) {
-  const i64 n = g->m[0]->n, nw = 3 * g->m[0]->W;
-  for (int r = 0; r < g->G; ++r) {
-    kano_ctx* ctx = g->m[(size_t)r];
-    if (ctx->n != n) return gfail(g, -EINVAL, "members hold different pod counts");
-    if (hipSetDevice(ctx->device) != hipSuccess) return gfail(g, -EIO, "hipSetDevice failed");
-    if (dalloc(ctx, ctx->xw, sizeof(u64) * std::max<i64>(1, nw)) ||
-        dalloc(ctx, ctx->xg, sizeof(u64) * std::max<i64>(1, nw * g->G)))
-      return gfail(g, -ENOMEM, "member " + std::to_string(r) + ": " + ctx->err);
-  }
-  if (g->idx_n != n) {
-    for (auto p : g->idx) (void)hipHostFree(p);
-    g->idx.assign((size_t)g->G, nullptr);
-    for (int r = 0; r < g->G; ++r)
-      if (hipHostMalloc(reinterpret_cast<void**>(&g->idx[(size_t)r]),
-                        sizeof(int32_t) * (size_t)std::max<i64>(16, 4 * n)) != hipSuccess)
-        return gfail(g, -ENOMEM, "pinned list buffers");
-    g->idx_n = n;
-  }
-  return 0;
-}
-
-// the global lists from member 0, system_isolation from its owner
-void group_lists(kano_group* g, const std::vector<std::array<int64_t, 4>>& cnt, int32_t* idx,
-                 int64_t* counts) {
-  i64 o = 0;
-  for (int k = 0; k < 3; ++k) {
-    const i64 c = cnt[0][(size_t)k];
-    i64 src = 0;
-    for (int q = 0; q < k; ++q) src += cnt[0][(size_t)q];
-    if (c > 0) std::memcpy(idx + o, g->idx[0] + src, sizeof(int32_t) * (size_t)c);
-    counts[k] = c;
-    o += c;
-  }
-  counts[3] = -1;
-  for (int r = 0; r < g->G; ++r) {
-    const i64 c = cnt[(size_t)r][3];
-    if (c < 0) continue;
-    const i64 src = cnt[(size_t)r][0] + cnt[(size_t)r][1] + cnt[(size_t)r][2];
-    if (c > 0) std::memcpy(idx + o, g->idx[(size_t)r] + src, sizeof(int32_t) * (size_t)c);
-    counts[3] = c;
-    break;
-  }
-}
-}  // namespace
-
-extern "C" {
-
-int kano_group_create(int ngpu, const int* devices, kano_group** out) {
-  if (!out || ngpu < 1) return -EINVAL;
-  *out = nullptr;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
-  kano_group* g = new kano_group();
-  g->G = ngpu;
-  for (int r = 0; r < ngpu; ++r) {
-    const int d = devices ? devices[r] : r;
-    if (d < 0 || d >= ndev) {
-      delete g;
-      return -EINVAL;
-    }
-    g->dev.push_back(d);
-  }
-  for (int r = 0; r < ngpu; ++r) {
-    kano_ctx* c = nullptr;
-    const int rc = kano_create(g->dev[(size_t)r], &c);
-    if (rc) {
-      kano_group_destroy(g);
-      return rc;
-    }
-    g->m.push_back(c);
-    hipEvent_t e = nullptr;
-    (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    g->ev.push_back(e);
-  }
-  // RCCL over xGMI when the devices are distinct (one communicator per
-  // device, ncclCommInitAll); device copies otherwise
-  std::vector<int> sorted(g->dev);
-  std::sort(sorted.begin(), sorted.end());
-  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  if (ngpu > 1 && distinct && !getenv("KANO_GROUP_COPY")) {
-    const Rccl& R = rccl_syms();
-    if (R.ok()) {
-      g->comms.assign((size_t)ngpu, nullptr);
-      if (R.init_all(g->comms.data(), ngpu, g->dev.data()) == 0) g->mode = 1;
-      else g->comms.clear();
-    }
-  }
-  *out = g;
-  return 0;
-}
-
-void kano_group_destroy(kano_group* g) {
-  if (!g) return;
-  for (kano_ctx* c : g->m) kano_destroy(c);
-  if (!g->comms.empty()) {
-    const Rccl& R = rccl_syms();
-    for (void* c : g->comms)
-      if (c && R.destroy) (void)R.destroy(c);
-  }
-  for (hipEvent_t e : g->ev)
-    if (e) (void)hipEventDestroy(e);
-  for (auto p : g->idx) (void)hipHostFree(p);
-  for (auto p : g->pairs)
-    if (p) (void)hipHostFree(p);
-  delete g;
-}
-
-const char* kano_group_last_error(const kano_group* g) { return g ? g->err.c_str() : "null group"; }
-
-int kano_group_info(kano_group* g, int32_t* out /* 2 */) {
-  if (!g || !out) return -EINVAL;
-  out[0] = g->G;
-  out[1] = g->mode;
-  return 0;
-}
-
-int kano_group_member(kano_group* g, int r, kano_ctx** ctx) {
-  if (!g || !ctx || r < 0 || r >= g->G) return -EINVAL;
-  *ctx = g->m[(size_t)r];
-  return 0;
-}
-
-int kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngroups,
-                      int64_t sys_row, int with_shadow, int32_t* idx, int64_t* counts,
-                      int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count) {
-  if (!g) return -EINVAL;
-  if (!counts || !idx) return gfail(g, -EINVAL, "kano_group_verify: idx / counts NULL");
-  if (with_shadow && !shadow_count)
-    return gfail(g, -EINVAL, "kano_group_verify: shadow_count NULL with with_shadow");
-  KTRY(group_buffers(g));
-  // every member's build and checks up to its column words
-  KTRY(group_each(g, [&](int r) {
-    kano_ctx* c = g->m[(size_t)r];
-    return kano_verify_shard(c, path, gid, ngroups, sys_row, with_shadow,
-                             reinterpret_cast<uint64_t*>(c->xw.p));
-  }));
-  KTRY(group_exchange(g));
-  // the combine on every member: the three global lists, its system row,
-  // its policy_shadow pairs (rank order = the reference's order)
-  const bool count_only = with_shadow == 2;
-  if ((int)g->pairs.size() != g->G) {
-    g->pairs.assign((size_t)g->G, nullptr);
-    g->pair_cap.assign((size_t)g->G, 0);
-  }
-  std::vector<std::array<int64_t, 4>> cnt((size_t)g->G);
-  std::vector<int64_t> sc((size_t)g->G, 0);
-  KTRY(group_each(g, [&](int r) {
-    kano_ctx* c = g->m[(size_t)r];
-    int32_t* pp = nullptr;
-    i64 cap = -1;
-    if (with_shadow && !count_only) {
-      if (!g->pairs[(size_t)r]) {
-        g->pair_cap[(size_t)r] = 1 << 16;
-        if (hipHostMalloc(reinterpret_cast<void**>(&g->pairs[(size_t)r]),
-                          sizeof(int32_t) * 2 * (size_t)g->pair_cap[(size_t)r]) != hipSuccess)
-          return fail(c, -ENOMEM, "pinned pair buffer");
-      }
-      pp = g->pairs[(size_t)r];
-      cap = g->pair_cap[(size_t)r];
-    }
-    KTRY(kano_verify_combine(c, reinterpret_cast<const uint64_t*>(c->xg.p), g->G, g->idx[(size_t)r], cnt[(size_t)r].data(), pp,
-                             cap, with_shadow ? &sc[(size_t)r] : nullptr));
-    if (pp && sc[(size_t)r] > cap) {   // grow and fetch the member's pairs
-      (void)hipHostFree(g->pairs[(size_t)r]);
-      g->pairs[(size_t)r] = nullptr;
-      g->pair_cap[(size_t)r] = 2 * sc[(size_t)r];
-      if (hipHostMalloc(reinterpret_cast<void**>(&g->pairs[(size_t)r]),
-                        sizeof(int32_t) * 2 * (size_t)g->pair_cap[(size_t)r]) != hipSuccess)
-        return fail(c, -ENOMEM, "pinned pair buffer");
-      KTRY(kano_shadow_fetch(c, g->pairs[(size_t)r]));
-    }
-    return 0;
-  }));
-  group_lists(g, cnt, idx, counts);
-  if (with_shadow) {
-    i64 total = 0;
-    for (int r = 0; r < g->G; ++r) total += sc[(size_t)r];
-    *shadow_count = total;
-    if (!count_only && shadow_pairs && total <= shadow_cap) {
-      i64 o = 0;
-      for (int r = 0; r < g->G; ++r) {
-        if (sc[(size_t)r] > 0)
-          std::memcpy(shadow_pairs + 2 * o, g->pairs[(size_t)r],
-                      sizeof(int32_t) * 2 * (size_t)sc[(size_t)r]);
-        o += sc[(size_t)r];
-      }
-    }
-  }
-  return 0;
-}
-
-int kano_group_checks(kano_group* g, const int32_t* gid, int32_t ngroups, int64_t sys_row,
-                      int32_t* idx, int64_t* counts) {
-  if (!g) return -EINVAL;
-  if (!counts || !idx) return gfail(g, -EINVAL, "kano_group_checks: idx / counts NULL");
-  KTRY(group_buffers(g));
-  KTRY(group_each(g, [&](int r) {
-    kano_ctx* c = g->m[(size_t)r];
-    return kano_checks_shard(c, gid, ngroups, sys_row, reinterpret_cast<uint64_t*>(c->xw.p));
-  }));
-  KTRY(group_exchange(g));
-  std::vector<std::array<int64_t, 4>> cnt((size_t)g->G);
-  KTRY(group_each(g, [&](int r) {
-    kano_ctx* c = g->m[(size_t)r];
-    return kano_verify_combine(c, reinterpret_cast<const uint64_t*>(c->xg.p), g->G, g->idx[(size_t)r],
-                               cnt[(size_t)r].data(),
-                               nullptr, -1, nullptr);
-  }));
-  group_lists(g, cnt, idx, counts);
-  return 0;
-}
-
-}  // extern "C"
+}  // namespace kano_int

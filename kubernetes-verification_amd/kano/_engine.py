@@ -60,6 +60,7 @@ class DeviceBuild:
                  stream: Optional[int] = None, build: bool = True):
         self.lib = nat.load()
         self.ctx = c_void_p()
+        self._owned = True            # close() destroys the context (not when adopted)
         rc = self.lib.kano_create(int(device), byref(self.ctx))
         if rc != 0:
             self.ctx = c_void_p()
@@ -82,10 +83,12 @@ class DeviceBuild:
     @classmethod
     def adopt(cls, ctx: c_void_p, device: int = 0, path: str = "auto") -> "DeviceBuild":
         """Wrap a context owned elsewhere (a kano_group member, kano/multi.py):
-        its owner destroys it."""
+        its owner destroys it: this wrapper never does (close() only drops
+        the handle)."""
         self = cls.__new__(cls)
         self.lib = nat.load()
         self.ctx = ctx
+        self._owned = False
         self.device = device
         self.path = path
         self._counts = None
@@ -99,7 +102,8 @@ class DeviceBuild:
 
     def close(self):
         if self.ctx:
-            self.lib.kano_destroy(self.ctx)
+            if getattr(self, "_owned", True):
+                self.lib.kano_destroy(self.ctx)
             self.ctx = c_void_p()
 
     def __del__(self):

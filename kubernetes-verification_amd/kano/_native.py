@@ -83,6 +83,11 @@ SIGNATURES = {
     "kano_group_verify": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int64, c_int, c_void_p,
                                   c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     "kano_group_checks": (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
+    "kano_group_upload": (c_int, [c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kano_group_build": (c_int, [c_void_p, c_int]),
+    "kano_group_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),
 }

@@ -91,13 +91,37 @@ class MultiBuild:
             self._chk(self.lib.kano_group_member(self.g, r, byref(ctx)), "kano_group_member")
             m = DeviceBuild.adopt(ctx, device=int(devices[r]) if devices is not None else r,
                                   path=path)
-            m.upload(tables)
-            m.set_rows(*self.bounds[r])
             self.members.append(m)
         self.device = self.members[0].device
         self._idx = None
+        self.upload(tables)
         if build:
             self.build(path)
+
+    def upload(self, t: Tables) -> None:
+        """kano_group_upload: the tables to every member at once, member r's
+        row shard set (the members' own threads)."""
+        self.tables = t
+        self.bounds = shard_bounds(t.n, self.G)
+        pv = np.ascontiguousarray(t.pod_val, dtype=np.int32)
+        ex = [None] * 4
+        E = 0
+        if getattr(t, "expr_col", None) is not None and len(t.expr_col):
+            ex = [np.ascontiguousarray(a, dtype=d) for a, d in (
+                (t.expr_col, np.int32), (t.expr_op, np.int32), (t.expr_off, np.int64),
+                (t.expr_val, np.int32))]
+            E = len(ex[0])
+        arrs = [np.ascontiguousarray(a, dtype=d) for a, d in (
+            (t.sel_off, np.int64), (t.sel_col, np.int32), (t.sel_val, np.int32),
+            (t.alw_off, np.int64), (t.alw_col, np.int32), (t.alw_val, np.int32))]
+        b = np.ascontiguousarray(np.asarray(self.bounds, dtype=np.int64).reshape(-1))
+        self._chk(self.lib.kano_group_upload(self.g, t.n, t.ncols, _ptr(pv), E,
+                                             *[_ptr(a) for a in ex], t.P,
+                                             *[_ptr(a) for a in arrs], _ptr(b)),
+                  "kano_group_upload")
+        for m, (a, bb) in zip(self.members, self.bounds):
+            m.tables = t
+            m.row_span = None if (a, bb) == (0, t.n) else (a, bb)
 
     # -- plumbing -------------------------------------------------------
     def _chk(self, rc, what):
@@ -109,7 +133,7 @@ class MultiBuild:
     def close(self):
         if self.g:
             for m in self.members:
-                m.ctx = c_void_p()          # owned by the group
+                m.close()                   # (adopted: drops the handle; the group owns it)
             self.lib.kano_group_destroy(self.g)
             self.g = c_void_p()
 
@@ -136,8 +160,18 @@ class MultiBuild:
         raise IndexError("row out of range")
 
     def build(self, path: Optional[str] = None) -> None:
-        for m in self.members:
-            m.build(path or self.path)
+        """kano_group_build: every member's row shard at once."""
+        self._chk(self.lib.kano_group_build(self.g, nat.PATHS[path or self.path]),
+                  "kano_group_build")
+
+    def set_groups(self, gid: np.ndarray, ngroups: int = 0) -> None:
+        """kano_group_set_groups: the pods' group ids on every member (then
+        ``verify(gid="stored")``)."""
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        if gid.shape[0] != self.n:
+            raise ValueError("gid must have one entry per pod")
+        self._chk(self.lib.kano_group_set_groups(self.g, _ptr(gid), int(ngroups)),
+                  "kano_group_set_groups")
 
     def info(self) -> dict:
         infos = [m.info() for m in self.members]
@@ -199,7 +233,12 @@ class MultiBuild:
         n = self.n
         if idx is None:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
-        g = None if gid is None else np.ascontiguousarray(gid, dtype=np.int32)
+        ngroups = 0
+        stored = isinstance(gid, str) and gid == "stored"
+        if stored:
+            g, ngroups = None, nat.STORED_GROUPS
+        else:
+            g = None if gid is None else np.ascontiguousarray(gid, dtype=np.int32)
         counts = np.zeros(4, dtype=np.int64)
         cnt = c_int64(0)
         cap = 0 if pairs is None else pairs.size // 2
@@ -207,11 +246,12 @@ class MultiBuild:
             cap = -1
         with_shadow = 0 if not shadow else (2 if shadow_count_only else 1)
         pth = nat.PATHS[path or self.path]
-        self._chk(self.lib.kano_group_verify(self.g, pth, _ptr(g), 0, int(sys_row), with_shadow,
+        self._chk(self.lib.kano_group_verify(self.g, pth, _ptr(g), ngroups, int(sys_row),
+                                             with_shadow,
                                              _ptr(idx), counts.ctypes.data, _ptr(pairs), int(cap),
                                              byref(cnt) if shadow else None), "kano_group_verify")
         out = self._lists(counts, idx)
-        if gid is None:
+        if gid is None and not stored:
             out["user_crosscheck"] = None
         if shadow:
             k = int(cnt.value)

@@ -110,7 +110,14 @@ class ShardExchange:
         """Every rank's words into ``gathered`` (rank order)."""
         torch, dist = self.torch, self.dist
         if dist is None:
+            # (the engine writes the words and reads the gathered buffer on its
+            # own streams when it has them: order the copy through the device)
+            on_dev = self.stream is None and self.words.is_cuda
+            if on_dev:
+                torch.cuda.synchronize()
             self.gathered[:3 * self.W].copy_(self.words)
+            if on_dev:
+                torch.cuda.synchronize()
         elif self.host_staged:
             if self.words.is_cuda:
                 torch.cuda.synchronize()      # the shard's kernels wrote the words

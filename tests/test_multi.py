@@ -84,3 +84,87 @@ def test_group_verify_c2(G):
     c = eng.verify(gid, sys_row=cl.n - 1, shadow=True, shadow_count_only=True)
     assert c["shadow_count"] == exp["policy_shadow"]["count"] and c["pairs"] is None
     eng.close()
+
+
+@pytest.mark.gpu
+def test_group_verify_stored_groups_c2():
+    """kano_group_set_groups + verify("stored") (the bench's form) against
+    kano_py's C2 record."""
+    from kano._intern import tables_from_cluster
+    from kano.multi import MultiBuild
+    from kano.synth import make_config, KEY_NAMES
+    exp = expected("C2")
+    cl = make_config("C2")
+    gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)[1].astype(np.int32)
+    eng = MultiBuild(tables_from_cluster(cl), 2, devices=[0, 0], build=False)
+    eng.set_groups(gid)
+    for _ in range(3):
+        r = eng.verify("stored", sys_row=0, shadow=True)
+        assert r["user_crosscheck"].tolist() == exp["user_crosscheck"]["result"]
+        assert r["all_isolated"].tolist() == exp["all_isolated"]
+        assert r["system_isolation"].tolist() == exp["system_isolation"]["result"]
+        assert sha(np.ascontiguousarray(r["pairs"])) == exp["policy_shadow"]["sha256"]
+    eng.build()       # kano_group_build: every member at once
+    assert sha(eng.rows(0, cl.n)) == exp["M_sha256"]
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_multibuild_failed_init_destroys_group_once(monkeypatch):
+    """A failing upload inside MultiBuild.__init__: the adopted member
+    wrappers never destroy their contexts, the group is destroyed exactly
+    once (double kano_destroy)."""
+    import gc
+    from kano import _native as nat
+    from kano._intern import tables_from_cluster
+    from kano.multi import MultiBuild
+    from kano.synth import make_config
+    lib = nat.load()
+    calls = {"ctx": 0, "group": 0}
+    real_ctx, real_group = lib.kano_destroy, lib.kano_group_destroy
+
+    def ctx_destroy(c):
+        calls["ctx"] += 1
+        return real_ctx(c)
+
+    def group_destroy(g):
+        calls["group"] += 1
+        return real_group(g)
+    monkeypatch.setattr(lib, "kano_destroy", ctx_destroy)
+    monkeypatch.setattr(lib, "kano_group_destroy", group_destroy)
+    t = tables_from_cluster(make_config("C2"))
+    import dataclasses
+    bad = dataclasses.replace(t, sel_col=np.full_like(t.sel_col, t.ncols + 5))
+    with pytest.raises(nat.KanoNativeError, match="term column out of range"):
+        MultiBuild(bad, 2, devices=[0, 0])
+    gc.collect()
+    assert calls == {"ctx": 0, "group": 1}
+    # the device is fine afterwards: a good group on the same tables
+    eng = MultiBuild(t, 2, devices=[0, 0])
+    assert eng.info()["U"] > 0
+    eng.close()
+    assert calls == {"ctx": 0, "group": 2}
+
+
+@pytest.mark.gpu
+def test_bench_group_line_two_members_one_device():
+    """bench.py --gpus 2 without torch.distributed.run: one process, a
+    kano_group of two members (KANO_DEVICES=0,0: device copies), one
+    verified JSON line on C3."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, KANO_DEVICES="0,0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--steps", "20", "--warmup", "3"], capture_output=True, text=True,
+                       timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["verified"] is True
+    assert line["config"]["exchange"] == "device copies"
+    assert line["config"]["devices"] == [0, 0]
+    assert line["value"] > 0 and line["result_sizes"]["policy_shadow"] > 0
