@@ -16,6 +16,19 @@ struct Big {            // a ScanJobsN-sized by-value argument
 __global__ void k_set(int* p, int v) { p[threadIdx.x] = v; }
 __global__ void k_set_big(int* p, Big b) { p[threadIdx.x] = b.v + (int)b.w[99]; }
 
+template <int N>
+__global__ void k_tset(int* p, Big b) { p[threadIdx.x] = b.v + N; }
+
+// the engine's round-3 launch helper as it was (commit 2a907f0): the handle
+// form with an event, the triple-chevron form without
+template <typename... KArgs, typename... Args>
+__attribute__((noinline)) void launch_marked_r3(void (*kernel)(KArgs...), dim3 grid, dim3 block,
+                                                size_t lds, hipStream_t st, hipEvent_t ev,
+                                                Args... args) {
+  if (ev) hipExtLaunchKernelGGL(kernel, grid, block, lds, st, nullptr, ev, 0, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+}
+
 template <typename... KArgs, typename... Args>
 __attribute__((noinline)) void via_ptr(void (*kernel)(KArgs...), hipStream_t st, Args... args) {
   hipLaunchKernelGGL(kernel, dim3(1), dim3(64), 0, st, args...);
@@ -62,6 +75,15 @@ int main() {
   bad += !check("function pointer <<<>>>, 808-B arg", d, 11, st);
   via_handle(k_set_big, st, d, b);
   bad += !check("by handle, 808-B arg", d, 11, st);
+  hipEvent_t ev;
+  (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  b.v = 20;
+  launch_marked_r3(k_tset<2>, dim3(1), dim3(64), 0, st, (hipEvent_t) nullptr, d, b);
+  bad += !check("r3 helper, template, no event", d, 22, st);
+  launch_marked_r3(k_tset<3>, dim3(1), dim3(64), 0, st, ev, d, b);
+  bad += !check("r3 helper, template, event", d, 23, st);
+  launch_marked_r3(k_tset<4>, dim3(2), dim3(64), 0, st, (hipEvent_t) nullptr, d, b);
+  bad += !check("r3 helper, template, no event, 2 blk", d, 24, st);
   std::printf("%s\n", bad ? "SOME LAUNCHES DID NOTHING" : "all launches dispatched");
   return bad ? 1 : 0;
 }
