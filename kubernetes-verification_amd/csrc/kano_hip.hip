@@ -289,6 +289,13 @@ struct kano_ctx {
   bool vs_open = false, vs_shadow = false, vs_cross_want = false, vs_cross_on = false;
   bool vs_have_sys = false, vs_sys_on = false;
   bool vs_rows = false;      // the combine writes the shard's rows (not after kano_checks_shard)
+  // one rank's kano_verify: the four lists written by the column pass itself
+  // (k_verify_cols_f: row r at idxd[r * n], its look-back states in vcst --
+  // two parity regions of 2 + 4 x tiles words, each launch zeroing the other)
+  bool vs_fused = false;
+  DBuf vcst;
+  i64 vc_cap = 0;
+  int vc_parity = 0;
   i64 vs_nb = 0, vs_rl = 0;
 };
 
@@ -2021,7 +2028,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
-                  &ctx->irows,  &ctx->xw,      &ctx->xg};
+                  &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->vcst};
   for (DBuf* b : bufs) dfree(*b);
   RowsInputs& ra = ctx->rin_alt;
   for (DBuf* b : {&ra.wioff, &ra.wicls, &ra.soffc, &ra.slist, &ra.aloff, &ra.alist, &ra.alcoff,
@@ -3112,9 +3119,37 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
       fa.r0 = ctx->r0;
       fa.r1 = ctx->r1;
     }
-    hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
+    ctx->vs_fused = !words_dev;
+    if (ctx->vs_fused) {
+      // one rank: the lists in this pass (k_verify_cols_f), no count scan
+      const i64 vtiles = std::max<i64>(1, nblk(W * 64, VC_TILE)), region = 2 + 4 * vtiles;
+      if (ctx->vc_cap < region) {
+        KTRY(dalloc(ctx, ctx->vcst, sizeof(u64) * 2 * (size_t)region));
+        KCHK(hipMemsetAsync(ctx->vcst.p, 0, sizeof(u64) * 2 * (size_t)region, ctx->stream));
+        ctx->vc_cap = region;
+        ctx->vc_parity = 0;
+      }
+      u64* st = P_<u64>(ctx->vcst);
+      FusedTail ft{};
+      ft.status = st + (ctx->vc_parity ? ctx->vc_cap : 0);
+      ft.clear = st + (ctx->vc_parity ? 0 : ctx->vc_cap);
+      ft.nclear = region;
+      ctx->vc_parity ^= 1;
+      ft.idx = P_<int32_t>(ctx->idxd);
+      ft.totals = P_<u64>(ctx->sizes) + SZ_IDX0;
+      ft.totals_host = ctx->gmirror_dev ? ctx->gmirror_dev + SZ_IDX0 : nullptr;
+      if (ctx->gmirror_dev) {
+        ft.pub_src[ft.npub] = P_<u64>(ctx->sizes) + SZ_ERR;
+        ft.pub_dst[ft.npub++] = ctx->gmirror_dev + SZ_ERR;
+      }
+      hipLaunchKernelGGL(k_verify_cols_f, dim3((unsigned)vtiles), dim3(TPB), 0, ctx->stream, fa,
+                         ft);
+    } else {
+      hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
+    }
     KLAUNCH();
   } else {
+    ctx->vs_fused = false;
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
   }
   // (issued after the column checks: the engine stream does not wait for it)
@@ -3176,7 +3211,8 @@ int spin_event(kano_ctx* ctx, hipEvent_t e) {
 // end is ev_pairs)
 int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts,
                        int32_t* shadow_pairs, void* pairs_h, int64_t shadow_cap,
-                       int64_t* shadow_count, bool async, bool compacted = false) {
+                       int64_t* shadow_count, bool async, bool compacted = false,
+                       bool fused = false) {
   using clk = std::chrono::steady_clock;
   auto tmark = clk::now();
   auto part = [&](int k) {
@@ -3190,6 +3226,20 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
   hipStream_t st = ctx->stream;
   const i64 nf = ctx->nflags, nt = (nf + SH_TILE - 1) / SH_TILE;
   i64 out_cap = 0;
+  const bool pairs_job = pairs_mode && pairs_h && rl > 0;
+  const u64* tots = P_<u64>(ctx->sizes) + SZ_IDX0;
+  if (fused) {
+    // the lists travel first, while policy_shadow's tail still runs on
+    // stream2 (the link is the bound: ~0.8 MB of lists, ~0.55 MB of pairs at
+    // C3); row r is at idxd[r * n], concatenated on the host
+    CopySegs cl{};
+    for (int r = 0; r < 4; ++r)
+      cl.j[r] = CopySeg{static_cast<const char*>(ctx->idxd.p) + sizeof(int32_t) * r * n,
+                        static_cast<char*>(idx_h), tots + r, 1, tots, r, 4, 4 * n};
+    hipExtLaunchKernelGGL(k_copy_segs, dim3(256, 4), dim3(TPB), 0, st, nullptr,
+                          pairs_job ? nullptr : ctx->ev_tail, 0, cl);
+    KLAUNCH();
+  }
   if (pairs_mode) {
     // L never exceeds the candidate pairs; out keeps the largest total seen
     KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nf)));
@@ -3211,21 +3261,25 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
       KLAUNCH();
     }
   }
-  CopyJobs cj{};
-  cj.j[0] = CopyJob{static_cast<const char*>(ctx->idxd.p), static_cast<char*>(idx_h),
-                    P_<u64>(ctx->sizes) + SZ_IDX0, 4, 4, 4 * n};
-  int njobs = 1;
-  if (pairs_mode && pairs_h && rl > 0) {
-    cj.j[1] = CopyJob{static_cast<const char*>(ctx->out.p), static_cast<char*>(pairs_h),
-                      reinterpret_cast<const u64*>(P_<i64>(ctx->poff) + rl), 1, 8,
-                      std::min<i64>(shadow_cap, out_cap)};
-    njobs = 2;
+  // the lists (one job, or one per row when the column pass wrote row r at
+  // idxd[r * n]) and the pairs; the copy's own dispatch marks ev_tail (no
+  // separate record: ~3 us less on the engine stream), which also starts the
+  // matrix write
+  CopySegs cj{};
+  int njobs = 0;
+  if (!fused)
+    cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->idxd.p), static_cast<char*>(idx_h),
+                            tots, 4, nullptr, 0, 4, 4 * n};
+  if (pairs_job) {
+    cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->out.p), static_cast<char*>(pairs_h),
+                            reinterpret_cast<const u64*>(P_<i64>(ctx->poff) + rl), 1, nullptr, 0,
+                            8, std::min<i64>(shadow_cap, out_cap)};
   }
-  // the copy's own dispatch marks ev_tail (no separate record: ~3 us less on
-  // the engine stream), which also starts the matrix write
-  hipExtLaunchKernelGGL(k_copy_out_dev, dim3(256, njobs), dim3(TPB), 0, st, nullptr, ctx->ev_tail,
-                        0, cj);
-  KLAUNCH();
+  if (njobs > 0) {
+    hipExtLaunchKernelGGL(k_copy_segs, dim3(256, njobs), dim3(TPB), 0, st, nullptr, ctx->ev_tail,
+                          0, cj);
+    KLAUNCH();
+  }
   if (ctx->vs_rows) {
     ctx->rows_overlap = async;
     ctx->rows_in = ctx->ev_tail;
@@ -3317,14 +3371,20 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KLAUNCH();
   }
   // the four result rows as index lists: all_reachable, all_isolated,
-  // user_crosscheck, system_isolation
-  for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
-    KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
-                SZ_IDX0 + r));
-  sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
+  // user_crosscheck, system_isolation (one rank: already written by the
+  // column pass, k_verify_cols_f, with the totals and the group-id check in
+  // the host mirror)
+  const bool fused = ctx->vs_fused && !gathered;
+  if (!fused) {
+    for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
+      KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
+                  SZ_IDX0 + r));
+    sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
+  }
   // (an earlier scan's total: one host signal for all; the side scans store
   // their totals to the host directly)
   if (want_shadow && !compacted) sb.publish(SZ_NL);
+  if (sb.jobs.count == 0) ctx->sig_armed = 0;   // (no scan raises the signal: an event)
   KTRY(sb.run());
   IdxRows ir{};
   ir.W = W;
@@ -3337,7 +3397,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   ir.row[3] = ctx->vs_sys_on ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
-  if (n > 0 && W > 0) {
+  if (n > 0 && W > 0 && !fused) {
     hipLaunchKernelGGL(k_idx_write, dim3((unsigned)nb, 4), dim3(TPB), 0, ctx->stream, ir,
                        P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
     KLAUNCH();
@@ -3351,7 +3411,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // host redoes it sized (first call, or a larger output).
   if (direct)
     return verify_back_direct(ctx, idx, idx_h, counts, shadow_pairs, pairs_h, shadow_cap,
-                              shadow_count, may_async && ctx->async_rows, compacted);
+                              shadow_count, may_async && ctx->async_rows, compacted, fused);
   // the list sizes, policy_shadow's sizes and the group check travel to the
   // host: it waits on the signal (or the event) only, then queues the tail
   // (policy_shadow's compaction and emission, the copies) on stream2 and the
@@ -3409,7 +3469,16 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     *shadow_count = total;
   }
   tmark = clk::now();
-  if (nidx > 0) KTRY(copy_out(ctx, idx, idx_dev, sizeof(int32_t) * nidx, cs));
+  if (fused) {   // row r at idxd[r * n]: the rows' copies, concatenated
+    i64 o = 0;
+    for (int r = 0; r < 4; ++r) {
+      const i64 c = std::max<i64>(0, counts[r]);
+      if (c > 0) KTRY(copy_out(ctx, idx + o, idx_dev + (i64)r * n, sizeof(int32_t) * c, cs));
+      o += c;
+    }
+  } else if (nidx > 0) {
+    KTRY(copy_out(ctx, idx, idx_dev, sizeof(int32_t) * nidx, cs));
+  }
   part(15);
   if (want_shadow && shadow_pairs && total > 0 && total <= shadow_cap)
     KTRY(copy_out(ctx, shadow_pairs, ctx->out.p, sizeof(int2) * total, cs));

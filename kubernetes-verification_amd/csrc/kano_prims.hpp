@@ -323,6 +323,68 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
   }
 }
 
+// Look-back for NJ scans that share their tiles: wave w publishes the
+// aggregates of jobs w, w + 4, ... of this tile and sums each job's
+// predecessors back to the nearest inclusive prefix (64 predecessors per
+// round, as k_scan_lb).  st: job q's tile states at st[q * tiles + t];
+// tot / excl: LDS, NJ entries each.  Every thread of the block calls it.
+template <int NJ>
+__device__ __forceinline__ void lookback_jobs(u64* st, i64 tiles, i64 tile, const i64* tot,
+                                              i64* excl) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int jq = wid; jq < NJ; jq += TPB / 64) {
+    u64* ts = st + (i64)jq * tiles;
+    const i64 t = tot[jq];
+    i64 ex = 0;
+    if (tile == 0) {
+      if (lane == 0) lb_store(&ts[0], LB_INC | ((u64)t & LB_VAL));
+    } else {
+      if (lane == 0) lb_store(&ts[tile], LB_AGG | ((u64)t & LB_VAL));
+      for (i64 q0 = tile - 1;; q0 -= 64) {
+        const i64 q = q0 - lane;
+        u64 w = LB_INC;
+        if (q >= 0) {
+          do { w = lb_load(&ts[q]); } while (w == 0);
+        }
+        const u64 inc = __ballot((w & ~LB_VAL) == LB_INC);
+        const int f = inc ? __ffsll((long long)inc) - 1 : 63;
+        ex += wave_sum(lane <= f ? (i64)(w & LB_VAL) : (i64)0);
+        if (inc) break;
+      }
+      if (lane == 0) lb_store(&ts[tile], LB_INC | ((u64)(ex + t) & LB_VAL));
+    }
+    if (lane == 0) excl[jq] = ex;
+  }
+  __syncthreads();
+}
+
+// True in exactly one block of the launch -- the last to get here.  Every
+// other block's memory operations before its call have completed by then
+// (each block waits for its own -- s_waitcnt -- before it counts itself), so
+// the last block reads their atomics' results with atomic loads.  No
+// agent-scope fence: on gfx950 it writes back and invalidates the whole L2
+// (buffer_wbl2 / buffer_inv sc1), per block.
+__device__ __forceinline__ bool last_block_done(u64* done_ctr, i64 nblocks) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u64 old =
+        __hip_atomic_fetch_add(done_ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old + 1 == (u64)nblocks;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// job q's total after every tile has looked back: the last tile's inclusive
+// state (st as lookback_jobs)
+__device__ __forceinline__ i64 lookback_total(u64* st, i64 tiles, int q) {
+  u64 w;
+  do { w = lb_load(&st[(i64)q * tiles + tiles - 1]); } while ((w & ~LB_VAL) != LB_INC);
+  return (i64)(w & LB_VAL);
+}
+
 // several fills in one launch: (ptr, count of 32-bit words, value)
 struct FillJob {
   uint32_t* ptr;

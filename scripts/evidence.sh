@@ -102,7 +102,7 @@ for step in ${STEPS:-tests b20}; do
         rm -rf gpurun_out/tr_$label
         KANO_TUNE="$tune" timeout -k 10 200 rocprofv3 --kernel-trace ${HIPTR:+--hip-trace} --stats \
           -d gpurun_out/tr_$label -o run --output-format csv -- \
-          python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --cold 0 $args > gpurun_out/tr_$label.log 2>&1 \
+          python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --cold 0 --alone 0 $args > gpurun_out/tr_$label.log 2>&1 \
           || { echo "$label failed"; tail -5 gpurun_out/tr_$label.log; exit 1; }
         python3 scripts/steps_tl.py "$(find gpurun_out/tr_$label -name "*kernel_trace.csv" | head -1)" \
           > gpurun_out/tl_$label.txt && tail -50 gpurun_out/tl_$label.txt

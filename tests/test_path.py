@@ -8,7 +8,7 @@ vectors; the GPU path (libkano_hip.so kano_path) must equal it bit for bit."""
 import numpy as np
 import pytest
 
-from _golden import cluster, expected, rows01_to_words
+from _golden import cluster, expected, rows01_to_words, sha
 
 
 def _rand_words(n, density, seed):
@@ -246,3 +246,47 @@ def test_path_c2_scale():
     again = DeviceBuild.empty(n)
     again.path_from(dst, 0, "auto")
     assert np.array_equal(again.rows(0, n), C)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["s_sparse_2000", "q_wide_select", "paper_example"])
+def test_entry_points_after_verify(name):
+    """Repeated kano_verify calls (asynchronous completion, the input sets
+    alternating), then the entry points that read the build's class-level
+    matrix Mc on the same context -- the standalone crosscheck, the path's
+    one-hop table -- agree with the oracle, and a verify after them too."""
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids
+    from kano import model
+    from kano.synth import objects_from_json
+    from kano._bits import set_bit_indices
+    from oracle import kano_oracle as orc
+    if name == "paper_example":
+        from sample import paper_example
+        cs, ps = paper_example()
+        label = "app"
+    else:
+        cs, ps = objects_from_json(cluster(name), model)
+        label = expected(name)["label"]
+    eng = DeviceBuild(intern(cs, ps), build=False)
+    n = eng.n
+    gid = group_ids(cs, label)
+    exp = expected(name)
+    for _ in range(3):
+        r = eng.verify(gid, sys_row=0, shadow=True)
+        assert r["user_crosscheck"].tolist() == exp["user_crosscheck"]["result"]
+        assert r["all_isolated"].tolist() == exp["all_isolated"]
+        assert r["system_isolation"].tolist() == exp["system_isolation"]["result"]
+    M = eng.rows(0, n)
+    assert sha(M) == exp["M_sha256"]
+    # Mc-based entry points on the same context
+    assert set_bit_indices(eng.crosscheck(gid), n).tolist() == exp["user_crosscheck"]["result"]
+    ref, _ = orc.path_c(M, n, 2)
+    dst = DeviceBuild.empty(n)
+    dst.path_from(eng, 2, "bitwise")
+    assert np.array_equal(dst.rows(0, n), ref)
+    # and a verify again after them
+    r = eng.verify(gid, sys_row=n - 1, shadow=True)
+    assert r["all_reachable"].tolist() == exp["all_reachable"]
+    dst.close()
+    eng.close()
