@@ -53,6 +53,8 @@ WORKLOADS = {
     "C3": "Synthetic 100k pods / 10k policies, sparse selectors (BASELINE configs[2])",
     "C4": "Synthetic 100k pods / 10k policies, broad namespace-wide selectors (BASELINE configs[3])",
     "C5": "Synthetic 1M pods / 100k policies, sparse selectors (BASELINE configs[4])",
+    "D1": "Synthetic 100k pods / 10k policies, dense selectors (4 tenants, 2,000 apps; the "
+          "MFMA path's line, not a BASELINE config)",
 }
 
 
@@ -332,7 +334,7 @@ def main():
 
     shadow = "off" if args.no_shadow else args.shadow
     if shadow == "auto":
-        shadow = "count" if args.config == "C4" else "pairs"
+        shadow = "count" if args.config in ("C4", "D1") else "pairs"
     cl = make_config(args.config)
     tables = tables_from_cluster(cl)
     n = cl.n
@@ -482,7 +484,10 @@ def main():
                                    if ra["launches"] else None)},
             # the dense path's int8 MFMA contraction (k_heavy_mc_mfma; --path
             # mfma or AUTO's dense choice): algorithmic ops / its event time
-            "mfma_roofline": ({"bound": "mfma", "kernel": "k_heavy_mc_mfma",
+            "mfma_roofline": ({"bound": "mfma",
+                               "kernel": {1: "k_heavy_mc_or (bitwise, timed for comparison)",
+                                          2: "k_heavy_mc_mfma (split K)",
+                                          3: "k_heavy_gemm"}.get(info["HEAVY_KERNEL"], "none"),
                                "achieved": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12,
                                "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
                                "frac": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12 /

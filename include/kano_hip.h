@@ -59,7 +59,9 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the list-based row kernel */
 #define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 2 k_rows, 0 none yet */
 #define KANO_INFO_ROWS_CUS 14   /* CUs the last matrix write's stream may use  */
-#define KANO_INFO_NSLOTS   15
+#define KANO_INFO_HEAVY_SEL 15  /* sum of |S(c)| over the heavy classes       */
+#define KANO_INFO_HEAVY_KERNEL 16 /* 0 none, 1 k_heavy_mc_or, 2 k_heavy_mc_mfma (split K), 3 k_heavy_gemm */
+#define KANO_INFO_NSLOTS   17
 
 /* Lifetime.  No reference counterpart: the reference keeps its state in
  * Python objects (kano_py/kano/model.py:167-169 ReachabilityMatrix.__init__). */

@@ -102,7 +102,7 @@ struct SideMatch {
 // counters) and read by the host with one copy per sync
 enum {
   SZ_UR = 0, SZ_UA, SZ_NNZ_SEL, SZ_NNZ_ALC, SZ_NNZ_ALW, SZ_NFLAGS, SZ_WI, SZ_HEAVY, SZ_MAXSEL,
-  SZ_LIGHT, SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 17,
+  SZ_LIGHT, SZ_HSEL, SZ_NL, SZ_PAIRS, SZ_IDX0, SZ_IDX1, SZ_IDX2, SZ_IDX3, SZ_ERR, SZ_SLOTS = 18,
   SZ_SIGNAL = SZ_SLOTS   // host mirror only: the scans' host signal word
 };
 
@@ -141,6 +141,14 @@ struct kano_ctx {
                              // holds more than path_dens % of the class-level bits
   int path_tm = 2;           // pathtm / pathtn: k_path_mfma tiles per wave
   int path_tn = 2;
+  int heavy_gemm = 22;       // hgemm: k_heavy_gemm's wave tile (TM TN: 22, 42, 44; 0: the
+                             // split-K kernel whatever the size)
+  // AUTO's dense-path rates (xomfma TOP/s, xoor GB/s): the GEMM's int8 ops
+  // and the bitwise OR's Mc-word reads per second, as measured on the
+  // crossover sweep (scripts/mfma_sweep.py)
+  double xo_mfma = 800e12, xo_or = 3000e9;
+  i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
+  int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
@@ -160,10 +168,12 @@ struct kano_ctx {
   SideMatch sm, am;          // selector side, allow side
   i64 UAW = 0, ldC = 0;      // words per class-level row (column classes)
   i64 nnz_sel = 0, nnz_alc = 0, nnz_alw = 0, heavy_count = 0, wi_total = 0, nflags = 0;
+  i64 heavy_sel = 0;         // sum of |S(c)| over the heavy classes (the bitwise OR's work)
   i64 light_cost = 0;        // allowed-pod entries the light classes' rows read
   bool rows_use_alist = false;
   int max_sel = 0;
   int heavy_path = 0;        // 1 bitwise, 2 mfma (last build)
+  int heavy_kernel = 0;      // KANO_INFO_HEAVY_KERNEL (last build)
   int rows_kernel = 0;       // the last matrix write: 2 k_rows, 0 none
 
   DBuf pv;
@@ -1148,6 +1158,7 @@ int do_front(kano_ctx* ctx, int path) {
     a.sq = P_<i64>(ctx->sq);
     a.maxs = reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_MAXSEL);  // low half
     a.light = P_<unsigned long long>(ctx->sizes) + SZ_LIGHT;
+    a.hsel = P_<unsigned long long>(ctx->sizes) + SZ_HSEL;
     hipLaunchKernelGGL(k_class_plan, dim3(nblk(Ur)), dim3(TPB), 0, ctx->stream, a);
     KLAUNCH();
   }
@@ -1160,14 +1171,15 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(sb.add(P_<i64>(ctx->sq), Ur, P_<i64>(ctx->pfoff), SZ_NFLAGS));
   sb.publish(SZ_MAXSEL);   // k_class_plan's atomics, for the host's sync 2
   sb.publish(SZ_LIGHT);
+  sb.publish(SZ_HSEL);
   KTRY(sb.run());
   return 0;
 }
 
 // host sync 2 of the build: every list size at once
 int read_sizes(kano_ctx* ctx) {
-  i64 v[SZ_LIGHT - SZ_NNZ_SEL + 1];
-  KTRY(mirror_wait(ctx, SZ_NNZ_SEL, SZ_LIGHT - SZ_NNZ_SEL + 1, v));
+  i64 v[SZ_HSEL - SZ_NNZ_SEL + 1];
+  KTRY(mirror_wait(ctx, SZ_NNZ_SEL, SZ_HSEL - SZ_NNZ_SEL + 1, v));
   ctx->nnz_sel = v[SZ_NNZ_SEL - SZ_NNZ_SEL];
   ctx->nnz_alc = v[SZ_NNZ_ALC - SZ_NNZ_SEL];
   ctx->nnz_alw = v[SZ_NNZ_ALW - SZ_NNZ_SEL];
@@ -1176,6 +1188,7 @@ int read_sizes(kano_ctx* ctx) {
   ctx->heavy_count = v[SZ_HEAVY - SZ_NNZ_SEL];
   ctx->max_sel = (int)(v[SZ_MAXSEL - SZ_NNZ_SEL] & 0xffffffff);
   ctx->light_cost = v[SZ_LIGHT - SZ_NNZ_SEL];
+  ctx->heavy_sel = v[SZ_HSEL - SZ_NNZ_SEL];
   return 0;
 }
 
@@ -1260,18 +1273,36 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
 // contraction; column checks at class level
 int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra) {
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
+  // the dense contraction's kernel: the tiled GEMM when it has enough wave
+  // tiles to fill the chip without a split, else the split-K kernel
+  const int tmg = ctx->heavy_gemm / 10, tng = ctx->heavy_gemm % 10;
+  const bool gemm_fits = tmg > 0 && ctx->PB * 8 * (TPB / 64) <= 64 * 1024 &&
+                         ((H + 32 * tmg - 1) / (32 * tmg)) *
+                                 ((ctx->cc.U + 32 * tng - 1) / (32 * tng)) >=
+                             ctx->heavy_gemm_min;
   ctx->heavy_path = 0;
   bool mfma = false;
   if (H > 0) {
     mfma = path == KANO_PATH_MFMA;
     if (path == KANO_PATH_AUTO) {
-      // the MFMA walks every policy for every heavy row, the OR only S(c):
-      // dense when the average |S(c)| is a large share of P
-      const double avg_s = (double)ctx->nnz_sel / std::max<i64>(1, U);
-      mfma = H >= 32 && ctx->cc.U >= 64 && avg_s * 16.0 >= (double)P;
+      if (gemm_fits) {
+        // the MFMA does 2 H P Ua ops whatever the density, the OR reads
+        // ldMc words per (heavy class, policy in S(c)): the cheaper by the
+        // measured rates ("The dense path: crossover")
+        const double t_mfma = 2.0 * (double)H * (double)P * (double)ctx->cc.U / ctx->xo_mfma;
+        const double t_or = 8.0 * (double)ctx->heavy_sel * (double)ldMc / ctx->xo_or;
+        mfma = t_mfma < t_or;
+      } else {
+        // (the split-K kernel, few heavy rows: dense when the average |S(c)|
+        // is a large share of P)
+        const double avg_s = (double)ctx->nnz_sel / std::max<i64>(1, U);
+        mfma = H >= 32 && ctx->cc.U >= 64 && avg_s * 16.0 >= (double)P;
+      }
     }
     ctx->heavy_path = mfma ? 2 : 1;
   }
+  const bool gemm = mfma && gemm_fits;
+  ctx->heavy_kernel = H == 0 ? 0 : !mfma ? 1 : gemm ? 3 : 2;
   FillJobs carried{};
   {
     FillBatch fb(ctx);
@@ -1282,9 +1313,11 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     KTRY(dalloc(ctx, ctx->wicls, sizeof(int32_t) * std::max<i64>(1, ctx->wi_total)));
     if (mfma) {
       KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, ctx->PB * ctx->cc.U)));
-      KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, ctx->PB * U)));
       KTRY(fb.add(ctx->ACT, sizeof(u64) * ctx->PB * ctx->cc.U, 0u));
-      KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
+      // (the GEMM's A is written whole by k_heavy_selT: no fill)
+      const i64 aw = gemm ? ctx->PB * H : ctx->PB * U;
+      KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, aw)));
+      if (!gemm) KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
     }
     if (extra) KTRY(extra(fb));   // the caller's fills (kano_verify: crosscheck, shadow)
     // (carried by k_sel_place's launch: it neither reads nor writes them)
@@ -1394,13 +1427,43 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                          P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                          P_<int32_t>(ctx->am.gmem), Ua, P_<u64>(ctx->ACT));
       KLAUNCH();
-      // class-major selector bits: selT[pb][c]
-      hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
-                         P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
-                         P_<int32_t>(ctx->sm.gmem), U, P_<u64>(ctx->scratch_words));
-      KLAUNCH();
+      // class-major selector bits: selT[pb][c] (the split-K kernel's A; the
+      // GEMM builds its own, heavy rows only)
+      if (!gemm) {
+        hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                           P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                           P_<int32_t>(ctx->sm.gmem), U, P_<u64>(ctx->scratch_words));
+        KLAUNCH();
+      }
       const u64* selT = P_<u64>(ctx->scratch_words);
       uint32_t* out = reinterpret_cast<uint32_t*>(P_<u64>(ctx->Mc));
+      if (gemm) {
+        // many heavy rows: the tiled GEMM, no split-K, on the heavy rows'
+        // own select bits (A, from the sorted S(c) lists)
+        const i64 nb = ((H + 64 * tmg - 1) / (64 * tmg)) * ((Ua + 64 * tng - 1) / (64 * tng));
+        const dim3 grid((unsigned)(8 * ((nb + 7) / 8)));
+        const int32_t* hl = P_<int32_t>(ctx->hlist);
+        u64* A = P_<u64>(ctx->scratch_words);
+        hipLaunchKernelGGL(k_heavy_selT, dim3(nblk(H, TPB / 64)), dim3(TPB),
+                           sizeof(u64) * (size_t)ctx->PB * (TPB / 64), ctx->stream, hl, H,
+                           P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), ctx->PB, A);
+        KLAUNCH();
+        KTRY(resolve_mfma_time(ctx));
+        KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
+        if (ctx->heavy_gemm == 22)
+          hipLaunchKernelGGL((k_heavy_gemm<2, 2>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        else if (ctx->heavy_gemm == 44)
+          hipLaunchKernelGGL((k_heavy_gemm<4, 4>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        else
+          hipLaunchKernelGGL((k_heavy_gemm<4, 2>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
+                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        KLAUNCH();
+        KCHK(hipEventRecord(ctx->ev_m1, ctx->stream));
+        ctx->mfma_time_pending = true;
+        ctx->mfma_ops_last = 2.0 * (double)H * (double)P * (double)Ua;
+      } else {
       // split K (policy blocks) so that the launch has ~2048 waves whatever
       // the number of 32-column tiles
       const i64 tiles = 2 * ldMc;
@@ -1432,11 +1495,23 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       // algorithmic work: the heavy rows' boolean product over every policy,
       // 2 ops (multiply, add) per (row class, policy, column class)
       ctx->mfma_ops_last = 2.0 * (double)H * (double)P * (double)Ua;
+      }
     } else {
+      // (timed like the contraction when asked, hortime=1: the same
+      // algorithmic work, for the dense-path crossover, scripts/mfma_sweep.py)
+      if (ctx->time_or) {
+        KTRY(resolve_mfma_time(ctx));
+        KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
+      }
       hipLaunchKernelGGL(k_heavy_mc_or, dim3((unsigned)H, nblk(ldMc, 64)), dim3(TPB), 0, ctx->stream,
                          P_<int32_t>(ctx->hlist), P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
                          P_<u64>(ctx->AC), ctx->ldC, ctx->UAW, P_<u64>(ctx->Mc), ldMc);
       KLAUNCH();
+      if (ctx->time_or) {
+        KCHK(hipEventRecord(ctx->ev_m1, ctx->stream));
+        ctx->mfma_time_pending = true;
+        ctx->mfma_ops_last = 2.0 * (double)H * (double)P * (double)ctx->cc.U;
+      }
     }
   }
   if (!ctx->cols_deferred) KTRY(mc_cols(ctx));
@@ -1911,6 +1986,11 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
+        if (k == "hgemm" && (v == 0 || v == 22 || v == 42 || v == 44)) ctx->heavy_gemm = v;
+        if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
+        if (k == "hortime") ctx->time_or = v;
+        if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
+        if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
       }
       pos = end + 1;
     }
@@ -2420,6 +2500,8 @@ int kano_info(kano_ctx* ctx, int64_t* out) {
   out[KANO_INFO_UA] = ctx->cc.U;
   out[KANO_INFO_HEAVY_PATH] = ctx->heavy_path;
   out[KANO_INFO_ROWS_CUS] = ctx->rows_cus;
+  out[KANO_INFO_HEAVY_SEL] = ctx->heavy_sel;
+  out[KANO_INFO_HEAVY_KERNEL] = ctx->heavy_kernel;
   out[KANO_INFO_WORK_ITEMS] = ctx->wi_total;
   out[KANO_INFO_ROWS_KERNEL] = ctx->rows_kernel;
   return 0;

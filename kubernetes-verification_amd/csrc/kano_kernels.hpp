@@ -1375,6 +1375,7 @@ struct ClassPlan {
   i64* sq;                 // out |S(c)|^2 for classes with local members
   int32_t* maxs;           // out max |S(c)| over classes with local members
   unsigned long long* light;  // out sum of cost * chunks over light classes
+  unsigned long long* hsel;   // out sum of |S(c)| over heavy classes
 };
 
 // A light class rebuilds its row per member chunk by scattering its allowed
@@ -1383,7 +1384,7 @@ struct ClassPlan {
 __global__ __launch_bounds__(TPB) void k_class_plan(ClassPlan a) {
   const i64 c = (i64)blockIdx.x * TPB + threadIdx.x;
   int32_t smax = 0;
-  unsigned long long light = 0;
+  unsigned long long light = 0, hsel = 0;
   if (c < a.U) {
     const int32_t s = a.scnt[c];
     const int32_t m = a.mcnt[c];
@@ -1399,26 +1400,31 @@ __global__ __launch_bounds__(TPB) void k_class_plan(ClassPlan a) {
     a.sq[c] = m > 0 ? (i64)s * s : 0;
     if (m > 0) smax = s;
     if (m > 0 && !hv) light = (unsigned long long)cost * (unsigned long long)chunks;
+    if (hv) hsel = (unsigned long long)s;
   }
   // one atomic pair per block (per wave, the two slots took ~700 contended
   // atomics on C3)
-  __shared__ unsigned long long sl[TPB / 64];
+  __shared__ unsigned long long sl[TPB / 64], sh[TPB / 64];
   __shared__ int32_t sx[TPB / 64];
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) smax = max(smax, __shfl_xor(smax, d, 64));
   light = wave_sum(light);
+  hsel = wave_sum(hsel);
   if ((threadIdx.x & 63) == 0) {
     sl[threadIdx.x >> 6] = light;
+    sh[threadIdx.x >> 6] = hsel;
     sx[threadIdx.x >> 6] = smax;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < TPB / 64; ++w) {
       light += sl[w];
+      hsel += sh[w];
       smax = max(smax, sx[w]);
     }
     if (smax > 0) atomicMax(a.maxs, smax);
     if (light) atomicAdd(a.light, light);
+    if (hsel) atomicAdd(a.hsel, hsel);
   }
 }
 
@@ -1544,6 +1550,130 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
       }
     }
   }
+}
+
+// The GEMM's A operand, heavy rows only: A[pb][h] bit q = policy 64 pb + q
+// selects heavy class hlist[h] -- one wave per heavy class sets the bits of
+// its (sorted) S(c) in an LDS column of PB words, then stores the column
+// (PB x H words; the k_classbits form sets U-wide columns with one global
+// atomic per select entry, 2e7 of them at the dense sweep's largest point).
+// LDS: PB words per wave (dynamic).
+__global__ __launch_bounds__(TPB) void k_heavy_selT(const int32_t* __restrict__ hlist, i64 H,
+                                                    const i64* __restrict__ soffc,
+                                                    const int32_t* __restrict__ slist, i64 PB,
+                                                    u64* __restrict__ A) {
+  extern __shared__ __attribute__((aligned(16))) u64 col[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const i64 h = (i64)blockIdx.x * (TPB / 64) + wv;
+  if (h >= H) return;                                 // wave-uniform; no block barrier
+  u64* cw = col + (i64)wv * PB;
+  for (i64 w = lane; w < PB; w += 64) cw[w] = 0ull;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  const int32_t c = hlist[h];
+  const i64 e1 = soffc[c + 1];
+  for (i64 e = soffc[c] + lane; e < e1; e += 64) {
+    const int32_t p = slist[e];
+    atomicOr(&cw[p >> 6], 1ull << (p & 63));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  for (i64 w = lane; w < PB; w += 64) A[w * H + h] = cw[w];
+}
+
+// The dense contraction at scale (many heavy row classes, broad selectors):
+// Mc[h][ca] = (sum_p Sel[h][p] Allow[p][ca] > 0) as an int8 GEMM tiled like
+// k_path_mfma -- one wave = (32 TM heavy rows) x (32 TN column classes), each
+// A fragment feeding TN MFMAs and each B fragment TM (the bit -> byte
+// expansion, VALU, is what bounds a narrow tile); block = 2 x 2 waves; K = all
+// policies, 64 per step, no split (the grid has >= HEAVY_GEMM_MIN_TILES wave
+// tiles).  A is the heavy rows' select bits [pb][h] (k_heavy_selT), B is
+// ACT[pb][ca]; both coalesced.  Every (row, 32-column word) belongs to one wave: plain stores
+// of the thresholded ballots into the zeroed Mc.  Blocks of one XCD (blockIdx
+// mod 8) walk a contiguous range of the tile order (GM block-rows at a time)
+// so that they share A and B panels in their L2.
+constexpr i64 HEAVY_GEMM_MIN_TILES = 512;
+template <int TM, int TN>
+__global__ __launch_bounds__(TPB) void k_heavy_gemm(const u64* __restrict__ A,
+                                                    const int32_t* __restrict__ hlist, i64 H,
+                                                    const u64* __restrict__ ACT, i64 Ua, i64 PB,
+                                                    uint32_t* __restrict__ Mc32, i64 ldMc) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  constexpr i64 GM = 8;
+  const i64 nbm = (H + 64 * TM - 1) / (64 * TM), nbn = (Ua + 64 * TN - 1) / (64 * TN);
+  const i64 total = nbm * nbn, per = (total + 7) / 8;
+  const i64 L = (i64)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= total) return;                             // block-uniform
+  const i64 grp = L / (GM * nbn), first = grp * GM;
+  const i64 gm = nbm - first < GM ? nbm - first : GM;
+  const i64 in = L - grp * GM * nbn;
+  const i64 bm = first + in % gm, bn = in / gm;
+  const int wv = threadIdx.x >> 6;
+  const i64 rb = (bm * 2 + (wv >> 1)) * 32 * TM, cb = (bn * 2 + (wv & 1)) * 32 * TN;
+  if (rb >= H || cb >= Ua) return;                    // wave-uniform; no block barrier
+  i64 rowv[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) rowv[t] = rb + 32 * t + l32;
+  i64 colv[TN];
+#pragma unroll
+  for (int u = 0; u < TN; ++u) colv[u] = cb + 32 * u + l32;
+  i32x16 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0;
+  // the next K step's words are loaded while this one's MFMAs run
+  u64 an[TM], bn_[TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) an[t] = rowv[t] < H ? A[rowv[t]] : 0ull;
+#pragma unroll
+  for (int u = 0; u < TN; ++u) bn_[u] = colv[u] < Ua ? ACT[colv[u]] : 0ull;
+  for (i64 kw = 0; kw < PB; ++kw) {
+    u64 aw[TM], bw[TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) aw[t] = an[t];
+#pragma unroll
+    for (int u = 0; u < TN; ++u) bw[u] = bn_[u];
+    if (kw + 1 < PB) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) an[t] = rowv[t] < H ? A[(kw + 1) * H + rowv[t]] : 0ull;
+#pragma unroll
+      for (int u = 0; u < TN; ++u) bn_[u] = colv[u] < Ua ? ACT[(kw + 1) * Ua + colv[u]] : 0ull;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int sh = ks * 32 + half * 16;
+      i32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) af[t] = expand16((uint32_t)(aw[t] >> sh) & 0xffffu);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) bf[u] = expand16((uint32_t)(bw[u] >> sh) & 0xffffu);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[t], bf[u], acc[t][u], 0, 0, 0);
+    }
+  }
+  // accumulator g of lane (l32, half): row (g&3) + 8 (g>>2) + 4 half, column
+  // l32 of its 32 x 32 tile; one ballot per g holds 32 columns of two rows
+  const i64 ld32 = 2 * ldMc;
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const i64 row = rb + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
+      const int32_t hr = row < H ? hlist[row] : -1;
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const u64 bal = __ballot(acc[t][u][g] > 0);
+        const i64 c32 = (cb + 32 * u) >> 5;
+        if (l32 == 0 && hr >= 0 && c32 < ld32)
+          Mc32[(i64)hr * ld32 + c32] = half ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+      }
+    }
 }
 
 // expansion: M[first member of heavy class h] bit j = Mc[h][cla[j]]; one wave

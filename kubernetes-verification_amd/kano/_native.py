@@ -92,9 +92,10 @@ SIGNATURES = {
     "kano_host_free": (None, [c_void_p]),
 }
 
-INFO_SLOTS = 15
+INFO_SLOTS = 17
 INFO = dict(N=0, W=1, P=2, U=3, NNZ_SEL=4, NNZ_ALW=5, HEAVY=6, ROW0=7, ROW1=8, MAXSEL=9,
-            UA=10, HEAVY_PATH=11, WORK_ITEMS=12, ROWS_KERNEL=13, ROWS_CUS=14)
+            UA=10, HEAVY_PATH=11, WORK_ITEMS=12, ROWS_KERNEL=13, ROWS_CUS=14,
+            HEAVY_SEL=15, HEAVY_KERNEL=16)
 PATHS = {"auto": 0, "bitwise": 1, "mfma": 2}
 STORED_GROUPS = -1   # KANO_STORED_GROUPS
 

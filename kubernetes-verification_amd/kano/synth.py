@@ -26,6 +26,14 @@ Policies pick ingress/egress with p=0.5.  ``sparse`` (C2, C3, C5): select =
 gets, w.p. 1%, an extra term whose key no pod carries (exercises quirk Q1,
 `kano_py/kano/model.py:143,146`).
 
+``dense`` (D1, the MFMA crossover sweep): egress only, ``tenants`` uniform
+tenants and ``apps`` uniform apps drawn independently per pod; a share
+``broad`` of the policies select and allow {tenant} of a (intra-tenant), the
+rest select {tenant, app} of a and allow {tenant, app} of b (which makes
+(tenant, app) the row and column classes).  Every row class is then selected by ~broad*P/tenants
+policies: the class x policy selector matrix is dense, the regime where the
+int8 MFMA contraction beats the bitwise OR ("The dense path").
+
 The generator emits integer tables directly (what the engine consumes) and can
 materialise the same cluster as kano API objects / JSON, so the host interning
 path and the direct-table path are checked against each other in tests.
@@ -57,6 +65,8 @@ CONFIGS = {
     "C3": (100_000, 10_000, "sparse", 1),
     "C4": (100_000, 10_000, "broad", 2),
     "C5": (1_000_000, 100_000, "sparse", 3),
+    # the dense-path config (not in BASELINE.json: the MFMA crossover's bench line)
+    "D1": (100_000, 10_000, "dense", 4, {"tenants": 4, "apps": 2000, "broad": 0.9}),
 }
 
 
@@ -155,7 +165,9 @@ class Cluster:
 
 
 def make_cluster(n: int, P: int, mode: str = "sparse", seed: int = 0,
-                 absent_frac: float = 0.01) -> Cluster:
+                 absent_frac: float = 0.01, **dense) -> Cluster:
+    if mode == "dense":
+        return make_dense(n, P, seed, absent_frac=absent_frac, **dense)
     if mode not in ("sparse", "broad"):
         raise ValueError(f"unknown mode {mode!r}")
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -219,9 +231,44 @@ def make_cluster(n: int, P: int, mode: str = "sparse", seed: int = 0,
     return Cluster(n, P, mode, seed, vals, ingress, so, sk, sv, ao, ak, av)
 
 
+def make_dense(n: int, P: int, seed: int = 0, tenants: int = 4, apps: int = 2000,
+               broad: float = 0.9, absent_frac: float = 0.01) -> Cluster:
+    """The ``dense`` mode (module docstring): few uniform tenants, broad
+    intra-tenant {tenant} policies plus narrow {tenant, app} ones, egress."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nk = len(KEY_NAMES)
+    vals = np.full((nk, n), -1, dtype=np.int32)
+    vals[K_TENANT] = rng.integers(0, tenants, size=n)
+    vals[K_APP] = rng.integers(0, apps, size=n)
+    vals[K_NS] = vals[K_APP] % 16
+    vals[K_ROLE] = rng.integers(0, N_ROLES, size=n)
+    ingress = np.zeros(P, dtype=bool)
+    a = rng.integers(0, n, size=P)
+    b = rng.integers(0, n, size=P)
+    is_broad = rng.random(P) < broad
+    abs_s = rng.random(P) < absent_frac
+    abs_a = rng.random(P) < absent_frac
+
+    def build(side_a: bool):
+        off, key, val = [0], [], []
+        for p in range(P):
+            pod = a[p] if (side_a or is_broad[p]) else b[p]
+            for k in ((K_TENANT,) if is_broad[p] else (K_TENANT, K_APP)):
+                key.append(k); val.append(int(vals[k, pod]))
+            if (abs_s[p] if side_a else abs_a[p]):
+                key.append(-1); val.append(-1)
+            off.append(len(key))
+        return (np.asarray(off, np.int64), np.asarray(key, np.int32),
+                np.asarray(val, np.int32))
+
+    so, sk, sv = build(True)
+    ao, ak, av = build(False)
+    return Cluster(n, P, "dense", seed, vals, ingress, so, sk, sv, ao, ak, av)
+
+
 def make_config(name: str) -> Cluster:
-    n, P, mode, seed = CONFIGS[name]
-    return make_cluster(n, P, mode, seed)
+    n, P, mode, seed, *kw = CONFIGS[name]
+    return make_cluster(n, P, mode, seed, **(kw[0] if kw else {}))
 
 
 def cluster_objects(cl: Cluster, model_module=None):

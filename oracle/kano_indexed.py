@@ -256,6 +256,13 @@ def policy_shadow(ix: Indexed, want_sha: bool = True):
             blk = inter[ug][:, ug].toarray()
             sub = blk == gsize[ug][None, :]          # sub[a, b]: allow_b <= allow_a
             sub |= (gsize[ug] == 0)[None, :]         # the empty set is in every set
+            if not want_sha:
+                # the count alone (D1: ~5e6 pairs per pod): sum over group
+                # pairs of |a| |b| [allow_b <= allow_a], minus the j == k pairs
+                cnt = np.bincount(inv, minlength=ug.shape[0]).astype(np.int64)
+                memo[key] = (int(cnt @ sub.astype(np.int64) @ cnt) - S.shape[0], b"")
+                pair_count[c] = memo[key][0]
+                continue
             m = sub[inv][:, inv]
             np.fill_diagonal(m, False)
             jj, kk = np.nonzero(m)

@@ -218,6 +218,36 @@ def test_c5_full_size_properties():
     assert np.array_equal(np.concatenate(pairs), full["pairs"])
 
 
+# --- D1: the dense path (MFMA GEMM) at full size ----------------------------
+def test_d1_dense_auto_picks_mfma():
+    """D1 (kano/synth.py dense mode: 8,000 row classes, each selected by
+    ~2,250 of 10^4 policies): AUTO takes the int8 MFMA GEMM for the heavy
+    classes, and kano_verify's lists, policy_shadow's count (every subset
+    test; the pairs would be ~5e11) and the digest of every row equal D1's record (tests/golden/make_c5.py,
+    oracle/kano_indexed.py); the bitwise OR writes the same rows."""
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.synth import make_config
+    cl = make_config("D1")
+    exp = expected("D1")
+    assert exp["seed"]["fingerprint"] == cl.fingerprint()
+    eng = DeviceBuild(tables_from_cluster(cl), build=False)
+    eng.set_groups(tenant_groups(cl))
+    r = eng.verify("stored", sys_row=0, shadow=True, shadow_count_only=True)
+    info = eng.info()
+    assert info["HEAVY_PATH"] == 2 and info["HEAVY_KERNEL"] == 3, info   # the MFMA GEMM
+    assert info["HEAVY"] >= 4096, info
+    check_verify(r, exp, shadow=False)
+    assert r["shadow_count"] == exp["policy_shadow"]["count"]   # ~5e11 pairs: the count
+    dig = eng.rows_digest(0, cl.n)
+    assert hashlib.sha256(np.ascontiguousarray(dig, dtype="<u8").tobytes()).hexdigest() == \
+        exp["row_digests_sha256"]
+    eng.verify("stored", sys_row=0, shadow=False, path="bitwise")
+    assert eng.info()["HEAVY_PATH"] == 1
+    assert np.array_equal(eng.rows_digest(0, cl.n), dig)
+    eng.close()
+
+
 # --- the reference generator's clusters (kano_py/tests/generate.py) ----------
 GEN_NAMES = sorted(f[:-5] for f in os.listdir(os.path.join(GOLDEN, "expected"))
                    if f.startswith("gen_"))

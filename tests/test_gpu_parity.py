@@ -115,12 +115,17 @@ def test_golden_cluster_api(name):
 
 @pytest.mark.parametrize("name", ["s_broad_300", "s_broad_1000", "s_sparse_1000",
                                   "s_sparse_2000", "q_dirs", "q_shadow"])
-@pytest.mark.parametrize("path", ["bitwise", "mfma", "auto"])
-def test_build_paths_agree(name, path):
-    """The bitwise (LDS scatter / OR) and int8-MFMA contraction paths give
-    the same matrix and column checks."""
+@pytest.mark.parametrize("path", ["bitwise", "mfma", "auto", "mfma-gemm22", "mfma-gemm42",
+                                  "mfma-gemm44"])
+def test_build_paths_agree(name, path, monkeypatch):
+    """The bitwise (LDS scatter / OR) and int8-MFMA contraction paths -- the
+    split-K kernel and the tiled GEMM in its three wave tiles, forced at
+    these sizes (hgemmmin=1) -- give kano_py's matrix and column checks."""
     from kano._engine import DeviceBuild
     from kano._intern import intern
+    if path.startswith("mfma-gemm"):
+        monkeypatch.setenv("KANO_TUNE", f"hgemm={path[-2:]},hgemmmin=1")
+        path = "mfma"
     obj = cluster(name)
     cs, ps = api_objects(obj)
     exp = expected(name)
@@ -133,6 +138,7 @@ def test_build_paths_agree(name, path):
     assert np.flatnonzero(~words_to_bool(co, n)).tolist() == exp["all_isolated"]
     if path == "mfma":
         assert eng.info()["HEAVY"] > 0 or exp["P"] == 0
+        assert eng.info()["HEAVY_PATH"] == 2 or exp["P"] == 0
     eng.close()
 
 

@@ -39,7 +39,9 @@ def check(path):
                     for b in front:
                         ins_b = rest if first else bl.get(b, [])
                         if any(STUB.search(x) for x in ins_b): ok = True
-                        term = ins_b[-1] if ins_b else ''
+                        # (the block's successors: its terminator, which for a
+                        # switch spans several lines; only terminators name labels)
+                        term = ' '.join(ins_b)
                         for t in re.findall(r'label %([\w.$-]+)', term):
                             if t not in seen: seen.add(t); nxt.append(t)
                     first = False
