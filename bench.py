@@ -197,7 +197,36 @@ def cold_drop_in(cl, config):
     res["policy_shadow_count"] = int(pairs.shape[0])
     verified, _ = verify_against_golden(config, cl, res, 1, 0, 0, "pairs")
     m.engine.close()
+    del m, cs, ps
+    # the same build_matrix in its parts, on fresh objects: host interning,
+    # context creation, upload of the tables, the first build (allocations
+    # included) and a second one (the steady state), the groups of
+    # user_crosscheck
+    from kano._engine import DeviceBuild
+    from kano._intern import intern, group_ids
+    cs, ps = cluster_objects(cl, model)
+    parts = {}
+    t = time.perf_counter()
+    tb = intern(cs, ps)
+    parts["intern"] = time.perf_counter() - t
+    t = time.perf_counter()
+    eng = DeviceBuild(None)
+    parts["context"] = time.perf_counter() - t
+    t = time.perf_counter()
+    eng.upload(tb)
+    parts["upload"] = time.perf_counter() - t
+    t = time.perf_counter()
+    eng.build()
+    parts["first_build"] = time.perf_counter() - t
+    t = time.perf_counter()
+    eng.build()
+    parts["second_build"] = time.perf_counter() - t
+    t = time.perf_counter()
+    group_ids(cs, "tenant")
+    parts["group_ids"] = time.perf_counter() - t
+    eng.close()
     return {"seconds": {k: round(v, 4) for k, v in sec.items()}, "total_s": round(total, 4),
+            "build_matrix_parts_s": {k: round(v, 4) for k, v in parts.items()},
             "objects_s": round(t_objects, 3), "verified": verified,
             "note": "build_matrix on fresh Container / Policy objects, then all_reachable, "
                     "all_isolated, user_crosscheck(tenant), system_isolation(0), policy_shadow "

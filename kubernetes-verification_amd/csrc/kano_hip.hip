@@ -30,6 +30,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cmath>
 #include <functional>
 #include <cerrno>
 #include <cstdint>
@@ -141,14 +142,16 @@ struct kano_ctx {
                              // holds more than path_dens % of the class-level bits
   int path_tm = 2;           // pathtm / pathtn: k_path_mfma tiles per wave
   int path_tn = 2;
-  int heavy_gemm = 22;       // hgemm: k_heavy_gemm's wave tile (TM TN: 22, 42, 44; 0: the
-                             // split-K kernel whatever the size)
+  int heavy_gemm = -1;       // hgemm: k_heavy_gemm's wave tile (TM TN: 22, 42, 44; 0: the
+                             // split-K kernel whatever the size; -1: 44 when it has the
+                             // tiles, else 22 -- the sweep's fastest at each size)
   // AUTO's dense-path rates (xomfma TOP/s, xoor GB/s): the GEMM's int8 ops
   // and the bitwise OR's Mc-word reads per second, as measured on the
   // crossover sweep (scripts/mfma_sweep.py)
-  double xo_mfma = 800e12, xo_or = 3000e9;
+  double xo_mfma = 1800e12, xo_or = 8500e9;
   i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
+  int heavy_expand_lds = 1;  // hexplds=0: the heavy rows' expansion from global memory
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
@@ -1275,11 +1278,15 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
   // the dense contraction's kernel: the tiled GEMM when it has enough wave
   // tiles to fill the chip without a split, else the split-K kernel
-  const int tmg = ctx->heavy_gemm / 10, tng = ctx->heavy_gemm % 10;
+  auto wave_tiles = [&](int tm, int tn) {
+    return ((H + 32 * tm - 1) / (32 * tm)) * ((ctx->cc.U + 32 * tn - 1) / (32 * tn));
+  };
+  int hg = ctx->heavy_gemm;
+  if (hg < 0) hg = wave_tiles(4, 4) >= ctx->heavy_gemm_min ? 44 : 22;
+  const int tmg = hg / 10, tng = hg % 10;
+  const i64 gtiles = tmg > 0 ? wave_tiles(tmg, tng) : 0;
   const bool gemm_fits = tmg > 0 && ctx->PB * 8 * (TPB / 64) <= 64 * 1024 &&
-                         ((H + 32 * tmg - 1) / (32 * tmg)) *
-                                 ((ctx->cc.U + 32 * tng - 1) / (32 * tng)) >=
-                             ctx->heavy_gemm_min;
+                         gtiles >= ctx->heavy_gemm_min;
   ctx->heavy_path = 0;
   bool mfma = false;
   if (H > 0) {
@@ -1289,7 +1296,11 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         // the MFMA does 2 H P Ua ops whatever the density, the OR reads
         // ldMc words per (heavy class, policy in S(c)): the cheaper by the
         // measured rates ("The dense path: crossover")
-        const double t_mfma = 2.0 * (double)H * (double)P * (double)ctx->cc.U / ctx->xo_mfma;
+        // (the GEMM's rate falls below ~2,048 wave tiles of 32 x 32: 1,030
+        // TOP/s at 1,024 tiles against 1,880 at 8,000 or more)
+        const double fill = std::pow(std::min(1.0, (double)gtiles / 2048.0), 0.85);
+        const double t_mfma =
+            2.0 * (double)H * (double)P * (double)ctx->cc.U / (ctx->xo_mfma * fill);
         const double t_or = 8.0 * (double)ctx->heavy_sel * (double)ldMc / ctx->xo_or;
         mfma = t_mfma < t_or;
       } else {
@@ -1450,10 +1461,10 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         KLAUNCH();
         KTRY(resolve_mfma_time(ctx));
         KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
-        if (ctx->heavy_gemm == 22)
+        if (hg == 22)
           hipLaunchKernelGGL((k_heavy_gemm<2, 2>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
                              P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
-        else if (ctx->heavy_gemm == 44)
+        else if (hg == 44)
           hipLaunchKernelGGL((k_heavy_gemm<4, 4>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
                              P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
         else
@@ -1574,11 +1585,25 @@ int launch_rows(kano_ctx* ctx) {
   if (ctx->rows_after) KCHK(hipStreamWaitEvent(rs, ctx->rows_after, 0));
   hipEvent_t e0 = ctx->ev_rt[set][0], e1 = ctx->ev_rt[set][1];
   if (ctx->heavy_count > 0) {
-    hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(ctx->heavy_count, HEXP_CLS)),
-                       dim3(TPB), 0, rs, P_<int32_t>(ctx->hlist), (i64)ctx->heavy_count,
-                       P_<u64>(ctx->Mc), ctx->ldC,
-                       P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
-                       P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
+    const i64 H = ctx->heavy_count, ldMc = ctx->ldC;
+    // nc classes' Mc rows in <= 32 KB of LDS (two blocks per CU), at most 64
+    const i64 nc = std::min<i64>(64, (32 * 1024) / (8 * std::max<i64>(1, ldMc)));
+    if (nc >= 1 && ctx->heavy_expand_lds) {
+      const i64 gy = (H + nc - 1) / nc;
+      // enough blocks to fill the chip, each over >= 8 words per wave
+      const i64 gx = std::max<i64>(
+          1, std::min<i64>((ldM + 4 * 8 - 1) / (4 * 8), (4096 + gy - 1) / gy));
+      hipLaunchKernelGGL(k_heavy_expand_lds, dim3((unsigned)gx, (unsigned)gy), dim3(TPB),
+                         sizeof(u64) * (size_t)(nc * ldMc), rs, P_<int32_t>(ctx->hlist), H,
+                         (int)nc, P_<u64>(ctx->Mc), ldMc, P_<int32_t>(ctx->cc.cls), n,
+                         P_<int32_t>(ctx->rc.moff), P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M),
+                         ldM, ctx->r0);
+    } else {
+      hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(H, HEXP_CLS)), dim3(TPB), 0, rs,
+                         P_<int32_t>(ctx->hlist), H, P_<u64>(ctx->Mc), ldMc,
+                         P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
+                         P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
+    }
     KLAUNCH();
   }
   const int cww = (int)std::min<i64>(ldM, ctx->rows_cww);
@@ -1986,9 +2011,11 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
-        if (k == "hgemm" && (v == 0 || v == 22 || v == 42 || v == 44)) ctx->heavy_gemm = v;
+        if (k == "hgemm" && (v == -1 || v == 0 || v == 22 || v == 42 || v == 44))
+          ctx->heavy_gemm = v;
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
         if (k == "hortime") ctx->time_or = v;
+        if (k == "hexplds") ctx->heavy_expand_lds = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
       }

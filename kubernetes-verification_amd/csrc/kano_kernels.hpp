@@ -1701,6 +1701,47 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict_
   }
 }
 
+// The expansion with the Mc rows in LDS: a block stages nc heavy classes'
+// Mc rows (nc * ldMc words, dynamic LDS) once, then its waves walk the pod
+// words (grid-stride over words; lane = pod): each lane reads its pod's
+// column class once and looks up nc bits in LDS, one ballot + store per
+// (class, word).  D1 (8,000 heavy classes x 10^5 pods): the global-memory form
+// above took 5.4 ms -- a dependent L1/L2 load per class per pod, and a
+// block of 256 pods re-read 16 Mc rows; grid = (word groups, class groups).
+__global__ __launch_bounds__(TPB) void k_heavy_expand_lds(const int32_t* __restrict__ hlist, i64 H,
+                                                          int nc, const u64* __restrict__ Mc,
+                                                          i64 ldMc,
+                                                          const int32_t* __restrict__ cla, i64 n,
+                                                          const int32_t* __restrict__ moff,
+                                                          const int32_t* __restrict__ mem,
+                                                          u64* __restrict__ M, i64 ldM, i64 r0) {
+  extern __shared__ __attribute__((aligned(16))) u64 rowsM[];
+  __shared__ i64 dst[64];
+  const i64 h0 = (i64)blockIdx.y * nc;
+  const int nh = (int)min((i64)nc, H - h0);
+  for (int q = threadIdx.x; q < nh; q += TPB) {
+    const int32_t c = hlist[h0 + q];
+    dst[q] = (i64)(mem[moff[c]] - r0) * ldM;
+  }
+  for (i64 e = threadIdx.x; e < (i64)nh * ldMc; e += TPB) {
+    const i64 q = e / ldMc, w = e - q * ldMc;
+    rowsM[e] = Mc[(i64)hlist[h0 + q] * ldMc + w];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const i64 wstride = (i64)gridDim.x * (TPB / 64);
+  for (i64 w = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6); w < ldM; w += wstride) {
+    const i64 j = w * 64 + lane;
+    const int32_t ca = j < n ? cla[j] : -1;
+    const int cw = ca >= 0 ? (ca >> 6) : 0, cb = ca & 63;
+    for (int q = 0; q < nh; ++q) {
+      const bool bit = ca >= 0 && ((rowsM[(i64)q * ldMc + cw] >> cb) & 1ull);
+      const u64 bal = __ballot(bit);
+      if (lane == 0) M[dst[q] + w] = bal;
+    }
+  }
+}
+
 // ===========================================================================
 // Matrix rows (model.py:158-160).  One block = one work item (class, up to
 // ch member pods, column chunk of cww words).  Light classes rebuild their

@@ -26,9 +26,12 @@ rule side -2 = no pod value equals the rule (matches nothing).
 from __future__ import annotations
 
 from dataclasses import dataclass
+from itertools import chain
 from typing import Any, Dict, List, Sequence
 
 import numpy as np
+
+from . import _kano_host   # csrc/kano_hostext.c, built in-tree by __graft_entry__.build()
 
 ABSENT = -1
 NO_MATCH_RULE = -2
@@ -110,6 +113,25 @@ class _ValueIndex:
         return NO_MATCH_RULE if got is None else got
 
 
+_MISSING = object()
+
+
+def _intern_column(labels, k, idx: "_ValueIndex", row: np.ndarray) -> bool:
+    """pod_id over one key's column at C speed (csrc/kano_hostext.c, the same
+    steps per pod: v != v first, then the dict of equality classes, ids in
+    first-seen order).  Returns False, idx untouched, when a value is
+    unhashable (the per-pod loop handles it)."""
+    out = np.empty(len(labels), np.int32)
+    ids: Dict[Any, int] = {}
+    try:
+        nxt = _kano_host.intern_column(labels, k, ids, out)
+    except TypeError:
+        return False
+    idx.ids, idx.next_id = ids, nxt
+    row[:] = out
+    return True
+
+
 def is_default_matcher(matcher) -> bool:
     from .model import DefaultEqualityLabelRelation
     return type(matcher).match is DefaultEqualityLabelRelation.match
@@ -118,17 +140,40 @@ def is_default_matcher(matcher) -> bool:
 def intern(containers: Sequence, policies: Sequence) -> Tables:
     n = len(containers)
     labels = [c.labels for c in containers]
-    keys: Dict[Any, None] = {}
-    for lab in labels:
-        for k in lab.keys():
-            keys[k] = None
 
     # working sides, read through the reference's own properties
-    sides = []
-    for pol in policies:
-        ws = pol.working_selector.labels
-        wa = pol.working_allow.labels
-        sides.append((ws, wa, pol.matcher))
+    sides = [(pol.working_selector.labels, pol.working_allow.labels, pol.matcher)
+             for pol in policies]
+
+    # KEYS (first-seen order, as a nested loop over every label dict) and the
+    # value-id columns of every key a policy term names, in one native pass
+    # over the label dicts (csrc/kano_hostext.c scan_labels); non-dict label
+    # maps or unhashable values: KEYS here, the columns one by one below
+    # (a side that is not a mapping -- e.g. None, which the term loop below
+    # reports as kano_py does -- leaves every column to that loop)
+    try:
+        cand = list(dict.fromkeys(chain.from_iterable(
+            chain.from_iterable((ws, wa) for ws, wa, _ in sides))))
+    except TypeError:
+        cand = None
+    scanned: Dict[Any, int] = {}
+    scan_ids, scan_out = [], None
+    keys: Dict[Any, None] = {}
+    if cand is not None:
+        scan_ids = [{} for _ in cand]
+        scan_out = np.empty((len(cand), n), np.int32)
+        try:
+            keys = _kano_host.scan_labels(labels, cand, scan_ids, scan_out)
+            scanned = {k: j for j, k in enumerate(cand)}
+        except (TypeError, ValueError):
+            cand = None
+    if cand is None:
+        keys = dict.fromkeys(chain.from_iterable(labels))
+
+    if scanned:
+        t = _intern_fast(n, labels, keys, sides, scanned, scan_ids, scan_out)
+        if t is not None:
+            return t
 
     col_of_key: Dict[Any, int] = {}
     col_specs: List[tuple] = []          # ("key", k) or ("custom", k, rule, matcher)
@@ -144,8 +189,11 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
     from .model import LabelExpression
     exprs: List[tuple] = []              # (key, LabelExpression)
     raw_terms = []                       # per policy: ([(col, rule|None)], [(col, rule|None)])
+    default_of: Dict[type, bool] = {}
     for ws, wa, matcher in sides:
-        default = is_default_matcher(matcher)
+        default = default_of.get(type(matcher))
+        if default is None:
+            default = default_of[type(matcher)] = is_default_matcher(matcher)
         per_side = []
         for side in (ws, wa):
             terms = []
@@ -172,15 +220,24 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
     ncols = len(col_specs)
     pod_val = np.full((ncols, n), ABSENT, dtype=np.int32)
     indexes: Dict[int, _ValueIndex] = {}
+    plain = None
     for c, spec in enumerate(col_specs):
         row = pod_val[c]
         if spec[0] == "key":
             k = spec[1]
             idx = _ValueIndex()
             indexes[c] = idx
-            for i, lab in enumerate(labels):
-                if k in lab:
-                    row[i] = idx.pod_id(lab[k])
+            j = scanned.get(k)
+            if j is not None:
+                row[:] = scan_out[j]
+                idx.ids, idx.next_id = scan_ids[j], len(scan_ids[j])
+                continue
+            if plain is None:
+                plain = all(type(lab) is dict for lab in labels)
+            if not (plain and _intern_column(labels, k, idx, row)):
+                for i, lab in enumerate(labels):
+                    if k in lab:
+                        row[i] = idx.pod_id(lab[k])
         else:
             _, k, rule, matcher = spec
             for i, lab in enumerate(labels):
@@ -188,18 +245,21 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
                     row[i] = 1 if matcher.match(rule, lab[k]) else 0
 
     def csr(which: int):
+        cnt = np.fromiter((len(per_side[which]) for per_side in raw_terms), np.int64,
+                          count=len(raw_terms))
         off = np.zeros(len(raw_terms) + 1, dtype=np.int64)
+        np.cumsum(cnt, out=off[1:])
         cols: List[int] = []
         vals: List[int] = []
-        for p, per_side in enumerate(raw_terms):
+        cadd, vadd = cols.append, vals.append
+        for per_side in raw_terms:
             for col, rule, custom in per_side[which]:
                 if custom == "expr":
-                    cols.append(ncols + rule)    # the engine's expression column
-                    vals.append(1)
+                    cadd(ncols + rule)    # the engine's expression column
+                    vadd(1)
                     continue
-                cols.append(col)
-                vals.append(1 if custom else indexes[col].rule_id(rule))
-            off[p + 1] = len(cols)
+                cadd(col)
+                vadd(1 if custom else indexes[col].rule_id(rule))
         return off, np.asarray(cols, dtype=np.int32), np.asarray(vals, dtype=np.int32)
 
     so, sc, sv = csr(0)
@@ -225,6 +285,34 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
         t.expr_off = np.asarray(eoff, np.int64)
         t.expr_val = np.asarray(evals, np.int32)
     return t
+
+
+def _intern_fast(n, labels, keys, sides, scanned, scan_ids, scan_out):
+    """intern's term loop in native code (csrc/kano_hostext.c policy_terms)
+    when every matcher is the default equality and no term is a
+    LabelExpression; None otherwise (intern's own loop then runs)."""
+    from .model import LabelExpression
+    dflt: Dict[type, bool] = {}
+    flags = [dflt[t] if (t := type(m)) in dflt else dflt.setdefault(t, is_default_matcher(m))
+             for _, _, m in sides]
+    try:
+        col_keys, so, sc, sv, ao, ac, av = _kano_host.policy_terms(
+            sides, flags, keys, scanned, scan_ids, LabelExpression)
+    except LookupError:
+        return None
+    ncols = len(col_keys)
+    rows = [scanned[k] for k in col_keys]
+    pod_val = scan_out[rows] if ncols else np.zeros((0, n), np.int32)
+    indexes: Dict[int, _ValueIndex] = {}
+    for c, j in enumerate(rows):
+        idx = _ValueIndex()
+        idx.ids, idx.next_id = scan_ids[j], len(scan_ids[j])
+        indexes[c] = idx
+    col_of_key = {k: c for c, k in enumerate(col_keys)}
+    arr = lambda b, d: np.frombuffer(b, dtype=d).copy()  # noqa: E731
+    st = _InternState(labels, keys, col_of_key, indexes, ncols)
+    return Tables(n, ncols, pod_val, arr(so, np.int64), arr(sc, np.int32), arr(sv, np.int32),
+                  arr(ao, np.int64), arr(ac, np.int32), arr(av, np.int32), st)
 
 
 class _InternState:
@@ -323,8 +411,20 @@ def tables_from_cluster(cl) -> Tables:
 def group_ids(containers: Sequence, label) -> np.ndarray:
     """gid[i] = dense id of container.getValueOrDefault(label, "") under the
     dict semantics of user_hashmap (kano_py/kano/algorithm.py:20-24)."""
+    from .model import Container
+    n = len(containers)
+    if n and type(containers) is list:
+        # (Container.getValueOrDefault is labels[key] if present, else the
+        # default: the native loop does that for exact Containers with dict
+        # labels, ids by first appearance as below; anything else -> the loop)
+        gid = np.empty(n, dtype=np.int32)
+        try:
+            _kano_host.group_ids(containers, Container, label, gid)
+            return gid
+        except ValueError:
+            pass
     groups: Dict[Any, int] = {}
-    gid = np.empty(len(containers), dtype=np.int32)
+    gid = np.empty(n, dtype=np.int32)
     for i, c in enumerate(containers):
         v = c.getValueOrDefault(label, "")
         g = groups.get(v)

@@ -122,7 +122,7 @@ def _fast_path(matrix, policies, containers) -> bool:
     for c in containers:
         if not isinstance(c, Container):
             return False
-        if c._sel or len(c._pending) != 1 or c._pending[0][0] is not lists:
+        if c._sel or len(c._pending) != 1 or c._pending[0] is not lists:
             return False
     return True
 

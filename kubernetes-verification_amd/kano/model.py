@@ -20,6 +20,8 @@ There is no CPU fallback: without the HIP library or a GPU the build raises
 """
 from __future__ import annotations
 
+import gc
+
 from abc import abstractmethod
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple, TypeVar
@@ -55,11 +57,29 @@ class _BuildLists:
     ``bid`` names the build's segment of every container's accumulated
     lists (quirk Q5: each build appends after the previous builds' entries)."""
 
-    def __init__(self, engine):
+    def __init__(self, engine, containers=None):
         self._engine = engine
         self._sel = None
         self._alw = None
         self.bid = next(_BUILD_IDS)
+        # the build's container list: a container's pending entry is this
+        # object itself (no per-container allocation), its row index found
+        # here on first use
+        self._containers = containers
+        self._pos = None
+        self._dups = None
+
+    def position(self, c, k: int = 0) -> int:
+        if self._pos is None:
+            pos: Dict[int, int] = {}
+            dups: Dict[int, List[int]] = {}
+            for i, x in enumerate(self._containers):
+                j = pos.setdefault(id(x), i)
+                if j != i:
+                    dups.setdefault(id(x), [j]).append(i)
+            self._pos, self._dups = pos, dups
+        d = self._dups.get(id(c))
+        return d[k] if d is not None else self._pos[id(c)]
 
     def select_list(self, i: int) -> List[int]:
         if self._sel is None:
@@ -140,10 +160,17 @@ class Container:
     def _flush(self) -> None:
         if self._pending:
             pend, self._pending = self._pending, []
-            for lists, i in pend:
-                if isinstance(lists, _Renumber):   # a policy removal, applied lazily
-                    lists.apply(self)
+            seen: Dict[int, int] = {}
+            for e in pend:
+                if type(e) is tuple:               # (a policy removal, applied lazily)
+                    e[0].apply(self)
                     continue
+                # a build's entry: the k-th for this build is this container's
+                # k-th position in the build's container list
+                lists = e
+                k = seen.get(lists.bid, 0)
+                seen[lists.bid] = k + 1
+                i = lists.position(self, k)
                 s0, a0 = len(self._sel), len(self._alw)
                 self._sel.extend(lists.select_list(i))
                 self._alw.extend(lists.allow_list(i))
@@ -468,21 +495,30 @@ class ReachabilityMatrix:
         from ._engine import DeviceBuild
         from ._intern import intern
         from .multi import MultiBuild, requested_devices, requested_gpus
-        tables = intern(containers, policies)
-        G = requested_gpus()
-        if G > 1:   # one process over G devices: rows sharded (kano/multi.py)
-            engine = MultiBuild(tables, G, devices=requested_devices(G))
-        else:
-            engine = DeviceBuild(tables)
-        for p, pol in enumerate(policies):
-            pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
-        lists = _BuildLists(engine)
-        for i, c in enumerate(containers):
-            if isinstance(c, Container):
-                c._pending.append((lists, i))
-            else:                        # foreign container type: materialise now
-                c.select_policies.extend(lists.select_list(i))
-                c.allow_policies.extend(lists.allow_list(i))
+        # (the cyclic GC paused over the bulk object work: with 10^5 live
+        # containers each full collection walks them all -- 0.18 s a pass on
+        # C3 -- and the per-policy objects below used to trigger several)
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            tables = intern(containers, policies)
+            G = requested_gpus()
+            if G > 1:   # one process over G devices: rows sharded (kano/multi.py)
+                engine = MultiBuild(tables, G, devices=requested_devices(G))
+            else:
+                engine = DeviceBuild(tables)
+            for p, pol in enumerate(policies):
+                pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
+            lists = _BuildLists(engine, containers)
+            for i, c in enumerate(containers):
+                if isinstance(c, Container):
+                    c._pending.append(lists)
+                else:                        # foreign container type: materialise now
+                    c.select_policies.extend(lists.select_list(i))
+                    c.allow_policies.extend(lists.allow_list(i))
+        finally:
+            if gc_was:
+                gc.enable()
         m = ReachabilityMatrix.__new__(ReachabilityMatrix)
         m.container_size = len(containers)
         m._engine = engine

@@ -191,6 +191,80 @@ def test_group_ids_dict_semantics():
     assert group_ids(cs, "u").tolist() == [0, 0, 0, 1, 1, 2]
 
 
+def _py_intern(cs, ps, monkeypatch):
+    """intern() with the native passes switched off (the per-pod Python loops)."""
+    from kano import _intern as I
+
+    class Off:
+        def __getattr__(self, name):
+            def f(*a):
+                raise TypeError("native pass off")
+            return f
+    with monkeypatch.context() as m:
+        m.setattr(I, "_kano_host", Off())
+        return I.intern(cs, ps)
+
+
+def _same_tables(a, b):
+    assert a.n == b.n and a.ncols == b.ncols
+    for f in ("pod_val", "sel_off", "sel_col", "sel_val", "alw_off", "alw_col", "alw_val"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert x.dtype == y.dtype and np.array_equal(x, y), f
+    assert list(a.state.keys) == list(b.state.keys)
+    assert a.state.col_of_key == b.state.col_of_key
+    for c, idx in a.state.indexes.items():
+        assert idx.ids == b.state.indexes[c].ids and idx.next_id == b.state.indexes[c].next_id
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_native_interning_equals_python_loops(seed, monkeypatch):
+    """csrc/kano_hostext.c (scan_labels, policy_terms, intern_column) against
+    intern's own per-pod / per-term loops on awkward values: NaN (float and
+    numpy, shared and distinct objects), 1 / 1.0 / True collapsing, None, a
+    key no pod carries (quirk Q1), rules no pod value equals, unhashable rule
+    values, and -- for seeds >= 3 -- an unhashable pod value and a custom
+    matcher, which send the columns / terms to the loops."""
+    from kano import model
+    from kano._intern import intern
+    rng = np.random.default_rng(seed)
+    nan = float("nan")
+    pool = [1, 1.0, True, 0, False, "a", "b", None, nan, float("nan"), np.float64("nan"), 2.5, "1"]
+    if seed >= 3:
+        pool.append(["unhashable"])
+    keys = ["k0", "k1", "k2", "k3"]
+    cs = []
+    for i in range(300):
+        lab = {k: pool[rng.integers(len(pool))] for k in keys if rng.random() < 0.7}
+        cs.append(model.Container(f"c{i}", lab))
+    rules = [1, True, "a", "zz", nan, None, ["x"], 2.5]
+    ps = []
+    for p in range(60):
+        sel = {k: rules[rng.integers(len(rules))] for k in keys + ["absent"] if rng.random() < 0.4}
+        alw = {k: rules[rng.integers(len(rules))] for k in keys if rng.random() < 0.4}
+        kw = {}
+        if seed >= 3 and p % 17 == 5:
+            class Loose(model.DefaultEqualityLabelRelation):
+                def match(self, rule, value):
+                    return str(rule) == str(value)
+            kw["matcher"] = Loose()
+        ps.append(model.Policy(f"p{p}", model.PolicySelect(sel), model.PolicyAllow(alw),
+                               model.PolicyIngress if p % 3 == 0 else model.PolicyEgress,
+                               model.PolicyProtocol(["TCP"]), **kw))
+    _same_tables(intern(cs, ps), _py_intern(cs, ps, monkeypatch))
+
+
+def test_native_group_ids_equal_loop(monkeypatch):
+    from kano import model, _intern as I
+    rng = np.random.default_rng(3)
+    pool = [1, 1.0, True, "", "x", None, 2.5]
+    cs = [model.Container(str(i), {"u": pool[rng.integers(len(pool))]} if rng.random() < 0.8
+                          else {}) for i in range(500)]
+    got = I.group_ids(cs, "u")
+    with monkeypatch.context() as m:
+        m.setattr(I._kano_host, "group_ids", lambda *a: (_ for _ in ()).throw(ValueError()))
+        assert np.array_equal(got, I.group_ids(cs, "u"))
+
+
 # --------------------------------------------------------------------------
 # parser vs kano_py's parser (tests/golden/expected/parser.json)
 # --------------------------------------------------------------------------
