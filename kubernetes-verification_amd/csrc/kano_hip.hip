@@ -1589,11 +1589,8 @@ int launch_rows(kano_ctx* ctx) {
     // nc classes' Mc rows in <= 32 KB of LDS (two blocks per CU), at most 64
     const i64 nc = std::min<i64>(64, (32 * 1024) / (8 * std::max<i64>(1, ldMc)));
     if (nc >= 1 && ctx->heavy_expand_lds) {
-      const i64 gy = (H + nc - 1) / nc;
-      // enough blocks to fill the chip, each over >= 8 words per wave
-      const i64 gx = std::max<i64>(
-          1, std::min<i64>((ldM + 4 * 8 - 1) / (4 * 8), (4096 + gy - 1) / gy));
-      hipLaunchKernelGGL(k_heavy_expand_lds, dim3((unsigned)gx, (unsigned)gy), dim3(TPB),
+      const i64 gy = (H + nc - 1) / nc, gx = (ldM + TPB - 1) / TPB;
+      hipLaunchKernelGGL(k_heavy_expand_w, dim3((unsigned)gx, (unsigned)gy), dim3(TPB),
                          sizeof(u64) * (size_t)(nc * ldMc), rs, P_<int32_t>(ctx->hlist), H,
                          (int)nc, P_<u64>(ctx->Mc), ldMc, P_<int32_t>(ctx->cc.cls), n,
                          P_<int32_t>(ctx->rc.moff), P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M),

@@ -21,6 +21,7 @@
  * No state, no GPU: plumbing for the host side of the drop-in boundary. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <structmember.h>
 #include <stdint.h>
 
 #define ABSENT (-1)
@@ -41,6 +42,36 @@ static int self_ne(PyObject* v) {
     t = 0;
   }
   return t;
+}
+
+/* The byte offset of a __slots__ member of type cls (a member descriptor),
+ * or -1: reading it directly skips the generic attribute lookup. */
+static Py_ssize_t slot_offset(PyObject* cls, const char* name) {
+  if (!PyType_Check(cls)) return -1;
+  PyObject* d = PyObject_GetAttrString(cls, name);
+  if (d == NULL) {
+    PyErr_Clear();
+    return -1;
+  }
+  Py_ssize_t off = -1;
+  if (Py_TYPE(d) == &PyMemberDescr_Type) {
+    PyMemberDef* m = ((PyMemberDescrObject*)d)->d_member;
+    if (m->type == T_OBJECT_EX || m->type == T_OBJECT) off = m->offset;
+  }
+  Py_DECREF(d);
+  return off;
+}
+
+/* a slot's value (new reference), AttributeError when unset */
+static PyObject* slot_get(PyObject* o, Py_ssize_t off, PyObject* name) {
+  if (off < 0) return PyObject_GetAttr(o, name);
+  PyObject* v = *(PyObject**)((char*)o + off);
+  if (v == NULL) {
+    PyErr_SetObject(PyExc_AttributeError, name);
+    return NULL;
+  }
+  Py_INCREF(v);
+  return v;
 }
 
 static int get_out(PyObject* obj, Py_buffer* view, Py_ssize_t n) {
@@ -334,13 +365,26 @@ static PyObject* group_ids(PyObject* self, PyObject* args) {
   PyObject* attr = PyUnicode_InternFromString("labels");
   PyObject* empty = PyUnicode_FromString("");
   if (groups == NULL || attr == NULL || empty == NULL) goto fail;
+  /* (memory-latency bound: every container, its label dict, the dict's
+   * table and the value are separate heap objects -- the containers are
+   * prefetched PF_FAR ahead, their label dicts and tables PF_NEAR ahead) */
+  enum { PF_FAR = 16, PF_NEAR = 8 };
+  const Py_ssize_t loff = slot_offset(cls, "labels");
   for (Py_ssize_t i = 0; i < n; ++i) {
+    if (i + PF_FAR < n) __builtin_prefetch(PyList_GET_ITEM(items, i + PF_FAR));
+    if (loff >= 0 && i + PF_NEAR < n) {
+      PyObject* cn = PyList_GET_ITEM(items, i + PF_NEAR);
+      if ((PyObject*)Py_TYPE(cn) == cls) {
+        PyObject* ln = *(PyObject**)((char*)cn + loff);
+        if (ln != NULL && PyDict_CheckExact(ln)) __builtin_prefetch(((PyDictObject*)ln)->ma_keys);
+      }
+    }
     PyObject* c = PyList_GET_ITEM(items, i);
     if ((PyObject*)Py_TYPE(c) != cls) {
       PyErr_SetString(PyExc_ValueError, "containers: exact Container objects expected");
       goto fail;
     }
-    PyObject* lab = PyObject_GetAttr(c, attr);          /* new reference */
+    PyObject* lab = slot_get(c, loff, attr);            /* new reference */
     if (lab == NULL) goto fail;
     if (!PyDict_CheckExact(lab)) {
       Py_DECREF(lab);
@@ -395,11 +439,110 @@ fail:
   return NULL;
 }
 
+/* pending_is(containers, cls, lists) -> bool
+ *   kano/algorithm.py _fast_path's per-container test: every container is
+ *   exactly `cls`, its own select list (_sel) is empty and its only pending
+ *   entry is `lists` (the build's view) -- its select_policies is still
+ *   exactly that build's list. */
+static PyObject* pending_is(PyObject* self, PyObject* args) {
+  PyObject *items, *cls, *lists;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!OO", &PyList_Type, &items, &cls, &lists)) return NULL;
+  PyObject* a_sel = PyUnicode_InternFromString("_sel");
+  PyObject* a_pend = PyUnicode_InternFromString("_pending");
+  if (a_sel == NULL || a_pend == NULL) {
+    Py_XDECREF(a_sel);
+    Py_XDECREF(a_pend);
+    return NULL;
+  }
+  int ok = 1;
+  const Py_ssize_t n = PyList_GET_SIZE(items);
+  const Py_ssize_t soff = slot_offset(cls, "_sel"), poff = slot_offset(cls, "_pending");
+  for (Py_ssize_t i = 0; i < n && ok; ++i) {
+    PyObject* c = PyList_GET_ITEM(items, i);
+    if ((PyObject*)Py_TYPE(c) != cls) {
+      ok = 0;
+      break;
+    }
+    PyObject* sel = slot_get(c, soff, a_sel);
+    PyObject* pend = sel ? slot_get(c, poff, a_pend) : NULL;
+    if (pend == NULL) {
+      Py_XDECREF(sel);
+      Py_DECREF(a_sel);
+      Py_DECREF(a_pend);
+      return NULL;
+    }
+    const int sel_empty = PyList_CheckExact(sel) ? PyList_GET_SIZE(sel) == 0 : PyObject_Not(sel);
+    ok = sel_empty == 1 && PyList_CheckExact(pend) && PyList_GET_SIZE(pend) == 1 &&
+         PyList_GET_ITEM(pend, 0) == lists;
+    Py_DECREF(sel);
+    Py_DECREF(pend);
+  }
+  Py_DECREF(a_sel);
+  Py_DECREF(a_pend);
+  if (PyErr_Occurred()) return NULL;
+  return PyBool_FromLong(ok);
+}
+
+/* pairs_list(buf, P) -> [(j, k), ...]
+ *   policy_shadow's result as kano_py returns it (a list of int tuples,
+ *   kano_py/kano/algorithm.py:58-80) from the engine's (T, 2) int32 pairs;
+ *   the ints of policy ids 0..P-1 made once and shared. */
+static PyObject* pairs_list(PyObject* self, PyObject* args) {
+  PyObject* obj;
+  Py_ssize_t P;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "On", &obj, &P)) return NULL;
+  Py_buffer view;
+  if (PyObject_GetBuffer(obj, &view, PyBUF_C_CONTIGUOUS) < 0) return NULL;
+  const Py_ssize_t T = view.len / (Py_ssize_t)(2 * sizeof(int32_t));
+  const int32_t* v = (const int32_t*)view.buf;
+  /* (68k tuples: the cyclic GC, run by the allocations, walked every live
+   * container of the build, 12 of 14 ms on C3) */
+  const int gc_was = PyGC_Disable();
+  PyObject* ints = PyList_New(P > 0 ? P : 0);
+  PyObject* out = ints ? PyList_New(T) : NULL;
+  if (out == NULL) goto fail;
+  for (Py_ssize_t p = 0; p < P; ++p) {
+    PyObject* x = PyLong_FromSsize_t(p);
+    if (x == NULL) goto fail;
+    PyList_SET_ITEM(ints, p, x);
+  }
+  for (Py_ssize_t t = 0; t < T; ++t) {
+    const int32_t a = v[2 * t], b = v[2 * t + 1];
+    PyObject* pa = (a >= 0 && a < P) ? PyList_GET_ITEM(ints, a) : NULL;
+    PyObject* pb = (b >= 0 && b < P) ? PyList_GET_ITEM(ints, b) : NULL;
+    if (pa) Py_INCREF(pa); else if ((pa = PyLong_FromLong(a)) == NULL) goto fail;
+    if (pb) Py_INCREF(pb); else if ((pb = PyLong_FromLong(b)) == NULL) { Py_DECREF(pa); goto fail; }
+    PyObject* tup = PyTuple_New(2);
+    if (tup == NULL) {
+      Py_DECREF(pa);
+      Py_DECREF(pb);
+      goto fail;
+    }
+    PyTuple_SET_ITEM(tup, 0, pa);
+    PyTuple_SET_ITEM(tup, 1, pb);
+    PyList_SET_ITEM(out, t, tup);
+  }
+  Py_DECREF(ints);
+  PyBuffer_Release(&view);
+  if (gc_was) PyGC_Enable();
+  return out;
+fail:
+  Py_XDECREF(ints);
+  Py_XDECREF(out);
+  PyBuffer_Release(&view);
+  if (gc_was) PyGC_Enable();
+  return NULL;
+}
+
 static PyMethodDef methods[] = {
     {"intern_column", intern_column, METH_VARARGS, "pod value ids of one key's column"},
     {"group_ids", group_ids, METH_VARARGS, "dense group ids of containers by one label"},
     {"scan_labels", scan_labels, METH_VARARGS, "KEYS and the candidate keys' value-id columns"},
     {"policy_terms", policy_terms, METH_VARARGS, "the working-term CSRs, default matchers"},
+    {"pending_is", pending_is, METH_VARARGS, "every container's lists still the build's"},
+    {"pairs_list", pairs_list, METH_VARARGS, "policy_shadow's pairs as a list of tuples"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_kano_host", NULL, -1, methods,

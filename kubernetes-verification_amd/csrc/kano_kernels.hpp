@@ -1701,20 +1701,22 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict_
   }
 }
 
-// The expansion with the Mc rows in LDS: a block stages nc heavy classes'
-// Mc rows (nc * ldMc words, dynamic LDS) once, then its waves walk the pod
-// words (grid-stride over words; lane = pod): each lane reads its pod's
-// column class once and looks up nc bits in LDS, one ballot + store per
-// (class, word).  D1 (8,000 heavy classes x 10^5 pods): the global-memory form
-// above took 5.4 ms -- a dependent L1/L2 load per class per pod, and a
-// block of 256 pods re-read 16 Mc rows; grid = (word groups, class groups).
-__global__ __launch_bounds__(TPB) void k_heavy_expand_lds(const int32_t* __restrict__ hlist, i64 H,
-                                                          int nc, const u64* __restrict__ Mc,
-                                                          i64 ldMc,
-                                                          const int32_t* __restrict__ cla, i64 n,
-                                                          const int32_t* __restrict__ moff,
-                                                          const int32_t* __restrict__ mem,
-                                                          u64* __restrict__ M, i64 ldM, i64 r0) {
+// The expansion with the Mc rows in LDS, lane = output word: a block stages
+// nc heavy classes' Mc rows (nc * ldMc words, dynamic LDS, read as 32-bit
+// halves), each thread owns one 64-pod word w of the rows: it loads its 64
+// pods' column classes once (16-byte loads, registers) and, per class,
+// gathers the 64 bits from LDS into one word, stored with the block's other
+// words (coalesced 512 B per wave).  D1 (8,000 heavy classes x 10^5 pods):
+// the lane-per-pod form above took 5.4 ms (a dependent load and a ballot per
+// class per pod, one 8-byte store per wave); grid = (word blocks, class
+// groups).
+__global__ __launch_bounds__(TPB) void k_heavy_expand_w(const int32_t* __restrict__ hlist, i64 H,
+                                                        int nc, const u64* __restrict__ Mc,
+                                                        i64 ldMc,
+                                                        const int32_t* __restrict__ cla, i64 n,
+                                                        const int32_t* __restrict__ moff,
+                                                        const int32_t* __restrict__ mem,
+                                                        u64* __restrict__ M, i64 ldM, i64 r0) {
   extern __shared__ __attribute__((aligned(16))) u64 rowsM[];
   __shared__ i64 dst[64];
   const i64 h0 = (i64)blockIdx.y * nc;
@@ -1728,17 +1730,39 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand_lds(const int32_t* __restr
     rowsM[e] = Mc[(i64)hlist[h0 + q] * ldMc + w];
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const i64 wstride = (i64)gridDim.x * (TPB / 64);
-  for (i64 w = (i64)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6); w < ldM; w += wstride) {
-    const i64 j = w * 64 + lane;
-    const int32_t ca = j < n ? cla[j] : -1;
-    const int cw = ca >= 0 ? (ca >> 6) : 0, cb = ca & 63;
-    for (int q = 0; q < nh; ++q) {
-      const bool bit = ca >= 0 && ((rowsM[(i64)q * ldMc + cw] >> cb) & 1ull);
-      const u64 bal = __ballot(bit);
-      if (lane == 0) M[dst[q] + w] = bal;
+  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (w >= ldM) return;                 // (after the block's only barrier)
+  // this word's 64 column classes (-1 past n); 16-byte loads when whole
+  int32_t ca[64];
+  if (w * 64 + 64 <= n && (reinterpret_cast<uintptr_t>(cla) & 15) == 0) {
+    const int4* src = reinterpret_cast<const int4*>(cla + w * 64);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int4 x = src[v];
+      ca[4 * v] = x.x;
+      ca[4 * v + 1] = x.y;
+      ca[4 * v + 2] = x.z;
+      ca[4 * v + 3] = x.w;
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 64; ++j) ca[j] = w * 64 + j < n ? cla[w * 64 + j] : -1;
+  }
+  const uint32_t* rows32 = reinterpret_cast<const uint32_t*>(rowsM);
+  const i64 ld32 = 2 * ldMc;
+  for (int q = 0; q < nh; ++q) {
+    const uint32_t* r = rows32 + (i64)q * ld32;
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      // (the index arithmetic stays inside the loop: hoisted over q it held
+      // 192 registers, one wave per SIMD)
+      int32_t a = ca[j];
+      asm volatile("" : "+v"(a));
+      const uint32_t bit = (r[max(a, 0) >> 5] >> (a & 31)) & (uint32_t)(a >= 0);
+      acc |= (u64)bit << j;
+    }
+    M[dst[q] + w] = acc;
   }
 }
 

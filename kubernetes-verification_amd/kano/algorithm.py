@@ -15,6 +15,7 @@ from .model import *  # noqa: F401,F403  (the reference does the same, algorithm
 from .model import BitArray, Container, Policy, ReachabilityMatrix
 from ._bits import bool_to_words, set_bit_indices, words_to_bool
 from ._intern import group_ids
+from . import _kano_host   # csrc/kano_hostext.c
 
 
 def _engine(matrix: ReachabilityMatrix, whole: bool = True):
@@ -99,10 +100,11 @@ def system_isolation(matrix: ReachabilityMatrix, idx: int) -> List[int]:
     return np.flatnonzero(~words_to_bool(row, n)).tolist()
 
 
-def _pairs_to_list(pairs: np.ndarray) -> List[Tuple[int, int]]:
+def _pairs_to_list(pairs: np.ndarray, P: int = 0) -> List[Tuple[int, int]]:
     if pairs.shape[0] == 0:
         return []
-    return list(zip(pairs[:, 0].tolist(), pairs[:, 1].tolist()))
+    # (csrc/kano_hostext.c: the tuples built natively, policy ints shared)
+    return _kano_host.pairs_list(np.ascontiguousarray(pairs, dtype=np.int32), int(P))
 
 
 def _fast_path(matrix, policies, containers) -> bool:
@@ -119,6 +121,8 @@ def _fast_path(matrix, policies, containers) -> bool:
         if any(a is not b for a, b in zip(cs, containers)):
             return False
     lists = matrix._lists
+    if type(containers) is list and _kano_host.pending_is(containers, Container, lists):
+        return True                  # (the loop below, natively, for exact Containers)
     for c in containers:
         if not isinstance(c, Container):
             return False
@@ -168,7 +172,7 @@ def policy_shadow(matrix: ReachabilityMatrix, policies: List[Policy],
     """Pairs (j, k) of policies selecting a common container with allow_k a
     subset of allow_j, one entry per container, in container order
     (algorithm.py:58-80; duplicates kept, quirk Q4)."""
-    return _pairs_to_list(policy_shadow_pairs(matrix, policies, containers))
+    return _pairs_to_list(policy_shadow_pairs(matrix, policies, containers), len(policies))
 
 
 def policy_conflict(matrix: ReachabilityMatrix, policies: List[Policy],
