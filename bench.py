@@ -441,9 +441,11 @@ def main():
     # write, so the write takes every CU (in the timed steps it runs on a
     # CU-masked stream beside the next step's build)
     eng.rows_timing(reset=True)
+    eng.mfma_timing(reset=True)
     for _ in range(args.alone):
         eng.build()
     ra = eng.rows_timing()
+    mta = eng.mfma_timing()
     alone_ms = ra["sum_ms"] / ra["launches"] if ra["launches"] else float("nan")
     rows_local = r1 - r0
     W = (n + 63) // 64
@@ -524,7 +526,17 @@ def main():
                                "ops_per_build": mt["ops_last"],
                                "avg_ms": mt["sum_ms"] / mt["builds"], "builds_timed": mt["builds"],
                                "heavy_classes": info["HEAVY"], "column_classes": info["UA"],
-                               "policies": cl.P}
+                               "policies": cl.P,
+                               # in the timed steps the contraction shares the
+                               # chip with the previous step's matrix write and
+                               # this step's policy_shadow work; alone = the
+                               # same launch in kano_build after the timed region
+                               "alone": ({"avg_ms": mta["sum_ms"] / mta["builds"],
+                                          "achieved": mta["ops_sum"] / (mta["sum_ms"] * 1e-3) / 1e12,
+                                          "frac": mta["ops_sum"] / (mta["sum_ms"] * 1e-3) / 1e12 /
+                                                  MFMA_I8_PEAK_TOPS,
+                                          "builds": mta["builds"]}
+                                         if mta["builds"] and mta["sum_ms"] > 0 else None)}
                               if mt["builds"] > 0 and mt["sum_ms"] > 0 else None),
             "step_ms": {"min": round(float(step_ms.min()), 4),
                         "median": round(float(np.median(step_ms)), 4),

@@ -107,6 +107,8 @@ enum {
   SZ_SIGNAL = SZ_SLOTS   // host mirror only: the scans' host signal word
 };
 
+constexpr size_t ROW_STAGE_BYTES = 256 * 1024;
+
 struct kano_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -152,6 +154,8 @@ struct kano_ctx {
   i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int heavy_expand_lds = 1;  // hexplds=0: the heavy rows' expansion from global memory
+  int gemm_lds = 1;          // hglds=0: k_heavy_gemm (operands from global memory, one
+                             // K-step of register prefetch) instead of k_heavy_gemm_lds
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
   int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
@@ -234,6 +238,7 @@ struct kano_ctx {
   // pinned, coherent mirror of the size slots that the scans write directly
   // (slot-indexed): the overlapped syncs poll the host signal word the last
   // scan with host totals raises (or wait on an event when no scan does)
+  void* row_stage = nullptr;  // page-locked, ROW_STAGE_BYTES (kano_get_rows)
   u64* gmirror = nullptr;     // SZ_SLOTS slots + the host signal word (SZ_SIGNAL)
   u64* gmirror_dev = nullptr;
   DBuf sig_ctr;              // the scans' arrival counter (one u32, zero between launches)
@@ -440,6 +445,7 @@ struct ScanBatch {
     j.in64 = sizeof(Tin) == 8;
     j.out64 = sizeof(Tout) == 8;
     j.gen = 0;
+    j.gcnt = nullptr;
     slots += 1 + scan_tiles(n);
     maxt = std::max<i64>(maxt, scan_tiles(n));
     return 0;
@@ -466,6 +472,18 @@ struct ScanBatch {
     j.gen = 2;
     j.gslot = cls;
     j.gloff = loff;
+    j.gm0 = m0;
+    return 0;
+  }
+  // the same offsets from the per-class counts themselves (cnt[c] = loff[c +
+  // 1] - loff[c]): queued beside loff's own scan, not after it
+  int add_class_counts(const int32_t* cls, const i64* cnt, i64 m0, i64 n, i64* out,
+                       int total_slot) {
+    KTRY(add(static_cast<const int32_t*>(nullptr), n, out, total_slot));
+    ScanJob& j = jobs.j[jobs.count - 1];
+    j.gen = 3;
+    j.gslot = cls;
+    j.gcnt = cnt;
     j.gm0 = m0;
     return 0;
   }
@@ -1285,7 +1303,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   if (hg < 0) hg = wave_tiles(4, 4) >= ctx->heavy_gemm_min ? 44 : 22;
   const int tmg = hg / 10, tng = hg % 10;
   const i64 gtiles = tmg > 0 ? wave_tiles(tmg, tng) : 0;
-  const bool gemm_fits = tmg > 0 && ctx->PB * 8 * (TPB / 64) <= 64 * 1024 &&
+  const bool gemm_fits = tmg > 0 && (ctx->PB + GK_KC) * 8 * (TPB / 64) <= 64 * 1024 &&
                          gtiles >= ctx->heavy_gemm_min;
   ctx->heavy_path = 0;
   bool mfma = false;
@@ -1314,6 +1332,12 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   const bool gemm = mfma && gemm_fits;
   ctx->heavy_kernel = H == 0 ? 0 : !mfma ? 1 : gemm ? 3 : 2;
+  // the staged GEMM's padded operands (k_heavy_gemm_lds): A [PBp][ldA],
+  // ACT [PBp][ldB]; the unstaged kernels use ldA = H, ldB = Ua, PBp = PB
+  const bool glds = gemm && ctx->gemm_lds;
+  const i64 ldA = glds ? (H + 64 * tmg - 1) / (64 * tmg) * (64 * tmg) : H;
+  const i64 ldB = glds ? (ctx->cc.U + 64 * tng - 1) / (64 * tng) * (64 * tng) : ctx->cc.U;
+  const i64 PBp = glds ? (ctx->PB + GK_KC - 1) / GK_KC * GK_KC : ctx->PB;
   FillJobs carried{};
   {
     FillBatch fb(ctx);
@@ -1323,10 +1347,10 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     KTRY(dalloc(ctx, ctx->hlist, sizeof(int32_t) * std::max<i64>(1, H)));
     KTRY(dalloc(ctx, ctx->wicls, sizeof(int32_t) * std::max<i64>(1, ctx->wi_total)));
     if (mfma) {
-      KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, ctx->PB * ctx->cc.U)));
-      KTRY(fb.add(ctx->ACT, sizeof(u64) * ctx->PB * ctx->cc.U, 0u));
-      // (the GEMM's A is written whole by k_heavy_selT: no fill)
-      const i64 aw = gemm ? ctx->PB * H : ctx->PB * U;
+      KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, PBp * ldB)));
+      KTRY(fb.add(ctx->ACT, sizeof(u64) * PBp * ldB, 0u));
+      // (the GEMM's A is written whole, padding included, by k_heavy_selT: no fill)
+      const i64 aw = gemm ? PBp * ldA : ctx->PB * U;
       KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, aw)));
       if (!gemm) KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
     }
@@ -1436,7 +1460,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       const i64 Ua = ctx->cc.U;
       hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                          P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
-                         P_<int32_t>(ctx->am.gmem), Ua, P_<u64>(ctx->ACT));
+                         P_<int32_t>(ctx->am.gmem), ldB, P_<u64>(ctx->ACT));
       KLAUNCH();
       // class-major selector bits: selT[pb][c] (the split-K kernel's A; the
       // GEMM builds its own, heavy rows only)
@@ -1455,13 +1479,24 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         const dim3 grid((unsigned)(8 * ((nb + 7) / 8)));
         const int32_t* hl = P_<int32_t>(ctx->hlist);
         u64* A = P_<u64>(ctx->scratch_words);
-        hipLaunchKernelGGL(k_heavy_selT, dim3(nblk(H, TPB / 64)), dim3(TPB),
-                           sizeof(u64) * (size_t)ctx->PB * (TPB / 64), ctx->stream, hl, H,
-                           P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), ctx->PB, A);
+        hipLaunchKernelGGL(k_heavy_selT, dim3(nblk(ldA, TPB / 64)), dim3(TPB),
+                           sizeof(u64) * (size_t)PBp * (TPB / 64), ctx->stream, hl, H, ldA,
+                           P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), PBp, A);
         KLAUNCH();
         KTRY(resolve_mfma_time(ctx));
         KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
-        if (hg == 22)
+        if (glds) {
+          const size_t lds = sizeof(u64) * 2 * GK_KC * (size_t)(64 * tmg + 64 * tng);
+          if (hg == 22)
+            hipLaunchKernelGGL((k_heavy_gemm_lds<2, 2>), grid, dim3(TPB), lds, ctx->stream, A,
+                               ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
+          else if (hg == 44)
+            hipLaunchKernelGGL((k_heavy_gemm_lds<4, 4>), grid, dim3(TPB), lds, ctx->stream, A,
+                               ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
+          else
+            hipLaunchKernelGGL((k_heavy_gemm_lds<4, 2>), grid, dim3(TPB), lds, ctx->stream, A,
+                               ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
+        } else if (hg == 22)
           hipLaunchKernelGGL((k_heavy_gemm<2, 2>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
                              P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
         else if (hg == 44)
@@ -2013,6 +2048,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
         if (k == "hortime") ctx->time_or = v;
         if (k == "hexplds") ctx->heavy_expand_lds = v;
+        if (k == "hglds") ctx->gemm_lds = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
       }
@@ -2031,6 +2067,16 @@ int kano_create(int device, kano_ctx** out) {
   }
   ctx->own_stream = true;
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  // the staged GEMM's LDS (128 KB at 4 x 4) is above the default dynamic cap
+  {
+    const int lds44 = (int)(sizeof(u64) * 2 * GK_KC * (256 + 256));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<4, 4>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<4, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<2, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
+  }
   if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
     ctx->stream3 = nullptr;
     kano_destroy(ctx);
@@ -2084,6 +2130,11 @@ int kano_create(int device, kano_ctx** out) {
     return -ENOMEM;
   }
   for (int k = 0; k <= SZ_SIGNAL; ++k) ctx->gmirror[k] = 0;
+  // page-locked staging for short row reads (system_isolation's row): a
+  // copy into pageable memory first set up the runtime's own staging, 8 ms
+  // on the first call of a process
+  if (hipHostMalloc(&ctx->row_stage, ROW_STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
+    ctx->row_stage = nullptr;
   if (dalloc(ctx, ctx->sig_ctr, sizeof(uint32_t) * 4) != 0 ||
       hipMemset(ctx->sig_ctr.p, 0, sizeof(uint32_t) * 4) != hipSuccess) {
     kano_destroy(ctx);
@@ -2102,6 +2153,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream3m) (void)hipStreamSynchronize(ctx->stream3m);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   if (ctx->gmirror) (void)hipHostFree(ctx->gmirror);
+  if (ctx->row_stage) (void)hipHostFree(ctx->row_stage);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
@@ -2589,10 +2641,14 @@ int kano_get_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* dst) {
   if (nrows < 0 || r0 < ctx->r0 || r0 + nrows > ctx->r1 || (!dst && nrows > 0))
     return fail(ctx, -EINVAL, "kano_get_rows: rows outside this shard");
   if (nrows == 0 || ctx->W == 0) return 0;
-  KCHK(hipMemcpy2DAsync(dst, sizeof(u64) * ctx->W, P_<u64>(ctx->M) + (r0 - ctx->r0) * ctx->ldM,
-                        sizeof(u64) * ctx->ldM, sizeof(u64) * ctx->W, (size_t)nrows,
-                        hipMemcpyDeviceToHost, ctx->stream));
-  return sync(ctx);
+  const size_t bytes = sizeof(u64) * (size_t)ctx->W * (size_t)nrows;
+  const bool staged = ctx->row_stage && bytes <= ROW_STAGE_BYTES;
+  KCHK(hipMemcpy2DAsync(staged ? ctx->row_stage : dst, sizeof(u64) * ctx->W,
+                        P_<u64>(ctx->M) + (r0 - ctx->r0) * ctx->ldM, sizeof(u64) * ctx->ldM,
+                        sizeof(u64) * ctx->W, (size_t)nrows, hipMemcpyDeviceToHost, ctx->stream));
+  KTRY(sync(ctx));
+  if (staged) std::memcpy(dst, ctx->row_stage, bytes);
+  return 0;
 }
 
 int kano_rows_digest(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* out) {
@@ -2754,7 +2810,8 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   sp.nf = ctx->nflags;
   sp.nt = (sp.nf + SH_TILE - 1) / SH_TILE;
   KTRY(dalloc(ctx, ctx->sizes, sizeof(u64) * SZ_SLOTS));
-  KTRY(dalloc(ctx, ctx->flags, ctx->vs_count_only ? 16 : sp.nf + 16));
+  // (the candidate pairs' flags as bits, one 64-bit word per 64 pairs)
+  KTRY(dalloc(ctx, ctx->flags, ctx->vs_count_only ? 16 : 8 * ((sp.nf + 63) / 64) + 16));
   KTRY(dalloc(ctx, ctx->T, sizeof(i64) * std::max<i64>(1, sp.U)));
   KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (sp.U + 1)));
   KTRY(dalloc(ctx, ctx->tp, sizeof(i64) * std::max<i64>(1, sp.rl)));
@@ -3263,25 +3320,21 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
     // the offset scans (toff: SZ_NL; loff), the compaction and the per-pod
     // pair counts, then their offsets (poff: SZ_PAIRS), all behind the tests
     hipStream_t s2 = ctx->stream2;
-    {
+    {   // with them, the per-pod pair offsets from the class counts T (poff:
+        // SZ_PAIRS); the compaction follows, its dispatch marks ev_pairs
       ScanBatch sbs(ctx, true);
       KTRY(shadow_stage_a_scans(ctx, sp, sbs));
-      KTRY(sbs.run());
+      KTRY(sbs.add_class_counts(P_<int32_t>(ctx->rc.cls), P_<i64>(ctx->T), ctx->r0, sp.rl,
+                                P_<i64>(ctx->poff), SZ_PAIRS));
+      KTRY(sbs.run(sp.nt > 0 ? nullptr : ctx->ev_pairs));
     }
     KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, sp.nf)));
     if (sp.nt > 0) {
-      hipLaunchKernelGGL(k_shadow_compact, dim3((unsigned)sp.nt), dim3(TPB), 0, s2,
-                         P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
-                         P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), sp.nf,
-                         P_<i64>(ctx->toff), P_<int2>(ctx->L), sp.nf);
+      launch_marked(k_shadow_compact, dim3((unsigned)sp.nt), dim3(TPB), 0, s2, ctx->ev_pairs,
+                    P_<i64>(ctx->soffc), ctx->rc.U, P_<int32_t>(ctx->slist),
+                    P_<i64>(ctx->pfoff), P_<uint8_t>(ctx->flags), sp.nf, P_<i64>(ctx->toff),
+                    P_<int2>(ctx->L), sp.nf);
       KLAUNCH();
-    }
-    {   // the pair offsets, each pod's count generated from loff in the scan
-        // (its dispatch marks ev_pairs)
-      ScanBatch sbs(ctx, true);
-      KTRY(sbs.add_class_lengths(P_<int32_t>(ctx->rc.cls), P_<i64>(ctx->loff), ctx->r0, sp.rl,
-                                 P_<i64>(ctx->poff), SZ_PAIRS));
-      KTRY(sbs.run(ctx->ev_pairs));
     }
     ctx->tail_compacted = true;
   }

@@ -1558,27 +1558,31 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
 // (PB x H words; the k_classbits form sets U-wide columns with one global
 // atomic per select entry, 2e7 of them at the dense sweep's largest point).
 // LDS: PB words per wave (dynamic).
+// (ldA >= H columns, PBp >= PB rows: the padding -- columns h >= H, rows
+// w >= PB -- is written as zeros, the staged GEMM reads whole tiles)
 __global__ __launch_bounds__(TPB) void k_heavy_selT(const int32_t* __restrict__ hlist, i64 H,
-                                                    const i64* __restrict__ soffc,
-                                                    const int32_t* __restrict__ slist, i64 PB,
+                                                    i64 ldA, const i64* __restrict__ soffc,
+                                                    const int32_t* __restrict__ slist, i64 PBp,
                                                     u64* __restrict__ A) {
   extern __shared__ __attribute__((aligned(16))) u64 col[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const i64 h = (i64)blockIdx.x * (TPB / 64) + wv;
-  if (h >= H) return;                                 // wave-uniform; no block barrier
-  u64* cw = col + (i64)wv * PB;
-  for (i64 w = lane; w < PB; w += 64) cw[w] = 0ull;
+  if (h >= ldA) return;                               // wave-uniform; no block barrier
+  u64* cw = col + (i64)wv * PBp;
+  for (i64 w = lane; w < PBp; w += 64) cw[w] = 0ull;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
-  const int32_t c = hlist[h];
-  const i64 e1 = soffc[c + 1];
-  for (i64 e = soffc[c] + lane; e < e1; e += 64) {
-    const int32_t p = slist[e];
-    atomicOr(&cw[p >> 6], 1ull << (p & 63));
+  if (h < H) {
+    const int32_t c = hlist[h];
+    const i64 e1 = soffc[c + 1];
+    for (i64 e = soffc[c] + lane; e < e1; e += 64) {
+      const int32_t p = slist[e];
+      atomicOr(&cw[p >> 6], 1ull << (p & 63));
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   __builtin_amdgcn_wave_barrier();
-  for (i64 w = lane; w < PB; w += 64) A[w * H + h] = cw[w];
+  for (i64 w = lane; w < PBp; w += 64) A[w * ldA + h] = cw[w];
 }
 
 // The dense contraction at scale (many heavy row classes, broad selectors):
@@ -1659,6 +1663,111 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm(const u64* __restrict__ A,
   }
   // accumulator g of lane (l32, half): row (g&3) + 8 (g>>2) + 4 half, column
   // l32 of its 32 x 32 tile; one ballot per g holds 32 columns of two rows
+  const i64 ld32 = 2 * ldMc;
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const i64 row = rb + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
+      const int32_t hr = row < H ? hlist[row] : -1;
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const u64 bal = __ballot(acc[t][u][g] > 0);
+        const i64 c32 = (cb + 32 * u) >> 5;
+        if (l32 == 0 && hr >= 0 && c32 < ld32)
+          Mc32[(i64)hr * ld32 + c32] = half ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+      }
+    }
+}
+
+// The GEMM with its operands staged through LDS: k_heavy_gemm's tiles, but a
+// block's A and B panels for GK_KC K-steps at a time (GK_KC x (64 TM + 64 TN)
+// words) are copied global -> LDS by the async 16-byte LDS-DMA loads
+// (global_load_lds_dwordx4, no register staging), double-buffered: chunk c+1
+// is in flight while chunk c's 32 TM TN MFMAs per step run, so the loads'
+// latency (the operands sit in the MALL, ~1-2 us away) hides behind
+// ~16 x 1,000 cycles of matrix work instead of one step's.  The operands are
+// padded (zero) to whole block tiles and K chunks (ldA = H rounded up to
+// 64 TM, ldB = Ua rounded up to 64 TN, PB rounded up to GK_KC), so no load
+// leaves its array.  LDS: 2 x GK_KC x (64 TM + 64 TN) x 8 B (128 KB at 4 x 4).
+constexpr int GK_KC = 16;
+template <int TM, int TN>
+__global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ A, i64 ldA,
+                                                        const int32_t* __restrict__ hlist, i64 H,
+                                                        const u64* __restrict__ B, i64 ldB,
+                                                        i64 Ua, i64 PBp,
+                                                        uint32_t* __restrict__ Mc32, i64 ldMc) {
+  constexpr int BM = 64 * TM, BN = 64 * TN;
+  constexpr int STAGE = GK_KC * (BM + BN);     // words per buffer
+  extern __shared__ __attribute__((aligned(16))) u64 smem[];
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const int wv = threadIdx.x >> 6;
+  constexpr i64 GM = 8;
+  const i64 nbm = (H + BM - 1) / BM, nbn = (Ua + BN - 1) / BN;
+  const i64 total = nbm * nbn, per = (total + 7) / 8;
+  const i64 L = (i64)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= total) return;                             // block-uniform
+  const i64 grp = L / (GM * nbn), first = grp * GM;
+  const i64 gm = nbm - first < GM ? nbm - first : GM;
+  const i64 in = L - grp * GM * nbn;
+  const i64 bm = first + in % gm, bn = in / gm;
+  const i64 rb0 = bm * BM, cb0 = bn * BN;
+  // the copy of one chunk: per K-step a row of BM words of A and BN of B,
+  // 128 words (1 KB) per wave instruction, the block's 4 waves round-robin
+  auto stage = [&](int buf, i64 k0) {
+    u64* dst = smem + (size_t)buf * STAGE;
+    constexpr int PIECES = GK_KC * (BM + BN) / 128;
+    for (int q = wv; q < PIECES; q += TPB / 64) {
+      const int w0 = q * 128;                         // word offset in the stage
+      const int kk = w0 < GK_KC * BM ? w0 / BM : (w0 - GK_KC * BM) / BN;
+      const u64* src = w0 < GK_KC * BM
+                           ? A + (k0 + kk) * ldA + rb0 + (w0 - kk * BM)
+                           : B + (k0 + kk) * ldB + cb0 + (w0 - GK_KC * BM - kk * BN);
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const void*>(src + 2 * lane),
+          (__attribute__((address_space(3))) void*)(dst + w0), 16, 0, 0);
+    }
+  };
+  const int wr = wv >> 1, wc = wv & 1;
+  i32x16 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0;
+  const i64 nchunks = PBp / GK_KC;
+  stage(0, 0);
+  for (i64 c = 0; c < nchunks; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                  // chunk c in LDS, chunk c-1 read by all
+    if (c + 1 < nchunks) stage((int)((c + 1) & 1), (c + 1) * GK_KC);
+    const u64* As = smem + (size_t)(c & 1) * STAGE;
+    const u64* Bs = As + GK_KC * BM;
+#pragma unroll 2
+    for (int kk = 0; kk < GK_KC; ++kk) {
+      u64 aw[TM], bw[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) aw[t] = As[kk * BM + wr * 32 * TM + 32 * t + l32];
+#pragma unroll
+      for (int u = 0; u < TN; ++u) bw[u] = Bs[kk * BN + wc * 32 * TN + 32 * u + l32];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int sh = ks * 32 + half * 16;
+        i32x4 af[TM], bf[TN];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) af[t] = expand16((uint32_t)(aw[t] >> sh) & 0xffffu);
+#pragma unroll
+        for (int u = 0; u < TN; ++u) bf[u] = expand16((uint32_t)(bw[u] >> sh) & 0xffffu);
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int u = 0; u < TN; ++u)
+            acc[t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[t], bf[u], acc[t][u], 0, 0, 0);
+      }
+    }
+  }
+  const i64 rb = rb0 + wr * 32 * TM, cb = cb0 + wc * 32 * TN;
   const i64 ld32 = 2 * ldMc;
 #pragma unroll
   for (int t = 0; t < TM; ++t)
@@ -2339,7 +2448,14 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
           f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
         }
       }
-      if (a.flags) a.flags[t] = (uint8_t)f;   // null: count only (T[c])
+    }
+    // the flags as bits, one ballot word per wave (the wave's 64 pairs are
+    // consecutive: b0 is a multiple of 256); null: count only (T[c])
+    {
+      const u64 bal = __ballot(f != 0);
+      const i64 w0 = b0 + (i64)(threadIdx.x & ~63);
+      if (a.flags && (threadIdx.x & 63) == 0 && w0 < nflags)
+        reinterpret_cast<u64*>(a.flags)[w0 >> 6] = bal;
     }
     const i64 cw = __shfl(c, 0, 64);
     if (__all(c == cw || c < 0)) {
@@ -2537,20 +2653,17 @@ __global__ __launch_bounds__(TPB) void k_shadow_compact(const i64* __restrict__ 
   if (tile_off[gridDim.x] > L_cap) return;        // grid-uniform
   tile_class_range(pfoff, U, nflags, rng);
   const i64 base = (i64)blockIdx.x * SH_TILE + (i64)threadIdx.x * SH_ITEMS;
-  u64 packed = 0;
-  if (base + SH_ITEMS <= nflags) {
-    packed = *reinterpret_cast<const u64*>(flags + base);
-  } else {
-    for (int k = 0; base + k < nflags; ++k) packed |= (u64)flags[base + k] << (8 * k);
-  }
-  const i64 cnt = __popcll(packed);   // flags are 0 / 1 bytes
+  static_assert(SH_ITEMS == 8, "one flag byte (8 pairs) per thread");
+  // (flags are bits, pair t at bit t & 7 of byte t >> 3; bits past nflags are 0)
+  const uint32_t packed = base < nflags ? flags[base >> 3] : 0u;
+  const i64 cnt = __popc(packed);
   i64 tot;
   i64 pos = block_excl_scan(cnt, sm, tot) + tile_off[blockIdx.x];
   if (cnt == 0) return;
   i64 c = class_of_pair(pfoff, rng[0], rng[1], base);
   i64 s0 = soffc[c], s = soffc[c + 1] - s0, p0 = pfoff[c], p1 = pfoff[c + 1];
   for (int k = 0; k < SH_ITEMS; ++k) {
-    if (!((packed >> (8 * k)) & 1ull)) continue;
+    if (!((packed >> k) & 1u)) continue;
     const i64 t = base + k;
     while (t >= p1) {
       ++c;

@@ -154,6 +154,9 @@ struct ScanJob {
   const int32_t* gslot;
   const i64* gloff;
   i64 gm0;
+  // gen = 3: element x is gcnt[gslot[m0 + x]] (policy_shadow's pairs per pod
+  // straight from the per-class counts T, before the lists are compacted)
+  const i64* gcnt;
 };
 constexpr int MAX_SCAN_JOBS = 8;
 constexpr int MAX_PUBLISH = 4;
@@ -255,6 +258,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
       const int32_t c = jb.gslot[jb.gm0 + x];
       v[k] = jb.gloff[c + 1] - jb.gloff[c];
     }
+    else if (jb.gen == 3) v[k] = jb.gcnt[jb.gslot[jb.gm0 + x]];
     else v[k] = jb.in64 ? static_cast<const i64*>(jb.in)[x]
                         : (i64) static_cast<const int32_t*>(jb.in)[x];
     s += v[k];

@@ -35,7 +35,9 @@ if d.get("host_us"):
                                                 "issue_mean", "between_mean") if k in d["host_us"]}
 if d.get("mfma_roofline"):
     m = d["mfma_roofline"]
-    out["mfma"] = {k: m[k] for k in ("achieved", "frac", "avg_ms", "ops_per_build")}
+    out["mfma"] = {k: round(m[k], 3) for k in ("achieved", "frac", "avg_ms")}
+    if m.get("alone"):
+        out["mfma"]["alone"] = (round(m["alone"]["avg_ms"], 3), round(m["alone"]["frac"], 3))
 if "cpu_baseline" in d:
     c = d["cpu_baseline"]
     out["cpu"] = (c["value"], c["cores"], c["verified"])

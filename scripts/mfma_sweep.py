@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "kubernetes-verification_amd"))
 
 VARIANTS = [("bitwise", "bitwise", "hortime=1"), ("gemm22", "mfma", "hgemm=22"),
             ("gemm42", "mfma", "hgemm=42"), ("gemm44", "mfma", "hgemm=44"),
+            ("gemm22reg", "mfma", "hgemm=22,hglds=0"), ("gemm44reg", "mfma", "hgemm=44,hglds=0"),
             ("splitk", "mfma", "hgemm=0"), ("auto", "auto", "hortime=1")]
 
 
@@ -74,7 +75,8 @@ def main():
     variants = VARIANTS
     if a.quick:
         points = [(4, 2000, 0.02), (4, 2000, 0.2), (4, 2000, 0.9)]
-        variants = [v for v in VARIANTS if v[0] in ("bitwise", "gemm22", "auto")]
+        variants = [v for v in VARIANTS if v[0] in ("bitwise", "gemm22", "gemm44", "gemm44reg",
+                                                     "auto")]
     for T, A, b in points:
         t0 = time.perf_counter()
         cl = make_cluster(a.n, a.P, "dense", seed=4, tenants=T, apps=A, broad=b)
