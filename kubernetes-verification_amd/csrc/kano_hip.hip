@@ -154,6 +154,8 @@ struct kano_ctx {
   i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int heavy_expand_lds = 1;  // hexplds=0: the heavy rows' expansion from global memory
+  i64 shadow_grid = 0;       // shgrid=K: k_shadow_test1s on at most K blocks (striding)
+  int scan_items = SCAN_ITEMS;   // scanitems: k_scan_lb's elements per thread (4/8/16/32)
   int gemm_lds = 1;          // hglds=0: k_heavy_gemm (operands from global memory, one
                              // K-step of register prefetch) instead of k_heavy_gemm_lds
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
@@ -396,7 +398,9 @@ void launch_marked(void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds, 
 }
 
 // ---- device-wide scans: batches of k_scan_lb jobs ------------------------
-inline i64 scan_tiles(i64 n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+inline i64 scan_tiles(i64 n, int items = SCAN_ITEMS) {
+  return (n + (i64)TPB * items - 1) / ((i64)TPB * items);
+}
 
 // status slots per region >= slots (grows, zeroing both regions in order)
 int scan_reserve(kano_ctx* ctx, i64 slots, bool side = false) {
@@ -416,7 +420,6 @@ int scan_reserve(kano_ctx* ctx, i64 slots, bool side = false) {
 struct ScanBatch {
   ScanJobs jobs{};
   kano_ctx* ctx;
-  i64 slots = 0, maxt = 1;
   bool side = false;   // on stream2 with its own status regions (no host totals)
   explicit ScanBatch(kano_ctx* c, bool on_side = false) : ctx(c), side(on_side) {
     jobs.count = 0;
@@ -441,13 +444,11 @@ struct ScanBatch {
     j.total = total_slot >= 0 ? P_<u64>(ctx->sizes) + total_slot : nullptr;
     j.total_host = total_slot >= 0 && ctx->gmirror_dev ? ctx->gmirror_dev + total_slot : nullptr;
     j.n = n;
-    j.st = slots;
+    j.st = 0;                  // (status offsets: run(), once the tile length is chosen)
     j.in64 = sizeof(Tin) == 8;
     j.out64 = sizeof(Tout) == 8;
     j.gen = 0;
     j.gcnt = nullptr;
-    slots += 1 + scan_tiles(n);
-    maxt = std::max<i64>(maxt, scan_tiles(n));
     return 0;
   }
   // class-id scan over the representative flags of pods [m0, m0 + n), the
@@ -488,7 +489,7 @@ struct ScanBatch {
     return 0;
   }
   // the launch with only the used job slots in its kernel argument
-  template <int NJ>
+  template <int NJ, int IT>
   void launch_n(dim3 g, u64* cur, u64* nxt, hipEvent_t mark) {
     ScanJobsN<NJ> a;
     for (int q = 0; q < NJ; ++q) a.j[q] = jobs.j[q];
@@ -502,12 +503,35 @@ struct ScanBatch {
     a.sig_val = jobs.sig_val;
     a.sig_ctr = jobs.sig_ctr;
     a.sig_n = jobs.sig_n;
-    launch_marked(k_scan_lb<NJ>, g, dim3(TPB), 0, side ? ctx->stream2 : ctx->stream, mark, a, cur,
-                  nxt, side ? ctx->scan_cap2 : ctx->scan_cap);
+    launch_marked(k_scan_lb<NJ, IT>, g, dim3(TPB), 0, side ? ctx->stream2 : ctx->stream, mark, a,
+                  cur, nxt, side ? ctx->scan_cap2 : ctx->scan_cap);
+  }
+  template <int IT>
+  void launch_it(dim3 g, u64* cur, u64* nxt, hipEvent_t mark) {
+    switch (jobs.count) {
+      case 1: launch_n<1, IT>(g, cur, nxt, mark); break;
+      case 2: launch_n<2, IT>(g, cur, nxt, mark); break;
+      case 3: launch_n<3, IT>(g, cur, nxt, mark); break;
+      case 4: launch_n<4, IT>(g, cur, nxt, mark); break;
+      case 5: launch_n<5, IT>(g, cur, nxt, mark); break;
+      case 6: launch_n<6, IT>(g, cur, nxt, mark); break;
+      case 7: launch_n<7, IT>(g, cur, nxt, mark); break;
+      default: launch_n<MAX_SCAN_JOBS, IT>(g, cur, nxt, mark); break;
+    }
   }
   // mark: an event this launch's dispatch marks (none when no job is queued)
   int run(hipEvent_t mark = nullptr) {
     if (jobs.count == 0) return 0;
+    // the tile length, 256 x 8 elements (knob scanitems: 4 / 16 / 32; longer
+    // tiles -- fewer look-back hops -- measured slower on C3's <= 100k-entry
+    // scans: 32 per thread 0.432 ms a step against 0.377 at 8, 16 0.380)
+    const int items = ctx->scan_items;
+    i64 slots = 0, maxt = 1;
+    for (int q = 0; q < jobs.count; ++q) {
+      jobs.j[q].st = slots;
+      slots += 1 + scan_tiles(jobs.j[q].n, items);
+      maxt = std::max<i64>(maxt, scan_tiles(jobs.j[q].n, items));
+    }
     KTRY(scan_reserve(ctx, slots, side));
     // the host signal: raised once every host mirror of this launch is written
     int writers = jobs.npub > 0 ? 1 : 0;
@@ -532,22 +556,14 @@ struct ScanBatch {
     u64* cur = st + (parity ? cap : 0);
     u64* nxt = st + (parity ? 0 : cap);
     const dim3 g((unsigned)maxt, (unsigned)jobs.count);
-    switch (jobs.count) {
-      case 1: launch_n<1>(g, cur, nxt, mark); break;
-      case 2: launch_n<2>(g, cur, nxt, mark); break;
-      case 3: launch_n<3>(g, cur, nxt, mark); break;
-      case 4: launch_n<4>(g, cur, nxt, mark); break;
-      case 5: launch_n<5>(g, cur, nxt, mark); break;
-      case 6: launch_n<6>(g, cur, nxt, mark); break;
-      case 7: launch_n<7>(g, cur, nxt, mark); break;
-      default: launch_n<MAX_SCAN_JOBS>(g, cur, nxt, mark); break;
-    }
+    if (items == 32) launch_it<32>(g, cur, nxt, mark);
+    else if (items == 16) launch_it<16>(g, cur, nxt, mark);
+    else if (items == 4) launch_it<4>(g, cur, nxt, mark);
+    else launch_it<SCAN_ITEMS>(g, cur, nxt, mark);
     KLAUNCH();
     parity ^= 1;
     jobs.count = 0;
     jobs.npub = 0;
-    slots = 0;
-    maxt = 1;
     return 0;
   }
 };
@@ -2049,6 +2065,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hortime") ctx->time_or = v;
         if (k == "hexplds") ctx->heavy_expand_lds = v;
         if (k == "hglds") ctx->gemm_lds = v;
+        if (k == "shgrid" && v >= 0) ctx->shadow_grid = v;
+        if (k == "scanitems" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->scan_items = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
       }
@@ -2927,7 +2945,8 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     // (one block per virtual block, or a capped striding grid when the test
     // may yield to the grouped count)
     const i64 nvb = sp.nt * SH_ITEMS;
-    const i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
+    i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
+    if (ctx->shadow_grid > 0) grid = std::min<i64>(grid, ctx->shadow_grid);
     // the block's S(c) entries staged in LDS, one candidate pair per thread
     hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
                        P_<i64>(ctx->tcnt));

@@ -206,9 +206,12 @@ __device__ __forceinline__ void scan_sig_arrive(const J& jobs) {
   }
 }
 
-template <int NJ>
+// IT: elements per thread (tile = 256 IT); short arrays take long tiles --
+// fewer tiles, a shorter look-back chain (each hop a cross-XCD round trip)
+template <int NJ, int IT = SCAN_ITEMS>
 __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status,
                                                  u64* __restrict__ clear, i64 nclear) {
+  constexpr i64 TILE = (i64)TPB * IT;
   __shared__ i64 sm[4];
   __shared__ i64 s_tile;
   __shared__ i64 s_prefix;
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
 #pragma unroll
   for (int q = 1; q < NJ; ++q)
     if ((int)blockIdx.y == q) jb = jobs.j[q];
-  const i64 tiles = (jb.n + SCAN_TILE - 1) / SCAN_TILE;
+  const i64 tiles = (jb.n + TILE - 1) / TILE;
   if (jb.n == 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       if (jb.out64) static_cast<i64*>(jb.out)[0] = 0;
@@ -242,11 +245,11 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
   __syncthreads();
   const i64 tile = s_tile;
   if (tile >= tiles) return;
-  const i64 base = tile * SCAN_TILE + (i64)threadIdx.x * SCAN_ITEMS;
-  i64 v[SCAN_ITEMS];
+  const i64 base = tile * TILE + (i64)threadIdx.x * IT;
+  i64 v[IT];
   i64 s = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const i64 x = base + k;
     if (x >= jb.n) v[k] = 0;
     else if (jb.gen == 1) {
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
   if (jb.out64) {
     i64* o = static_cast<i64*>(jb.out);
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
+    for (int k = 0; k < IT; ++k) {
       if (base + k < jb.n) o[base + k] = pre;
       pre += v[k];
     }
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(TPB) void k_scan_lb(ScanJobsN<NJ> jobs, u64* status
   } else {
     int32_t* o = static_cast<int32_t*>(jb.out);
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
+    for (int k = 0; k < IT; ++k) {
       if (base + k < jb.n) o[base + k] = (int32_t)pre;
       pre += v[k];
     }
