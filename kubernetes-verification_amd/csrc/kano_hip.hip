@@ -154,6 +154,8 @@ struct kano_ctx {
   i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int heavy_expand_lds = 1;  // hexplds=0: the heavy rows' expansion from global memory
+  int sel_early = 1;         // selearly=0: k_sel_place only after build sync 2
+  i64 sel_early_cap = -1;    // the early placement's list capacity (-1: none this build)
   i64 shadow_grid = 0;       // shgrid=K: k_shadow_test1s on at most K blocks (striding)
   int scan_items = SCAN_ITEMS;   // scanitems: k_scan_lb's elements per thread (4/8/16/32)
   int gemm_lds = 1;          // hglds=0: k_heavy_gemm (operands from global memory, one
@@ -272,6 +274,7 @@ struct kano_ctx {
   // while the previous matrix write ends
   hipStream_t stream3 = nullptr;
   hipStream_t stream3m = nullptr;    // CU-masked (rows_cu_off), for writes <= rows_cu_bytes
+  bool stream3m_tried = false;       // (made on first use, ensure_masked_stream)
   hipStream_t rows_last = nullptr;   // the stream of the last matrix write
   RowsInputs rin_alt;        // the other set of k_rows' inputs
   int rows_set = 0;          // which physical set the ctx fields hold
@@ -1354,6 +1357,15 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   const i64 ldA = glds ? (H + 64 * tmg - 1) / (64 * tmg) * (64 * tmg) : H;
   const i64 ldB = glds ? (ctx->cc.U + 64 * tng - 1) / (64 * tng) * (64 * tng) : ctx->cc.U;
   const i64 PBp = glds ? (ctx->PB + GK_KC - 1) / GK_KC * GK_KC : ctx->PB;
+  // k_sel_place went out before the sizes (sel_place_early): kept when the
+  // list fitted its capacity, else the sized placement below, on zeroed
+  // cursors, once the early one has ended
+  const bool early_ok = ctx->sel_early_cap >= 0 && ctx->nnz_sel <= ctx->sel_early_cap;
+  if (ctx->sel_early_cap >= 0 && !early_ok) {
+    KCHK(hipStreamSynchronize(ctx->stream));
+    KCHK(hipMemsetAsync(ctx->scur.p, 0, sizeof(int32_t) * std::max<i64>(1, U), ctx->stream));
+  }
+  ctx->sel_early_cap = -1;
   FillJobs carried{};
   {
     FillBatch fb(ctx);
@@ -1371,17 +1383,20 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
       if (!gemm) KTRY(fb.add(ctx->scratch_words, sizeof(u64) * ctx->PB * U, 0u));
     }
     if (extra) KTRY(extra(fb));   // the caller's fills (kano_verify: crosscheck, shadow)
-    // (carried by k_sel_place's launch: it neither reads nor writes them)
+    // (carried by k_sel_place's launch -- or by the lists' launch after an
+    // early placement -- neither of which reads or writes them)
     if (U > 0 && P > 0) carried = fb.take();
     else KTRY(fb.run());
   }
-  if (U > 0 && P > 0) {
+  if (U > 0 && P > 0 && !early_ok) {
     const unsigned nbs = nblk(P, sel_spb(ctx)), nbf = fill_ride_blocks(carried);
     hipLaunchKernelGGL(k_sel_place, dim3(nbs + nbf), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
                        P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur),
-                       P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), sel_spb(ctx), carried, nbs);
+                       P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), sel_spb(ctx), carried, nbs,
+                       std::max<i64>(1, ctx->nnz_sel));
     KLAUNCH();
+    carried = FillJobs{};
   }
   // S(c) sorted, heavy list and work-item map (k_class_lists) and the
   // allowed classes + bits per policy (k_pol_allow_fill): independent, one
@@ -1404,10 +1419,16 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // (the fork point of kano_verify's side stream, when it has one: marked by
   // this dispatch itself, not by a separate event record)
   hipEvent_t fev = ctx->fork_hook ? ctx->ev_fork2 : nullptr;
+  if (!(lists_on && allow_on) && carried.count > 0) {
+    hipLaunchKernelGGL(k_fill_many, dim3(fill_ride_blocks(carried)), dim3(TPB), 0, ctx->stream,
+                       carried);
+    KLAUNCH();
+    carried = FillJobs{};
+  }
   if (lists_on && allow_on) {
-    const unsigned nb1 = nblk(U, TPB / 64);
-    launch_marked(k_lists_allow, dim3(nb1 + nblk(P, WPB)), dim3(TPB), lds, ctx->stream, fev, cla,
-                  paa, nb1);
+    const unsigned nb1 = nblk(U, TPB / 64), nb2 = nblk(P, WPB);
+    launch_marked(k_lists_allow, dim3(nb1 + nb2 + fill_ride_blocks(carried)), dim3(TPB), lds,
+                  ctx->stream, fev, cla, paa, nb1, nb2, carried);
     KLAUNCH();
   } else if (lists_on) {
     launch_marked(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, fev, cla);
@@ -1604,6 +1625,29 @@ int do_rows(kano_ctx* ctx) {
 // in LDS and streamed to its members (k_rows).  It runs on stream3 behind
 // the engine stream's marker ev_rin; unless rows_overlap (kano_verify's
 // asynchronous completion) the engine stream then waits for it.
+// The CU-masked write stream, made on the first write that overlaps a
+// kano_verify build (creating it took ~15 ms of kano_create: every cold
+// build_matrix paid it, and it serves only the pipelined steps)
+int ensure_masked_stream(kano_ctx* ctx) {
+  if (ctx->stream3m || ctx->stream3m_tried || ctx->rows_cu_off <= 0) return 0;
+  ctx->stream3m_tried = true;
+  // bit i = 32a + 8b + c off when (c - a) mod 8 < t and b < beta, K = t * beta:
+  // K CUs of every XCD whether the CUs are numbered XCD-major (XCD a) or
+  // round-robin (XCD c)
+  const int K = ctx->rows_cu_off, t = K < 4 ? 1 : K / 4, beta = K < 4 ? K : 4;
+  uint32_t mask[8];
+  for (int w = 0; w < 8; ++w) {
+    mask[w] = 0xffffffffu;
+    for (int bit = 0; bit < 32; ++bit) {
+      const int i = w * 32 + bit, a = i / 32, b = (i / 8) % 4, c = i % 8;
+      if (((c - a) & 7) < t && b < beta) mask[w] &= ~(1u << bit);
+    }
+  }
+  // (no masked stream: every write takes stream3)
+  if (hipExtStreamCreateWithCUMask(&ctx->stream3m, 8, mask) != hipSuccess) ctx->stream3m = nullptr;
+  return 0;
+}
+
 int launch_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
@@ -1612,6 +1656,7 @@ int launch_rows(kano_ctx* ctx) {
   // (the CU mask only where the write overlaps the next call's build --
   // kano_verify's asynchronous completion; a write the caller waits for
   // takes every CU)
+  if (ctx->rows_overlap) KTRY(ensure_masked_stream(ctx));
   const bool masked = ctx->rows_overlap && ctx->stream3m &&
                       (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
   hipStream_t rs = masked ? ctx->stream3m : ctx->stream3;
@@ -2026,7 +2071,18 @@ int kano_create(int device, kano_ctx** out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
   if (device < 0 || device >= ndev) return -EINVAL;
+  // KANO_CREATE_TRACE=1: the time of each part of context creation (stderr)
+  const bool trace = getenv("KANO_CREATE_TRACE") != nullptr;
+  auto tc0 = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!trace) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "kano_create %s %.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(t - tc0).count());
+    tc0 = t;
+  };
   if (hipSetDevice(device) != hipSuccess) return -EIO;
+  mark("set_device");
   kano_ctx* ctx = new kano_ctx();
   ctx->device = device;
   (void)hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -2066,6 +2122,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hexplds") ctx->heavy_expand_lds = v;
         if (k == "hglds") ctx->gemm_lds = v;
         if (k == "shgrid" && v >= 0) ctx->shadow_grid = v;
+        if (k == "selearly") ctx->sel_early = v;
         if (k == "scanitems" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->scan_items = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
@@ -2084,7 +2141,9 @@ int kano_create(int device, kano_ctx** out) {
     return -EIO;
   }
   ctx->own_stream = true;
+  mark("stream");
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  mark("stage_events");
   // the staged GEMM's LDS (128 KB at 4 x 4) is above the default dynamic cap
   {
     const int lds44 = (int)(sizeof(u64) * 2 * GK_KC * (256 + 256));
@@ -2095,27 +2154,13 @@ int kano_create(int device, kano_ctx** out) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<2, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
   }
+  mark("func_attributes");
   if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
     ctx->stream3 = nullptr;
     kano_destroy(ctx);
     return -EIO;
   }
-  if (ctx->rows_cu_off > 0) {
-    // bit i = 32a + 8b + c off when (c - a) mod 8 < t and b < beta, K = t * beta:
-    // K CUs of every XCD whether the CUs are numbered XCD-major (XCD a) or
-    // round-robin (XCD c)
-    const int K = ctx->rows_cu_off, t = K < 4 ? 1 : K / 4, beta = K < 4 ? K : 4;
-    uint32_t mask[8];
-    for (int w = 0; w < 8; ++w) {
-      mask[w] = 0xffffffffu;
-      for (int bit = 0; bit < 32; ++bit) {
-        const int i = w * 32 + bit, a = i / 32, b = (i / 8) % 4, c = i % 8;
-        if (((c - a) & 7) < t && b < beta) mask[w] &= ~(1u << bit);
-      }
-    }
-    // (no masked stream: every write takes stream3)
-    if (hipExtStreamCreateWithCUMask(&ctx->stream3m, 8, mask) != hipSuccess) ctx->stream3m = nullptr;
-  }
+  mark("write_streams");
   if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
@@ -2135,6 +2180,7 @@ int kano_create(int device, kano_ctx** out) {
     kano_destroy(ctx);
     return -EIO;
   }
+  mark("stream2_events");
   if (hipHostMalloc(reinterpret_cast<void**>(&ctx->ghost), sizeof(u64) * SZ_SLOTS,
                     hipHostMallocDefault) != hipSuccess) {
     kano_destroy(ctx);
@@ -2158,6 +2204,7 @@ int kano_create(int device, kano_ctx** out) {
     kano_destroy(ctx);
     return -ENOMEM;
   }
+  mark("pinned_and_device_buffers");
   *out = ctx;
   return 0;
 }
@@ -2520,6 +2567,24 @@ namespace {
 // rows_now: launch the matrix write here; defer_cols: leave the column
 // checks to the crosscheck pass over Mc (kano_verify), finish_cols() after
 using ExtraFills = std::function<int(FillBatch&)>;
+// k_sel_place before the host has the list sizes (build sync 2): into the
+// lists as the previous build left them, whose capacity bounds the writes;
+// do_back keeps it when the total fitted.  The placement then runs in the
+// sync's round trip instead of after it (C3: ~13 us of the step)
+int sel_place_early(kano_ctx* ctx) {
+  ctx->sel_early_cap = -1;
+  const i64 U = ctx->rc.U, P = ctx->P;
+  if (!ctx->sel_early || U == 0 || P == 0 || !ctx->slist.p || !ctx->ecls.p) return 0;
+  const i64 cap = (i64)(std::min(ctx->slist.bytes, ctx->ecls.bytes) / sizeof(int32_t));
+  hipLaunchKernelGGL(k_sel_place, dim3(nblk(P, sel_spb(ctx))), dim3(TPB), 0, ctx->stream, P,
+                     P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen), P_<int32_t>(ctx->sm.gmem),
+                     P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur), P_<int32_t>(ctx->slist),
+                     P_<int32_t>(ctx->ecls), sel_spb(ctx), FillJobs{}, nblk(P, sel_spb(ctx)), cap);
+  KLAUNCH();
+  ctx->sel_early_cap = cap;
+  return 0;
+}
+
 int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
                const ExtraFills& extra = ExtraFills(), const ExtraFills& pre_fill = ExtraFills(),
                const PreRun& pre_run = PreRun()) {
@@ -2535,6 +2600,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->cols_valid = false;
   ctx->shadow_total = -1;
   ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
+  ctx->sel_early_cap = -1;
   const i64 rl = rows_local(ctx);
   if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
     KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM)));
@@ -2546,6 +2612,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   // of the back end (zeroed AC / Mc, the crosscheck's group-key sort)
   KTRY(mirror_begin(ctx));
   KTRY(do_back_pre(ctx, pre_fill, pre_run));
+  KTRY(sel_place_early(ctx));
   KTRY(read_sizes(ctx));
   KTRY(stage_mark(ctx, 3, ctx->stream));
   ctx->cols_deferred = defer_cols;

@@ -748,7 +748,10 @@ __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict_
                                                    const i64* __restrict__ soffc, int32_t* scur,
                                                    int32_t* __restrict__ slist,
                                                    int32_t* __restrict__ ecls, int spb,
-                                                   FillJobs fj, unsigned nbs) {
+                                                   FillJobs fj, unsigned nbs, i64 cap) {
+  // cap: the entries slist / ecls hold -- launched before the host knows
+  // their total (the previous build's capacity), an entry past it is dropped
+  // and the host, seeing the total, places again into a larger list
   if (blockIdx.x >= nbs) {                         // block-uniform
     fill_item(fj, blockIdx.x - nbs, gridDim.x - nbs);
     return;
@@ -779,8 +782,10 @@ __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict_
         atomicAdd(&lcnt[t], 1);
       } else {
         const i64 e = soffc[c] + atomicAdd(&scur[c], 1);
-        slist[e] = (int32_t)p;
-        ecls[e] = c;
+        if (e < cap) {
+          slist[e] = (int32_t)p;
+          ecls[e] = c;
+        }
       }
     }
   }
@@ -804,8 +809,10 @@ __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict_
       const int t = lds_class_slot(lkey, c, false);
       if (t < 0) continue;                            // placed in pass 1
       const i64 e = soffc[c] + lbase[t] + atomicAdd(&lcnt[t], 1);
-      slist[e] = (int32_t)p;
-      ecls[e] = c;
+      if (e < cap) {
+        slist[e] = (int32_t)p;
+        ecls[e] = c;
+      }
     }
   }
 }
@@ -1010,10 +1017,12 @@ __global__ __launch_bounds__(TPB) void k_pol_allow_fill(PolAllowArgs a) {
 
 // k_class_lists and k_pol_allow_fill in one launch (independent; both one
 // wave per item, no block barrier): blocks [0, nb1) take the class lists
+// (fills riding in the launch: blocks past nb1 + nb2)
 __global__ __launch_bounds__(TPB) void k_lists_allow(ClassListsArgs a, PolAllowArgs b,
-                                                     unsigned nb1) {
+                                                     unsigned nb1, unsigned nb2, FillJobs fj) {
   if (blockIdx.x < nb1) class_lists_item(a, blockIdx.x);
-  else pol_allow_item(b, blockIdx.x - nb1);
+  else if (blockIdx.x < nb1 + nb2) pol_allow_item(b, blockIdx.x - nb1);
+  else fill_item(fj, blockIdx.x - nb1 - nb2, gridDim.x - nb1 - nb2);
 }
 
 // class-major policy bits for the MFMA path: out[pb][c] bit p%64 = policy p
