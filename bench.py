@@ -210,7 +210,7 @@ def cold_drop_in(cl, config):
     tb = intern(cs, ps)
     parts["intern"] = time.perf_counter() - t
     t = time.perf_counter()
-    eng = DeviceBuild(None)
+    eng = DeviceBuild(None, lean=True)        # (what build_matrix creates)
     parts["context"] = time.perf_counter() - t
     t = time.perf_counter()
     eng.upload(tb)

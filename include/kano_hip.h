@@ -66,6 +66,10 @@ typedef struct kano_ctx kano_ctx;
 /* Lifetime.  No reference counterpart: the reference keeps its state in
  * Python objects (kano_py/kano/model.py:167-169 ReachabilityMatrix.__init__). */
 int  kano_create(int device, kano_ctx** out);
+/* kano_create for builds the caller waits for (the drop-in build_matrix): no
+ * CU-masked write stream (~15 ms of the 23 ms creation); a kano_verify step
+ * on it still overlaps its matrix write with the next call, on every CU */
+int  kano_create_lean(int device, kano_ctx** out);
 void kano_destroy(kano_ctx* ctx);
 const char* kano_last_error(const kano_ctx* ctx);
 int  kano_set_stream(kano_ctx* ctx, void* hip_stream);   /* NULL = own stream */

@@ -1625,9 +1625,9 @@ int do_rows(kano_ctx* ctx) {
 // in LDS and streamed to its members (k_rows).  It runs on stream3 behind
 // the engine stream's marker ev_rin; unless rows_overlap (kano_verify's
 // asynchronous completion) the engine stream then waits for it.
-// The CU-masked write stream, made on the first write that overlaps a
-// kano_verify build (creating it took ~15 ms of kano_create: every cold
-// build_matrix paid it, and it serves only the pipelined steps)
+// The CU-masked write stream (~15 ms to create; it serves only the
+// pipelined kano_verify steps: kano_create_lean skips it)
+thread_local bool g_create_lean = false;
 int ensure_masked_stream(kano_ctx* ctx) {
   if (ctx->stream3m || ctx->stream3m_tried || ctx->rows_cu_off <= 0) return 0;
   ctx->stream3m_tried = true;
@@ -1656,7 +1656,6 @@ int launch_rows(kano_ctx* ctx) {
   // (the CU mask only where the write overlaps the next call's build --
   // kano_verify's asynchronous completion; a write the caller waits for
   // takes every CU)
-  if (ctx->rows_overlap) KTRY(ensure_masked_stream(ctx));
   const bool masked = ctx->rows_overlap && ctx->stream3m &&
                       (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
   hipStream_t rs = masked ? ctx->stream3m : ctx->stream3;
@@ -2065,6 +2064,13 @@ int crosscheck_impl(kano_ctx* ctx, const int32_t* gid, int32_t ngroups = 0) {
 // ===========================================================================
 extern "C" {
 
+int kano_create_lean(int device, kano_ctx** out) {
+  g_create_lean = true;
+  const int rc = kano_create(device, out);
+  g_create_lean = false;
+  return rc;
+}
+
 int kano_create(int device, kano_ctx** out) {
   if (!out) return -EINVAL;
   *out = nullptr;
@@ -2160,6 +2166,11 @@ int kano_create(int device, kano_ctx** out) {
     kano_destroy(ctx);
     return -EIO;
   }
+  // (the CU-masked write stream right after stream3: created later -- on the
+  // first overlapped write -- it shared a hardware queue with the engine
+  // stream and the pipelined step went 0.38 -> 0.68 ms; a lean context, for
+  // builds the caller waits for, has none)
+  if (!g_create_lean) KTRY(ensure_masked_stream(ctx));
   mark("write_streams");
   if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||

@@ -57,11 +57,14 @@ class DeviceBuild:
 
     def __init__(self, tables: Optional[Tables] = None, device: int = 0,
                  rows: Optional[Tuple[int, int]] = None, path: str = "auto",
-                 stream: Optional[int] = None, build: bool = True):
+                 stream: Optional[int] = None, build: bool = True, lean: bool = False):
         self.lib = nat.load()
         self.ctx = c_void_p()
         self._owned = True            # close() destroys the context (not when adopted)
-        rc = self.lib.kano_create(int(device), byref(self.ctx))
+        # lean: kano_create_lean (no CU-masked write stream: builds the caller
+        # waits for, the drop-in build_matrix)
+        create = self.lib.kano_create_lean if lean else self.lib.kano_create
+        rc = create(int(device), byref(self.ctx))
         if rc != 0:
             self.ctx = c_void_p()
             raise nat.KanoNativeError(

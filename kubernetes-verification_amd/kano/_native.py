@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get(
 # Exported symbols, exactly the declarations of include/kano_hip.h.
 SIGNATURES = {
     "kano_create": (c_int, [c_int, POINTER(c_void_p)]),
+"kano_create_lean": (c_int, [c_int, POINTER(c_void_p)]),
     "kano_destroy": (None, [c_void_p]),
     "kano_last_error": (ctypes.c_char_p, [c_void_p]),
     "kano_set_stream": (c_int, [c_void_p, c_void_p]),

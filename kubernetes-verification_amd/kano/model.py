@@ -506,7 +506,7 @@ class ReachabilityMatrix:
             if G > 1:   # one process over G devices: rows sharded (kano/multi.py)
                 engine = MultiBuild(tables, G, devices=requested_devices(G))
             else:
-                engine = DeviceBuild(tables)
+                engine = DeviceBuild(tables, lean=True)
             for p, pol in enumerate(policies):
                 pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
             lists = _BuildLists(engine, containers)

@@ -12,8 +12,10 @@ sys.path.insert(0, os.path.join(HERE, "..", "kubernetes-verification_amd"))
 
 from kano._engine import DeviceBuild  # noqa: E402
 
-for k in range(3):
+for k in range(4):
+    lean = k % 2 == 1                  # kano_create, kano_create_lean alternately
     t = time.perf_counter()
-    e = DeviceBuild(None)
-    print(f"total {(time.perf_counter() - t) * 1e3:.3f} ms", file=sys.stderr, flush=True)
+    e = DeviceBuild(None, lean=lean)
+    print(f"total{' (lean)' if lean else ''} {(time.perf_counter() - t) * 1e3:.3f} ms",
+          file=sys.stderr, flush=True)
     e.close()

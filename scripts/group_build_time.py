@@ -63,7 +63,7 @@ def main():
             ph = []
             for _ in range(3):
                 t0 = time.perf_counter()
-                e = DeviceBuild(None) if g == 1 else MultiBuild(tb, g, devices=[int(x) for x in
+                e = DeviceBuild(None, lean=True) if g == 1 else MultiBuild(tb, g, devices=[int(x) for x in
                                                                                devs.split(",")],
                                                                 build=False)
                 t1 = time.perf_counter()
