@@ -284,7 +284,10 @@ struct kano_ctx {
   // engine stream where the write may start (instead of recording ev_rin)
   hipEvent_t rows_in = nullptr;
   hipEvent_t ev_rin = nullptr;          // k_rows' inputs complete (engine stream)
-  hipEvent_t ev_rows_end[2] = {};       // set k's matrix write done (stream3)
+  hipEvent_t ev_rows_end[2] = {};       // (spare)
+  // set k's matrix write done: the stop event of its k_rows dispatch (a
+  // separate record cost the write stream ~4.5 us between two writes)
+  hipEvent_t rows_end_ev[2] = {};
   bool rows_end_rec[2] = {false, false};
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_sizes = nullptr;
@@ -694,9 +697,9 @@ int swap_rows_inputs(kano_ctx* ctx) {
   ctx->alist_valid = false;
   // (usually long over: then no wait packet on the engine stream)
   if (ctx->rows_end_rec[ctx->rows_set]) {
-    const hipError_t q = hipEventQuery(ctx->ev_rows_end[ctx->rows_set]);
+    const hipError_t q = hipEventQuery(ctx->rows_end_ev[ctx->rows_set]);
     if (q == hipErrorNotReady)
-      KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows_end[ctx->rows_set], 0));
+      KCHK(hipStreamWaitEvent(ctx->stream, ctx->rows_end_ev[ctx->rows_set], 0));
     else
       KCHK(q);
   }
@@ -1311,6 +1314,16 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
 // list) and the compressed matrix Mc (row classes x column classes): light
 // classes by scatter, heavy classes by bitwise OR or the int8 MFMA
 // contraction; column checks at class level
+// the engine stream waits for e -- unless e has completed already: a wait
+// packet on a done event still held the stream ~5 us (the side work's joins)
+int join_event(kano_ctx* ctx, hipEvent_t e) {
+  const hipError_t q = hipEventQuery(e);
+  if (q == hipSuccess) return 0;
+  if (q != hipErrorNotReady) KCHK(q);
+  KCHK(hipStreamWaitEvent(ctx->stream, e, 0));
+  return 0;
+}
+
 int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra) {
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
   // the dense contraction's kernel: the tiled GEMM when it has enough wave
@@ -1414,7 +1427,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // crosscheck's fills and key sort) before the Mc writers below
   if (ctx->pre_ac_pending) {
     ctx->pre_ac_pending = false;
-    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_ac, 0));
+    KTRY(join_event(ctx, ctx->ev_pre_ac));
   }
   // (the fork point of kano_verify's side stream, when it has one: marked by
   // this dispatch itself, not by a separate event record)
@@ -1443,7 +1456,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                                              // engine stream's launches go first)
   if (ctx->pre_side_pending) {
     ctx->pre_side_pending = false;
-    KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_pre_done, 0));
+    KTRY(join_event(ctx, ctx->ev_pre_done));
   }
   // Light rows read either the flat allowed-pod lists (materialised here,
   // one pass over nnz_alw entries) or the column-class member lists (n
@@ -1675,7 +1688,7 @@ int launch_rows(kano_ctx* ctx) {
   KCHK(hipStreamWaitEvent(rs, rin, 0));
   // writes stay in order across the two write streams (M, the input sets)
   if (ctx->rows_last && ctx->rows_last != rs && ctx->rows_end_rec[set ^ 1])
-    KCHK(hipStreamWaitEvent(rs, ctx->ev_rows_end[set ^ 1], 0));
+    KCHK(hipStreamWaitEvent(rs, ctx->rows_end_ev[set ^ 1], 0));
   ctx->rows_last = rs;
   if (ctx->rows_after) KCHK(hipStreamWaitEvent(rs, ctx->rows_after, 0));
   hipEvent_t e0 = ctx->ev_rt[set][0], e1 = ctx->ev_rt[set][1];
@@ -1737,9 +1750,9 @@ int launch_rows(kano_ctx* ctx) {
   ctx->rows_kernel = 2;
   ctx->rows_timed = true;
   ctx->rows_time_pending[set] = true;
-  KCHK(hipEventRecord(ctx->ev_rows_end[set], rs));
+  ctx->rows_end_ev[set] = e1;
   ctx->rows_end_rec[set] = true;
-  if (!ctx->rows_overlap) KCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_rows_end[set], 0));
+  if (!ctx->rows_overlap) KCHK(hipStreamWaitEvent(ctx->stream, e1, 0));
   return 0;
 }
 
@@ -2205,9 +2218,7 @@ int kano_create(int device, kano_ctx** out) {
     return -ENOMEM;
   }
   for (int k = 0; k <= SZ_SIGNAL; ++k) ctx->gmirror[k] = 0;
-  // page-locked staging for short row reads (system_isolation's row): a
-  // copy into pageable memory first set up the runtime's own staging, 8 ms
-  // on the first call of a process
+  // page-locked staging for short row reads (system_isolation's row)
   if (hipHostMalloc(&ctx->row_stage, ROW_STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
     ctx->row_stage = nullptr;
   if (dalloc(ctx, ctx->sig_ctr, sizeof(uint32_t) * 4) != 0 ||
@@ -2739,9 +2750,15 @@ int kano_get_rows(kano_ctx* ctx, int64_t r0, int64_t nrows, uint64_t* dst) {
   if (nrows == 0 || ctx->W == 0) return 0;
   const size_t bytes = sizeof(u64) * (size_t)ctx->W * (size_t)nrows;
   const bool staged = ctx->row_stage && bytes <= ROW_STAGE_BYTES;
-  KCHK(hipMemcpy2DAsync(staged ? ctx->row_stage : dst, sizeof(u64) * ctx->W,
-                        P_<u64>(ctx->M) + (r0 - ctx->r0) * ctx->ldM, sizeof(u64) * ctx->ldM,
-                        sizeof(u64) * ctx->W, (size_t)nrows, hipMemcpyDeviceToHost, ctx->stream));
+  const u64* src = P_<u64>(ctx->M) + (r0 - ctx->r0) * ctx->ldM;
+  void* to = staged ? ctx->row_stage : dst;
+  // (contiguous rows: a linear copy -- the first strided copy of a process
+  // set up its blit kernel, ~8 ms on the first system_isolation call)
+  if (nrows == 1 || ctx->ldM == ctx->W)
+    KCHK(hipMemcpyAsync(to, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  else
+    KCHK(hipMemcpy2DAsync(to, sizeof(u64) * ctx->W, src, sizeof(u64) * ctx->ldM,
+                          sizeof(u64) * ctx->W, (size_t)nrows, hipMemcpyDeviceToHost, ctx->stream));
   KTRY(sync(ctx));
   if (staged) std::memcpy(dst, ctx->row_stage, bytes);
   return 0;
