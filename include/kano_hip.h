@@ -419,6 +419,8 @@ int kano_host_times(kano_ctx* ctx, double* out /* 20 */, int reset);
  * kano_group_info: out[0] = G, out[1] = exchange mode. */
 typedef struct kano_group kano_group;
 int  kano_group_create(int ngpu, const int* devices, kano_group** out);
+/* the same with lean members (kano_create_lean): for the drop-in build_matrix */
+int  kano_group_create_lean(int ngpu, const int* devices, kano_group** out);
 void kano_group_destroy(kano_group* g);
 const char* kano_group_last_error(const kano_group* g);
 int  kano_group_info(kano_group* g, int32_t* out /* 2 */);

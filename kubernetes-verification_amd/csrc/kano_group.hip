@@ -323,9 +323,21 @@ int member_pairs(kano_group* g, int r, i64 cap) {
 
 }  // namespace
 
+static int group_create(int ngpu, const int* devices, bool lean, kano_group** out);
+
 extern "C" {
 
 int kano_group_create(int ngpu, const int* devices, kano_group** out) {
+  return group_create(ngpu, devices, false, out);
+}
+
+int kano_group_create_lean(int ngpu, const int* devices, kano_group** out) {
+  return group_create(ngpu, devices, true, out);
+}
+
+}  // extern "C"
+
+static int group_create(int ngpu, const int* devices, bool lean, kano_group** out) {
   if (!out || ngpu < 1) return -EINVAL;
   *out = nullptr;
   int ndev = 0;
@@ -347,9 +359,9 @@ int kano_group_create(int ngpu, const int* devices, kano_group** out) {
   g->pool.start(g->dev);
   g->m.assign((size_t)ngpu, nullptr);
   g->ev.assign((size_t)ngpu, nullptr);
-  const std::function<int(int)> make = [g](int r) -> int {
+  const std::function<int(int)> make = [g, lean](int r) -> int {
     kano_ctx* c = nullptr;
-    const int rc = kano_create(g->dev[(size_t)r], &c);
+    const int rc = lean ? kano_create_lean(g->dev[(size_t)r], &c) : kano_create(g->dev[(size_t)r], &c);
     if (rc) return rc;
     g->m[(size_t)r] = c;
     return hipEventCreateWithFlags(&g->ev[(size_t)r], hipEventDisableTiming) == hipSuccess ? 0
@@ -380,6 +392,8 @@ int kano_group_create(int ngpu, const int* devices, kano_group** out) {
   *out = g;
   return 0;
 }
+
+extern "C" {
 
 void kano_group_destroy(kano_group* g) {
   if (!g) return;

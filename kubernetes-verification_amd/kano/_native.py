@@ -77,6 +77,7 @@ SIGNATURES = {
     "kano_host_times": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_mfma_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_group_create": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
+"kano_group_create_lean": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
     "kano_group_destroy": (None, [c_void_p]),
     "kano_group_last_error": (ctypes.c_char_p, [c_void_p]),
     "kano_group_info": (c_int, [c_void_p, c_void_p]),

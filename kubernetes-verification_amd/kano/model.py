@@ -21,6 +21,7 @@ There is no CPU fallback: without the HIP library or a GPU the build raises
 from __future__ import annotations
 
 import gc
+import threading
 
 from abc import abstractmethod
 from dataclasses import dataclass, field
@@ -501,12 +502,33 @@ class ReachabilityMatrix:
         gc_was = gc.isenabled()
         gc.disable()
         try:
-            tables = intern(containers, policies)
+            # the engine's contexts are made on a second thread while this
+            # one interns (the native calls release the GIL): ~7 ms per
+            # context off the cold call
             G = requested_gpus()
-            if G > 1:   # one process over G devices: rows sharded (kano/multi.py)
-                engine = MultiBuild(tables, G, devices=requested_devices(G))
-            else:
-                engine = DeviceBuild(tables, lean=True)
+            made: Dict[str, Any] = {}
+
+            def make():
+                try:
+                    made["e"] = (MultiBuild(None, G, devices=requested_devices(G), lean=True)
+                                 if G > 1 else DeviceBuild(None, lean=True))
+                except BaseException as exc:   # noqa: BLE001 (re-raised below)
+                    made["x"] = exc
+            maker = threading.Thread(target=make, name="kano-create")
+            maker.start()
+            try:
+                tables = intern(containers, policies)
+            except BaseException:
+                maker.join()
+                if "e" in made:
+                    made["e"].close()
+                raise
+            maker.join()
+            if "x" in made:
+                raise made["x"]
+            engine = made["e"]
+            engine.upload(tables)
+            engine.build()
             for p, pol in enumerate(policies):
                 pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
             lists = _BuildLists(engine, containers)

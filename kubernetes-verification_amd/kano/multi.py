@@ -65,15 +65,18 @@ def requested_devices(G: int) -> Optional[List[int]]:
 class MultiBuild:
     """A kano_group: G row-shard contexts in one process (see module doc)."""
 
-    def __init__(self, tables: Tables, ngpu: int, devices: Optional[List[int]] = None,
-                 path: str = "auto", build: bool = True):
+    def __init__(self, tables: Optional[Tables], ngpu: int, devices: Optional[List[int]] = None,
+                 path: str = "auto", build: bool = True, lean: bool = False):
         self.lib = nat.load()
         self.g = c_void_p()
         G = int(ngpu)
         devs = None
         if devices is not None:
             devs = np.ascontiguousarray(devices, dtype=np.int32)
-        rc = self.lib.kano_group_create(G, _ptr(devs), byref(self.g))
+        # lean: members without the CU-masked write stream (kano_create_lean;
+        # the drop-in build_matrix)
+        create = self.lib.kano_group_create_lean if lean else self.lib.kano_group_create
+        rc = create(G, _ptr(devs), byref(self.g))
         if rc != 0:
             self.g = c_void_p()
             raise nat.KanoNativeError(f"kano_group_create({G}) failed (rc={rc})")
@@ -81,7 +84,7 @@ class MultiBuild:
         self.path = path
         self.tables = tables
         self.row_span = None
-        self.bounds = shard_bounds(tables.n, G)
+        self.bounds = shard_bounds(tables.n, G) if tables is not None else None
         info = np.zeros(2, dtype=np.int32)
         self.lib.kano_group_info(self.g, _ptr(info))
         self.mode = {1: "rccl all-gather", 2: "device copies"}[int(info[1])]
@@ -94,9 +97,10 @@ class MultiBuild:
             self.members.append(m)
         self.device = self.members[0].device
         self._idx = None
-        self.upload(tables)
-        if build:
-            self.build(path)
+        if tables is not None:   # (None: the caller uploads, then builds)
+            self.upload(tables)
+            if build:
+                self.build(path)
 
     def upload(self, t: Tables) -> None:
         """kano_group_upload: the tables to every member at once, member r's

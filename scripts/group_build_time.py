@@ -63,9 +63,8 @@ def main():
             ph = []
             for _ in range(3):
                 t0 = time.perf_counter()
-                e = DeviceBuild(None, lean=True) if g == 1 else MultiBuild(tb, g, devices=[int(x) for x in
-                                                                               devs.split(",")],
-                                                                build=False)
+                e = DeviceBuild(None, lean=True) if g == 1 else MultiBuild(
+                    tb, g, devices=[int(x) for x in devs.split(",")], build=False, lean=True)
                 t1 = time.perf_counter()
                 if g == 1:
                     e.upload(tb)
