@@ -154,6 +154,9 @@ struct kano_ctx {
   i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int heavy_expand_lds = 1;  // hexplds=0: the heavy rows' expansion from global memory
+  int dx_on = 1;             // dx=0: never the class-indexed LDS counters (k_*_dx); 2: always
+  bool dense_sel = false;    // this build takes them (do_front)
+  int ac_lds = 1;            // aclds=0: AC / ACT bits by global atomics, not LDS rows
   int sel_early = 1;         // selearly=0: k_sel_place only after build sync 2
   i64 sel_early_cap = -1;    // the early placement's list capacity (-1: none this build)
   i64 shadow_grid = 0;       // shgrid=K: k_shadow_test1s on at most K blocks (striding)
@@ -1096,6 +1099,10 @@ int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
 // per-class plan; two host syncs (class counts, list sizes)
 // policies per block of k_pol_counts / k_sel_place: combine the per-class
 // atomics in LDS when many policies share few row classes (broad selectors)
+// policies per block of the class-indexed LDS forms: ~256 blocks (each
+// block flushes its whole table: fewer, fuller blocks)
+int dx_ppb(i64 P) { return (int)std::max<i64>(16, (P + 255) / 256); }
+
 int sel_spb(const kano_ctx* ctx) {
   return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
 }
@@ -1177,7 +1184,22 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(stage_mark(ctx, 2, ctx->stream));
   // allowed classes / pods per policy, then |S(c)| and the rebuild cost
   // (one wave per policy, both sides)
-  if (P > 0) {
+  // broad selectors over few row classes (the previous build's |S| sum >= 32
+  // per class): the class counters meet in LDS tables (k_pol_counts_dx,
+  // k_sel_place_dx); either form gives the same counts and lists
+  ctx->dense_sel = ctx->dx_on && Ur > 0 && Ur <= DX_MAX &&
+                   (ctx->dx_on == 2 || ctx->nnz_sel >= 32 * Ur);   // (dx=2: forced)
+  if (P > 0 && ctx->dense_sel) {
+    const int ppb = dx_ppb(P);
+    hipLaunchKernelGGL(k_pol_counts_dx, dim3((unsigned)((P + ppb - 1) / ppb)), dim3(TPB),
+                       (size_t)(12 * Ur), ctx->stream, P, P_<i64>(ctx->am.pstart),
+                       P_<int32_t>(ctx->am.plen), P_<int32_t>(ctx->am.gmem),
+                       P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca), P_<int32_t>(ctx->acnt),
+                       P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                       P_<int32_t>(ctx->sm.gmem), P_<int32_t>(ctx->scnt),
+                       P_<unsigned long long>(ctx->cost), Ur, ppb);
+    KLAUNCH();
+  } else if (P > 0) {
     const bool sel = Ur > 0;
     hipLaunchKernelGGL(k_pol_counts, dim3(nblk(P, sel_spb(ctx))), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
@@ -1324,6 +1346,18 @@ int join_event(kano_ctx* ctx, hipEvent_t e) {
   return 0;
 }
 
+int sel_place_dx(kano_ctx* ctx, i64 cap) {
+  const i64 U = ctx->rc.U, P = ctx->P;
+  const int ppb = dx_ppb(P);
+  hipLaunchKernelGGL(k_sel_place_dx, dim3((unsigned)((P + ppb - 1) / ppb)), dim3(TPB),
+                     (size_t)(8 * U), ctx->stream, P, P_<i64>(ctx->sm.pstart),
+                     P_<int32_t>(ctx->sm.plen), P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc),
+                     P_<int32_t>(ctx->scur), P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), U,
+                     ppb, cap);
+  KLAUNCH();
+  return 0;
+}
+
 int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra) {
   const i64 U = ctx->rc.U, P = ctx->P, H = ctx->heavy_count, ldMc = ctx->ldC;
   // the dense contraction's kernel: the tiled GEMM when it has enough wave
@@ -1401,7 +1435,9 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     if (U > 0 && P > 0) carried = fb.take();
     else KTRY(fb.run());
   }
-  if (U > 0 && P > 0 && !early_ok) {
+  if (U > 0 && P > 0 && !early_ok && ctx->dense_sel) {
+    KTRY(sel_place_dx(ctx, std::max<i64>(1, ctx->nnz_sel)));
+  } else if (U > 0 && P > 0 && !early_ok) {
     const unsigned nbs = nblk(P, sel_spb(ctx)), nbf = fill_ride_blocks(carried);
     hipLaunchKernelGGL(k_sel_place, dim3(nbs + nbf), dim3(TPB), 0, ctx->stream, P,
                        P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
@@ -1421,8 +1457,12 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   const PolAllowArgs paa{P, P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                          P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
                          P_<u64>(ctx->AC), ctx->ldC};
-  const size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
-                         ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
+  size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
+                   ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
+  // AC[p] built in the wave's LDS row when the rows fit (k_pol_allow)
+  const size_t ac_lds = sizeof(u64) * (size_t)ctx->ldC * WPB;
+  const int ac_rows = ctx->ac_lds && ac_lds <= 64 * 1024 ? 1 : 0;
+  if (ac_rows) lds = std::max(lds, ac_lds);
   // the side work's joins: AC zeroed before the lists, the rest (Mc, the
   // crosscheck's fills and key sort) before the Mc writers below
   if (ctx->pre_ac_pending) {
@@ -1441,13 +1481,14 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   if (lists_on && allow_on) {
     const unsigned nb1 = nblk(U, TPB / 64), nb2 = nblk(P, WPB);
     launch_marked(k_lists_allow, dim3(nb1 + nb2 + fill_ride_blocks(carried)), dim3(TPB), lds,
-                  ctx->stream, fev, cla, paa, nb1, nb2, carried);
+                  ctx->stream, fev, cla, paa, nb1, nb2, carried, ac_rows);
     KLAUNCH();
   } else if (lists_on) {
     launch_marked(k_class_lists, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, fev, cla);
     KLAUNCH();
   } else if (allow_on) {
-    launch_marked(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), 0, ctx->stream, fev, paa);
+    launch_marked(k_pol_allow_fill, dim3(nblk(P, WPB)), dim3(TPB), ac_rows ? ac_lds : 0,
+                  ctx->stream, fev, paa, ac_rows);
     KLAUNCH();
   } else {
     fev = nullptr;
@@ -1508,9 +1549,19 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   if (H > 0) {
     if (mfma) {
       const i64 Ua = ctx->cc.U;
-      hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
-                         P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
-                         P_<int32_t>(ctx->am.gmem), ldB, P_<u64>(ctx->ACT));
+      if (ctx->ac_lds && ldB * 8 <= 64 * 1024 + 2048) {
+        // (ACT rows through LDS, one block per 64 policies)
+        const i64 ns = std::min<i64>(8, std::max<i64>(1, 512 / std::max<i64>(1, ctx->PB)));
+        const i64 sw = (ldB + ns - 1) / ns;
+        hipLaunchKernelGGL(k_classbits_rows, dim3((unsigned)ctx->PB, (unsigned)ns), dim3(TPB),
+                           sizeof(u64) * (size_t)sw, ctx->stream, P_<i64>(ctx->am.pstart),
+                           P_<int32_t>(ctx->am.plen), P_<int32_t>(ctx->am.gmem), P, ldB, sw,
+                           P_<u64>(ctx->ACT));
+      } else {
+        hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
+                           P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
+                           P_<int32_t>(ctx->am.gmem), ldB, P_<u64>(ctx->ACT));
+      }
       KLAUNCH();
       // class-major selector bits: selT[pb][c] (the split-K kernel's A; the
       // GEMM builds its own, heavy rows only)
@@ -2142,6 +2193,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hglds") ctx->gemm_lds = v;
         if (k == "shgrid" && v >= 0) ctx->shadow_grid = v;
         if (k == "selearly") ctx->sel_early = v;
+        if (k == "dx") ctx->dx_on = v;
+        if (k == "aclds") ctx->ac_lds = v;
         if (k == "scanitems" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->scan_items = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
@@ -2172,6 +2225,10 @@ int kano_create(int device, kano_ctx** out) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<2, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pol_counts_dx),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 12 * DX_MAX);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_classbits_rows),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 8448);
   }
   mark("func_attributes");
   if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {
@@ -2598,6 +2655,11 @@ int sel_place_early(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, P = ctx->P;
   if (!ctx->sel_early || U == 0 || P == 0 || !ctx->slist.p || !ctx->ecls.p) return 0;
   const i64 cap = (i64)(std::min(ctx->slist.bytes, ctx->ecls.bytes) / sizeof(int32_t));
+  if (ctx->dense_sel) {
+    KTRY(sel_place_dx(ctx, cap));
+    ctx->sel_early_cap = cap;
+    return 0;
+  }
   hipLaunchKernelGGL(k_sel_place, dim3(nblk(P, sel_spb(ctx))), dim3(TPB), 0, ctx->stream, P,
                      P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen), P_<int32_t>(ctx->sm.gmem),
                      P_<i64>(ctx->soffc), P_<int32_t>(ctx->scur), P_<int32_t>(ctx->slist),
@@ -2929,9 +2991,14 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   KTRY(dalloc(ctx, ctx->loff, sizeof(i64) * (sp.U + 1)));
   KTRY(dalloc(ctx, ctx->tp, sizeof(i64) * std::max<i64>(1, sp.rl)));
   KTRY(dalloc(ctx, ctx->poff, sizeof(i64) * (sp.rl + 1)));
-  KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, sp.nt)));
-  KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
-  KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));   // accumulated
+  // (the tiles' pair counts and their offsets feed only the compaction: the
+  // count-only form has none -- at D1, 2e7 tiles, a 160 MB fill and a
+  // 0.3 ms scan)
+  if (!ctx->vs_count_only) {
+    KTRY(dalloc(ctx, ctx->tcnt, sizeof(i64) * std::max<i64>(1, sp.nt)));
+    KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
+    KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));   // accumulated
+  }
   return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
 }
 
@@ -3044,14 +3111,14 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     if (ctx->shadow_grid > 0) grid = std::min<i64>(grid, ctx->shadow_grid);
     // the block's S(c) entries staged in LDS, one candidate pair per thread
     hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
-                       P_<i64>(ctx->tcnt));
+                       ctx->vs_count_only ? (i64*)nullptr : P_<i64>(ctx->tcnt));
     KLAUNCH();
   }
   return 0;
 }
 
 int shadow_stage_a_scans(kano_ctx* ctx, const ShadowPlan& sp, ScanBatch& sb) {
-  KTRY(sb.add(P_<i64>(ctx->tcnt), sp.nt, P_<i64>(ctx->toff), SZ_NL));
+  if (!ctx->vs_count_only) KTRY(sb.add(P_<i64>(ctx->tcnt), sp.nt, P_<i64>(ctx->toff), SZ_NL));
   KTRY(sb.add(P_<i64>(ctx->T), sp.U, P_<i64>(ctx->loff)));
   return 0;
 }
@@ -3120,6 +3187,7 @@ extern "C" {
 
 int kano_shadow(kano_ctx* ctx, int64_t* count) {
   KTRY(ensure_built(ctx));
+  ctx->vs_count_only = false;   // (the pairs: a count-only kano_verify may have run last)
   KTRY(shadow_front(ctx));
   i64 tot[2] = {0, 0};
   KTRY(read_slots(ctx, SZ_NL, 2, tot));

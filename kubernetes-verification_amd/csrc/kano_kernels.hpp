@@ -988,6 +988,139 @@ __global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict
 }
 
 
+// ---- broad selectors over few row classes (D1: every class selected by
+// ~2,250 of 10^4 policies): the per-class counters of k_pol_counts /
+// k_sel_place meet in LDS tables indexed by class (U <= DX_MAX), one global
+// atomic per (block, class) instead of one per select entry -- 36M contended
+// atomics on 8,000 addresses became ~2.5M.  ppb policies per block, one wave
+// per policy; dynamic LDS: 12 U bytes (counts) / 8 U bytes (placement).
+constexpr int DX_MAX = 8192;
+__global__ __launch_bounds__(TPB) void k_pol_counts_dx(i64 P, const i64* __restrict__ apstart,
+                                                       const int32_t* __restrict__ aplen,
+                                                       const int32_t* __restrict__ apcls,
+                                                       const int32_t* __restrict__ csize,
+                                                       int32_t* __restrict__ nca,
+                                                       int32_t* __restrict__ acnt,
+                                                       const i64* __restrict__ spstart,
+                                                       const int32_t* __restrict__ splen,
+                                                       const int32_t* __restrict__ spcls,
+                                                       int32_t* scnt, unsigned long long* cost,
+                                                       i64 U, int ppb) {
+  extern __shared__ __attribute__((aligned(16))) u64 dx[];
+  unsigned long long* lcost = reinterpret_cast<unsigned long long*>(dx);
+  int32_t* lcnt = reinterpret_cast<int32_t*>(dx + U);
+  for (i64 t = threadIdx.x; t < U; t += TPB) {
+    lcost[t] = 0ull;
+    lcnt[t] = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int q = wv; q < ppb; q += TPB / 64) {
+    const i64 p = (i64)blockIdx.x * ppb + q;
+    if (p >= P) break;                               // wave-uniform
+    const int32_t* L = apcls + apstart[p];
+    const int32_t len = aplen[p];
+    i64 pods = 0;
+    for (int32_t k = lane; k < len; k += 64) pods += csize[L[k]];
+    pods = wave_sum(pods);
+    if (lane == 0) {
+      nca[p] = len;
+      acnt[p] = (int32_t)pods;
+    }
+    const int32_t* S = spcls + spstart[p];
+    const int32_t slen = splen[p];
+    const unsigned long long a = (unsigned long long)(int32_t)pods;
+    for (int32_t k = lane; k < slen; k += 64) {
+      const int32_t c = S[k];
+      atomicAdd(&lcnt[c], 1);
+      if (a) atomicAdd(&lcost[c], a);
+    }
+  }
+  __syncthreads();
+  for (i64 t = threadIdx.x; t < U; t += TPB) {
+    if (lcnt[t]) atomicAdd(&scnt[t], lcnt[t]);
+    if (lcost[t]) atomicAdd(&cost[t], lcost[t]);
+  }
+}
+
+// the placement: count per class in LDS, one cursor reservation per (block,
+// class), then the entries at LDS cursors (S(c) is sorted afterwards)
+__global__ __launch_bounds__(TPB) void k_sel_place_dx(i64 P, const i64* __restrict__ pstart,
+                                                      const int32_t* __restrict__ plen,
+                                                      const int32_t* __restrict__ pcls,
+                                                      const i64* __restrict__ soffc,
+                                                      int32_t* scur, int32_t* __restrict__ slist,
+                                                      int32_t* __restrict__ ecls, i64 U, int ppb,
+                                                      i64 cap) {
+  extern __shared__ __attribute__((aligned(16))) u64 dx[];
+  int32_t* lcnt = reinterpret_cast<int32_t*>(dx);
+  int32_t* lbase = lcnt + U;
+  for (i64 t = threadIdx.x; t < U; t += TPB) lcnt[t] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int q = wv; q < ppb; q += TPB / 64) {
+    const i64 p = (i64)blockIdx.x * ppb + q;
+    if (p >= P) break;
+    const int32_t* L = pcls + pstart[p];
+    const int32_t len = plen[p];
+    for (int32_t k = lane; k < len; k += 64) atomicAdd(&lcnt[L[k]], 1);
+  }
+  __syncthreads();
+  for (i64 t = threadIdx.x; t < U; t += TPB) {
+    if (lcnt[t]) {
+      lbase[t] = atomicAdd(&scur[t], lcnt[t]);
+      lcnt[t] = 0;
+    }
+  }
+  __syncthreads();
+  for (int q = wv; q < ppb; q += TPB / 64) {
+    const i64 p = (i64)blockIdx.x * ppb + q;
+    if (p >= P) break;
+    const int32_t* L = pcls + pstart[p];
+    const int32_t len = plen[p];
+    for (int32_t k = lane; k < len; k += 64) {
+      const int32_t c = L[k];
+      const i64 e = soffc[c] + lbase[c] + atomicAdd(&lcnt[c], 1);
+      if (e < cap) {
+        slist[e] = (int32_t)p;
+        ecls[e] = c;
+      }
+    }
+  }
+}
+
+// ACT rows through LDS: block pb takes policies [64 pb, 64 pb + 64), ORs
+// each one's allowed classes into an LDS row of ld words, then stores the row
+// (every word once, no global atomics; the k_classbits form put ~2e7 global
+// atomics on ACT at D1).  Dynamic LDS: ld words (<= 8,448).
+// (blockIdx.y: a slice [c0, c0 + sw) of the row, so that PB blocks become
+// PB x gridDim.y -- each block reads every list of its 64 policies, keeps
+// the entries of its slice)
+__global__ __launch_bounds__(TPB) void k_classbits_rows(const i64* __restrict__ pstart,
+                                                        const int32_t* __restrict__ plen,
+                                                        const int32_t* __restrict__ pcls, i64 P,
+                                                        i64 ld, i64 sw, u64* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) u64 row[];
+  const i64 c0 = (i64)blockIdx.y * sw, c1 = min(ld, c0 + sw);
+  for (i64 w = threadIdx.x; w < c1 - c0; w += TPB) row[w] = 0ull;
+  __syncthreads();
+  const i64 pb = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int q = wv; q < 64; q += TPB / 64) {
+    const i64 p = pb * 64 + q;
+    if (p >= P) break;
+    const int32_t* L = pcls + pstart[p];
+    const int32_t len = plen[p];
+    // (the row is class-indexed, word ca of bit q: u64 atomics in LDS)
+    for (int32_t k = lane; k < len; k += 64) {
+      const i64 ca = L[k];
+      if (ca >= c0 && ca < c1) atomicOr(&row[ca - c0], 1ull << q);
+    }
+  }
+  __syncthreads();
+  for (i64 w = threadIdx.x; w < c1 - c0; w += TPB) out[pb * ld + c0 + w] = row[w];
+}
+
 // block per policy: allowed class list (alc) and its bits AC[p]
 struct PolAllowArgs {
   i64 P;
@@ -999,29 +1132,50 @@ struct PolAllowArgs {
   u64* AC;
   i64 ldC;
 };
-__device__ __forceinline__ void pol_allow_item(const PolAllowArgs& a, i64 vb) {
+// (lds_row: the wave builds AC[p] in its LDS row of ldC words and stores it
+// whole -- long allow lists put thousands of same-word global atomics on
+// one row; the row needs ldC * 8 * WPB bytes of the launch's dynamic LDS)
+__device__ __forceinline__ void pol_allow_item(const PolAllowArgs& a, i64 vb, bool lds_row) {
   const i64 p = vb * WPB + (threadIdx.x >> 6);
-  if (p >= a.P) return;
+  if (p >= a.P) return;                          // wave-uniform; no block barrier
   const int32_t* L = a.pcls + a.pstart[p];
   const int32_t len = a.plen[p];
   int32_t* out = a.alc + a.alcoff[p];
-  for (int32_t k = threadIdx.x & 63; k < len; k += 64) {
+  const int lane = threadIdx.x & 63;
+  if (lds_row) {
+    extern __shared__ __attribute__((aligned(16))) u64 lds_rows[];
+    u64* r = lds_rows + (i64)(threadIdx.x >> 6) * a.ldC;
+    for (i64 w = lane; w < a.ldC; w += 64) r[w] = 0ull;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int32_t k = lane; k < len; k += 64) {
+      const int32_t ca = L[k];
+      out[k] = ca;
+      atomicOr(&r[ca >> 6], 1ull << (ca & 63));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (i64 w = lane; w < a.ldC; w += 64) a.AC[p * a.ldC + w] = r[w];
+    return;
+  }
+  for (int32_t k = lane; k < len; k += 64) {
     const int32_t ca = L[k];
     out[k] = ca;
     atomicOr(&a.AC[p * a.ldC + (ca >> 6)], 1ull << (ca & 63));
   }
 }
-__global__ __launch_bounds__(TPB) void k_pol_allow_fill(PolAllowArgs a) {
-  pol_allow_item(a, blockIdx.x);
+__global__ __launch_bounds__(TPB) void k_pol_allow_fill(PolAllowArgs a, int lds_row) {
+  pol_allow_item(a, blockIdx.x, lds_row != 0);
 }
 
 // k_class_lists and k_pol_allow_fill in one launch (independent; both one
 // wave per item, no block barrier): blocks [0, nb1) take the class lists
 // (fills riding in the launch: blocks past nb1 + nb2)
 __global__ __launch_bounds__(TPB) void k_lists_allow(ClassListsArgs a, PolAllowArgs b,
-                                                     unsigned nb1, unsigned nb2, FillJobs fj) {
+                                                     unsigned nb1, unsigned nb2, FillJobs fj,
+                                                     int lds_row) {
   if (blockIdx.x < nb1) class_lists_item(a, blockIdx.x);
-  else if (blockIdx.x < nb1 + nb2) pol_allow_item(b, blockIdx.x - nb1);
+  else if (blockIdx.x < nb1 + nb2) pol_allow_item(b, blockIdx.x - nb1, lds_row != 0);
   else fill_item(fj, blockIdx.x - nb1 - nb2, gridDim.x - nb1 - nb2);
 }
 
@@ -2475,7 +2629,7 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
       atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
     }
     const i64 tot = block_sum((i64)f, sm);
-    if (threadIdx.x == 0 && tot)
+    if (threadIdx.x == 0 && tot && tile_cnt)   // (null: count only)
       atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
     if ((i64)gridDim.x >= nvb) break;           // one virtual block per block (uniform)
     __syncthreads();                             // LDS reused by the next virtual block
