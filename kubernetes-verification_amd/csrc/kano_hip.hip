@@ -158,6 +158,8 @@ struct kano_ctx {
   bool dense_sel = false;    // this build takes them (do_front)
   int ac_lds = 1;            // aclds=0: AC / ACT bits by global atomics, not LDS rows
   int sel_early = 1;         // selearly=0: k_sel_place only after build sync 2
+  int rows_early = 1;        // rowsearly=0: kano_verify's write waits for the tail's copy
+  bool rin_marked = false;   // this build's last Mc launch marked ev_rin_e
   i64 sel_early_cap = -1;    // the early placement's list capacity (-1: none this build)
   i64 shadow_grid = 0;       // shgrid=K: k_shadow_test1s on at most K blocks (striding)
   int scan_items = SCAN_ITEMS;   // scanitems: k_scan_lb's elements per thread (4/8/16/32)
@@ -287,6 +289,7 @@ struct kano_ctx {
   // engine stream where the write may start (instead of recording ev_rin)
   hipEvent_t rows_in = nullptr;
   hipEvent_t ev_rin = nullptr;          // k_rows' inputs complete (engine stream)
+  hipEvent_t ev_rin_e = nullptr;        // the same, marked by do_back's last launch
   hipEvent_t ev_rows_end[2] = {};       // (spare)
   // set k's matrix write done: the stop event of its k_rows dispatch (a
   // separate record cost the write stream ~4.5 us between two writes)
@@ -1516,7 +1519,13 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   const bool scatter_on = U > 0 && ctx->nnz_sel > 0;
   const bool pods_in_scatter = ctx->rows_use_alist && scatter_on && P > 0 && ctx->cc.U > 0;
   if (ctx->rows_use_alist) KTRY(build_alist(ctx, nullptr, !pods_in_scatter));
+  ctx->rin_marked = false;
   if (U == 0) return ctx->fork_hook ? ctx->fork_hook(fork_marked) : 0;
+  // (with no heavy rows and the column checks deferred, the owner launch
+  // below is the last producer of every k_rows input: its dispatch marks
+  // ev_rin_e, where kano_verify's write may start -- beside this call's tail
+  // instead of behind it)
+  hipEvent_t rin_mark = ctx->rows_early && H == 0 && ctx->cols_deferred ? ctx->ev_rin_e : nullptr;
   if (scatter_on && (size_t)ldMc * 8 * (TPB / 64) <= 64 * 1024) {
     // light Mc rows by their owner (a wave per row class, the row in LDS,
     // plain stores)
@@ -1527,24 +1536,27 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
                         P_<u64>(ctx->Mc), ldMc};
     if (pods_in_scatter) {
       const unsigned nb1 = nblk(P, WPB);
-      hipLaunchKernelGGL(k_pods_own, dim3(nb1 + nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream,
-                         pol_pods_args(ctx), moa, nb1);
+      hipExtLaunchKernelGGL(k_pods_own, dim3(nb1 + nblk(U, TPB / 64)), dim3(TPB), lds,
+                            ctx->stream, nullptr, rin_mark, 0, pol_pods_args(ctx), moa, nb1);
     } else {
-      hipLaunchKernelGGL(k_mc_own, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream, moa);
+      hipExtLaunchKernelGGL(k_mc_own, dim3(nblk(U, TPB / 64)), dim3(TPB), lds, ctx->stream,
+                            nullptr, rin_mark, 0, moa);
     }
     KLAUNCH();
+    ctx->rin_marked = rin_mark != nullptr;
   } else if (scatter_on) {
     // very wide class-level rows: the select entries' allowed classes OR-ed
     // into Mc with atomics (one wave per select entry)
     if (pods_in_scatter) {
       const unsigned nb1 = nblk(P, WPB);
-      hipLaunchKernelGGL(k_pods_scatter, dim3(nb1 + nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
-                         ctx->stream, pol_pods_args(ctx), msa, nb1);
+      hipExtLaunchKernelGGL(k_pods_scatter, dim3(nb1 + nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB),
+                            0, ctx->stream, nullptr, rin_mark, 0, pol_pods_args(ctx), msa, nb1);
     } else {
-      hipLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
-                         ctx->stream, msa);
+      hipExtLaunchKernelGGL(k_mc_scatter, dim3(nblk(ctx->nnz_sel, TPB / 64)), dim3(TPB), 0,
+                            ctx->stream, nullptr, rin_mark, 0, msa);
     }
     KLAUNCH();
+    ctx->rin_marked = rin_mark != nullptr;
   }
   if (H > 0) {
     if (mfma) {
@@ -2193,6 +2205,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hglds") ctx->gemm_lds = v;
         if (k == "shgrid" && v >= 0) ctx->shadow_grid = v;
         if (k == "selearly") ctx->sel_early = v;
+        if (k == "rowsearly") ctx->rows_early = v;
         if (k == "dx") ctx->dx_on = v;
         if (k == "aclds") ctx->ac_lds = v;
         if (k == "scanitems" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->scan_items = v;
@@ -2247,6 +2260,7 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rin, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rin_e, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming) != hipSuccess ||
@@ -2341,7 +2355,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamDestroy(ctx->stream3m);
-  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_sizes,
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_rin_e, ctx->ev_sizes,
                        ctx->ev_fork2, ctx->ev_join2, ctx->ev_pre, ctx->ev_pre_done, ctx->ev_pre_ac, ctx->ev_pairs, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
                        ctx->ev_rows_end[1], ctx->ev_rt[0][0], ctx->ev_rt[0][1], ctx->ev_rt[1][0],
                        ctx->ev_rt[1][1]})
@@ -3623,7 +3637,10 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
   }
   if (ctx->vs_rows) {
     ctx->rows_overlap = async;
-    ctx->rows_in = ctx->ev_tail;
+    // (the build's last Mc launch, when it marked one: the write need not
+    // wait for the checks, the pairs and the copies)
+    ctx->rows_in = ctx->rin_marked ? ctx->ev_rin_e : ctx->ev_tail;
+    ctx->rin_marked = false;
     const int rc = launch_rows(ctx);
     ctx->rows_overlap = false;
     ctx->rows_in = nullptr;
