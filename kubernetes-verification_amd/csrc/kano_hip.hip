@@ -57,8 +57,16 @@ using namespace kano;
 
 namespace {
 constexpr int MAX_CWW = 8192;   // column-chunk width in words (64 KB of LDS)
+// (the pipelined write's chunk: whole rows up to 1M columns in 128 KB of LDS,
+// one block per CU -- measured C5 rank 0 of 8: each chunk re-reads every
+// allowed-pod entry of S(c), so two 64-KB chunks cost 0.3 ms of row builds a
+// step, 8.4 -> 8.0 ms; C5 on one GPU neutral)
+constexpr int MAX_CWW_KNOB = 16384;
 constexpr int HT_ROWS = 128;    // heavy rows per MFMA launch (HT = 4)
-constexpr int ROWS_CH = 16;     // member rows per k_rows work item
+// member rows per k_rows work item (each item rebuilds its class row: C3,
+// 300-step A/Bs, 16 -> 24 took the masked write 0.362 -> 0.355 ms and the
+// step 0.373-0.377 -> 0.361-0.365; 8: 0.443; 64: 0.372)
+constexpr int ROWS_CH = 24;
 constexpr int LD_ALIGN = 16;    // M row pitch multiple, in words (128-B rows: measured +22% k_rows)
 constexpr int MFMA_KMIN = 8;    // min policy blocks (64 policies each) per MFMA wave
 
@@ -166,7 +174,8 @@ struct kano_ctx {
   int gemm_lds = 1;          // hglds=0: k_heavy_gemm (operands from global memory, one
                              // K-step of register prefetch) instead of k_heavy_gemm_lds
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
-  int rows_cww = MAX_CWW;    // cww: k_rows column chunk (words); the chunking wide matrices
+  int rows_ch = ROWS_CH;     // rch=: member rows per k_rows work item
+  int rows_cww = MAX_CWW_KNOB;   // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
   int stream_prio = 1;       // prio=0: every stream at normal priority
   // The matrix write shares the device with the next kano_verify's build
@@ -1219,7 +1228,7 @@ int do_front(kano_ctx* ctx, int path) {
     a.cost = P_<unsigned long long>(ctx->cost);
     a.mcnt = P_<int32_t>(ctx->rc.mcnt);
     a.W = ctx->W;
-    a.ch = ROWS_CH;
+    a.ch = ctx->rows_ch;
     a.force = path == KANO_PATH_MFMA ? 2 : 0;
     a.wicnt = P_<int32_t>(ctx->wicnt);
     a.hflag = P_<int32_t>(ctx->hflag);
@@ -1797,7 +1806,7 @@ int launch_rows(kano_ctx* ctx) {
   a.r0 = ctx->r0;
   a.n = n;
   a.W = W;
-  a.ch = ROWS_CH;
+  a.ch = ctx->rows_ch;
   a.cww = cww;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
@@ -2185,7 +2194,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "packed") ctx->cls_packed = v;
         if (k == "podword") ctx->cls_podword = v;
         if (k == "store") ctx->rows_plain = v == 0;
-        if (k == "cww" && v >= 16 && v <= MAX_CWW && v % 16 == 0) ctx->rows_cww = v;
+        if (k == "cww" && v >= 16 && v <= MAX_CWW_KNOB && v % 16 == 0) ctx->rows_cww = v;
+        if (k == "rch" && v >= 1 && v <= 1024) ctx->rows_ch = v;
         if (k == "async") ctx->async_rows = v;
         if (k == "shcount" && v >= 0 && v <= 2) ctx->shadow_count_mode = v;
         if (k == "pathdens" && v >= 0 && v <= 101) ctx->path_dens = v;
@@ -2238,6 +2248,9 @@ int kano_create(int device, kano_ctx** out) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<2, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows<1024>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(u64) * MAX_CWW_KNOB);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pol_counts_dx),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 12 * DX_MAX);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_classbits_rows),
