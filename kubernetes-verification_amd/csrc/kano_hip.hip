@@ -178,6 +178,7 @@ struct kano_ctx {
   int rows_cww = MAX_CWW_KNOB;   // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
   int stream_prio = 1;       // prio=0: every stream at normal priority
+  int engine_mask = 0;       // emask=1: engine streams on the CUs the write stream leaves
   // The matrix write shares the device with the next kano_verify's build
   // (asynchronous completion): a write that saturates HBM starves the
   // build's latency-bound kernels (fill 6 -> 62-107 us, class insert 25 ->
@@ -1713,14 +1714,8 @@ int do_rows(kano_ctx* ctx) {
 // The CU-masked write stream (~15 ms to create; it serves only the
 // pipelined kano_verify steps: kano_create_lean skips it)
 thread_local bool g_create_lean = false;
-int ensure_masked_stream(kano_ctx* ctx) {
-  if (ctx->stream3m || ctx->stream3m_tried || ctx->rows_cu_off <= 0) return 0;
-  ctx->stream3m_tried = true;
-  // bit i = 32a + 8b + c off when (c - a) mod 8 < t and b < beta, K = t * beta:
-  // K CUs of every XCD whether the CUs are numbered XCD-major (XCD a) or
-  // round-robin (XCD c)
-  const int K = ctx->rows_cu_off, t = K < 4 ? 1 : K / 4, beta = K < 4 ? K : 4;
-  uint32_t mask[8];
+void rows_cu_mask(int K, uint32_t* mask) {
+  const int t = K < 4 ? 1 : K / 4, beta = K < 4 ? K : 4;
   for (int w = 0; w < 8; ++w) {
     mask[w] = 0xffffffffu;
     for (int bit = 0; bit < 32; ++bit) {
@@ -1728,6 +1723,15 @@ int ensure_masked_stream(kano_ctx* ctx) {
       if (((c - a) & 7) < t && b < beta) mask[w] &= ~(1u << bit);
     }
   }
+}
+int ensure_masked_stream(kano_ctx* ctx) {
+  if (ctx->stream3m || ctx->stream3m_tried || ctx->rows_cu_off <= 0) return 0;
+  ctx->stream3m_tried = true;
+  // bit i = 32a + 8b + c off when (c - a) mod 8 < t and b < beta, K = t * beta:
+  // K CUs of every XCD whether the CUs are numbered XCD-major (XCD a) or
+  // round-robin (XCD c)
+  uint32_t mask[8];
+  rows_cu_mask(ctx->rows_cu_off, mask);
   // (no masked stream: every write takes stream3)
   if (hipExtStreamCreateWithCUMask(&ctx->stream3m, 8, mask) != hipSuccess) ctx->stream3m = nullptr;
   return 0;
@@ -2203,6 +2207,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
         if (k == "prio") ctx->stream_prio = v;
+        if (k == "emask") ctx->engine_mask = v;
         if (k == "sidepre") ctx->side_pre = v;
         if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
@@ -2231,7 +2236,15 @@ int kano_create(int device, kano_ctx** out) {
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   const int prio_main = ctx->stream_prio ? prio_hi : prio_lo;
-  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_main) != hipSuccess) {
+  uint32_t emask[8];
+  const bool em = ctx->engine_mask && !g_create_lean && ctx->rows_cu_off > 0;
+  if (em) {
+    rows_cu_mask(ctx->rows_cu_off, emask);
+    for (auto& w : emask) w = ~w;
+  }
+  if ((em ? hipExtStreamCreateWithCUMask(&ctx->stream, 8, emask)
+          : hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_main)) !=
+      hipSuccess) {
     delete ctx;
     return -EIO;
   }
@@ -2268,7 +2281,9 @@ int kano_create(int device, kano_ctx** out) {
   // builds the caller waits for, has none)
   if (!g_create_lean) KTRY(ensure_masked_stream(ctx));
   mark("write_streams");
-  if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main) != hipSuccess ||
+  if ((em ? hipExtStreamCreateWithCUMask(&ctx->stream2, 8, emask)
+          : hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main)) !=
+          hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
