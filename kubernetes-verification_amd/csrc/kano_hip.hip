@@ -178,6 +178,8 @@ struct kano_ctx {
   int rows_cww = MAX_CWW_KNOB;   // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
   int stream_prio = 1;       // prio=0: every stream at normal priority
+  int shg_sub_lds = 1;       // shgsub=0: k_shg_sub's word-by-word row compare
+  int side_prio = 1;         // sideprio=0: stream2 (the build's side work) at normal priority
   int engine_mask = 0;       // emask=1: engine streams on the CUs the write stream leaves
   // The matrix write shares the device with the next kano_verify's build
   // (asynchronous completion): a write that saturates HBM starves the
@@ -2208,6 +2210,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
         if (k == "prio") ctx->stream_prio = v;
         if (k == "emask") ctx->engine_mask = v;
+        if (k == "sideprio") ctx->side_prio = v;
+        if (k == "shgsub") ctx->shg_sub_lds = v;
         if (k == "sidepre") ctx->side_pre = v;
         if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
@@ -2282,7 +2286,8 @@ int kano_create(int device, kano_ctx** out) {
   if (!g_create_lean) KTRY(ensure_masked_stream(ctx));
   mark("write_streams");
   if ((em ? hipExtStreamCreateWithCUMask(&ctx->stream2, 8, emask)
-          : hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main)) !=
+          : hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking,
+                                        ctx->side_prio ? prio_main : prio_lo)) !=
           hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
@@ -3088,9 +3093,15 @@ int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   const int32_t* Gp = P_<int32_t>(ctx->shg_gidx) + P;
   const u64* nfp = P_<u64>(ctx->sizes) + SZ_NFLAGS;
   const int force = ctx->shadow_count_mode == 2 ? 2 : 0;
-  hipLaunchKernelGGL(k_shg_sub, dim3(nblk(std::min<i64>(P, SHG_MAX), WPB)), dim3(TPB), 0, st, Gp,
-                     P_<int32_t>(ctx->shg_reps), AC, ctx->ldC, ctx->UAW, P_<u64>(ctx->shg_sub),
-                     GW, P_<int32_t>(ctx->shg_err), nfp, force);
+  // (a's allowed classes in LDS, b's through its class list: shgsub=0 the
+  // word-by-word form)
+  const size_t shg_lds = sizeof(u64) * (size_t)WPB * (size_t)ctx->UAW;
+  const int shg_lds_row = ctx->shg_sub_lds && shg_lds <= 64 * 1024 ? 1 : 0;
+  hipLaunchKernelGGL(k_shg_sub, dim3(nblk(std::min<i64>(P, SHG_MAX), WPB)), dim3(TPB),
+                     shg_lds_row ? shg_lds : 0, st, Gp, P_<int32_t>(ctx->shg_reps), AC, ctx->ldC,
+                     ctx->UAW, P_<u64>(ctx->shg_sub), GW, P_<int32_t>(ctx->shg_err), nfp, force,
+                     P_<int32_t>(ctx->nca), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
+                     shg_lds_row);
   KLAUNCH();
   ShadowArgs a{};
   a.U = U;

@@ -345,7 +345,7 @@ def test_rows_variants_forced(name, tune, monkeypatch):
 
 
 # --- policy_shadow's count without the pairs --------------------------------
-@pytest.mark.parametrize("mode", ["shcount=0", "shcount=1", "shcount=2"])
+@pytest.mark.parametrize("mode", ["shcount=0", "shcount=1", "shcount=2", "shcount=2,shgsub=0"])
 @pytest.mark.parametrize("name", ["C2", "s_broad_1000", "s_broad_300", "s_sparse_2000", "q_shadow",
                                   "q_wide_select", "gen_s5_10000", "gen_s4_4000"])
 def test_shadow_count_only_vs_kano_py(name, mode, tmp_path, monkeypatch):
