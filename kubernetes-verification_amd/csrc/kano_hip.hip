@@ -178,6 +178,7 @@ struct kano_ctx {
   int rows_cww = MAX_CWW_KNOB;   // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
   int stream_prio = 1;       // prio=0: every stream at normal priority
+  int dx_ppb = 0;            // dxppb=: policies per block of the dx kernels (0: ~256 blocks)
   int shg_sub_lds = 1;       // shgsub=0: k_shg_sub's word-by-word row compare
   int side_prio = 1;         // sideprio=0: stream2 (the build's side work) at normal priority
   int engine_mask = 0;       // emask=1: engine streams on the CUs the write stream leaves
@@ -1116,7 +1117,9 @@ int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
 // atomics in LDS when many policies share few row classes (broad selectors)
 // policies per block of the class-indexed LDS forms: ~256 blocks (each
 // block flushes its whole table: fewer, fuller blocks)
-int dx_ppb(i64 P) { return (int)std::max<i64>(16, (P + 255) / 256); }
+int dx_ppb(const kano_ctx* ctx, i64 P) {
+  return ctx->dx_ppb > 0 ? ctx->dx_ppb : (int)std::max<i64>(16, (P + 255) / 256);
+}
 
 int sel_spb(const kano_ctx* ctx) {
   return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
@@ -1205,7 +1208,7 @@ int do_front(kano_ctx* ctx, int path) {
   ctx->dense_sel = ctx->dx_on && Ur > 0 && Ur <= DX_MAX &&
                    (ctx->dx_on == 2 || ctx->nnz_sel >= 32 * Ur);   // (dx=2: forced)
   if (P > 0 && ctx->dense_sel) {
-    const int ppb = dx_ppb(P);
+    const int ppb = dx_ppb(ctx, P);
     hipLaunchKernelGGL(k_pol_counts_dx, dim3((unsigned)((P + ppb - 1) / ppb)), dim3(TPB),
                        (size_t)(12 * Ur), ctx->stream, P, P_<i64>(ctx->am.pstart),
                        P_<int32_t>(ctx->am.plen), P_<int32_t>(ctx->am.gmem),
@@ -1363,7 +1366,7 @@ int join_event(kano_ctx* ctx, hipEvent_t e) {
 
 int sel_place_dx(kano_ctx* ctx, i64 cap) {
   const i64 U = ctx->rc.U, P = ctx->P;
-  const int ppb = dx_ppb(P);
+  const int ppb = dx_ppb(ctx, P);
   hipLaunchKernelGGL(k_sel_place_dx, dim3((unsigned)((P + ppb - 1) / ppb)), dim3(TPB),
                      (size_t)(8 * U), ctx->stream, P, P_<i64>(ctx->sm.pstart),
                      P_<int32_t>(ctx->sm.plen), P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc),
@@ -2212,6 +2215,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "emask") ctx->engine_mask = v;
         if (k == "sideprio") ctx->side_prio = v;
         if (k == "shgsub") ctx->shg_sub_lds = v;
+        if (k == "dxppb" && v >= 0 && v <= 4096) ctx->dx_ppb = v;
         if (k == "sidepre") ctx->side_pre = v;
         if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
@@ -2269,6 +2273,8 @@ int kano_create(int device, kano_ctx** out) {
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sizeof(u64) * MAX_CWW_KNOB);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pol_counts_dx),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 12 * DX_MAX);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sel_place_dx),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 12 * DX_MAX);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_classbits_rows),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 8448);

@@ -995,6 +995,7 @@ __global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict
 // atomics on 8,000 addresses became ~2.5M.  ppb policies per block, one wave
 // per policy; dynamic LDS: 12 U bytes (counts) / 8 U bytes (placement).
 constexpr int DX_MAX = 8192;
+constexpr int DX_UNROLL = 4;
 __global__ __launch_bounds__(TPB) void k_pol_counts_dx(i64 P, const i64* __restrict__ apstart,
                                                        const int32_t* __restrict__ aplen,
                                                        const int32_t* __restrict__ apcls,
@@ -1021,7 +1022,14 @@ __global__ __launch_bounds__(TPB) void k_pol_counts_dx(i64 P, const i64* __restr
     const int32_t* L = apcls + apstart[p];
     const int32_t len = aplen[p];
     i64 pods = 0;
-    for (int32_t k = lane; k < len; k += 64) pods += csize[L[k]];
+    // (DX_UNROLL independent loads in flight per lane)
+    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
+      int32_t c[DX_UNROLL];
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) pods += c[u] >= 0 ? csize[c[u]] : 0;
+    }
     pods = wave_sum(pods);
     if (lane == 0) {
       nca[p] = len;
@@ -1030,10 +1038,16 @@ __global__ __launch_bounds__(TPB) void k_pol_counts_dx(i64 P, const i64* __restr
     const int32_t* S = spcls + spstart[p];
     const int32_t slen = splen[p];
     const unsigned long long a = (unsigned long long)(int32_t)pods;
-    for (int32_t k = lane; k < slen; k += 64) {
-      const int32_t c = S[k];
-      atomicAdd(&lcnt[c], 1);
-      if (a) atomicAdd(&lcost[c], a);
+    for (int32_t k0 = lane; k0 < slen; k0 += 64 * DX_UNROLL) {
+      int32_t c[DX_UNROLL];
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < slen ? S[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) {
+        if (c[u] < 0) continue;
+        atomicAdd(&lcnt[c[u]], 1);
+        if (a) atomicAdd(&lcost[c[u]], a);
+      }
     }
   }
   __syncthreads();
@@ -1052,6 +1066,8 @@ __global__ __launch_bounds__(TPB) void k_sel_place_dx(i64 P, const i64* __restri
                                                       int32_t* scur, int32_t* __restrict__ slist,
                                                       int32_t* __restrict__ ecls, i64 U, int ppb,
                                                       i64 cap) {
+  // (8 U B of LDS: two blocks per CU at U = 8,192; an i64 base with soffc
+  // folded in, 12 U B, took one and measured slower, 515 -> 549 us at D1)
   extern __shared__ __attribute__((aligned(16))) u64 dx[];
   int32_t* lcnt = reinterpret_cast<int32_t*>(dx);
   int32_t* lbase = lcnt + U;
@@ -1063,7 +1079,14 @@ __global__ __launch_bounds__(TPB) void k_sel_place_dx(i64 P, const i64* __restri
     if (p >= P) break;
     const int32_t* L = pcls + pstart[p];
     const int32_t len = plen[p];
-    for (int32_t k = lane; k < len; k += 64) atomicAdd(&lcnt[L[k]], 1);
+    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
+      int32_t c[DX_UNROLL];
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u)
+        if (c[u] >= 0) atomicAdd(&lcnt[c[u]], 1);
+    }
   }
   __syncthreads();
   for (i64 t = threadIdx.x; t < U; t += TPB) {
@@ -1078,12 +1101,18 @@ __global__ __launch_bounds__(TPB) void k_sel_place_dx(i64 P, const i64* __restri
     if (p >= P) break;
     const int32_t* L = pcls + pstart[p];
     const int32_t len = plen[p];
-    for (int32_t k = lane; k < len; k += 64) {
-      const int32_t c = L[k];
-      const i64 e = soffc[c] + lbase[c] + atomicAdd(&lcnt[c], 1);
-      if (e < cap) {
-        slist[e] = (int32_t)p;
-        ecls[e] = c;
+    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
+      int32_t c[DX_UNROLL];
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) {
+        if (c[u] < 0) continue;
+        const i64 e = soffc[c[u]] + lbase[c[u]] + atomicAdd(&lcnt[c[u]], 1);
+        if (e < cap) {
+          slist[e] = (int32_t)p;
+          ecls[e] = c[u];
+        }
       }
     }
   }
@@ -1112,9 +1141,13 @@ __global__ __launch_bounds__(TPB) void k_classbits_rows(const i64* __restrict__ 
     const int32_t* L = pcls + pstart[p];
     const int32_t len = plen[p];
     // (the row is class-indexed, word ca of bit q: u64 atomics in LDS)
-    for (int32_t k = lane; k < len; k += 64) {
-      const i64 ca = L[k];
-      if (ca >= c0 && ca < c1) atomicOr(&row[ca - c0], 1ull << q);
+    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
+      int32_t c[DX_UNROLL];
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < DX_UNROLL; ++u)
+        if (c[u] >= c0 && c[u] < c1) atomicOr(&row[c[u] - c0], 1ull << q);
     }
   }
   __syncthreads();
