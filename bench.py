@@ -646,6 +646,8 @@ def group_main(args, torch, cl, tables, gid, shadow):
         step()
     for m in eng.members:
         m.rows_timing(reset=True)
+    # the exchange's own time: HIP events around it on member 0's stream
+    eng.exchange_timing(enable=True, reset=True)
     import gc
     gc.collect()
     gc.disable()
@@ -667,8 +669,11 @@ def group_main(args, torch, cl, tables, gid, shadow):
         ms = rt["sum_ms"] / rt["launches"] if rt["launches"] else float("nan")
         rows.append({"rows": [a, b], "avg_launch_ms": ms, "launches": rt["launches"],
                      "achieved": 8.0 * (b - a) * W / (ms * 1e-3) / 1e9 if ms > 0 else 0.0})
-    # the dominant kernel's roofline: member 0's matrix write (its row shard)
+    xt = eng.exchange_timing(enable=False)
+    # the dominant kernel's roofline: member 0's matrix write (its row shard);
+    # every member's beside it
     r0 = rows[0]
+    fr = [r["achieved"] / HBM_PEAK_GBS for r in rows]
     verified, vdetail = verify_against_golden(args.config, cl, step.results, 1, 0, 0, shadow)
     out = {
         "metric": METRIC, "value": float(n) * n / (elapsed / args.steps), "unit": "pod-pairs/s",
@@ -680,6 +685,7 @@ def group_main(args, torch, cl, tables, gid, shadow):
                    "parallelism": f"rows{N} in one process (kano_group, {eng.mode})",
                    "devices": devices, "path": args.path,
                    "exchange": eng.mode,
+                   "exchange_mode": 1 if eng.mode.startswith("rccl") else 2,
                    "checks": "all_reachable, all_isolated, user_crosscheck(tenant), "
                              "system_isolation(0)" +
                              {"pairs": ", policy_shadow (pairs to the host)",
@@ -691,7 +697,10 @@ def group_main(args, torch, cl, tables, gid, shadow):
                      "frac": r0["achieved"] / HBM_PEAK_GBS, "traffic": None,
                      "alg_bytes_per_launch": 8.0 * (r0["rows"][1] - r0["rows"][0]) * W,
                      "avg_launch_ms": r0["avg_launch_ms"], "launches_timed": r0["launches"],
-                     "members": rows},
+                     "members": rows, "member_frac_min": min(fr), "member_frac_max": max(fr)},
+        "exchange_ms": {"what": f"{3 * W} u64 words per member ({eng.mode}), HIP events on "
+                                "member 0's stream around the exchange",
+                        "calls": xt["calls"], "avg": xt["avg_ms"], "max": xt["max_ms"]},
         "step_ms": {"min": round(float(step_ms.min()), 4),
                     "median": round(float(np.median(step_ms)), 4),
                     "p90": round(float(np.percentile(step_ms, 90)), 4),

@@ -395,10 +395,14 @@ int kano_host_times(kano_ctx* ctx, double* out /* 20 */, int reset);
  * the group): a group call hands every member its part and returns when all
  * are done, so the members' uploads, builds and host syncs overlap.  The
  * column checks exchange the members' [OR | cross | NAND] words: ncclAllGather
- * over xGMI (communicators from ncclCommInitAll) when the devices are
- * distinct and RCCL loads (mode 1), device-to-device copies otherwise (mode
- * 2, e.g. G members on one device; env KANO_GROUP_COPY forces it); every
- * member ORs the gathered words on its device.
+ * over xGMI (communicators from ncclCommInitAll; mode 1) when the devices are
+ * distinct or the flag KANO_GROUP_RCCL asks for it (also for one member),
+ * device-to-device copies (mode 2) when members share a device or
+ * KANO_GROUP_COPY (flag or environment variable) asks for them; every member
+ * ORs the gathered words on its device.  An RCCL exchange that should run and
+ * cannot (librccl missing, ncclCommInitAll failing) fails the create: there is
+ * no silent fall back to copies.  kano_group_last_error(NULL) says why the
+ * last create on this thread failed.
  *   kano_group_upload: kano_set_pods (+ kano_set_expressions when E > 0) +
  *     kano_set_policies on every member, member r's rows [bounds[2r],
  *     bounds[2r+1]) (kano_set_shard) -- the inputs of ReachabilityMatrix.
@@ -406,7 +410,8 @@ int kano_host_times(kano_ctx* ctx, double* out /* 20 */, int reset);
  *   kano_group_build: kano_build on every member at once (the whole matrix).
  *   kano_group_set_groups: kano_set_groups on every member (user_hashmap's
  *     groups, algorithm.py:20-24); kano_group_verify / _checks then take
- *     gid = NULL, ngroups = KANO_STORED_GROUPS.
+ *     gid = NULL, ngroups = KANO_STORED_GROUPS.  gid holds n entries (n of
+ *     kano_group_upload), as for kano_set_groups: the members read all n.
  *   kano_group_verify: kano_verify over the whole matrix -- the three
  *     column lists (all_reachable, all_isolated, user_crosscheck) of every
  *     row, system_isolation(sys_row) from the row's owner, policy_shadow's
@@ -416,11 +421,27 @@ int kano_host_times(kano_ctx* ctx, double* out /* 20 */, int reset);
  *     exchange between two barriers of the member threads, every combine.
  *   kano_group_checks: the same checks over the members' matrices as they
  *     stand (kano_checks_shard), no policy_shadow.
+ *   kano_group_add_policies / kano_group_remove_policies: kano_add_policies /
+ *     kano_remove_policies on every member's rows (§8(f) rank 4); the
+ *     members' new policy ids agree (first_id).
+ *   kano_group_path: kubesv's path relation (kubesv/kubesv/constraint.py:
+ *     233-237) of src's row-sharded matrix into dst (a group over the same
+ *     devices and row bounds holding an n x n matrix): every member's part of
+ *     the one-hop table (kano_path_shard), one exchange (the transport
+ *     above), every member's rows (kano_path_combine); info as kano_path.
+ *   kano_group_exchange_timing: enable >= 0 switches timing of the verify
+ *     exchange (two events on member 0's stream) on / off; out (may be NULL)
+ *     = [exchanges timed, total ms, max ms]; reset != 0 zeroes them.
  * kano_group_info: out[0] = G, out[1] = exchange mode. */
 typedef struct kano_group kano_group;
+#define KANO_GROUP_LEAN 1   /* lean members (kano_create_lean) */
+#define KANO_GROUP_RCCL 2   /* the RCCL exchange even for one member; an error if it fails */
+#define KANO_GROUP_COPY 4   /* device copies even over distinct devices */
 int  kano_group_create(int ngpu, const int* devices, kano_group** out);
 /* the same with lean members (kano_create_lean): for the drop-in build_matrix */
 int  kano_group_create_lean(int ngpu, const int* devices, kano_group** out);
+int  kano_group_create_ex(int ngpu, const int* devices, int flags /* KANO_GROUP_* */,
+                          kano_group** out);
 void kano_group_destroy(kano_group* g);
 const char* kano_group_last_error(const kano_group* g);
 int  kano_group_info(kano_group* g, int32_t* out /* 2 */);
@@ -438,6 +459,13 @@ int  kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngro
                        int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count);
 int  kano_group_checks(kano_group* g, const int32_t* gid, int32_t ngroups, int64_t sys_row,
                        int32_t* idx, int64_t* counts);
+int  kano_group_add_policies(kano_group* g, int64_t Pn, int32_t ncols_x, const int32_t* xval,
+                             const int64_t* sel_off, const int32_t* sel_col,
+                             const int32_t* sel_val, const int64_t* alw_off,
+                             const int32_t* alw_col, const int32_t* alw_val, int64_t* first_id);
+int  kano_group_remove_policies(kano_group* g, int64_t count, const int64_t* ids);
+int  kano_group_path(kano_group* src, kano_group* dst, int hops, int mode, int64_t* info /* 6 */);
+int  kano_group_exchange_timing(kano_group* g, int enable, double* out /* 3 */, int reset);
 
 /* Page-locked host buffers for fast device-to-host result copies. */
 int  kano_host_alloc(size_t bytes, void** out);

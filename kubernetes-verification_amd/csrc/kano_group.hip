@@ -31,6 +31,8 @@
 #include <thread>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "kano_hip.h"
 #include "kano_internal.hpp"
 
@@ -89,9 +91,8 @@ struct Pool {
         cpu_relax();
         if ((k & 0x3ff) == 0 && clk::now() - t0 > std::chrono::milliseconds(2)) {
           std::unique_lock<std::mutex> lk(mu);
-          cv.wait_for(lk, std::chrono::milliseconds(100), [&] {
-            return seq.load(std::memory_order_acquire) != seen || quit.load();
-          });
+          // (no timeout: run() and stop() change seq / quit under the mutex)
+          cv.wait(lk, [&] { return seq.load(std::memory_order_acquire) != seen || quit.load(); });
           t0 = clk::now();
         }
       }
@@ -139,32 +140,43 @@ struct Pool {
   }
 };
 
-typedef int (*NcclCommInitAll)(void**, int, const int*);
-typedef int (*NcclGroupFn)();
-typedef int (*NcclCommDestroy)(void*);
-typedef int (*NcclAllGather)(const void*, void*, size_t, int, void*, hipStream_t);
-constexpr int RCCL_UINT64 = 5;   // ncclUint64 (rccl.h)
-
+// RCCL's entry points, resolved at run time from the librccl already mapped
+// into the process (torch's) or the system one; the types are rccl.h's own
 struct Rccl {
-  NcclCommInitAll init_all = nullptr;
-  NcclGroupFn group_start = nullptr, group_end = nullptr;
-  NcclCommDestroy destroy = nullptr;
-  NcclAllGather all_gather = nullptr;
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
   bool ok() const { return init_all && group_start && group_end && destroy && all_gather; }
+  const char* what(ncclResult_t e) const {
+    return error_string ? error_string(e) : "(no ncclGetErrorString)";
+  }
 };
+
+template <typename F>
+void resolve(F& f, const char* name) {
+  f = reinterpret_cast<F>(kano_int::rccl_symbol(name));
+}
 
 const Rccl& rccl_syms() {
   static Rccl r = [] {
     Rccl x;
-    x.init_all = reinterpret_cast<NcclCommInitAll>(kano_int::rccl_symbol("ncclCommInitAll"));
-    x.group_start = reinterpret_cast<NcclGroupFn>(kano_int::rccl_symbol("ncclGroupStart"));
-    x.group_end = reinterpret_cast<NcclGroupFn>(kano_int::rccl_symbol("ncclGroupEnd"));
-    x.destroy = reinterpret_cast<NcclCommDestroy>(kano_int::rccl_symbol("ncclCommDestroy"));
-    x.all_gather = reinterpret_cast<NcclAllGather>(kano_int::rccl_symbol("ncclAllGather"));
+    resolve(x.init_all, "ncclCommInitAll");
+    resolve(x.group_start, "ncclGroupStart");
+    resolve(x.group_end, "ncclGroupEnd");
+    resolve(x.destroy, "ncclCommDestroy");
+    resolve(x.all_gather, "ncclAllGather");
+    resolve(x.error_string, "ncclGetErrorString");
     return x;
   }();
   return r;
 }
+
+// why the last kano_group_create failed (no group to hold it):
+// kano_group_last_error(NULL)
+thread_local std::string g_create_err;
 
 }  // namespace
 
@@ -173,7 +185,7 @@ struct kano_group {
   std::vector<int> dev;
   std::vector<kano_ctx*> m;
   int mode = 2;                       // 1 RCCL all-gather, 2 device copies
-  std::vector<void*> comms;
+  std::vector<ncclComm_t> comms;
   std::vector<hipEvent_t> ev;         // a member's words are written
   std::vector<void*> xw, xg;          // members' exchange buffers (device)
   std::string err;
@@ -183,6 +195,11 @@ struct kano_group {
   i64 idx_n = -1;
   Pool pool;
   std::atomic<int> failed{0};         // a member's step failed (inside one job)
+  // the verify exchange's time on member 0's stream (kano_group_exchange_timing)
+  bool xtime_on = false;
+  bool xtime_pending = false;
+  hipEvent_t xt0 = nullptr, xt1 = nullptr;
+  double xt_calls = 0, xt_sum = 0, xt_max = 0;
 };
 
 #define KANO_GROUP_TRY(expr) \
@@ -214,48 +231,71 @@ int group_each(kano_group* g, const std::function<int(int)>& f) {
   return 0;
 }
 
-// inside a job: every member's words are written (on its stream) -> every
-// member's gathered buffer holds all of them, rank-major.  Called by every
-// worker; the workers meet at the barriers even when one failed.
-int member_exchange(kano_group* g, int r, int rc) {
-  const i64 nw = 3 * kano_int::ctx_W(g->m[0]);
+// inside a job: member s's nw words at send[s] (written on its stream) ->
+// every member's recv[r] holds all of them, rank-major (send[s] may alias
+// recv[s] + s nw: RCCL's in-place all-gather).  Called by every worker; the
+// workers meet at the barriers even when one failed.  timed: the exchange is
+// bracketed by g->xt0 / xt1 on member 0's stream.
+int member_exchange(kano_group* g, int r, int rc, const std::vector<void*>& send,
+                    const std::vector<void*>& recv, i64 nw, bool timed) {
   kano_ctx* c = g->m[(size_t)r];
+  hipStream_t st = kano_int::ctx_stream(c);
   if (rc) g->failed.store(1);
-  if (g->mode == 2 && !rc && nw > 0 && hipEventRecord(g->ev[(size_t)r], kano_int::ctx_stream(c)) != hipSuccess) {
+  if (g->mode == 2 && !rc && nw > 0 && hipEventRecord(g->ev[(size_t)r], st) != hipSuccess) {
     g->failed.store(1);
     rc = kano_int::ctx_fail(c, -EIO, "recording the member's words event failed");
   }
   g->pool.bar.wait();
   if (g->failed.load()) return rc ? rc : -ECANCELED;
+  if (timed && r == 0 && nw > 0) (void)hipEventRecord(g->xt0, st);
   if (nw > 0 && g->mode == 1) {
     // one thread issues the grouped all-gather over every communicator
     if (r == 0) {
       const Rccl& R = rccl_syms();
-      int e = R.group_start();
-      for (int s = 0; e == 0 && s < g->G; ++s)
-        e = R.all_gather(g->xw[(size_t)s], g->xg[(size_t)s], (size_t)nw, RCCL_UINT64,
+      ncclResult_t e = R.group_start();
+      for (int s = 0; e == ncclSuccess && s < g->G; ++s)
+        e = R.all_gather(send[(size_t)s], recv[(size_t)s], (size_t)nw, ncclUint64,
                          g->comms[(size_t)s], kano_int::ctx_stream(g->m[(size_t)s]));
-      const int e2 = R.group_end();
-      if (e || e2) {
+      const ncclResult_t e2 = R.group_end();
+      if (e != ncclSuccess || e2 != ncclSuccess) {
         g->failed.store(1);
-        rc = kano_int::ctx_fail(c, -EIO, "ncclAllGather over the group failed");
+        rc = kano_int::ctx_fail(c, -EIO, std::string("ncclAllGather over the group failed: ") +
+                                             R.what(e != ncclSuccess ? e : e2));
       }
     }
   } else if (nw > 0) {
-    // device copies: this member pulls every member's words onto its stream
-    hipStream_t st = kano_int::ctx_stream(c);
+    // device copies: this member pulls every other member's words onto its stream
     for (int s = 0; s < g->G && !rc; ++s) {
+      void* dst = static_cast<u64*>(recv[(size_t)r]) + (i64)s * nw;
+      if (dst == send[(size_t)s]) continue;
       if (hipStreamWaitEvent(st, g->ev[(size_t)s], 0) != hipSuccess ||
-          hipMemcpyAsync(static_cast<u64*>(g->xg[(size_t)r]) + (i64)s * nw, g->xw[(size_t)s],
-                         sizeof(u64) * nw, hipMemcpyDefault, st) != hipSuccess) {
+          hipMemcpyAsync(dst, send[(size_t)s], sizeof(u64) * nw, hipMemcpyDefault, st) !=
+              hipSuccess) {
         g->failed.store(1);
         rc = kano_int::ctx_fail(c, -EIO, "the words' device copy failed");
       }
     }
   }
+  if (timed && r == 0 && nw > 0) {
+    (void)hipEventRecord(g->xt1, st);
+    g->xtime_pending = true;
+  }
   g->pool.bar.wait();
   if (g->failed.load()) return rc ? rc : -ECANCELED;
   return 0;
+}
+
+// the last verify's exchange time, once its events are done
+void exchange_time_collect(kano_group* g) {
+  if (!g->xtime_pending) return;
+  g->xtime_pending = false;
+  float ms = 0.f;
+  if (hipEventSynchronize(g->xt1) == hipSuccess &&
+      hipEventElapsedTime(&ms, g->xt0, g->xt1) == hipSuccess) {
+    g->xt_calls += 1;
+    g->xt_sum += ms;
+    g->xt_max = std::max<double>(g->xt_max, ms);
+  }
 }
 
 int group_buffers(kano_group* g) {
@@ -323,37 +363,57 @@ int member_pairs(kano_group* g, int r, i64 cap) {
 
 }  // namespace
 
-static int group_create(int ngpu, const int* devices, bool lean, kano_group** out);
+static int group_create(int ngpu, const int* devices, int flags, kano_group** out);
 
 extern "C" {
 
 int kano_group_create(int ngpu, const int* devices, kano_group** out) {
-  return group_create(ngpu, devices, false, out);
+  return group_create(ngpu, devices, 0, out);
 }
 
 int kano_group_create_lean(int ngpu, const int* devices, kano_group** out) {
-  return group_create(ngpu, devices, true, out);
+  return group_create(ngpu, devices, KANO_GROUP_LEAN, out);
+}
+
+int kano_group_create_ex(int ngpu, const int* devices, int flags, kano_group** out) {
+  return group_create(ngpu, devices, flags, out);
 }
 
 }  // extern "C"
 
-static int group_create(int ngpu, const int* devices, bool lean, kano_group** out) {
-  if (!out || ngpu < 1) return -EINVAL;
+static int create_fail(kano_group* g, int cur, int code, const std::string& msg) {
+  g_create_err = msg;
+  if (g) kano_group_destroy(g);
+  (void)hipSetDevice(cur);
+  return code;
+}
+
+static int group_create(int ngpu, const int* devices, int flags, kano_group** out) {
+  g_create_err.clear();
+  if (!out || ngpu < 1) {
+    g_create_err = "kano_group_create: ngpu < 1 or out NULL";
+    return -EINVAL;
+  }
   *out = nullptr;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -ENODEV;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_create_err = "kano_group_create: no HIP device";
+    return -ENODEV;
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
   kano_group* g = new kano_group();
   g->G = ngpu;
   for (int r = 0; r < ngpu; ++r) {
     const int d = devices ? devices[r] : r;
-    if (d < 0 || d >= ndev) {
-      delete g;
-      return -EINVAL;
-    }
+    if (d < 0 || d >= ndev)
+      return create_fail(g, cur, -EINVAL,
+                         "kano_group_create: device " + std::to_string(d) + " of member " +
+                             std::to_string(r) + " does not exist (" + std::to_string(ndev) +
+                             " devices)");
     g->dev.push_back(d);
   }
-  int cur = 0;
-  (void)hipGetDevice(&cur);
+  const bool lean = flags & KANO_GROUP_LEAN;
   // the member contexts, created at once by their own threads (a context's
   // streams, events and pinned buffers: ~7 ms each, serial for G members)
   g->pool.start(g->dev);
@@ -369,24 +429,40 @@ static int group_create(int ngpu, const int* devices, bool lean, kano_group** ou
   };
   g->pool.run(make);
   for (int r = 0; r < ngpu; ++r)
-    if (g->pool.rc[(size_t)r]) {
-      const int rc = g->pool.rc[(size_t)r];
-      kano_group_destroy(g);
-      (void)hipSetDevice(cur);
-      return rc;
-    }
-  // RCCL over xGMI when the devices are distinct (one communicator per
-  // device, ncclCommInitAll); device copies otherwise
+    if (g->pool.rc[(size_t)r])
+      return create_fail(g, cur, g->pool.rc[(size_t)r],
+                         "kano_group_create: member " + std::to_string(r) + "'s context failed");
+  if (hipEventCreate(&g->xt0) != hipSuccess || hipEventCreate(&g->xt1) != hipSuccess)
+    return create_fail(g, cur, -EIO, "kano_group_create: timing events");
+  // the exchange: RCCL over xGMI (one communicator per device,
+  // ncclCommInitAll) when the devices are distinct, or when asked for
+  // (KANO_GROUP_RCCL: also one member, so that the transport runs on a
+  // one-GPU box); device copies when members share a device or when asked
+  // for (KANO_GROUP_COPY / env KANO_GROUP_COPY).  An RCCL that should run and
+  // does not is an error, never a silent fall back to copies.
   std::vector<int> sorted(g->dev);
   std::sort(sorted.begin(), sorted.end());
   const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  if (ngpu > 1 && distinct && !getenv("KANO_GROUP_COPY")) {
+  const bool copy = (flags & KANO_GROUP_COPY) || getenv("KANO_GROUP_COPY");
+  const bool want = (flags & KANO_GROUP_RCCL) || (ngpu > 1 && distinct && !copy);
+  if (want) {
+    if (!distinct)
+      return create_fail(g, cur, -EINVAL,
+                         "kano_group_create: the RCCL exchange needs distinct devices");
     const Rccl& R = rccl_syms();
-    if (R.ok()) {
-      g->comms.assign((size_t)ngpu, nullptr);
-      if (R.init_all(g->comms.data(), ngpu, g->dev.data()) == 0) g->mode = 1;
-      else g->comms.clear();
+    if (!R.ok())
+      return create_fail(g, cur, -ENOSYS,
+                         "kano_group_create: RCCL is not loadable (librccl: ncclCommInitAll / "
+                         "ncclAllGather missing); KANO_GROUP_COPY selects device copies");
+    g->comms.assign((size_t)ngpu, nullptr);
+    const ncclResult_t e = R.init_all(g->comms.data(), ngpu, g->dev.data());
+    if (e != ncclSuccess) {
+      g->comms.clear();
+      return create_fail(g, cur, -EIO,
+                         std::string("kano_group_create: ncclCommInitAll failed: ") + R.what(e) +
+                             "; KANO_GROUP_COPY selects device copies");
     }
+    g->mode = 1;
   }
   (void)hipSetDevice(cur);
   *out = g;
@@ -402,18 +478,22 @@ void kano_group_destroy(kano_group* g) {
     if (c) kano_destroy(c);
   if (!g->comms.empty()) {
     const Rccl& R = rccl_syms();
-    for (void* c : g->comms)
+    for (ncclComm_t c : g->comms)
       if (c && R.destroy) (void)R.destroy(c);
   }
   for (hipEvent_t e : g->ev)
     if (e) (void)hipEventDestroy(e);
+  if (g->xt0) (void)hipEventDestroy(g->xt0);
+  if (g->xt1) (void)hipEventDestroy(g->xt1);
   for (auto p : g->idx) (void)hipHostFree(p);
   for (auto p : g->pairs)
     if (p) (void)hipHostFree(p);
   delete g;
 }
 
-const char* kano_group_last_error(const kano_group* g) { return g ? g->err.c_str() : "null group"; }
+const char* kano_group_last_error(const kano_group* g) {
+  return g ? g->err.c_str() : g_create_err.c_str();
+}
 
 int kano_group_info(kano_group* g, int32_t* out /* 2 */) {
   if (!g || !out) return -EINVAL;
@@ -477,7 +557,7 @@ int kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngrou
     kano_ctx* c = g->m[(size_t)r];
     int rc = kano_verify_shard(c, path, gid, ngroups, sys_row, with_shadow,
                                static_cast<uint64_t*>(g->xw[(size_t)r]));
-    rc = member_exchange(g, r, rc);
+    rc = member_exchange(g, r, rc, g->xw, g->xg, 3 * kano_int::ctx_W(g->m[0]), g->xtime_on);
     if (rc) return rc;
     int32_t* pp = nullptr;
     i64 cap = -1;
@@ -496,6 +576,7 @@ int kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngrou
     }
     return rc;
   }));
+  exchange_time_collect(g);
   group_lists(g, cnt, idx, counts);
   if (with_shadow) {
     i64 total = 0;
@@ -523,12 +604,104 @@ int kano_group_checks(kano_group* g, const int32_t* gid, int32_t ngroups, int64_
   KANO_GROUP_TRY(group_each(g, [&](int r) {
     kano_ctx* c = g->m[(size_t)r];
     int rc = kano_checks_shard(c, gid, ngroups, sys_row, static_cast<uint64_t*>(g->xw[(size_t)r]));
-    rc = member_exchange(g, r, rc);
+    rc = member_exchange(g, r, rc, g->xw, g->xg, 3 * kano_int::ctx_W(g->m[0]), false);
     if (rc) return rc;
     return kano_verify_combine(c, static_cast<const uint64_t*>(g->xg[(size_t)r]), g->G,
                                g->idx[(size_t)r], cnt[(size_t)r].data(), nullptr, -1, nullptr);
   }));
   group_lists(g, cnt, idx, counts);
+  return 0;
+}
+
+int kano_group_exchange_timing(kano_group* g, int enable, double* out, int reset) {
+  if (!g) return -EINVAL;
+  exchange_time_collect(g);
+  if (enable >= 0) g->xtime_on = enable != 0;
+  if (out) {
+    out[0] = g->xt_calls;
+    out[1] = g->xt_sum;
+    out[2] = g->xt_max;
+  }
+  if (reset) g->xt_calls = g->xt_sum = g->xt_max = 0;
+  return 0;
+}
+
+// incremental updates on every member's row shard (kano_add_policies /
+// kano_remove_policies write only the member's rows; model.py:125-165 over
+// the updated policy list)
+int kano_group_add_policies(kano_group* g, int64_t Pn, int32_t ncols_x, const int32_t* xval,
+                            const int64_t* sel_off, const int32_t* sel_col,
+                            const int32_t* sel_val, const int64_t* alw_off,
+                            const int32_t* alw_col, const int32_t* alw_val, int64_t* first_id) {
+  if (!g) return -EINVAL;
+  std::vector<int64_t> first((size_t)g->G, -1);
+  KANO_GROUP_TRY(group_each(g, [&](int r) {
+    return kano_add_policies(g->m[(size_t)r], Pn, ncols_x, xval, sel_off, sel_col, sel_val,
+                             alw_off, alw_col, alw_val, &first[(size_t)r]);
+  }));
+  for (int r = 1; r < g->G; ++r)
+    if (first[(size_t)r] != first[0])
+      return gfail(g, -EPROTO, "kano_group_add_policies: the members' policy ids diverged");
+  if (first_id) *first_id = first[0];
+  return 0;
+}
+
+int kano_group_remove_policies(kano_group* g, int64_t count, const int64_t* ids) {
+  if (!g) return -EINVAL;
+  return group_each(g, [&](int r) { return kano_remove_policies(g->m[(size_t)r], count, ids); });
+}
+
+// kubesv's path relation (kubesv/kubesv/constraint.py:233-237) over the
+// group's row-sharded matrix: every member writes its rows' part of the
+// one-hop table (kano_path_shard), one exchange gathers the parts (the same
+// transport as the column words: in-place ncclAllGather or device copies),
+// then every member's rows of the path matrix are written into dst's member
+// on the same device (kano_path_combine).  dst: a group over the same
+// devices and row bounds whose members hold a matrix of the same size.
+int kano_group_path(kano_group* src, kano_group* dst, int hops, int mode, int64_t* info) {
+  if (!src || !dst || src == dst) return -EINVAL;
+  if (dst->G != src->G || dst->dev != src->dev)
+    return gfail(src, -EINVAL, "kano_group_path: the groups' devices differ");
+  const int G = src->G;
+  std::vector<int64_t> nws((size_t)G, 0);
+  KANO_GROUP_TRY(group_each(src, [&](int r) {
+    return kano_path_shard_words(src->m[(size_t)r], &nws[(size_t)r]);
+  }));
+  for (int r = 1; r < G; ++r)
+    if (nws[(size_t)r] != nws[0])
+      return gfail(src, -EPROTO, "kano_group_path: the members' column classes differ");
+  const i64 nw = nws[0];
+  std::vector<void*> recv((size_t)G, nullptr), send((size_t)G, nullptr);
+  std::vector<std::array<int64_t, 6>> inf((size_t)G);
+  const int rc = group_each(src, [&](int r) {
+    kano_ctx* c = src->m[(size_t)r];
+    int rc1 = 0;
+    if (nw > 0 && hipMalloc(&recv[(size_t)r], sizeof(u64) * (size_t)(nw * G)) != hipSuccess)
+      rc1 = kano_int::ctx_fail(c, -ENOMEM, "kano_group_path: the gathered table");
+    if (!rc1 && nw > 0) {
+      send[(size_t)r] = static_cast<u64*>(recv[(size_t)r]) + (i64)r * nw;
+      rc1 = kano_path_shard(c, static_cast<uint64_t*>(send[(size_t)r]));
+    }
+    // (every member's buffers exist before anyone reads them: the exchange's
+    // first barrier)
+    rc1 = member_exchange(src, r, rc1, send, recv, nw, false);
+    if (!rc1 && hipStreamSynchronize(kano_int::ctx_stream(c)) != hipSuccess)
+      rc1 = kano_int::ctx_fail(c, -EIO, "kano_group_path: the exchange failed");
+    if (!rc1) {
+      rc1 = kano_path_combine(c, dst->m[(size_t)r], static_cast<const uint64_t*>(recv[(size_t)r]),
+                              G, hops, mode, inf[(size_t)r].data());
+      if (rc1)
+        (void)kano_int::ctx_fail(c, rc1, std::string("kano_path_combine: ") +
+                                             kano_last_error(dst->m[(size_t)r]));
+    }
+    return rc1;
+  });
+  group_each(src, [&](int r) {
+    if (recv[(size_t)r]) (void)hipFree(recv[(size_t)r]);
+    return 0;
+  });
+  if (rc) return rc;
+  if (info) std::memcpy(info, inf[0].data(), sizeof(int64_t) * 6);
   return 0;
 }
 

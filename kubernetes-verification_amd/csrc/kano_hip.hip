@@ -3537,7 +3537,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
       FusedTail ft{};
       ft.status = st + (ctx->vc_parity ? ctx->vc_cap : 0);
       ft.clear = st + (ctx->vc_parity ? 0 : ctx->vc_cap);
-      ft.nclear = region;
+      ft.nclear = ctx->vc_cap;   // the whole other region: a larger earlier launch left words past `region`
       ctx->vc_parity ^= 1;
       ft.idx = P_<int32_t>(ctx->idxd);
       ft.totals = P_<u64>(ctx->sizes) + SZ_IDX0;

@@ -439,15 +439,19 @@ fail:
   return NULL;
 }
 
-/* pending_is(containers, cls, lists) -> bool
+/* pending_is(containers, cls, lists[, order]) -> bool
  *   kano/algorithm.py _fast_path's per-container test: every container is
  *   exactly `cls`, its own select list (_sel) is empty and its only pending
  *   entry is `lists` (the build's view) -- its select_policies is still
- *   exactly that build's list. */
+ *   exactly that build's list; with `order` (the build's container list),
+ *   container i is also order[i] (the caller did not reorder its list). */
 static PyObject* pending_is(PyObject* self, PyObject* args) {
-  PyObject *items, *cls, *lists;
+  PyObject *items, *cls, *lists, *order = NULL;
   (void)self;
-  if (!PyArg_ParseTuple(args, "O!OO", &PyList_Type, &items, &cls, &lists)) return NULL;
+  if (!PyArg_ParseTuple(args, "O!OO|O!", &PyList_Type, &items, &cls, &lists, &PyList_Type,
+                        &order))
+    return NULL;
+  if (order != NULL && PyList_GET_SIZE(order) != PyList_GET_SIZE(items)) Py_RETURN_FALSE;
   PyObject* a_sel = PyUnicode_InternFromString("_sel");
   PyObject* a_pend = PyUnicode_InternFromString("_pending");
   if (a_sel == NULL || a_pend == NULL) {
@@ -460,7 +464,7 @@ static PyObject* pending_is(PyObject* self, PyObject* args) {
   const Py_ssize_t soff = slot_offset(cls, "_sel"), poff = slot_offset(cls, "_pending");
   for (Py_ssize_t i = 0; i < n && ok; ++i) {
     PyObject* c = PyList_GET_ITEM(items, i);
-    if ((PyObject*)Py_TYPE(c) != cls) {
+    if ((PyObject*)Py_TYPE(c) != cls || (order != NULL && PyList_GET_ITEM(order, i) != c)) {
       ok = 0;
       break;
     }

@@ -31,7 +31,10 @@ from typing import Any, Dict, List, Sequence
 
 import numpy as np
 
-from . import _kano_host   # csrc/kano_hostext.c, built in-tree by __graft_entry__.build()
+try:
+    from . import _kano_host   # csrc/kano_hostext.c, built in-tree by __graft_entry__.build()
+except ImportError:            # (missing or built for another interpreter ABI: the
+    _kano_host = None          # Python loops below are the same steps, slower)
 
 ABSENT = -1
 NO_MATCH_RULE = -2
@@ -121,6 +124,8 @@ def _intern_column(labels, k, idx: "_ValueIndex", row: np.ndarray) -> bool:
     steps per pod: v != v first, then the dict of equality classes, ids in
     first-seen order).  Returns False, idx untouched, when a value is
     unhashable (the per-pod loop handles it)."""
+    if _kano_host is None:
+        return False
     out = np.empty(len(labels), np.int32)
     ids: Dict[Any, int] = {}
     try:
@@ -159,6 +164,8 @@ def intern(containers: Sequence, policies: Sequence) -> Tables:
     scanned: Dict[Any, int] = {}
     scan_ids, scan_out = [], None
     keys: Dict[Any, None] = {}
+    if _kano_host is None:
+        cand = None
     if cand is not None:
         scan_ids = [{} for _ in cand]
         scan_out = np.empty((len(cand), n), np.int32)
@@ -292,6 +299,8 @@ def _intern_fast(n, labels, keys, sides, scanned, scan_ids, scan_out):
     when every matcher is the default equality and no term is a
     LabelExpression; None otherwise (intern's own loop then runs)."""
     from .model import LabelExpression
+    if _kano_host is None:
+        return None
     dflt: Dict[type, bool] = {}
     flags = [dflt[t] if (t := type(m)) in dflt else dflt.setdefault(t, is_default_matcher(m))
              for _, _, m in sides]
@@ -413,7 +422,7 @@ def group_ids(containers: Sequence, label) -> np.ndarray:
     dict semantics of user_hashmap (kano_py/kano/algorithm.py:20-24)."""
     from .model import Container
     n = len(containers)
-    if n and type(containers) is list:
+    if n and type(containers) is list and _kano_host is not None:
         # (Container.getValueOrDefault is labels[key] if present, else the
         # default: the native loop does that for exact Containers with dict
         # labels, ids by first appearance as below; anything else -> the loop)

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get(
 # Exported symbols, exactly the declarations of include/kano_hip.h.
 SIGNATURES = {
     "kano_create": (c_int, [c_int, POINTER(c_void_p)]),
-"kano_create_lean": (c_int, [c_int, POINTER(c_void_p)]),
+    "kano_create_lean": (c_int, [c_int, POINTER(c_void_p)]),
     "kano_destroy": (None, [c_void_p]),
     "kano_last_error": (ctypes.c_char_p, [c_void_p]),
     "kano_set_stream": (c_int, [c_void_p, c_void_p]),
@@ -77,7 +77,8 @@ SIGNATURES = {
     "kano_host_times": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_mfma_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_group_create": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
-"kano_group_create_lean": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
+    "kano_group_create_lean": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
+    "kano_group_create_ex": (c_int, [c_int, c_void_p, c_int, POINTER(c_void_p)]),
     "kano_group_destroy": (None, [c_void_p]),
     "kano_group_last_error": (ctypes.c_char_p, [c_void_p]),
     "kano_group_info": (c_int, [c_void_p, c_void_p]),
@@ -90,6 +91,11 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kano_group_build": (c_int, [c_void_p, c_int]),
     "kano_group_set_groups": (c_int, [c_void_p, c_void_p, c_int32]),
+    "kano_group_add_policies": (c_int, [c_void_p, c_int64, c_int32, c_void_p] + [c_void_p] * 6 +
+                                [POINTER(c_int64)]),
+    "kano_group_remove_policies": (c_int, [c_void_p, c_int64, c_void_p]),
+    "kano_group_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "kano_group_exchange_timing": (c_int, [c_void_p, c_int, c_void_p, c_int]),
     "kano_host_alloc": (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
     "kano_host_free": (None, [c_void_p]),
 }
@@ -100,6 +106,7 @@ INFO = dict(N=0, W=1, P=2, U=3, NNZ_SEL=4, NNZ_ALW=5, HEAVY=6, ROW0=7, ROW1=8, M
             HEAVY_SEL=15, HEAVY_KERNEL=16)
 PATHS = {"auto": 0, "bitwise": 1, "mfma": 2}
 STORED_GROUPS = -1   # KANO_STORED_GROUPS
+GROUP_LEAN, GROUP_RCCL, GROUP_COPY = 1, 2, 4   # KANO_GROUP_* flags
 
 
 class KanoNativeError(RuntimeError):

@@ -15,7 +15,10 @@ from .model import *  # noqa: F401,F403  (the reference does the same, algorithm
 from .model import BitArray, Container, Policy, ReachabilityMatrix
 from ._bits import bool_to_words, set_bit_indices, words_to_bool
 from ._intern import group_ids
-from . import _kano_host   # csrc/kano_hostext.c
+try:
+    from . import _kano_host   # csrc/kano_hostext.c (host-side loops, no GPU work)
+except ImportError:            # (missing or built for another interpreter: the
+    _kano_host = None          # Python loops below do the same work)
 
 
 def _engine(matrix: ReachabilityMatrix, whole: bool = True):
@@ -104,6 +107,8 @@ def _pairs_to_list(pairs: np.ndarray, P: int = 0) -> List[Tuple[int, int]]:
     if pairs.shape[0] == 0:
         return []
     # (csrc/kano_hostext.c: the tuples built natively, policy ints shared)
+    if _kano_host is None:
+        return [tuple(p) for p in pairs.tolist()]
     return _kano_host.pairs_list(np.ascontiguousarray(pairs, dtype=np.int32), int(P))
 
 
@@ -116,15 +121,15 @@ def _fast_path(matrix, policies, containers) -> bool:
         return False
     if len(containers) != matrix._ncontainers:
         return False
-    if matrix._containers is not containers:
-        cs = matrix._containers
-        if any(a is not b for a, b in zip(cs, containers)):
-            return False
     lists = matrix._lists
-    if type(containers) is list and _kano_host.pending_is(containers, Container, lists):
+    order = lists._containers        # (the build's container order, snapshotted)
+    if (_kano_host is not None and type(containers) is list and type(order) is list and
+            _kano_host.pending_is(containers, Container, lists, order)):
         return True                  # (the loop below, natively, for exact Containers)
-    for c in containers:
-        if not isinstance(c, Container):
+    if len(order) != len(containers):
+        return False
+    for c, o in zip(containers, order):
+        if not isinstance(c, Container) or c is not o:
             return False
         if c._sel or len(c._pending) != 1 or c._pending[0] is not lists:
             return False
@@ -198,11 +203,14 @@ def policy_conflict(matrix: ReachabilityMatrix, policies: List[Policy],
 
 def _path_matrix(matrix: ReachabilityMatrix, hops: int, mode: str) -> ReachabilityMatrix:
     from ._engine import DeviceBuild
+    from .multi import MultiBuild
     src = _engine(matrix)
     n = matrix.container_size
     out = ReachabilityMatrix.__new__(ReachabilityMatrix)
     out.container_size = n
-    out._engine = DeviceBuild.empty(n, device=src.device)
+    # a row-sharded group's path matrix is sharded the same way
+    out._engine = (MultiBuild.empty(n, src.G, devices=src.devices)
+                   if isinstance(src, MultiBuild) else DeviceBuild.empty(n, device=src.device))
     out._containers = None
     out._policies = None
     out._ncontainers = n

@@ -527,11 +527,17 @@ class ReachabilityMatrix:
             if "x" in made:
                 raise made["x"]
             engine = made["e"]
-            engine.upload(tables)
-            engine.build()
+            try:
+                engine.upload(tables)
+                engine.build()
+            except BaseException:
+                engine.close()           # (the contexts and their device memory now)
+                raise
             for p, pol in enumerate(policies):
                 pol.store_bcp(_LazySet(engine, p, "sel"), _LazySet(engine, p, "allow"))
-            lists = _BuildLists(engine, containers)
+            # (the build's order, snapshotted: a caller reordering its list
+            # afterwards must not move the lists between containers)
+            lists = _BuildLists(engine, list(containers))
             for i, c in enumerate(containers):
                 if isinstance(c, Container):
                     c._pending.append(lists)

@@ -16,9 +16,21 @@ needs no communication; the whole-matrix checks run on the device:
   getrow / getcol / [i, j]       the owner / every member's part, in order
   (model.py:171-184)
 
+  add_policies /                 every member's rows (kano_group_add_policies /
+  remove_policies (§8(f) rank 4) kano_group_remove_policies)
+  two_hop / k_hop / closure      each member's part of the one-hop table,
+  (kubesv constraint.py:233-237) gathered, then each member's rows
+                                 (kano_group_path)
+
 Shard boundaries are multiples of 64 rows, so a column is the members' word
 arrays concatenated.  The engine offers the DeviceBuild methods the drop-in
-API calls; incremental updates and multi-hop products stay single-device.
+API calls.
+
+The exchange is RCCL (``ncclAllGather`` over communicators from
+``ncclCommInitAll``) whenever the devices are distinct; ``exchange="rccl"`` (or
+``KANO_GROUP_RCCL=1``) asks for it even for one member, ``exchange="copy"``
+(or ``KANO_GROUP_COPY=1``) for device copies.  A failing RCCL raises: the group
+never falls back to copies on its own.
 """
 from __future__ import annotations
 
@@ -52,6 +64,14 @@ def requested_gpus() -> int:
         return 1
 
 
+def requested_exchange() -> Optional[str]:
+    if os.environ.get("KANO_GROUP_RCCL", "") not in ("", "0"):
+        return "rccl"
+    if os.environ.get("KANO_GROUP_COPY", "") not in ("", "0"):
+        return "copy"
+    return None
+
+
 def requested_devices(G: int) -> Optional[List[int]]:
     spec = os.environ.get("KANO_DEVICES")
     if not spec:
@@ -66,7 +86,8 @@ class MultiBuild:
     """A kano_group: G row-shard contexts in one process (see module doc)."""
 
     def __init__(self, tables: Optional[Tables], ngpu: int, devices: Optional[List[int]] = None,
-                 path: str = "auto", build: bool = True, lean: bool = False):
+                 path: str = "auto", build: bool = True, lean: bool = False,
+                 exchange: Optional[str] = None):
         self.lib = nat.load()
         self.g = c_void_p()
         G = int(ngpu)
@@ -75,12 +96,21 @@ class MultiBuild:
             devs = np.ascontiguousarray(devices, dtype=np.int32)
         # lean: members without the CU-masked write stream (kano_create_lean;
         # the drop-in build_matrix)
-        create = self.lib.kano_group_create_lean if lean else self.lib.kano_group_create
-        rc = create(G, _ptr(devs), byref(self.g))
+        exchange = exchange if exchange is not None else requested_exchange()
+        if exchange not in (None, "rccl", "copy"):
+            raise ValueError(f"exchange must be 'rccl' or 'copy', not {exchange!r}")
+        flags = ((nat.GROUP_LEAN if lean else 0) | (nat.GROUP_RCCL if exchange == "rccl" else 0) |
+                 (nat.GROUP_COPY if exchange == "copy" else 0))
+        rc = self.lib.kano_group_create_ex(G, _ptr(devs), flags, byref(self.g))
         if rc != 0:
             self.g = c_void_p()
-            raise nat.KanoNativeError(f"kano_group_create({G}) failed (rc={rc})")
+            why = self.lib.kano_group_last_error(None)
+            raise nat.KanoNativeError(f"kano_group_create({G}) failed (rc={rc}): "
+                                      f"{why.decode(errors='replace') if why else ''}")
         self.G = G
+        self.devices = list(devices) if devices is not None else list(range(G))
+        self.lean = lean
+        self.exchange = exchange
         self.path = path
         self.tables = tables
         self.row_span = None
@@ -97,6 +127,7 @@ class MultiBuild:
             self.members.append(m)
         self.device = self.members[0].device
         self._idx = None
+        self._inc = False
         if tables is not None:   # (None: the caller uploads, then builds)
             self.upload(tables)
             if build:
@@ -355,15 +386,61 @@ class MultiBuild:
         a = self.members[0].policy_sets(p, False, True)[1] if allow else None
         return s, a
 
-    # -- single-device only -----------------------------------------------
-    def _single(self, what):
-        raise NotImplementedError(f"{what} runs on a single-device matrix (KANO_NGPU=1)")
+    # -- incremental updates -------------------------
+    def add_policies(self, xval: np.ndarray, sel_csr, alw_csr) -> int:
+        """kano_group_add_policies: every member's rows; returns the first
+        new engine id (equal on every member)."""
+        so, sc, sv = (np.ascontiguousarray(a, dtype=d) for a, d in
+                      zip(sel_csr, (np.int64, np.int32, np.int32)))
+        ao, ac, av = (np.ascontiguousarray(a, dtype=d) for a, d in
+                      zip(alw_csr, (np.int64, np.int32, np.int32)))
+        xv = np.ascontiguousarray(xval, dtype=np.int32)
+        first = c_int64(0)
+        self._chk(self.lib.kano_group_add_policies(
+            self.g, int(so.shape[0] - 1), int(xv.shape[0]), _ptr(xv), _ptr(so), _ptr(sc),
+            _ptr(sv), _ptr(ao), _ptr(ac), _ptr(av), byref(first)), "kano_group_add_policies")
+        self._inc = True
+        return int(first.value)
 
-    def add_policies(self, *a, **k):
-        self._single("add_policies")
+    def remove_policies(self, ids) -> None:
+        a = np.ascontiguousarray(np.asarray(ids, dtype=np.int64).reshape(-1))
+        self._chk(self.lib.kano_group_remove_policies(self.g, int(a.shape[0]), _ptr(a)),
+                  "kano_group_remove_policies")
+        self._inc = True
 
-    def remove_policies(self, *a, **k):
-        self._single("remove_policies")
+    def added_policy_sets(self, eid: int) -> Tuple[np.ndarray, np.ndarray]:
+        # (the added policies' sets cover every pod on every member)
+        return self.members[0].added_policy_sets(eid)
 
-    def path_from(self, *a, **k):
-        self._single("multi-hop reachability")
+    # -- multi-hop reachability (SURVEY.md §8(f) rank 3) ------------------------
+    @classmethod
+    def empty(cls, n: int, ngpu: int, devices: Optional[List[int]] = None) -> "MultiBuild":
+        """A group holding an n x n matrix in the same row shards and no
+        policies (the target of path_from)."""
+        z64 = np.zeros(1, np.int64)
+        e = np.zeros(0, np.int32)
+        t = Tables(int(n), 0, np.zeros((0, int(n)), np.int32), z64, e, e, z64, e, e)
+        return cls(t, ngpu, devices=devices, lean=True, exchange="copy")
+
+    def path_from(self, src: "MultiBuild", hops: int = 2, mode: str = "auto") -> dict:
+        """This group's rows := the multi-hop reachability of src's row-sharded
+        matrix (kano_group_path; kubesv/kubesv/constraint.py:233-237): one
+        exchange of the members' one-hop table parts over src's transport."""
+        if not isinstance(src, MultiBuild) or src.G != self.G or src.devices != self.devices:
+            raise ValueError("path_from needs a group over the same devices")
+        info = np.zeros(6, dtype=np.int64)
+        self._chk(self.lib.kano_group_path(src.g, self.g, int(hops), nat.PATHS[mode], _ptr(info)),
+                  "kano_group_path")
+        keys = ("steps", "steps_run", "mfma_steps", "row_classes", "col_classes", "identity")
+        return {k: int(v) for k, v in zip(keys, info)}
+
+    # -- measurement ------------------------------------------------------------
+    def exchange_timing(self, enable: Optional[bool] = None, reset: bool = False) -> dict:
+        """The verify exchange's time on member 0's stream (HIP events around
+        the all-gather or the copies; enable=True switches it on)."""
+        out = np.zeros(3, dtype=np.float64)
+        self._chk(self.lib.kano_group_exchange_timing(
+            self.g, -1 if enable is None else int(bool(enable)), _ptr(out), int(reset)),
+            "kano_group_exchange_timing")
+        return {"calls": int(out[0]), "total_ms": float(out[1]), "max_ms": float(out[2]),
+                "avg_ms": float(out[1] / out[0]) if out[0] else None}

@@ -292,17 +292,20 @@ def main():
         return
     names = [a for a in sys.argv[1:] if not a.startswith("--")]
     if big and names:
-        # BASELINE configs C2/C3/C4 written by make_clusters.py --big NAMES;
-        # C4's policy_shadow (~1e11 tuples) is left to the C oracle
+        # BASELINE configs C2/C3/C4 (and the dense-path cluster D1) written by
+        # make_clusters.py --big NAMES; C4's and D1's policy_shadow (~1e11 /
+        # ~5e11 tuples) are left to the oracles.  D1.json holds the indexed
+        # restatement's record, so kano_py's own goes to D1_kano_py.json.
         for name in names:
             obj = json.load(open(f"/tmp/kano_golden_{name}.json"))
             t = time.time()
             rec = run_cluster(name, obj, obj.get("label", "tenant"),
-                              shadow="--no-shadow" not in sys.argv and name != "C4",
+                              shadow="--no-shadow" not in sys.argv and name not in ("C4", "D1"),
                               verbose=True)
             print(f"{name}: {time.time() - t:.1f}s  timings={rec['reference_seconds']}",
                   flush=True)
-            with open(os.path.join(EXPECTED, name + ".json"), "w") as f:
+            out = name + ("_kano_py" if name == "D1" else "")
+            with open(os.path.join(EXPECTED, out + ".json"), "w") as f:
                 json.dump(rec, f, separators=(",", ":"))
         return
     os.makedirs(EXPECTED, exist_ok=True)

@@ -268,6 +268,110 @@ def test_verify_async_completion(tune, monkeypatch):
     pin.close()
 
 
+def test_verify_status_regions_after_a_smaller_call():
+    """k_verify_cols_f's look-back status regions (two, alternating) on one
+    context: a large call, a small call, then a DIFFERENT cluster at the
+    large size.  The third call reads the region the first call used; every
+    word of it must have been cleared (only the small call's
+    prefix was, and stale look-back prefixes of the first cluster survived)."""
+    from kano._engine import DeviceBuild
+    from kano._intern import group_ids, intern, tables_from_cluster
+    from kano.synth import make_cluster, make_config, KEY_NAMES
+    from oracle import kano_oracle as orc
+    cl = make_config("C2")
+    _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
+    eng = DeviceBuild(tables_from_cluster(cl), build=False)
+    r = eng.verify(gid, sys_row=0, shadow=False)
+    assert r["all_isolated"].tolist() == expected("C2")["all_isolated"]
+    small = cluster("s_sparse_500")
+    cs, ps = api_objects(small)
+    eng.upload(intern(cs, ps))
+    r = eng.verify(group_ids(cs, small["label"]), sys_row=0, shadow=False)
+    assert r["user_crosscheck"].tolist() == expected("s_sparse_500")["user_crosscheck"]["result"]
+    other = make_cluster(10_000, 1_000, "sparse", seed=123).to_json_obj()
+    ref = orc.run_c(other, label="tenant")
+    cs, ps = api_objects(other)
+    eng.upload(intern(cs, ps))
+    for _ in range(2):
+        r = eng.verify(group_ids(cs, "tenant"), sys_row=0, shadow=True)
+        assert r["all_reachable"].tolist() == ref["all_reachable"]
+        assert r["all_isolated"].tolist() == ref["all_isolated"]
+        assert r["user_crosscheck"].tolist() == ref["user_crosscheck"]
+        assert r["system_isolation"].tolist() == ref["system_isolation"]
+        assert np.array_equal(np.ascontiguousarray(r["pairs"]).reshape(-1, 2),
+                              ref["shadow"].reshape(-1, 2))
+    eng.close()
+
+
+def test_build_matrix_closes_engine_when_build_raises(monkeypatch):
+    """ReachabilityMatrix.build_matrix whose upload or build raises destroys
+    the context it made (no device memory left until GC)."""
+    import gc
+    from kano import _native as nat
+    from kano._engine import DeviceBuild
+    from kano.model import ReachabilityMatrix
+    lib = nat.load()
+    made, destroyed = [], []
+    real_create, real_destroy = lib.kano_create_lean, lib.kano_destroy
+
+    def create(dev, out):
+        made.append(dev)
+        return real_create(dev, out)
+
+    def destroy(c):
+        destroyed.append(c)
+        return real_destroy(c)
+    monkeypatch.setattr(lib, "kano_create_lean", create)
+    monkeypatch.setattr(lib, "kano_destroy", destroy)
+    cs, ps = api_objects(cluster("s_sparse_200"))
+    for what in ("upload", "build"):
+        def boom(self, *a, **k):
+            raise nat.KanoNativeError(f"injected {what} failure")
+        monkeypatch.setattr(DeviceBuild, what, boom)
+        gc.disable()
+        try:
+            ReachabilityMatrix.build_matrix(cs, ps)
+            raise AssertionError("build_matrix did not raise")
+        except nat.KanoNativeError as e:
+            assert "injected" in str(e)
+            # (checked while the traceback, and every frame's engine, lives)
+            assert len(destroyed) == len(made), (what, made, destroyed)
+        finally:
+            gc.enable()
+        monkeypatch.undo()
+        monkeypatch.setattr(lib, "kano_create_lean", create)
+        monkeypatch.setattr(lib, "kano_destroy", destroy)
+    assert len(made) == 2
+
+
+def test_lists_follow_the_build_order_after_reordering():
+    """The containers' lists belong to the build's order even when the caller
+    reorders, pops or inserts into its list after build_matrix (ADVICE r4:
+    the lists were mapped through the live list on first use); policy_shadow
+    then iterates the containers in their new order (algorithm.py:58-80)."""
+    from kano import algorithm as alg
+    from kano.model import ReachabilityMatrix
+    obj = cluster("s_sparse_200")
+    exp = expected("s_sparse_200")
+    cs, ps = api_objects(obj)
+    build_order = list(cs)
+    m = ReachabilityMatrix.build_matrix(cs, ps)
+    cs.reverse()
+    cs.pop(0)
+    cs.insert(3, cs[10])
+    sel = exp["select_policies"]
+    pos = {id(c): i for i, c in enumerate(build_order)}
+    for c in cs:
+        assert c.select_policies == sel[pos[id(c)]]
+        assert c.allow_policies == exp["allow_policies"][pos[id(c)]]
+    # policy_shadow over the reordered list: kano_py's loop on these lists
+    allow = [{i for i, ch in enumerate(a) if ch == "1"} for a in exp["allow"]]
+    want = [(j, k) for c in cs for j in c.select_policies for k in c.select_policies
+            if j != k and allow[k] <= allow[j]]
+    assert alg.policy_shadow(m, ps, cs) == want
+    m.engine.close()
+
+
 def test_verify_declared_groups_checked():
     """A group id outside the declared [0, ngroups) is an error, not a fault
     (the check in k_cls_group_range_m)."""
