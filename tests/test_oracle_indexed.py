@@ -41,6 +41,17 @@ def test_policy_shadow(pinned):
         assert digest == sh["sha256"]
 
 
+def test_policy_shadow_count_branch(pinned):
+    """The count-only branch (the one D1's record uses: group counts, no
+    pairs) against kano_py's own pair count where kano_py holds the list."""
+    name, cl, ix, exp = pinned
+    sh = exp["policy_shadow"]
+    if "count" not in sh:
+        pytest.skip("C4: kano_py's list does not fit; test_policy_shadow pins it")
+    cnt, digest = K.policy_shadow(ix, want_sha=False)
+    assert digest is None and cnt == sh["count"]
+
+
 def test_sets_and_lists(pinned):
     name, cl, ix, exp = pinned
     if name != "C2":
