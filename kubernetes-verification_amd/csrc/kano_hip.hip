@@ -161,27 +161,19 @@ struct kano_ctx {
   double xo_mfma = 1800e12, xo_or = 8500e9;
   i64 heavy_gemm_min = HEAVY_GEMM_MIN_TILES;   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
-  int heavy_expand_lds = 1;  // hexplds=0: the heavy rows' expansion from global memory
+  int heavy_expand_lds = 1;  // hexplds=0: forces the heavy rows' expansion from global
+                             // memory (the form Mc rows wider than 32 KB of LDS take)
   int dx_on = 1;             // dx=0: never the class-indexed LDS counters (k_*_dx); 2: always
   bool dense_sel = false;    // this build takes them (do_front)
   int ac_lds = 1;            // aclds=0: AC / ACT bits by global atomics, not LDS rows
-  int sel_early = 1;         // selearly=0: k_sel_place only after build sync 2
-  int rows_early = 1;        // rowsearly=0: kano_verify's write waits for the tail's copy
   bool rin_marked = false;   // this build's last Mc launch marked ev_rin_e
   i64 sel_early_cap = -1;    // the early placement's list capacity (-1: none this build)
-  i64 shadow_grid = 0;       // shgrid=K: k_shadow_test1s on at most K blocks (striding)
-  int scan_items = SCAN_ITEMS;   // scanitems: k_scan_lb's elements per thread (4/8/16/32)
-  int gemm_lds = 1;          // hglds=0: k_heavy_gemm (operands from global memory, one
-                             // K-step of register prefetch) instead of k_heavy_gemm_lds
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table
   int rows_ch = ROWS_CH;     // rch=: member rows per k_rows work item
   int rows_cww = MAX_CWW_KNOB;   // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
-  int stream_prio = 1;       // prio=0: every stream at normal priority
-  int dx_ppb = 0;            // dxppb=: policies per block of the dx kernels (0: ~256 blocks)
-  int shg_sub_lds = 1;       // shgsub=0: k_shg_sub's word-by-word row compare
-  int side_prio = 1;         // sideprio=0: stream2 (the build's side work) at normal priority
-  int engine_mask = 0;       // emask=1: engine streams on the CUs the write stream leaves
+  int shg_sub_lds = 1;       // shgsub=0: forces k_shg_sub's word-by-word row compare (the
+                             // form rows wider than 64 KB of LDS take)
   // The matrix write shares the device with the next kano_verify's build
   // (asynchronous completion): a write that saturates HBM starves the
   // build's latency-bound kernels (fill 6 -> 62-107 us, class insert 25 ->
@@ -218,9 +210,7 @@ struct kano_ctx {
   int scan_parity2 = 0;
   // The build's size-independent side work on stream2 beside the join chain:
   // AC / Mc zero fills and the crosscheck's group-key sort, forked after the
-  // classes (ev_pre) and joined before the lists (ev_pre_done).  sidepre=0
-  // keeps them on the engine stream.
-  int side_pre = 1;
+  // classes (ev_pre) and joined before the lists (ev_pre_done).
   // (ev_pre_ac: AC zeroed, joined before the lists; ev_pre_done: the rest,
   // joined before the Mc writers -- each join well after its work ends, so
   // the engine stream's barrier finds it complete)
@@ -229,8 +219,6 @@ struct kano_ctx {
   // policy_shadow's offset scans and compaction on stream2 right after its
   // tests (pairs mode), beside the crosscheck pass and the column checks;
   // the emission stays on the engine stream behind the index lists
-  // (sidetail=0: scans and compaction on the engine stream too)
-  int side_tail = 1;
   bool tail_compacted = false;
   hipEvent_t ev_pairs = nullptr;   // the compaction done (stream2)
   DBuf gid, gids, cgroup, R, multi, A1, A2, own, cross, gmin, gmax, ckey, corder, kcnt, koff;
@@ -547,10 +535,10 @@ struct ScanBatch {
   // mark: an event this launch's dispatch marks (none when no job is queued)
   int run(hipEvent_t mark = nullptr) {
     if (jobs.count == 0) return 0;
-    // the tile length, 256 x 8 elements (knob scanitems: 4 / 16 / 32; longer
-    // tiles -- fewer look-back hops -- measured slower on C3's <= 100k-entry
-    // scans: 32 per thread 0.432 ms a step against 0.377 at 8, 16 0.380)
-    const int items = ctx->scan_items;
+    // the tile length, 256 x 8 elements (round 4: longer tiles -- fewer
+    // look-back hops -- measured slower on C3's <= 100k-entry scans: 32 per
+    // thread 0.432 ms a step against 0.377 at 8, 16 0.380)
+    const int items = SCAN_ITEMS;
     i64 slots = 0, maxt = 1;
     for (int q = 0; q < jobs.count; ++q) {
       jobs.j[q].st = slots;
@@ -1118,7 +1106,8 @@ int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
 // policies per block of the class-indexed LDS forms: ~256 blocks (each
 // block flushes its whole table: fewer, fuller blocks)
 int dx_ppb(const kano_ctx* ctx, i64 P) {
-  return ctx->dx_ppb > 0 ? ctx->dx_ppb : (int)std::max<i64>(16, (P + 255) / 256);
+  (void)ctx;
+  return (int)std::max<i64>(16, (P + 255) / 256);
 }
 
 int sel_spb(const kano_ctx* ctx) {
@@ -1152,7 +1141,7 @@ int do_front(kano_ctx* ctx, int path) {
   // the side work of do_back_pre needs the classes only: it forks after the
   // member lists (their fill's dispatch marks ev_pre)
   ctx->pre_forked = false;
-  const bool fork_pre = ctx->side_pre && ctx->stream2;
+  const bool fork_pre = ctx->stream2 != nullptr;
   bool pre_marked = false;
   KTRY(classify_phase2a(ctx, fork_pre ? ctx->ev_pre : nullptr, &pre_marked));
   if (fork_pre) {
@@ -1418,7 +1407,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   ctx->heavy_kernel = H == 0 ? 0 : !mfma ? 1 : gemm ? 3 : 2;
   // the staged GEMM's padded operands (k_heavy_gemm_lds): A [PBp][ldA],
   // ACT [PBp][ldB]; the unstaged kernels use ldA = H, ldB = Ua, PBp = PB
-  const bool glds = gemm && ctx->gemm_lds;
+  const bool glds = gemm;
   const i64 ldA = glds ? (H + 64 * tmg - 1) / (64 * tmg) * (64 * tmg) : H;
   const i64 ldB = glds ? (ctx->cc.U + 64 * tng - 1) / (64 * tng) * (64 * tng) : ctx->cc.U;
   const i64 PBp = glds ? (ctx->PB + GK_KC - 1) / GK_KC * GK_KC : ctx->PB;
@@ -1540,7 +1529,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // below is the last producer of every k_rows input: its dispatch marks
   // ev_rin_e, where kano_verify's write may start -- beside this call's tail
   // instead of behind it)
-  hipEvent_t rin_mark = ctx->rows_early && H == 0 && ctx->cols_deferred ? ctx->ev_rin_e : nullptr;
+  hipEvent_t rin_mark = H == 0 && ctx->cols_deferred ? ctx->ev_rin_e : nullptr;
   if (scatter_on && (size_t)ldMc * 8 * (TPB / 64) <= 64 * 1024) {
     // light Mc rows by their owner (a wave per row class, the row in LDS,
     // plain stores)
@@ -1613,7 +1602,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         KLAUNCH();
         KTRY(resolve_mfma_time(ctx));
         KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
-        if (glds) {
+        {
           const size_t lds = sizeof(u64) * 2 * GK_KC * (size_t)(64 * tmg + 64 * tng);
           if (hg == 22)
             hipLaunchKernelGGL((k_heavy_gemm_lds<2, 2>), grid, dim3(TPB), lds, ctx->stream, A,
@@ -1624,15 +1613,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
           else
             hipLaunchKernelGGL((k_heavy_gemm_lds<4, 2>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
-        } else if (hg == 22)
-          hipLaunchKernelGGL((k_heavy_gemm<2, 2>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
-                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
-        else if (hg == 44)
-          hipLaunchKernelGGL((k_heavy_gemm<4, 4>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
-                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
-        else
-          hipLaunchKernelGGL((k_heavy_gemm<4, 2>), grid, dim3(TPB), 0, ctx->stream, A, hl, H,
-                             P_<u64>(ctx->ACT), Ua, ctx->PB, out, ldMc);
+        }
         KLAUNCH();
         KCHK(hipEventRecord(ctx->ev_m1, ctx->stream));
         ctx->mfma_time_pending = true;
@@ -2211,13 +2192,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathtm" && (v == 1 || v == 2 || v == 4)) ctx->path_tm = v;
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
-        if (k == "prio") ctx->stream_prio = v;
-        if (k == "emask") ctx->engine_mask = v;
-        if (k == "sideprio") ctx->side_prio = v;
         if (k == "shgsub") ctx->shg_sub_lds = v;
-        if (k == "dxppb" && v >= 0 && v <= 4096) ctx->dx_ppb = v;
-        if (k == "sidepre") ctx->side_pre = v;
-        if (k == "sidetail") ctx->side_tail = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
         if (k == "hgemm" && (v == -1 || v == 0 || v == 22 || v == 42 || v == 44))
@@ -2225,13 +2200,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
         if (k == "hortime") ctx->time_or = v;
         if (k == "hexplds") ctx->heavy_expand_lds = v;
-        if (k == "hglds") ctx->gemm_lds = v;
-        if (k == "shgrid" && v >= 0) ctx->shadow_grid = v;
-        if (k == "selearly") ctx->sel_early = v;
-        if (k == "rowsearly") ctx->rows_early = v;
         if (k == "dx") ctx->dx_on = v;
         if (k == "aclds") ctx->ac_lds = v;
-        if (k == "scanitems" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->scan_items = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
       }
@@ -2243,16 +2213,12 @@ int kano_create(int device, kano_ctx** out) {
   // write (stream3, normal priority) frees
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  const int prio_main = ctx->stream_prio ? prio_hi : prio_lo;
-  uint32_t emask[8];
-  const bool em = ctx->engine_mask && !g_create_lean && ctx->rows_cu_off > 0;
-  if (em) {
-    rows_cu_mask(ctx->rows_cu_off, emask);
-    for (auto& w : emask) w = ~w;
-  }
-  if ((em ? hipExtStreamCreateWithCUMask(&ctx->stream, 8, emask)
-          : hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_main)) !=
-      hipSuccess) {
+  (void)prio_lo;
+  // (round 4: the engine streams confined to the CUs the write leaves, and
+  // stream2 at normal priority, measured neutral at C3 and slower where the
+  // engine kernels are heavy: D1, C5 row shards)
+  const int prio_main = prio_hi;
+  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_main) != hipSuccess) {
     delete ctx;
     return -EIO;
   }
@@ -2291,10 +2257,7 @@ int kano_create(int device, kano_ctx** out) {
   // builds the caller waits for, has none)
   if (!g_create_lean) KTRY(ensure_masked_stream(ctx));
   mark("write_streams");
-  if ((em ? hipExtStreamCreateWithCUMask(&ctx->stream2, 8, emask)
-          : hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking,
-                                        ctx->side_prio ? prio_main : prio_lo)) !=
-          hipSuccess ||
+  if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_main) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_sizes, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
@@ -2706,7 +2669,7 @@ using ExtraFills = std::function<int(FillBatch&)>;
 int sel_place_early(kano_ctx* ctx) {
   ctx->sel_early_cap = -1;
   const i64 U = ctx->rc.U, P = ctx->P;
-  if (!ctx->sel_early || U == 0 || P == 0 || !ctx->slist.p || !ctx->ecls.p) return 0;
+  if (U == 0 || P == 0 || !ctx->slist.p || !ctx->ecls.p) return 0;
   const i64 cap = (i64)(std::min(ctx->slist.bytes, ctx->ecls.bytes) / sizeof(int32_t));
   if (ctx->dense_sel) {
     KTRY(sel_place_dx(ctx, cap));
@@ -3167,7 +3130,6 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     // may yield to the grouped count)
     const i64 nvb = sp.nt * SH_ITEMS;
     i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
-    if (ctx->shadow_grid > 0) grid = std::min<i64>(grid, ctx->shadow_grid);
     // the block's S(c) entries staged in LDS, one candidate pair per thread
     hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
                        ctx->vs_count_only ? (i64*)nullptr : P_<i64>(ctx->tcnt));
@@ -3436,7 +3398,7 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
   ctx->fork_pending = false;
   ctx->tail_compacted = false;
   bool fork_marked = false;
-  const bool side_sh = want_shadow && !count_only && ctx->side_tail;
+  const bool side_sh = want_shadow && !count_only;
   if (want_shadow) {
     ctx->fork_hook = [&](bool marked) -> int {
       if (!marked) KCHK(hipEventRecord(ctx->ev_fork2, ctx->stream));

@@ -1788,97 +1788,12 @@ __global__ __launch_bounds__(TPB) void k_heavy_selT(const int32_t* __restrict__ 
 // expansion, VALU, is what bounds a narrow tile); block = 2 x 2 waves; K = all
 // policies, 64 per step, no split (the grid has >= HEAVY_GEMM_MIN_TILES wave
 // tiles).  A is the heavy rows' select bits [pb][h] (k_heavy_selT), B is
-// ACT[pb][ca]; both coalesced.  Every (row, 32-column word) belongs to one wave: plain stores
+// ACT[pb][ca].  Every (row, 32-column word) belongs to one wave: plain stores
 // of the thresholded ballots into the zeroed Mc.  Blocks of one XCD (blockIdx
 // mod 8) walk a contiguous range of the tile order (GM block-rows at a time)
 // so that they share A and B panels in their L2.
-constexpr i64 HEAVY_GEMM_MIN_TILES = 512;
-template <int TM, int TN>
-__global__ __launch_bounds__(TPB) void k_heavy_gemm(const u64* __restrict__ A,
-                                                    const int32_t* __restrict__ hlist, i64 H,
-                                                    const u64* __restrict__ ACT, i64 Ua, i64 PB,
-                                                    uint32_t* __restrict__ Mc32, i64 ldMc) {
-  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
-  constexpr i64 GM = 8;
-  const i64 nbm = (H + 64 * TM - 1) / (64 * TM), nbn = (Ua + 64 * TN - 1) / (64 * TN);
-  const i64 total = nbm * nbn, per = (total + 7) / 8;
-  const i64 L = (i64)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (L >= total) return;                             // block-uniform
-  const i64 grp = L / (GM * nbn), first = grp * GM;
-  const i64 gm = nbm - first < GM ? nbm - first : GM;
-  const i64 in = L - grp * GM * nbn;
-  const i64 bm = first + in % gm, bn = in / gm;
-  const int wv = threadIdx.x >> 6;
-  const i64 rb = (bm * 2 + (wv >> 1)) * 32 * TM, cb = (bn * 2 + (wv & 1)) * 32 * TN;
-  if (rb >= H || cb >= Ua) return;                    // wave-uniform; no block barrier
-  i64 rowv[TM];
-#pragma unroll
-  for (int t = 0; t < TM; ++t) rowv[t] = rb + 32 * t + l32;
-  i64 colv[TN];
-#pragma unroll
-  for (int u = 0; u < TN; ++u) colv[u] = cb + 32 * u + l32;
-  i32x16 acc[TM][TN];
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0;
-  // the next K step's words are loaded while this one's MFMAs run
-  u64 an[TM], bn_[TN];
-#pragma unroll
-  for (int t = 0; t < TM; ++t) an[t] = rowv[t] < H ? A[rowv[t]] : 0ull;
-#pragma unroll
-  for (int u = 0; u < TN; ++u) bn_[u] = colv[u] < Ua ? ACT[colv[u]] : 0ull;
-  for (i64 kw = 0; kw < PB; ++kw) {
-    u64 aw[TM], bw[TN];
-#pragma unroll
-    for (int t = 0; t < TM; ++t) aw[t] = an[t];
-#pragma unroll
-    for (int u = 0; u < TN; ++u) bw[u] = bn_[u];
-    if (kw + 1 < PB) {
-#pragma unroll
-      for (int t = 0; t < TM; ++t) an[t] = rowv[t] < H ? A[(kw + 1) * H + rowv[t]] : 0ull;
-#pragma unroll
-      for (int u = 0; u < TN; ++u) bn_[u] = colv[u] < Ua ? ACT[(kw + 1) * Ua + colv[u]] : 0ull;
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int sh = ks * 32 + half * 16;
-      i32x4 af[TM], bf[TN];
-#pragma unroll
-      for (int t = 0; t < TM; ++t) af[t] = expand16((uint32_t)(aw[t] >> sh) & 0xffffu);
-#pragma unroll
-      for (int u = 0; u < TN; ++u) bf[u] = expand16((uint32_t)(bw[u] >> sh) & 0xffffu);
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int u = 0; u < TN; ++u)
-          acc[t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[t], bf[u], acc[t][u], 0, 0, 0);
-    }
-  }
-  // accumulator g of lane (l32, half): row (g&3) + 8 (g>>2) + 4 half, column
-  // l32 of its 32 x 32 tile; one ballot per g holds 32 columns of two rows
-  const i64 ld32 = 2 * ldMc;
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const i64 row = rb + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
-      const int32_t hr = row < H ? hlist[row] : -1;
-#pragma unroll
-      for (int u = 0; u < TN; ++u) {
-        const u64 bal = __ballot(acc[t][u][g] > 0);
-        const i64 c32 = (cb + 32 * u) >> 5;
-        if (l32 == 0 && hr >= 0 && c32 < ld32)
-          Mc32[(i64)hr * ld32 + c32] = half ? (uint32_t)(bal >> 32) : (uint32_t)bal;
-      }
-    }
-}
-
-// The GEMM with its operands staged through LDS: k_heavy_gemm's tiles, but a
-// block's A and B panels for GK_KC K-steps at a time (GK_KC x (64 TM + 64 TN)
-// words) are copied global -> LDS by the async 16-byte LDS-DMA loads
+// A block's A and B panels for GK_KC K-steps at a time (GK_KC x (64 TM + 64
+// TN) words) are copied global -> LDS by the async 16-byte LDS-DMA loads
 // (global_load_lds_dwordx4, no register staging), double-buffered: chunk c+1
 // is in flight while chunk c's 32 TM TN MFMAs per step run, so the loads'
 // latency (the operands sit in the MALL, ~1-2 us away) hides behind
@@ -1886,6 +1801,11 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm(const u64* __restrict__ A,
 // padded (zero) to whole block tiles and K chunks (ldA = H rounded up to
 // 64 TM, ldB = Ua rounded up to 64 TN, PB rounded up to GK_KC), so no load
 // leaves its array.  LDS: 2 x GK_KC x (64 TM + 64 TN) x 8 B (128 KB at 4 x 4).
+// (Round 5, scripts/micro/gemm_bits.hip: with the expansion removed this loop
+// reaches 0.51-0.53 of the int8 peak and the MFMAs alone 0.76-0.87; sharing
+// the expansion through LDS or streaming the words into a register ring
+// with the expansion interleaved measured slower, 0.33 / 0.42.)
+constexpr i64 HEAVY_GEMM_MIN_TILES = 512;
 constexpr int GK_KC = 16;
 template <int TM, int TN>
 __global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ A, i64 ldA,
@@ -2213,6 +2133,30 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   const int32_t m0 = m_begin + (int32_t)(chunk * a.ch);
   const int32_t m1 = min(m_end, m0 + a.ch);
   const bool heavy = a.hflag && a.hflag[c];
+  // a class no policy selects (C3: 9,143 of 21,535 row classes): its rows are
+  // zero -- stored straight from registers, no row build, no barrier
+  if (!heavy && a.soffc[c + 1] == a.soffc[c]) {
+    const u64x2 z = {0ull, 0ull};
+    for (int32_t m = m0; m < m1; ++m) {
+      const int32_t pod = __builtin_amdgcn_readfirstlane(a.mem[m]);
+      u64* dst = a.M + (i64)(pod - a.r0) * ldw + base;
+      if (a.plain) {
+        for (int w = threadIdx.x * 2; w < nw; w += NT * 2) *(u64x2*)&dst[w] = z;
+      } else {
+        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+          __builtin_nontemporal_store(z, (u64x2*)&dst[w]);
+      }
+    }
+    if (chunk == 0 && a.color) {
+      for (int w = threadIdx.x; w < nw; w += NT) {
+        const i64 gw = base + w;
+        if (gw >= a.W) break;
+        const u64 vm = valid_mask(gw, a.n);
+        if (vm & ~a.colnand[gw]) atomicOr(&a.colnand[gw], vm);
+      }
+    }
+    return;
+  }
 
   if (heavy) {
     const u64* src = a.M + (i64)(a.mem[m_begin] - a.r0) * ldw + base;

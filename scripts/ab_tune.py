@@ -2,7 +2,8 @@
 
     python scripts/ab_tune.py --config C3 --steps 300 --reps 2 -- "" "store=2" ...
 
-Each setting runs as its own bench.py process (timeout-bounded), in turn,
+A setting is "TUNE" or "LIB|TUNE" (LIB: a libkano_hip.so to load through
+KANO_HIP_LIB, e.g. a baseline build, paths relative to the repo).  Each setting runs as its own bench.py process (timeout-bounded), in turn,
 `reps` times; prints one summary line per run and writes the JSON lines to
 gpurun_out/ab_<config>.jsonl."""
 import argparse
@@ -28,7 +29,10 @@ def main():
     out = open(os.path.join(ROOT, "gpurun_out", f"ab_{a.config}.jsonl"), "a")
     for rep in range(a.reps):
         for t in a.tunes or [""]:
-            env = dict(os.environ, KANO_TUNE=t)
+            lib, _, tune = t.rpartition("|")
+            env = dict(os.environ, KANO_TUNE=tune)
+            if lib:
+                env["KANO_HIP_LIB"] = os.path.join(ROOT, lib)
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", a.config,
                    "--steps", str(a.steps), "--warmup", str(a.warmup), "--cpu-baseline", "0",
                    "--cold", "0"] + a.extra.split()

@@ -312,8 +312,8 @@ def _lists(cs, which):
 
 # --- matrix-write forms ------------------------------------------------------
 @pytest.mark.parametrize("tune", ["", "store=0", "cww=64", "cww=16", "async=0", "podword=0",
-                                  "hexplds=0", "dx=2", "aclds=0", "selearly=0", "rch=3",
-                                  "rch=64,cww=16384", "rowsearly=0"])
+                                  "hexplds=0", "dx=2", "aclds=0", "rch=3",
+                                  "rch=64,cww=16384"])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
     """The matrix write (k_rows) with non-temporal and plain stores, in the
