@@ -172,6 +172,7 @@ struct kano_ctx {
   int rows_ch = ROWS_CH;     // rch=: member rows per k_rows work item
   int rows_cww = MAX_CWW_KNOB;   // cww: k_rows column chunk (words); the chunking wide matrices
                              // (n > 524k) take, forced at small n
+  int shadow_r = 0;          // shr=1/2/4/8: k_shadow_test1s's 256-pair rounds per block (0: auto)
   int shg_sub_lds = 1;       // shgsub=0: forces k_shg_sub's word-by-word row compare (the
                              // form rows wider than 64 KB of LDS take)
   // The matrix write shares the device with the next kano_verify's build
@@ -2193,6 +2194,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "pathlds") ctx->path_lds = v;
         if (k == "pathtn" && (v == 2 || v == 4)) ctx->path_tn = v;
         if (k == "shgsub") ctx->shg_sub_lds = v;
+        if (k == "shr" && (v == 1 || v == 2 || v == 4 || v == 8)) ctx->shadow_r = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
         if (k == "hgemm" && (v == -1 || v == 0 || v == 22 || v == 42 || v == 44))
@@ -2214,6 +2216,7 @@ int kano_create(int device, kano_ctx** out) {
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   (void)prio_lo;
+
   // (round 4: the engine streams confined to the CUs the write leaves, and
   // stream2 at normal priority, measured neutral at C3 and slower where the
   // engine kernels are heavy: D1, C5 row shards)
@@ -3126,13 +3129,24 @@ int shadow_test_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
     a.ldC = ctx->ldC;
     a.flags = ctx->vs_count_only ? nullptr : P_<uint8_t>(ctx->flags);   // count only: T[c]
     a.T = P_<i64>(ctx->T);
-    // (one block per virtual block, or a capped striding grid when the test
-    // may yield to the grouped count)
-    const i64 nvb = sp.nt * SH_ITEMS;
+    // (one block per virtual block of R x 256 pairs, or a capped striding
+    // grid when the test may yield to the grouped count); R = 8 once the
+    // candidate pairs run to ~10^7 (C5 row shards: 7e7 pairs, the test 2.39
+    // -> 1.65 ms at R = 4, the step 7.76 -> 6.91 ms; R = 8 6.77), 1 below
+    // (C3: ~10^6, on the side stream)
+    const int R = ctx->shadow_r > 0 ? ctx->shadow_r : (sp.nf >= (i64)1 << 24 ? 8 : 1);
+    const i64 nvb = (sp.nf + (i64)TPB * R - 1) / ((i64)TPB * R);
     i64 grid = a.shg_G ? std::min<i64>(nvb, SH_YIELD_GRID) : nvb;
-    // the block's S(c) entries staged in LDS, one candidate pair per thread
-    hipLaunchKernelGGL(k_shadow_test1s<1024>, dim3((unsigned)grid), dim3(TPB), 0, st, a, sp.nf,
-                       ctx->vs_count_only ? (i64*)nullptr : P_<i64>(ctx->tcnt));
+    i64* tc = ctx->vs_count_only ? (i64*)nullptr : P_<i64>(ctx->tcnt);
+    // (direct launches, no kernel-pointer variable: tests/test_launch_ir.py)
+#define KANO_SHT(RR)                                                                        \
+  hipLaunchKernelGGL((k_shadow_test1s<1024, RR>), dim3((unsigned)grid), dim3(TPB), 0, st, a, \
+                     sp.nf, tc)
+    if (R == 8) KANO_SHT(8);
+    else if (R == 4) KANO_SHT(4);
+    else if (R == 2) KANO_SHT(2);
+    else KANO_SHT(1);
+#undef KANO_SHT
     KLAUNCH();
   }
   return 0;

@@ -1165,6 +1165,7 @@ struct PolAllowArgs {
   u64* AC;
   i64 ldC;
 };
+
 // (lds_row: the wave builds AC[p] in its LDS row of ldC words and stores it
 // whole -- long allow lists put thousands of same-word global atomics on
 // one row; the row needs ldC * 8 * WPB bytes of the launch's dynamic LDS)
@@ -2486,7 +2487,13 @@ constexpr int SHS_CLS = TPB + 2;
 // SEG: staged S(c) entries per block (1024: ~25 KB of LDS; 512, ten blocks
 // per CU, measured slightly slower beside the main stream's kernels)
 constexpr int SHS_U = 8;
-template <int SHS_SEG>
+// R: 256-pair rounds per block on one staging (the class range and the S(c)
+// segment of all R x 256 pairs): with ~7e7 candidate pairs (C5 row shards)
+// the per-block staging chain -- two wave searches, then the classes, then
+// the segment, each a dependent global round trip -- was the kernel's time
+// (C5 rank 0 of 8: 2.39 -> 1.65 ms at R = 4, a little less at 8).  A per-policy 64-bit allow-set
+// signature tested before AC (round 5) measured slower there too (1.78 ms).
+template <int SHS_SEG, int R>
 __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
                                                       i64* __restrict__ tile_cnt) {
   __shared__ i64 sm[4];
@@ -2498,16 +2505,17 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
   __shared__ int32_t s_pol[SHS_SEG];
   __shared__ int32_t s_nca[SHS_SEG];
   __shared__ int32_t s_x0[SHS_SEG];
+  static_assert(SH_TILE % (TPB * R) == 0, "a block's pairs stay inside one tile");
   if (a.shg_G && shg_grouped(a.shg_G, a.shg_err, a.shg_nf, a.shg_force)) return;
-  const i64 nvb = (nflags + SH_TILE - 1) / SH_TILE * SH_ITEMS;
+  constexpr i64 PB = (i64)TPB * R;               // pairs per virtual block
+  const i64 nvb = (nflags + PB - 1) / PB;
   for (i64 vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-    const i64 tile = vb / SH_ITEMS, part = vb % SH_ITEMS;
-    const i64 b0 = tile * SH_TILE + part * TPB;
-    if (b0 >= nflags) break;                     // block-uniform (b0 rises with vb)
-    const i64 b1 = min(b0 + (i64)TPB, nflags) - 1;
+    const i64 B0 = vb * PB;
+    if (B0 >= nflags) break;                     // block-uniform (B0 rises with vb)
+    const i64 B1 = min(B0 + PB, nflags) - 1;
     if ((threadIdx.x >> 6) < 2) {
       const int wv = threadIdx.x >> 6;
-      const i64 cr = wave_class_of(a.pfoff, 0, a.U - 1, wv == 0 ? b0 : b1);
+      const i64 cr = wave_class_of(a.pfoff, 0, a.U - 1, wv == 0 ? B0 : B1);
       if ((threadIdx.x & 63) == 0) rng[wv] = cr;
     }
     __syncthreads();
@@ -2538,76 +2546,81 @@ __global__ __launch_bounds__(TPB) void k_shadow_test1s(ShadowArgs a, i64 nflags,
       }
       __syncthreads();
     }
-    const i64 t = b0 + threadIdx.x;
-    int f = 0;
-    i64 c = -1;
-    if (t < nflags) {
-      if (staged) {
-        i64 lo = 0, hi = ncls - 1;               // last class with pfoff <= t
-        while (lo < hi) {
-          const i64 mid = (lo + hi + 1) >> 1;
-          if (s_pf[mid] <= t) lo = mid; else hi = mid - 1;
-        }
-        c = c0 + lo;
-        const i64 e0 = s_so[lo] - seg0, s = s_so[lo + 1] - s_so[lo], q = t - s_pf[lo];
-        const i64 x = q / s, y = q - x * s;
-        if (s_mc[lo] > 0 && x != y) {
-          const int32_t j = s_pol[e0 + x], kk = s_pol[e0 + y];
-          const int32_t ck = s_nca[e0 + y];
-          if (j != kk) {
-            if (ck == 0) {
-              f = 1;
-            } else if (ck <= s_nca[e0 + x]) {
-              const u64* aj = a.AC + (i64)j * a.ldC;
-              int32_t xe = s_x0[e0 + y];
-              bool ok = (aj[xe >> 6] >> (xe & 63)) & 1ull;
-              // the rest of k's list SHS_U entries at a time: the loads of
-              // a round are independent (a subset's full walk is the long
-              // pole of a wave)
-              const int32_t* L = a.alc + s_ao[e0 + y];
-              for (int32_t e = 1; ok && e < ck; e += SHS_U) {
-                int32_t xs[SHS_U];
+    for (int r = 0; r < R; ++r) {
+      const i64 b0 = B0 + (i64)r * TPB;
+      if (b0 >= nflags) break;                   // block-uniform
+      const i64 tile = b0 / SH_TILE;
+      const i64 t = b0 + threadIdx.x;
+      int f = 0;
+      i64 c = -1;
+      if (t < nflags) {
+        if (staged) {
+          i64 lo = 0, hi = ncls - 1;             // last class with pfoff <= t
+          while (lo < hi) {
+            const i64 mid = (lo + hi + 1) >> 1;
+            if (s_pf[mid] <= t) lo = mid; else hi = mid - 1;
+          }
+          c = c0 + lo;
+          const i64 e0 = s_so[lo] - seg0, s = s_so[lo + 1] - s_so[lo], q = t - s_pf[lo];
+          const i64 x = q / s, y = q - x * s;
+          if (s_mc[lo] > 0 && x != y) {
+            const int32_t j = s_pol[e0 + x], kk = s_pol[e0 + y];
+            const int32_t ck = s_nca[e0 + y];
+            if (j != kk) {
+              if (ck == 0) {
+                f = 1;
+              } else if (ck <= s_nca[e0 + x]) {
+                const u64* aj = a.AC + (i64)j * a.ldC;
+                int32_t xe = s_x0[e0 + y];
+                bool ok = (aj[xe >> 6] >> (xe & 63)) & 1ull;
+                // the rest of k's list SHS_U entries at a time: the loads of
+                // a round are independent (a subset's full walk is the long
+                // pole of a wave)
+                const int32_t* L = a.alc + s_ao[e0 + y];
+                for (int32_t e = 1; ok && e < ck; e += SHS_U) {
+                  int32_t xs[SHS_U];
 #pragma unroll
-                for (int u = 0; u < SHS_U; ++u) xs[u] = e + u < ck ? L[e + u] : xe;
-                u64 ws[SHS_U];
+                  for (int u = 0; u < SHS_U; ++u) xs[u] = e + u < ck ? L[e + u] : xe;
+                  u64 ws[SHS_U];
 #pragma unroll
-                for (int u = 0; u < SHS_U; ++u) ws[u] = aj[xs[u] >> 6];
+                  for (int u = 0; u < SHS_U; ++u) ws[u] = aj[xs[u] >> 6];
 #pragma unroll
-                for (int u = 0; u < SHS_U; ++u) ok = ok && ((ws[u] >> (xs[u] & 63)) & 1ull);
+                  for (int u = 0; u < SHS_U; ++u) ok = ok && ((ws[u] >> (xs[u] & 63)) & 1ull);
+                }
+                f = ok;
               }
-              f = ok;
             }
           }
-        }
-      } else {
-        c = class_of_pair(a.pfoff, c0, c1, t);
-        const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
-        const i64 x = q / s, y = q - x * s;
-        if (a.mcnt[c] > 0 && x != y) {
-          const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
-          f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+        } else {
+          c = class_of_pair(a.pfoff, c0, c1, t);
+          const i64 s0 = a.soffc[c], s = a.soffc[c + 1] - s0, q = t - a.pfoff[c];
+          const i64 x = q / s, y = q - x * s;
+          if (a.mcnt[c] > 0 && x != y) {
+            const int32_t j = a.slist[s0 + x], kk = a.slist[s0 + y];
+            f = (j != kk) && subset_of(kk, j, a.nca, a.alcoff, a.alc, a.AC, a.ldC);
+          }
         }
       }
+      // the flags as bits, one ballot word per wave (the wave's 64 pairs are
+      // consecutive: b0 is a multiple of 256); null: count only (T[c])
+      {
+        const u64 bal = __ballot(f != 0);
+        const i64 w0 = b0 + (i64)(threadIdx.x & ~63);
+        if (a.flags && (threadIdx.x & 63) == 0 && w0 < nflags)
+          reinterpret_cast<u64*>(a.flags)[w0 >> 6] = bal;
+      }
+      const i64 cw = __shfl(c, 0, 64);
+      if (__all(c == cw || c < 0)) {
+        const int rr = wave_sum(f);
+        if ((threadIdx.x & 63) == 0 && rr && cw >= 0)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[cw]), (unsigned long long)rr);
+      } else if (f) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
+      }
+      const i64 tot = block_sum((i64)f, sm);
+      if (threadIdx.x == 0 && tot && tile_cnt)   // (null: count only)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
     }
-    // the flags as bits, one ballot word per wave (the wave's 64 pairs are
-    // consecutive: b0 is a multiple of 256); null: count only (T[c])
-    {
-      const u64 bal = __ballot(f != 0);
-      const i64 w0 = b0 + (i64)(threadIdx.x & ~63);
-      if (a.flags && (threadIdx.x & 63) == 0 && w0 < nflags)
-        reinterpret_cast<u64*>(a.flags)[w0 >> 6] = bal;
-    }
-    const i64 cw = __shfl(c, 0, 64);
-    if (__all(c == cw || c < 0)) {
-      const int r = wave_sum(f);
-      if ((threadIdx.x & 63) == 0 && r && cw >= 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[cw]), (unsigned long long)r);
-    } else if (f) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(&a.T[c]), 1ull);
-    }
-    const i64 tot = block_sum((i64)f, sm);
-    if (threadIdx.x == 0 && tot && tile_cnt)   // (null: count only)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&tile_cnt[tile]), (unsigned long long)tot);
     if ((i64)gridDim.x >= nvb) break;           // one virtual block per block (uniform)
     __syncthreads();                             // LDS reused by the next virtual block
   }

@@ -248,6 +248,34 @@ def test_d1_dense_auto_picks_mfma():
     eng.close()
 
 
+def test_d1_vs_kano_py():
+    """D1 bit-exact against kano_py itself (tests/golden/expected/
+    D1_kano_py.json, make_golden.py --big D1: kano_py's build_matrix and
+    checks on the same seeded cluster, ~2 h on one core): the matrix, both
+    list CSRs, the policies' working sets and the four index lists, through
+    the bench's step with the MFMA GEMM chosen.  policy_shadow (~5e11 pairs)
+    is beyond kano_py's list: its count stays pinned by D1.json (the indexed
+    restatement, whose count-only branch equals kano_py's counts on C2 / C3,
+    tests/test_oracle_indexed.py)."""
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.synth import make_config
+    if not os.path.exists(os.path.join(GOLDEN, "expected", "D1_kano_py.json")):
+        pytest.skip("no kano_py record of D1")
+    cl = make_config("D1")
+    exp = expected("D1_kano_py")
+    assert exp["seed"]["fingerprint"] == cl.fingerprint()
+    eng = DeviceBuild(tables_from_cluster(cl), build=False)
+    eng.set_groups(tenant_groups(cl))
+    r = eng.verify("stored", sys_row=0, shadow=True, shadow_count_only=True)
+    info = eng.info()
+    assert info["HEAVY_PATH"] == 2 and info["HEAVY_KERNEL"] == 3, info   # the MFMA GEMM
+    check_verify(r, exp, shadow=False)
+    assert r["shadow_count"] == expected("D1")["policy_shadow"]["count"]
+    check_build(eng, exp, cl.n, cl.P)
+    eng.close()
+
+
 # --- the reference generator's clusters (kano_py/tests/generate.py) ----------
 GEN_NAMES = sorted(f[:-5] for f in os.listdir(os.path.join(GOLDEN, "expected"))
                    if f.startswith("gen_"))
@@ -313,7 +341,7 @@ def _lists(cs, which):
 # --- matrix-write forms ------------------------------------------------------
 @pytest.mark.parametrize("tune", ["", "store=0", "cww=64", "cww=16", "async=0", "podword=0",
                                   "hexplds=0", "dx=2", "aclds=0", "rch=3",
-                                  "rch=64,cww=16384"])
+                                  "rch=64,cww=16384", "shr=4", "shr=8"])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
     """The matrix write (k_rows) with non-temporal and plain stores, in the
@@ -345,7 +373,8 @@ def test_rows_variants_forced(name, tune, monkeypatch):
 
 
 # --- policy_shadow's count without the pairs --------------------------------
-@pytest.mark.parametrize("mode", ["shcount=0", "shcount=1", "shcount=2", "shcount=2,shgsub=0"])
+@pytest.mark.parametrize("mode", ["shcount=0", "shcount=1", "shcount=2", "shcount=2,shgsub=0",
+                                  "shcount=1,shr=4", "shcount=1,shr=8"])
 @pytest.mark.parametrize("name", ["C2", "s_broad_1000", "s_broad_300", "s_sparse_2000", "q_shadow",
                                   "q_wide_select", "gen_s5_10000", "gen_s4_4000"])
 def test_shadow_count_only_vs_kano_py(name, mode, tmp_path, monkeypatch):

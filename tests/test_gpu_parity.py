@@ -678,7 +678,7 @@ def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("tune", ["", "async=0", "store=0", "packed=0", "podword=0"])
+@pytest.mark.parametrize("tune", ["", "async=0", "store=0", "packed=0", "podword=0", "shr=4"])
 @pytest.mark.parametrize("n,P", [(1, 0), (1, 1), (2, 3), (5, 1), (63, 7), (64, 64), (65, 9),
                                  (130, 40)])
 def test_verify_small_shapes_vs_oracle(n, P, tune, monkeypatch):

@@ -80,3 +80,21 @@ def test_c5_record_matches_cluster():
     assert exp["n"] == cl.n and exp["P"] == cl.P
     s = exp["row_digest_sample"]
     assert len(s["rows"]) == len(s["digest"]) >= 500
+
+
+def test_d1_record_vs_kano_py():
+    """D1.json (the indexed restatement, which also carries policy_shadow's
+    count) against kano_py's own record of the same cluster: every index
+    list and the matrix density."""
+    import os
+    here = os.path.join(HERE, "golden", "expected")
+    if not os.path.exists(os.path.join(here, "D1_kano_py.json")):
+        pytest.skip("no kano_py record of D1")
+    mine, ref = expected("D1"), expected("D1_kano_py")
+    assert mine["seed"]["fingerprint"] == ref["seed"]["fingerprint"]
+    for k in ("all_reachable", "all_isolated"):
+        assert mine[k] == ref[k], k
+    for k in ("user_crosscheck", "system_isolation"):
+        assert mine[k]["result"] == ref[k]["result"], k
+    assert abs(mine["density"] - ref["density"]) < 1e-9
+
