@@ -150,35 +150,4 @@ __global__ __launch_bounds__(TPB) void k_inc_rewrite(
   }
 }
 
-// matchExpressions columns (kano/model.py
-// LabelExpression): out[e * n + i] = 1 when pod i meets requirement e, else 0.
-// v = the pod's value id in the key's column (-1: absent, also when no pod
-// carries the key: col < 0), set = sorted value ids.  In: v listed; NotIn:
-// absent or not listed; Exists: present; DoesNotExist: absent.
-__global__ __launch_bounds__(TPB) void k_expr_cols(const int32_t* __restrict__ pv, i64 n,
-                                                   const int32_t* __restrict__ ecol,
-                                                   const int32_t* __restrict__ eop,
-                                                   const i64* __restrict__ eoff,
-                                                   const int32_t* __restrict__ eval,
-                                                   int32_t* __restrict__ out) {
-  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
-  const i64 e = blockIdx.y;
-  if (i >= n) return;
-  const int32_t c = ecol[e];
-  const int32_t v = c >= 0 ? pv[(i64)c * n + i] : -1;
-  bool listed = false;
-  if (v >= 0) {
-    i64 lo = eoff[e], hi = eoff[e + 1];
-    while (lo < hi) {
-      const i64 mid = (lo + hi) >> 1;
-      if (eval[mid] < v) lo = mid + 1; else hi = mid;
-    }
-    listed = lo < eoff[e + 1] && eval[lo] == v;
-  }
-  const int op = eop[e];
-  const bool present = v != -1;
-  const bool m = op == 0 ? listed : op == 1 ? !listed : op == 2 ? present : !present;
-  out[e * n + i] = m ? 1 : 0;
-}
-
 }  // namespace kano

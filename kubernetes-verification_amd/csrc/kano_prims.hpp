@@ -415,7 +415,7 @@ __device__ __forceinline__ void fill_item(const FillJobs& jobs, i64 vb, i64 nvb)
     for (i64 i = vb * TPB + threadIdx.x; i < nw; i += stride) p[i] = v;
   }
 }
-__global__ __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
+static __global__ __attribute__((unused)) __launch_bounds__(TPB) void k_fill_many(FillJobs jobs) {
   fill_item(jobs, blockIdx.x, gridDim.x);
 }
 constexpr int FILL_RIDE_BLOCKS = 512;   // blocks a carried fill gets (grid-stride)
@@ -549,7 +549,7 @@ __device__ __forceinline__ uint32_t hfin(uint32_t h) {
 // host buffer directly (16 bytes per lane, a grid-stride loop): the
 // runtime's copy of a D2H range into the same buffer occasionally stalled the
 // host ~7 ms inside hipMemcpyAsync (kano_verify's tail, MI355X).
-__global__ __launch_bounds__(TPB) void k_copy_out(const uint4* __restrict__ src, uint4* dst,
+static __global__ __attribute__((unused)) __launch_bounds__(TPB) void k_copy_out(const uint4* __restrict__ src, uint4* dst,
                                                  i64 n16, const uint32_t* __restrict__ src_tail,
                                                  uint32_t* dst_tail, int ntail) {
   const i64 stride = (i64)gridDim.x * TPB;
@@ -572,7 +572,7 @@ struct CopyJob {
 struct CopyJobs {
   CopyJob j[2];
 };
-__global__ __launch_bounds__(TPB) void k_copy_out_dev(CopyJobs jobs) {
+static __global__ __attribute__((unused)) __launch_bounds__(TPB) void k_copy_out_dev(CopyJobs jobs) {
   const CopyJob a = jobs.j[blockIdx.y];
   i64 cnt = 0;
   for (int q = 0; q < a.ncnt; ++q) cnt += (i64)a.cnt[q];

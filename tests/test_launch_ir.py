@@ -32,7 +32,7 @@ FLAGS = {
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc missing")
-@pytest.mark.parametrize("src", ["kano_hip.hip", "kano_group.hip"])
+@pytest.mark.parametrize("src", ["kano_hip.hip", "kano_ext.hip", "kano_group.hip"])
 @pytest.mark.parametrize("flags", sorted(FLAGS))
 def test_no_kernel_launch_dropped(src, flags, tmp_path):
     from launch_ir_check import check

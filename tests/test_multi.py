@@ -113,25 +113,46 @@ def test_group_verify_stored_groups_c2():
 def test_multibuild_failed_init_destroys_group_once(monkeypatch):
     """A failing upload inside MultiBuild.__init__: the adopted member
     wrappers never destroy their contexts, the group is destroyed exactly
-    once (double kano_destroy)."""
+    once (double kano_destroy).  Only this test's groups and
+    members are counted (a collection may free earlier tests' engines)."""
     import gc
     from kano import _native as nat
     from kano._intern import tables_from_cluster
     from kano.multi import MultiBuild
     from kano.synth import make_config
     lib = nat.load()
+    gc.collect()          # (earlier tests' engines in reference cycles: not ours)
     calls = {"ctx": 0, "group": 0}
     real_ctx, real_group = lib.kano_destroy, lib.kano_group_destroy
+    real_member = lib.kano_group_member
+    members = set()
+
+    def member(g, r, out):
+        rc = real_member(g, r, out)
+        members.add(out._obj.value)
+        return rc
 
     def ctx_destroy(c):
-        calls["ctx"] += 1
+        if (c.value if hasattr(c, "value") else c) in members:
+            calls["ctx"] += 1
         return real_ctx(c)
 
+    real_create = lib.kano_group_create_ex
+    groups = set()
+
+    def group_create(ngpu, devs, flags, out):
+        rc = real_create(ngpu, devs, flags, out)
+        groups.add(out._obj.value)
+        return rc
+
     def group_destroy(g):
-        calls["group"] += 1
+        if (g.value if hasattr(g, "value") else g) in groups:
+            calls["group"] += 1
         return real_group(g)
     monkeypatch.setattr(lib, "kano_destroy", ctx_destroy)
     monkeypatch.setattr(lib, "kano_group_destroy", group_destroy)
+    monkeypatch.setattr(lib, "kano_group_member", member)
+    monkeypatch.setattr(lib, "kano_group_create_ex", group_create)
     t = tables_from_cluster(make_config("C2"))
     import dataclasses
     bad = dataclasses.replace(t, sel_col=np.full_like(t.sel_col, t.ncols + 5))
