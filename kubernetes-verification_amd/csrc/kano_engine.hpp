@@ -121,6 +121,12 @@ struct kano_ctx {
   int cls_packed = 1;        // packed=0: classification without packed keys (the wide-key form)
   int cls_podword = 1;       // podword=0: packed slots without the member (the smin form)
   int rows_plain = 0;        // store=0: k_rows with plain stores (non-temporal by default)
+  int rows_wide = 1;         // rw=0: wide row chunks through k_rows, not k_rows_prep + k_rows_w
+                             // (rw=2: k_rows_w at every chunk width -- the parity variants)
+  DBuf rw_items, rw_segs, rw_ticket;  // k_rows_prep's work-item descriptors, S(c) segments
+  DBuf slist_tmp;            // k_class_lists' windowed sort of long S(c) lists (P > 49k)
+  int sort_ww = 768;         // sww: that sort's window (bitmap words per wave, <= SORT_LDS_WW)
+  i64 rows_w_grid = 0;       // rwg: k_rows_w's persistent grid (0: one block per CU slot)
   int async_rows = 1;        // async=0: kano_verify waits for its matrix write
   int shadow_count_mode = 0; // shcount=1|2: count-only policy_shadow pairwise | grouped
                              // (0: the device picks, shg_grouped)

@@ -1124,17 +1124,23 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // allowed classes + bits per policy (k_pol_allow_fill): independent, one
   // launch when both run
   const bool lists_on = U > 0, allow_on = P > 0 && ctx->cc.U > 0;
+  // (the long lists' sort: bitmap windows of at most SORT_LDS_WW words per wave)
+  const i64 sort_pw = (P + 63) / 64, sort_ww = std::min<i64>(sort_pw, ctx->sort_ww);
+  const bool sort_big = P > 0 && ctx->max_sel > SORT_WAVE_MAX;
+  if (sort_big && sort_pw > sort_ww)
+    KTRY(dalloc(ctx, ctx->slist_tmp, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
   const ClassListsArgs cla{P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), P > 0 ? 1 : 0,
                            P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), P_<int32_t>(ctx->hlist),
-                           P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls)};
+                           P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls), std::max<i64>(1, sort_ww),
+                           P_<int32_t>(ctx->slist_tmp)};
   const PolAllowArgs paa{P, P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                          P_<int32_t>(ctx->am.gmem), P_<i64>(ctx->alcoff), P_<int32_t>(ctx->alc),
                          P_<u64>(ctx->AC), ctx->ldC};
-  size_t lds = (P > 0 && ctx->max_sel > SORT_WAVE_MAX)
-                   ? sizeof(u64) * (size_t)((P + 63) / 64) * (TPB / 64) : 0;
-  // AC[p] built in the wave's LDS row when the rows fit (k_pol_allow)
+  size_t lds = sort_big ? sizeof(u64) * (size_t)sort_ww * (TPB / 64) : 0;
+  // AC[p] built in the wave's LDS row when the rows fit (k_pol_allow; at
+  // most 32 KB, so that the launch fits beside a wide k_rows_w block)
   const size_t ac_lds = sizeof(u64) * (size_t)ctx->ldC * WPB;
-  const int ac_rows = ctx->ac_lds && ac_lds <= 64 * 1024 ? 1 : 0;
+  const int ac_rows = ctx->ac_lds && ac_lds <= 32 * 1024 ? 1 : 0;
   if (ac_rows) lds = std::max(lds, ac_lds);
   // the side work's joins: AC zeroed before the lists, the rest (Mc, the
   // crosscheck's fills and key sort) before the Mc writers below
@@ -1471,7 +1477,32 @@ int launch_rows(kano_ctx* ctx) {
   const int nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   const size_t lds = sizeof(u64) * cww;
   const dim3 grid((unsigned)ctx->wi_total, ncc);
-  if (nt == 1024) hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, a);
+  if ((nt == 1024 || ctx->rows_wide == 2) && ctx->rows_wide && a.alist && ctx->rows_ch <= 64) {
+    // wide chunks: the items' chains resolved ahead (k_rows_prep), then
+    // persistent blocks (one per CU, or rwg: a grid of that many, the parity
+    // variants' multi-unit blocks) drawing (item, chunk) units by ticket
+    const i64 nitems = ctx->wi_total;
+    KTRY(dalloc(ctx, ctx->rw_items, sizeof(RowsItem) * (size_t)nitems));
+    KTRY(dalloc(ctx, ctx->rw_segs, sizeof(RowsSeg) * (size_t)std::max<i64>(1, ctx->nnz_sel)));
+    RowsItem* items = P_<RowsItem>(ctx->rw_items);
+    RowsSeg* segs = P_<RowsSeg>(ctx->rw_segs);
+    const i64 per_cu = lds <= 72 * 1024 ? 2 : 1;
+    const i64 slots = ctx->rows_w_grid > 0 ? ctx->rows_w_grid : per_cu * ctx->rows_cus;
+    const i64 nunits = nitems * (i64)ncc;
+    const bool persist = nunits > slots;
+    int32_t* ticket = nullptr;
+    if (persist) {
+      KTRY(dalloc(ctx, ctx->rw_ticket, sizeof(int32_t)));
+      ticket = P_<int32_t>(ctx->rw_ticket);
+    }
+    hipLaunchKernelGGL(k_rows_prep, dim3(nblk(nitems, TPB / 64)), dim3(TPB), 0, rs, a, nitems,
+                       items, segs, ticket);
+    KLAUNCH();
+    const unsigned gx = (unsigned)(persist ? slots : nunits);
+    hipExtLaunchKernelGGL(k_rows_w<1024>, dim3(gx), dim3(1024), lds, rs, e0, e1, 0, a,
+                          (const RowsItem*)items, nitems, (const RowsSeg*)segs, ticket,
+                          (int)ncc);
+  } else if (nt == 1024) hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, a);
   else if (nt == 512) hipExtLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, e0, e1, 0, a);
   else hipExtLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, e0, e1, 0, a);
   KLAUNCH();
@@ -1852,6 +1883,9 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "packed") ctx->cls_packed = v;
         if (k == "podword") ctx->cls_podword = v;
         if (k == "store") ctx->rows_plain = v == 0;
+        if (k == "rw" && v >= 0 && v <= 2) ctx->rows_wide = v;   // 2: at every width
+        if (k == "rwg" && v >= 0) ctx->rows_w_grid = v;
+        if (k == "sww" && v >= 1 && v <= SORT_LDS_WW) ctx->sort_ww = v;
         if (k == "cww" && v >= 16 && v <= MAX_CWW_KNOB && v % 16 == 0) ctx->rows_cww = v;
         if (k == "rch" && v >= 1 && v <= 1024) ctx->rows_ch = v;
         if (k == "async") ctx->async_rows = v;
@@ -1906,6 +1940,9 @@ int kano_create(int device, kano_ctx** out) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<2, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows<1024>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(u64) * MAX_CWW_KNOB);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_w<1024>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sizeof(u64) * MAX_CWW_KNOB);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pol_counts_dx),
@@ -2014,7 +2051,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
-                  &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->vcst};
+                  &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->vcst,
+                  &ctx->rw_items, &ctx->rw_segs, &ctx->rw_ticket, &ctx->slist_tmp};
   for (DBuf* b : bufs) dfree(*b);
   RowsInputs& ra = ctx->rin_alt;
   for (DBuf* b : {&ra.wioff, &ra.wicls, &ra.soffc, &ra.slist, &ra.aloff, &ra.alist, &ra.alcoff,

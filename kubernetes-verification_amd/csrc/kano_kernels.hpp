@@ -853,12 +853,17 @@ __global__ __launch_bounds__(TPB) void k_sel_place(i64 P, const i64* __restrict_
 // rank sort in registers; larger lists are left to k_sort_lists_big (block
 // bitmap over all policies).
 constexpr int SORT_WAVE_MAX = 64;
+constexpr int SORT_LDS_WW = 768;   // bitmap words per wave (WPB x 6 KB)
 
 // One wave per class, three jobs in one launch: the class's entry in the
 // heavy list, its k_rows work items' owner map (k_flag_list), and S(c)
 // sorted ascending (with sort != 0): a rank sort in registers for s <= 64,
-// else the wave's own LDS bitmap of all P policies (dynamic LDS: WPB x
-// ceil(P/64) words, passed only when some list is longer than 64).
+// else the wave's own LDS bitmap over windows of sort_ww words of policy ids
+// (dynamic LDS: WPB x sort_ww words, passed only when some list is longer
+// than 64).  One window covers all P policies up to 49k policies; past that
+// (C5: 100k) the windows write the sorted list to stmp, copied back at the
+// end -- the block's LDS stays within 24 KB, so the lists run beside a wide
+// k_rows_w block (125 KB) on the same CU.
 struct ClassListsArgs {
   const i64* soffc;
   i64 U, P;
@@ -869,6 +874,8 @@ struct ClassListsArgs {
   int32_t* hlist;
   const int32_t* wioff;
   int32_t* wicls;
+  i64 sort_ww;           // bitmap words per wave (window)
+  int32_t* stmp;         // nnz_sel entries (windows past the first)
 };
 __device__ __forceinline__ void class_lists_item(const ClassListsArgs& a, i64 vb) {
   const i64* __restrict__ soffc = a.soffc;
@@ -897,26 +904,38 @@ __device__ __forceinline__ void class_lists_item(const ClassListsArgs& a, i64 vb
     if (lane < s) L[r] = v;
     return;
   }
-  const i64 PW = (P + 63) / 64;
-  u64* bm = lds_bm + (i64)wid * PW;
-  for (i64 w = lane; w < PW; w += 64) bm[w] = 0ull;
-  __builtin_amdgcn_wave_barrier();
-  for (i64 k = lane; k < s; k += 64) {
-    const int32_t v = L[k];
-    atomicOr(&bm[v >> 6], 1ull << (v & 63));
-  }
-  __builtin_amdgcn_wave_barrier();
+  const i64 PW = (P + 63) / 64, WW = a.sort_ww;
+  u64* bm = lds_bm + (i64)wid * WW;
+  const bool multi = PW > WW;       // (the first window's writes would clobber L)
+  int32_t* out = multi ? a.stmp + s0 : L;
   i64 base = 0;
-  for (i64 w0 = 0; w0 < PW; w0 += 64) {
-    const i64 w = w0 + lane;
-    u64 v = w < PW ? bm[w] : 0ull;
-    i64 tot;
-    i64 pos = base + wave_excl_scan((i64)__popcll(v), tot);
-    while (v) {
-      L[pos++] = (int32_t)(w * 64 + __builtin_ctzll(v));
-      v &= v - 1;
+  for (i64 v0 = 0; v0 < PW; v0 += WW) {
+    const i64 nwin = min(WW, PW - v0);
+    for (i64 w = lane; w < nwin; w += 64) bm[w] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    for (i64 k = lane; k < s; k += 64) {
+      const int32_t v = L[k];
+      const i64 vw = (i64)(v >> 6) - v0;
+      if (vw >= 0 && vw < nwin) atomicOr(&bm[vw], 1ull << (v & 63));
     }
-    base += tot;
+    __builtin_amdgcn_wave_barrier();
+    for (i64 w0 = 0; w0 < nwin; w0 += 64) {
+      const i64 w = w0 + lane;
+      u64 v = w < nwin ? bm[w] : 0ull;
+      i64 tot;
+      i64 pos = base + wave_excl_scan((i64)__popcll(v), tot);
+      while (v) {
+        out[pos++] = (int32_t)((v0 + w) * 64 + __builtin_ctzll(v));
+        v &= v - 1;
+      }
+      base += tot;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (multi) {
+    __builtin_amdgcn_s_waitcnt(0);   // the wave's scratch stores before its reads
+    __builtin_amdgcn_wave_barrier();
+    for (i64 k = lane; k < s; k += 64) L[k] = out[k];
   }
 }
 
@@ -2228,6 +2247,162 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) u64 row[];
   rows_item<NT>(a, blockIdx.x, row);
+}
+
+// ---------------------------------------------------------------------------
+// Wide rows (a row chunk of more than 4,096 words, e.g. C5's 125 KB rows): the
+// chunk fills most of a CU's LDS, so one k_rows block runs per CU and nothing
+// hides its work item's chain of dependent loads (item -> class -> S(c) ->
+// list offsets -> allowed pods -> member ids; at C5's 1/8 row shard, ~3
+// member rows per class, the SQ counters put 68 % of k_rows' wave cycles in
+// s_waitcnt).  k_rows_prep resolves the chain ahead, one wave per work item:
+// its member range, its kind, its S(c) range and the flattened length of its
+// allowed-pod lists, and (first item of a class) each S(c) entry's list
+// start re-based on the entry's prefix within the class.  k_rows_w then
+// walks the items persistently with the next item's descriptor in flight,
+// the member ids and segment table read together, each wave streaming its
+// own slice of the class's flattened lists (no block scan, no table in LDS).
+// ---------------------------------------------------------------------------
+struct RowsItem {     // 32 B
+  i64 s0;             // S(c) = slist[s0, s0 + ns)
+  i64 total;          // sum of |allowed pods(p)| over p in S(c) (light items)
+  int32_t m0, m1;     // member rows mem[m0, m1)
+  int32_t ns;
+  int32_t src;        // >= 0: heavy (copy row src, prebuilt); -1 light; -2 zero row
+};
+struct RowsSeg {      // entry e of S(c): alist index of flat id f = base + f
+  i64 base, pre;      // pre: flat id of the entry's first pod
+};
+
+__global__ __launch_bounds__(TPB) void k_rows_prep(RowsArgs a, i64 nitems,
+                                                   RowsItem* __restrict__ items,
+                                                   RowsSeg* __restrict__ segs,
+                                                   int32_t* __restrict__ ticket) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (ticket && blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0;
+  const i64 b = (i64)blockIdx.x * (TPB / 64) + wid;
+  if (b >= nitems) return;                  // wave-uniform
+  const int32_t c = a.wicls[b];
+  const i64 chunk = b - a.wioff[c];
+  const int32_t mb = a.moff[c], me = a.moff[c + 1];
+  const int32_t m0 = mb + (int32_t)(chunk * a.ch), m1 = min(me, m0 + a.ch);
+  const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
+  int32_t src = -1;
+  i64 run = 0;
+  if (a.hflag && a.hflag[c]) {
+    src = a.mem[mb];
+  } else if (s1 == s0) {
+    src = -2;
+  } else {
+    for (i64 e0 = s0; e0 < s1; e0 += 64) {
+      const i64 e = e0 + lane;
+      i64 st = 0, len = 0;
+      if (e < s1) {
+        const int32_t p = a.slist[e];
+        st = a.aloff[p];
+        len = a.aloff[p + 1] - st;
+      }
+      i64 tot;
+      const i64 pre = run + wave_excl_scan(len, tot);
+      if (chunk == 0 && e < s1) segs[e] = RowsSeg{st - pre, pre};
+      run += tot;
+    }
+  }
+  if (lane == 0) items[b] = RowsItem{s0, run, m0, m1, (int32_t)(s1 - s0), src};
+}
+
+__device__ __forceinline__ i64 readlane64(i64 v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)((u64)v >> 32), l);
+  return (i64)(((u64)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+constexpr int ROWSW_UNROLL = 8;
+// Units are (item, column chunk) pairs, u = item * ncc + chunk (a chunk
+// holds up to 16,384 words: one chunk per row up to 1M pods; half-row chunks
+// measured 3.78 -> 5.22 ms at C5's 1/8 shard, each chunk walking every
+// entry).  ticket (persistent grids): the next unit is gridDim.x +
+// ticket[0]++, drawn at the start of the current unit's build and its
+// descriptor loaded during the current unit's stores; nullptr: one unit per
+// block (or a static stride)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_w(RowsArgs a, const RowsItem* __restrict__ items,
+                                               i64 nitems, const RowsSeg* __restrict__ segs,
+                                               int32_t* __restrict__ ticket, int ncc) {
+  __shared__ i64 s_next;
+  extern __shared__ __attribute__((aligned(16))) u64 row[];
+  constexpr int NW = NT / 64;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const i64 nunits = nitems * ncc;
+  const i64 G = gridDim.x;
+  for (int w = threadIdx.x; w < a.cww; w += NT) row[w] = 0ull;
+  __syncthreads();
+  i64 u = blockIdx.x;
+  RowsItem nx{};
+  if (u < nunits) nx = items[u / ncc];
+  while (u < nunits) {
+    const RowsItem d = nx;
+    if (ticket && threadIdx.x == 0) s_next = G + atomicAdd(ticket, 1);
+    const i64 base = (u % ncc) * a.cww;
+    const int nw = (int)min((i64)a.cww, a.wW - base);   // even (ldM and cww are), > 0
+    const i64 col_lo = base * 64, col_hi = (base + nw) * 64;
+    const int nm = d.m1 - d.m0;                       // <= 64 (host: ch <= 64)
+    const int32_t mv = lane < nm ? a.mem[d.m0 + lane] : -1;
+    if (d.src >= 0) {
+      const u64* src = a.M + (i64)(d.src - a.r0) * a.ldM + base;
+      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+        *(u64x2*)&row[w] = *(const u64x2*)&src[w];
+    } else if (d.src == -1) {
+      // this wave's slice [r0, r1) of the class's flattened lists
+      const i64 T = d.total;
+      const i64 r0 = T * wid / NW, r1 = T * (wid + 1) / NW;
+      for (int i0 = 0; i0 < d.ns && r0 < r1; i0 += 64) {
+        const int e = i0 + lane;
+        i64 sb = 0, sp = T, sn = T;
+        if (e < d.ns) {
+          const RowsSeg s = segs[d.s0 + e];
+          sb = s.base;
+          sp = s.pre;
+          if (e + 1 < d.ns) sn = segs[d.s0 + e + 1].pre;
+        }
+        const int cnt = min(64, d.ns - i0);
+        for (int i = 0; i < cnt; ++i) {
+          const i64 lo = max(readlane64(sp, i), r0), hi = min(readlane64(sn, i), r1);
+          if (lo >= hi) continue;                     // wave-uniform
+          const int32_t* L = a.alist + readlane64(sb, i);
+          for (i64 j0 = lo; j0 < hi; j0 += 64 * ROWSW_UNROLL) {
+            int32_t jv[ROWSW_UNROLL];
+#pragma unroll
+            for (int u = 0; u < ROWSW_UNROLL; ++u) {
+              const i64 j = j0 + lane + 64 * u;
+              jv[u] = j < hi ? L[j] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < ROWSW_UNROLL; ++u) {
+              const i64 j = jv[u];
+              if (j >= col_lo && j < col_hi) atomicOr(&row[(j >> 6) - base], 1ull << (j & 63));
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const i64 next = ticket ? s_next : u + G;
+    if (next < nunits) nx = items[next / ncc];        // in flight during the stores
+    for (int k = 0; k < nm; ++k) {
+      const int32_t pod = __builtin_amdgcn_readlane(mv, k);
+      if (pod == d.src) continue;
+      u64* dst = a.M + (i64)(pod - a.r0) * a.ldM + base;
+      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+        __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
+    }
+    // each thread clears the words it streamed (the next item's atomics
+    // start after the barrier)
+    const u64x2 z = {0ull, 0ull};
+    for (int w = threadIdx.x * 2; w < nw; w += NT * 2) *(u64x2*)&row[w] = z;
+    __syncthreads();
+    u = next;
+  }
 }
 
 
