@@ -433,7 +433,10 @@ def main():
     value = float(n) * n / (elapsed / args.steps)
     rt = eng.rows_timing()
     k_rows_ms = rt["sum_ms"] / rt["launches"] if rt["launches"] else float("nan")
-    rows_kernel = {2: "k_rows"}.get(info["ROWS_KERNEL"], "none")
+    rows_kernel = {2: "k_rows", 3: "k_rows_w (k_rows_prep before it)",
+                   4: "k_heavy_rows_t (every class heavy; k_ptrans before it, no k_rows)",
+                   5: "k_heavy_rows_t then k_rows (timed from k_ptrans' start to k_rows' end)",
+                   }.get(info["ROWS_KERNEL"], "none")
     mt = eng.mfma_timing()
     host = eng.host_times()
     # k_rows alone (untimed, after the timed region): the same matrix write of

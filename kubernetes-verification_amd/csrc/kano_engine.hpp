@@ -143,9 +143,15 @@ struct kano_ctx {
   double xo_mfma = 1800e12, xo_or = 8500e9;
   i64 heavy_gemm_min = 512;     // HEAVY_GEMM_MIN_TILES (kano_kernels.hpp)   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
-  int heavy_expand_lds = 1;  // hexplds=0: forces the heavy rows' expansion from global
-                             // memory (the form Mc rows wider than 32 KB of LDS take)
-  int dx_on = 1;             // dx=0: never the class-indexed LDS counters (k_*_dx); 2: always
+  int heavy_expand_lds = 2;  // hexplds: heavy rows by wave transposes (k_heavy_rows_t):
+                             // every member row (3), the first member's with k_rows
+                             // copying it (4), or by class size (2); the first row
+                             // by LDS gathers (1, k_heavy_expand_w) or from global
+                             // memory (0), k_rows copying it
+  int dx_on = 1;             // dx=0: never the dense path's bit matrices (k_*_dx); 2: always
+  DBuf dx_sc, dx_sa;         // its SC (policy-major) and SA (class-indexed policy words)
+  DBuf mct;                  // the heavy rows' McT (k_heavy_rows_t)
+  i64 dx_ldY = 0, dx_PBo = 0;
   bool dense_sel = false;    // this build takes them (do_front)
   int ac_lds = 1;            // aclds=0: AC / ACT bits by global atomics, not LDS rows
   bool rin_marked = false;   // this build's last Mc launch marked ev_rin_e

@@ -771,11 +771,6 @@ int match_dense(kano_ctx* ctx, SideMatch& sx, ClassSet& cs) {
 // atomics in LDS when many policies share few row classes (broad selectors)
 // policies per block of the class-indexed LDS forms: ~256 blocks (each
 // block flushes its whole table: fewer, fuller blocks)
-int dx_ppb(const kano_ctx* ctx, i64 P) {
-  (void)ctx;
-  return (int)std::max<i64>(16, (P + 255) / 256);
-}
-
 int sel_spb(const kano_ctx* ctx) {
   return ctx->P >= 8 * std::max<i64>(1, ctx->rc.U) ? TPB : WPB;
 }
@@ -863,14 +858,27 @@ int do_front(kano_ctx* ctx, int path) {
   ctx->dense_sel = ctx->dx_on && Ur > 0 && Ur <= DX_MAX &&
                    (ctx->dx_on == 2 || ctx->nnz_sel >= 32 * Ur);   // (dx=2: forced)
   if (P > 0 && ctx->dense_sel) {
-    const int ppb = dx_ppb(ctx, P);
-    hipLaunchKernelGGL(k_pol_counts_dx, dim3((unsigned)((P + ppb - 1) / ppb)), dim3(TPB),
-                       (size_t)(12 * Ur), ctx->stream, P, P_<i64>(ctx->am.pstart),
-                       P_<int32_t>(ctx->am.plen), P_<int32_t>(ctx->am.gmem),
-                       P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca), P_<int32_t>(ctx->acnt),
-                       P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
-                       P_<int32_t>(ctx->sm.gmem), P_<int32_t>(ctx->scnt),
-                       P_<unsigned long long>(ctx->cost), Ur, ppb);
+    // the select side as bit matrices (k_selrows_dx -> k_ptrans -> counts):
+    // SA[pw][c] is also the GEMM's A when every class is heavy
+    const i64 ldU = (Ur + 63) / 64;
+    ctx->dx_ldY = (Ur + 255) / 256 * 256;
+    ctx->dx_PBo = (ctx->PB + GK_KC - 1) / GK_KC * GK_KC;
+    KTRY(dalloc(ctx, ctx->dx_sc, sizeof(u64) * (size_t)(P * ldU)));
+    KTRY(dalloc(ctx, ctx->dx_sa, sizeof(u64) * (size_t)(ctx->dx_PBo * ctx->dx_ldY)));
+    hipLaunchKernelGGL(k_selrows_dx, dim3(nblk(P, WPB)), dim3(TPB), sizeof(u64) * WPB * ldU,
+                       ctx->stream, P, P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
+                       P_<int32_t>(ctx->am.gmem), P_<int32_t>(ctx->cc.mcnt), P_<int32_t>(ctx->nca),
+                       P_<int32_t>(ctx->acnt), P_<i64>(ctx->sm.pstart), P_<int32_t>(ctx->sm.plen),
+                       P_<int32_t>(ctx->sm.gmem), ldU, P_<u64>(ctx->dx_sc));
+    KLAUNCH();
+    const i64 tiles = ctx->dx_PBo * (ctx->dx_ldY / 64);
+    hipLaunchKernelGGL(k_ptrans, dim3(nblk(tiles, WPB)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->dx_sc), ldU, P, P_<u64>(ctx->dx_sa), ctx->dx_ldY, ctx->dx_PBo,
+                       (const int32_t*)nullptr);
+    KLAUNCH();
+    hipLaunchKernelGGL(k_cls_counts_dx, dim3(nblk(Ur, WPB)), dim3(TPB), 0, ctx->stream,
+                       P_<u64>(ctx->dx_sa), ctx->dx_ldY, ctx->PB, Ur, P_<int32_t>(ctx->acnt),
+                       P_<int32_t>(ctx->scnt), P_<unsigned long long>(ctx->cost));
     KLAUNCH();
   } else if (P > 0) {
     const bool sel = Ur > 0;
@@ -1019,14 +1027,16 @@ int join_event(kano_ctx* ctx, hipEvent_t e) {
   return 0;
 }
 
+// S(c) of the dense path, ascending, from the class-indexed bits
 int sel_place_dx(kano_ctx* ctx, i64 cap) {
-  const i64 U = ctx->rc.U, P = ctx->P;
-  const int ppb = dx_ppb(ctx, P);
-  hipLaunchKernelGGL(k_sel_place_dx, dim3((unsigned)((P + ppb - 1) / ppb)), dim3(TPB),
-                     (size_t)(8 * U), ctx->stream, P, P_<i64>(ctx->sm.pstart),
-                     P_<int32_t>(ctx->sm.plen), P_<int32_t>(ctx->sm.gmem), P_<i64>(ctx->soffc),
-                     P_<int32_t>(ctx->scur), P_<int32_t>(ctx->slist), P_<int32_t>(ctx->ecls), U,
-                     ppb, cap);
+  const i64 U = ctx->rc.U;
+  // (ecls feeds only the scatter form of Mc, taken by rows wider than the
+  // owner form's LDS: see do_back)
+  const bool need_ecls = (size_t)ctx->ldC * 8 * (TPB / 64) > 64 * 1024;
+  hipLaunchKernelGGL(k_sel_lists_dx, dim3(nblk(U, WPB)), dim3(TPB),
+                     sizeof(int32_t) * WPB * SEL_DX_BUF, ctx->stream, P_<u64>(ctx->dx_sa),
+                     ctx->dx_ldY, ctx->PB, U, P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist),
+                     need_ecls ? P_<int32_t>(ctx->ecls) : (int32_t*)nullptr, cap);
   KLAUNCH();
   return 0;
 }
@@ -1096,7 +1106,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
     KTRY(dalloc(ctx, ctx->wicls, sizeof(int32_t) * std::max<i64>(1, ctx->wi_total)));
     if (mfma) {
       KTRY(dalloc(ctx, ctx->ACT, sizeof(u64) * std::max<i64>(1, PBp * ldB)));
-      KTRY(fb.add(ctx->ACT, sizeof(u64) * PBp * ldB, 0u));
+      if (!ctx->dense_sel) KTRY(fb.add(ctx->ACT, sizeof(u64) * PBp * ldB, 0u));
       // (the GEMM's A is written whole, padding included, by k_heavy_selT: no fill)
       const i64 aw = gemm ? PBp * ldA : ctx->PB * U;
       KTRY(dalloc(ctx, ctx->scratch_words, sizeof(u64) * std::max<i64>(1, aw)));
@@ -1126,10 +1136,11 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   const bool lists_on = U > 0, allow_on = P > 0 && ctx->cc.U > 0;
   // (the long lists' sort: bitmap windows of at most SORT_LDS_WW words per wave)
   const i64 sort_pw = (P + 63) / 64, sort_ww = std::min<i64>(sort_pw, ctx->sort_ww);
-  const bool sort_big = P > 0 && ctx->max_sel > SORT_WAVE_MAX;
+  const bool sort_on = P > 0 && !ctx->dense_sel;   // (the dense lists come sorted)
+  const bool sort_big = sort_on && ctx->max_sel > SORT_WAVE_MAX;
   if (sort_big && sort_pw > sort_ww)
     KTRY(dalloc(ctx, ctx->slist_tmp, sizeof(int32_t) * std::max<i64>(1, ctx->nnz_sel)));
-  const ClassListsArgs cla{P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), P > 0 ? 1 : 0,
+  const ClassListsArgs cla{P_<i64>(ctx->soffc), U, P, P_<int32_t>(ctx->slist), sort_on ? 1 : 0,
                            P_<int32_t>(ctx->hflag), P_<int32_t>(ctx->hoff), P_<int32_t>(ctx->hlist),
                            P_<int32_t>(ctx->wioff), P_<int32_t>(ctx->wicls), std::max<i64>(1, sort_ww),
                            P_<int32_t>(ctx->slist_tmp)};
@@ -1237,7 +1248,12 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   if (H > 0) {
     if (mfma) {
       const i64 Ua = ctx->cc.U;
-      if (ctx->ac_lds && ldB * 8 <= 64 * 1024 + 2048) {
+      if (ctx->dense_sel) {
+        // (ACT = AC's 64 x 64 bit blocks transposed: every word written)
+        hipLaunchKernelGGL(k_ptrans, dim3(nblk(PBp * ((ldB + 63) / 64), WPB)), dim3(TPB), 0,
+                           ctx->stream, P_<u64>(ctx->AC), ctx->ldC, P, P_<u64>(ctx->ACT), ldB,
+                           PBp, (const int32_t*)nullptr);
+      } else if (ctx->ac_lds && ldB * 8 <= 64 * 1024 + 2048) {
         // (ACT rows through LDS, one block per 64 policies)
         const i64 ns = std::min<i64>(8, std::max<i64>(1, 512 / std::max<i64>(1, ctx->PB)));
         const i64 sw = (ldB + ns - 1) / ns;
@@ -1268,10 +1284,18 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         const dim3 grid((unsigned)(8 * ((nb + 7) / 8)));
         const int32_t* hl = P_<int32_t>(ctx->hlist);
         u64* A = P_<u64>(ctx->scratch_words);
-        hipLaunchKernelGGL(k_heavy_selT, dim3(nblk(ldA, TPB / 64)), dim3(TPB),
-                           sizeof(u64) * (size_t)PBp * (TPB / 64), ctx->stream, hl, H, ldA,
-                           P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), PBp, A);
-        KLAUNCH();
+        if (ctx->dense_sel && H == U && ldA == ctx->dx_ldY && PBp == ctx->dx_PBo) {
+          A = P_<u64>(ctx->dx_sa);   // every class heavy: SA is A as it stands
+        } else if (ctx->dense_sel) {
+          hipLaunchKernelGGL(k_sa_gather, dim3(nblk(PBp * ldA)), dim3(TPB), 0, ctx->stream,
+                             P_<u64>(ctx->dx_sa), ctx->dx_ldY, hl, H, PBp, A, ldA);
+          KLAUNCH();
+        } else {
+          hipLaunchKernelGGL(k_heavy_selT, dim3(nblk(ldA, TPB / 64)), dim3(TPB),
+                             sizeof(u64) * (size_t)PBp * (TPB / 64), ctx->stream, hl, H, ldA,
+                             P_<i64>(ctx->soffc), P_<int32_t>(ctx->slist), PBp, A);
+          KLAUNCH();
+        }
         KTRY(resolve_mfma_time(ctx));
         KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
         {
@@ -1426,11 +1450,44 @@ int launch_rows(kano_ctx* ctx) {
   ctx->rows_last = rs;
   if (ctx->rows_after) KCHK(hipStreamWaitEvent(rs, ctx->rows_after, 0));
   hipEvent_t e0 = ctx->ev_rt[set][0], e1 = ctx->ev_rt[set][1];
+  // (the write's time: from the first kernel's start to k_rows' end)
+  hipEvent_t e0_rows = e0;
+  bool heavy_whole = false, rows_needed = true, rows_wide_used = false;
   if (ctx->heavy_count > 0) {
     const i64 H = ctx->heavy_count, ldMc = ctx->ldC;
     // nc classes' Mc rows in <= 32 KB of LDS (two blocks per CU), at most 64
     const i64 nc = std::min<i64>(64, (32 * 1024) / (8 * std::max<i64>(1, ldMc)));
-    if (nc >= 1 && ctx->heavy_expand_lds) {
+    if (ctx->heavy_expand_lds >= 2) {
+      // the heavy classes' first member rows (hexplds=3: every member row,
+      // k_rows then skips them) from McT (k_ptrans of their Mc rows) by
+      // wave transposes
+      const i64 HW = (H + 63) / 64, ldT = std::max<i64>(1, ctx->cc.U);
+      KTRY(dalloc(ctx, ctx->mct, sizeof(u64) * (size_t)(HW * ldT)));
+      hipExtLaunchKernelGGL(k_ptrans, dim3(nblk(HW * ((ldT + 63) / 64), WPB)), dim3(TPB), 0, rs,
+                            e0, nullptr, 0, P_<u64>(ctx->Mc), ldMc, H, P_<u64>(ctx->mct), ldT,
+                            HW, P_<int32_t>(ctx->hlist));
+      KLAUNCH();
+      e0_rows = nullptr;
+      // (every member row: the members split over Z blocks, so that ~2,048
+      // blocks run whatever the class sizes -- C4's 99 classes of ~1,000 pods)
+      // whole (every member row) for small heavy classes (D1: 12.5 pods a
+      // class, step 1.40 -> 1.32 ms), first rows + k_rows' copies for large
+      // ones (C4: ~1,000 pods a class, 0.465 against 0.488 ms)
+      const bool whole = ctx->heavy_expand_lds == 3 ||
+                         (ctx->heavy_expand_lds == 2 && rows_local(ctx) <= 32 * H);
+      const i64 nxy = (i64)nblk(ldM, HXB) * HW;
+      const unsigned Z = whole ? (unsigned)std::min<i64>(64, std::max<i64>(1, 2048 / nxy)) : 1u;
+      // (every class heavy and written whole: no k_rows, this launch ends the write)
+      const bool last = whole && H == U;
+      hipExtLaunchKernelGGL(k_heavy_rows_t, dim3(nblk(ldM, HXB), (unsigned)HW, Z), dim3(TPB), 0,
+                            rs, nullptr, last ? e1 : nullptr, 0, P_<u64>(ctx->mct), ldT,
+                            P_<int32_t>(ctx->hlist), H, P_<int32_t>(ctx->cc.cls), n,
+                            P_<int32_t>(ctx->rc.moff), P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M),
+                            ldM, ctx->r0, whole ? 0 : 1);
+      KLAUNCH();
+      heavy_whole = whole;
+      rows_needed = !last;
+    } else if (nc >= 1 && ctx->heavy_expand_lds) {
       const i64 gy = (H + nc - 1) / nc, gx = (ldM + TPB - 1) / TPB;
       hipLaunchKernelGGL(k_heavy_expand_w, dim3((unsigned)gx, (unsigned)gy), dim3(TPB),
                          sizeof(u64) * (size_t)(nc * ldMc), rs, P_<int32_t>(ctx->hlist), H,
@@ -1473,11 +1530,16 @@ int launch_rows(kano_ctx* ctx) {
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
   a.plain = ctx->rows_plain;
+  a.heavy_skip = heavy_whole ? 1 : 0;
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
   const int nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
   const size_t lds = sizeof(u64) * cww;
   const dim3 grid((unsigned)ctx->wi_total, ncc);
-  if ((nt == 1024 || ctx->rows_wide == 2) && ctx->rows_wide && a.alist && ctx->rows_ch <= 64) {
+  if (!rows_needed) {
+    // (the heavy rows' launch carries the write's stop event)
+  } else if ((nt == 1024 || ctx->rows_wide == 2) && ctx->rows_wide && a.alist &&
+             ctx->rows_ch <= 64) {
+    rows_wide_used = true;
     // wide chunks: the items' chains resolved ahead (k_rows_prep), then
     // persistent blocks (one per CU, or rwg: a grid of that many, the parity
     // variants' multi-unit blocks) drawing (item, chunk) units by ticket
@@ -1499,14 +1561,20 @@ int launch_rows(kano_ctx* ctx) {
                        items, segs, ticket);
     KLAUNCH();
     const unsigned gx = (unsigned)(persist ? slots : nunits);
-    hipExtLaunchKernelGGL(k_rows_w<1024>, dim3(gx), dim3(1024), lds, rs, e0, e1, 0, a,
+    hipExtLaunchKernelGGL(k_rows_w<1024>, dim3(gx), dim3(1024), lds, rs, e0_rows, e1, 0, a,
                           (const RowsItem*)items, nitems, (const RowsSeg*)segs, ticket,
                           (int)ncc);
-  } else if (nt == 1024) hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0, e1, 0, a);
-  else if (nt == 512) hipExtLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, e0, e1, 0, a);
-  else hipExtLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, e0, e1, 0, a);
+  } else if (nt == 1024) {
+    hipExtLaunchKernelGGL(k_rows<1024>, grid, dim3(1024), lds, rs, e0_rows, e1, 0, a);
+  } else if (nt == 512) {
+    hipExtLaunchKernelGGL(k_rows<512>, grid, dim3(512), lds, rs, e0_rows, e1, 0, a);
+  } else {
+    hipExtLaunchKernelGGL(k_rows<256>, grid, dim3(256), lds, rs, e0_rows, e1, 0, a);
+  }
   KLAUNCH();
-  ctx->rows_kernel = 2;
+  // (KANO_INFO_ROWS_KERNEL: 2 k_rows, 3 k_rows_prep + k_rows_w, 4 the heavy
+  // rows whole with no k_rows, 5 the heavy rows then k_rows)
+  ctx->rows_kernel = !rows_needed ? 4 : e0_rows == nullptr ? 5 : rows_wide_used ? 3 : 2;
   ctx->rows_timed = true;
   ctx->rows_time_pending[set] = true;
   ctx->rows_end_ev[set] = e1;
@@ -1945,10 +2013,6 @@ int kano_create(int device, kano_ctx** out) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_w<1024>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sizeof(u64) * MAX_CWW_KNOB);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pol_counts_dx),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 12 * DX_MAX);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sel_place_dx),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 12 * DX_MAX);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_classbits_rows),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 8448);
   }
@@ -2052,7 +2116,8 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
                   &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->vcst,
-                  &ctx->rw_items, &ctx->rw_segs, &ctx->rw_ticket, &ctx->slist_tmp};
+                  &ctx->rw_items, &ctx->rw_segs, &ctx->rw_ticket, &ctx->slist_tmp,
+                  &ctx->dx_sc, &ctx->dx_sa, &ctx->mct};
   for (DBuf* b : bufs) dfree(*b);
   RowsInputs& ra = ctx->rin_alt;
   for (DBuf* b : {&ra.wioff, &ra.wicls, &ra.soffc, &ra.slist, &ra.aloff, &ra.alist, &ra.alcoff,

@@ -1039,133 +1039,184 @@ __global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict
 
 
 // ---- broad selectors over few row classes (D1: every class selected by
-// ~2,250 of 10^4 policies): the per-class counters of k_pol_counts /
-// k_sel_place meet in LDS tables indexed by class (U <= DX_MAX), one global
-// atomic per (block, class) instead of one per select entry -- 36M contended
-// atomics on 8,000 addresses became ~2.5M.  ppb policies per block, one wave
-// per policy; dynamic LDS: 12 U bytes (counts) / 8 U bytes (placement).
+// ~2,250 of 10^4 policies, 18M select entries on 8,000 classes) as bit
+// matrices instead of per-entry counters and cursors:
+//   k_selrows_dx   each policy's selected classes as a bit row SC[p] (U bits,
+//                  built in the wave's LDS row, stored whole), and its allowed
+//                  classes' and pods' counts (nca, acnt);
+//   k_ptrans       64 x 64 bit-block transposes, policy-major bit rows ->
+//                  class-indexed policy words: SA[pw][c] bit q = policy
+//                  64 pw + q selects c (also ACT from AC on the allow side,
+//                  the GEMM's operands as they are);
+//   k_cls_counts_dx |S(c)| and the rebuild cost from SA's column c;
+//   k_sel_lists_dx S(c) ascending (set-bit order) at soffc[c], with ecls.
+// (round 4's k_pol_counts_dx / k_sel_place_dx put the 18M entries through
+// LDS class counters and cursors: 193 + 486 us at D1, plus a sort)
 constexpr int DX_MAX = 8192;
-constexpr int DX_UNROLL = 4;
-__global__ __launch_bounds__(TPB) void k_pol_counts_dx(i64 P, const i64* __restrict__ apstart,
-                                                       const int32_t* __restrict__ aplen,
-                                                       const int32_t* __restrict__ apcls,
-                                                       const int32_t* __restrict__ csize,
-                                                       int32_t* __restrict__ nca,
-                                                       int32_t* __restrict__ acnt,
-                                                       const i64* __restrict__ spstart,
-                                                       const int32_t* __restrict__ splen,
-                                                       const int32_t* __restrict__ spcls,
-                                                       int32_t* scnt, unsigned long long* cost,
-                                                       i64 U, int ppb) {
+constexpr int DX_UNROLL = 4;   // list loads in flight per lane (k_classbits_rows)
+constexpr int SR_UNROLL = 8;   // the same in k_selrows_dx
+__global__ __launch_bounds__(TPB) void k_selrows_dx(i64 P, const i64* __restrict__ apstart,
+                                                    const int32_t* __restrict__ aplen,
+                                                    const int32_t* __restrict__ apcls,
+                                                    const int32_t* __restrict__ csize,
+                                                    int32_t* __restrict__ nca,
+                                                    int32_t* __restrict__ acnt,
+                                                    const i64* __restrict__ spstart,
+                                                    const int32_t* __restrict__ splen,
+                                                    const int32_t* __restrict__ spcls, i64 ldU,
+                                                    u64* __restrict__ SC) {
   extern __shared__ __attribute__((aligned(16))) u64 dx[];
-  unsigned long long* lcost = reinterpret_cast<unsigned long long*>(dx);
-  int32_t* lcnt = reinterpret_cast<int32_t*>(dx + U);
-  for (i64 t = threadIdx.x; t < U; t += TPB) {
-    lcost[t] = 0ull;
-    lcnt[t] = 0;
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int q = wv; q < ppb; q += TPB / 64) {
-    const i64 p = (i64)blockIdx.x * ppb + q;
-    if (p >= P) break;                               // wave-uniform
-    const int32_t* L = apcls + apstart[p];
-    const int32_t len = aplen[p];
-    i64 pods = 0;
-    // (DX_UNROLL independent loads in flight per lane)
-    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
-      int32_t c[DX_UNROLL];
+  const i64 p = (i64)blockIdx.x * WPB + wv;
+  if (p >= P) return;                                // wave-uniform; no block barrier
+  u64* r = dx + (i64)wv * ldU;
+  for (i64 w = lane; w < ldU; w += 64) r[w] = 0ull;
+  const int32_t* L = apcls + apstart[p];
+  const int32_t len = aplen[p];
+  i64 pods = 0;
+  for (int32_t k0 = lane; k0 < len; k0 += 64 * SR_UNROLL) {
+    int32_t c[SR_UNROLL];
 #pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
+    for (int u = 0; u < SR_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
 #pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) pods += c[u] >= 0 ? csize[c[u]] : 0;
-    }
-    pods = wave_sum(pods);
-    if (lane == 0) {
-      nca[p] = len;
-      acnt[p] = (int32_t)pods;
-    }
-    const int32_t* S = spcls + spstart[p];
-    const int32_t slen = splen[p];
-    const unsigned long long a = (unsigned long long)(int32_t)pods;
-    for (int32_t k0 = lane; k0 < slen; k0 += 64 * DX_UNROLL) {
-      int32_t c[DX_UNROLL];
+    for (int u = 0; u < SR_UNROLL; ++u) pods += c[u] >= 0 ? csize[c[u]] : 0;
+  }
+  pods = wave_sum(pods);
+  if (lane == 0) {
+    nca[p] = len;
+    acnt[p] = (int32_t)pods;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  const int32_t* S = spcls + spstart[p];
+  const int32_t slen = splen[p];
+  for (int32_t k0 = lane; k0 < slen; k0 += 64 * SR_UNROLL) {
+    int32_t c[SR_UNROLL];
 #pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < slen ? S[k0 + 64 * u] : -1;
+    for (int u = 0; u < SR_UNROLL; ++u) c[u] = k0 + 64 * u < slen ? S[k0 + 64 * u] : -1;
 #pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) {
-        if (c[u] < 0) continue;
-        atomicAdd(&lcnt[c[u]], 1);
-        if (a) atomicAdd(&lcost[c[u]], a);
-      }
+    for (int u = 0; u < SR_UNROLL; ++u)
+      if (c[u] >= 0) atomicOr(&r[c[u] >> 6], 1ull << (c[u] & 63));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  for (i64 w = lane; w < ldU; w += 64) SC[p * ldU + w] = r[w];
+}
+
+// 64 x 64 bit transpose across a wave: lane r holds row r (bit c = element
+// (r, c)); returns lane r's column r (bit j = element (j, r)).  Six butterfly
+// stages, each swapping the off-diagonal s x s blocks between lanes r and
+// r ^ s (a 64-bit shuffle and six bit operations a stage, against 64 ballots)
+__device__ __forceinline__ u64 wave_transpose64(u64 x, int lane) {
+  constexpr u64 MS[6] = {0x00000000ffffffffull, 0x0000ffff0000ffffull, 0x00ff00ff00ff00ffull,
+                         0x0f0f0f0f0f0f0f0full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int sft = 32 >> k;
+    const u64 m = MS[k];
+    const u64 y = __shfl_xor(x, sft, 64);
+    x = (lane & sft) ? ((x & ~m) | ((y & ~m) >> sft)) : ((x & m) | ((y & m) << sft));
+  }
+  return x;
+}
+
+// Y[pw][c] (c < ldY, pw < PBo) = the policy word of class c: bit q = bit c of
+// X's row 64 pw + q (rows >= P and words >= ldX read as zero; rmap: row r is
+// X's row rmap[r]).  One wave per 64 x 64 tile: lane r holds row 64 pw + r's
+// word g, wave_transpose64 turns it.
+__global__ __launch_bounds__(TPB) void k_ptrans(const u64* __restrict__ X, i64 ldX, i64 P,
+                                                u64* __restrict__ Y, i64 ldY, i64 PBo,
+                                                const int32_t* __restrict__ rmap) {
+  const int lane = threadIdx.x & 63;
+  const i64 G = (ldY + 63) / 64;
+  const i64 t = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (t >= PBo * G) return;
+  const i64 pw = t / G, g = t - pw * G;
+  const i64 row = pw * 64 + lane;
+  const u64 x = row < P && g < ldX ? X[(rmap ? (i64)rmap[row] : row) * ldX + g] : 0ull;
+  const u64 y = wave_transpose64(x, lane);
+  const i64 c = g * 64 + lane;
+  if (c < ldY) Y[pw * ldY + c] = y;
+}
+
+// |S(c)| and the rebuild cost sum_{p in S(c)} |allowed pods(p)|, one wave per
+// class over SA's column c
+__global__ __launch_bounds__(TPB) void k_cls_counts_dx(const u64* __restrict__ SA, i64 ldY,
+                                                       i64 PB, i64 U,
+                                                       const int32_t* __restrict__ acnt,
+                                                       int32_t* __restrict__ scnt,
+                                                       unsigned long long* __restrict__ cost) {
+  const int lane = threadIdx.x & 63;
+  const i64 c = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (c >= U) return;
+  i64 cnt = 0;
+  unsigned long long cs = 0ull;
+  for (i64 pw = lane; pw < PB; pw += 64) {
+    u64 w = SA[pw * ldY + c];
+    cnt += __popcll(w);
+    while (w) {
+      cs += (unsigned long long)(int32_t)acnt[pw * 64 + __builtin_ctzll(w)];
+      w &= w - 1;
     }
   }
-  __syncthreads();
-  for (i64 t = threadIdx.x; t < U; t += TPB) {
-    if (lcnt[t]) atomicAdd(&scnt[t], lcnt[t]);
-    if (lcost[t]) atomicAdd(&cost[t], lcost[t]);
+  cnt = wave_sum(cnt);
+  cs = wave_sum(cs);
+  if (lane == 0) {
+    scnt[c] = (int32_t)cnt;
+    cost[c] = cs;
   }
 }
 
-// the placement: count per class in LDS, one cursor reservation per (block,
-// class), then the entries at LDS cursors (S(c) is sorted afterwards)
-__global__ __launch_bounds__(TPB) void k_sel_place_dx(i64 P, const i64* __restrict__ pstart,
-                                                      const int32_t* __restrict__ plen,
-                                                      const int32_t* __restrict__ pcls,
+// S(c) ascending at soffc[c] (entries past cap dropped: the early placement
+// into the previous build's capacity), ecls[e] = c (nullable: only the
+// scatter form of Mc reads it).  One wave per class; each 64-word chunk of
+// SA's column is expanded into the wave's LDS buffer (dynamic LDS: WPB x
+// SEL_DX_BUF entries) and copied out in coalesced stores.
+constexpr int SEL_DX_BUF = 4096;
+__global__ __launch_bounds__(TPB) void k_sel_lists_dx(const u64* __restrict__ SA, i64 ldY,
+                                                      i64 PB, i64 U,
                                                       const i64* __restrict__ soffc,
-                                                      int32_t* scur, int32_t* __restrict__ slist,
-                                                      int32_t* __restrict__ ecls, i64 U, int ppb,
-                                                      i64 cap) {
-  // (8 U B of LDS: two blocks per CU at U = 8,192; an i64 base with soffc
-  // folded in, 12 U B, took one and measured slower, 515 -> 549 us at D1)
-  extern __shared__ __attribute__((aligned(16))) u64 dx[];
-  int32_t* lcnt = reinterpret_cast<int32_t*>(dx);
-  int32_t* lbase = lcnt + U;
-  for (i64 t = threadIdx.x; t < U; t += TPB) lcnt[t] = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int q = wv; q < ppb; q += TPB / 64) {
-    const i64 p = (i64)blockIdx.x * ppb + q;
-    if (p >= P) break;
-    const int32_t* L = pcls + pstart[p];
-    const int32_t len = plen[p];
-    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
-      int32_t c[DX_UNROLL];
-#pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
-#pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u)
-        if (c[u] >= 0) atomicAdd(&lcnt[c[u]], 1);
+                                                      int32_t* __restrict__ slist,
+                                                      int32_t* __restrict__ ecls, i64 cap) {
+  extern __shared__ int32_t lbuf[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const i64 c = (i64)blockIdx.x * WPB + wid;
+  if (c >= U) return;                                // wave-uniform; no block barrier
+  int32_t* buf = lbuf + wid * SEL_DX_BUF;
+  i64 base = soffc[c];
+  for (i64 pw0 = 0; pw0 < PB; pw0 += 64) {
+    const i64 pw = pw0 + lane;
+    u64 w = pw < PB ? SA[pw * ldY + c] : 0ull;
+    int tot;
+    int pos = wave_excl_scan((int)__popcll(w), tot);
+    while (w) {
+      buf[pos++] = (int32_t)(pw * 64 + __builtin_ctzll(w));
+      w &= w - 1;
     }
-  }
-  __syncthreads();
-  for (i64 t = threadIdx.x; t < U; t += TPB) {
-    if (lcnt[t]) {
-      lbase[t] = atomicAdd(&scur[t], lcnt[t]);
-      lcnt[t] = 0;
-    }
-  }
-  __syncthreads();
-  for (int q = wv; q < ppb; q += TPB / 64) {
-    const i64 p = (i64)blockIdx.x * ppb + q;
-    if (p >= P) break;
-    const int32_t* L = pcls + pstart[p];
-    const int32_t len = plen[p];
-    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
-      int32_t c[DX_UNROLL];
-#pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
-#pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) {
-        if (c[u] < 0) continue;
-        const i64 e = soffc[c[u]] + lbase[c[u]] + atomicAdd(&lcnt[c[u]], 1);
-        if (e < cap) {
-          slist[e] = (int32_t)p;
-          ecls[e] = c[u];
-        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lane; k < tot; k += 64) {
+      const i64 e = base + k;
+      if (e < cap) {
+        slist[e] = buf[k];
+        if (ecls) ecls[e] = (int32_t)c;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    base += tot;
   }
+}
+
+// the GEMM's A over the heavy classes: A[pw][h] = SA[pw][hlist[h]] (zero
+// past H), when the heavy classes are not all of them
+__global__ __launch_bounds__(TPB) void k_sa_gather(const u64* __restrict__ SA, i64 ldY,
+                                                   const int32_t* __restrict__ hlist, i64 H,
+                                                   i64 PBo, u64* __restrict__ A, i64 ldA) {
+  const i64 i = (i64)blockIdx.x * TPB + threadIdx.x;
+  if (i >= PBo * ldA) return;
+  const i64 pw = i / ldA, h = i - pw * ldA;
+  A[i] = h < H ? SA[pw * ldY + hlist[h]] : 0ull;
 }
 
 // ACT rows through LDS: block pb takes policies [64 pb, 64 pb + 64), ORs
@@ -1216,6 +1267,7 @@ struct PolAllowArgs {
   i64 ldC;
 };
 
+constexpr int PA_UNROLL = 8;
 // (lds_row: the wave builds AC[p] in its LDS row of ldC words and stores it
 // whole -- long allow lists put thousands of same-word global atomics on
 // one row; the row needs ldC * 8 * WPB bytes of the launch's dynamic LDS)
@@ -1232,10 +1284,17 @@ __device__ __forceinline__ void pol_allow_item(const PolAllowArgs& a, i64 vb, bo
     for (i64 w = lane; w < a.ldC; w += 64) r[w] = 0ull;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
-    for (int32_t k = lane; k < len; k += 64) {
-      const int32_t ca = L[k];
-      out[k] = ca;
-      atomicOr(&r[ca >> 6], 1ull << (ca & 63));
+    // (PA_UNROLL list loads in flight per lane: D1's lists hold ~1,760 classes)
+    for (int32_t k0 = lane; k0 < len; k0 += 64 * PA_UNROLL) {
+      int32_t ca[PA_UNROLL];
+#pragma unroll
+      for (int u = 0; u < PA_UNROLL; ++u) ca[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < PA_UNROLL; ++u) {
+        if (ca[u] < 0) continue;
+        out[k0 + 64 * u] = ca[u];
+        atomicOr(&r[ca[u] >> 6], 1ull << (ca[u] & 63));
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -2042,6 +2101,60 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand_w(const int32_t* __restric
   }
 }
 
+// Heavy rows straight from the class-level matrix, every member row: McT
+// (k_ptrans of Mc's heavy rows: McT[hw][a] bit i = heavy class 64 hw + i
+// reaches column class a).  Block (64-word range, heavy word hw): lane j of
+// a wave looks up pod 64 w + j's column class in McT, a wave transpose turns
+// the 64 pods x 64 classes bits into the 64 classes' words of row word w, kept in
+// LDS; then the first member row of each class (first_only: k_rows copies
+// it to the others in whole-row stores) or every member row takes the 512-B
+// segment.  (k_heavy_expand_w gathered 64 bits per output word from LDS:
+// 0.63 ms at D1 before k_rows' 0.60 ms copy)
+constexpr int HXB = 64;          // row words per block
+constexpr int HXS = HXB + 2;     // LDS row stride (16-B aligned rows)
+__global__ __launch_bounds__(TPB) void k_heavy_rows_t(const u64* __restrict__ McT, i64 ldT,
+                                                      const int32_t* __restrict__ hlist, i64 H,
+                                                      const int32_t* __restrict__ cla, i64 n,
+                                                      const int32_t* __restrict__ moff,
+                                                      const int32_t* __restrict__ mem,
+                                                      u64* __restrict__ M, i64 ldM, i64 r0,
+                                                      int first_only) {
+  __shared__ __attribute__((aligned(16))) u64 T[64 * HXS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const i64 hw = blockIdx.y;
+  const i64 w0 = (i64)blockIdx.x * HXB;
+  const int nwb = (int)min((i64)HXB, ldM - w0);     // even: ldM and HXB are
+  for (int q = wid; q < nwb; q += WPB) {
+    const i64 pod = (w0 + q) * 64 + lane;
+    const int32_t a = pod < n ? cla[pod] : -1;
+    const u64 x = a >= 0 ? McT[hw * ldT + a] : 0ull;
+    T[lane * HXS + q] = wave_transpose64(x, lane);
+  }
+  __syncthreads();
+  // a wave per class, two member rows per store instruction (32 lanes x 16 B)
+  const int nh = (int)min((i64)64, H - hw * 64);
+  const int half = lane >> 5, l = lane & 31;
+  for (int i = wid; i < nh; i += WPB) {
+    const int32_t c = hlist[hw * 64 + i];
+    const int32_t mb = moff[c], me = first_only ? min(moff[c + 1], mb + 1) : moff[c + 1];
+    const u64* src = T + i * HXS;
+    // (members mb + z, mb + z + Z, ... : blockIdx.z of gridDim.z = Z)
+    const int32_t Z = (int32_t)gridDim.z;
+    for (int32_t k0 = mb + (int32_t)blockIdx.z; k0 < me; k0 += 64 * Z) {
+      const int32_t idx = k0 + lane * Z;
+      const int32_t mv = idx < me ? mem[idx] : -1;
+      const int cnt = min(64, (me - k0 + Z - 1) / Z);
+      for (int t = 0; t < cnt; t += 2) {
+        const int32_t pod = __shfl(mv, t + half, 64);
+        if (t + half >= cnt) continue;
+        u64* dst = M + (i64)(pod - r0) * ldM + w0;
+        for (int u = 2 * l; u < nwb; u += 64)
+          __builtin_nontemporal_store(*(const u64x2*)&src[u], (u64x2*)&dst[u]);
+      }
+    }
+  }
+}
+
 // ===========================================================================
 // Matrix rows (model.py:158-160).  One block = one work item (class, up to
 // ch member pods, column chunk of cww words).  Light classes rebuild their
@@ -2074,6 +2187,7 @@ struct RowsArgs {
   int ch;
   int cww;
   int plain;             // plain 16-byte stores (else non-temporal)
+  int heavy_skip;        // heavy classes' rows written whole by k_heavy_rows_t
   u64* color;
   u64* colnand;
 };
@@ -2184,6 +2298,7 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   const int32_t m0 = m_begin + (int32_t)(chunk * a.ch);
   const int32_t m1 = min(m_end, m0 + a.ch);
   const bool heavy = a.hflag && a.hflag[c];
+  if (heavy && a.heavy_skip) return;
   // a class no policy selects (C3: 9,143 of 21,535 row classes): its rows are
   // zero -- stored straight from registers, no row build, no barrier
   if (!heavy && a.soffc[c + 1] == a.soffc[c]) {
@@ -2285,12 +2400,14 @@ __global__ __launch_bounds__(TPB) void k_rows_prep(RowsArgs a, i64 nitems,
   const int32_t c = a.wicls[b];
   const i64 chunk = b - a.wioff[c];
   const int32_t mb = a.moff[c], me = a.moff[c + 1];
-  const int32_t m0 = mb + (int32_t)(chunk * a.ch), m1 = min(me, m0 + a.ch);
+  const int32_t m0 = mb + (int32_t)(chunk * a.ch);
+  int32_t m1 = min(me, m0 + a.ch);
   const i64 s0 = a.soffc[c], s1 = a.soffc[c + 1];
   int32_t src = -1;
   i64 run = 0;
   if (a.hflag && a.hflag[c]) {
     src = a.mem[mb];
+    if (a.heavy_skip) m1 = m0;       // (written whole by k_heavy_rows_t)
   } else if (s1 == s0) {
     src = -2;
   } else {
