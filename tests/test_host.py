@@ -297,3 +297,33 @@ def test_parser_shares_labels_and_walks_directory(tmp_path, capsys):
     assert ps[1].protocol == ["TCP", 5432]
     assert ConfigParser().parse() is None
     assert "no filepath specified" in capsys.readouterr().out
+
+
+# --------------------------------------------------------------------------
+# wave_transpose64 (csrc/kano_kernels.hpp): the butterfly, lane by lane
+# --------------------------------------------------------------------------
+def _wave_transpose64_model(x):
+    """The kernel's six stages on 64 lanes' words: stage s pairs lanes r and
+    r ^ s; the lower lane keeps its bits c with c & s == 0 and takes the
+    partner's into c | s, the upper lane the converse (kano_kernels.hpp,
+    wave_transpose64)."""
+    masks = [0x00000000ffffffff, 0x0000ffff0000ffff, 0x00ff00ff00ff00ff,
+             0x0f0f0f0f0f0f0f0f, 0x3333333333333333, 0x5555555555555555]
+    full = (1 << 64) - 1
+    x = [int(v) for v in x]
+    for k, m in enumerate(masks):
+        s = 32 >> k
+        y = [x[r ^ s] for r in range(64)]
+        x = [((x[r] & ~m & full) | ((y[r] & ~m & full) >> s)) if r & s
+             else ((x[r] & m) | (((y[r] & m) << s) & full)) for r in range(64)]
+    return x
+
+
+def test_wave_transpose64_butterfly_is_the_transpose():
+    rng = np.random.default_rng(7)
+    for density in (0.5, 0.05, 0.95):
+        bits = rng.random((64, 64)) < density
+        rows = [sum(1 << c for c in range(64) if bits[r, c]) for r in range(64)]
+        out = _wave_transpose64_model(rows)
+        for r in range(64):
+            assert out[r] == sum(1 << j for j in range(64) if bits[j, r]), (density, r)
