@@ -436,6 +436,7 @@ def main():
     rows_kernel = {2: "k_rows", 3: "k_rows_w (k_rows_prep before it)",
                    4: "k_heavy_rows_t (every class heavy; k_ptrans before it, no k_rows)",
                    5: "k_heavy_rows_t then k_rows (timed from k_ptrans' start to k_rows' end)",
+                   6: "k_heavy_rows_t then k_rows_w (timed from k_ptrans' start to k_rows_w's end)",
                    }.get(info["ROWS_KERNEL"], "none")
     mt = eng.mfma_timing()
     host = eng.host_times()

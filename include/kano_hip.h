@@ -59,8 +59,8 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the list-based row kernel */
 #define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 2 k_rows, 3 k_rows_prep + k_rows_w
                                     (wide rows), 4 k_ptrans + k_heavy_rows_t (every class
-                                    heavy, k_rows not launched), 5 the same then k_rows;
-                                    0 none yet */
+                                    heavy, k_rows not launched), 5 the same then k_rows,
+                                    6 the same then k_rows_w; 0 none yet */
 #define KANO_INFO_ROWS_CUS 14   /* CUs the last matrix write's stream may use  */
 #define KANO_INFO_HEAVY_SEL 15  /* sum of |S(c)| over the heavy classes       */
 #define KANO_INFO_HEAVY_KERNEL 16 /* 0 none, 1 k_heavy_mc_or, 2 k_heavy_mc_mfma (split K), 3 k_heavy_gemm */

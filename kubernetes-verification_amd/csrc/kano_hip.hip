@@ -1573,8 +1573,11 @@ int launch_rows(kano_ctx* ctx) {
   }
   KLAUNCH();
   // (KANO_INFO_ROWS_KERNEL: 2 k_rows, 3 k_rows_prep + k_rows_w, 4 the heavy
-  // rows whole with no k_rows, 5 the heavy rows then k_rows)
-  ctx->rows_kernel = !rows_needed ? 4 : e0_rows == nullptr ? 5 : rows_wide_used ? 3 : 2;
+  // rows whole with no k_rows, 5 the heavy rows then k_rows, 6 the heavy rows
+  // then k_rows_w)
+  ctx->rows_kernel = !rows_needed ? 4
+                     : e0_rows == nullptr ? (rows_wide_used ? 6 : 5)
+                                          : (rows_wide_used ? 3 : 2);
   ctx->rows_timed = true;
   ctx->rows_time_pending[set] = true;
   ctx->rows_end_ev[set] = e1;

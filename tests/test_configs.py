@@ -368,9 +368,7 @@ def test_rows_variants_forced(name, tune, monkeypatch):
     r = eng.verify(gid, sys_row=0, shadow=True)
     check_verify(r, exp)
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
-    assert eng.info()["ROWS_KERNEL"] in (2, 3, 4, 5)
-    if "rw=2" in tune and eng.info()["ROWS_KERNEL"] == 3:
-        pass                                    # (k_rows_w ran: alist path)
+    assert eng.info()["ROWS_KERNEL"] in (2, 3, 4, 5, 6)
     eng.build()
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     eng.close()
