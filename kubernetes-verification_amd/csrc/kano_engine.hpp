@@ -151,6 +151,7 @@ struct kano_ctx {
   int dx_on = 1;             // dx=0: never the dense path's bit matrices (k_*_dx); 2: always
   DBuf dx_sc, dx_sa;         // its SC (policy-major) and SA (class-indexed policy words)
   DBuf mct;                  // the heavy rows' McT (k_heavy_rows_t)
+  bool shg_prefilled = false;  // the grouped count's table cleared by the build's fills
   i64 dx_ldY = 0, dx_PBo = 0;
   bool dense_sel = false;    // this build takes them (do_front)
   int ac_lds = 1;            // aclds=0: AC / ACT bits by global atomics, not LDS rows

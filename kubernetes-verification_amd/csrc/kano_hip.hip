@@ -876,7 +876,7 @@ int do_front(kano_ctx* ctx, int path) {
                        P_<u64>(ctx->dx_sc), ldU, P, P_<u64>(ctx->dx_sa), ctx->dx_ldY, ctx->dx_PBo,
                        (const int32_t*)nullptr);
     KLAUNCH();
-    hipLaunchKernelGGL(k_cls_counts_dx, dim3(nblk(Ur, WPB)), dim3(TPB), 0, ctx->stream,
+    hipLaunchKernelGGL(k_cls_counts_dx, dim3((unsigned)Ur), dim3(TPB), 0, ctx->stream,
                        P_<u64>(ctx->dx_sa), ctx->dx_ldY, ctx->PB, Ur, P_<int32_t>(ctx->acnt),
                        P_<int32_t>(ctx->scnt), P_<unsigned long long>(ctx->cost));
     KLAUNCH();
@@ -2477,6 +2477,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->shadow_total = -1;
   ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
   ctx->sel_early_cap = -1;
+  ctx->shg_prefilled = false;   // (set by this build's shadow_prepare only)
   const i64 rl = rows_local(ctx);
   if (!ctx->defer_alloc)   // kano_build_classes: M is allocated on first use
     KTRY(dalloc(ctx, ctx->M, sizeof(u64) * std::max<i64>(1, rl * ctx->ldM)));
@@ -2771,6 +2772,12 @@ struct ShadowPlan {
   i64 U = 0, rl = 0, nf = 0, nt = 0;
 };
 
+i64 shg_table_size(i64 P) {
+  i64 Th = 64;
+  while (Th < 2 * P) Th <<= 1;
+  return Th;
+}
+
 int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
   sp.U = ctx->rc.U;
   sp.rl = rows_local(ctx);
@@ -2791,6 +2798,18 @@ int shadow_prepare(kano_ctx* ctx, ShadowPlan& sp, FillBatch& fb) {
     KTRY(dalloc(ctx, ctx->toff, sizeof(i64) * (sp.nt + 1)));
     KTRY(fb.add(ctx->tcnt, sizeof(i64) * sp.nt, 0u));   // accumulated
   }
+  if (ctx->vs_count_only && ctx->P > 0 && sp.U > 0) {
+    // the grouped count's hash table and error word, cleared with the build's
+    // fills (three runtime fills on the side stream cost it ~30 us at C4)
+    const i64 Th = shg_table_size(ctx->P);
+    KTRY(dalloc(ctx, ctx->shg_tkey, sizeof(u64) * Th));
+    KTRY(dalloc(ctx, ctx->shg_trep, sizeof(int32_t) * Th));
+    KTRY(dalloc(ctx, ctx->shg_err, sizeof(int32_t) * 4));
+    KTRY(fb.add(ctx->shg_tkey, sizeof(u64) * Th, 0xffffffffu));
+    KTRY(fb.add(ctx->shg_trep, sizeof(int32_t) * Th, 0x7f7f7f7fu));
+    KTRY(fb.add(ctx->shg_err, sizeof(int32_t) * 4, 0u));
+    ctx->shg_prefilled = true;
+  }
   return fb.add(ctx->T, sizeof(i64) * sp.U, 0u);
 }
 
@@ -2799,8 +2818,7 @@ int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   const i64 P = ctx->P, U = sp.U;
   ctx->shg_ran = false;
   if (P == 0 || U == 0) return 0;
-  i64 Th = 64;
-  while (Th < 2 * P) Th <<= 1;
+  const i64 Th = shg_table_size(P);
   const i64 GW = (SHG_MAX + 63) / 64;
   KTRY(dalloc(ctx, ctx->shg_h, sizeof(u64) * P));
   KTRY(dalloc(ctx, ctx->shg_tkey, sizeof(u64) * Th));
@@ -2812,9 +2830,12 @@ int shadow_group_launch(kano_ctx* ctx, const ShadowPlan& sp, hipStream_t st) {
   KTRY(dalloc(ctx, ctx->shg_reps, sizeof(int32_t) * SHG_MAX));
   KTRY(dalloc(ctx, ctx->shg_sub, sizeof(u64) * SHG_MAX * GW));
   KTRY(dalloc(ctx, ctx->shg_err, sizeof(int32_t) * 4));
-  KCHK(hipMemsetAsync(ctx->shg_tkey.p, 0xff, sizeof(u64) * Th, st));
-  KCHK(hipMemsetAsync(ctx->shg_trep.p, 0x7f, sizeof(int32_t) * Th, st));
-  KCHK(hipMemsetAsync(ctx->shg_err.p, 0, sizeof(int32_t) * 4, st));
+  if (!ctx->shg_prefilled) {
+    KCHK(hipMemsetAsync(ctx->shg_tkey.p, 0xff, sizeof(u64) * Th, st));
+    KCHK(hipMemsetAsync(ctx->shg_trep.p, 0x7f, sizeof(int32_t) * Th, st));
+    KCHK(hipMemsetAsync(ctx->shg_err.p, 0, sizeof(int32_t) * 4, st));
+  }
+  ctx->shg_prefilled = false;
   const u64* AC = P_<u64>(ctx->AC);
   hipLaunchKernelGGL(k_shg_hash, dim3(nblk(P, WPB)), dim3(TPB), 0, st, P, AC, ctx->ldC, ctx->UAW,
                      P_<u64>(ctx->shg_h));

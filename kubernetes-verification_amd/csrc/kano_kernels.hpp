@@ -1139,31 +1139,31 @@ __global__ __launch_bounds__(TPB) void k_ptrans(const u64* __restrict__ X, i64 l
   if (c < ldY) Y[pw * ldY + c] = y;
 }
 
-// |S(c)| and the rebuild cost sum_{p in S(c)} |allowed pods(p)|, one wave per
-// class over SA's column c
+// |S(c)| and the rebuild cost sum_{p in S(c)} |allowed pods(p)|, one block
+// per class over SA's column c, a policy word a thread (C4's 100 classes: a
+// wave per class walked ~500 set bits a lane, 48-68 us)
 __global__ __launch_bounds__(TPB) void k_cls_counts_dx(const u64* __restrict__ SA, i64 ldY,
                                                        i64 PB, i64 U,
                                                        const int32_t* __restrict__ acnt,
                                                        int32_t* __restrict__ scnt,
                                                        unsigned long long* __restrict__ cost) {
-  const int lane = threadIdx.x & 63;
-  const i64 c = (i64)blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (c >= U) return;
-  i64 cnt = 0;
-  unsigned long long cs = 0ull;
-  for (i64 pw = lane; pw < PB; pw += 64) {
+  __shared__ i64 sm[4];
+  const i64 c = blockIdx.x;
+  if (c >= U) return;                               // block-uniform
+  i64 cnt = 0, cs = 0;
+  for (i64 pw = threadIdx.x; pw < PB; pw += TPB) {
     u64 w = SA[pw * ldY + c];
     cnt += __popcll(w);
     while (w) {
-      cs += (unsigned long long)(int32_t)acnt[pw * 64 + __builtin_ctzll(w)];
+      cs += acnt[pw * 64 + __builtin_ctzll(w)];
       w &= w - 1;
     }
   }
-  cnt = wave_sum(cnt);
-  cs = wave_sum(cs);
-  if (lane == 0) {
+  cnt = block_sum(cnt, sm);
+  cs = block_sum(cs, sm);
+  if (threadIdx.x == 0) {
     scnt[c] = (int32_t)cnt;
-    cost[c] = cs;
+    cost[c] = (unsigned long long)cs;
   }
 }
 
@@ -2983,12 +2983,20 @@ __global__ __launch_bounds__(TPB) void k_shg_insert(i64 P, const u64* __restrict
   if (p >= P) return;
   const unsigned long long key = h[p];
   uint32_t s = (uint32_t)(key ^ (key >> 29)) & tmask;
+  // (a read before the CAS and the min: C4's 10^4 policies fall into ~10^2
+  // groups, and every atomic on a taken slot serialised behind the others)
   for (;;) {
-    const unsigned long long prev = atomicCAS(&tkey[s], ~0ull, key);
-    if (prev == ~0ull || prev == key) break;
+    const unsigned long long cur = __hip_atomic_load(&tkey[s], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) break;
+    if (cur == ~0ull) {
+      const unsigned long long prev = atomicCAS(&tkey[s], ~0ull, key);
+      if (prev == ~0ull || prev == key) break;
+    }
     s = (s + 1) & tmask;
   }
-  atomicMin(&trep[s], (int32_t)p);
+  if (__hip_atomic_load(&trep[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (int32_t)p)
+    atomicMin(&trep[s], (int32_t)p);
   slot_of[p] = (int32_t)s;
 }
 
