@@ -610,7 +610,13 @@ int classify_phase2a(kano_ctx* ctx, hipEvent_t mark = nullptr, bool* marked = nu
   const i64 mr = ctx->rc.m1 - ctx->rc.m0, ma = ctx->cc.m1 - ctx->cc.m0;
   const i64 rl = std::max(mr, ma);
   if (rl > 0) {   // ids and member counts in one pass
-    hipLaunchKernelGGL(k_cls_assign_count, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, pr);
+    // (several pods a thread when the previous build had few classes; the
+    // kernel is correct for any count -- a full LDS table goes global)
+    const i64 prevU = std::max(ctx->rc.U, ctx->cc.U);
+    const int ipt = ctx->assign_ipt > 0 ? ctx->assign_ipt
+                                        : (prevU > 0 && prevU <= 1024 ? ASSIGN_IPT : 1);
+    hipLaunchKernelGGL(k_cls_assign_count, dim3(nblk(rl, (i64)TPB * ipt), 2), dim3(TPB), 0,
+                       ctx->stream, pr, ipt);
     KLAUNCH();
   }
   ScanBatch sb(ctx);
@@ -1956,6 +1962,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "store") ctx->rows_plain = v == 0;
         if (k == "rw" && v >= 0 && v <= 2) ctx->rows_wide = v;   // 2: at every width
         if (k == "rwg" && v >= 0) ctx->rows_w_grid = v;
+        if (k == "aipt" && v >= 0 && v <= ASSIGN_IPT) ctx->assign_ipt = v;
         if (k == "sww" && v >= 1 && v <= SORT_LDS_WW) ctx->sort_ww = v;
         if (k == "cww" && v >= 16 && v <= MAX_CWW_KNOB && v % 16 == 0) ctx->rows_cww = v;
         if (k == "rch" && v >= 1 && v <= 1024) ctx->rows_ch = v;

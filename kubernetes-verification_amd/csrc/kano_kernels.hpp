@@ -253,10 +253,14 @@ __global__ __launch_bounds__(TPB) void k_cls_insert(const int32_t* __restrict__ 
 
 // k_cls_assign and k_cls_mcount in one pass: the class id of every pod of
 // [m0, m1), the representatives, the member counts
-__global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
+// ipt pods a thread (<= ASSIGN_IPT): with few classes (C4: ~100 row and
+// ~160 column classes) the per-block reservations still put ~300 global
+// atomics on each class counter; ipt blocks' worth of pods per block cut them
+// ipt-fold.  A pod whose class finds the LDS table full takes its place with a
+// global atomic of its own (the table then never needs to hold every class).
+constexpr int ASSIGN_IPT = 8;
+__global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr, int ipt) {
   const ClsSide a = blockIdx.y ? pr.s[1] : pr.s[0];
-  const i64 i = a.m0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  const bool act = i < a.m1;
   // the block's pods are counted per class in LDS; one atomic per distinct
   // class per block reserves the block's places in the class's member list
   // (the counter's old value + the pod's LDS rank is its place: k_cls_mfill
@@ -267,30 +271,43 @@ __global__ __launch_bounds__(TPB) void k_cls_assign_count(ClsPair pr) {
     lcnt[t] = 0;
   }
   __syncthreads();
-  int32_t c = 0, t = -1, r = 0;
-  bool lead = false;
-  if (act) {
+  int32_t cs[ASSIGN_IPT], ts[ASSIGN_IPT], rs[ASSIGN_IPT];
+  bool lead[ASSIGN_IPT];
+  const i64 i0 = a.m0 + (i64)blockIdx.x * TPB * ipt + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < ASSIGN_IPT; ++k) {
+    ts[k] = -2;                                     // -2: no pod
+    lead[k] = false;
+    const i64 i = i0 + (i64)k * TPB;
+    if (k >= ipt || i >= a.m1) continue;
     const int32_t sl = a.slot_of[i];
     const int32_t rp = a.pbits ? (int32_t)(reinterpret_cast<const u64*>(a.table)[sl] &
                                            ((1ull << a.pbits) - 1ull))
                                : a.smin[sl];
-    c = a.cid[rp - a.m0];
+    const int32_t c = a.cid[rp - a.m0];
+    cs[k] = c;
     a.cls[i] = c;
     if (rp == (int32_t)i) a.rep[c] = (int32_t)i;
     uint32_t h = hfin(hmix(0x2545f491u, (uint32_t)c)) & (CLS_LDS - 1);
-    for (;;) {
+    int t = -1;
+    for (int probe = 0; probe < CLS_LDS; ++probe) {
       const int32_t prev = atomicCAS(&lkey[h], -1, c);
-      if (prev == -1) { lead = true; break; }
-      if (prev == c) break;
+      if (prev == -1) { lead[k] = true; t = (int)h; break; }
+      if (prev == c) { t = (int)h; break; }
       h = (h + 1) & (CLS_LDS - 1);
     }
-    t = (int)h;
-    r = atomicAdd(&lcnt[t], 1);
+    ts[k] = t;
+    if (t >= 0) rs[k] = atomicAdd(&lcnt[t], 1);
+    else a.mcur[i - a.m0] = atomicAdd(&a.mcnt[c], 1);   // (the table is full)
   }
   __syncthreads();
-  if (lead) lbase[t] = atomicAdd(&a.mcnt[c], lcnt[t]);
+#pragma unroll
+  for (int k = 0; k < ASSIGN_IPT; ++k)
+    if (lead[k]) lbase[ts[k]] = atomicAdd(&a.mcnt[cs[k]], lcnt[ts[k]]);
   __syncthreads();
-  if (act) a.mcur[i - a.m0] = lbase[t] + r;
+#pragma unroll
+  for (int k = 0; k < ASSIGN_IPT; ++k)
+    if (ts[k] >= 0) a.mcur[i0 + (i64)k * TPB - a.m0] = lbase[ts[k]] + rs[k];
 }
 
 
