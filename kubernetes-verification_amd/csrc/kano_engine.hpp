@@ -127,6 +127,7 @@ struct kano_ctx {
   DBuf slist_tmp;            // k_class_lists' windowed sort of long S(c) lists (P > 49k)
   int sort_ww = 768;         // sww: that sort's window (bitmap words per wave, <= SORT_LDS_WW)
   i64 rows_w_grid = 0;       // rwg: k_rows_w's persistent grid (0: one block per CU slot)
+  int rows_early_heavy = 2;  // rheavy: with heavy classes the write starts after their Mc, not the tail (0: never, 1: always, 2: wide rows)
   int assign_ipt = 0;        // aipt: pods a thread in k_cls_assign_count (0: by class count)
   int async_rows = 1;        // async=0: kano_verify waits for its matrix write
   int shadow_count_mode = 0; // shcount=1|2: count-only policy_shadow pairwise | grouped

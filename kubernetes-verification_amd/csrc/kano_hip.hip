@@ -1370,6 +1370,18 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         ctx->mfma_ops_last = 2.0 * (double)H * (double)P * (double)ctx->cc.U;
       }
     }
+    // (the heavy rows' Mc was the write's last input: kano_verify's write
+    // may start here, beside the crosscheck pass and the tail -- C5's 5 ms
+    // PCIe copy of the pairs, until now in front of a 19 ms write).  rheavy=2
+    // (default): only for a wide-row write; C3's 0.35 ms write beside the
+    // tail measured 1% slower (profiles/r05_c5_rheavy_ab)
+    const bool early = ctx->rows_early_heavy == 1 ||
+                       (ctx->rows_early_heavy == 2 &&
+                        std::min<i64>(ctx->ldM, ctx->rows_cww) > 4096);
+    if (early && ctx->cols_deferred && !ctx->rin_marked) {
+      KCHK(hipEventRecord(ctx->ev_rin_e, ctx->stream));
+      ctx->rin_marked = true;
+    }
   }
   if (!ctx->cols_deferred) KTRY(mc_cols(ctx));
   // kano_verify's side stream forks from the lists (ev_fork2)
@@ -1962,6 +1974,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "store") ctx->rows_plain = v == 0;
         if (k == "rw" && v >= 0 && v <= 2) ctx->rows_wide = v;   // 2: at every width
         if (k == "rwg" && v >= 0) ctx->rows_w_grid = v;
+        if (k == "rheavy" && v >= 0 && v <= 2) ctx->rows_early_heavy = v;
         if (k == "aipt" && v >= 0 && v <= ASSIGN_IPT) ctx->assign_ipt = v;
         if (k == "sww" && v >= 1 && v <= SORT_LDS_WW) ctx->sort_ww = v;
         if (k == "cww" && v >= 16 && v <= MAX_CWW_KNOB && v % 16 == 0) ctx->rows_cww = v;
