@@ -3230,13 +3230,39 @@ __global__ __launch_bounds__(TPB) void k_shadow_emit(const int32_t* __restrict__
                                                      const i64* __restrict__ poff,
                                                      int2* __restrict__ out, i64 out_cap,
                                                      const i64* __restrict__ L_total, i64 L_cap) {
-  const i64 i = r0 + (i64)blockIdx.x * TPB + threadIdx.x;
-  if (i >= r1) return;
+  // a wave per 64 consecutive pods, whose pairs are one contiguous range of
+  // out: lane q of each 64-pair step finds its pod (the last lane whose
+  // offset is <= q: pods with no pairs share the next one's offset) by a
+  // binary search over the lanes' offsets, so loads and stores are
+  // coalesced (a thread walking its own pod's list wrote 64 streams a wave:
+  // 4.2 ms for C5's 33M pairs)
+  const int lane = threadIdx.x & 63;
+  const i64 wb = r0 + ((i64)blockIdx.x * TPB + threadIdx.x - lane);
+  if (wb >= r1) return;
   if (poff[r1 - r0] > out_cap || (L_total && *L_total > L_cap)) return;   // as k_shadow_compact
-  const int32_t c = cls[i];
-  const i64 l0 = loff[c], len = loff[c + 1] - l0;
-  const i64 o = poff[i - r0];
-  for (i64 k = 0; k < len; ++k) out[o + k] = L[l0 + k];
+  const i64 we = min(wb + 64, r1), i = wb + lane;
+  const i64 ob = poff[wb - r0], oe = poff[we - r0];
+  i64 l0 = 0, o = oe;
+  if (i < we) {
+    l0 = loff[cls[i]];
+    o = poff[i - r0];
+  }
+  if (oe - ob > (i64)INT32_MAX) {   // (past 2^31 pairs a wave: each lane its own list)
+    if (i < we)
+      for (i64 k = 0, len = poff[i + 1 - r0] - o; k < len; ++k) out[o + k] = L[l0 + k];
+    return;
+  }
+  const int rel = (int)(o - ob), tot = (int)(oe - ob);
+  for (int q0 = 0; q0 < tot; q0 += 64) {
+    const int q = q0 + lane;
+    int j = 0;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1)
+      if (__shfl(rel, j + s, 64) <= q) j += s;
+    const int rj = __shfl(rel, j, 64);
+    const i64 lj = __shfl(l0, j, 64);
+    if (q < tot) out[ob + q] = L[lj + (q - rj)];
+  }
 }
 
 // ===========================================================================
