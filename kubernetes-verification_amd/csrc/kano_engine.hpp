@@ -228,8 +228,6 @@ struct kano_ctx {
   std::vector<uint8_t> dead;       // P + inc_A entries
   bool user_edited = false;        // put_rows / set_bit / import: removal cannot rewrite rows
   i64 shadow_total = -1;
-  int host_emit = 0;            // hemit: kano_verify emits the pairs into the caller's pinned buffer
-  bool shadow_on_host = false;  // ... and the device buffer does not hold them (kano_shadow_fetch re-emits)
   // policy_shadow count-only (kano_verify with shadow_cap < 0): the grouped
   // count (k_shg_*) instead of the pair-by-pair flags
   bool vs_count_only = false;

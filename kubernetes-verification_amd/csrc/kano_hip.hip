@@ -1975,7 +1975,6 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "rw" && v >= 0 && v <= 2) ctx->rows_wide = v;   // 2: at every width
         if (k == "rwg" && v >= 0) ctx->rows_w_grid = v;
         if (k == "rheavy" && v >= 0 && v <= 2) ctx->rows_early_heavy = v;
-        if (k == "hemit") ctx->host_emit = v != 0;
         if (k == "aipt" && v >= 0 && v <= ASSIGN_IPT) ctx->assign_ipt = v;
         if (k == "sww" && v >= 1 && v <= SORT_LDS_WW) ctx->sort_ww = v;
         if (k == "cww" && v >= 16 && v <= MAX_CWW_KNOB && v % 16 == 0) ctx->rows_cww = v;
@@ -2496,7 +2495,6 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   ctx->rows_dirty = false;
   ctx->cols_valid = false;
   ctx->shadow_total = -1;
-  ctx->shadow_on_host = false;
   ctx->sig_armed = 0;   // the syncs below wait on this build's scans only
   ctx->sel_early_cap = -1;
   ctx->shg_prefilled = false;   // (set by this build's shadow_prepare only)
@@ -3029,7 +3027,6 @@ int shadow_back(kano_ctx* ctx, i64 nl, i64 total, hipStream_t st = nullptr) {
   }
   KTRY(stage_mark(ctx, 6, st));
   ctx->shadow_total = total;
-  ctx->shadow_on_host = false;
   return 0;
 }
 
@@ -3053,17 +3050,6 @@ int kano_shadow_fetch(kano_ctx* ctx, int32_t* pairs) {
   if (ctx->shadow_total < 0) return fail(ctx, -EINVAL, "kano_shadow_fetch before kano_shadow");
   if (ctx->shadow_total > 0) {
     if (!pairs) return fail(ctx, -EINVAL, "kano_shadow_fetch: NULL buffer");
-    if (ctx->shadow_on_host) {
-      // (kano_verify emitted the pairs into its caller's buffer: again here)
-      const i64 total = ctx->shadow_total;
-      KTRY(dalloc(ctx, ctx->out, sizeof(int2) * total));
-      hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rows_local(ctx))), dim3(TPB), 0, ctx->stream,
-                         P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
-                         P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out), total,
-                         (const i64*)nullptr, ctx->nflags);
-      KLAUNCH();
-      ctx->shadow_on_host = false;
-    }
     KCHK(hipMemcpyAsync(pairs, ctx->out.p, sizeof(int2) * ctx->shadow_total,
                         hipMemcpyDeviceToHost, ctx->stream));
   }
@@ -3431,10 +3417,6 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
   const i64 nf = ctx->nflags, nt = (nf + SH_TILE - 1) / SH_TILE;
   i64 out_cap = 0;
   const bool pairs_job = pairs_mode && pairs_h && rl > 0;
-  // hemit: the emission stores the pairs into the caller's pinned buffer
-  // itself (link-bound, as the copy was), not into HBM for a copy after it
-  const bool hemit = pairs_job && ctx->host_emit;
-  ctx->shadow_on_host = false;
   const u64* tots = P_<u64>(ctx->sizes) + SZ_IDX0;
   if (fused) {
     // the lists travel first, while policy_shadow's tail still runs on
@@ -3464,9 +3446,7 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
     if (rl > 0) {
       hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
                          P_<int32_t>(ctx->rc.cls), ctx->r0, ctx->r1, P_<i64>(ctx->loff),
-                         P_<int2>(ctx->L), P_<i64>(ctx->poff),
-                         hemit ? static_cast<int2*>(pairs_h) : P_<int2>(ctx->out),
-                         hemit ? shadow_cap : out_cap,
+                         P_<int2>(ctx->L), P_<i64>(ctx->poff), P_<int2>(ctx->out), out_cap,
                          nt > 0 ? P_<i64>(ctx->toff) + nt : (const i64*)nullptr, nf);
       KLAUNCH();
     }
@@ -3480,7 +3460,7 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
   if (!fused)
     cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->idxd.p), static_cast<char*>(idx_h),
                             tots, 4, nullptr, 0, 4, 4 * n};
-  if (pairs_job && !hemit) {
+  if (pairs_job) {
     cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->out.p), static_cast<char*>(pairs_h),
                             reinterpret_cast<const u64*>(P_<i64>(ctx->poff) + rl), 1, nullptr, 0,
                             8, std::min<i64>(shadow_cap, out_cap)};
@@ -3521,10 +3501,8 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
     const i64 total = v[SZ_PAIRS - SZ_NL];
     *shadow_count = total;
     ctx->shadow_total = pairs_mode ? total : -1;
-    if (hemit && total <= shadow_cap) ctx->shadow_on_host = true;
-    if (pairs_mode && total > (hemit ? shadow_cap : out_cap)) {
-      // past the emission buffer: the sized emission, then the copy (kept
-      // on the device for kano_shadow_fetch when it is past shadow_cap)
+    if (pairs_mode && total > out_cap) {
+      // past the emission buffer: the sized emission, then the copy
       KTRY(dalloc(ctx, ctx->out, sizeof(int2) * (total + total / 4)));
       if (rl > 0) {
         hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
@@ -3676,12 +3654,10 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
       KTRY(shadow_back(ctx, v[0], total, cs));
       part(13);
       ctx->shadow_total = total;
-      ctx->shadow_on_host = false;
     } else {
       // count only: every subset test ran (the flags and the per-pod counts
       // above); the pairs are neither compacted nor emitted (C4: ~1e11)
       ctx->shadow_total = -1;
-      ctx->shadow_on_host = false;
     }
     *shadow_count = total;
   }

@@ -343,7 +343,7 @@ def _lists(cs, which):
                                   "hexplds=0", "hexplds=1", "hexplds=3", "hexplds=4", "dx=2", "aclds=0", "rch=3",
                                   "rch=64,cww=16384", "shr=4", "shr=8", "rw=2", "rw=2,rch=1",
                                   "rw=2,cww=16", "rw=2,rch=64,async=0", "rw=2,rwg=3",
-                                  "rw=2,rwg=1,rch=1", "sww=1", "sww=3", "aipt=8", "aipt=3", "rheavy=0", "rheavy=1", "hemit=1"])
+                                  "rw=2,rwg=1,rch=1", "sww=1", "sww=3", "aipt=8", "aipt=3", "rheavy=0", "rheavy=1"])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
     """The matrix write (k_rows) with non-temporal and plain stores, in the

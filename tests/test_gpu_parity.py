@@ -275,41 +275,6 @@ def test_verify_async_completion(tune, monkeypatch):
     pin.close()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("tune", ["hemit=1", "hemit=0"])
-def test_verify_pairs_into_pinned_buffer_then_fetch(tune, monkeypatch):
-    """policy_shadow's pairs emitted straight into the caller's pinned buffer
-    (hemit, the default) or into HBM then copied (hemit=0): the returned pairs,
-    a kano_shadow_fetch after the call (the emission again, on the device),
-    and a buffer too small for them (the pairs then come from the device
-    through kano_shadow_fetch) all match kano_py's C2 record."""
-    monkeypatch.setenv("KANO_TUNE", tune)
-    from kano._engine import DeviceBuild, PinnedBuffer
-    from kano._intern import tables_from_cluster
-    from kano.synth import make_config, KEY_NAMES
-    exp = expected("C2")
-    cl = make_config("C2")
-    _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
-    eng = DeviceBuild(tables_from_cluster(cl), build=False)
-    eng.set_groups(gid)
-    want = exp["policy_shadow"]
-    k = want["count"]
-    assert k > 16
-    big = PinnedBuffer((k + 64) * 8)
-    small = PinnedBuffer(16 * 8)
-    for _ in range(2):
-        r = eng.verify("stored", sys_row=0, shadow=True, pairs=big.view(np.int32, 2 * (k + 64)))
-        assert r["shadow_count"] == k
-        assert sha(np.ascontiguousarray(r["pairs"])) == want["sha256"]
-        assert sha(np.ascontiguousarray(eng.shadow_fetch(k))) == want["sha256"]
-        r = eng.verify("stored", sys_row=0, shadow=True, pairs=small.view(np.int32, 32))
-        assert r["shadow_count"] == k
-        assert sha(np.ascontiguousarray(r["pairs"])) == want["sha256"]
-    eng.close()
-    big.close()
-    small.close()
-
-
 def test_verify_pairs_then_fetch():
     """policy_shadow's pairs returned by kano_verify, a kano_shadow_fetch after
     the call, and a buffer too small for them (the pairs then come from the
