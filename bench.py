@@ -466,8 +466,12 @@ def main():
     # the last step's results against kano_py's own outputs on this cluster
     # (tests/golden/expected/<config>.json); on row shards rank 0 checks the
     # combined column lists and the system row it owns
-    verified, vdetail = verify_against_golden(args.config, cl, step.results, world, rank,
-                                             args.rank_of, shadow)
+    if args.rank_of > 1:
+        verified, vdetail = verify_shard_alone(args.config, cl, tables, gid, eng, step.results,
+                                               r0, r1, shadow)
+    else:
+        verified, vdetail = verify_against_golden(args.config, cl, step.results, world, rank,
+                                                 args.rank_of, shadow)
     if dist is not None:
         t = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -776,6 +780,53 @@ def verify_against_golden(config, cl, res, world, rank, rank_of, shadow):
                       if shadow != "off" and world == 1 else "")
     who = exp.get("source", "kano_py on the same seeded cluster")
     return True, f"{src} ({who}): {what} equal"
+
+
+def verify_shard_alone(config, cl, tables, gid, eng, res, r0, r1, shadow):
+    """--rank-of N: what rank 0's shard can check without the other ranks'
+    words (the emulated gather leaves them zero, so its column lists are
+    partial).  After the timed region, one unsharded build of the same cluster
+    is verified against the record (verify_against_golden); then the shard's
+    rows must equal that build's rows [r0, r1) (per-row digests), its
+    policy_shadow pairs the full list's first ones (pairs are emitted per pod
+    in row order, algorithm.py:58-80, and rank 0 holds rows from 0), and its
+    system_isolation(0) list the record's (row 0 is rank 0's)."""
+    from kano._engine import DeviceBuild
+    assert r0 == 0
+    shard = {k: np.array(v, copy=True) for k, v in res.items()
+             if v is not None and hasattr(v, "__len__")}
+    cnt = int(res.get("policy_shadow_count", -1))
+    full = DeviceBuild(tables, build=False)
+    try:
+        fr = full.verify(gid, sys_row=0, shadow=shadow != "off",
+                         shadow_count_only=shadow == "count")
+        fres = {k: fr[k] for k in ("all_reachable", "all_isolated", "user_crosscheck",
+                                   "system_isolation")}
+        if shadow != "off":
+            fres["policy_shadow"] = fr["pairs"]
+            fres["policy_shadow_count"] = fr["shadow_count"]
+        ok, detail = verify_against_golden(config, cl, fres, 1, 0, 0, shadow)
+        if ok is not True:
+            return ok, "unsharded build: " + detail
+        bad = []
+        if not np.array_equal(eng.rows_digest(r0, r1 - r0), full.rows_digest(r0, r1 - r0)):
+            bad.append("row digests")
+        if not _list_ok(shard.get("system_isolation", []), fres["system_isolation"]):
+            bad.append("system_isolation")
+        if shadow == "pairs":
+            fp = np.asarray(fres["policy_shadow"], np.int32).reshape(-1, 2)
+            sp = np.asarray(shard["policy_shadow"], np.int32).reshape(-1, 2)
+            if cnt > fp.shape[0] or not np.array_equal(sp[:cnt], fp[:cnt]):
+                bad.append("policy_shadow pairs")
+    finally:
+        full.close()
+    if bad:
+        return False, f"rank 0 of the shards: {', '.join(bad)} differ from the unsharded build"
+    what = "row digests, system_isolation" + (", policy_shadow pairs (prefix of the full list)"
+                                              if shadow == "pairs" else "")
+    return True, (f"rank 0's shard [{r0}, {r1}) against an unsharded build verified by "
+                  f"{detail}: {what} equal (the column lists need every rank's words: not "
+                  "checked here)")
 
 
 def kano_py_measured(config):

@@ -66,7 +66,7 @@ struct ClassSet {
 // One side of the policies (working selector or working allow): terms sorted
 // by class-key slot, the distinct slot sets ("masks") and, after matching,
 // each policy's class list pcls[pstart[p] .. + plen[p]).
-// What the matrix write reads (launch_rows: k_heavy_expand, k_rows) -- held
+// What the matrix write reads (launch_rows: k_heavy_rows_t, k_rows) -- held
 // twice: back-to-back kano_verify calls build into one set while the previous
 // call's k_rows still reads the other (swap_rows_inputs)
 struct RowsInputs {
@@ -119,8 +119,6 @@ struct kano_ctx {
   // shipped forms that compute the same results; none changes a result.
   int stage_timing = 0;      // timing=1: the stage events of kano_stage_times (slots 0-5)
   int cls_packed = 1;        // packed=0: classification without packed keys (the wide-key form)
-  int cls_podword = 1;       // podword=0: packed slots without the member (the smin form)
-  int rows_plain = 0;        // store=0: k_rows with plain stores (non-temporal by default)
   int rows_wide = 1;         // rw=0: wide row chunks through k_rows, not k_rows_prep + k_rows_w
                              // (rw=2: k_rows_w at every chunk width -- the parity variants)
   DBuf rw_items, rw_segs, rw_ticket;  // k_rows_prep's work-item descriptors, S(c) segments
@@ -147,9 +145,7 @@ struct kano_ctx {
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int heavy_expand_lds = 2;  // hexplds: heavy rows by wave transposes (k_heavy_rows_t):
                              // every member row (3), the first member's with k_rows
-                             // copying it (4), or by class size (2); the first row
-                             // by LDS gathers (1, k_heavy_expand_w) or from global
-                             // memory (0), k_rows copying it
+                             // copying it (4), or by class size (2)
   int dx_on = 1;             // dx=0: never the dense path's bit matrices (k_*_dx); 2: always
   DBuf dx_sc, dx_sa;         // its SC (policy-major) and SA (class-indexed policy words)
   DBuf mct;                  // the heavy rows' McT (k_heavy_rows_t)

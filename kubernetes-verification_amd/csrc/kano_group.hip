@@ -195,6 +195,9 @@ struct kano_group {
   i64 idx_n = -1;
   Pool pool;
   std::atomic<int> failed{0};         // a member's step failed (inside one job)
+  // an update that reached some members and not others: the shards hold
+  // different policy lists, so every later call refuses until a new upload
+  std::string poisoned;
   // the verify exchange's time on member 0's stream (kano_group_exchange_timing)
   bool xtime_on = false;
   bool xtime_pending = false;
@@ -213,6 +216,12 @@ namespace {
 int gfail(kano_group* g, int code, const std::string& msg) {
   g->err = msg;
   return code;
+}
+
+// calls on a group whose members diverged (a partial update) fail loudly
+int group_usable(kano_group* g) {
+  if (g->poisoned.empty()) return 0;
+  return gfail(g, -EPROTO, g->poisoned + "; upload the tables again (kano_group_upload)");
 }
 
 // f(r) on every member's worker; the first error wins
@@ -247,7 +256,9 @@ int member_exchange(kano_group* g, int r, int rc, const std::vector<void*>& send
   }
   g->pool.bar.wait();
   if (g->failed.load()) return rc ? rc : -ECANCELED;
-  if (timed && r == 0 && nw > 0) (void)hipEventRecord(g->xt0, st);
+  // (the timing events live on member 0's device: kano_group_create makes
+  // them there; a failed record leaves this call untimed, never half-timed)
+  const bool timing = timed && r == 0 && nw > 0 && hipEventRecord(g->xt0, st) == hipSuccess;
   if (nw > 0 && g->mode == 1) {
     // one thread issues the grouped all-gather over every communicator
     if (r == 0) {
@@ -276,10 +287,7 @@ int member_exchange(kano_group* g, int r, int rc, const std::vector<void*>& send
       }
     }
   }
-  if (timed && r == 0 && nw > 0) {
-    (void)hipEventRecord(g->xt1, st);
-    g->xtime_pending = true;
-  }
+  if (timing && hipEventRecord(g->xt1, st) == hipSuccess) g->xtime_pending = true;
   g->pool.bar.wait();
   if (g->failed.load()) return rc ? rc : -ECANCELED;
   return 0;
@@ -432,7 +440,10 @@ static int group_create(int ngpu, const int* devices, int flags, kano_group** ou
     if (g->pool.rc[(size_t)r])
       return create_fail(g, cur, g->pool.rc[(size_t)r],
                          "kano_group_create: member " + std::to_string(r) + "'s context failed");
-  if (hipEventCreate(&g->xt0) != hipSuccess || hipEventCreate(&g->xt1) != hipSuccess)
+  // the exchange-timing events on member 0's device (they are recorded on its
+  // stream), whatever the calling thread's current device
+  if (hipSetDevice(g->dev[0]) != hipSuccess || hipEventCreate(&g->xt0) != hipSuccess ||
+      hipEventCreate(&g->xt1) != hipSuccess)
     return create_fail(g, cur, -EIO, "kano_group_create: timing events");
   // the exchange: RCCL over xGMI (one communicator per device,
   // ncclCommInitAll) when the devices are distinct, or when asked for
@@ -443,7 +454,9 @@ static int group_create(int ngpu, const int* devices, int flags, kano_group** ou
   std::vector<int> sorted(g->dev);
   std::sort(sorted.begin(), sorted.end());
   const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  const bool copy = (flags & KANO_GROUP_COPY) || getenv("KANO_GROUP_COPY");
+  // (the environment is the Python layer's business: kano/multi.py passes
+  // KANO_GROUP_COPY / KANO_GROUP_RCCL through the flags)
+  const bool copy = flags & KANO_GROUP_COPY;
   const bool want = (flags & KANO_GROUP_RCCL) || (ngpu > 1 && distinct && !copy);
   if (want) {
     if (!distinct)
@@ -515,6 +528,7 @@ int kano_group_upload(kano_group* g, int64_t n, int32_t ncols, const int32_t* po
                       const int32_t* alw_col, const int32_t* alw_val, const int64_t* bounds) {
   if (!g) return -EINVAL;
   if (!bounds) return gfail(g, -EINVAL, "kano_group_upload: bounds NULL");
+  g->poisoned.clear();   // (every member's tables and policy list replaced)
   for (int r = 0; r < g->G; ++r)
     if (bounds[2 * r] < 0 || bounds[2 * r + 1] < bounds[2 * r] || bounds[2 * r + 1] > n)
       return gfail(g, -EINVAL, "kano_group_upload: bad row range of member " + std::to_string(r));
@@ -531,11 +545,13 @@ int kano_group_upload(kano_group* g, int64_t n, int32_t ncols, const int32_t* po
 
 int kano_group_build(kano_group* g, int path) {
   if (!g) return -EINVAL;
+  KANO_GROUP_TRY(group_usable(g));
   return group_each(g, [&](int r) { return kano_build(g->m[(size_t)r], path); });
 }
 
 int kano_group_set_groups(kano_group* g, const int32_t* gid, int32_t ngroups) {
   if (!g) return -EINVAL;
+  KANO_GROUP_TRY(group_usable(g));
   return group_each(g, [&](int r) { return kano_set_groups(g->m[(size_t)r], gid, ngroups); });
 }
 
@@ -544,6 +560,7 @@ int kano_group_verify(kano_group* g, int path, const int32_t* gid, int32_t ngrou
                       int32_t* shadow_pairs, int64_t shadow_cap, int64_t* shadow_count) {
   if (!g) return -EINVAL;
   if (!counts || !idx) return gfail(g, -EINVAL, "kano_group_verify: idx / counts NULL");
+  KANO_GROUP_TRY(group_usable(g));
   if (with_shadow && !shadow_count)
     return gfail(g, -EINVAL, "kano_group_verify: shadow_count NULL with with_shadow");
   KANO_GROUP_TRY(group_buffers(g));
@@ -599,6 +616,7 @@ int kano_group_checks(kano_group* g, const int32_t* gid, int32_t ngroups, int64_
                       int32_t* idx, int64_t* counts) {
   if (!g) return -EINVAL;
   if (!counts || !idx) return gfail(g, -EINVAL, "kano_group_checks: idx / counts NULL");
+  KANO_GROUP_TRY(group_usable(g));
   KANO_GROUP_TRY(group_buffers(g));
   std::vector<std::array<int64_t, 4>> cnt((size_t)g->G);
   KANO_GROUP_TRY(group_each(g, [&](int r) {
@@ -634,21 +652,46 @@ int kano_group_add_policies(kano_group* g, int64_t Pn, int32_t ncols_x, const in
                             const int32_t* sel_val, const int64_t* alw_off,
                             const int32_t* alw_col, const int32_t* alw_val, int64_t* first_id) {
   if (!g) return -EINVAL;
+  KANO_GROUP_TRY(group_usable(g));
   std::vector<int64_t> first((size_t)g->G, -1);
-  KANO_GROUP_TRY(group_each(g, [&](int r) {
+  const int rc = group_each(g, [&](int r) {
     return kano_add_policies(g->m[(size_t)r], Pn, ncols_x, xval, sel_off, sel_col, sel_val,
                              alw_off, alw_col, alw_val, &first[(size_t)r]);
-  }));
+  });
+  // members apply the update independently: one that failed while others
+  // succeeded leaves the shards on different policy lists
+  const auto partial = [&](const std::string& why) {
+    bool any = false;
+    for (int r = 0; r < g->G; ++r) any |= first[(size_t)r] >= 0;
+    if (any) g->poisoned = "kano_group: a partial kano_group_add_policies (" + why + ")";
+  };
+  if (rc) {
+    const std::string why = g->err;
+    partial(why);
+    g->err = why;
+    return rc;
+  }
   for (int r = 1; r < g->G; ++r)
-    if (first[(size_t)r] != first[0])
+    if (first[(size_t)r] != first[0]) {
+      partial("the members' policy ids diverged");
       return gfail(g, -EPROTO, "kano_group_add_policies: the members' policy ids diverged");
+    }
   if (first_id) *first_id = first[0];
   return 0;
 }
 
 int kano_group_remove_policies(kano_group* g, int64_t count, const int64_t* ids) {
   if (!g) return -EINVAL;
-  return group_each(g, [&](int r) { return kano_remove_policies(g->m[(size_t)r], count, ids); });
+  KANO_GROUP_TRY(group_usable(g));
+  std::vector<int> done((size_t)g->G, 0);
+  const int rc = group_each(g, [&](int r) {
+    const int rc1 = kano_remove_policies(g->m[(size_t)r], count, ids);
+    done[(size_t)r] = rc1 == 0;
+    return rc1;
+  });
+  if (rc && std::find(done.begin(), done.end(), 1) != done.end())
+    g->poisoned = "kano_group: a partial kano_group_remove_policies (" + g->err + ")";
+  return rc;
 }
 
 // kubesv's path relation (kubesv/kubesv/constraint.py:233-237) over the
@@ -662,6 +705,8 @@ int kano_group_path(kano_group* src, kano_group* dst, int hops, int mode, int64_
   if (!src || !dst || src == dst) return -EINVAL;
   if (dst->G != src->G || dst->dev != src->dev)
     return gfail(src, -EINVAL, "kano_group_path: the groups' devices differ");
+  KANO_GROUP_TRY(group_usable(src));
+  KANO_GROUP_TRY(group_usable(dst));
   const int G = src->G;
   std::vector<int64_t> nws((size_t)G, 0);
   KANO_GROUP_TRY(group_each(src, [&](int r) {
@@ -696,7 +741,12 @@ int kano_group_path(kano_group* src, kano_group* dst, int hops, int mode, int64_
     }
     return rc1;
   });
+  // cleanup: a member that failed after queuing its copies (mode 2) may still
+  // read the other members' recv buffers on its stream -- every member drains
+  // its own stream and meets the others before any buffer is freed
   group_each(src, [&](int r) {
+    (void)hipStreamSynchronize(kano_int::ctx_stream(src->m[(size_t)r]));
+    src->pool.bar.wait();
     if (recv[(size_t)r]) (void)hipFree(recv[(size_t)r]);
     return 0;
   });

@@ -519,7 +519,7 @@ i64 table_size(i64 n) {
 // slot inserts or finds its class and lowers the member in one atomic
 // round trip (no smin array); 0 when they do not fit (the smin form)
 int cls_pod_bits(const kano_ctx* ctx, const ClassSet& cs) {
-  if (!cs.packed || !ctx->cls_podword) return 0;
+  if (!cs.packed) return 0;
   int pb = 1;
   while (pb < 31 && ((i64)1 << pb) < ctx->n) ++pb;
   return cs.tbits + pb <= 63 ? pb : 0;
@@ -1259,15 +1259,9 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         hipLaunchKernelGGL(k_ptrans, dim3(nblk(PBp * ((ldB + 63) / 64), WPB)), dim3(TPB), 0,
                            ctx->stream, P_<u64>(ctx->AC), ctx->ldC, P, P_<u64>(ctx->ACT), ldB,
                            PBp, (const int32_t*)nullptr);
-      } else if (ctx->ac_lds && ldB * 8 <= 64 * 1024 + 2048) {
-        // (ACT rows through LDS, one block per 64 policies)
-        const i64 ns = std::min<i64>(8, std::max<i64>(1, 512 / std::max<i64>(1, ctx->PB)));
-        const i64 sw = (ldB + ns - 1) / ns;
-        hipLaunchKernelGGL(k_classbits_rows, dim3((unsigned)ctx->PB, (unsigned)ns), dim3(TPB),
-                           sizeof(u64) * (size_t)sw, ctx->stream, P_<i64>(ctx->am.pstart),
-                           P_<int32_t>(ctx->am.plen), P_<int32_t>(ctx->am.gmem), P, ldB, sw,
-                           P_<u64>(ctx->ACT));
       } else {
+        // (the contraction without the dense front end: forced, or past
+        // DX_MAX row classes)
         hipLaunchKernelGGL(k_classbits, dim3((unsigned)P), dim3(TPB), 0, ctx->stream,
                            P_<i64>(ctx->am.pstart), P_<int32_t>(ctx->am.plen),
                            P_<int32_t>(ctx->am.gmem), ldB, P_<u64>(ctx->ACT));
@@ -1473,9 +1467,7 @@ int launch_rows(kano_ctx* ctx) {
   bool heavy_whole = false, rows_needed = true, rows_wide_used = false;
   if (ctx->heavy_count > 0) {
     const i64 H = ctx->heavy_count, ldMc = ctx->ldC;
-    // nc classes' Mc rows in <= 32 KB of LDS (two blocks per CU), at most 64
-    const i64 nc = std::min<i64>(64, (32 * 1024) / (8 * std::max<i64>(1, ldMc)));
-    if (ctx->heavy_expand_lds >= 2) {
+    {
       // the heavy classes' first member rows (hexplds=3: every member row,
       // k_rows then skips them) from McT (k_ptrans of their Mc rows) by
       // wave transposes
@@ -1505,18 +1497,6 @@ int launch_rows(kano_ctx* ctx) {
       KLAUNCH();
       heavy_whole = whole;
       rows_needed = !last;
-    } else if (nc >= 1 && ctx->heavy_expand_lds) {
-      const i64 gy = (H + nc - 1) / nc, gx = (ldM + TPB - 1) / TPB;
-      hipLaunchKernelGGL(k_heavy_expand_w, dim3((unsigned)gx, (unsigned)gy), dim3(TPB),
-                         sizeof(u64) * (size_t)(nc * ldMc), rs, P_<int32_t>(ctx->hlist), H,
-                         (int)nc, P_<u64>(ctx->Mc), ldMc, P_<int32_t>(ctx->cc.cls), n,
-                         P_<int32_t>(ctx->rc.moff), P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M),
-                         ldM, ctx->r0);
-    } else {
-      hipLaunchKernelGGL(k_heavy_expand, dim3(nblk(ldM * 64), nblk(H, HEXP_CLS)), dim3(TPB), 0, rs,
-                         P_<int32_t>(ctx->hlist), H, P_<u64>(ctx->Mc), ldMc,
-                         P_<int32_t>(ctx->cc.cls), n, P_<int32_t>(ctx->rc.moff),
-                         P_<int32_t>(ctx->rc.mem), P_<u64>(ctx->M), ldM, ctx->r0);
     }
     KLAUNCH();
   }
@@ -1547,7 +1527,6 @@ int launch_rows(kano_ctx* ctx) {
   a.cww = cww;
   a.color = nullptr;  // column checks come from Mc
   a.colnand = nullptr;
-  a.plain = ctx->rows_plain;
   a.heavy_skip = heavy_whole ? 1 : 0;
   // wide chunks hold few blocks per CU (LDS): give those blocks more waves
   const int nt = cww > 4096 ? 1024 : (cww > 2048 ? 512 : 256);
@@ -1970,8 +1949,6 @@ int kano_create(int device, kano_ctx** out) {
         const int v = atoi(kv.c_str() + eq + 1);
         if (k == "timing") ctx->stage_timing = v;
         if (k == "packed") ctx->cls_packed = v;
-        if (k == "podword") ctx->cls_podword = v;
-        if (k == "store") ctx->rows_plain = v == 0;
         if (k == "rw" && v >= 0 && v <= 2) ctx->rows_wide = v;   // 2: at every width
         if (k == "rwg" && v >= 0) ctx->rows_w_grid = v;
         if (k == "rheavy" && v >= 0 && v <= 2) ctx->rows_early_heavy = v;
@@ -1993,7 +1970,7 @@ int kano_create(int device, kano_ctx** out) {
           ctx->heavy_gemm = v;
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
         if (k == "hortime") ctx->time_or = v;
-        if (k == "hexplds") ctx->heavy_expand_lds = v;
+        if (k == "hexplds" && v >= 2 && v <= 4) ctx->heavy_expand_lds = v;
         if (k == "dx") ctx->dx_on = v;
         if (k == "aclds") ctx->ac_lds = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
@@ -2036,8 +2013,6 @@ int kano_create(int device, kano_ctx** out) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_w<1024>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sizeof(u64) * MAX_CWW_KNOB);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_classbits_rows),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 8448);
   }
   mark("func_attributes");
   if (hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking) != hipSuccess) {

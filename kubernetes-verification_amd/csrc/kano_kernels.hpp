@@ -1070,7 +1070,6 @@ __global__ __launch_bounds__(TPB) void k_pol_counts(i64 P, const i64* __restrict
 // (round 4's k_pol_counts_dx / k_sel_place_dx put the 18M entries through
 // LDS class counters and cursors: 193 + 486 us at D1, plus a sort)
 constexpr int DX_MAX = 8192;
-constexpr int DX_UNROLL = 4;   // list loads in flight per lane (k_classbits_rows)
 constexpr int SR_UNROLL = 8;   // the same in k_selrows_dx
 __global__ __launch_bounds__(TPB) void k_selrows_dx(i64 P, const i64* __restrict__ apstart,
                                                     const int32_t* __restrict__ aplen,
@@ -1234,42 +1233,6 @@ __global__ __launch_bounds__(TPB) void k_sa_gather(const u64* __restrict__ SA, i
   if (i >= PBo * ldA) return;
   const i64 pw = i / ldA, h = i - pw * ldA;
   A[i] = h < H ? SA[pw * ldY + hlist[h]] : 0ull;
-}
-
-// ACT rows through LDS: block pb takes policies [64 pb, 64 pb + 64), ORs
-// each one's allowed classes into an LDS row of ld words, then stores the row
-// (every word once, no global atomics; the k_classbits form put ~2e7 global
-// atomics on ACT at D1).  Dynamic LDS: ld words (<= 8,448).
-// (blockIdx.y: a slice [c0, c0 + sw) of the row, so that PB blocks become
-// PB x gridDim.y -- each block reads every list of its 64 policies, keeps
-// the entries of its slice)
-__global__ __launch_bounds__(TPB) void k_classbits_rows(const i64* __restrict__ pstart,
-                                                        const int32_t* __restrict__ plen,
-                                                        const int32_t* __restrict__ pcls, i64 P,
-                                                        i64 ld, i64 sw, u64* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) u64 row[];
-  const i64 c0 = (i64)blockIdx.y * sw, c1 = min(ld, c0 + sw);
-  for (i64 w = threadIdx.x; w < c1 - c0; w += TPB) row[w] = 0ull;
-  __syncthreads();
-  const i64 pb = blockIdx.x;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int q = wv; q < 64; q += TPB / 64) {
-    const i64 p = pb * 64 + q;
-    if (p >= P) break;
-    const int32_t* L = pcls + pstart[p];
-    const int32_t len = plen[p];
-    // (the row is class-indexed, word ca of bit q: u64 atomics in LDS)
-    for (int32_t k0 = lane; k0 < len; k0 += 64 * DX_UNROLL) {
-      int32_t c[DX_UNROLL];
-#pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u) c[u] = k0 + 64 * u < len ? L[k0 + 64 * u] : -1;
-#pragma unroll
-      for (int u = 0; u < DX_UNROLL; ++u)
-        if (c[u] >= c0 && c[u] < c1) atomicOr(&row[c[u] - c0], 1ull << q);
-    }
-  }
-  __syncthreads();
-  for (i64 w = threadIdx.x; w < c1 - c0; w += TPB) out[pb * ld + c0 + w] = row[w];
 }
 
 // block per policy: allowed class list (alc) and its bits AC[p]
@@ -2028,96 +1991,6 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ 
     }
 }
 
-// expansion: M[first member of heavy class h] bit j = Mc[h][cla[j]]; one wave
-// per 64-pod word, the whole padded row is written.  A block takes HEXP_CLS
-// heavy classes (grid.y = ceil(H / HEXP_CLS)): the pods' column classes are
-// read once per block, not once per class (C5: 1,027 heavy classes x 1M pods)
-constexpr int HEXP_CLS = 16;
-__global__ __launch_bounds__(TPB) void k_heavy_expand(const int32_t* __restrict__ hlist, i64 H,
-                                                      const u64* __restrict__ Mc, i64 ldMc,
-                                                      const int32_t* __restrict__ cla, i64 n,
-                                                      const int32_t* __restrict__ moff,
-                                                      const int32_t* __restrict__ mem,
-                                                      u64* __restrict__ M, i64 ldM, i64 r0) {
-  const i64 j = (i64)blockIdx.x * TPB + threadIdx.x;
-  const i64 w = j >> 6;
-  if ((w << 6) >= ldM * 64) return;                 // wave-uniform
-  const int32_t ca = j < n ? cla[j] : -1;
-  const i64 h0 = (i64)blockIdx.y * HEXP_CLS;
-  const int nh = (int)min((i64)HEXP_CLS, H - h0);
-  for (int q = 0; q < nh; ++q) {
-    const int32_t c = hlist[h0 + q];
-    const bool bit = ca >= 0 && ((Mc[(i64)c * ldMc + (ca >> 6)] >> (ca & 63)) & 1ull);
-    const u64 bal = __ballot(bit);
-    if ((threadIdx.x & 63) == 0 && w < ldM) M[(i64)(mem[moff[c]] - r0) * ldM + w] = bal;
-  }
-}
-
-// The expansion with the Mc rows in LDS, lane = output word: a block stages
-// nc heavy classes' Mc rows (nc * ldMc words, dynamic LDS, read as 32-bit
-// halves), each thread owns one 64-pod word w of the rows: it loads its 64
-// pods' column classes once (16-byte loads, registers) and, per class,
-// gathers the 64 bits from LDS into one word, stored with the block's other
-// words (coalesced 512 B per wave).  D1 (8,000 heavy classes x 10^5 pods):
-// the lane-per-pod form above took 5.4 ms (a dependent load and a ballot per
-// class per pod, one 8-byte store per wave); grid = (word blocks, class
-// groups).
-__global__ __launch_bounds__(TPB) void k_heavy_expand_w(const int32_t* __restrict__ hlist, i64 H,
-                                                        int nc, const u64* __restrict__ Mc,
-                                                        i64 ldMc,
-                                                        const int32_t* __restrict__ cla, i64 n,
-                                                        const int32_t* __restrict__ moff,
-                                                        const int32_t* __restrict__ mem,
-                                                        u64* __restrict__ M, i64 ldM, i64 r0) {
-  extern __shared__ __attribute__((aligned(16))) u64 rowsM[];
-  __shared__ i64 dst[64];
-  const i64 h0 = (i64)blockIdx.y * nc;
-  const int nh = (int)min((i64)nc, H - h0);
-  for (int q = threadIdx.x; q < nh; q += TPB) {
-    const int32_t c = hlist[h0 + q];
-    dst[q] = (i64)(mem[moff[c]] - r0) * ldM;
-  }
-  for (i64 e = threadIdx.x; e < (i64)nh * ldMc; e += TPB) {
-    const i64 q = e / ldMc, w = e - q * ldMc;
-    rowsM[e] = Mc[(i64)hlist[h0 + q] * ldMc + w];
-  }
-  __syncthreads();
-  const i64 w = (i64)blockIdx.x * TPB + threadIdx.x;
-  if (w >= ldM) return;                 // (after the block's only barrier)
-  // this word's 64 column classes (-1 past n); 16-byte loads when whole
-  int32_t ca[64];
-  if (w * 64 + 64 <= n && (reinterpret_cast<uintptr_t>(cla) & 15) == 0) {
-    const int4* src = reinterpret_cast<const int4*>(cla + w * 64);
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int4 x = src[v];
-      ca[4 * v] = x.x;
-      ca[4 * v + 1] = x.y;
-      ca[4 * v + 2] = x.z;
-      ca[4 * v + 3] = x.w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 64; ++j) ca[j] = w * 64 + j < n ? cla[w * 64 + j] : -1;
-  }
-  const uint32_t* rows32 = reinterpret_cast<const uint32_t*>(rowsM);
-  const i64 ld32 = 2 * ldMc;
-  for (int q = 0; q < nh; ++q) {
-    const uint32_t* r = rows32 + (i64)q * ld32;
-    u64 acc = 0;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      // (the index arithmetic stays inside the loop: hoisted over q it held
-      // 192 registers, one wave per SIMD)
-      int32_t a = ca[j];
-      asm volatile("" : "+v"(a));
-      const uint32_t bit = (r[max(a, 0) >> 5] >> (a & 31)) & (uint32_t)(a >= 0);
-      acc |= (u64)bit << j;
-    }
-    M[dst[q] + w] = acc;
-  }
-}
-
 // Heavy rows straight from the class-level matrix, every member row: McT
 // (k_ptrans of Mc's heavy rows: McT[hw][a] bit i = heavy class 64 hw + i
 // reaches column class a).  Block (64-word range, heavy word hw): lane j of
@@ -2125,8 +1998,8 @@ __global__ __launch_bounds__(TPB) void k_heavy_expand_w(const int32_t* __restric
 // the 64 pods x 64 classes bits into the 64 classes' words of row word w, kept in
 // LDS; then the first member row of each class (first_only: k_rows copies
 // it to the others in whole-row stores) or every member row takes the 512-B
-// segment.  (k_heavy_expand_w gathered 64 bits per output word from LDS:
-// 0.63 ms at D1 before k_rows' 0.60 ms copy)
+// segment.  (The round-4 form gathered 64 bits per output word from LDS:
+// 0.63 ms at D1 before k_rows' 0.60 ms copy.)
 constexpr int HXB = 64;          // row words per block
 constexpr int HXS = HXB + 2;     // LDS row stride (16-B aligned rows)
 __global__ __launch_bounds__(TPB) void k_heavy_rows_t(const u64* __restrict__ McT, i64 ldT,
@@ -2203,7 +2076,6 @@ struct RowsArgs {
   i64 n, W;
   int ch;
   int cww;
-  int plain;             // plain 16-byte stores (else non-temporal)
   int heavy_skip;        // heavy classes' rows written whole by k_heavy_rows_t
   u64* color;
   u64* colnand;
@@ -2323,12 +2195,8 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
     for (int32_t m = m0; m < m1; ++m) {
       const int32_t pod = __builtin_amdgcn_readfirstlane(a.mem[m]);
       u64* dst = a.M + (i64)(pod - a.r0) * ldw + base;
-      if (a.plain) {
-        for (int w = threadIdx.x * 2; w < nw; w += NT * 2) *(u64x2*)&dst[w] = z;
-      } else {
-        for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-          __builtin_nontemporal_store(z, (u64x2*)&dst[w]);
-      }
+      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+        __builtin_nontemporal_store(z, (u64x2*)&dst[w]);
     }
     if (chunk == 0 && a.color) {
       for (int w = threadIdx.x; w < nw; w += NT) {
@@ -2349,18 +2217,14 @@ __device__ __forceinline__ void rows_item(const RowsArgs& a, i64 b, u64* row) {
   } else {
     build_light_row<NT>(a, c, base, nw, row);
   }
-  // 16-byte stores, non-temporal unless a.plain (round 2 measured non-
-  // temporal 5-7 % faster on two boxes; box to box the order varies)
+  // non-temporal 16-byte stores (round 2: 5-7 % faster than plain stores
+  // alone; round 5: plain stores beside the next build evict its working
+  // set, C3 step 0.37 -> 0.50 ms)
   for (int32_t m = m0; m < m1; ++m) {
     if (heavy && m == m_begin) continue;
     u64* dst = a.M + (i64)(a.mem[m] - a.r0) * ldw + base;
-    if (a.plain) {
-      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-        *(u64x2*)&dst[w] = *(const u64x2*)&row[w];
-    } else {
-      for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
-        __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
-    }
+    for (int w = threadIdx.x * 2; w < nw; w += NT * 2)
+      __builtin_nontemporal_store(*(const u64x2*)&row[w], (u64x2*)&dst[w]);
   }
   if (chunk == 0 && a.color) {
     for (int w = threadIdx.x; w < nw; w += NT) {

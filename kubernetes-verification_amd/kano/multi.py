@@ -127,7 +127,6 @@ class MultiBuild:
             self.members.append(m)
         self.device = self.members[0].device
         self._idx = None
-        self._inc = False
         if tables is not None:   # (None: the caller uploads, then builds)
             self.upload(tables)
             if build:
@@ -399,14 +398,12 @@ class MultiBuild:
         self._chk(self.lib.kano_group_add_policies(
             self.g, int(so.shape[0] - 1), int(xv.shape[0]), _ptr(xv), _ptr(so), _ptr(sc),
             _ptr(sv), _ptr(ao), _ptr(ac), _ptr(av), byref(first)), "kano_group_add_policies")
-        self._inc = True
         return int(first.value)
 
     def remove_policies(self, ids) -> None:
         a = np.ascontiguousarray(np.asarray(ids, dtype=np.int64).reshape(-1))
         self._chk(self.lib.kano_group_remove_policies(self.g, int(a.shape[0]), _ptr(a)),
                   "kano_group_remove_policies")
-        self._inc = True
 
     def added_policy_sets(self, eid: int) -> Tuple[np.ndarray, np.ndarray]:
         # (the added policies' sets cover every pod on every member)

@@ -218,6 +218,64 @@ def test_c5_full_size_properties():
     assert np.array_equal(np.concatenate(pairs), full["pairs"])
 
 
+@pytest.mark.parametrize("N", [2, 4, 8])
+def test_c3_row_shards_vs_kano_py(N):
+    """C3 -- the headline config the metric quotes at 1/2/4/8 GPUs -- as N row
+    shards (kano/shard.py row_range, the multi-GPU partition), every shard
+    alive at once on this device: each shard's kano_verify_shard writes its
+    column words into one gathered buffer (what the all-gather delivers), then
+    every shard's kano_verify_combine must give kano_py's all_reachable,
+    all_isolated and user_crosscheck lists (algorithm.py:4-42), the owner of
+    row 0 its system_isolation list (algorithm.py:45-55); the shards' rows
+    concatenated in rank order hash to kano_py's M (model.py:158-160), and
+    their policy_shadow pairs concatenated in rank order equal kano_py's list
+    (algorithm.py:58-80: per pod in row order)."""
+    import torch
+    from kano._engine import DeviceBuild
+    from kano._intern import tables_from_cluster
+    from kano.shard import row_range
+    from kano.synth import make_config
+    cl = make_config("C3")
+    exp = expected("C3")
+    assert cl.fingerprint() == exp["seed"]["fingerprint"]
+    tb = tables_from_cluster(cl)
+    gid = tenant_groups(cl)
+    n = cl.n
+    W = (n + 63) // 64
+    gathered = torch.zeros(N * 3 * W, dtype=torch.int64, device="cuda")
+    spans = [row_range(n, N, k) for k in range(N)]
+    engs = []
+    try:
+        for k, (r0, r1) in enumerate(spans):
+            e = DeviceBuild(tb, rows=(r0, r1), build=False)
+            engs.append(e)
+            e.verify_shard(gathered.data_ptr() + 8 * 3 * W * k, gid=gid, sys_row=0, shadow=True)
+        torch.cuda.synchronize()   # every shard's words are in (the all-gather's end)
+        h = hashlib.sha256()
+        pairs, total = [], 0
+        for k, (e, (r0, r1)) in enumerate(zip(engs, spans)):
+            r = e.verify_combine(gathered.data_ptr(), N)
+            for key in ("all_reachable", "all_isolated"):
+                assert index_list_matches(r[key], exp[key]), (N, k, key)
+            assert index_list_matches(r["user_crosscheck"], exp["user_crosscheck"]["result"]), \
+                (N, k)
+            if r0 == 0:
+                assert index_list_matches(r["system_isolation"],
+                                          exp["system_isolation"]["result"]), (N, k)
+            else:
+                assert r["system_isolation"] is None
+            total += r["shadow_count"]
+            pairs.append(np.array(r["pairs"], copy=True))
+            h.update(np.ascontiguousarray(e.rows(r0, r1 - r0)).tobytes())
+        assert h.hexdigest() == exp["M_sha256"]
+        assert total == exp["policy_shadow"]["count"]
+        allp = np.ascontiguousarray(np.concatenate(pairs), dtype=np.int32)
+        assert sha(allp) == exp["policy_shadow"]["sha256"]
+    finally:
+        for e in engs:
+            e.close()
+
+
 # --- D1: the dense path (MFMA GEMM) at full size ----------------------------
 def test_d1_dense_auto_picks_mfma():
     """D1 (kano/synth.py dense mode: 8,000 row classes, each selected by
@@ -339,16 +397,17 @@ def _lists(cs, which):
 
 
 # --- matrix-write forms ------------------------------------------------------
-@pytest.mark.parametrize("tune", ["", "store=0", "cww=64", "cww=16", "async=0", "podword=0",
-                                  "hexplds=0", "hexplds=1", "hexplds=3", "hexplds=4", "dx=2", "aclds=0", "rch=3",
+@pytest.mark.parametrize("tune", ["", "cww=64", "cww=16", "async=0",
+                                  "hexplds=3", "hexplds=4", "dx=2", "aclds=0", "rch=3",
                                   "rch=64,cww=16384", "shr=4", "shr=8", "rw=2", "rw=2,rch=1",
                                   "rw=2,cww=16", "rw=2,rch=64,async=0", "rw=2,rwg=3",
                                   "rw=2,rwg=1,rch=1", "sww=1", "sww=3", "aipt=8", "aipt=3", "rheavy=0", "rheavy=1"])
 @pytest.mark.parametrize("name", ["C2", "s_sparse_2000", "s_broad_1000", "q_wide_select"])
 def test_rows_variants_forced(name, tune, monkeypatch):
-    """The matrix write (k_rows) with non-temporal and plain stores, in the
-    column chunks wide matrices take (forced at small n), with and without
-    asynchronous completion: against kano_py's matrix and lists."""
+    """The matrix write's shipped forms -- k_rows and the persistent k_rows_w,
+    the heavy rows' forms, the column chunks wide matrices take (forced at
+    small n), with and without asynchronous completion -- against kano_py's
+    matrix and lists."""
     from kano._engine import DeviceBuild
     from kano._intern import intern, group_ids, tables_from_cluster
     from kano.synth import make_config, objects_from_json

@@ -715,13 +715,13 @@ def test_mixed_types_packed_and_unpacked(seed, packed, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("tune", ["", "async=0", "store=0", "packed=0", "podword=0", "shr=4"])
+@pytest.mark.parametrize("tune", ["", "async=0", "packed=0", "shr=4"])
 @pytest.mark.parametrize("n,P", [(1, 0), (1, 1), (2, 3), (5, 1), (63, 7), (64, 64), (65, 9),
                                  (130, 40)])
 def test_verify_small_shapes_vs_oracle(n, P, tune, monkeypatch):
     """kano_verify on tiny and word-boundary shapes (1, 63, 64, 65 pods; no
     policy; more policies than pods) with synchronous and asynchronous
-    completion, both store forms of the matrix write and both classification forms: every
+    completion and both classification forms: every
     list, the pairs and the count-only count equal the C oracle's (a
     restatement of algorithm.py:4-80)."""
     from kano._engine import DeviceBuild
