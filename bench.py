@@ -811,7 +811,8 @@ def verify_shard_alone(config, cl, tables, gid, eng, res, r0, r1, shadow):
         bad = []
         if not np.array_equal(eng.rows_digest(r0, r1 - r0), full.rows_digest(r0, r1 - r0)):
             bad.append("row digests")
-        if not _list_ok(shard.get("system_isolation", []), fres["system_isolation"]):
+        if not np.array_equal(np.asarray(shard.get("system_isolation", []), np.int32),
+                              np.asarray(fres["system_isolation"], np.int32)):
             bad.append("system_isolation")
         if shadow == "pairs":
             fp = np.asarray(fres["policy_shadow"], np.int32).reshape(-1, 2)
