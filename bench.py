@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--alone", type=int, default=5,
                     help="k_rows launches timed alone (kano_build) after the timed region "
                          "(roofline.alone; 0: none)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="kano_set_pipeline: each step queues the next step's prologue behind a "
+                         "gate the next step opens (0: off)")
     ap.add_argument("--rank-of", type=int, default=0,
                     help="diagnostic: time rank 0's shard step of an N-rank run on one GPU "
                          "(the all-gather replaced by a local copy; not a bench line)")
@@ -395,7 +398,18 @@ def main():
                 torch=torch, stream=stream, emulate=args.rank_of if args.rank_of > 1 else 0)
     up_groups_ms = (time.perf_counter() - t_up) * 1e3
 
+    # (pipelined steps: the engine calls alone order its streams -- the fused
+    # kano_verify, the emulated gather, the native RCCL gather; a torch
+    # collective between the halves synchronises the device, so not there)
+    pipelined = bool(args.pipeline) and (not step.shard_path or step.xchg.comm is not None
+                                         or (step.xchg.dist is None and step.xchg.emulate_native))
+    eng.set_pipeline(pipelined)
+
     def barrier():
+        # (a queued prologue first: its gate would hold a device-wide sync;
+        # the last timed step's queued prologue runs here, inside the timed
+        # region -- one prologue more than the K steps need)
+        eng.settle()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -486,6 +500,7 @@ def main():
             "dtype": "u64", "data": "synthetic",
             "config": {"workload": WORKLOADS[args.config], "name": args.config, "pods": n,
                        "policies": cl.P, "mode": cl.mode, "seed": cl.seed,
+                       "pipelined": pipelined,
                        "parallelism": (f"rows{world}" if args.rank_of <= 1 else
                                        f"rank 0 of {args.rank_of} emulated on one GPU, "
                                        "no collective (diagnostic, not a bench line)"),

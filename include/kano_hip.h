@@ -191,6 +191,27 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
                 int32_t* idx, int64_t* counts, int32_t* shadow_pairs, int64_t shadow_cap,
                 int64_t* shadow_count);
 
+/* Pipelined verification (no reference counterpart: a serving loop that
+ * re-runs build_matrix + the checks on the resident inputs, as the benchmark
+ * does).  With on != 0, a kano_verify / kano_verify_gather that completes
+ * asynchronously also queues the NEXT call's prologue -- the build's fills
+ * and classification up to the member lists, which read only the uploaded
+ * tables -- on the context stream behind a gate kernel that polls a
+ * page-locked word; the next kano_verify / kano_verify_gather opens the gate
+ * on entry (nothing runs before the call that asks for it), so the host's
+ * issue of those launches leaves the step's critical path.  Every other entry
+ * point, and kano_set_pipeline(ctx, 0), opens the gate, waits and puts the
+ * context back as the last call left it.  A device-wide synchronisation
+ * outside the engine (hipDeviceSynchronize, torch.cuda.synchronize) while a
+ * prologue is queued waits for the gate's timeout (200 ms): call
+ * kano_settle first.  Default off. */
+int kano_set_pipeline(kano_ctx* ctx, int on);
+
+/* The context's queued work finished: a primed prologue's gate opened (the
+ * prologue runs and is put back), an asynchronously completing matrix write
+ * waited for.  Afterwards no engine work is pending on the device. */
+int kano_settle(kano_ctx* ctx);
+
 /* kano_verify for one row shard of a multi-GPU build, in two
  * halves around the ranks' exchange step.
  *   kano_verify_shard: the build of this shard's rows and every check up to

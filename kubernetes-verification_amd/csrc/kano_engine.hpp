@@ -291,6 +291,27 @@ struct kano_ctx {
   // engine stream, behind which every later engine operation queues, and
   // every other entry point settles it first
   bool async_pending = false;
+  // Pipelined calls (kano_set_pipeline): an asynchronously completing
+  // kano_verify queues the next call's prologue -- the build's fills and
+  // classification up to the member lists, which read only the resident
+  // inputs -- behind a gate kernel (k_gate) on the engine stream, into the
+  // next input set and a private size-slot array.  The next kano_verify
+  // rings the bell (a store to page-locked memory) instead of issuing those
+  // launches; any other entry point rings it, waits, and puts both sets back
+  // (unprime).  So no work moves ahead of the call that asks for it; the
+  // host's issue of the prologue moves off the step's critical path.
+  int pipeline = 0;
+  bool primed = false;
+  bool priming = false;            // (prime_next is queuing it: no unprime from inside)
+  bool consume_prime = false;      // verify_front -> build_impl: this build takes it
+  bool prime_pre_marked = false;   // the prologue's member-list fill marked ev_pre
+  bool prime_alist_valid = false;  // (restored by unprime)
+  u64 prime_sig = 0;               // the prologue's class-count scan's host signal
+  u64* bell = nullptr;             // page-locked, coherent; bell_dev its device address
+  u64* bell_dev = nullptr;
+  u64 bell_seq = 0;
+  u64 gate_ticks = 0;              // k_gate's timeout in wall-clock ticks (200 ms)
+  DBuf sizes_alt;                  // the size slots the primed prologue writes
   hipEvent_t ev_tail = nullptr;    // the result copies of kano_verify's tail
   // the matrix write's launch times (ev_rt[set][0] -> [1], recorded by its
   // own dispatch), resolved once the launch is known to be complete: the

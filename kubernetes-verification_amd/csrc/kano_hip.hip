@@ -303,13 +303,56 @@ int FillBatch::run() {
   return 0;
 }
 
+// the two physical sets of k_rows' inputs exchanged (pointers only)
+void swap_rows_ptrs(kano_ctx* ctx) {
+  RowsInputs& a = ctx->rin_alt;
+  std::swap(ctx->wioff, a.wioff);
+  std::swap(ctx->wicls, a.wicls);
+  std::swap(ctx->soffc, a.soffc);
+  std::swap(ctx->slist, a.slist);
+  std::swap(ctx->aloff, a.aloff);
+  std::swap(ctx->alist, a.alist);
+  std::swap(ctx->alcoff, a.alcoff);
+  std::swap(ctx->alc, a.alc);
+  std::swap(ctx->rc.moff, a.rmoff);
+  std::swap(ctx->rc.mem, a.rmem);
+  std::swap(ctx->cc.moff, a.cmoff);
+  std::swap(ctx->cc.mem, a.cmem);
+  std::swap(ctx->cc.cls, a.ccls);
+  std::swap(ctx->hflag, a.hflag);
+  std::swap(ctx->hlist, a.hlist);
+  std::swap(ctx->Mc, a.Mc);
+  ctx->rows_set ^= 1;
+}
+
+// ---- pipelined calls: the next kano_verify's prologue behind a gate ------
+// (kano_set_pipeline; the fields' comment in kano_engine.hpp)
+void ring_bell(kano_ctx* ctx) {
+  if (ctx->bell) __atomic_store_n(ctx->bell, ctx->bell_seq, __ATOMIC_SEQ_CST);
+}
+
+// a primed prologue not taken by a kano_verify: open the gate, let it run
+// (into the private size slots and the next input set), put both back
+int unprime(kano_ctx* ctx) {
+  if (!ctx->primed || ctx->priming) return 0;
+  ctx->primed = false;
+  ring_bell(ctx);
+  KCHK(hipStreamSynchronize(ctx->stream));
+  std::swap(ctx->sizes, ctx->sizes_alt);
+  swap_rows_ptrs(ctx);
+  ctx->alist_valid = ctx->prime_alist_valid;
+  return 0;
+}
+
 int sync(kano_ctx* ctx) {
+  KTRY(unprime(ctx));
   KCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 
 // an asynchronously completing kano_verify's matrix write, finished
 int settle(kano_ctx* ctx) {
+  KTRY(unprime(ctx));
   if (!ctx->async_pending) return 0;
   ctx->async_pending = false;
   KCHK(hipSetDevice(ctx->device));
@@ -349,24 +392,7 @@ int resolve_rows_time(kano_ctx* ctx, bool block = true) {
 // calls back, which last read it, has ended -- an event wait on the engine
 // stream, not on the host)
 int swap_rows_inputs(kano_ctx* ctx) {
-  RowsInputs& a = ctx->rin_alt;
-  std::swap(ctx->wioff, a.wioff);
-  std::swap(ctx->wicls, a.wicls);
-  std::swap(ctx->soffc, a.soffc);
-  std::swap(ctx->slist, a.slist);
-  std::swap(ctx->aloff, a.aloff);
-  std::swap(ctx->alist, a.alist);
-  std::swap(ctx->alcoff, a.alcoff);
-  std::swap(ctx->alc, a.alc);
-  std::swap(ctx->rc.moff, a.rmoff);
-  std::swap(ctx->rc.mem, a.rmem);
-  std::swap(ctx->cc.moff, a.cmoff);
-  std::swap(ctx->cc.mem, a.cmem);
-  std::swap(ctx->cc.cls, a.ccls);
-  std::swap(ctx->hflag, a.hflag);
-  std::swap(ctx->hlist, a.hlist);
-  std::swap(ctx->Mc, a.Mc);
-  ctx->rows_set ^= 1;
+  swap_rows_ptrs(ctx);
   ctx->alist_valid = false;
   // (usually long over: then no wait packet on the engine stream)
   if (ctx->rows_end_rec[ctx->rows_set]) {
@@ -378,6 +404,7 @@ int swap_rows_inputs(kano_ctx* ctx) {
   }
   return 0;
 }
+
 
 // the last build's MFMA contraction time, once its end event is complete
 int resolve_mfma_time(kano_ctx* ctx) {
@@ -791,7 +818,10 @@ int front_fills(kano_ctx* ctx, FillBatch& fb) {
   return 0;
 }
 
-int do_front(kano_ctx* ctx, int path) {
+// The build's prologue, up to the member lists: it reads only the resident
+// inputs (the label tables), so a pipelined kano_verify queues it for the
+// next call behind the gate (prime_next)
+int front_a(kano_ctx* ctx) {
   ctx->rc.m0 = ctx->r0;
   ctx->rc.m1 = ctx->r1;
   ctx->cc.m0 = 0;
@@ -807,14 +837,31 @@ int do_front(kano_ctx* ctx, int path) {
   KTRY(mirror_begin(ctx));
   // the side work of do_back_pre needs the classes only: it forks after the
   // member lists (their fill's dispatch marks ev_pre)
-  ctx->pre_forked = false;
-  const bool fork_pre = ctx->stream2 != nullptr;
-  bool pre_marked = false;
-  KTRY(classify_phase2a(ctx, fork_pre ? ctx->ev_pre : nullptr, &pre_marked));
-  if (fork_pre) {
-    if (!pre_marked) KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
-    ctx->pre_forked = true;
+  if (ctx->stream2) {
+    bool marked = false;
+    KTRY(classify_phase2a(ctx, ctx->ev_pre, &marked));
+    if (!marked) KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
+  } else {
+    KTRY(classify_phase2a(ctx));
   }
+  return 0;
+}
+
+// primed: the prologue was queued by the previous kano_verify (its gate is
+// open: kano_verify rang the bell on entry)
+int do_front(kano_ctx* ctx, int path, bool primed = false) {
+  if (primed) {
+    ctx->primed = false;
+    ring_bell(ctx);
+    ctx->rc.m0 = ctx->r0;
+    ctx->rc.m1 = ctx->r1;
+    ctx->cc.m0 = 0;
+    ctx->cc.m1 = ctx->n;
+    ctx->sig_wait = ctx->prime_sig;   // (its class-count scan raises this signal)
+  } else {
+    KTRY(front_a(ctx));
+  }
+  ctx->pre_forked = ctx->stream2 != nullptr;
   i64 u[2] = {0, 0};
   KTRY(mirror_wait(ctx, SZ_UR, 2, u));
   // an earlier matrix write's time, when it has ended (no wait: the
@@ -2060,6 +2107,23 @@ int kano_create(int device, kano_ctx** out) {
     return -ENOMEM;
   }
   for (int k = 0; k <= SZ_SIGNAL; ++k) ctx->gmirror[k] = 0;
+  // the pipelined prologue's bell (kano_set_pipeline): one coherent word the
+  // gate kernel polls; its timeout in wall-clock ticks (200 ms)
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->bell), 64,
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->bell_dev), ctx->bell, 0) !=
+          hipSuccess) {
+    kano_destroy(ctx);
+    return -ENOMEM;
+  }
+  ctx->bell[0] = 0;
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess ||
+        khz <= 0)
+      khz = 100000;   // (gfx950's wall clock: 100 MHz)
+    ctx->gate_ticks = (u64)khz * 200;
+  }
   // page-locked staging for short row reads (system_isolation's row)
   if (hipHostMalloc(&ctx->row_stage, ROW_STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
     ctx->row_stage = nullptr;
@@ -2076,6 +2140,7 @@ int kano_create(int device, kano_ctx** out) {
 void kano_destroy(kano_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  ring_bell(ctx);   // (a primed prologue's gate opens: the syncs below finish)
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
@@ -2083,6 +2148,8 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   if (ctx->gmirror) (void)hipHostFree(ctx->gmirror);
   if (ctx->row_stage) (void)hipHostFree(ctx->row_stage);
+  if (ctx->bell) (void)hipHostFree(ctx->bell);
+  dfree(ctx->sizes_alt);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
@@ -2460,6 +2527,10 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
                const ExtraFills& extra = ExtraFills(), const ExtraFills& pre_fill = ExtraFills(),
                const PreRun& pre_run = PreRun()) {
   if (!ctx) return -EINVAL;
+  // (a primed prologue is this build's only when kano_verify's front asked)
+  const bool consume = ctx->primed && ctx->consume_prime;
+  ctx->consume_prime = false;
+  if (!consume) KTRY(unprime(ctx));
   if (!ctx->have_pods || !ctx->have_pols) return fail(ctx, -EINVAL, "kano_build: inputs not set");
   if (path < 0 || path > 2) return fail(ctx, -EINVAL, "kano_build: unknown path");
   KCHK(hipSetDevice(ctx->device));
@@ -2479,7 +2550,7 @@ int build_impl(kano_ctx* ctx, int path, bool rows_now, bool defer_cols = false,
   KTRY(dalloc(ctx, ctx->color, sizeof(u64) * ctx->ldM));
   KTRY(dalloc(ctx, ctx->colnand, sizeof(u64) * ctx->ldM));
   KTRY(stage_mark(ctx, 0, ctx->stream));
-  KTRY(do_front(ctx, path));
+  KTRY(do_front(ctx, path, consume));
   // host sync 2 (the list sizes), overlapped with the size-independent part
   // of the back end (zeroed AC / Mc, the crosscheck's group-key sort)
   KTRY(mirror_begin(ctx));
@@ -3168,8 +3239,9 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
                  bool want_shadow, u64* words_dev, bool count_only = false) {
   ctx->vs_count_only = want_shadow && count_only;
   // the previous call's matrix write may still run: build into the other
-  // input set instead of waiting for it
-  if (ctx->async_pending) KTRY(swap_rows_inputs(ctx));
+  // input set instead of waiting for it (a primed prologue already writes it)
+  ctx->consume_prime = ctx->primed;
+  if (ctx->async_pending && !ctx->primed) KTRY(swap_rows_inputs(ctx));
   const bool stored = !gid && ngroups == KANO_STORED_GROUPS;
   const bool want_cross = gid || stored;
   // the crosscheck and policy_shadow buffers are filled in the build's last
@@ -3372,6 +3444,38 @@ int spin_event(kano_ctx* ctx, hipEvent_t e) {
   }
 }
 
+// The next kano_verify's prologue (front_a) behind a gate on the engine
+// stream: into the next input set (the write just launched reads this one)
+// and the private size slots; the next call rings the bell, anything else
+// unprimes.  Nothing of it runs before the next call asks (or the gate's
+// 200 ms timeout: then it has run on the same resident inputs).
+int prime_next(kano_ctx* ctx) {
+  if (ctx->primed || !ctx->bell || ctx->stage_timing) return 0;
+  KTRY(dalloc(ctx, ctx->sizes_alt, sizeof(u64) * SZ_SLOTS));
+  ctx->prime_alist_valid = ctx->alist_valid;
+  KTRY(swap_rows_inputs(ctx));
+  std::swap(ctx->sizes, ctx->sizes_alt);
+  ctx->primed = true;
+  ctx->priming = true;
+  const u64 armed = ctx->sig_armed, waiting = ctx->sig_wait;
+  hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, ctx->stream, (const u64*)ctx->bell_dev,
+                     ++ctx->bell_seq, ctx->gate_ticks);
+  int rc = hipGetLastError() == hipSuccess ? 0 : fail(ctx, -EIO, "k_gate launch failed");
+  if (!rc) {
+    ctx->sig_armed = 0;
+    rc = front_a(ctx);
+  }
+  ctx->priming = false;
+  if (rc) {
+    (void)unprime(ctx);
+    return rc;
+  }
+  ctx->prime_sig = ctx->sig_wait;
+  ctx->sig_armed = armed;
+  ctx->sig_wait = waiting;
+  return 0;
+}
+
 // compacted: policy_shadow's compaction ran on stream2 (verify_front; its
 // end is ev_pairs)
 int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts,
@@ -3456,6 +3560,9 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
     ctx->rows_in = nullptr;
     KTRY(rc);
   }
+  // the next call's prologue, queued behind its gate while this call's tail
+  // still runs (kano_set_pipeline)
+  if (async && ctx->pipeline) KTRY(prime_next(ctx));
   part(12);
   const auto tw0 = clk::now();
   KTRY(spin_event(ctx, ctx->ev_tail));
@@ -3477,7 +3584,9 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
     *shadow_count = total;
     ctx->shadow_total = pairs_mode ? total : -1;
     if (pairs_mode && total > out_cap) {
-      // past the emission buffer: the sized emission, then the copy
+      // past the emission buffer: the sized emission, then the copy (on a
+      // stream without the gate: the next call builds unprimed)
+      KTRY(unprime(ctx));
       KTRY(dalloc(ctx, ctx->out, sizeof(int2) * (total + total / 4)));
       if (rl > 0) {
         hipLaunchKernelGGL(k_shadow_emit, dim3(nblk(rl)), dim3(TPB), 0, st,
@@ -3708,6 +3817,7 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
   if (!ctx) return -EINVAL;
   if (!counts || (!idx && ctx->n > 0))
     return fail(ctx, -EINVAL, "kano_verify: idx / counts must not be NULL");
+  ring_bell(ctx);   // (a primed prologue starts now: this call takes it)
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   ctx->ht_wait = 0;
@@ -3719,6 +3829,19 @@ int kano_verify(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, in
       verify_back(ctx, nullptr, 0, idx, counts, shadow_pairs, shadow_cap, shadow_count, true);
   host_time_record(ctx, t0, t1, clk::now());
   return rc;
+}
+
+int kano_set_pipeline(kano_ctx* ctx, int on) {
+  if (!ctx) return -EINVAL;
+  if (!on) KTRY(unprime(ctx));
+  ctx->pipeline = on ? 1 : 0;
+  return 0;
+}
+
+int kano_settle(kano_ctx* ctx) {
+  if (!ctx) return -EINVAL;
+  KCHK(hipSetDevice(ctx->device));
+  return settle(ctx);
 }
 
 int kano_host_times(kano_ctx* ctx, double* out, int reset) {
@@ -3761,6 +3884,7 @@ int kano_verify_gather(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngro
     return fail(ctx, -EINVAL, "kano_verify_gather: idx / counts must not be NULL");
   if (with_shadow && !shadow_count)
     return fail(ctx, -EINVAL, "kano_verify_gather: shadow_count is NULL but with_shadow is set");
+  ring_bell(ctx);   // (a primed prologue starts now: this call takes it)
   // comm NULL: rank 0 of nranks emulated on this device (a timing diagnostic:
   // the other ranks' words are zero, the all-gather a device copy)
   const RcclAllGather ag = comm ? rccl_all_gather() : nullptr;

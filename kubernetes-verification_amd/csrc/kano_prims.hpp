@@ -420,6 +420,22 @@ static __global__ __attribute__((unused)) __launch_bounds__(TPB) void k_fill_man
 }
 constexpr int FILL_RIDE_BLOCKS = 512;   // blocks a carried fill gets (grid-stride)
 
+// The gate in front of a primed prologue (kano_set_pipeline): one lane polls
+// the bell -- a word in page-locked, coherent host memory that the next
+// kano_verify stores -- with system-scope loads, sleeping between polls,
+// until it reaches `want`; past `ticks` of the wall clock it opens by itself,
+// so the engine stream never stays closed (the prologue reads only resident
+// inputs, so it is valid whenever it runs).  One wave, no other work.
+static __global__ __attribute__((unused)) __launch_bounds__(64) void k_gate(const u64* bell,
+                                                                            u64 want, u64 ticks) {
+  if (threadIdx.x != 0) return;
+  const u64 t0 = wall_clock64();
+  while (__hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+    if (wall_clock64() - t0 > ticks) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // atomicAdd(&ctr[key], 1) for every active lane, lanes with equal keys merged
 // into one atomic: up to AGG_ROUNDS rounds each take the first remaining
 // lane's key and every lane sharing it (Zipf keys: the hot keys repeat

@@ -570,6 +570,18 @@ class DeviceBuild:
         return dict(sum_ms=float(out[0]), builds=int(out[1]), ops_sum=float(out[2]),
                     ops_last=float(out[3]))
 
+    def set_pipeline(self, on: bool = True) -> None:
+        """kano_set_pipeline: each asynchronously completing verify queues the
+        next call's prologue behind a gate that the next verify opens (a loop
+        of verify calls on the resident inputs).  Call ``settle()`` before a
+        device-wide synchronisation outside the engine."""
+        self._chk(self.lib.kano_set_pipeline(self.ctx, int(bool(on))), "kano_set_pipeline")
+
+    def settle(self) -> None:
+        """kano_settle: no engine work left pending on the device (a queued
+        prologue run and put back, the last matrix write finished)."""
+        self._chk(self.lib.kano_settle(self.ctx), "kano_settle")
+
     def host_times(self, reset: bool = False) -> dict:
         """kano_verify's host time by phase (us): sums and maxima since the
         last reset (kano_host_times)."""

@@ -75,6 +75,8 @@ SIGNATURES = {
     "kano_stage_times": (c_int, [c_void_p, c_void_p]),
     "kano_rows_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_host_times": (c_int, [c_void_p, c_void_p, c_int]),
+    "kano_set_pipeline": (c_int, [c_void_p, c_int]),
+    "kano_settle": (c_int, [c_void_p]),
     "kano_mfma_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_group_create": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
     "kano_group_create_lean": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),

@@ -211,6 +211,106 @@ def test_verify_fused_c2(cap):
     pin.close()
 
 
+def test_verify_pipelined(monkeypatch):
+    """kano_set_pipeline: every asynchronously completing verify queues the
+    next call's prologue behind a gate the next verify opens.  Every call's
+    results equal kano_py's (C2's record) whatever comes between two calls:
+    nothing, a matrix read, a re-upload, another cluster's tables, a plain
+    build, a pause past the gate's timeout (the prologue then ran by itself on
+    the same inputs), count-only mode, the emulated shard path, the pipeline
+    switched off while a prologue is queued, and a close while one is queued."""
+    import time
+    import torch
+    from kano._engine import DeviceBuild, PinnedBuffer
+    from kano._intern import tables_from_cluster, intern, group_ids
+    from kano.synth import make_config, KEY_NAMES
+    exp = expected("C2")
+    cl = make_config("C2")
+    n = cl.n
+    _, gid = np.unique(cl.vals[KEY_NAMES.index("tenant")], return_inverse=True)
+    tables = tables_from_cluster(cl)
+    eng = DeviceBuild(tables, build=False)
+    eng.set_pipeline(True)
+    pin = PinnedBuffer((1 << 22) * 8)
+    pairs = pin.view(np.int32, 2 << 22)
+    eng.set_groups(gid)
+
+    def check(r, e=exp, count_only=False):
+        assert r["all_isolated"].tolist() == e["all_isolated"]
+        assert r["all_reachable"].tolist() == e["all_reachable"]
+        assert r["user_crosscheck"].tolist() == e["user_crosscheck"]["result"]
+        assert r["shadow_count"] == e["policy_shadow"]["count"]
+        if not count_only:
+            assert sha(np.ascontiguousarray(r["pairs"])) == e["policy_shadow"]["sha256"]
+
+    for k in range(10):
+        r = eng.verify("stored", sys_row=0, shadow=True, pairs=pairs)
+        check(r)
+        assert r["system_isolation"].tolist() == exp["system_isolation"]["result"]
+        if k == 2:
+            assert sha(eng.rows(0, n)) == exp["M_sha256"]    # (unprimes, then reads)
+        if k == 4:
+            eng.upload(tables)
+            eng.set_groups(gid)
+        if k == 5:
+            time.sleep(0.35)     # past the gate's 200 ms: the prologue ran by itself
+        if k == 6:
+            eng.build()          # a plain build takes no primed prologue
+            assert sha(eng.rows(0, n)) == exp["M_sha256"]
+        if k == 7:
+            r = eng.verify("stored", sys_row=0, shadow=True, shadow_count_only=True)
+            check(r, count_only=True)
+    assert sha(eng.rows(0, n)) == exp["M_sha256"]
+    # another cluster's tables right behind a primed call, and back
+    r = eng.verify("stored", sys_row=0, shadow=True, pairs=pairs)
+    obj = cluster("s_sparse_2000")
+    cs, ps = api_objects(obj)
+    eng.upload(intern(cs, ps))
+    e2 = expected("s_sparse_2000")
+    for _ in range(3):
+        rb = eng.verify(group_ids(cs, obj["label"]), sys_row=0, shadow=True, pairs=pairs)
+        assert rb["all_isolated"].tolist() == e2["all_isolated"]
+        assert rb["user_crosscheck"].tolist() == e2["user_crosscheck"]["result"]
+        assert rb["shadow_count"] == e2["policy_shadow"]["count"]
+    assert sha(eng.rows(0, len(cs))) == e2["M_sha256"]
+    eng.upload(tables)
+    eng.set_groups(gid)
+    for _ in range(3):
+        check(eng.verify("stored", sys_row=0, shadow=True, pairs=pairs))
+    # settle: nothing of the engine left on the device, so a device-wide
+    # synchronisation returns at once (no gate's timeout)
+    eng.settle()
+    t = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t < 0.1
+    check(eng.verify("stored", sys_row=0, shadow=True, pairs=pairs))
+    eng.set_pipeline(False)          # with a prologue queued
+    check(eng.verify("stored", sys_row=0, shadow=True, pairs=pairs))
+    eng.set_pipeline(True)
+    check(eng.verify("stored", sys_row=0, shadow=True, pairs=pairs))
+    t = time.perf_counter()
+    eng.close()                      # with a prologue queued: opens its gate
+    assert time.perf_counter() - t < 0.15
+    # the emulated shard path (kano_verify_gather, comm NULL) pipelined: its
+    # rows and pairs equal the unpipelined call's
+    ref = DeviceBuild(tables, rows=(0, n // 4), build=False)
+    ref.set_groups(gid)
+    r0 = ref.verify_gather(0, 4, gid="stored", sys_row=0, shadow=True)
+    r0 = {k: (np.array(v, copy=True) if v is not None else None) for k, v in r0.items()}
+    d0 = ref.rows_digest(0, n // 4)
+    ref.close()
+    e = DeviceBuild(tables, rows=(0, n // 4), build=False)
+    e.set_groups(gid)
+    e.set_pipeline(True)
+    for _ in range(4):
+        r = e.verify_gather(0, 4, gid="stored", sys_row=0, shadow=True)
+        for key in ("all_isolated", "user_crosscheck", "system_isolation", "pairs"):
+            assert np.array_equal(r[key], r0[key]), key
+    assert np.array_equal(e.rows_digest(0, n // 4), d0)
+    e.close()
+    pin.close()
+
+
 @pytest.mark.parametrize("tune", ["async=1", "async=0"])
 def test_verify_async_completion(tune, monkeypatch):
     """kano_verify returns once its host results are in host memory, its
