@@ -1028,6 +1028,14 @@ int build_alist(kano_ctx* ctx, hipStream_t st = nullptr, bool launch = true) {
 // Mc, cursors and class-level column words, then the caller's fills and
 // launches (kano_verify: the crosscheck's group keys) -- queued while the
 // list sizes travel to the host
+// AC[p] built whole in a wave's LDS row (pol_allow_item's lds_row form: at
+// most 32 KB a block, so that the launch fits beside a wide k_rows_w block):
+// every row is stored whole, so AC needs no zero fill
+bool ac_whole_rows(const kano_ctx* ctx) {
+  return ctx->ac_lds && ctx->P > 0 && ctx->cc.U > 0 &&
+         sizeof(u64) * (size_t)ctx->ldC * WPB <= 32 * 1024;
+}
+
 using PreLaunch = std::function<int(FillBatch&)>;
 using PreRun = std::function<int(hipStream_t)>;
 // With the side work forked (ev_pre, recorded after the classes), all of it
@@ -1042,7 +1050,9 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
   KTRY(dalloc(ctx, ctx->Mc, sizeof(u64) * std::max<i64>(1, U * ldMc)));
   KTRY(dalloc(ctx, ctx->col_or_c, sizeof(u64) * ldMc));
   KTRY(dalloc(ctx, ctx->col_nand_c, sizeof(u64) * ldMc));
-  if (side) {   // AC first: the lists' launch needs it before anything else here
+  // (AC written whole by its builder: no fill, no join before the lists)
+  const bool ac_fill = !ac_whole_rows(ctx);
+  if (side && ac_fill) {   // AC first: the lists' launch needs it before anything else here
     FillBatch fa(ctx, ss);
     KTRY(fa.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
     KTRY(fa.run());
@@ -1051,7 +1061,7 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
   }
   {
     FillBatch fb(ctx, ss);
-    if (!side) KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
+    if (!side && ac_fill) KTRY(fb.add(ctx->AC, sizeof(u64) * P * ctx->ldC, 0u));
     KTRY(fb.add(ctx->Mc, sizeof(u64) * U * ldMc, 0u));
     KTRY(fb.add(ctx->col_or_c, sizeof(u64) * ldMc, 0u));
     KTRY(fb.add(ctx->col_nand_c, sizeof(u64) * ldMc, 0u));
@@ -1204,7 +1214,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // AC[p] built in the wave's LDS row when the rows fit (k_pol_allow; at
   // most 32 KB, so that the launch fits beside a wide k_rows_w block)
   const size_t ac_lds = sizeof(u64) * (size_t)ctx->ldC * WPB;
-  const int ac_rows = ctx->ac_lds && ac_lds <= 32 * 1024 ? 1 : 0;
+  const int ac_rows = ac_whole_rows(ctx) ? 1 : 0;   // (do_back_pre skipped AC's fill)
   if (ac_rows) lds = std::max(lds, ac_lds);
   // the side work's joins: AC zeroed before the lists, the rest (Mc, the
   // crosscheck's fills and key sort) before the Mc writers below
@@ -1815,7 +1825,8 @@ int cross_stage_a(kano_ctx* ctx, const CrossPlan& cp, ScanBatch& sb, hipStream_t
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds) {   // classes in group order: per-block LDS histograms
     const KeySort ks = cross_sort(ctx, cp);
-    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB), 0, s, ks);
+    hipLaunchKernelGGL(k_key_hist, dim3((unsigned)cp.knb), dim3(TPB),
+                       sizeof(int32_t) * (size_t)(G + 1), s, ks);
     KLAUNCH();
     if (!st) KTRY(sb.add(ks.hist, cp.kslots, P_<int32_t>(ctx->koff)));
   } else {
@@ -1836,11 +1847,11 @@ int cross_stage_b1(kano_ctx* ctx, const CrossPlan& cp, hipStream_t st = nullptr)
   const hipStream_t s = st ? st : ctx->stream;
   int32_t* kcnt = P_<int32_t>(ctx->kcnt);
   if (cp.key_lds && st) {
-    hipLaunchKernelGGL(k_key_place_scan, dim3((unsigned)cp.knb), dim3(TPB), 0, s,
-                       cross_sort(ctx, cp));
+    hipLaunchKernelGGL(k_key_place_scan, dim3((unsigned)cp.knb), dim3(TPB),
+                       sizeof(int32_t) * (size_t)(G + 1), s, cross_sort(ctx, cp));
   } else if (cp.key_lds) {
-    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB), 0, s,
-                       cross_sort(ctx, cp));
+    hipLaunchKernelGGL(k_key_place_lds, dim3((unsigned)cp.knb), dim3(TPB),
+                       sizeof(int32_t) * (size_t)(G + 1), s, cross_sort(ctx, cp));
   } else {
     hipLaunchKernelGGL(k_cls_key_place, dim3(nblk(U)), dim3(TPB), 0, s, U,
                        P_<int32_t>(ctx->ckey), P_<int32_t>(ctx->koff), kcnt + G + 1,

@@ -64,8 +64,11 @@ struct KeySort {
 };
 
 // (block-uniform: every thread of the block calls it)
+// (the histogram's LDS is dynamic, (G + 1) words: a static 32 KB table kept
+// the sort off the CUs a wide k_rows_w block fills -- C5's 1/8 shard: 0.32 ->
+// 2.64 ms beside the write, the next build's Mc chain waiting for it)
 __device__ __forceinline__ void key_hist_block(const KeySort& k, i64 b) {
-  __shared__ int32_t h[KEY_LDS_MAX];
+  extern __shared__ int32_t h[];
   const int nk = k.G + 1;
   for (int q = threadIdx.x; q < nk; q += TPB) h[q] = 0;
   __syncthreads();
@@ -83,7 +86,7 @@ __device__ __forceinline__ void key_hist_block(const KeySort& k, i64 b) {
 }
 
 __device__ __forceinline__ void key_place_block(const KeySort& k, i64 b) {
-  __shared__ int32_t h[KEY_LDS_MAX];
+  extern __shared__ int32_t h[];
   const int nk = k.G + 1;
   for (int q = threadIdx.x; q < nk; q += TPB) h[q] = k.hoff[(i64)q * k.nb + b];
   __syncthreads();
@@ -1521,7 +1524,7 @@ __global__ __launch_bounds__(TPB) void k_key_place_lds(KeySort k) {
 // scan status region of its own.
 constexpr int KEY_SCAN_ITEMS = 8;
 __global__ __launch_bounds__(TPB) void k_key_place_scan(KeySort k) {
-  __shared__ int32_t h[KEY_LDS_MAX];
+  extern __shared__ int32_t h[];
   __shared__ i64 sm[TPB / 64];
   const int nk = k.G + 1;
   const i64 b = blockIdx.x, nb = k.nb, ns = (i64)nk * nb;

@@ -428,6 +428,15 @@ def test_rows_variants_forced(name, tune, monkeypatch):
     check_verify(r, exp)
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     assert eng.info()["ROWS_KERNEL"] in (2, 3, 4, 5, 6)
+    # the bench's form: page-locked result buffers (the whole tail queued at
+    # once, sized on the device), twice back to back
+    from kano._engine import PinnedBuffer
+    pi, pp = PinnedBuffer(16 * max(t.n, 1)), PinnedBuffer(8 << 20)
+    for _ in range(2):
+        r = eng.verify(gid, sys_row=0, shadow=True, idx=pi.view(np.int32, 4 * max(t.n, 1)),
+                       pairs=pp.view(np.int32, 2 << 20))
+        check_verify(r, exp)
+    assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     eng.build()
     assert sha(eng.rows(0, t.n)) == exp["M_sha256"]
     eng.close()
