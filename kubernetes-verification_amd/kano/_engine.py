@@ -522,14 +522,19 @@ class DeviceBuild:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
         elif idx.size < 4 * n:
             raise ValueError("idx buffer needs 4*n entries")
-        counts = np.zeros(4, dtype=np.int64)
-        cnt = c_int64(0)
+        if self._counts is None:   # reused result slots (no per-call allocation)
+            self._counts = np.zeros(4, dtype=np.int64)
+            self._cnt = c_int64(0)
+            self._cnt_ref = byref(self._cnt)
+        counts, cnt = self._counts, self._cnt
         shadow = self._shard_shadow
         cap = 0 if pairs is None else pairs.size // 2
         if shadow_count_only:
             cap = -1
-        self._chk(call(_ptr(idx), _ptr(counts), _ptr(pairs), int(cap),
-                       byref(cnt) if shadow else None), what)
+        rc = call(_ptr(idx), counts.ctypes.data, _ptr(pairs), int(cap),
+                  self._cnt_ref if shadow else None)
+        if rc != 0:
+            self._chk(rc, what)
         out, o = {}, 0
         for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
                                   "system_isolation")):
