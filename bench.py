@@ -476,7 +476,8 @@ def main():
         dist.all_reduce(t)
         shadow_cnt = int(t.item())
     out = None
-    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
+    traffic, traffic_src = (pmc_traffic(args.config, args.rank_of, info["ROWS_KERNEL"])
+                            if world == 1 else (None, None))
     # the last step's results against kano_py's own outputs on this cluster
     # (tests/golden/expected/<config>.json); on row shards rank 0 checks the
     # combined column lists and the system row it owns
@@ -881,16 +882,20 @@ def box_store_rate(torch, nbytes):
         return None
 
 
-def pmc_traffic(config):
-    """HBM bytes per k_rows launch from the committed PMC summary of this
-    workload (scripts/pmc.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3
-    passes of this same bench command, FETCH doubled for gfx950)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+def pmc_traffic(config, rank_of=0, rows_kernel=2):
+    """HBM bytes per launch of the matrix write's main kernel (k_rows, or
+    k_rows_w for wide rows) from the committed PMC summary of this workload
+    (scripts/pmc.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
+    same bench command, FETCH doubled for gfx950): profiles/pmc_<config>.json,
+    pmc_<config>r<N>.json for --rank-of N."""
+    name = f"pmc_{config}" + (f"r{rank_of}" if rank_of > 1 else "") + ".json"
+    path = os.path.join(ROOT, "profiles", name)
+    want = "kano::k_rows_w<" if rows_kernel in (3, 6) else "kano::k_rows<"
     try:
         with open(path) as f:
             d = json.load(f)
         # the kernel's name as rocprofv3 prints it ("void kano::k_rows<256>")
-        k = next(v for name, v in d["kernels"].items() if "kano::k_rows" in name)
+        k = next(v for nm, v in d["kernels"].items() if want in nm)
         return float(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
     except (OSError, KeyError, ValueError, TypeError, StopIteration):
         return None, None
