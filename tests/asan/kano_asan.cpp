@@ -166,6 +166,31 @@ int main() {
   std::vector<u64> dig((size_t)n);
   CHECK(kano_rows_digest(ctx, 0, n, dig.data()) == 0);
 
+  // pipelined calls (page-locked results: the direct tail, where the next
+  // call's prologue is queued behind its gate), then a matrix read (unprime)
+  {
+    void* pidx = nullptr;
+    void* ppairs = nullptr;
+    CHECK(kano_host_alloc(sizeof(int32_t) * (size_t)(4 * n), &pidx) == 0);
+    CHECK(kano_host_alloc(sizeof(int32_t) * 2 * (size_t)4000000, &ppairs) == 0);
+    CHECK(kano_set_pipeline(ctx, 1) == 0);
+    for (int rep = 0; rep < 3; ++rep) {
+      int64_t cnt2[4] = {0, 0, 0, 0}, sh2 = -1;
+      CHECK(kano_verify(ctx, KANO_PATH_AUTO, gid.data(), 0, 0, static_cast<int32_t*>(pidx), cnt2,
+                        static_cast<int32_t*>(ppairs), 4000000, &sh2) == 0);
+      CHECK(sh2 == shadow);
+      CHECK((int64_t)isol.size() == cnt2[1]);
+    }
+    CHECK(kano_get_rows(ctx, 0, n, rows.data()) == 0);
+    CHECK(rows == M);
+    CHECK(kano_verify(ctx, KANO_PATH_AUTO, gid.data(), 0, 0, static_cast<int32_t*>(pidx), counts,
+                      static_cast<int32_t*>(ppairs), 4000000, &shadow2) == 0);
+    CHECK(kano_settle(ctx) == 0);
+    CHECK(kano_set_pipeline(ctx, 0) == 0);
+    kano_host_free(pidx);
+    kano_host_free(ppairs);
+  }
+
   // error paths: every one returns an error code, none faults
   CHECK(kano_get_rows(ctx, n - 1, 2, rows.data()) == -EINVAL);
   CHECK(kano_get_rows(ctx, -1, 1, rows.data()) == -EINVAL);
