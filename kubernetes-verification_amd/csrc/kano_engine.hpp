@@ -153,6 +153,8 @@ struct kano_ctx {
   i64 dx_ldY = 0, dx_PBo = 0;
   bool dense_sel = false;    // this build takes them (do_front)
   int ac_lds = 1;            // aclds=0: AC / ACT bits by global atomics, not LDS rows
+  int mlists_side_ok = 1;    // mlside=0: the member lists on the engine stream
+  bool mlists_side = false;  // this build's member lists went to stream2 (classify_phase2a)
   bool rin_marked = false;   // this build's last Mc launch marked ev_rin_e
   i64 sel_early_cap = -1;    // the early placement's list capacity (-1: none this build)
   int path_lds = 1;          // pathlds=0: k_path_expand16 without the LDS table

@@ -338,6 +338,7 @@ int unprime(kano_ctx* ctx) {
   ctx->primed = false;
   ring_bell(ctx);
   KCHK(hipStreamSynchronize(ctx->stream));
+  KCHK(hipStreamSynchronize(ctx->stream2));   // (its member lists run on stream2)
   std::swap(ctx->sizes, ctx->sizes_alt);
   swap_rows_ptrs(ctx);
   ctx->alist_valid = ctx->prime_alist_valid;
@@ -631,31 +632,39 @@ int classify_alloc2(kano_ctx* ctx, ClassSet& cs) {
 // count; the entries past U are zero), member lists of pods [m0, m1)
 // mark: an event the member-list fill's dispatch marks (returns false, and
 // marks nothing, when there is no fill)
-int classify_phase2a(kano_ctx* ctx, hipEvent_t mark = nullptr, bool* marked = nullptr) {
-  if (marked) *marked = false;
+int classify_phase2a(kano_ctx* ctx) {
   ClsPair pr{{cls_side(ctx, ctx->rc), cls_side(ctx, ctx->cc)}};
   const i64 mr = ctx->rc.m1 - ctx->rc.m0, ma = ctx->cc.m1 - ctx->cc.m0;
   const i64 rl = std::max(mr, ma);
+  // The member lists (their offsets' scan and the fill) feed only the side
+  // work, the lists' consumers past the side stream's join (k_pods_own: the
+  // column classes' members) and the matrix write: they run on stream2,
+  // forked at the member-count pass (its dispatch marks ev_pre), so the
+  // engine stream goes from the class ids straight to the join (two launches
+  // fewer on it).  Without stream2 they stay on the engine stream.
+  hipStream_t side = ctx->mlists_side ? ctx->stream2 : nullptr;
   if (rl > 0) {   // ids and member counts in one pass
     // (several pods a thread when the previous build had few classes; the
     // kernel is correct for any count -- a full LDS table goes global)
     const i64 prevU = std::max(ctx->rc.U, ctx->cc.U);
     const int ipt = ctx->assign_ipt > 0 ? ctx->assign_ipt
                                         : (prevU > 0 && prevU <= 1024 ? ASSIGN_IPT : 1);
-    hipLaunchKernelGGL(k_cls_assign_count, dim3(nblk(rl, (i64)TPB * ipt), 2), dim3(TPB), 0,
-                       ctx->stream, pr, ipt);
+    launch_marked(k_cls_assign_count, dim3(nblk(rl, (i64)TPB * ipt), 2), dim3(TPB), 0,
+                  ctx->stream, side ? ctx->ev_pre : nullptr, pr, ipt);
     KLAUNCH();
+  } else if (side) {
+    KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
   }
-  ScanBatch sb(ctx);
+  if (side) KCHK(hipStreamWaitEvent(side, ctx->ev_pre, 0));
+  ScanBatch sb(ctx, side != nullptr);
   KTRY(sb.add(P_<int32_t>(ctx->rc.mcnt), mr, P_<int32_t>(ctx->rc.moff)));
   KTRY(sb.add(P_<int32_t>(ctx->cc.mcnt), ma, P_<int32_t>(ctx->cc.moff)));
   KTRY(sb.run());
   if (rl > 0) {
-    launch_marked(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, ctx->stream, mark, pr,
-                  (const int32_t*)nullptr, 0, (int32_t*)nullptr, (int32_t*)nullptr,
-                  reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR));
+    hipLaunchKernelGGL(k_cls_mfill, dim3(nblk(rl), 2), dim3(TPB), 0, side ? side : ctx->stream, pr,
+                       (const int32_t*)nullptr, 0, (int32_t*)nullptr, (int32_t*)nullptr,
+                       reinterpret_cast<int32_t*>(P_<u64>(ctx->sizes) + SZ_ERR));
     KLAUNCH();
-    if (marked) *marked = mark != nullptr;
   }
   return 0;
 }
@@ -835,16 +844,15 @@ int front_a(kano_ctx* ctx) {
   // host sync 1 of the build (the class counts), overlapped: the counts
   // travel while phase 2a runs
   KTRY(mirror_begin(ctx));
-  // the side work of do_back_pre needs the classes only: it forks after the
-  // member lists (their fill's dispatch marks ev_pre)
-  if (ctx->stream2) {
-    bool marked = false;
-    KTRY(classify_phase2a(ctx, ctx->ev_pre, &marked));
-    if (!marked) KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
-  } else {
+  // the member lists and then the side work of do_back_pre go to stream2,
+  // forked at the member counts (ev_pre)
+  ctx->mlists_side = ctx->stream2 != nullptr && ctx->mlists_side_ok;
+  if (!ctx->mlists_side && ctx->stream2) {
     KTRY(classify_phase2a(ctx));
+    KCHK(hipEventRecord(ctx->ev_pre, ctx->stream));
+    return 0;
   }
-  return 0;
+  return classify_phase2a(ctx);
 }
 
 // primed: the prologue was queued by the previous kano_verify (its gate is
@@ -2031,6 +2039,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "hexplds" && v >= 2 && v <= 4) ctx->heavy_expand_lds = v;
         if (k == "dx") ctx->dx_on = v;
         if (k == "aclds") ctx->ac_lds = v;
+        if (k == "mlside") ctx->mlists_side_ok = v;
         if (k == "xomfma" && v > 0) ctx->xo_mfma = (double)v * 1e12;
         if (k == "xoor" && v > 0) ctx->xo_or = (double)v * 1e9;
       }
