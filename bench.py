@@ -48,6 +48,7 @@ import numpy as np  # noqa: E402
 METRIC = "pod-pairs/sec for reachability build + all-checks latency, 100k pods, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_I8_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md: int8 MFMA 2x the BF16 rate (~2.5 PF dense)
+MFMA_F4_PEAK_TOPS = 10000.0    # MI355X_MICROARCH.md: block-scaled fp4 4x the BF16 rate (~10 PF dense)
 WORKLOADS = {
     "C2": "Synthetic 10k pods / 1k policies, Zipf labels (BASELINE configs[1])",
     "C3": "Synthetic 100k pods / 10k policies, sparse selectors (BASELINE configs[2])",
@@ -537,16 +538,22 @@ def main():
                                     "launches": ra["launches"],
                                     "how": "kano_build x %d after the timed region" % args.alone}
                                    if ra["launches"] else None)},
-            # the dense path's int8 MFMA contraction (k_heavy_mc_mfma; --path
-            # mfma or AUTO's dense choice): algorithmic ops / its event time
+            # the dense path's MFMA contraction (k_heavy_gemm_f4 / k_heavy_mc_mfma,
+            # block-scaled fp4 on 0/1 operands; --path mfma or AUTO's dense
+            # choice): algorithmic ops / its event time, against the fp4
+            # instruction's dense peak (and, for comparison with the round-5
+            # int8 form, the int8 peak)
             "mfma_roofline": ({"bound": "mfma",
                                "kernel": {1: "k_heavy_mc_or (bitwise, timed for comparison)",
-                                          2: "k_heavy_mc_mfma (split K)",
-                                          3: "k_heavy_gemm"}.get(info["HEAVY_KERNEL"], "none"),
+                                          2: "k_heavy_mc_mfma (split K, fp4)",
+                                          3: "k_heavy_gemm_f4"}.get(info["HEAVY_KERNEL"], "none"),
+                               "dtype": "fp4 e2m1 (0/1 operands), f32 accumulate",
                                "achieved": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12,
-                               "peak": MFMA_I8_PEAK_TOPS, "unit": "TOP/s",
+                               "peak": MFMA_F4_PEAK_TOPS, "unit": "TOP/s",
                                "frac": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12 /
-                                       MFMA_I8_PEAK_TOPS,
+                                       MFMA_F4_PEAK_TOPS,
+                               "frac_vs_int8_peak": mt["ops_sum"] / (mt["sum_ms"] * 1e-3) / 1e12 /
+                                                    MFMA_I8_PEAK_TOPS,
                                "ops_per_build": mt["ops_last"],
                                "avg_ms": mt["sum_ms"] / mt["builds"], "builds_timed": mt["builds"],
                                "heavy_classes": info["HEAVY"], "column_classes": info["UA"],
@@ -558,7 +565,10 @@ def main():
                                "alone": ({"avg_ms": mta["sum_ms"] / mta["builds"],
                                           "achieved": mta["ops_sum"] / (mta["sum_ms"] * 1e-3) / 1e12,
                                           "frac": mta["ops_sum"] / (mta["sum_ms"] * 1e-3) / 1e12 /
-                                                  MFMA_I8_PEAK_TOPS,
+                                                  MFMA_F4_PEAK_TOPS,
+                                          "frac_vs_int8_peak": mta["ops_sum"] /
+                                                               (mta["sum_ms"] * 1e-3) / 1e12 /
+                                                               MFMA_I8_PEAK_TOPS,
                                           "builds": mta["builds"]}
                                          if mta["builds"] and mta["sum_ms"] > 0 else None)}
                               if mt["builds"] > 0 and mt["sum_ms"] > 0 else None),

@@ -137,7 +137,7 @@ struct kano_ctx {
   int heavy_gemm = -1;       // hgemm: k_heavy_gemm's wave tile (TM TN: 22, 42, 44; 0: the
                              // split-K kernel whatever the size; -1: 44 when it has the
                              // tiles, else 22 -- the sweep's fastest at each size)
-  // AUTO's dense-path rates (xomfma TOP/s, xoor GB/s): the GEMM's int8 ops
+  // AUTO's dense-path rates (xomfma TOP/s, xoor GB/s): the GEMM's 0/1 MACs x 2
   // and the bitwise OR's Mc-word reads per second, as measured on the
   // crossover sweep (scripts/mfma_sweep.py)
   double xo_mfma = 1800e12, xo_or = 8500e9;
@@ -320,7 +320,7 @@ struct kano_ctx {
   // last one, and sums since kano_rows_timing's reset
   hipEvent_t ev_rt[2][2] = {};
   bool rows_time_pending[2] = {false, false};
-  // the heavy classes' int8 MFMA contraction (k_heavy_mc_mfma, every launch
+  // the heavy classes' MFMA contraction (k_heavy_gemm_f4 / k_heavy_mc_mfma, every launch
   // of a build between one pair of events), for kano_mfma_timing
   hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr;
   bool mfma_time_pending = false;

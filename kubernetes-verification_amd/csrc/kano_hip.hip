@@ -21,7 +21,7 @@
 //   select   selT[pb][c]: bit q = policy 64*pb+q selects row class c
 //   plan     per row class |S(c)|, rebuild cost, work items, heavy flag
 //   heavy    rows whose rebuild is expensive: Mc = OR over S(c) of AC rows
-//            (bitwise) or the int8 MFMA contraction Sel x Allow over column
+//            (bitwise) or the fp4 MFMA contraction Sel x Allow over column
 //            classes (dense path), then expanded to pods at the first member
 //   rows     (class, <=ch members, column chunk) work items: LDS row from the
 //            allowed-pod lists (light) or a copy (heavy), streamed to the
@@ -1086,7 +1086,7 @@ int do_back_pre(kano_ctx* ctx, const PreLaunch& pre_fill, const PreRun& pre_run)
 
 // lists (S(c) ascending, allowed classes + bits + pods per policy, heavy
 // list) and the compressed matrix Mc (row classes x column classes): light
-// classes by scatter, heavy classes by bitwise OR or the int8 MFMA
+// classes by scatter, heavy classes by bitwise OR or the fp4 MFMA
 // contraction; column checks at class level
 // the engine stream waits for e -- unless e has completed already: a wait
 // packet on a done event still held the stream ~5 us (the side work's joins)
@@ -1152,7 +1152,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   }
   const bool gemm = mfma && gemm_fits;
   ctx->heavy_kernel = H == 0 ? 0 : !mfma ? 1 : gemm ? 3 : 2;
-  // the staged GEMM's padded operands (k_heavy_gemm_lds): A [PBp][ldA],
+  // the staged GEMM's padded operands (k_heavy_gemm_f4): A [PBp][ldA],
   // ACT [PBp][ldB]; the unstaged kernels use ldA = H, ldB = Ua, PBp = PB
   const bool glds = gemm;
   const i64 ldA = glds ? (H + 64 * tmg - 1) / (64 * tmg) * (64 * tmg) : H;
@@ -1366,13 +1366,13 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         {
           const size_t lds = sizeof(u64) * 2 * GK_KC * (size_t)(64 * tmg + 64 * tng);
           if (hg == 22)
-            hipLaunchKernelGGL((k_heavy_gemm_lds<2, 2>), grid, dim3(TPB), lds, ctx->stream, A,
+            hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
           else if (hg == 44)
-            hipLaunchKernelGGL((k_heavy_gemm_lds<4, 4>), grid, dim3(TPB), lds, ctx->stream, A,
+            hipLaunchKernelGGL((k_heavy_gemm_f4<4, 4>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
           else
-            hipLaunchKernelGGL((k_heavy_gemm_lds<4, 2>), grid, dim3(TPB), lds, ctx->stream, A,
+            hipLaunchKernelGGL((k_heavy_gemm_f4<4, 2>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
         }
         KLAUNCH();
@@ -2068,11 +2068,11 @@ int kano_create(int device, kano_ctx** out) {
   // the staged GEMM's LDS (128 KB at 4 x 4) is above the default dynamic cap
   {
     const int lds44 = (int)(sizeof(u64) * 2 * GK_KC * (256 + 256));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<4, 4>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 4>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<4, 2>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<2, 2>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<2, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows<1024>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,

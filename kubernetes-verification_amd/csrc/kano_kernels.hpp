@@ -1758,14 +1758,14 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_or(const int32_t* __restrict__
   if (pp == 0 && wl < wc) Mc[(i64)c * ldMc + w] = red[threadIdx.x];
 }
 
-// int8 MFMA contraction (the dense path):
-//   C[h][ca] = sum_p Sel[h][p] * Allow[p][ca]   (i8 x i8 -> i32),  bit = C > 0
+// MFMA contraction (the dense path):
+//   C[h][ca] = sum_p Sel[h][p] * Allow[p][ca]   (0/1 operands),  bit = C > 0
 // A = selT[pb][c] bits of the heavy row classes, B = ACT[pb][ca] bits of the
-// column classes (class-major), both expanded to 0/1 bytes in registers.
-// v_mfma_i32_32x32x32_i8: lane l supplies A[l&31][16*(l>>5)+0..15] and
-// B[16*(l>>5)+0..15][l&31]; accumulator reg g of lane l holds row
-// (g&3)+8*(g>>2)+4*(l>>5), column l&31 (cdna_hip_programming.md §3).  Any
-// consistent k order gives the same sum, so A and B share the byte order.
+// column classes (class-major), both expanded in registers.  The 32x32 MFMA
+// forms: lane l supplies row / column l&31 of A / B and half l>>5 of the
+// K-step; accumulator reg g of lane l holds row (g&3)+8*(g>>2)+4*(l>>5),
+// column l&31 (cdna_hip_programming.md §3).  Any consistent k order gives the
+// same sum, so A and B share one bit -> element order.
 // One wave = up to 32*HT heavy rows x 32 column classes; K = all policies.
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
@@ -1781,6 +1781,26 @@ __device__ __forceinline__ i32x4 expand16(uint32_t b16) {
   r[1] = (int32_t)spread4((b16 >> 4) & 15u);
   r[2] = (int32_t)spread4((b16 >> 8) & 15u);
   r[3] = (int32_t)spread4((b16 >> 12) & 15u);
+  return r;
+}
+
+// The block-scaled fp4 MFMA's operand from 32 bits (e2m1, unit scales): nibble
+// j of register v holds bit 4 j + v of x in place -- x & 0x11.. (0.5), x &
+// 0x22.. (1.0), x & 0x44.. (2.0) -- and bit 4 j + 3 (the nibble's sign bit)
+// moved down one, (x >> 1) & 0x44.. (2.0): five instructions for the four
+// registers.  Every element is 0 or positive, so a product sum is > 0 iff
+// some k has both bits (sums of 0.25 / 1 / 4 stay exact in f32); registers
+// 4..7 (the fp8 width) are unused by e2m1.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
+constexpr int FP4_ONE_SCALE = 127;   // e8m0 2^0
+__device__ __forceinline__ i32x8 bits_to_fp4(uint32_t x) {
+  i32x8 r;
+  r[0] = (int32_t)(x & 0x11111111u);
+  r[1] = (int32_t)(x & 0x22222222u);
+  r[2] = (int32_t)(x & 0x44444444u);
+  r[3] = (int32_t)((x >> 1) & 0x44444444u);
+  r[4] = r[5] = r[6] = r[7] = 0;
   return r;
 }
 
@@ -1805,37 +1825,37 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_mfma(const u64* __restrict__ s
     const int h = t * 32 + l32;
     hc[t] = h < H ? hlist[h] : -1;
   }
-  i32x16 acc[HT];
+  f32x16 acc[HT];
 #pragma unroll
   for (int t = 0; t < HT; ++t)
 #pragma unroll
-    for (int g = 0; g < 16; ++g) acc[t][g] = 0;
+    for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
   const i64 pb0 = (i64)blockIdx.y * kchunk, pb1 = min(PB, pb0 + kchunk);
   for (i64 pb = pb0; pb < pb1; ++pb) {
+    // (one fp4 MFMA per 64-policy word: lane half `half` takes 32 of its bits)
     const u64 bw = ca < Ua ? ACT[pb * Ua + ca] : 0ull;
-    u64 aw[HT];
+    const i32x8 bfrag = bits_to_fp4((uint32_t)(bw >> (32 * half)));
 #pragma unroll
-    for (int t = 0; t < HT; ++t) aw[t] = hc[t] >= 0 ? selT[pb * U + hc[t]] : 0ull;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int sh = ks * 32 + half * 16;
-      const i32x4 bfrag = expand16((uint32_t)(bw >> sh) & 0xffffu);
-#pragma unroll
-      for (int t = 0; t < HT; ++t) {
-        const i32x4 afrag = expand16((uint32_t)(aw[t] >> sh) & 0xffffu);
-        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag, bfrag, acc[t], 0, 0, 0);
-      }
+    for (int t = 0; t < HT; ++t) {
+      const u64 aw = hc[t] >= 0 ? selT[pb * U + hc[t]] : 0ull;
+      const i32x8 afrag = bits_to_fp4((uint32_t)(aw >> (32 * half)));
+      acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(afrag, bfrag, acc[t], 4, 4, 0,
+                                                               FP4_ONE_SCALE, 0, FP4_ONE_SCALE);
     }
   }
 #pragma unroll
   for (int t = 0; t < HT; ++t) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const u64 bal = __ballot(acc[t][g] > 0);
+      const u64 bal = __ballot(acc[t][g] > 0.f);
+      // (the class of row 32 t + r from lane r's hc[t], loaded before the K loop)
+      const int r = (g & 3) + 8 * (g >> 2);
+      const int32_t c0 = __builtin_amdgcn_readlane(hc[t], r);
+      const int32_t c1 = __builtin_amdgcn_readlane(hc[t], r + 4);
       if (lane == 0 || lane == 32) {
-        const int r = t * 32 + (g & 3) + 8 * (g >> 2) + (lane == 32 ? 4 : 0);
+        const int32_t c = lane == 0 ? c0 : c1;
         const uint32_t word = lane == 0 ? (uint32_t)bal : (uint32_t)(bal >> 32);
-        if (r < H && word) atomicOr(&Mc32[(i64)hlist[r] * ldMc * 2 + jt], word);
+        if (c >= 0 && word) atomicOr(&Mc32[(i64)c * ldMc * 2 + jt], word);
       }
     }
   }
@@ -1875,37 +1895,44 @@ __global__ __launch_bounds__(TPB) void k_heavy_selT(const int32_t* __restrict__ 
 }
 
 // The dense contraction at scale (many heavy row classes, broad selectors):
-// Mc[h][ca] = (sum_p Sel[h][p] Allow[p][ca] > 0) as an int8 GEMM tiled like
-// k_path_mfma -- one wave = (32 TM heavy rows) x (32 TN column classes), each
-// A fragment feeding TN MFMAs and each B fragment TM (the bit -> byte
-// expansion, VALU, is what bounds a narrow tile); block = 2 x 2 waves; K = all
-// policies, 64 per step, no split (the grid has >= HEAVY_GEMM_MIN_TILES wave
-// tiles).  A is the heavy rows' select bits [pb][h] (k_heavy_selT), B is
-// ACT[pb][ca].  Every (row, 32-column word) belongs to one wave: plain stores
-// of the thresholded ballots into the zeroed Mc.  Blocks of one XCD (blockIdx
-// mod 8) walk a contiguous range of the tile order (GM block-rows at a time)
-// so that they share A and B panels in their L2.
-// A block's A and B panels for GK_KC K-steps at a time (GK_KC x (64 TM + 64
-// TN) words) are copied global -> LDS by the async 16-byte LDS-DMA loads
+// Mc[h][ca] = (sum_p Sel[h][p] Allow[p][ca] > 0) as a GEMM on 0/1 operands
+// tiled like k_path_mfma -- one wave = (32 TM heavy rows) x (32 TN column
+// classes), each A fragment feeding TN MFMAs and each B fragment TM; block =
+// 2 x 2 waves; K = all policies, 64 per step, no split (the grid has >=
+// HEAVY_GEMM_MIN_TILES wave tiles).  A is the heavy rows' select bits [pb][h]
+// (k_heavy_selT), B is ACT[pb][ca].  Every (row, 32-column word) belongs to
+// one wave: plain stores of the thresholded ballots into the zeroed Mc.
+// Blocks of one XCD (blockIdx mod 8) walk a contiguous range of the tile
+// order (GM block-rows at a time) so that they share A and B panels in their
+// L2.  A block's A and B panels for GK_KC K-steps at a time (GK_KC x (64 TM +
+// 64 TN) words) are copied global -> LDS by the async 16-byte LDS-DMA loads
 // (global_load_lds_dwordx4, no register staging), double-buffered: chunk c+1
-// is in flight while chunk c's 32 TM TN MFMAs per step run, so the loads'
-// latency (the operands sit in the MALL, ~1-2 us away) hides behind
-// ~16 x 1,000 cycles of matrix work instead of one step's.  The operands are
-// padded (zero) to whole block tiles and K chunks (ldA = H rounded up to
-// 64 TM, ldB = Ua rounded up to 64 TN, PB rounded up to GK_KC), so no load
-// leaves its array.  LDS: 2 x GK_KC x (64 TM + 64 TN) x 8 B (128 KB at 4 x 4).
-// (Round 5, scripts/micro/gemm_bits.hip: with the expansion removed this loop
-// reaches 0.51-0.53 of the int8 peak and the MFMAs alone 0.76-0.87; sharing
-// the expansion through LDS or streaming the words into a register ring
-// with the expansion interleaved measured slower, 0.33 / 0.42.)
+// is in flight while chunk c's MFMAs run, so the loads' latency (the operands
+// sit in the MALL, ~1-2 us away) hides behind the matrix work of 16 K-steps
+// instead of one.  The operands are padded (zero) to whole block tiles and K
+// chunks (ldA = H rounded up to 64 TM, ldB = Ua rounded up to 64 TN, PB
+// rounded up to GK_KC), so no load leaves its array.  LDS: 2 x GK_KC x (64 TM
+// + 64 TN) x 8 B (128 KB at 4 x 4).
 constexpr i64 HEAVY_GEMM_MIN_TILES = 512;
 constexpr int GK_KC = 16;
+
+// The MFMA is the block-scaled fp4 form (v_mfma_scale_f32_32x32x64_f8f6f4,
+// e2m1 operands, unit scales): the cycles of the i8 32x32x32 form at twice
+// the K, so one instruction per 64-policy word instead of two.  A 0/1 bit
+// becomes a positive fp4 value or 0, so the f32 sum is > 0 iff some policy
+// has both bits -- the bit an i8 contraction gives.  The expansion needs no
+// spread: any K order shared by A and B gives the same sum, so a lane's 32
+// bits go to its four operand registers as whole nibbles (bits_to_fp4, five
+// instructions; the round-5 i8 form spread 4 bits to 4 bytes with a multiply,
+// three instructions a register and twice the registers per K;
+// scripts/micro/gemm_f4.hip: D1's 8,000 x 10,000 x 8,000 in 0.338 ms against
+// 0.577, identical Mc).
 template <int TM, int TN>
-__global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ A, i64 ldA,
-                                                        const int32_t* __restrict__ hlist, i64 H,
-                                                        const u64* __restrict__ B, i64 ldB,
-                                                        i64 Ua, i64 PBp,
-                                                        uint32_t* __restrict__ Mc32, i64 ldMc) {
+__global__ __launch_bounds__(TPB) void k_heavy_gemm_f4(const u64* __restrict__ A, i64 ldA,
+                                                       const int32_t* __restrict__ hlist, i64 H,
+                                                       const u64* __restrict__ B, i64 ldB,
+                                                       i64 Ua, i64 PBp,
+                                                       uint32_t* __restrict__ Mc32, i64 ldMc) {
   constexpr int BM = 64 * TM, BN = 64 * TN;
   constexpr int STAGE = GK_KC * (BM + BN);     // words per buffer
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
@@ -1921,13 +1948,11 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ 
   const i64 in = L - grp * GM * nbn;
   const i64 bm = first + in % gm, bn = in / gm;
   const i64 rb0 = bm * BM, cb0 = bn * BN;
-  // the copy of one chunk: per K-step a row of BM words of A and BN of B,
-  // 128 words (1 KB) per wave instruction, the block's 4 waves round-robin
   auto stage = [&](int buf, i64 k0) {
     u64* dst = smem + (size_t)buf * STAGE;
     constexpr int PIECES = GK_KC * (BM + BN) / 128;
     for (int q = wv; q < PIECES; q += TPB / 64) {
-      const int w0 = q * 128;                         // word offset in the stage
+      const int w0 = q * 128;
       const int kk = w0 < GK_KC * BM ? w0 / BM : (w0 - GK_KC * BM) / BN;
       const u64* src = w0 < GK_KC * BM
                            ? A + (k0 + kk) * ldA + rb0 + (w0 - kk * BM)
@@ -1938,55 +1963,62 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ 
     }
   };
   const int wr = wv >> 1, wc = wv & 1;
-  i32x16 acc[TM][TN];
+  // lane l32 holds the class of the wave's row 32 t + l32 (-1 past H)
+  int32_t hrow[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const i64 row = rb0 + wr * 32 * TM + 32 * t + l32;
+    hrow[t] = row < H ? hlist[row] : -1;
+  }
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
     for (int u = 0; u < TN; ++u)
 #pragma unroll
-      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0;
+      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0.f;
   const i64 nchunks = PBp / GK_KC;
   stage(0, 0);
   for (i64 c = 0; c < nchunks; ++c) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();                                  // chunk c in LDS, chunk c-1 read by all
     if (c + 1 < nchunks) stage((int)((c + 1) & 1), (c + 1) * GK_KC);
-    const u64* As = smem + (size_t)(c & 1) * STAGE;
-    const u64* Bs = As + GK_KC * BM;
-#pragma unroll 2
+    // (a lane's 32 bits: half `half` of its row's / column's word)
+    const uint32_t* As = reinterpret_cast<const uint32_t*>(smem + (size_t)(c & 1) * STAGE) +
+                         2 * (wr * 32 * TM + l32) + half;
+    const uint32_t* Bs = reinterpret_cast<const uint32_t*>(smem + (size_t)(c & 1) * STAGE +
+                                                           GK_KC * BM) +
+                         2 * (wc * 32 * TN + l32) + half;
+#pragma unroll 4
     for (int kk = 0; kk < GK_KC; ++kk) {
-      u64 aw[TM], bw[TN];
+      i32x8 af[TM], bf[TN];
 #pragma unroll
-      for (int t = 0; t < TM; ++t) aw[t] = As[kk * BM + wr * 32 * TM + 32 * t + l32];
+      for (int t = 0; t < TM; ++t) af[t] = bits_to_fp4(As[2 * (kk * BM + 32 * t)]);
 #pragma unroll
-      for (int u = 0; u < TN; ++u) bw[u] = Bs[kk * BN + wc * 32 * TN + 32 * u + l32];
+      for (int u = 0; u < TN; ++u) bf[u] = bits_to_fp4(Bs[2 * (kk * BN + 32 * u)]);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int sh = ks * 32 + half * 16;
-        i32x4 af[TM], bf[TN];
+      for (int t = 0; t < TM; ++t)
 #pragma unroll
-        for (int t = 0; t < TM; ++t) af[t] = expand16((uint32_t)(aw[t] >> sh) & 0xffffu);
-#pragma unroll
-        for (int u = 0; u < TN; ++u) bf[u] = expand16((uint32_t)(bw[u] >> sh) & 0xffffu);
-#pragma unroll
-        for (int t = 0; t < TM; ++t)
-#pragma unroll
-          for (int u = 0; u < TN; ++u)
-            acc[t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[t], bf[u], acc[t][u], 0, 0, 0);
-      }
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+              af[t], bf[u], acc[t][u], 4, 4, 0, FP4_ONE_SCALE, 0, FP4_ONE_SCALE);
     }
   }
-  const i64 rb = rb0 + wr * 32 * TM, cb = cb0 + wc * 32 * TN;
+  const i64 cb = cb0 + wc * 32 * TN;
   const i64 ld32 = 2 * ldMc;
+  // (the rows' classes were loaded before the K loop: a load here would put a
+  // wait for every store issued so far in front of each row's ballots)
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const i64 row = rb + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
-      const int32_t hr = row < H ? hlist[row] : -1;
+      const int r = (g & 3) + 8 * (g >> 2);
+      const int32_t hr0 = __builtin_amdgcn_readlane(hrow[t], r);
+      const int32_t hr1 = __builtin_amdgcn_readlane(hrow[t], r + 4);
+      const int32_t hr = half ? hr1 : hr0;
 #pragma unroll
       for (int u = 0; u < TN; ++u) {
-        const u64 bal = __ballot(acc[t][u][g] > 0);
+        const u64 bal = __ballot(acc[t][u][g] > 0.f);
         const i64 c32 = (cb + 32 * u) >> 5;
         if (l32 == 0 && hr >= 0 && c32 < ld32)
           Mc32[(i64)hr * ld32 + c32] = half ? (uint32_t)(bal >> 32) : (uint32_t)bal;

@@ -1,6 +1,6 @@
 """The dense path's crossover: the heavy classes' Mc rows by the bitwise OR
 (k_heavy_mc_or, reads ldMc words per (heavy class, policy in S(c))) against
-the int8 MFMA GEMM (k_heavy_gemm, 2 H P Ua ops whatever the density) and the
+the fp4 MFMA GEMM (k_heavy_gemm_f4, 2 H P Ua ops whatever the density) and the
 split-K MFMA kernel (k_heavy_mc_mfma), on `dense` clusters (kano/synth.py)
 whose selector density broad/tenants is swept at a fixed class count.
 
@@ -26,7 +26,6 @@ sys.path.insert(0, os.path.join(ROOT, "kubernetes-verification_amd"))
 
 VARIANTS = [("bitwise", "bitwise", "hortime=1"), ("gemm22", "mfma", "hgemm=22"),
             ("gemm42", "mfma", "hgemm=42"), ("gemm44", "mfma", "hgemm=44"),
-            ("gemm22reg", "mfma", "hgemm=22,hglds=0"), ("gemm44reg", "mfma", "hgemm=44,hglds=0"),
             ("splitk", "mfma", "hgemm=0"), ("auto", "auto", "hortime=1")]
 
 

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "kano_kernels.hpp"
+#include "gemm_i8_ref.hpp"
 
 using namespace kano;
 

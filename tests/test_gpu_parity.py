@@ -116,13 +116,11 @@ def test_golden_cluster_api(name):
 @pytest.mark.parametrize("name", ["s_broad_300", "s_broad_1000", "s_sparse_1000",
                                   "s_sparse_2000", "q_dirs", "q_shadow"])
 @pytest.mark.parametrize("path", ["bitwise", "mfma", "auto", "mfma-gemm22", "mfma-gemm42",
-                                  "mfma-gemm44", "mfma-gemm22reg", "mfma-gemm44reg", "mfma-dx",
-                                  "mfma-dx22", "bitwise-dx"])
+                                  "mfma-gemm44", "mfma-dx", "mfma-dx22", "bitwise-dx"])
 def test_build_paths_agree(name, path, monkeypatch):
-    """The bitwise (LDS scatter / OR) and int8-MFMA contraction paths -- the
-    split-K kernel and the tiled GEMM in its three wave tiles, operands
-    staged through LDS or read from global memory (reg), forced at these
-    sizes (hgemmmin=1) -- give kano_py's matrix and column checks."""
+    """The bitwise (LDS scatter / OR) and fp4-MFMA contraction paths -- the
+    split-K kernel and the tiled GEMM in its three wave tiles, forced at
+    these sizes (hgemmmin=1) -- give kano_py's matrix and column checks."""
     from kano._engine import DeviceBuild
     from kano._intern import intern
     if path == "mfma-dx":    # the dense path's bit matrices; A is SA as it stands
@@ -136,8 +134,7 @@ def test_build_paths_agree(name, path, monkeypatch):
         path = "bitwise"
     if path.startswith("mfma-gemm"):
         tile = path[len("mfma-gemm"):len("mfma-gemm") + 2]
-        monkeypatch.setenv("KANO_TUNE", f"hgemm={tile},hgemmmin=1" +
-                           (",hglds=0" if path.endswith("reg") else ""))
+        monkeypatch.setenv("KANO_TUNE", f"hgemm={tile},hgemmmin=1")
         path = "mfma"
     obj = cluster(name)
     cs, ps = api_objects(obj)
