@@ -134,9 +134,8 @@ struct kano_ctx {
                              // holds more than path_dens % of the class-level bits
   int path_tm = 2;           // pathtm / pathtn: k_path_mfma tiles per wave
   int path_tn = 2;
-  int heavy_gemm = -1;       // hgemm: k_heavy_gemm's wave tile (TM TN: 22, 42, 44; 0: the
-                             // split-K kernel whatever the size; -1: 44 when it has the
-                             // tiles, else 22 -- the sweep's fastest at each size)
+  int heavy_gemm = -1;       // hgemm: k_heavy_gemm_f4's wave tile (TM TN: 22, 42, 44; 0:
+                             // the split-K kernel whatever the size; -1: 22)
   // AUTO's dense-path rates (xomfma TOP/s, xoor GB/s): the GEMM's 0/1 MACs x 2
   // and the bitwise OR's Mc-word reads per second, as measured on the
   // crossover sweep (scripts/mfma_sweep.py)

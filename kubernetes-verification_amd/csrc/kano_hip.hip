@@ -1119,8 +1119,12 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   auto wave_tiles = [&](int tm, int tn) {
     return ((H + 32 * tm - 1) / (32 * tm)) * ((ctx->cc.U + 32 * tn - 1) / (32 * tn));
   };
+  // (2 x 2 wave tiles: 64 KB of LDS and 140 registers a wave, so two blocks
+  // share a CU -- as fast as 4 x 4 alone, and 0.47 -> 0.39 ms in D1's step,
+  // where the previous step's heavy-row write holds part of every CU;
+  // profiles/r06_f4/d1_tile_ab.jsonl)
   int hg = ctx->heavy_gemm;
-  if (hg < 0) hg = wave_tiles(4, 4) >= ctx->heavy_gemm_min ? 44 : 22;
+  if (hg < 0) hg = 22;
   const int tmg = hg / 10, tng = hg % 10;
   const i64 gtiles = tmg > 0 ? wave_tiles(tmg, tng) : 0;
   const bool gemm_fits = tmg > 0 && (ctx->PB + GK_KC) * 8 * (TPB / 64) <= 64 * 1024 &&
@@ -1364,15 +1368,16 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         KTRY(resolve_mfma_time(ctx));
         KCHK(hipEventRecord(ctx->ev_m0, ctx->stream));
         {
-          const size_t lds = sizeof(u64) * 2 * GK_KC * (size_t)(64 * tmg + 64 * tng);
+          const size_t lds =
+              sizeof(u64) * 2 * gemm_kc(tmg, tng) * (size_t)(64 * tmg + 64 * tng);
           if (hg == 22)
-            hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2>), grid, dim3(TPB), lds, ctx->stream, A,
+            hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2, gemm_kc(2, 2)>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
           else if (hg == 44)
-            hipLaunchKernelGGL((k_heavy_gemm_f4<4, 4>), grid, dim3(TPB), lds, ctx->stream, A,
+            hipLaunchKernelGGL((k_heavy_gemm_f4<4, 4, gemm_kc(4, 4)>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
           else
-            hipLaunchKernelGGL((k_heavy_gemm_f4<4, 2>), grid, dim3(TPB), lds, ctx->stream, A,
+            hipLaunchKernelGGL((k_heavy_gemm_f4<4, 2, gemm_kc(4, 2)>), grid, dim3(TPB), lds, ctx->stream, A,
                                ldA, hl, H, P_<u64>(ctx->ACT), ldB, Ua, PBp, out, ldMc);
         }
         KLAUNCH();
@@ -2068,11 +2073,11 @@ int kano_create(int device, kano_ctx** out) {
   // the staged GEMM's LDS (128 KB at 4 x 4) is above the default dynamic cap
   {
     const int lds44 = (int)(sizeof(u64) * 2 * GK_KC * (256 + 256));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 4>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 4, gemm_kc(4, 4)>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 2>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 2, gemm_kc(4, 2)>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<2, 2>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<2, 2, gemm_kc(2, 2)>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds44);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows<1024>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -1767,23 +1767,6 @@ __global__ __launch_bounds__(TPB) void k_heavy_mc_or(const int32_t* __restrict__
 // column l&31 (cdna_hip_programming.md §3).  Any consistent k order gives the
 // same sum, so A and B share one bit -> element order.
 // One wave = up to 32*HT heavy rows x 32 column classes; K = all policies.
-typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
-typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-
-// bit i of b4 -> bit 8 i: b4 * (1 + 2^7 + 2^14 + 2^21) puts bit i at i, i+7,
-// i+14, i+21 (no carries); the mask keeps bit 8 i (one v_mul_u32_u24 + and)
-__device__ __forceinline__ uint32_t spread4(uint32_t b4) {
-  return __umul24(b4, 0x204081u) & 0x01010101u;
-}
-__device__ __forceinline__ i32x4 expand16(uint32_t b16) {
-  i32x4 r;
-  r[0] = (int32_t)spread4(b16 & 15u);
-  r[1] = (int32_t)spread4((b16 >> 4) & 15u);
-  r[2] = (int32_t)spread4((b16 >> 8) & 15u);
-  r[3] = (int32_t)spread4((b16 >> 12) & 15u);
-  return r;
-}
-
 // The block-scaled fp4 MFMA's operand from 32 bits (e2m1, unit scales): nibble
 // j of register v holds bit 4 j + v of x in place -- x & 0x11.. (0.5), x &
 // 0x22.. (1.0), x & 0x44.. (2.0) -- and bit 4 j + 3 (the nibble's sign bit)
@@ -1904,17 +1887,21 @@ __global__ __launch_bounds__(TPB) void k_heavy_selT(const int32_t* __restrict__ 
 // one wave: plain stores of the thresholded ballots into the zeroed Mc.
 // Blocks of one XCD (blockIdx mod 8) walk a contiguous range of the tile
 // order (GM block-rows at a time) so that they share A and B panels in their
-// L2.  A block's A and B panels for GK_KC K-steps at a time (GK_KC x (64 TM +
-// 64 TN) words) are copied global -> LDS by the async 16-byte LDS-DMA loads
+// L2.  A block's A and B panels for KC K-steps at a time (KC x (64 TM + 64
+// TN) words) are copied global -> LDS by the async 16-byte LDS-DMA loads
 // (global_load_lds_dwordx4, no register staging), double-buffered: chunk c+1
 // is in flight while chunk c's MFMAs run, so the loads' latency (the operands
-// sit in the MALL, ~1-2 us away) hides behind the matrix work of 16 K-steps
+// sit in the MALL, ~1-2 us away) hides behind the matrix work of KC K-steps
 // instead of one.  The operands are padded (zero) to whole block tiles and K
 // chunks (ldA = H rounded up to 64 TM, ldB = Ua rounded up to 64 TN, PB
-// rounded up to GK_KC), so no load leaves its array.  LDS: 2 x GK_KC x (64 TM
-// + 64 TN) x 8 B (128 KB at 4 x 4).
+// rounded up to GK_KC, a multiple of every KC), so no load leaves its array.
+// LDS: 2 x KC x (64 TM + 64 TN) x 8 B (KC K-steps a chunk: 32 KB at 2 x 2 and
+// KC = 8, the engine's form; 128 KB at 4 x 4 and KC = 16).
 constexpr i64 HEAVY_GEMM_MIN_TILES = 512;
 constexpr int GK_KC = 16;
+// the engine's chunk depth for a wave tile: 2 x 2 stages 8 K-steps (32 KB, so
+// that several blocks share a CU), the wide tiles 16
+constexpr int gemm_kc(int tm, int tn) { return tm == 2 && tn == 2 ? 8 : GK_KC; }
 
 // The MFMA is the block-scaled fp4 form (v_mfma_scale_f32_32x32x64_f8f6f4,
 // e2m1 operands, unit scales): the cycles of the i8 32x32x32 form at twice
@@ -1927,14 +1914,14 @@ constexpr int GK_KC = 16;
 // three instructions a register and twice the registers per K;
 // scripts/micro/gemm_f4.hip: D1's 8,000 x 10,000 x 8,000 in 0.338 ms against
 // 0.577, identical Mc).
-template <int TM, int TN>
+template <int TM, int TN, int KC>
 __global__ __launch_bounds__(TPB) void k_heavy_gemm_f4(const u64* __restrict__ A, i64 ldA,
                                                        const int32_t* __restrict__ hlist, i64 H,
                                                        const u64* __restrict__ B, i64 ldB,
                                                        i64 Ua, i64 PBp,
                                                        uint32_t* __restrict__ Mc32, i64 ldMc) {
   constexpr int BM = 64 * TM, BN = 64 * TN;
-  constexpr int STAGE = GK_KC * (BM + BN);     // words per buffer
+  constexpr int STAGE = KC * (BM + BN);        // words per buffer
   extern __shared__ __attribute__((aligned(16))) u64 smem[];
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
   const int wv = threadIdx.x >> 6;
@@ -1950,13 +1937,13 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm_f4(const u64* __restrict__ A
   const i64 rb0 = bm * BM, cb0 = bn * BN;
   auto stage = [&](int buf, i64 k0) {
     u64* dst = smem + (size_t)buf * STAGE;
-    constexpr int PIECES = GK_KC * (BM + BN) / 128;
+    constexpr int PIECES = KC * (BM + BN) / 128;
     for (int q = wv; q < PIECES; q += TPB / 64) {
       const int w0 = q * 128;
-      const int kk = w0 < GK_KC * BM ? w0 / BM : (w0 - GK_KC * BM) / BN;
-      const u64* src = w0 < GK_KC * BM
+      const int kk = w0 < KC * BM ? w0 / BM : (w0 - KC * BM) / BN;
+      const u64* src = w0 < KC * BM
                            ? A + (k0 + kk) * ldA + rb0 + (w0 - kk * BM)
-                           : B + (k0 + kk) * ldB + cb0 + (w0 - GK_KC * BM - kk * BN);
+                           : B + (k0 + kk) * ldB + cb0 + (w0 - KC * BM - kk * BN);
       __builtin_amdgcn_global_load_lds(
           reinterpret_cast<const void*>(src + 2 * lane),
           (__attribute__((address_space(3))) void*)(dst + w0), 16, 0, 0);
@@ -1977,20 +1964,20 @@ __global__ __launch_bounds__(TPB) void k_heavy_gemm_f4(const u64* __restrict__ A
     for (int u = 0; u < TN; ++u)
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[t][u][g] = 0.f;
-  const i64 nchunks = PBp / GK_KC;
+  const i64 nchunks = PBp / KC;
   stage(0, 0);
   for (i64 c = 0; c < nchunks; ++c) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();                                  // chunk c in LDS, chunk c-1 read by all
-    if (c + 1 < nchunks) stage((int)((c + 1) & 1), (c + 1) * GK_KC);
+    if (c + 1 < nchunks) stage((int)((c + 1) & 1), (c + 1) * KC);
     // (a lane's 32 bits: half `half` of its row's / column's word)
     const uint32_t* As = reinterpret_cast<const uint32_t*>(smem + (size_t)(c & 1) * STAGE) +
                          2 * (wr * 32 * TM + l32) + half;
     const uint32_t* Bs = reinterpret_cast<const uint32_t*>(smem + (size_t)(c & 1) * STAGE +
-                                                           GK_KC * BM) +
+                                                           KC * BM) +
                          2 * (wc * 32 * TN + l32) + half;
 #pragma unroll 4
-    for (int kk = 0; kk < GK_KC; ++kk) {
+    for (int kk = 0; kk < KC; ++kk) {
       i32x8 af[TM], bf[TN];
 #pragma unroll
       for (int t = 0; t < TM; ++t) af[t] = bits_to_fp4(As[2 * (kk * BM + 32 * t)]);

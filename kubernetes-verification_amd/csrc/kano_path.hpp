@@ -12,9 +12,10 @@
 // depends on rc(j) only).  Two kernels compute the step:
 //   * k_path_or: semi-naive bit-packed OR -- only the bits that are new in
 //     R_k (the delta D_k) are expanded: R_{k+1} = R_k | OR_{b in D_k} T[b].
-//   * k_path_mfma: the boolean contraction R_k . T as an int8 MFMA GEMM
-//     (v_mfma_i32_32x32x32_i8) on bits expanded in registers, thresholded
-//     > 0 and OR-ed with Mc in the epilogue (dense R_k).
+//   * k_path_mfma: the boolean contraction R_k . T as an MFMA GEMM on the
+//     block-scaled fp4 form (v_mfma_scale_f32_32x32x64_f8f6f4) over bits
+//     expanded in registers, thresholded > 0 and OR-ed with Mc in the
+//     epilogue (dense R_k).
 // k_path_expand writes the pod matrix: P[i] bit j = R[rc(i)][cc(j)].
 // After an edit of M the classes are the pods themselves (identity).
 #pragma once
@@ -255,21 +256,20 @@ __global__ __launch_bounds__(TPB) void k_bit_transpose(const u64* __restrict__ X
   }
 }
 
-typedef int32_t p_i32x16 __attribute__((ext_vector_type(16)));
-typedef int32_t p_i32x4 __attribute__((ext_vector_type(4)));
+typedef float p_f32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t p_i32x8 __attribute__((ext_vector_type(8)));
 
-// 16 bits -> 16 int8 lanes of 0 / 1 (bit t -> byte t).  4 bits -> 4 bytes
-// is one 24-bit multiply: b * (1 + 2^7 + 2^14 + 2^21) puts bit i at bits
-// i, i+7, i+14, i+21 (no carries), and the mask keeps bit i at 8 i.
-__device__ __forceinline__ uint32_t pspread4(uint32_t b4) {
-  return __umul24(b4, 0x204081u) & 0x01010101u;
-}
-__device__ __forceinline__ p_i32x4 pexpand16(uint32_t b16) {
-  p_i32x4 r;
-  r[0] = (int32_t)pspread4(b16 & 15u);
-  r[1] = (int32_t)pspread4((b16 >> 4) & 15u);
-  r[2] = (int32_t)pspread4((b16 >> 8) & 15u);
-  r[3] = (int32_t)pspread4((b16 >> 12) & 15u);
+// 32 bits -> the block-scaled fp4 MFMA's operand (e2m1, unit scales): nibble
+// j of register v holds bit 4 j + v in place (0.5 / 1.0 / 2.0) or, for the
+// nibble's sign bit, moved down one (2.0); every element is 0 or positive
+// (kano_kernels.hpp bits_to_fp4, the same map)
+__device__ __forceinline__ p_i32x8 pbits_to_fp4(uint32_t x) {
+  p_i32x8 r;
+  r[0] = (int32_t)(x & 0x11111111u);
+  r[1] = (int32_t)(x & 0x22222222u);
+  r[2] = (int32_t)(x & 0x44444444u);
+  r[3] = (int32_t)((x >> 1) & 0x44444444u);
+  r[4] = r[5] = r[6] = r[7] = 0;
   return r;
 }
 
@@ -286,9 +286,10 @@ struct PathMfmaArgs {
 };
 
 // R_{k+1} = Mc | (R_k . T > 0).  One wave = (32*TM rows) x (32*TN columns);
-// K = 64 column classes per step, two v_mfma_i32_32x32x32_i8 per tile pair.
-// A and B fragments are the same 16-bit slices of their words expanded to
-// int8 0/1 (the same k order on both sides gives the same dot product).
+// K = 64 column classes per step, one v_mfma_scale_f32_32x32x64_f8f6f4 per
+// tile pair (fp4 operands, f32 sums of positive terms: > 0 iff some k has
+// both bits).  Lane half h takes bits 32 h .. 32 h + 31 of its A and B words
+// (the same k order on both sides gives the same dot product).
 template <int TM, int TN>
 __global__ __launch_bounds__(TPB) void k_path_mfma(PathMfmaArgs a) {
   const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
@@ -309,35 +310,28 @@ __global__ __launch_bounds__(TPB) void k_path_mfma(PathMfmaArgs a) {
   const i64 tm = bm * 2 + (wv >> 1), tn = bn * 2 + (wv & 1);
   const i64 rb = tm * 32 * TM, cb = tn * 32 * TN;
   if (rb >= a.ldA) return;                            // wave-uniform
-  p_i32x16 acc[TM][TN];
+  p_f32x16 acc[TM][TN];
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
     for (int u = 0; u < TN; ++u)
 #pragma unroll
-      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0;
-  const u64* pa = a.A + rb + l32;
-  const u64* pb = a.B + cb + l32;
+      for (int g = 0; g < 16; ++g) acc[t][u][g] = 0.f;
+  // (the lane's 32-bit half of each word)
+  const uint32_t* pa = reinterpret_cast<const uint32_t*>(a.A + rb + l32) + half;
+  const uint32_t* pb = reinterpret_cast<const uint32_t*>(a.B + cb + l32) + half;
   for (i64 kw = 0; kw < a.KW; ++kw) {
-    u64 aw[TM], bw[TN];
+    p_i32x8 af[TM], bf[TN];
 #pragma unroll
-    for (int t = 0; t < TM; ++t) aw[t] = pa[kw * a.ldA + 32 * t];
+    for (int t = 0; t < TM; ++t) af[t] = pbits_to_fp4(pa[2 * (kw * a.ldA + 32 * t)]);
 #pragma unroll
-    for (int u = 0; u < TN; ++u) bw[u] = pb[kw * a.ldB + 32 * u];
+    for (int u = 0; u < TN; ++u) bf[u] = pbits_to_fp4(pb[2 * (kw * a.ldB + 32 * u)]);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int sh = ks * 32 + half * 16;
-      p_i32x4 af[TM], bf[TN];
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int t = 0; t < TM; ++t) af[t] = pexpand16((uint32_t)(aw[t] >> sh) & 0xffffu);
-#pragma unroll
-      for (int u = 0; u < TN; ++u) bf[u] = pexpand16((uint32_t)(bw[u] >> sh) & 0xffffu);
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int u = 0; u < TN; ++u)
-          acc[t][u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[t], bf[u], acc[t][u], 0, 0, 0);
-    }
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[t], bf[u], acc[t][u], 4, 4,
+                                                                    0, 127, 0, 127);
   }
   // epilogue: accumulator g of lane (l32, half) is row (g&3) + 8*(g>>2) +
   // 4*half, column l32 of its tile; one ballot per g gives 32 columns of two
@@ -354,7 +348,7 @@ __global__ __launch_bounds__(TPB) void k_path_mfma(PathMfmaArgs a) {
       const i64 c32 = (cb + 32 * u) >> 5;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const u64 bal = __ballot(acc[t][u][g] > 0);
+        const u64 bal = __ballot(acc[t][u][g] > 0.f);
         if (l32 == 0) {
           const i64 row = rb + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
           if (row < a.rows && c32 < ld32) {

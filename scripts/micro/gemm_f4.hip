@@ -2,7 +2,8 @@
 // on bit-packed operands, D1's shape (8,000 x 10,000 x 8,000) by default:
 //   i8   k_heavy_gemm_lds<4,4>  (v_mfma_i32_32x32x32_i8, bits spread to bytes)
 //   f4   k_heavy_gemm_f4<4,4>   (v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 nibbles)
-//   f4_42 / f4_22               (smaller wave tiles)
+//   f4_42 / f4_22               (smaller wave tiles; f4_22k8: 8 K-steps a chunk,
+//                               the engine's form)
 // Every form's Mc must equal the i8 form's word for word, and the i8 form a
 // host reference on sampled rows.  Prints one line per kernel: median / best
 // of `reps` launches, TOP/s, and the fraction of the int8 (5 POP/s) and fp4
@@ -181,11 +182,11 @@ int main(int argc, char** argv) {
   auto lds_of = [](int tm, int tn) { return (int)(sizeof(u64) * 2 * GK_KC * (64 * tm + 64 * tn)); };
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_lds<4, 4>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(4, 4)));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 4>),
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 4, 16>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(4, 4)));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 2>),
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 2, 16>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(4, 2)));
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<2, 2>),
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<2, 2, 16>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(2, 2)));
   auto grid_of = [&](int tm, int tn) {
     const i64 nb = ((H + 64 * tm - 1) / (64 * tm)) * ((Ua + 64 * tn - 1) / (64 * tn));
@@ -236,22 +237,30 @@ int main(int argc, char** argv) {
   i64 bad_forms = 0;
   CK(hipMemset(dM1, 0, mcb));
   timeit("f4", [&] {
-    hipLaunchKernelGGL((k_heavy_gemm_f4<4, 4>), grid_of(4, 4), dim3(TPB), lds_of(4, 4), 0, dA,
+    hipLaunchKernelGGL((k_heavy_gemm_f4<4, 4, 16>), grid_of(4, 4), dim3(TPB), lds_of(4, 4), 0, dA,
                        ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
   });
   bad_forms += compare("f4") != 0;
   CK(hipMemset(dM1, 0, mcb));
   timeit("f4_42", [&] {
-    hipLaunchKernelGGL((k_heavy_gemm_f4<4, 2>), grid_of(4, 2), dim3(TPB), lds_of(4, 2), 0, dA,
+    hipLaunchKernelGGL((k_heavy_gemm_f4<4, 2, 16>), grid_of(4, 2), dim3(TPB), lds_of(4, 2), 0, dA,
                        ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
   });
   bad_forms += compare("f4_42") != 0;
   CK(hipMemset(dM1, 0, mcb));
   timeit("f4_22", [&] {
-    hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2>), grid_of(2, 2), dim3(TPB), lds_of(2, 2), 0, dA,
+    hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2, 16>), grid_of(2, 2), dim3(TPB), lds_of(2, 2), 0, dA,
                        ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
   });
   bad_forms += compare("f4_22") != 0;
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<2, 2, 8>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(2, 2) / 2));
+  CK(hipMemset(dM1, 0, mcb));
+  timeit("f4_22k8", [&] {   // the engine's form
+    hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2, 8>), grid_of(2, 2), dim3(TPB), lds_of(2, 2) / 2, 0,
+                       dA, ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
+  });
+  bad_forms += compare("f4_22k8") != 0;
   {
     const int l8 = (int)(sizeof(u64) * 2 * 8 * 512), l32 = (int)(sizeof(u64) * 2 * 32 * 256);
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_f4_var<4, 4, 8, 0>),
@@ -274,6 +283,22 @@ int main(int argc, char** argv) {
                          H, dB, ldB, Ua, PBp, o1, ldMc);
     });
     if (PBp % 32 == 0) bad_forms += compare("22kc32") != 0;
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_f4_var<2, 2, 8, 0>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(u64) * 2 * 8 * 256)));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_f4_var<2, 2, 16, 0>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(2, 2)));
+    CK(hipMemset(dM1, 0, mcb));
+    timeit("22kc8", [&] {
+      hipLaunchKernelGGL((k_f4_var<2, 2, 8, 0>), grid_of(2, 2), dim3(TPB), (int)(sizeof(u64) * 2 * 8 * 256), 0, dA, ldA, dl,
+                         H, dB, ldB, Ua, PBp, o1, ldMc);
+    });
+    bad_forms += compare("22kc8") != 0;
+    CK(hipMemset(dM1, 0, mcb));
+    timeit("22kc16v", [&] {
+      hipLaunchKernelGGL((k_f4_var<2, 2, 16, 0>), grid_of(2, 2), dim3(TPB), lds_of(2, 2), 0, dA, ldA, dl,
+                         H, dB, ldB, Ua, PBp, o1, ldMc);
+    });
+    bad_forms += compare("22kc16v") != 0;
     timeit("noexp", [&] {
       hipLaunchKernelGGL((k_f4_var<4, 4, 16, 1>), grid_of(4, 4), dim3(TPB), lds_of(4, 4), 0, dA,
                          ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);

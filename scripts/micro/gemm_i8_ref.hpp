@@ -6,6 +6,25 @@
 #include "kano_kernels.hpp"
 
 namespace kano {
+
+// bits -> int8 0/1 bytes (the round-5 expansion)
+typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+// bit i of b4 -> bit 8 i: b4 * (1 + 2^7 + 2^14 + 2^21) puts bit i at i, i+7,
+// i+14, i+21 (no carries); the mask keeps bit 8 i (one v_mul_u32_u24 + and)
+__device__ __forceinline__ uint32_t spread4(uint32_t b4) {
+  return __umul24(b4, 0x204081u) & 0x01010101u;
+}
+__device__ __forceinline__ i32x4 expand16(uint32_t b16) {
+  i32x4 r;
+  r[0] = (int32_t)spread4(b16 & 15u);
+  r[1] = (int32_t)spread4((b16 >> 4) & 15u);
+  r[2] = (int32_t)spread4((b16 >> 8) & 15u);
+  r[3] = (int32_t)spread4((b16 >> 12) & 15u);
+  return r;
+}
+
 template <int TM, int TN>
 __global__ __launch_bounds__(TPB) void k_heavy_gemm_lds(const u64* __restrict__ A, i64 ldA,
                                                         const int32_t* __restrict__ hlist, i64 H,

@@ -13,7 +13,7 @@ for rep in $(seq 1 ${REPS:-2}); do
     python3 -c "
 import json
 d=json.loads(open('gpurun_out/ab.json').read().strip().splitlines()[-1])
-print(json.dumps({'tune':'$t','mean':round(d['ms_per_step'],4),'median':d['step_ms']['median'],'verified':d['verified'],'rows_ms':round(d['roofline']['avg_launch_ms'],4),'cus':d['roofline']['cus']}))" >> gpurun_out/tune_ab.jsonl
+print(json.dumps({'tune':'$t','mean':round(d['ms_per_step'],4),'median':d['step_ms']['median'],'verified':d['verified'],'rows_ms':round(d['roofline']['avg_launch_ms'],4),'cus':d['roofline']['cus'],'gemm_ms':round((d.get('mfma_roofline') or {}).get('avg_ms',0),4)}))" >> gpurun_out/tune_ab.jsonl
   done
 done
 cat gpurun_out/tune_ab.jsonl
