@@ -138,8 +138,9 @@ struct kano_ctx {
                              // the split-K kernel whatever the size; -1: 22)
   // AUTO's dense-path rates (xomfma TOP/s, xoor GB/s): the GEMM's 0/1 MACs x 2
   // and the bitwise OR's Mc-word reads per second, as measured on the
-  // crossover sweep (scripts/mfma_sweep.py)
-  double xo_mfma = 1800e12, xo_or = 8500e9;
+  // crossover sweep (scripts/mfma_sweep.py; round 6, the fp4 GEMM's 2 x 2 tile:
+  // 4,500-4,700 TOP/s at >= 2,048 wave tiles, profiles/r06_mfma_sweep.jsonl)
+  double xo_mfma = 4500e12, xo_or = 8500e9;
   i64 heavy_gemm_min = 512;     // HEAVY_GEMM_MIN_TILES (kano_kernels.hpp)   // hgemmmin: the GEMM's minimum wave tiles
   int time_or = 0;           // hortime=1: k_heavy_mc_or timed like the MFMA kernels
   int heavy_expand_lds = 2;  // hexplds: heavy rows by wave transposes (k_heavy_rows_t):

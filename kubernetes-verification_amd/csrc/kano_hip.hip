@@ -1138,8 +1138,8 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         // the MFMA does 2 H P Ua ops whatever the density, the OR reads
         // ldMc words per (heavy class, policy in S(c)): the cheaper by the
         // measured rates ("The dense path: crossover")
-        // (the GEMM's rate falls below ~2,048 wave tiles of 32 x 32: 1,030
-        // TOP/s at 1,024 tiles against 1,880 at 8,000 or more)
+        // (the GEMM's rate falls below ~2,048 wave tiles: the 2 x 2 tile at
+        // H = Ua = 2,000, 1,024 tiles, 2,190 TOP/s against 4,670 at 8,000)
         const double fill = std::pow(std::min(1.0, (double)gtiles / 2048.0), 0.85);
         const double t_mfma =
             2.0 * (double)H * (double)P * (double)ctx->cc.U / (ctx->xo_mfma * fill);

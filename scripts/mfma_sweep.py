@@ -74,7 +74,7 @@ def main():
     variants = VARIANTS
     if a.quick:
         points = [(4, 2000, 0.02), (4, 2000, 0.2), (4, 2000, 0.9)]
-        variants = [v for v in VARIANTS if v[0] in ("bitwise", "gemm22", "gemm44", "gemm44reg",
+        variants = [v for v in VARIANTS if v[0] in ("bitwise", "gemm22", "gemm44",
                                                      "auto")]
     for T, A, b in points:
         t0 = time.perf_counter()
