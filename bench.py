@@ -418,6 +418,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # the pipelined calls' gates: how long each held the engine stream (its
+    # idle time at the step boundary, device wall clock, no profiler)
+    eng.gate_timing(reset=True)
     # k_rows' HIP-event times accumulate in the engine over the timed steps
     # (read once afterwards: kano_verify returns before its matrix write ends)
     eng.rows_timing(reset=True)
@@ -455,6 +458,7 @@ def main():
                    }.get(info["ROWS_KERNEL"], "none")
     mt = eng.mfma_timing()
     host = eng.host_times()
+    gate = eng.gate_timing() if pipelined else None
     # k_rows alone (untimed, after the timed region): the same matrix write of
     # the same inputs with nothing beside it -- kano_build, which waits for its
     # write, so the write takes every CU (in the timed steps it runs on a
@@ -594,6 +598,12 @@ def main():
                                               - host["tailwait_sum"]) / max(1.0, host["calls"]), 1),
                          "between_mean": round(host["gap_sum"] / max(1.0, host["calls"] - 1), 1)}
                         if host["calls"] > 0 else None),
+            # the engine stream's idle time at the step boundary: how long each
+            # pipelined call's gate held it (from the previous call's last
+            # engine-stream kernel to this call's bell; device wall clock over
+            # the last <= 64 timed steps, kano_gate_timing)
+            "boundary_idle_us": ({"mean": round(gate["mean_us"], 1), "max": round(gate["max_us"], 1),
+                                  "gates": gate["gates"]} if gate and gate["gates"] else None),
             "classes": info["U"], "nnz_select": info["NNZ_SEL"], "nnz_allow": info["NNZ_ALW"],
             "heavy_classes": info["HEAVY"], "shadow_pairs": shadow_cnt,
             "result_sizes": {k: int(len(v)) for k, v in res.items() if hasattr(v, "__len__")},

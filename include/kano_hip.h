@@ -212,6 +212,15 @@ int kano_set_pipeline(kano_ctx* ctx, int on);
  * waited for.  Afterwards no engine work is pending on the device. */
 int kano_settle(kano_ctx* ctx);
 
+/* The pipelined calls' gates (kano_set_pipeline): how long each held the
+ * engine stream -- from the end of the previous call's last engine-stream
+ * kernel to the next call's bell, i.e. that stream's idle time at the step
+ * boundary, timed on the device's wall clock without a profiler.  Over the
+ * last min(64, gates since the last reset) gates; settles first.  reset != 0
+ * starts a new window. */
+int kano_gate_timing(kano_ctx* ctx, int reset, int64_t* gates, double* mean_us,
+                     double* max_us);
+
 /* kano_verify for one row shard of a multi-GPU build, in two
  * halves around the ranks' exchange step.
  *   kano_verify_shard: the build of this shard's rows and every check up to

@@ -313,6 +313,10 @@ struct kano_ctx {
   u64* bell_dev = nullptr;
   u64 bell_seq = 0;
   u64 gate_ticks = 0;              // k_gate's timeout in wall-clock ticks (200 ms)
+  u64 wall_khz = 100000;           // the device's wall clock (k_gate's ticks)
+  DBuf gate_wait;                  // k_gate's waits, a ring of GATE_RING slots
+  u64 gate_seq0 = 0;               // bell_seq at kano_gate_timing's last reset
+  u64 gate_forced = 0;             // the last gate an unprime opened
   DBuf sizes_alt;                  // the size slots the primed prologue writes
   hipEvent_t ev_tail = nullptr;    // the result copies of kano_verify's tail
   // the matrix write's launch times (ev_rt[set][0] -> [1], recorded by its

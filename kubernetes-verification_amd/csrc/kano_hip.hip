@@ -337,6 +337,7 @@ int unprime(kano_ctx* ctx) {
   if (!ctx->primed || ctx->priming) return 0;
   ctx->primed = false;
   ring_bell(ctx);
+  ctx->gate_forced = ctx->bell_seq;           // (not a step boundary: kano_gate_timing)
   KCHK(hipStreamSynchronize(ctx->stream));
   KCHK(hipStreamSynchronize(ctx->stream2));   // (its member lists run on stream2)
   std::swap(ctx->sizes, ctx->sizes_alt);
@@ -2148,6 +2149,7 @@ int kano_create(int device, kano_ctx** out) {
         khz <= 0)
       khz = 100000;   // (gfx950's wall clock: 100 MHz)
     ctx->gate_ticks = (u64)khz * 200;
+    ctx->wall_khz = (u64)khz;
   }
   // page-locked staging for short row reads (system_isolation's row)
   if (hipHostMalloc(&ctx->row_stage, ROW_STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
@@ -2175,6 +2177,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->row_stage) (void)hipHostFree(ctx->row_stage);
   if (ctx->bell) (void)hipHostFree(ctx->bell);
   dfree(ctx->sizes_alt);
+  dfree(ctx->gate_wait);
   for (ClassSet* cs : {&ctx->rc, &ctx->cc}) {
     DBuf* b[] = {&cs->keys_d, &cs->table, &cs->smin, &cs->slot_of, &cs->flag, &cs->cid, &cs->cls,
                  &cs->rep,    &cs->mcnt,  &cs->mcur, &cs->moff,    &cs->mem,  &cs->cval};
@@ -3483,8 +3486,12 @@ int prime_next(kano_ctx* ctx) {
   ctx->primed = true;
   ctx->priming = true;
   const u64 armed = ctx->sig_armed, waiting = ctx->sig_wait;
+  if (!ctx->gate_wait.p) {
+    KTRY(dalloc(ctx, ctx->gate_wait, sizeof(u64) * GATE_RING));
+    KCHK(hipMemsetAsync(ctx->gate_wait.p, 0, sizeof(u64) * GATE_RING, ctx->stream));
+  }
   hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, ctx->stream, (const u64*)ctx->bell_dev,
-                     ++ctx->bell_seq, ctx->gate_ticks);
+                     ++ctx->bell_seq, ctx->gate_ticks, P_<u64>(ctx->gate_wait));
   int rc = hipGetLastError() == hipSuccess ? 0 : fail(ctx, -EIO, "k_gate launch failed");
   if (!rc) {
     ctx->sig_armed = 0;
@@ -3871,6 +3878,32 @@ int kano_settle(kano_ctx* ctx) {
   if (!ctx) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
   return settle(ctx);
+}
+
+int kano_gate_timing(kano_ctx* ctx, int reset, int64_t* gates, double* mean_us,
+                     double* max_us) {
+  if (!ctx) return -EINVAL;
+  KCHK(hipSetDevice(ctx->device));
+  KTRY(settle(ctx));   // (every queued gate open and ended)
+  // (the latest gate is left out when an unprime opened it: it waited for
+  // whatever came after the last call, not for the next call)
+  const u64 last = ctx->bell_seq - (ctx->gate_forced == ctx->bell_seq ? 1 : 0);
+  const u64 n = last > ctx->gate_seq0 ? std::min<u64>(last - ctx->gate_seq0, GATE_RING) : 0;
+  double sum = 0.0, mx = 0.0;
+  if (n > 0 && ctx->gate_wait.p) {
+    u64 ring[GATE_RING];
+    KCHK(hipMemcpy(ring, ctx->gate_wait.p, sizeof(ring), hipMemcpyDeviceToHost));
+    for (u64 q = 0; q < n; ++q) {
+      const double us = (double)ring[(last - q) % GATE_RING] * 1e3 / (double)ctx->wall_khz;
+      sum += us;
+      mx = std::max(mx, us);
+    }
+  }
+  if (gates) *gates = (int64_t)n;
+  if (mean_us) *mean_us = n ? sum / (double)n : 0.0;
+  if (max_us) *max_us = mx;
+  if (reset) ctx->gate_seq0 = ctx->bell_seq;
+  return 0;
 }
 
 int kano_host_times(kano_ctx* ctx, double* out, int reset) {

@@ -426,14 +426,20 @@ constexpr int FILL_RIDE_BLOCKS = 512;   // blocks a carried fill gets (grid-stri
 // until it reaches `want`; past `ticks` of the wall clock it opens by itself,
 // so the engine stream never stays closed (the prologue reads only resident
 // inputs, so it is valid whenever it runs).  One wave, no other work.
+// (waited: the ticks the gate held the engine stream, into slot want % 64 of
+// a device ring -- the engine stream's idle time at the step boundary,
+// measured without a profiler: kano_gate_timing)
+constexpr int GATE_RING = 64;
 static __global__ __attribute__((unused)) __launch_bounds__(64) void k_gate(const u64* bell,
-                                                                            u64 want, u64 ticks) {
+                                                                            u64 want, u64 ticks,
+                                                                            u64* waited) {
   if (threadIdx.x != 0) return;
   const u64 t0 = wall_clock64();
   while (__hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
     if (wall_clock64() - t0 > ticks) break;
     __builtin_amdgcn_s_sleep(1);
   }
+  if (waited) waited[want % GATE_RING] = wall_clock64() - t0;
 }
 
 // atomicAdd(&ctr[key], 1) for every active lane, lanes with equal keys merged

@@ -587,6 +587,17 @@ class DeviceBuild:
         prologue run and put back, the last matrix write finished)."""
         self._chk(self.lib.kano_settle(self.ctx), "kano_settle")
 
+    def gate_timing(self, reset: bool = False) -> dict:
+        """kano_gate_timing: how long the pipelined calls' gates held the engine
+        stream (its idle time at the step boundary), over the last min(64,
+        gates since the last reset) gates; settles first."""
+        import ctypes
+        g, mean, mx = ctypes.c_int64(0), ctypes.c_double(0.0), ctypes.c_double(0.0)
+        self._chk(self.lib.kano_gate_timing(self.ctx, int(bool(reset)), ctypes.byref(g),
+                                            ctypes.byref(mean), ctypes.byref(mx)),
+                  "kano_gate_timing")
+        return dict(gates=int(g.value), mean_us=float(mean.value), max_us=float(mx.value))
+
     def host_times(self, reset: bool = False) -> dict:
         """kano_verify's host time by phase (us): sums and maxima since the
         last reset (kano_host_times)."""

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_uint8, c_uint64, c_void_p
+from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_int64, c_uint8, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
@@ -77,6 +77,8 @@ SIGNATURES = {
     "kano_host_times": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_set_pipeline": (c_int, [c_void_p, c_int]),
     "kano_settle": (c_int, [c_void_p]),
+    "kano_gate_timing": (c_int, [c_void_p, c_int, POINTER(c_int64), POINTER(c_double),
+                                 POINTER(c_double)]),
     "kano_mfma_timing": (c_int, [c_void_p, c_void_p, c_int]),
     "kano_group_create": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
     "kano_group_create_lean": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
