@@ -261,6 +261,20 @@ int main(int argc, char** argv) {
                        dA, ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
   });
   bad_forms += compare("f4_22k8") != 0;
+  CK(hipMemset(dM1, 0, mcb));
+  timeit("f4_22k4", [&] {
+    hipLaunchKernelGGL((k_heavy_gemm_f4<2, 2, 4>), grid_of(2, 2), dim3(TPB), lds_of(2, 2) / 4, 0,
+                       dA, ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
+  });
+  bad_forms += compare("f4_22k4") != 0;
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_heavy_gemm_f4<4, 2, 8>),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_of(4, 2) / 2));
+  CK(hipMemset(dM1, 0, mcb));
+  timeit("f4_42k8", [&] {
+    hipLaunchKernelGGL((k_heavy_gemm_f4<4, 2, 8>), grid_of(4, 2), dim3(TPB), lds_of(4, 2) / 2, 0,
+                       dA, ldA, dl, H, dB, ldB, Ua, PBp, o1, ldMc);
+  });
+  bad_forms += compare("f4_42k8") != 0;
   {
     const int l8 = (int)(sizeof(u64) * 2 * 8 * 512), l32 = (int)(sizeof(u64) * 2 * 32 * 256);
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_f4_var<4, 4, 8, 0>),
