@@ -13,7 +13,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 fatal() { case "$1" in 0) ;; *) echo "fatal rc=$1 at $2"; exit "$1" ;; esac; }
 rm -rf $O/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
-  python3 bench.py --steps 20 --warmup 5 --alone 0 > $O/c3_profiled.json 2> $O/c3_profiled.err
+  python3 bench.py --steps 20 --warmup 5 --alone 0 --cold 0 > $O/c3_profiled.json 2> $O/c3_profiled.err
 fatal $? prof
 python3 scripts/steps_tl.py $(find $O/prof -name "*kernel_trace.csv" | head -1) > $O/c3_step_timeline.txt
 for tag in C3 C5r8; do
