@@ -1160,7 +1160,13 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
   // the staged GEMM's padded operands (k_heavy_gemm_f4): A [PBp][ldA],
   // ACT [PBp][ldB]; the unstaged kernels use ldA = H, ldB = Ua, PBp = PB
   const bool glds = gemm;
-  const i64 ldA = glds ? (H + 64 * tmg - 1) / (64 * tmg) * (64 * tmg) : H;
+  const i64 ldA0 = glds ? (H + 64 * tmg - 1) / (64 * tmg) * (64 * tmg) : H;
+  // (every class heavy on the dense path: A is SA as it stands -- zero past
+  // U, pitch dx_ldY -- when that pitch is a whole number of block tiles; no
+  // gather)
+  const bool a_is_sa = glds && ctx->dense_sel && H == U && ctx->dx_ldY >= ldA0 &&
+                       ctx->dx_ldY % (64 * tmg) == 0;
+  const i64 ldA = a_is_sa ? ctx->dx_ldY : ldA0;
   const i64 ldB = glds ? (ctx->cc.U + 64 * tng - 1) / (64 * tng) * (64 * tng) : ctx->cc.U;
   const i64 PBp = glds ? (ctx->PB + GK_KC - 1) / GK_KC * GK_KC : ctx->PB;
   // k_sel_place went out before the sizes (sel_place_early): kept when the
@@ -1354,7 +1360,7 @@ int do_back(kano_ctx* ctx, int path, const std::function<int(FillBatch&)>& extra
         const dim3 grid((unsigned)(8 * ((nb + 7) / 8)));
         const int32_t* hl = P_<int32_t>(ctx->hlist);
         u64* A = P_<u64>(ctx->scratch_words);
-        if (ctx->dense_sel && H == U && ldA == ctx->dx_ldY && PBp == ctx->dx_PBo) {
+        if (a_is_sa && PBp == ctx->dx_PBo) {
           A = P_<u64>(ctx->dx_sa);   // every class heavy: SA is A as it stands
         } else if (ctx->dense_sel) {
           hipLaunchKernelGGL(k_sa_gather, dim3(nblk(PBp * ldA)), dim3(TPB), 0, ctx->stream,

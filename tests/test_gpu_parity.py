@@ -126,7 +126,7 @@ def test_build_paths_agree(name, path, monkeypatch):
     if path == "mfma-dx":    # the dense path's bit matrices; A is SA as it stands
         monkeypatch.setenv("KANO_TUNE", "dx=2,hgemm=44,hgemmmin=1")
         path = "mfma"
-    if path == "mfma-dx22":  # the same, A gathered from SA (ldA differs)
+    if path == "mfma-dx22":  # the same on the 2 x 2 tile (A is SA when its pitch fits)
         monkeypatch.setenv("KANO_TUNE", "dx=2,hgemm=22,hgemmmin=1")
         path = "mfma"
     if path == "bitwise-dx":
