@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="kano_set_pipeline: each step queues the next step's prologue behind a "
                          "gate the next step opens (0: off)")
+    ap.add_argument("--gather1", action="store_true",
+                    help="diagnostic: the one-rank step through kano_verify_gather (the "
+                         "emulated exchange, a device copy) instead of the fused kano_verify")
     ap.add_argument("--rank-of", type=int, default=0,
                     help="diagnostic: time rank 0's shard step of an N-rank run on one GPU "
                          "(the all-gather replaced by a local copy; not a bench line)")
@@ -122,6 +125,7 @@ class Step:
         self.PinnedBuffer = PinnedBuffer
         self.results = {}
         self.verify_max_ms = 0.0    # the slowest engine call (host hiccups show here or not)
+        self.gather1 = False
 
     def __call__(self):
         eng, n = self.eng, self.n
@@ -138,7 +142,11 @@ class Step:
             self.idx_view = self.pin_idx.view(np.int32, 4 * max(n, 1))
         idx = self.idx_view
         tv = time.perf_counter()
-        if not self.shard_path:
+        if self.gather1:
+            # (diagnostic: the same step through the gathered tail, one rank)
+            r = eng.verify_gather(0, 1, gid="stored", sys_row=0, shadow=self.shadow,
+                                  shadow_count_only=self.count_only, pairs=pairs, idx=idx)
+        elif not self.shard_path:
             # the fused entry point: build + every check, three host syncs;
             # results arrive as the reference's index lists
             r = eng.verify("stored", sys_row=0, shadow=self.shadow, pairs=pairs, idx=idx,
@@ -398,6 +406,7 @@ def main():
     step = Step(eng, gid, n, rank, world, r0, r1, shadow=shadow, dist=dist,
                 torch=torch, stream=stream, emulate=args.rank_of if args.rank_of > 1 else 0)
     up_groups_ms = (time.perf_counter() - t_up) * 1e3
+    step.gather1 = bool(args.gather1) and not step.shard_path
 
     # (pipelined steps: the engine calls alone order its streams -- the fused
     # kano_verify, the emulated gather, the native RCCL gather; a torch

@@ -337,13 +337,6 @@ struct kano_ctx {
   bool vs_open = false, vs_shadow = false, vs_cross_want = false, vs_cross_on = false;
   bool vs_have_sys = false, vs_sys_on = false;
   bool vs_rows = false;      // the combine writes the shard's rows (not after kano_checks_shard)
-  // one rank's kano_verify: the four lists written by the column pass itself
-  // (k_verify_cols_f: row r at idxd[r * n], its look-back states in vcst --
-  // two parity regions of 2 + 4 x tiles words, each launch zeroing the other)
-  bool vs_fused = false;
-  DBuf vcst;
-  i64 vc_cap = 0;
-  int vc_parity = 0;
   i64 vs_nb = 0, vs_rl = 0;
 };
 

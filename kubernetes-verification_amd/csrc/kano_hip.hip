@@ -2214,7 +2214,7 @@ void kano_destroy(kano_ctx* ctx) {
                   &ctx->pT,     &ctx->pR[0],   &ctx->pR[1],   &ctx->pD[0],     &ctx->pD[1],
                   &ctx->pA,     &ctx->pB,      &ctx->pcnt,
                   &ctx->xv,     &ctx->asel,    &ctx->aalw,    &ctx->iterm,     &ctx->idead,
-                  &ctx->irows,  &ctx->xw,      &ctx->xg,      &ctx->vcst,
+                  &ctx->irows,  &ctx->xw,      &ctx->xg,
                   &ctx->rw_items, &ctx->rw_segs, &ctx->rw_ticket, &ctx->slist_tmp,
                   &ctx->dx_sc, &ctx->dx_sa, &ctx->mct};
   for (DBuf* b : bufs) dfree(*b);
@@ -3394,37 +3394,14 @@ int verify_front(kano_ctx* ctx, int path, const int32_t* gid, int32_t ngroups, i
       fa.r0 = ctx->r0;
       fa.r1 = ctx->r1;
     }
-    ctx->vs_fused = !words_dev;
-    if (ctx->vs_fused) {
-      // one rank: the lists in this pass (k_verify_cols_f), no count scan
-      const i64 vtiles = std::max<i64>(1, nblk(W * 64, VC_TILE)), region = 2 + 4 * vtiles;
-      if (ctx->vc_cap < region) {
-        KTRY(dalloc(ctx, ctx->vcst, sizeof(u64) * 2 * (size_t)region));
-        KCHK(hipMemsetAsync(ctx->vcst.p, 0, sizeof(u64) * 2 * (size_t)region, ctx->stream));
-        ctx->vc_cap = region;
-        ctx->vc_parity = 0;
-      }
-      u64* st = P_<u64>(ctx->vcst);
-      FusedTail ft{};
-      ft.status = st + (ctx->vc_parity ? ctx->vc_cap : 0);
-      ft.clear = st + (ctx->vc_parity ? 0 : ctx->vc_cap);
-      ft.nclear = ctx->vc_cap;   // the whole other region: a larger earlier launch left words past `region`
-      ctx->vc_parity ^= 1;
-      ft.idx = P_<int32_t>(ctx->idxd);
-      ft.totals = P_<u64>(ctx->sizes) + SZ_IDX0;
-      ft.totals_host = ctx->gmirror_dev ? ctx->gmirror_dev + SZ_IDX0 : nullptr;
-      if (ctx->gmirror_dev) {
-        ft.pub_src[ft.npub] = P_<u64>(ctx->sizes) + SZ_ERR;
-        ft.pub_dst[ft.npub++] = ctx->gmirror_dev + SZ_ERR;
-      }
-      hipLaunchKernelGGL(k_verify_cols_f, dim3((unsigned)vtiles), dim3(TPB), 0, ctx->stream, fa,
-                         ft);
-    } else {
-      hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
-    }
+    // (round 6: the four lists written by the column pass itself, with a
+    // decoupled look-back over the tiles -- k_verify_cols_f -- measured slower
+    // than this pass plus the count scan and k_idx_write at every config: C3
+    // 0.355 -> 0.348 ms, C4 0.396 -> 0.391, D1 0.887 -> 0.879,
+    // profiles/r06_c3_vfused_ab.jsonl, r06_c4_vfused_ab.jsonl)
+    hipLaunchKernelGGL(k_verify_cols, dim3((unsigned)nb), dim3(TPB), 0, ctx->stream, fa);
     KLAUNCH();
   } else {
-    ctx->vs_fused = false;
     KCHK(hipMemsetAsync(ctx->icnt.p, 0, sizeof(i64) * 4 * nb, ctx->stream));
   }
   // (issued after the column checks: the engine stream does not wait for it)
@@ -3518,8 +3495,7 @@ int prime_next(kano_ctx* ctx) {
 // end is ev_pairs)
 int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts,
                        int32_t* shadow_pairs, void* pairs_h, int64_t shadow_cap,
-                       int64_t* shadow_count, bool async, bool compacted = false,
-                       bool fused = false) {
+                       int64_t* shadow_count, bool async, bool compacted = false) {
   using clk = std::chrono::steady_clock;
   auto tmark = clk::now();
   auto part = [&](int k) {
@@ -3535,20 +3511,6 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
   i64 out_cap = 0;
   const bool pairs_job = pairs_mode && pairs_h && rl > 0;
   const u64* tots = P_<u64>(ctx->sizes) + SZ_IDX0;
-  // the lists (row r at idxd[r * n], concatenated on the host): with pairs to
-  // copy they travel in the same launch as the pairs, after the emission --
-  // one PCIe-bound copy of both (C3: 0.8 + 0.55 MB) instead of two launches
-  // with the emission between them
-  CopySegs cl{};
-  if (fused)
-    for (int r = 0; r < 4; ++r)
-      cl.j[r] = CopySeg{static_cast<const char*>(ctx->idxd.p) + sizeof(int32_t) * r * n,
-                        static_cast<char*>(idx_h), tots + r, 1, tots, r, 4, 4 * n};
-  if (fused && !pairs_job) {
-    hipExtLaunchKernelGGL(k_copy_segs, dim3(256, 4), dim3(TPB), 0, st, nullptr, ctx->ev_tail, 0,
-                          cl);
-    KLAUNCH();
-  }
   if (pairs_mode) {
     // L never exceeds the candidate pairs; out keeps the largest total seen
     KTRY(dalloc(ctx, ctx->L, sizeof(int2) * std::max<i64>(1, nf)));
@@ -3576,11 +3538,8 @@ int verify_back_direct(kano_ctx* ctx, int32_t* idx, void* idx_h, int64_t* counts
   // matrix write
   CopySegs cj{};
   int njobs = 0;
-  if (!fused)
-    cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->idxd.p), static_cast<char*>(idx_h),
-                            tots, 4, nullptr, 0, 4, 4 * n};
-  else if (pairs_job)
-    for (int r = 0; r < 4; ++r) cj.j[njobs++] = cl.j[r];
+  cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->idxd.p), static_cast<char*>(idx_h),
+                          tots, 4, nullptr, 0, 4, 4 * n};
   if (pairs_job) {
     cj.j[njobs++] = CopySeg{static_cast<const char*>(ctx->out.p), static_cast<char*>(pairs_h),
                             reinterpret_cast<const u64*>(P_<i64>(ctx->poff) + rl), 1, nullptr, 0,
@@ -3690,16 +3649,11 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     KLAUNCH();
   }
   // the four result rows as index lists: all_reachable, all_isolated,
-  // user_crosscheck, system_isolation (one rank: already written by the
-  // column pass, k_verify_cols_f, with the totals and the group-id check in
-  // the host mirror)
-  const bool fused = ctx->vs_fused && !gathered;
-  if (!fused) {
-    for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
-      KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
-                  SZ_IDX0 + r));
-    sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
-  }
+  // user_crosscheck, system_isolation
+  for (int r = 0; r < 4; ++r)   // one job per row; row totals land in SZ_IDX0..3
+    KTRY(sb.add(P_<i64>(ctx->icnt) + r * nb, nb, P_<i64>(ctx->ioff) + r * (nb + 1),
+                SZ_IDX0 + r));
+  sb.publish(SZ_ERR);   // the group-id check's atomics, for the host's sync 3
   // (an earlier scan's total: one host signal for all; the side scans store
   // their totals to the host directly)
   if (want_shadow && !compacted) sb.publish(SZ_NL);
@@ -3716,7 +3670,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   ir.row[3] = ctx->vs_sys_on ? P_<u64>(ctx->sysrow) : nullptr;
   ir.inv[3] = 1;
   int32_t* idx_dev = P_<int32_t>(ctx->idxd);
-  if (n > 0 && W > 0 && !fused) {
+  if (n > 0 && W > 0) {
     hipLaunchKernelGGL(k_idx_write, dim3((unsigned)nb, 4), dim3(TPB), 0, ctx->stream, ir,
                        P_<i64>(ctx->ioff), nb + 1, P_<u64>(ctx->sizes) + SZ_IDX0, idx_dev);
     KLAUNCH();
@@ -3730,7 +3684,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
   // host redoes it sized (first call, or a larger output).
   if (direct)
     return verify_back_direct(ctx, idx, idx_h, counts, shadow_pairs, pairs_h, shadow_cap,
-                              shadow_count, may_async && ctx->async_rows, compacted, fused);
+                              shadow_count, may_async && ctx->async_rows, compacted);
   // the list sizes, policy_shadow's sizes and the group check travel to the
   // host: it waits on the signal (or the event) only, then queues the tail
   // (policy_shadow's compaction and emission, the copies) on stream2 and the
@@ -3788,14 +3742,7 @@ int verify_back(kano_ctx* ctx, const u64* gathered, int32_t nranks, int32_t* idx
     *shadow_count = total;
   }
   tmark = clk::now();
-  if (fused) {   // row r at idxd[r * n]: the rows' copies, concatenated
-    i64 o = 0;
-    for (int r = 0; r < 4; ++r) {
-      const i64 c = std::max<i64>(0, counts[r]);
-      if (c > 0) KTRY(copy_out(ctx, idx + o, idx_dev + (i64)r * n, sizeof(int32_t) * c, cs));
-      o += c;
-    }
-  } else if (nidx > 0) {
+  if (nidx > 0) {
     KTRY(copy_out(ctx, idx, idx_dev, sizeof(int32_t) * nidx, cs));
   }
   part(15);

@@ -3260,127 +3260,6 @@ __global__ __launch_bounds__(TPB) void k_verify_cols(FinishArgs a) {
   }
 }
 
-// ---- kano_verify's list tail in the column pass itself (one rank) ----------
-// k_verify_cols plus the four lists (all_reachable, all_isolated,
-// user_crosscheck, system_isolation: algorithm.py:4-55) written in the same
-// launch: each block is a tile of TPB pods (drawn by ticket, so a tile's
-// predecessors are already running), scans its four rows' bits in LDS, and
-// finds its rows' starts by a decoupled look-back over the earlier tiles'
-// published counts (wave r looks back for row r) -- no count scan, no
-// separate index pass.  Row r's list lands at idx[r * n ...] (device); the
-// last tile writes the four totals to their size slots and host mirrors,
-// and forwards the size slots the host reads with them (pub).
-// status: ticket, done count, 4 x tiles states, zeroed before the launch;
-// the launch zeroes `clear` (the other parity's region) for the next one.
-struct FusedTail {
-  u64* status;
-  u64* clear;
-  i64 nclear;
-  int32_t* idx;          // 4 x n entries (device)
-  u64* totals;           // 4 size slots (SZ_IDX0..3)
-  u64* totals_host;      // their host mirrors (nullable)
-  int npub;              // size slots copied to their host mirrors by the last tile
-  u64* pub_src[2];
-  u64* pub_dst[2];
-};
-
-// TPB-pod slices per tile of k_verify_cols_f (C3, one per tile: 391 tiles,
-// 20 us; eight: 49 tiles, 26.6 us -- each thread's eight dependent lookups
-// in a row cost more than the longer look-back)
-constexpr int VC_ITEMS = 1;
-constexpr i64 VC_TILE = (i64)TPB * VC_ITEMS;
-__global__ __launch_bounds__(TPB) void k_verify_cols_f(FinishArgs a, FusedTail f) {
-  __shared__ i64 cnt[4][VC_ITEMS][TPB / 64];
-  __shared__ i64 s_tot[4], s_excl[4];
-  __shared__ i64 s_tile;
-  {
-    const i64 nthr = (i64)gridDim.x * TPB;
-    for (i64 i = (i64)blockIdx.x * TPB + threadIdx.x; i < f.nclear; i += nthr) f.clear[i] = 0;
-  }
-  if (threadIdx.x == 0)
-    s_tile = (i64)__hip_atomic_fetch_add(f.status, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const i64 tile = s_tile, tiles = gridDim.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const u64 below = (1ull << lane) - 1ull;
-  uint32_t bits = 0;            // bit q * 4 + r: row r lists pod (tile, slice q, thread)
-  int32_t rank[VC_ITEMS][4];    // the pod's rank among its wave's listed pods
-#pragma unroll
-  for (int q = 0; q < VC_ITEMS; ++q) {
-    const i64 j = tile * VC_TILE + (i64)q * TPB + threadIdx.x;   // the tiles cover W * 64
-    const bool live = j < a.n;
-    if (a.tp && j >= a.r0 && j < a.r1) {
-      const int32_t c = a.rcls[j];
-      a.tp[j - a.r0] = a.loff[c + 1] - a.loff[c];
-    }
-    const int32_t ca = live ? a.cla[j] : 0;
-    const bool orb = live && mc_bit(a.col_or_c, ca);
-    const bool nab = live && mc_bit(a.col_nand_c, ca);
-    bool crb = false;
-    if (a.gid && live) {
-      const int32_t g = a.gid[j];
-      bool own = false;
-      if (g < 0 || g >= a.G) atomicOr(a.err, 1);
-      else own = mc_bit(a.R + (i64)g * a.ldC, ca);
-      crb = mc_bit(a.multi, ca) || mc_bit(a.A2, ca) || (mc_bit(a.A1, ca) && !own);
-    }
-    const bool syb = a.Mc && live && mc_bit(a.Mc + (i64)a.clr[a.sys_row] * a.ldC, ca);
-    const u64 wo = __ballot(orb), wn = __ballot(nab), wc = __ballot(crb), ws = __ballot(syb);
-    const i64 w = j >> 6;
-    if (lane == 0 && w < a.W) {
-      a.color[w] = wo;
-      a.colnand[w] = wn;
-      a.col_and[w] = ~wn & valid_mask(w, a.n);
-      if (a.gid) a.cross[w] = wc;
-      if (a.Mc) a.sysrow[w] = ws;
-    }
-    // the four listed rows: all_reachable (no row misses j), all_isolated (no
-    // row reaches j), the cross bit, the system row's zeros
-    const bool bit[4] = {live && !nab, live && !orb, crb, a.Mc && live && !syb};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const u64 bw = __ballot(bit[r]);
-      rank[q][r] = (int32_t)__popcll(bw & below);
-      if (lane == 0) cnt[r][q][wid] = (i64)__popcll(bw);
-      if (bit[r]) bits |= 1u << (q * 4 + r);
-    }
-  }
-  __syncthreads();
-  // per row, the (slice, wave) counts to exclusive starts within the tile
-  if (threadIdx.x < 4) {
-    i64 t = 0;
-    for (int q = 0; q < VC_ITEMS; ++q)
-      for (int ww = 0; ww < TPB / 64; ++ww) {
-        const i64 x = cnt[threadIdx.x][q][ww];
-        cnt[threadIdx.x][q][ww] = t;
-        t += x;
-      }
-    s_tot[threadIdx.x] = t;
-  }
-  __syncthreads();
-  lookback_jobs<4>(f.status + 2, tiles, tile, s_tot, s_excl);
-#pragma unroll
-  for (int q = 0; q < VC_ITEMS; ++q) {
-    const i64 j = tile * VC_TILE + (i64)q * TPB + threadIdx.x;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (bits & (1u << (q * 4 + r)))
-        f.idx[(i64)r * a.n + s_excl[r] + cnt[r][q][wid] + rank[q][r]] = (int32_t)j;
-  }
-  // the last block to finish: the four totals, the forwarded size slots
-  if (!last_block_done(f.status + 1, tiles)) return;
-  if (threadIdx.x < 4) {
-    const u64 t = (u64)lookback_total(f.status + 2, tiles, threadIdx.x);
-    f.totals[threadIdx.x] = t;
-    if (f.totals_host) mirror_store(f.totals_host + threadIdx.x, t);
-  }
-  if (threadIdx.x == 0) {
-    for (int q = 0; q < f.npub; ++q)
-      mirror_store(f.pub_dst[q], __hip_atomic_load(f.pub_src[q], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT));
-  }
-}
-
 // Up to five device -> host copies sized on the device (kano_verify's
 // tail): job y's element count is the sum of cnt[0..ncnt), its destination
 // offset (elements) the sum of off[0..noff); a job past its capacity copies
