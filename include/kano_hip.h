@@ -41,7 +41,7 @@ typedef struct kano_ctx kano_ctx;
 /* Build paths for kano_build(). */
 #define KANO_PATH_AUTO    0   /* per-class choice by estimated cost          */
 #define KANO_PATH_BITWISE 1   /* LDS scatter / bitwise OR of allow rows      */
-#define KANO_PATH_MFMA    2   /* heavy classes by int8 MFMA contraction      */
+#define KANO_PATH_MFMA    2   /* heavy classes by the MFMA contraction       */
 
 /* kano_info() slots */
 #define KANO_INFO_N        0
@@ -55,7 +55,7 @@ typedef struct kano_ctx kano_ctx;
 #define KANO_INFO_ROW1     8
 #define KANO_INFO_MAXSEL   9   /* max over classes of |S(c)|                  */
 #define KANO_INFO_UA      10   /* column classes (pods with equal allow keys) */
-#define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 int8 MFMA          */
+#define KANO_INFO_HEAVY_PATH 11 /* 0 none, 1 bitwise OR, 2 MFMA (fp4)         */
 #define KANO_INFO_WORK_ITEMS 12 /* (class, member chunk) items of the list-based row kernel */
 #define KANO_INFO_ROWS_KERNEL 13 /* the last matrix write: 2 k_rows, 3 k_rows_prep + k_rows_w
                                     (wide rows), 4 k_ptrans + k_heavy_rows_t (every class
@@ -292,11 +292,12 @@ int kano_stage_times(kano_ctx* ctx, float* ms /* 8 */);
  * its timed region, kano_verify's own launches stay asynchronous). */
 int kano_rows_timing(kano_ctx* ctx, double* out /* 4 */, int reset);
 
-/* The heavy classes' int8 MFMA contraction (k_heavy_mc_mfma, the dense
- * path of build_matrix, model.py:158-160 as Sel x Allow thresholded > 0)
- * timed per build (HIP events around its launches on the context stream):
- * out[4] = [sum ms, builds timed, sum of algorithmic int8 ops (2 x heavy row
- * classes x policies x column classes per build), the last build's ops];
+/* The heavy classes' MFMA contraction (k_heavy_gemm_f4 / k_heavy_mc_mfma on
+ * the block-scaled fp4 MFMA, 0/1 operands; the dense path of build_matrix,
+ * model.py:158-160 as Sel x Allow thresholded > 0) timed per build (HIP
+ * events around its launches on the context stream): out[4] = [sum ms,
+ * builds timed, sum of algorithmic ops (2 x heavy row classes x policies x
+ * column classes per build), the last build's ops];
  * reset != 0 zeroes the sums after reading. */
 int kano_mfma_timing(kano_ctx* ctx, double* out /* 4 */, int reset);
 
@@ -311,7 +312,7 @@ int kano_mfma_timing(kano_ctx* ctx, double* out /* 4 */, int reset);
  * holding a matrix (e.g. a build with no policies); afterwards it is an
  * edited matrix that every query and check of this header reads.  src must
  * hold every row (no row shard).  mode: KANO_PATH_AUTO picks per step
- * between the semi-naive bit-packed OR (sparse delta) and the int8 MFMA
+ * between the semi-naive bit-packed OR (sparse delta) and the fp4 MFMA
  * contraction (dense); KANO_PATH_BITWISE / KANO_PATH_MFMA force one.
  * info (nullable, 6 slots): [composition steps that added pairs, steps run,
  * steps on the MFMA, row classes, column classes, identity classes]. */
