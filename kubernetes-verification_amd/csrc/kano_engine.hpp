@@ -38,6 +38,8 @@ constexpr int MAX_CWW = 8192;   // column-chunk width in words (64 KB of LDS)
 // allowed-pod entry of S(c), so two 64-KB chunks cost 0.3 ms of row builds a
 // step, 8.4 -> 8.0 ms; C5 on one GPU neutral)
 constexpr int MAX_CWW_KNOB = 16384;
+constexpr int XCD_WRITE = 3;   // whole XCDs the write takes in the XCD split (96 CUs)
+constexpr long long XCD_MIN_BYTES = 1ll << 30;   // the split for writes of >= 1 GiB
 constexpr int HT_ROWS = 128;    // heavy rows per MFMA launch (HT = 4)
 // member rows per k_rows work item (each item rebuilds its class row: C3,
 // 300-step A/Bs, 16 -> 24 took the masked write 0.362 -> 0.355 ms and the
@@ -172,6 +174,17 @@ struct kano_ctx {
   // (C3: 96 of 256 CUs, k_rows 0.26 -> 0.35 ms, step 0.52 -> 0.43 ms); a
   // larger write, which outlasts any build (C5: 125 GB), takes every CU.
   int rows_cu_off = 20;      // rcu=K (0: no masked stream)
+  // The XCD split (xcd=0: off): when the last build's write ran CU-masked
+  // beside the next build (pipelined calls, a matrix under rows_cu_bytes) and
+  // took no GEMM, the next builds run their engine streams on XCDs 3-7 and
+  // the write on whole XCDs 0-2 (its own L2s), instead of every XCD with 96
+  // CUs spread over them for the write.  The unmasked pair is kept in
+  // stream_x / stream2_x while the masked pair is in use (and vice versa).
+  int xcd_split = 1;
+  i64 xcd_min_bytes = XCD_MIN_BYTES;   // xcdmin=KiB (the parity test forces small ones)
+  bool xcd_tried = false, eng_on_xcd = false, xcd_last_ok = false;
+  hipStream_t stream_x = nullptr, stream2_x = nullptr, stream3x = nullptr;
+  hipEvent_t ev_sw = nullptr, ev_sw2 = nullptr;
   i64 rows_cu_bytes = 8ll << 30;   // rcubytes=G (GiB)
   int num_cus = 0, rows_cus = 0;   // the device's CUs; those of the last write's stream
 

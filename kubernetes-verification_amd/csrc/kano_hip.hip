@@ -360,6 +360,7 @@ int settle(kano_ctx* ctx) {
   KCHK(hipSetDevice(ctx->device));
   KCHK(hipStreamSynchronize(ctx->stream3));
   if (ctx->stream3m) KCHK(hipStreamSynchronize(ctx->stream3m));
+  if (ctx->stream3x) KCHK(hipStreamSynchronize(ctx->stream3x));
   return sync(ctx);
 }
 
@@ -828,10 +829,13 @@ int front_fills(kano_ctx* ctx, FillBatch& fb) {
   return 0;
 }
 
+int select_engine_streams(kano_ctx* ctx);
+
 // The build's prologue, up to the member lists: it reads only the resident
 // inputs (the label tables), so a pipelined kano_verify queues it for the
 // next call behind the gate (prime_next)
 int front_a(kano_ctx* ctx) {
+  KTRY(select_engine_streams(ctx));
   ctx->rc.m0 = ctx->r0;
   ctx->rc.m1 = ctx->r1;
   ctx->cc.m0 = 0;
@@ -1508,6 +1512,61 @@ int ensure_masked_stream(kano_ctx* ctx) {
   return 0;
 }
 
+// CUs of XCDs [x0, x1) (CU i on XCD i / 32: the masks' numbering, measured --
+// the round-robin reading gave the write every CU's time)
+void xcd_mask(int x0, int x1, uint32_t* mask) {
+  for (int w = 0; w < 8; ++w) mask[w] = (w >= x0 && w < x1) ? 0xffffffffu : 0u;
+}
+int ensure_xcd_streams(kano_ctx* ctx) {
+  if (ctx->stream_x || ctx->xcd_tried) return 0;
+  ctx->xcd_tried = true;
+  uint32_t wm[8], em[8];
+  xcd_mask(0, XCD_WRITE, wm);
+  xcd_mask(XCD_WRITE, 8, em);
+  hipStream_t a = nullptr, b = nullptr, c = nullptr;
+  if (hipExtStreamCreateWithCUMask(&a, 8, em) != hipSuccess ||
+      hipExtStreamCreateWithCUMask(&b, 8, em) != hipSuccess ||
+      hipExtStreamCreateWithCUMask(&c, 8, wm) != hipSuccess) {
+    for (hipStream_t x : {a, b, c})
+      if (x) (void)hipStreamDestroy(x);
+    return 0;   // (no split: the spread mask stays)
+  }
+  ctx->stream_x = a;
+  ctx->stream2_x = b;
+  ctx->stream3x = c;
+  return 0;
+}
+// The engine stream pair for the build about to start (front_a): the
+// XCD-masked pair when the last build qualified, else the unmasked one; a
+// switch orders the new pair behind everything queued on the old one.
+int select_engine_streams(kano_ctx* ctx) {
+  const bool want = ctx->xcd_split && ctx->own_stream && ctx->pipeline && ctx->xcd_last_ok &&
+                    ctx->stream3m && ctx->num_cus == 256;
+  if (want) KTRY(ensure_xcd_streams(ctx));
+  const bool target = want && ctx->stream_x;
+  if (target == ctx->eng_on_xcd) return 0;
+  KCHK(hipEventRecord(ctx->ev_sw, ctx->stream));
+  KCHK(hipEventRecord(ctx->ev_sw2, ctx->stream2));
+  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x}) {
+    KCHK(hipStreamWaitEvent(t, ctx->ev_sw, 0));
+    KCHK(hipStreamWaitEvent(t, ctx->ev_sw2, 0));
+  }
+  std::swap(ctx->stream, ctx->stream_x);
+  std::swap(ctx->stream2, ctx->stream2_x);
+  ctx->eng_on_xcd = target;
+  return 0;
+}
+// back to the unmasked pair, everything drained (kano_set_stream)
+int leave_xcd_streams(kano_ctx* ctx) {
+  if (!ctx->eng_on_xcd) return 0;
+  for (hipStream_t t : {ctx->stream, ctx->stream2, ctx->stream_x, ctx->stream2_x})
+    KCHK(hipStreamSynchronize(t));
+  std::swap(ctx->stream, ctx->stream_x);
+  std::swap(ctx->stream2, ctx->stream2_x);
+  ctx->eng_on_xcd = false;
+  return 0;
+}
+
 int launch_rows(kano_ctx* ctx) {
   const i64 U = ctx->rc.U, W = ctx->W, ldM = ctx->ldM, n = ctx->n;
   const i64 rl = rows_local(ctx);
@@ -1518,8 +1577,16 @@ int launch_rows(kano_ctx* ctx) {
   // takes every CU)
   const bool masked = ctx->rows_overlap && ctx->stream3m &&
                       (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
-  hipStream_t rs = masked ? ctx->stream3m : ctx->stream3;
-  ctx->rows_cus = ctx->num_cus - (masked ? 8 * ctx->rows_cu_off : 0);
+  const bool on_xcd = masked && ctx->eng_on_xcd;
+  hipStream_t rs = on_xcd ? ctx->stream3x : masked ? ctx->stream3m : ctx->stream3;
+  ctx->rows_cus = on_xcd ? 32 * XCD_WRITE : ctx->num_cus - (masked ? 8 * ctx->rows_cu_off : 0);
+  // (the next build's streams: the split when this write is masked, large
+  // enough to bound the step -- C3's and C4's 1.25 GB; a half-row shard's
+  // 0.63 GB is shorter than the build beside it and measured +5 % with the
+  // split -- and the build took no GEMM: the dense contraction wants every
+  // XCD)
+  ctx->xcd_last_ok = masked && ctx->heavy_kernel != 3 &&
+                     (i64)sizeof(u64) * rl * ldM >= ctx->xcd_min_bytes;
   const int set = ctx->rows_set;
   // this set's pair was last used two writes back (ended: the engine stream
   // waited for it before this build wrote the set)
@@ -2044,6 +2111,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "shr" && (v == 1 || v == 2 || v == 4 || v == 8)) ctx->shadow_r = v;
         if (k == "rcu" && v >= 0 && v <= 28 && (v < 4 || v % 4 == 0)) ctx->rows_cu_off = v;
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
+        if (k == "xcd") ctx->xcd_split = v;
+        if (k == "xcdmin" && v >= 0) ctx->xcd_min_bytes = (i64)v << 10;
         if (k == "hgemm" && (v == -1 || v == 0 || v == 22 || v == 42 || v == 44))
           ctx->heavy_gemm = v;
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
@@ -2116,6 +2185,8 @@ int kano_create(int device, kano_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pre_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pre_ac, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_sw, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_sw2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pairs, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&ctx->ev_m0) != hipSuccess || hipEventCreate(&ctx->ev_m1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_rows_end[0], hipEventDisableTiming) != hipSuccess ||
@@ -2178,6 +2249,8 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamSynchronize(ctx->stream3m);
+  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x, ctx->stream3x})
+    if (t) (void)hipStreamSynchronize(t);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   if (ctx->gmirror) (void)hipHostFree(ctx->gmirror);
   if (ctx->row_stage) (void)hipHostFree(ctx->row_stage);
@@ -2229,6 +2302,10 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamDestroy(ctx->stream3m);
+  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x, ctx->stream3x})
+    if (t) (void)hipStreamDestroy(t);
+  for (hipEvent_t e : {ctx->ev_sw, ctx->ev_sw2})
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->ev_fork, ctx->ev_tail, ctx->ev_rin, ctx->ev_rin_e, ctx->ev_sizes,
                        ctx->ev_fork2, ctx->ev_join2, ctx->ev_pre, ctx->ev_pre_done, ctx->ev_pre_ac, ctx->ev_pairs, ctx->ev_m0, ctx->ev_m1, ctx->ev_rows_end[0],
                        ctx->ev_rows_end[1], ctx->ev_rt[0][0], ctx->ev_rt[0][1], ctx->ev_rt[1][0],
@@ -2243,9 +2320,11 @@ int kano_set_stream(kano_ctx* ctx, void* s) {
   if (!ctx) return -EINVAL;
   KCHK(hipSetDevice(ctx->device));
   KTRY(settle(ctx));
+  KTRY(leave_xcd_streams(ctx));
   KCHK(hipStreamSynchronize(ctx->stream2));
   KCHK(hipStreamSynchronize(ctx->stream3));
   if (ctx->stream3m) KCHK(hipStreamSynchronize(ctx->stream3m));
+  if (ctx->stream3x) KCHK(hipStreamSynchronize(ctx->stream3x));
   if (ctx->own_stream && ctx->stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);

@@ -208,14 +208,19 @@ def test_verify_fused_c2(cap):
     pin.close()
 
 
-def test_verify_pipelined(monkeypatch):
+@pytest.mark.parametrize("tune", ["", "xcdmin=0"])
+def test_verify_pipelined(tune, monkeypatch):
     """kano_set_pipeline: every asynchronously completing verify queues the
     next call's prologue behind a gate the next verify opens.  Every call's
     results equal kano_py's (C2's record) whatever comes between two calls:
     nothing, a matrix read, a re-upload, another cluster's tables, a plain
     build, a pause past the gate's timeout (the prologue then ran by itself on
     the same inputs), count-only mode, the emulated shard path, the pipeline
-    switched off while a prologue is queued, and a close while one is queued."""
+    switched off while a prologue is queued, and a close while one is queued.
+    xcdmin=0: the XCD split at C2's size (engine streams on XCDs 3-7, the
+    write on 0-2, switched between calls as the last write qualifies)."""
+    if tune:
+        monkeypatch.setenv("KANO_TUNE", tune)
     import time
     import torch
     from kano._engine import DeviceBuild, PinnedBuffer
