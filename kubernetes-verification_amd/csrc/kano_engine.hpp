@@ -182,6 +182,8 @@ struct kano_ctx {
   // stream_x / stream2_x while the masked pair is in use (and vice versa).
   int xcd_split = 1;
   i64 xcd_min_bytes = XCD_MIN_BYTES;   // xcdmin=KiB (the parity test forces small ones)
+  int xcd_write = XCD_WRITE;           // xcdw: XCDs 0..xcdw-1 for the write
+  int xcd_eng0 = -1;                   // xcde: first XCD of the build's streams (-1: xcdw)
   bool xcd_tried = false, eng_on_xcd = false, xcd_last_ok = false;
   hipStream_t stream_x = nullptr, stream2_x = nullptr, stream3x = nullptr;
   hipEvent_t ev_sw = nullptr, ev_sw2 = nullptr;

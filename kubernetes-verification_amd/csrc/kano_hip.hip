@@ -1521,8 +1521,8 @@ int ensure_xcd_streams(kano_ctx* ctx) {
   if (ctx->stream_x || ctx->xcd_tried) return 0;
   ctx->xcd_tried = true;
   uint32_t wm[8], em[8];
-  xcd_mask(0, XCD_WRITE, wm);
-  xcd_mask(XCD_WRITE, 8, em);
+  xcd_mask(0, ctx->xcd_write, wm);
+  xcd_mask(ctx->xcd_eng0 < 0 ? ctx->xcd_write : ctx->xcd_eng0, 8, em);
   hipStream_t a = nullptr, b = nullptr, c = nullptr;
   if (hipExtStreamCreateWithCUMask(&a, 8, em) != hipSuccess ||
       hipExtStreamCreateWithCUMask(&b, 8, em) != hipSuccess ||
@@ -1579,7 +1579,7 @@ int launch_rows(kano_ctx* ctx) {
                       (i64)sizeof(u64) * rl * ldM <= ctx->rows_cu_bytes;
   const bool on_xcd = masked && ctx->eng_on_xcd;
   hipStream_t rs = on_xcd ? ctx->stream3x : masked ? ctx->stream3m : ctx->stream3;
-  ctx->rows_cus = on_xcd ? 32 * XCD_WRITE : ctx->num_cus - (masked ? 8 * ctx->rows_cu_off : 0);
+  ctx->rows_cus = on_xcd ? 32 * ctx->xcd_write : ctx->num_cus - (masked ? 8 * ctx->rows_cu_off : 0);
   // (the next build's streams: the split when this write is masked, large
   // enough to bound the step -- C3's and C4's 1.25 GB; a half-row shard's
   // 0.63 GB is shorter than the build beside it and measured +5 % with the
@@ -2113,6 +2113,8 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "rcubytes" && v >= 0) ctx->rows_cu_bytes = (i64)v << 30;
         if (k == "xcd") ctx->xcd_split = v;
         if (k == "xcdmin" && v >= 0) ctx->xcd_min_bytes = (i64)v << 10;
+        if (k == "xcdw" && v >= 1 && v <= 7) ctx->xcd_write = v;
+        if (k == "xcde" && v >= 0 && v <= 7) ctx->xcd_eng0 = v;
         if (k == "hgemm" && (v == -1 || v == 0 || v == 22 || v == 42 || v == 44))
           ctx->heavy_gemm = v;
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
