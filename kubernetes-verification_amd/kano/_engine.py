@@ -374,6 +374,23 @@ class DeviceBuild:
             raise ValueError("gid must have one entry per pod")
         self._chk(self.lib.kano_set_groups(self.ctx, _ptr(gid), int(ngroups)), "kano_set_groups")
 
+    def _result_slots(self) -> None:
+        # reused result slots (no per-call allocation)
+        self._counts = np.zeros(4, dtype=np.int64)
+        self._counts_p = self._counts.ctypes.data
+        self._cnt = c_int64(0)
+        self._cnt_ref = byref(self._cnt)
+        self._bufs = (None, None, None, None)
+
+    def _buf_ptrs(self, idx, pairs):
+        # the caller's reused idx / pairs buffers: their addresses once (the
+        # held references keep both arrays, and so their addresses, alive)
+        b_idx, p_idx, b_pairs, p_pairs = self._bufs
+        if idx is not b_idx or pairs is not b_pairs:
+            b_idx, p_idx, b_pairs, p_pairs = idx, _ptr(idx), pairs, _ptr(pairs)
+            self._bufs = (b_idx, p_idx, b_pairs, p_pairs)
+        return p_idx, p_pairs
+
     def verify(self, gid=None, sys_row: int = 0, shadow: bool = True,
                pairs: Optional[np.ndarray] = None, idx: Optional[np.ndarray] = None,
                ngroups: int = 0, path: Optional[str] = None,
@@ -403,24 +420,22 @@ class DeviceBuild:
                 gid = np.ascontiguousarray(gid, dtype=np.int32)
             if gid.shape[0] != n:
                 raise ValueError("gid must have one entry per pod")
-        if self._counts is None:   # reused result slots (no per-call allocation)
-            self._counts = np.zeros(4, dtype=np.int64)
-            self._cnt = c_int64(0)
-            self._cnt_ref = byref(self._cnt)
+        if self._counts is None:
+            self._result_slots()
         counts, cnt = self._counts, self._cnt
         cap = 0 if pairs is None else pairs.size // 2
         if shadow_count_only:
             cap = -1
+        p_idx, p_pairs = self._buf_ptrs(idx, pairs)
         pth = nat.PATHS[path or self.path]
-        rc = self.lib.kano_verify(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), _ptr(idx),
-                                  counts.ctypes.data, _ptr(pairs), int(cap),
+        rc = self.lib.kano_verify(self.ctx, pth, _ptr(gid), int(ngroups), int(sys_row), p_idx,
+                                  self._counts_p, p_pairs, int(cap),
                                   self._cnt_ref if shadow else None)
         if rc != 0:
             self._chk(rc, "kano_verify")
         out, o = {}, 0
-        for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
-                                  "system_isolation")):
-            k = int(counts[r])
+        for name, k in zip(("all_reachable", "all_isolated", "user_crosscheck",
+                            "system_isolation"), counts.tolist()):
             out[name] = idx[o:o + k] if k >= 0 else None
             o += max(k, 0)
         if gid is None and not stored:
@@ -522,23 +537,20 @@ class DeviceBuild:
             idx = np.empty(max(4 * n, 1), dtype=np.int32)
         elif idx.size < 4 * n:
             raise ValueError("idx buffer needs 4*n entries")
-        if self._counts is None:   # reused result slots (no per-call allocation)
-            self._counts = np.zeros(4, dtype=np.int64)
-            self._cnt = c_int64(0)
-            self._cnt_ref = byref(self._cnt)
+        if self._counts is None:
+            self._result_slots()
         counts, cnt = self._counts, self._cnt
         shadow = self._shard_shadow
         cap = 0 if pairs is None else pairs.size // 2
         if shadow_count_only:
             cap = -1
-        rc = call(_ptr(idx), counts.ctypes.data, _ptr(pairs), int(cap),
-                  self._cnt_ref if shadow else None)
+        p_idx, p_pairs = self._buf_ptrs(idx, pairs)
+        rc = call(p_idx, self._counts_p, p_pairs, int(cap), self._cnt_ref if shadow else None)
         if rc != 0:
             self._chk(rc, what)
         out, o = {}, 0
-        for r, name in enumerate(("all_reachable", "all_isolated", "user_crosscheck",
-                                  "system_isolation")):
-            k = int(counts[r])
+        for name, k in zip(("all_reachable", "all_isolated", "user_crosscheck",
+                            "system_isolation"), counts.tolist()):
             out[name] = idx[o:o + k] if k >= 0 else None
             o += max(k, 0)
         if shadow:
