@@ -185,7 +185,10 @@ struct kano_ctx {
   int xcd_write = XCD_WRITE;           // xcdw: XCDs 0..xcdw-1 for the write
   int xcd_eng0 = -1;                   // xcde: first XCD of the build's streams (-1: xcdw)
   bool xcd_tried = false, eng_on_xcd = false, xcd_last_ok = false;
+  int side_mode = 0;   // the side stream in use: 0 stream2, 1 stream2_x (XCDs 3-7), 2 stream2_u
+  int xcd_side = -1;   // xcdside: the side stream on XCDs 3-7 (1), on all (0), -1: 1 when heavy
   hipStream_t stream_x = nullptr, stream2_x = nullptr, stream3x = nullptr;
+  hipStream_t stream2_u = nullptr;   // the side stream with an every-XCD mask (its own queue)
   hipEvent_t ev_sw = nullptr, ev_sw2 = nullptr;
   i64 rows_cu_bytes = 8ll << 30;   // rcubytes=G (GiB)
   int num_cus = 0, rows_cus = 0;   // the device's CUs; those of the last write's stream

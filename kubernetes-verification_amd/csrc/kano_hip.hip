@@ -1520,50 +1520,68 @@ void xcd_mask(int x0, int x1, uint32_t* mask) {
 int ensure_xcd_streams(kano_ctx* ctx) {
   if (ctx->stream_x || ctx->xcd_tried) return 0;
   ctx->xcd_tried = true;
-  uint32_t wm[8], em[8];
+  uint32_t wm[8], em[8], am[8];
   xcd_mask(0, ctx->xcd_write, wm);
   xcd_mask(ctx->xcd_eng0 < 0 ? ctx->xcd_write : ctx->xcd_eng0, 8, em);
-  hipStream_t a = nullptr, b = nullptr, c = nullptr;
+  xcd_mask(0, 8, am);
+  hipStream_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
   if (hipExtStreamCreateWithCUMask(&a, 8, em) != hipSuccess ||
       hipExtStreamCreateWithCUMask(&b, 8, em) != hipSuccess ||
-      hipExtStreamCreateWithCUMask(&c, 8, wm) != hipSuccess) {
-    for (hipStream_t x : {a, b, c})
+      hipExtStreamCreateWithCUMask(&c, 8, wm) != hipSuccess ||
+      hipExtStreamCreateWithCUMask(&d, 8, am) != hipSuccess) {
+    for (hipStream_t x : {a, b, c, d})
       if (x) (void)hipStreamDestroy(x);
     return 0;   // (no split: the spread mask stays)
   }
   ctx->stream_x = a;
   ctx->stream2_x = b;
   ctx->stream3x = c;
+  ctx->stream2_u = d;
   return 0;
 }
-// The engine stream pair for the build about to start (front_a): the
-// XCD-masked pair when the last build qualified, else the unmasked one; a
-// switch orders the new pair behind everything queued on the old one.
+// The engine streams for the build about to start (front_a): the engine
+// stream on XCDs 3-7 when the last build qualified; the side stream with it
+// when that build had heavy classes, else on a stream masked to every XCD
+// (C3, no heavy classes: 5 % faster; C4's heavy side work beside the write on
+// XCDs 0-2: 6 % slower, r06_xcd_side_ab.jsonl -- and the original unmasked
+// side stream beside the masked ones: 0.64 ms, r06_xcd_side_auto_ab.jsonl).
+// A switch orders the new streams behind everything queued on the old ones.
+void side_swap(kano_ctx* ctx, int mode) {
+  if (mode == 1) std::swap(ctx->stream2, ctx->stream2_x);
+  if (mode == 2) std::swap(ctx->stream2, ctx->stream2_u);
+}
 int select_engine_streams(kano_ctx* ctx) {
   const bool want = ctx->xcd_split && ctx->own_stream && ctx->pipeline && ctx->xcd_last_ok &&
                     ctx->stream3m && ctx->num_cus == 256;
   if (want) KTRY(ensure_xcd_streams(ctx));
-  const bool target = want && ctx->stream_x;
-  if (target == ctx->eng_on_xcd) return 0;
+  const bool eng = want && ctx->stream_x;
+  const bool heavy_side = ctx->xcd_side < 0 ? ctx->heavy_count > 0 : ctx->xcd_side == 1;
+  const int side = !eng ? 0 : heavy_side ? 1 : 2;
+  if (eng == ctx->eng_on_xcd && side == ctx->side_mode) return 0;
   KCHK(hipEventRecord(ctx->ev_sw, ctx->stream));
   KCHK(hipEventRecord(ctx->ev_sw2, ctx->stream2));
-  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x}) {
+  if (eng != ctx->eng_on_xcd) std::swap(ctx->stream, ctx->stream_x);
+  if (side != ctx->side_mode) {
+    side_swap(ctx, ctx->side_mode);   // (back to stream2, then to the new one)
+    side_swap(ctx, side);
+  }
+  for (hipStream_t t : {ctx->stream, ctx->stream2}) {
     KCHK(hipStreamWaitEvent(t, ctx->ev_sw, 0));
     KCHK(hipStreamWaitEvent(t, ctx->ev_sw2, 0));
   }
-  std::swap(ctx->stream, ctx->stream_x);
-  std::swap(ctx->stream2, ctx->stream2_x);
-  ctx->eng_on_xcd = target;
+  ctx->eng_on_xcd = eng;
+  ctx->side_mode = side;
   return 0;
 }
-// back to the unmasked pair, everything drained (kano_set_stream)
+// back to the unmasked streams, everything drained (kano_set_stream)
 int leave_xcd_streams(kano_ctx* ctx) {
-  if (!ctx->eng_on_xcd) return 0;
-  for (hipStream_t t : {ctx->stream, ctx->stream2, ctx->stream_x, ctx->stream2_x})
+  if (!ctx->eng_on_xcd && !ctx->side_mode) return 0;
+  for (hipStream_t t : {ctx->stream, ctx->stream2, ctx->stream_x, ctx->stream2_x, ctx->stream2_u})
     KCHK(hipStreamSynchronize(t));
-  std::swap(ctx->stream, ctx->stream_x);
-  std::swap(ctx->stream2, ctx->stream2_x);
+  if (ctx->eng_on_xcd) std::swap(ctx->stream, ctx->stream_x);
+  side_swap(ctx, ctx->side_mode);
   ctx->eng_on_xcd = false;
+  ctx->side_mode = 0;
   return 0;
 }
 
@@ -2115,6 +2133,7 @@ int kano_create(int device, kano_ctx** out) {
         if (k == "xcdmin" && v >= 0) ctx->xcd_min_bytes = (i64)v << 10;
         if (k == "xcdw" && v >= 1 && v <= 7) ctx->xcd_write = v;
         if (k == "xcde" && v >= 0 && v <= 7) ctx->xcd_eng0 = v;
+        if (k == "xcdside" && v >= -1 && v <= 1) ctx->xcd_side = v;
         if (k == "hgemm" && (v == -1 || v == 0 || v == 22 || v == 42 || v == 44))
           ctx->heavy_gemm = v;
         if (k == "hgemmmin" && v > 0) ctx->heavy_gemm_min = v;
@@ -2251,7 +2270,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamSynchronize(ctx->stream3m);
-  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x, ctx->stream3x})
+  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x, ctx->stream3x, ctx->stream2_u})
     if (t) (void)hipStreamSynchronize(t);
   if (ctx->ghost) (void)hipHostFree(ctx->ghost);
   if (ctx->gmirror) (void)hipHostFree(ctx->gmirror);
@@ -2304,7 +2323,7 @@ void kano_destroy(kano_ctx* ctx) {
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->stream3m) (void)hipStreamDestroy(ctx->stream3m);
-  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x, ctx->stream3x})
+  for (hipStream_t t : {ctx->stream_x, ctx->stream2_x, ctx->stream3x, ctx->stream2_u})
     if (t) (void)hipStreamDestroy(t);
   for (hipEvent_t e : {ctx->ev_sw, ctx->ev_sw2})
     if (e) (void)hipEventDestroy(e);

@@ -208,7 +208,7 @@ def test_verify_fused_c2(cap):
     pin.close()
 
 
-@pytest.mark.parametrize("tune", ["", "xcdmin=0"])
+@pytest.mark.parametrize("tune", ["", "xcdmin=0", "xcdmin=0,xcdside=0", "xcdmin=0,xcdside=1"])
 def test_verify_pipelined(tune, monkeypatch):
     """kano_set_pipeline: every asynchronously completing verify queues the
     next call's prologue behind a gate the next verify opens.  Every call's
@@ -217,8 +217,10 @@ def test_verify_pipelined(tune, monkeypatch):
     build, a pause past the gate's timeout (the prologue then ran by itself on
     the same inputs), count-only mode, the emulated shard path, the pipeline
     switched off while a prologue is queued, and a close while one is queued.
-    xcdmin=0: the XCD split at C2's size (engine streams on XCDs 3-7, the
-    write on 0-2, switched between calls as the last write qualifies)."""
+    xcdmin=0: the XCD split at C2's size (the engine stream on XCDs 3-7, the
+    write on 0-2, switched between calls as the last write qualifies);
+    xcdside=0 / 1 keep the side stream unmasked / move it with the engine
+    stream whatever the last build's heavy classes."""
     if tune:
         monkeypatch.setenv("KANO_TUNE", tune)
     import time
